@@ -1,0 +1,118 @@
+/*
+ * fm_oracle.h — CPU restatement of the reference FM-index query path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library under
+ * compressed-fm-index-implementation-with-learned-optimizations_amd/) links,
+ * loads or calls this code.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py use it, and only as the checker / the timed CPU
+ * baseline.
+ *
+ * Parity is pinned: tests/test_oracle_golden.py checks every function here
+ * against golden vectors produced by the genuine reference (oracle/_ref, built
+ * from /root/reference sources by oracle/Makefile) and against the known-answer
+ * values in the reference's own tests (tests/fm_search_tests.cpp,
+ * tests/wavelet_tests.cpp, tests/bitvector_tests.cpp).
+ *
+ * Every function cites the reference file:line it restates (paths relative to
+ * the reference root).  Positions are 64-bit throughout; for n < 2^32 every value
+ * equals the reference's uint32 tables (src/api/fm_index.hpp:43-44,
+ * src/core/bitvector.hpp:97, src/core/ssa.hpp:9).
+ */
+#ifndef CS_FM_ORACLE_H
+#define CS_FM_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes shared with locate (src/api/fm_index.cpp:136-146). */
+#define ORC_OK 0
+#define ORC_ERR_LF_OVERRUN 1     /* "locate: LF walk exceeded text length" */
+#define ORC_ERR_SSA_RANGE 2      /* "locate: SSA sample index out of range: ..." */
+#define ORC_ERR_CAPACITY 3       /* output buffer too small (oracle-only) */
+#define ORC_ERR_NOSA 4           /* index built from a BWT only: no SSA */
+
+/* Geometry of include/cs/config.hpp:56-63. */
+#define ORC_SUPER 2048
+#define ORC_SUB 256
+
+typedef struct orc_bv orc_bv;
+typedef struct orc_index orc_index;
+
+/* --- BitVector (src/core/bitvector.{hpp,cpp}) --- */
+orc_bv* orc_bv_build(const uint8_t* bits, uint64_t nbits);           /* bitvector.cpp:14-92 */
+orc_bv* orc_bv_build_from_words(const uint64_t* words, uint64_t nwords,
+                                uint64_t nbits);                      /* bitvector.cpp:98-159 */
+void orc_bv_free(orc_bv* bv);
+uint64_t orc_bv_size(const orc_bv* bv);
+uint64_t orc_bv_rank1(const orc_bv* bv, uint64_t i, int faithful);   /* bitvector.cpp:165-230 */
+uint64_t orc_bv_rank0(const orc_bv* bv, uint64_t i, int faithful);   /* bitvector.hpp:72-75 */
+uint64_t orc_bv_count_ones(const orc_bv* bv);                         /* bitvector.cpp:236-248 */
+uint8_t orc_bv_get(const orc_bv* bv, uint64_t i);                     /* bitvector.hpp:48-53 */
+/* raw tables, for layout checks: counts in *_len */
+const uint64_t* orc_bv_words(const orc_bv* bv, uint64_t* len);
+const uint64_t* orc_bv_super(const orc_bv* bv, uint64_t* len);
+const uint16_t* orc_bv_blocks(const orc_bv* bv, uint64_t* len);
+
+/* --- Suffix array / BWT (src/core/sais.hpp:8-16, src/core/bwt.hpp:7-15) --- */
+void orc_sa_naive(const uint8_t* text, uint64_t n, uint64_t* sa);
+void orc_sa_doubling(const uint8_t* text, uint64_t n, uint64_t* sa);
+void orc_bwt_from_sa(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_t* bwt);
+
+/* --- FM index (src/api/fm_index.{hpp,cpp}) --- */
+/* sa_algo: 0 auto (naive for n <= 4096, doubling above), 1 naive, 2 doubling. */
+orc_index* orc_build(const uint8_t* text, uint64_t n, uint32_t ssa_stride, int sa_algo);
+/* count-only index from a BWT (no text, no SA): used by the CPU baseline */
+orc_index* orc_build_from_bwt(const uint8_t* bwt, uint64_t n);
+void orc_free(orc_index* idx);
+uint64_t orc_n(const orc_index* idx);
+uint32_t orc_ssa_stride(const orc_index* idx);
+void orc_get_sa(const orc_index* idx, uint64_t* out);        /* n entries */
+void orc_get_bwt(const orc_index* idx, uint8_t* out);        /* n bytes */
+void orc_get_C(const orc_index* idx, uint64_t* out);         /* 257 entries */
+uint64_t orc_ssa_len(const orc_index* idx);
+void orc_get_ssa(const orc_index* idx, uint64_t* out);
+const orc_bv* orc_level(const orc_index* idx, int level);    /* wavelet level 0..7 */
+
+uint64_t orc_wt_rank(const orc_index* idx, uint8_t c, uint64_t i, int faithful); /* wavelet.cpp:59-96 */
+uint8_t orc_wt_access(const orc_index* idx, uint64_t i, int faithful);          /* wavelet.cpp:102-128 */
+uint64_t orc_lf(const orc_index* idx, uint64_t i, int faithful);               /* fm_index.hpp:62-66 */
+
+uint64_t orc_count(const orc_index* idx, const uint8_t* p, uint64_t m, int faithful); /* fm_index.cpp:79-101 */
+/* fm_index.cpp:107-157.  Writes up to cap positions; *nout = number produced.
+ * On ORC_ERR_SSA_RANGE, aux[0]=idx, aux[1]=size (the message arguments). */
+int orc_locate(const orc_index* idx, const uint8_t* p, uint64_t m, uint64_t limit,
+               uint64_t* out, uint64_t cap, uint64_t* nout, int faithful, uint64_t* aux);
+/* fm_index.cpp:163-167; returns bytes written (clamped). */
+uint64_t orc_extract(const orc_index* idx, uint64_t pos, uint64_t len, uint8_t* out);
+
+/* Batched drivers: nthreads host threads on disjoint contiguous slices (the
+ * reference's query methods are const and re-entrant).  lat_ns, if non-NULL,
+ * receives each query's wall time (ns), as tools/benchmark.cpp:154-157 times
+ * each call. */
+void orc_count_batch(const orc_index* idx, const uint8_t* pats, const uint64_t* offs,
+                     uint64_t npat, uint64_t* out, int nthreads, int faithful,
+                     uint64_t* lat_ns);
+/* out_offs: npat+1 CSR offsets into out_pos (row-order positions per pattern).
+ * Returns ORC_OK or the first error code. */
+int orc_locate_batch(const orc_index* idx, const uint8_t* pats, const uint64_t* offs,
+                     uint64_t npat, uint64_t limit, uint64_t* out_offs, uint64_t* out_pos,
+                     uint64_t cap, int nthreads, int faithful);
+
+/* --- Synthetic inputs --- */
+uint64_t orc_splitmix64(uint64_t* state);
+/* DNA: 32 bases per draw, 2 bits each LSB-first -> "ACGT", then '$'.  Writes len+1 bytes. */
+void orc_gen_dna(uint64_t seed, uint64_t len, uint8_t* out);
+/* bytes: 8 per draw, b -> 1 + ((b*255)>>8), then 0x00.  Writes len+1 bytes. */
+void orc_gen_bytes(uint64_t seed, uint64_t len, uint8_t* out);
+/* Q_text: pattern k = T[x_k % (N-m), +m) with x_k the k-th splitmix64 draw. */
+void orc_gen_patterns_text(const uint8_t* text, uint64_t N, uint64_t m, uint64_t npat,
+                           uint64_t seed, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,89 @@
+// ref_shim.cpp — extern "C" handle around the GENUINE reference cs::FMIndex.
+//
+// TEST INFRASTRUCTURE ONLY: built by `make -C oracle ref` into oracle/_ref/ from the
+// reference sources in place.  Used in the build container to (a) time the real
+// reference count() beside the C restatement (calibration) and (b)
+// produce golden vectors at sizes where the reference's naive suffix sort
+// (src/core/sais.hpp:8-16, O(n^2 log n)) is too slow: ref_build_from_sa fills the
+// index members exactly as build_from_text does (src/api/fm_index.cpp:16-69) from
+// a suffix array the caller supplies (checked equal to build_sa_naive at small n
+// by tests/test_oracle_golden.py).  Technique per SURVEY.md §7 step 1.
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <filesystem>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#define private public
+#include "api/fm_index.hpp"
+#undef private
+#include "core/bwt.hpp"
+
+extern "C" {
+
+void* ref_build_from_text(const uint8_t* text, uint64_t n, uint32_t stride) {
+  cs::BuildParams bp;
+  bp.ssa_stride = stride;
+  std::string t(reinterpret_cast<const char*>(text), n);
+  return new cs::FMIndex(cs::FMIndex::build_from_text(t, bp));
+}
+
+void* ref_build_from_sa(const uint8_t* text, uint64_t n, const uint32_t* sa, uint32_t stride) {
+  auto* idx = new cs::FMIndex();
+  idx->text_.assign(reinterpret_cast<const char*>(text), n);
+  idx->meta_.n = n;
+  idx->sa_.assign(sa, sa + n);
+  idx->bwt_ = cs::build_bwt_from_sa(idx->text_, idx->sa_);
+  idx->C_.assign(257, 0u);
+  std::array<uint32_t, 256> freq{};
+  for (unsigned char ch : idx->bwt_) freq[ch]++;
+  uint32_t cum = 0;
+  for (int c = 0; c < 256; ++c) { idx->C_[c] = cum; cum += freq[c]; }
+  idx->C_[256] = cum;
+  std::vector<uint8_t> bwt_bytes(idx->bwt_.begin(), idx->bwt_.end());
+  idx->wavelet_.build(bwt_bytes);
+  idx->ssa_.stride = stride;
+  const size_t ns = (idx->sa_.size() + stride - 1) / stride;
+  idx->ssa_.samples.resize(ns);
+  for (size_t i = 0; i < idx->sa_.size(); ++i)
+    if (i % stride == 0) idx->ssa_.samples[i / stride] = idx->sa_[i];
+  return idx;
+}
+
+void ref_free(void* h) { delete static_cast<cs::FMIndex*>(h); }
+
+void ref_get_sa(void* h, uint32_t* out) {
+  auto* idx = static_cast<cs::FMIndex*>(h);
+  std::memcpy(out, idx->sa_.data(), idx->sa_.size() * 4);
+}
+
+uint64_t ref_count(void* h, const uint8_t* p, uint64_t m) {
+  return static_cast<cs::FMIndex*>(h)->count(std::string_view(reinterpret_cast<const char*>(p), m));
+}
+
+// returns number of positions (<= cap), or -1 on exception
+int64_t ref_locate(void* h, const uint8_t* p, uint64_t m, uint64_t limit, uint64_t* out, uint64_t cap) {
+  try {
+    auto v = static_cast<cs::FMIndex*>(h)->locate(
+        std::string_view(reinterpret_cast<const char*>(p), m), limit);
+    const uint64_t k = std::min<uint64_t>(v.size(), cap);
+    std::memcpy(out, v.data(), k * 8);
+    return (int64_t)v.size();
+  } catch (...) {
+    return -1;
+  }
+}
+
+uint64_t ref_wt_rank(void* h, uint8_t c, uint64_t i) {
+  return static_cast<cs::FMIndex*>(h)->wavelet_.rank(c, i);
+}
+
+uint64_t ref_level_rank1(void* h, int level, uint64_t i) {
+  return static_cast<cs::FMIndex*>(h)->wavelet_.levels_[level].rank1(i);
+}
+
+}  // extern "C"

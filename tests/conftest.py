@@ -1,0 +1,56 @@
+import importlib.util
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+PKG_DIR = os.path.join(ROOT, "compressed-fm-index-implementation-with-learned-optimizations_amd")
+
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")
+    config.addinivalue_line("markers", "slow: multi-second CPU test")
+
+
+def load_pkg():
+    """Import the product package (its directory name is not a Python identifier)."""
+    if "cs_fmindex_amd" in sys.modules:
+        return sys.modules["cs_fmindex_amd"]
+    spec = importlib.util.spec_from_file_location(
+        "cs_fmindex_amd", os.path.join(PKG_DIR, "__init__.py"),
+        submodule_search_locations=[PKG_DIR])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["cs_fmindex_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def golden_text(spec) -> bytes:
+    import oracle as O
+    if "hex" in spec:
+        return bytes.fromhex(spec["hex"])
+    if "file" in spec:
+        with open(os.path.join(GOLDEN, spec["file"]), "rb") as f:
+            return f.read() + bytes.fromhex(spec.get("append_hex", ""))
+    if spec["gen"] == "dna":
+        return O.gen_dna(spec["seed"], spec["len"]).tobytes()
+    return O.gen_bytes(spec["seed"], spec["len"]).tobytes()
+
+
+def fm_golden_cases(*files):
+    out = []
+    for f in files:
+        for c in load_golden(f)["cases"]:
+            out.append(pytest.param(c, id="%s:%s" % (f.split(".")[0], c["name"])))
+    return out

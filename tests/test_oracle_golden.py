@@ -1,0 +1,117 @@
+"""Pin the CPU restatement (oracle/) against the genuine reference's golden vectors.
+
+CPU-only.  The fixtures in tests/golden/ were produced by the reference itself
+(tests/golden/make_golden.py driving oracle/_ref/).  Both rank modes of the oracle
+(faithful = reference cost model, fast = precomputed totals) must reproduce them
+bit for bit, quirks included (cyclic BWT without terminator, duplicate '$', row
+order, limit truncation, the LF-overrun exception).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import fm_golden_cases, golden_text, load_golden
+
+
+def _check_fm_case(case, faithful):
+    text = golden_text(case["text"])
+    assert len(text) == case["n"]
+    idx = O.Index(text, ssa_stride=case["ssa_stride"])
+    for ph, cnt, loc in zip(case["patterns_hex"], case["count"], case["locate"]):
+        p = bytes.fromhex(ph)
+        assert idx.count(p, faithful=faithful) == cnt, (case["name"], p)
+        if "error" in loc:
+            with pytest.raises(RuntimeError) as ei:
+                idx.locate(p, limit=case["limit"], faithful=faithful)
+            if loc["error"] != "exception":
+                assert str(ei.value) == loc["error"]
+        else:
+            assert idx.locate(p, limit=case["limit"], faithful=faithful) == loc["pos"], (case["name"], p)
+    for ex in case.get("extract", []):
+        assert idx.extract(ex["pos"], ex["len"]).hex() == ex["hex"]
+
+
+@pytest.mark.parametrize("case", fm_golden_cases("fm_kat.json"))
+@pytest.mark.parametrize("faithful", [True, False])
+def test_fm_kat(case, faithful):
+    _check_fm_case(case, faithful)
+
+
+@pytest.mark.parametrize("case", fm_golden_cases("fm_100k.json", "fm_1m.json"))
+def test_fm_large_fast(case):
+    _check_fm_case(case, faithful=False)
+
+
+def test_fm_100k_faithful_sample():
+    """Faithful mode (with the O(n) count_ones scans) on a sample of the 1e5 case."""
+    case = load_golden("fm_100k.json")["cases"][0]
+    text = golden_text(case["text"])
+    idx = O.Index(text, ssa_stride=case["ssa_stride"])
+    for k in range(0, len(case["patterns_hex"]), 97):
+        p = bytes.fromhex(case["patterns_hex"][k])
+        assert idx.count(p, faithful=True) == case["count"][k]
+
+
+def test_batch_drivers_match_golden():
+    case = load_golden("fm_100k.json")["cases"][0]
+    idx = O.Index(golden_text(case["text"]), ssa_stride=32)
+    pats = [bytes.fromhex(h) for h in case["patterns_hex"]]
+    got = idx.count_batch(pats, nthreads=4)
+    assert got.tolist() == case["count"]
+    offs, pos = idx.locate_batch(pats, limit=case["limit"], nthreads=4)
+    for q, loc in enumerate(case["locate"]):
+        assert pos[offs[q]:offs[q + 1]].tolist() == loc["pos"]
+
+
+@pytest.mark.parametrize("case", load_golden("bitvector.json")["cases"], ids=lambda c: c["name"])
+def test_bitvector(case):
+    n = case["n"]
+    bits = np.unpackbits(np.frombuffer(bytes.fromhex(case["bits_hex"]), np.uint8),
+                         bitorder="little")[:n]
+    bv = O.BitVector(bits)
+    assert bv.count_ones() == case["count_ones"]
+    for i in range(n + 2):
+        for faithful in (True, False):
+            assert bv.rank1(i, faithful) == case["rank1"][i]
+        assert bv.rank0(i) == case["rank0"][i]
+
+
+def test_bitvector_from_words():
+    """tests/bitvector_tests.cpp:186-202."""
+    bv = O.BitVector(words=np.array([0xAAAAAAAAAAAAAAAA, 0x5555555555555555], np.uint64), nbits=128)
+    assert bv.size() == 128 and bv.count_ones() == 64
+    assert bv.rank1(64) == 32 and bv.rank1(128) == 64
+
+
+@pytest.mark.parametrize("case", load_golden("wavelet.json")["cases"], ids=lambda c: c["name"])
+def test_wavelet(case):
+    seq = bytes.fromhex(case["seq_hex"])
+    # the wavelet over an arbitrary sequence = the index's wavelet over a BWT equal to it
+    idx = O.Index(bwt=seq)
+    n = len(seq)
+    for sym, ranks in case["rank"].items():
+        c = int(sym)
+        for i in range(n + 2):
+            assert idx.wt_rank(c, i, faithful=(i % 7 == 0)) == ranks[i], (case["name"], c, i)
+    assert [idx.wt_access(i) for i in range(n)] == case["access"]
+
+
+def test_sa_doubling_equals_naive():
+    """The doubling SA used for big fixtures equals sais.hpp's naive order."""
+    rng = np.random.default_rng(3)
+    for trial in range(60):
+        n = int(rng.integers(0, 300))
+        alpha = [b"ab", b"ACGT$", bytes(range(256)), b"a"][trial % 4]
+        t = bytes(rng.choice(list(alpha), size=n).astype(np.uint8))
+        assert O.sa_naive(t).tolist() == O.sa_doubling(t).tolist()
+
+
+def test_synthetic_generators():
+    """SURVEY §8(d) generators: terminator placement and alphabet."""
+    d = O.gen_dna(42, 1000)
+    assert d[-1] == ord("$") and set(d[:-1].tobytes()) <= set(b"ACGT")
+    b = O.gen_bytes(42, 1000)
+    assert b[-1] == 0 and b[:-1].min() >= 1
+    q = O.gen_patterns_text(d, 20, 50, seed=4242)
+    s = d.tobytes()
+    assert all(bytes(p) in s for p in q)
