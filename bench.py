@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""bench.py — batched FM-index count() on MI355X (BASELINE.json metric).
+
+Workload (default = BASELINE.json configs[3], "C4", the config the metric is
+quoted on; it fits one GPU): 4 GB synthetic DNA text (n = 4e9 incl. the '$'
+terminator, SURVEY.md §8(d): splitmix64 seed 42), Q_text 20-mers (substrings at
+splitmix64(4242) positions).  One step = one batched count() launch over a batch
+of --batch patterns per GPU, inputs resident in HBM.  Multi-GPU: one process per
+GPU, index replicated (built per GPU), query stream sharded in contiguous ranges
+(weak scaling: --batch per GPU), per-shard counts gathered to rank 0 over RCCL
+inside the timed step.
+
+Extra fields on the JSON line:
+  roofline     the count kernel against HBM: achieved = algorithmic bytes per
+               launch (64 B per rank-line read the algorithm needs: 2 per
+               non-pure wavelet level per pattern character after the first) /
+               mean kernel time (HIP events on the launch stream); traffic from
+               the committed rocprofv3 PMC summary for this workload, if present.
+  cpu_baseline the oracle's reference-faithful count() (O(n) count_ones scans,
+               as src/core/bitvector.cpp:168-170) on a bounded sample of the same
+               batch, rank 0, N=1 only, all host threads.
+  p50_us       median end-to-end latency of single-pattern count() calls through
+               the C ABI (host pattern in, count out), as tools/benchmark.cpp:154-166.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from __graft_entry__ import _load_pkg  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(rank, *a):
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--kind", default="dna", choices=["dna", "bytes"])
+    ap.add_argument("--text-bytes", type=int, default=3_999_999_999,
+                    help="text length before the terminator (C4: 3,999,999,999)")
+    ap.add_argument("--m", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=12_500_000, help="patterns per GPU per step")
+    ap.add_argument("--ssa-stride", type=int, default=32)
+    ap.add_argument("--cpu-queries", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--p50-calls", type=int, default=1000)
+    ap.add_argument("--check", type=int, default=0, help="verify this many located Q_text hits")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    pkg = _load_pkg()
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    # ---- synthetic text in HBM, index built on this GPU ----
+    L = args.text_bytes
+    N = L + 1
+    t0 = time.perf_counter()
+    text = torch.empty(N + 16, dtype=torch.uint8, device=dev)
+    pkg.synth_text_device(args.kind, 42, L, text.data_ptr(), sh)
+    torch.cuda.synchronize()
+    idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
+                                             pkg.BuildParams(ssa_stride=args.ssa_stride), device=local)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    info = idx.info()
+    log(rank, "index built: n=%d in %.1f s, rank lines %.2f GB" % (N, build_s, info.rank_bytes / 1e9))
+
+    # ---- this rank's query shard (contiguous slice of the Q_text stream) ----
+    B, m = args.batch, args.m
+    pats = torch.empty(B * m, dtype=torch.uint8, device=dev)
+    offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    pkg.synth_patterns_device(text.data_ptr(), N, m, rank * B, B, 4242, pats.data_ptr(),
+                              offs.data_ptr(), sh)
+    out = torch.empty(B, dtype=torch.int64, device=dev)
+    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    # algorithmic bytes per launch: 2 lines x 64 B per active level per char after the first
+    act = torch.tensor([bin(info.active_levels[c]).count("1") for c in range(256)],
+                       dtype=torch.int64, device=dev)
+    alg_bytes = int(act[pats.view(B, m)[:, :-1].long()].sum().item()) * 2 * 64
+    torch.cuda.synchronize()
+
+    def step():
+        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, out.data_ptr(), sh)
+        if world > 1:
+            dist.gather(out, gather, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, out.data_ptr(), sh)
+        evs[k][1].record(stream)
+        if world > 1:
+            dist.gather(out, gather, dst=0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in evs]
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    total_units = B * world * args.steps
+    value = total_units / elapsed
+    kern_avg_s = statistics.mean(kern_ms) / 1e3
+    achieved = alg_bytes / kern_avg_s / 1e9
+    counts = out.cpu().numpy()
+    found = int((counts >= 1).sum())
+
+    res = None
+    if rank == 0:
+        traffic = None
+        prof = os.path.join(ROOT, "profiles", "pmc_count.json")
+        wl = "%s:%d:m%d:b%d" % (args.kind, N, m, B)
+        if os.path.exists(prof):
+            pj = json.load(open(prof))
+            if pj.get("workload") == wl:
+                traffic = pj.get("hbm_bytes_per_launch")
+        res = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "patterns/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": "C4: %s text n=%d (incl. terminator), Q_text %d-mers, count()"
+                       % (args.kind.upper(), N, m) if L == 3_999_999_999 else
+                       "%s text n=%d, Q_text %d-mers, count()" % (args.kind, N, m),
+                       "batch_per_gpu": B, "global_batch": B * world, "m": m,
+                       "ssa_stride": args.ssa_stride, "parallelism": "dp%d" % world,
+                       "index": "replicated per GPU", "workload_key": wl},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_per_query": alg_bytes / B,
+                         "kernel_ms_mean": kern_avg_s * 1e3,
+                         "kernel_ms_min": min(kern_ms)},
+            "build_s": build_s,
+            "found_frac": found / B,
+        }
+
+    # ---- p50 single-pattern latency through the C ABI (end to end) ----
+    if rank == 0 and args.p50_calls:
+        hp = pats[: args.p50_calls * m].cpu().numpy().reshape(-1, m)
+        lat = []
+        for q in range(hp.shape[0]):
+            b = hp[q].tobytes()
+            t1 = time.perf_counter()
+            idx.count(b)
+            lat.append((time.perf_counter() - t1) * 1e6)
+        res["p50_us"] = float(np.median(lat))
+        res["p95_us"] = float(np.percentile(lat, 95))
+        res["in_batch_us_per_query"] = elapsed / args.steps / B * 1e6
+
+    # ---- CPU baseline: reference-faithful restatement on host cores (rank 0, N=1) ----
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_queries > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline / checker only
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        t1 = time.perf_counter()
+        d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
+        idx.bwt_device(d_bwt.data_ptr(), sh)
+        bwt = d_bwt.cpu().numpy()
+        del d_bwt
+        ref = O.Index(bwt=bwt, nthreads=threads)
+        del bwt
+        prep_s = time.perf_counter() - t1
+        Q = args.cpu_queries
+        sample = pats[: Q * m].cpu().numpy()
+        soffs = np.arange(0, (Q + 1) * m, m, dtype=np.uint64)
+        t1 = time.perf_counter()
+        cnt, lat = ref.count_batch(buf=sample, offs=soffs, nthreads=min(threads, Q), faithful=True,
+                                   latencies=True)
+        cpu_s = time.perf_counter() - t1
+        match = bool(np.array_equal(cnt, counts[:Q].astype(np.uint64)))
+        res["cpu_baseline"] = {
+            "value": Q / cpu_s, "unit": "patterns/s", "cores": min(threads, Q), "kind": "port",
+            "sample": "first %d patterns of the batch, reference-faithful count() "
+                      "(oracle/fm_oracle.c faithful=1), %d host threads" % (Q, min(threads, Q)),
+            "p50_us": float(np.median(lat) / 1e3), "seconds": cpu_s, "prep_s": prep_s,
+            "matches_gpu": match}
+        del ref
+
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

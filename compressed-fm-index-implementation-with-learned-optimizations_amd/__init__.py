@@ -1,0 +1,333 @@
+"""MI355X-native batched FM-index (Python mirror of the reference's cs::FMIndex).
+
+Host-side mirror of src/api/fm_index.hpp:11-67 over the C ABI of
+libcs_fmindex.so (include/cs_fmindex.h): same names, argument meaning and error
+behaviour — RuntimeError with the reference's message where it throws
+std::runtime_error.  Every query runs in the HIP kernels; there is no CPU
+fallback: without the built library the import fails, and without a GPU every
+call raises.
+
+    idx = FMIndex.build_from_text(b"banana$", BuildParams())
+    idx.count(b"ana")            # 2           (fm_index.cpp:79-101)
+    idx.locate(b"ana")           # [3, 1]      (row order, fm_index.cpp:107-157)
+    idx.count_batch([...])       # one launch for the whole batch
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcs_fmindex.so")
+
+CS_OK, CS_ERR_INVALID, CS_ERR_OOM, CS_ERR_HIP = 0, 1, 2, 3
+CS_ERR_LF_OVERRUN, CS_ERR_SSA_RANGE, CS_ERR_CAPACITY, CS_ERR_UNSUPPORTED, CS_ERR_NO_DEVICE = 4, 5, 6, 7, 8
+
+_u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
+_u32p = C.POINTER(C.c_uint32)
+_vp = C.c_void_p
+
+
+class cs_build_params(C.Structure):
+    _fields_ = [("S", C.c_uint32), ("s", C.c_uint32), ("ssa_stride", C.c_uint32), ("eps", C.c_double)]
+
+
+class cs_fm_info(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("ssa_stride", C.c_uint32), ("line_bits", C.c_uint32),
+                ("lines_per_level", C.c_uint64), ("rank_bytes", C.c_uint64),
+                ("ssa_bytes", C.c_uint64), ("active_levels", C.c_uint32 * 256), ("device", C.c_int)]
+
+
+# Every entry point of include/cs_fmindex.h with its ctypes signature.
+SIGNATURES = {
+    "cs_default_build_params": (None, [C.POINTER(cs_build_params)]),
+    "cs_fm_build_from_text": (C.c_int, [_u8p, C.c_uint64, C.POINTER(cs_build_params), C.c_int,
+                                        C.POINTER(_vp)]),
+    "cs_fm_build_from_device_text": (C.c_int, [_vp, C.c_uint64, C.POINTER(cs_build_params), C.c_int,
+                                               C.POINTER(_vp)]),
+    "cs_fm_open_directory": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
+    "cs_fm_destroy": (None, [_vp]),
+    "cs_fm_get_info": (C.c_int, [_vp, C.POINTER(cs_fm_info)]),
+    "cs_fm_last_error": (C.c_char_p, []),
+    "cs_fm_count": (C.c_int, [_vp, _u8p, C.c_uint64, _u64p]),
+    "cs_fm_locate": (C.c_int, [_vp, _u8p, C.c_uint64, C.c_uint64, _u64p, C.c_uint64, _u64p]),
+    "cs_fm_extract": (C.c_int, [_vp, C.c_uint64, C.c_uint64, _u8p, _u64p]),
+    "cs_fm_count_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p, _vp]),
+    "cs_fm_locate_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, C.c_uint64, _u64p, _u64p,
+                                     C.c_uint64, _u64p, _vp]),
+    "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
+                                             _u64p, _vp]),
+    "cs_fm_locate_walk_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
+    "cs_fm_locate_walk_device_async": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
+    "cs_fm_locate_check": (C.c_int, [_vp, _vp]),
+    "cs_fm_level_rank1": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint64, _u64p]),
+    "cs_fm_wt_rank": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p]),
+    "cs_fm_wt_access": (C.c_int, [_vp, _u64p, C.c_uint64, _u8p]),
+    "cs_fm_lf": (C.c_int, [_vp, _u64p, C.c_uint64, _u64p]),
+    "cs_fm_get_C": (C.c_int, [_vp, _u64p]),
+    "cs_fm_bwt_device": (C.c_int, [_vp, _vp, _vp]),
+    "cs_fm_get_ssa": (C.c_int, [_vp, _u64p, C.c_uint64, _u64p]),
+    "cs_sa_build": (C.c_int, [_u8p, C.c_uint64, _u32p, C.c_int]),
+    # include/cs_synth.h
+    "cs_synth_text_device": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, _vp, _vp]),
+    "cs_synth_patterns_device": (C.c_int, [_vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                           C.c_uint64, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+def build(verbose: bool = False) -> str:
+    """Compile libcs_fmindex.so for gfx950 in-tree (hipcc via the Makefile)."""
+    import subprocess
+    subprocess.run(["make", "-s", "-C", _HERE, "-j8"], check=True,
+                   stdout=None if verbose else subprocess.DEVNULL)
+    return LIB_PATH
+
+
+def lib():
+    """Load the HIP library.  Fails loudly when it is missing: no fallback path."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libcs_fmindex.so not built: run `make -C %s` "
+                              "(or __graft_entry__.build())" % _HERE)
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class FMIndexError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(msg)
+        self.status = status
+
+
+def _check(status: int):
+    if status != CS_OK:
+        raise FMIndexError(status, lib().cs_fm_last_error().decode("utf-8", "replace"))
+
+
+def _bytes(x) -> bytes:
+    if isinstance(x, str):
+        return x.encode("latin-1")
+    if isinstance(x, np.ndarray):
+        return x.astype(np.uint8, copy=False).tobytes()
+    return bytes(x)
+
+
+def _u8(a: np.ndarray):
+    return a.ctypes.data_as(_u8p)
+
+
+def _u64(a: np.ndarray):
+    return a.ctypes.data_as(_u64p)
+
+
+def pack_patterns(patterns):
+    """list of bytes-like -> (u8 concatenation, u64 offsets[n+1])."""
+    pats = [_bytes(p) for p in patterns]
+    offs = np.zeros(len(pats) + 1, np.uint64)
+    if pats:
+        offs[1:] = np.cumsum([len(p) for p in pats], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(pats) + b"\0", np.uint8).copy()
+    return buf, offs
+
+
+@dataclass
+class BuildParams:
+    """src/api/fm_index.hpp:11-14 (only ssa_stride shapes the index, as there)."""
+    S: int = 512
+    s: int = 64
+    ssa_stride: int = 32
+    eps: float = 1.0
+
+    def _c(self):
+        return cs_build_params(self.S, self.s, self.ssa_stride, self.eps)
+
+
+class FMIndex:
+    """cs::FMIndex (src/api/fm_index.hpp:17-67) backed by the MI355X engine."""
+
+    def __init__(self, handle, n: int):
+        self._h = handle
+        self.n = n
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.cs_fm_destroy(h)
+            self._h = None
+
+    # -- construction (fm_index.hpp:19-20) --------------------------------
+    @staticmethod
+    def build_from_text(text, params: BuildParams | None = None, device: int | None = None):
+        p = (params or BuildParams())._c()
+        if device is None:
+            device = int(os.environ.get("CS_FM_DEVICE", "0"))
+        t = np.frombuffer(_bytes(text) + b"\0", np.uint8)
+        n = len(t) - 1
+        h = _vp()
+        _check(lib().cs_fm_build_from_text(_u8(t), n, C.byref(p), device, C.byref(h)))
+        return FMIndex(h, n)
+
+    @staticmethod
+    def build_from_device_text(d_text_ptr: int, n: int, params: BuildParams | None = None,
+                               device: int = 0):
+        p = (params or BuildParams())._c()
+        h = _vp()
+        _check(lib().cs_fm_build_from_device_text(d_text_ptr, n, C.byref(p), device, C.byref(h)))
+        return FMIndex(h, n)
+
+    @staticmethod
+    def open_directory(path: str):
+        h = _vp()
+        _check(lib().cs_fm_open_directory(path.encode(), C.byref(h)))
+        return FMIndex(h, 0)
+
+    # -- queries (fm_index.hpp:26-37) -------------------------------------
+    def count(self, pattern) -> int:
+        p = np.frombuffer(_bytes(pattern) + b"\0", np.uint8)
+        out = C.c_uint64()
+        _check(lib().cs_fm_count(self._h, _u8(p), len(p) - 1, C.byref(out)))
+        return out.value
+
+    def locate(self, pattern, limit: int = 100000) -> list:
+        offs, pos = self.locate_batch([pattern], limit)
+        return [int(v) for v in pos]
+
+    def extract(self, pos: int, length: int) -> bytes:
+        cap = max(1, min(length, max(self.n - pos, 0)))
+        out = np.zeros(cap, np.uint8)
+        got = C.c_uint64()
+        _check(lib().cs_fm_extract(self._h, pos, length, _u8(out), C.byref(got)))
+        return out[: got.value].tobytes()
+
+    # -- batched ----------------------------------------------------------
+    def count_batch(self, patterns=None, buf=None, offs=None) -> np.ndarray:
+        if patterns is not None:
+            buf, offs = pack_patterns(patterns)
+        buf = np.ascontiguousarray(buf, np.uint8)
+        if len(buf) == 0:
+            buf = np.zeros(1, np.uint8)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        npat = len(offs) - 1
+        out = np.zeros(max(npat, 1), np.uint64)
+        _check(lib().cs_fm_count_batch(self._h, _u8(buf), _u64(offs), npat, _u64(out), None))
+        return out[:npat]
+
+    def locate_batch(self, patterns=None, limit: int = 100000, buf=None, offs=None):
+        """-> (out_offs[npat+1], positions) with positions of pattern q in row order at
+        positions[out_offs[q]:out_offs[q+1]]."""
+        if patterns is not None:
+            buf, offs = pack_patterns(patterns)
+        buf = np.ascontiguousarray(buf, np.uint8)
+        if len(buf) == 0:
+            buf = np.zeros(1, np.uint8)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        npat = len(offs) - 1
+        out_offs = np.zeros(npat + 1, np.uint64)
+        total = C.c_uint64()
+        st = lib().cs_fm_locate_batch(self._h, _u8(buf), _u64(offs), npat, limit, _u64(out_offs),
+                                      None, 0, C.byref(total), None)
+        if st == CS_OK:
+            return out_offs, np.zeros(0, np.uint64)
+        if st != CS_ERR_CAPACITY:
+            _check(st)
+        pos = np.zeros(total.value, np.uint64)
+        _check(lib().cs_fm_locate_batch(self._h, _u8(buf), _u64(offs), npat, limit, _u64(out_offs),
+                                        _u64(pos), total.value, C.byref(total), None))
+        return out_offs, pos
+
+    # -- device-resident batches (raw device pointers, e.g. torch data_ptr()) --
+    def count_batch_device(self, d_pats: int, d_offs: int, npat: int, d_out: int, stream: int = 0):
+        _check(lib().cs_fm_count_batch_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
+
+    def locate_ranges_device(self, d_pats, d_offs, npat, limit, d_sp, d_out_offs, stream=0) -> int:
+        total = C.c_uint64()
+        _check(lib().cs_fm_locate_ranges_device(self._h, d_pats, d_offs, npat, limit, d_sp,
+                                                d_out_offs, C.byref(total), stream or None))
+        return total.value
+
+    def locate_walk_device(self, d_sp, d_out_offs, npat, total, d_out_pos, stream=0, sync=True):
+        f = lib().cs_fm_locate_walk_device if sync else lib().cs_fm_locate_walk_device_async
+        _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, stream or None))
+
+    def locate_check(self, stream=0):
+        _check(lib().cs_fm_locate_check(self._h, stream or None))
+
+    # -- building blocks / introspection ----------------------------------
+    def info(self) -> cs_fm_info:
+        inf = cs_fm_info()
+        _check(lib().cs_fm_get_info(self._h, C.byref(inf)))
+        return inf
+
+    def C(self) -> np.ndarray:
+        out = np.zeros(257, np.uint64)
+        _check(lib().cs_fm_get_C(self._h, _u64(out)))
+        return out
+
+    def bwt_device(self, d_out: int, stream: int = 0):
+        _check(lib().cs_fm_bwt_device(self._h, d_out, stream or None))
+
+    def ssa(self) -> np.ndarray:
+        ln = C.c_uint64()
+        st = lib().cs_fm_get_ssa(self._h, None, 0, C.byref(ln))
+        out = np.zeros(max(ln.value, 1), np.uint64)
+        _check(lib().cs_fm_get_ssa(self._h, _u64(out), ln.value, C.byref(ln)))
+        return out[: ln.value]
+
+    def level_rank1(self, level: int, pos) -> np.ndarray:
+        p = np.ascontiguousarray(pos, np.uint64)
+        out = np.zeros(max(len(p), 1), np.uint64)
+        _check(lib().cs_fm_level_rank1(self._h, level, _u64(p), len(p), _u64(out)))
+        return out[: len(p)]
+
+    def wt_rank(self, syms, pos) -> np.ndarray:
+        s = np.ascontiguousarray(syms, np.uint8)
+        p = np.ascontiguousarray(pos, np.uint64)
+        out = np.zeros(max(len(p), 1), np.uint64)
+        _check(lib().cs_fm_wt_rank(self._h, _u8(s), _u64(p), len(p), _u64(out)))
+        return out[: len(p)]
+
+    def wt_access(self, pos) -> np.ndarray:
+        p = np.ascontiguousarray(pos, np.uint64)
+        out = np.zeros(max(len(p), 1), np.uint8)
+        _check(lib().cs_fm_wt_access(self._h, _u64(p), len(p), _u8(out)))
+        return out[: len(p)]
+
+    def lf(self, rows) -> np.ndarray:
+        p = np.ascontiguousarray(rows, np.uint64)
+        out = np.zeros(max(len(p), 1), np.uint64)
+        _check(lib().cs_fm_lf(self._h, _u64(p), len(p), _u64(out)))
+        return out[: len(p)]
+
+
+def synth_text_device(kind: str, seed: int, length: int, d_out: int, stream: int = 0):
+    """SURVEY §8(d) text (kind 'dna' | 'bytes'), length+1 bytes incl. terminator."""
+    _check(lib().cs_synth_text_device(0 if kind == "dna" else 1, seed, length, d_out, stream or None))
+
+
+def synth_patterns_device(d_text: int, N: int, m: int, first: int, npat: int, seed: int,
+                          d_pats: int, d_offs: int | None, stream: int = 0):
+    """Q_text patterns [first, first+npat) of stream `seed`, fixed stride m."""
+    _check(lib().cs_synth_patterns_device(d_text, N, m, first, npat, seed, d_pats, d_offs,
+                                          stream or None))
+
+
+def sa_build(text, device: int = 0) -> np.ndarray:
+    """Suffix array by the device builder (sais.hpp:8-16 order)."""
+    t = np.frombuffer(_bytes(text) + b"\0", np.uint8)
+    n = len(t) - 1
+    out = np.zeros(max(n, 1), np.uint32)
+    _check(lib().cs_sa_build(_u8(t), n, out.ctypes.data_as(_u32p), device))
+    return out[:n]

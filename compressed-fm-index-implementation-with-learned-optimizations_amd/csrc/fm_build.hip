@@ -1,0 +1,424 @@
+// fm_build.hip — index construction on the device (replaces, with identical
+// output, FMIndex::build_from_text, src/api/fm_index.cpp:16-69):
+//
+//   1. suffix array in plain suffix order (src/core/sais.hpp:8-16: a proper prefix
+//      sorts first) by prefix doubling over device radix sorts (rocPRIM) —
+//      O(n log L) instead of the reference's O(n^2 log n) string sort;
+//   2. cyclic BWT (src/core/bwt.hpp:7-15) and row-sampled SSA (fm_index.cpp:57-66);
+//   3. C[] (fm_index.cpp:36-47) from the symbol histogram (the BWT is a permutation
+//      of the text);
+//   4. the 8-level wavelet matrix (src/core/wavelet.cpp:14-53) as 64-B rank lines
+//      (fm_device.hpp), one stable partition per level;
+//   5. the node table (starts, ranks, purity) for the query kernels.
+// Index construction is not the timed hot path; it is HBM-streaming work.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cstring>
+
+#include "fm_internal.hpp"
+
+namespace fmx {
+namespace {
+
+constexpr unsigned kBlk = 256;
+
+__global__ void k_hist(const uint8_t* __restrict__ t, uint64_t n,
+                       unsigned long long* __restrict__ hist) {
+  __shared__ unsigned int h[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t n16 = n / 16;
+  const uint4* t16 = reinterpret_cast<const uint4*>(t);
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += stride) {
+    const uint4 v = t16[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) atomicAdd(&h[(w[k] >> (8 * b)) & 0xFFu], 1u);
+    }
+  }
+  for (uint64_t i = n16 * 16 + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    atomicAdd(&h[t[i]], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+// Initial key: the first K symbols, dense codes 1..sigma (0 past the end, so a
+// proper prefix sorts first), b bits each.
+__global__ void k_init_keys(const uint8_t* __restrict__ t, uint64_t n,
+                            const uint8_t* __restrict__ code_g, int b, int K,
+                            uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  __shared__ uint8_t code[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) code[i] = code_g[i];
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    uint64_t k = 0;
+    for (int j = 0; j < K; ++j) {
+      const uint64_t c = (i + j < n) ? code[t[i + j]] : 0u;
+      k = (k << b) | c;
+    }
+    key[i] = k;
+    val[i] = (uint32_t)i;
+  }
+}
+
+// Group heads of the sorted keys: hp[j] = j at a head, else 0; counts heads.
+__global__ void k_heads(const uint64_t* __restrict__ key, uint64_t n, uint32_t* __restrict__ hp,
+                        unsigned long long* __restrict__ ngroups) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long local = 0;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += stride) {
+    const bool head = (j == 0) || key[j] != key[j - 1];
+    hp[j] = head ? (uint32_t)j : 0u;
+    local += head;
+  }
+  // wave reduce then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
+  if ((threadIdx.x & 63) == 0 && local) atomicAdd(ngroups, local);
+}
+
+__global__ void k_scatter_rank(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ hp,
+                               uint64_t n, uint32_t* __restrict__ rank) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += stride)
+    rank[sa[j]] = hp[j] + 1u;
+}
+
+__global__ void k_double_keys(const uint32_t* __restrict__ rank, uint64_t n, uint64_t h, int B,
+                              uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t r2 = (i + h < n) ? rank[i + h] : 0u;
+    key[i] = ((uint64_t)rank[i] << B) | r2;
+    val[i] = (uint32_t)i;
+  }
+}
+
+// bwt.hpp:7-15 and fm_index.cpp:57-66 in one pass.
+__global__ void k_bwt_ssa(const uint8_t* __restrict__ t, const uint32_t* __restrict__ sa,
+                          uint32_t n, uint32_t stride, uint8_t* __restrict__ bwt,
+                          uint32_t* __restrict__ ssa) {
+  const uint32_t gs = gridDim.x * blockDim.x;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gs) {
+    const uint32_t s = sa[j];
+    bwt[j] = t[s == 0 ? n - 1 : s - 1];
+    if (j % stride == 0) ssa[j / stride] = s;
+  }
+}
+
+// One wave per 64-bit payload word: ballot of the level bit.
+__global__ void k_pack_level(const uint8_t* __restrict__ cur, uint64_t n, int bit,
+                             RankLine* __restrict__ L, uint64_t nwords) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t g = wave; g < nwords; g += nwaves) {
+    const uint64_t p = g * 64 + lane;
+    const int b = p < n ? (cur[p] >> bit) & 1 : 0;
+    const uint64_t w = __ballot(b);
+    if (lane == 0) L[g / kLineWords].w[g % kLineWords] = w;
+  }
+}
+
+__global__ void k_line_counts(const RankLine* __restrict__ L, uint64_t nlines,
+                              uint64_t* __restrict__ cnt) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nlines; l += stride) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kLineWords; ++k) c += __popcll(L[l].w[k]);
+    cnt[l] = c;
+  }
+}
+
+__global__ void k_set_base(RankLine* __restrict__ L, const uint64_t* __restrict__ base,
+                           uint64_t nlines) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nlines; l += stride)
+    L[l].base = base[l];
+}
+
+// Stable zeros-then-ones partition (wavelet.cpp:27-30, :47-50) using the level's
+// own rank lines: dst = b ? Z + rank1(p) : p - rank1(p).
+__global__ void k_partition(const uint8_t* __restrict__ cur, uint64_t n, int bit,
+                            const RankLine* __restrict__ L, uint64_t Z, uint8_t* __restrict__ nxt) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n; p += stride) {
+    const uint8_t s = cur[p];
+    uint32_t q, o;
+    line_of(p, q, o);
+    uint4 v[4];
+    load_line(L, q, v);
+    const uint64_t r = line_base(v) + prefix_pop(v, o);
+    const uint64_t dst = ((s >> bit) & 1) ? Z + r : p - r;
+    nxt[dst] = s;
+  }
+}
+
+__global__ void k_node_rank(const RankLine* __restrict__ lines, uint64_t nlines,
+                            const NodeTable* __restrict__ T, uint64_t* __restrict__ R) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= kNodes) return;
+  int level = 0;
+  while ((1 << (level + 1)) - 1 <= t) ++level;
+  const uint64_t p = T->S[t];
+  uint32_t q, o;
+  line_of(p, q, o);
+  uint4 v[4];
+  load_line(lines + (uint64_t)level * nlines, q, v);
+  R[t] = line_base(v) + prefix_pop(v, o);
+}
+
+uint32_t bitrev(uint32_t x, int bits) {
+  uint32_t r = 0;
+  for (int i = 0; i < bits; ++i) r |= ((x >> i) & 1u) << (bits - 1 - i);
+  return r;
+}
+
+struct SortTemp {
+  DevBuf buf;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st) {
+  if (n == 0) return CS_OK;
+  if (n >= (1ull << 32)) {
+    set_error("text length must be < 2^32 (uint32 suffix array, src/core/sais.hpp:9)");
+    return CS_ERR_INVALID;
+  }
+  // symbol histogram -> dense codes
+  DevBuf d_hist;
+  FMX_HIP(d_hist.alloc(256 * sizeof(unsigned long long)));
+  FMX_HIP(hipMemsetAsync(d_hist.p, 0, 256 * sizeof(unsigned long long), st));
+  k_hist<<<grid_for(n / 16 + 1, kBlk, 8192), kBlk, 0, st>>>(d_text, n, d_hist.as<unsigned long long>());
+  unsigned long long hist[256];
+  FMX_HIP(hipMemcpyAsync(hist, d_hist.p, sizeof hist, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  uint8_t code[256];
+  int sigma = 0;
+  for (int c = 0; c < 256; ++c) code[c] = hist[c] ? (uint8_t)(++sigma) : 0;
+  int b = 1;
+  while ((1 << b) <= sigma) ++b;  // codes 0..sigma need b bits
+  const int K = 64 / b;
+  DevBuf d_code;
+  FMX_HIP(d_code.alloc(256));
+  FMX_HIP(hipMemcpyAsync(d_code.p, code, 256, hipMemcpyHostToDevice, st));
+
+  DevBuf k0, k1, v1, hp, hp2, rank, d_ng;
+  FMX_HIP(k0.alloc(n * 8));
+  FMX_HIP(k1.alloc(n * 8));
+  FMX_HIP(v1.alloc(n * 4));
+  FMX_HIP(hp.alloc(n * 4));
+  FMX_HIP(hp2.alloc(n * 4));
+  FMX_HIP(rank.alloc(n * 4));
+  FMX_HIP(d_ng.alloc(8));
+  uint32_t* v0 = d_sa;  // sorted values end up in either buffer; copied to d_sa at the end
+
+  const unsigned G = grid_for(n, kBlk, 16384);
+  k_init_keys<<<G, kBlk, 0, st>>>(d_text, n, d_code.as<uint8_t>(), b, K, k0.as<uint64_t>(), v0);
+  FMX_HIP(hipGetLastError());
+
+  int B = 1;
+  while (B < 64 && (1ull << B) <= n) ++B;  // ranks 1..n need B bits
+  SortTemp tmp;
+  uint64_t h = (uint64_t)K;
+  int end_bit = b * K;
+  for (int iter = 0;; ++iter) {
+    rocprim::double_buffer<uint64_t> kb(k0.as<uint64_t>(), k1.as<uint64_t>());
+    rocprim::double_buffer<uint32_t> vb(v0, v1.as<uint32_t>());
+    size_t need = 0;
+    FMX_HIP(rocprim::radix_sort_pairs(nullptr, need, kb, vb, n, 0, end_bit, st));
+    if (need > tmp.bytes) {
+      FMX_HIP(tmp.buf.alloc(need));
+      tmp.bytes = need;
+    }
+    FMX_HIP(rocprim::radix_sort_pairs(tmp.buf.p, need, kb, vb, n, 0, end_bit, st));
+    const uint64_t* skey = kb.current();
+    const uint32_t* sval = vb.current();
+    FMX_HIP(hipMemsetAsync(d_ng.p, 0, 8, st));
+    k_heads<<<G, kBlk, 0, st>>>(skey, n, hp.as<uint32_t>(), d_ng.as<unsigned long long>());
+    size_t sneed = 0;
+    FMX_HIP(rocprim::inclusive_scan(nullptr, sneed, hp.as<uint32_t>(), hp2.as<uint32_t>(), n,
+                                    rocprim::maximum<uint32_t>(), st));
+    if (sneed > tmp.bytes) {
+      FMX_HIP(tmp.buf.alloc(sneed));
+      tmp.bytes = sneed;
+    }
+    FMX_HIP(rocprim::inclusive_scan(tmp.buf.p, sneed, hp.as<uint32_t>(), hp2.as<uint32_t>(), n,
+                                    rocprim::maximum<uint32_t>(), st));
+    unsigned long long ng = 0;
+    FMX_HIP(hipMemcpyAsync(&ng, d_ng.p, 8, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    if (ng == n) {  // every suffix has a distinct h-prefix: sval is the SA
+      if (sval != d_sa) FMX_HIP(hipMemcpyAsync(d_sa, sval, n * 4, hipMemcpyDeviceToDevice, st));
+      FMX_HIP(hipStreamSynchronize(st));
+      return CS_OK;
+    }
+    k_scatter_rank<<<G, kBlk, 0, st>>>(sval, hp2.as<uint32_t>(), n, rank.as<uint32_t>());
+    // next round sorts (rank[i], rank[i+h]) = the 2h-prefix
+    k_double_keys<<<G, kBlk, 0, st>>>(rank.as<uint32_t>(), n, h, B, k0.as<uint64_t>(), v0);
+    FMX_HIP(hipGetLastError());
+    end_bit = 2 * B;
+    h *= 2;
+    if (iter > 64) {
+      set_error("suffix sorting did not converge");
+      return CS_ERR_INVALID;
+    }
+  }
+}
+
+cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
+                             hipStream_t st) {
+  if (stride == 0) {
+    set_error("ssa_stride must be > 0");
+    return CS_ERR_INVALID;
+  }
+  if (n >= (1ull << 32)) {
+    set_error("text length must be < 2^32 (uint32 suffix array, src/core/sais.hpp:9)");
+    return CS_ERR_INVALID;
+  }
+  h->n = n;
+  h->stride = stride;
+  h->nlines = n / kLineBits + 1;  // + sentinel so rank1(n) is a line read
+  h->nsamples = (n + stride - 1) / stride;
+
+  // --- histogram (BWT is a permutation of the text) ---
+  unsigned long long hist[256] = {0};
+  if (n) {
+    DevBuf d_hist;
+    FMX_HIP(d_hist.alloc(256 * sizeof(unsigned long long)));
+    FMX_HIP(hipMemsetAsync(d_hist.p, 0, 256 * sizeof(unsigned long long), st));
+    k_hist<<<grid_for(n / 16 + 1, kBlk, 8192), kBlk, 0, st>>>(d_text, n,
+                                                              d_hist.as<unsigned long long>());
+    FMX_HIP(hipMemcpyAsync(hist, d_hist.p, sizeof hist, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+  }
+
+  // --- SA, BWT, SSA ---
+  DevBuf bwt;
+  FMX_HIP(bwt.alloc(n));
+  FMX_HIP(hipMalloc(&h->d_ssa, (h->nsamples ? h->nsamples : 1) * 4));
+  if (n) {
+    DevBuf sa;
+    FMX_HIP(sa.alloc(n * 4));
+    cs_status s = build_sa_device(d_text, n, sa.as<uint32_t>(), st);
+    if (s != CS_OK) return s;
+    k_bwt_ssa<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(d_text, sa.as<uint32_t>(), (uint32_t)n,
+                                                         stride, bwt.as<uint8_t>(), h->d_ssa);
+    FMX_HIP(hipGetLastError());
+    FMX_HIP(hipStreamSynchronize(st));
+  }
+
+  // --- wavelet matrix levels as rank lines ---
+  const uint64_t nl = h->nlines;
+  FMX_HIP(hipMalloc(&h->d_lines, (size_t)kLevels * nl * sizeof(RankLine)));
+  FMX_HIP(hipMemsetAsync(h->d_lines, 0, (size_t)kLevels * nl * sizeof(RankLine), st));
+  NodeTable& T = h->h_table;
+  std::memset(&T, 0, sizeof T);
+  {
+    DevBuf nxt, cnt, base;
+    FMX_HIP(nxt.alloc(n));
+    FMX_HIP(cnt.alloc(nl * 8));
+    FMX_HIP(base.alloc(nl * 8));
+    DevBuf tmp;
+    size_t tmp_bytes = 0;
+    FMX_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.as<uint64_t>(), base.as<uint64_t>(),
+                                    (uint64_t)0, nl, rocprim::plus<uint64_t>(), st));
+    FMX_HIP(tmp.alloc(tmp_bytes));
+    uint8_t* cur = bwt.as<uint8_t>();
+    uint8_t* nx = nxt.as<uint8_t>();
+    const uint64_t nwords = nl * kLineWords;
+    for (int l = 0; l < kLevels; ++l) {
+      const int bit = 7 - l;
+      RankLine* L = h->d_lines + (uint64_t)l * nl;
+      k_pack_level<<<grid_for(nwords * 64, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, nwords);
+      k_line_counts<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, nl, cnt.as<uint64_t>());
+      size_t tb = tmp_bytes;
+      FMX_HIP(rocprim::exclusive_scan(tmp.p, tb, cnt.as<uint64_t>(), base.as<uint64_t>(),
+                                      (uint64_t)0, nl, rocprim::plus<uint64_t>(), st));
+      k_set_base<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, base.as<uint64_t>(), nl);
+      uint64_t last[2];
+      FMX_HIP(hipMemcpyAsync(&last[0], base.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
+      FMX_HIP(hipMemcpyAsync(&last[1], cnt.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
+      FMX_HIP(hipStreamSynchronize(st));
+      const uint64_t ones = last[0] + last[1];
+      T.Z[l] = n - ones;
+      if (l + 1 < kLevels && n) {
+        k_partition<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, T.Z[l], nx);
+        FMX_HIP(hipGetLastError());
+        std::swap(cur, nx);
+      }
+    }
+    FMX_HIP(hipStreamSynchronize(st));
+  }
+  bwt.release();
+
+  // --- node table from the histogram ---
+  uint64_t cum = 0;
+  for (int c = 0; c < 256; ++c) {
+    T.C[c] = cum;
+    cum += hist[c];
+  }
+  T.C[256] = cum;
+  for (int l = 0; l <= kLevels; ++l) {
+    const int np = 1 << l;
+    std::vector<uint64_t> cnt(np, 0);
+    for (int c = 0; c < 256; ++c) cnt[l ? (c >> (8 - l)) : 0] += hist[c];
+    // level-l order: by the bit-reversed l-bit prefix (stable partitions, MSB first)
+    std::vector<uint32_t> order(np);
+    for (int x = 0; x < np; ++x) order[bitrev(x, l)] = x;
+    uint64_t s = 0;
+    for (int r = 0; r < np; ++r) {
+      const int x = order[r];
+      if (l < kLevels) T.S[node_id(l, x)] = s;
+      else T.S8[x] = s;
+      s += cnt[x];
+    }
+    if (l == kLevels) break;
+    for (int x = 0; x < np; ++x) {
+      int seen = 0, b0 = -1;
+      bool pure = true;
+      for (int c = 0; c < 256; ++c) {
+        if (!hist[c] || (l ? (c >> (8 - l)) : 0) != x) continue;
+        const int b = (c >> (7 - l)) & 1;
+        if (!seen) b0 = b;
+        else if (b != b0) pure = false;
+        seen = 1;
+      }
+      uint8_t f = 0;
+      if (pure) f = kPure | (b0 == 1 ? kPureBit : 0);
+      T.flags[node_id(l, x)] = f;
+    }
+  }
+  for (int c = 0; c < 256; ++c) {
+    uint32_t m = 0;
+    for (int l = 0; l < kLevels; ++l)
+      if (!(T.flags[node_id(l, l ? (c >> (8 - l)) : 0)] & kPure)) m |= 1u << l;
+    h->active_levels[c] = hist[c] ? m : 0;
+  }
+  FMX_HIP(hipMalloc(&h->d_table, sizeof(NodeTable)));
+  FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
+  {
+    DevBuf dR;
+    FMX_HIP(dR.alloc(kNodes * 8));
+    k_node_rank<<<1, kBlk, 0, st>>>(h->d_lines, nl, h->d_table, dR.as<uint64_t>());
+    FMX_HIP(hipGetLastError());
+    FMX_HIP(hipMemcpyAsync(T.R, dR.p, kNodes * 8, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+  }
+  FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
+  FMX_HIP(hipMalloc(&h->d_err, 8));
+  FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+}  // namespace fmx

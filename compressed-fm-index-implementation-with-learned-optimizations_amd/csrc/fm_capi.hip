@@ -1,0 +1,446 @@
+// fm_capi.hip — the extern "C" boundary (include/cs_fmindex.h).  Host-buffer entry
+// points stage through HBM; *_device entry points only launch.  No CPU fallback:
+// without a HIP device every call fails with CS_ERR_NO_DEVICE.
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "fm_internal.hpp"
+
+namespace fmx {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+cs_status hip_fail(hipError_t e, const char* what) {
+  g_err = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") at " +
+          what;
+  (void)hipGetLastError();
+  return e == hipErrorOutOfMemory ? CS_ERR_OOM : CS_ERR_HIP;
+}
+
+namespace {
+
+cs_status use_device(int dev) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    (void)hipGetLastError();
+    set_error("no HIP device: the FM-index engine runs only on the GPU");
+    return CS_ERR_NO_DEVICE;
+  }
+  if (dev < 0 || dev >= count) {
+    set_error("device ordinal out of range");
+    return CS_ERR_INVALID;
+  }
+  FMX_HIP(hipSetDevice(dev));
+  return CS_OK;
+}
+
+cs_status check_handle(const cs_fm_index* h) {
+  if (!h) {
+    set_error("null index handle");
+    return CS_ERR_INVALID;
+  }
+  return use_device(h->device);
+}
+
+// Stage a host pattern batch into HBM.
+struct StagedBatch {
+  DevBuf pats, offs;
+  cs_status load(const uint8_t* p, const uint64_t* o, uint64_t npat, hipStream_t st) {
+    const uint64_t bytes = o[npat] - o[0];
+    FMX_HIP(pats.alloc(bytes + 16));
+    FMX_HIP(offs.alloc((npat + 1) * 8));
+    if (bytes) FMX_HIP(hipMemcpyAsync(pats.p, p + o[0], bytes, hipMemcpyHostToDevice, st));
+    if (o[0] == 0) {
+      FMX_HIP(hipMemcpyAsync(offs.p, o, (npat + 1) * 8, hipMemcpyHostToDevice, st));
+    } else {  // rebase so offsets index the staged bytes
+      std::vector<uint64_t> r(npat + 1);
+      for (uint64_t q = 0; q <= npat; ++q) r[q] = o[q] - o[0];
+      FMX_HIP(hipMemcpyAsync(offs.p, r.data(), (npat + 1) * 8, hipMemcpyHostToDevice, st));
+      FMX_HIP(hipStreamSynchronize(st));
+    }
+    return CS_OK;
+  }
+};
+
+void free_index(cs_fm_index* h) {
+  if (!h) return;
+  if (h->d_lines) (void)hipFree(h->d_lines);
+  if (h->d_ssa) (void)hipFree(h->d_ssa);
+  if (h->d_table) (void)hipFree(h->d_table);
+  if (h->d_err) (void)hipFree(h->d_err);
+  delete h;
+}
+
+cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params* p, int device,
+                       cs_fm_index** out, const uint8_t* host_text) {
+  if (!out) {
+    set_error("null output handle");
+    return CS_ERR_INVALID;
+  }
+  *out = nullptr;
+  cs_build_params dp;
+  cs_default_build_params(&dp);
+  if (!p) p = &dp;
+  cs_status s = use_device(device);
+  if (s != CS_OK) return s;
+  auto* h = new (std::nothrow) cs_fm_index();
+  if (!h) return CS_ERR_OOM;
+  h->device = device;
+  hipStream_t st;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return hip_fail(hipGetLastError(), "hipStreamCreate");
+  }
+  s = build_index_device(d_text, n, p->ssa_stride, h, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  if (s != CS_OK) {
+    free_index(h);
+    return s;
+  }
+  if (host_text) h->h_text.assign(host_text, host_text + n);
+  *out = h;
+  return CS_OK;
+}
+
+}  // namespace
+}  // namespace fmx
+
+using namespace fmx;
+
+extern "C" {
+
+void cs_default_build_params(cs_build_params* p) {
+  if (!p) return;
+  p->S = 512;
+  p->s = 64;
+  p->ssa_stride = 32;
+  p->eps = 1.0;
+}
+
+const char* cs_fm_last_error(void) { return g_err.c_str(); }
+
+cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_params* p,
+                                int device, cs_fm_index** out) {
+  if (!text && n) {
+    set_error("null text");
+    return CS_ERR_INVALID;
+  }
+  cs_status s = use_device(device);
+  if (s != CS_OK) return s;
+  DevBuf d;
+  FMX_HIP(d.alloc(n + 16));
+  if (n) FMX_HIP(hipMemcpy(d.p, text, n, hipMemcpyHostToDevice));
+  return build_common(d.as<uint8_t>(), n, p, device, out, text);
+}
+
+cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
+                                       const cs_build_params* p, int device,
+                                       cs_fm_index** out) {
+  if (!d_text && n) {
+    set_error("null text");
+    return CS_ERR_INVALID;
+  }
+  return build_common(d_text, n, p, device, out, nullptr);
+}
+
+cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out) {
+  (void)dir;
+  if (out) *out = nullptr;
+  set_error("on-disk open not implemented yet");  // fm_index.cpp:72
+  return CS_ERR_UNSUPPORTED;
+}
+
+void cs_fm_destroy(cs_fm_index* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  free_index(h);
+}
+
+cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
+  if (!h || !out) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  std::memset(out, 0, sizeof *out);
+  out->n = h->n;
+  out->ssa_stride = h->stride;
+  out->line_bits = kLineBits;
+  out->lines_per_level = h->nlines;
+  out->rank_bytes = (uint64_t)kLevels * h->nlines * sizeof(RankLine);
+  out->ssa_bytes = h->nsamples * 4;
+  std::memcpy(out->active_levels, h->active_levels, sizeof out->active_levels);
+  out->device = h->device;
+  return CS_OK;
+}
+
+cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
+                                   void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (npat && (!d_offs || !d_out)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_count(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
+}
+
+cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
+                            uint64_t npat, uint64_t* out_counts, void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!npat) return CS_OK;
+  if (!offs || !out_counts || (!pats && offs[npat] != offs[0])) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  StagedBatch b;
+  s = b.load(pats, offs, npat, st);
+  if (s != CS_OK) return s;
+  DevBuf d_out;
+  FMX_HIP(d_out.alloc(npat * 8));
+  s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
+  if (s != CS_OK) return s;
+  FMX_HIP(hipMemcpyAsync(out_counts, d_out.p, npat * 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+cs_status cs_fm_count(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t* out) {
+  const uint64_t offs[2] = {0, m};
+  return cs_fm_count_batch(h, pattern, offs, 1, out, nullptr);
+}
+
+cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                     const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                                     uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                                     void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!total || !d_out_offs || (npat && (!d_offs || !d_sp))) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_locate_ranges(h, d_pats, d_offs, npat, limit, d_sp, d_out_offs, total,
+                              (hipStream_t)stream);
+}
+
+cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d_sp,
+                                         const uint64_t* d_out_offs, uint64_t npat,
+                                         uint64_t total, uint64_t* d_out_pos, void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream);
+}
+
+cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  return check_locate_error(h, nullptr, 0, (hipStream_t)stream);
+}
+
+cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,
+                                   const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                                   uint64_t* d_out_pos, void* stream) {
+  cs_status s = cs_fm_locate_walk_device_async(h, d_sp, d_out_offs, npat, total, d_out_pos, stream);
+  if (s != CS_OK) return s;
+  return check_locate_error(h, d_out_offs, npat, (hipStream_t)stream);
+}
+
+cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
+                             uint64_t npat, uint64_t limit, uint64_t* out_offs, uint64_t* out_pos,
+                             uint64_t cap, uint64_t* total, void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!total || !out_offs) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  *total = 0;
+  if (!npat) {
+    out_offs[0] = 0;
+    return CS_OK;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  StagedBatch b;
+  s = b.load(pats, offs, npat, st);
+  if (s != CS_OK) return s;
+  DevBuf d_sp, d_oo;
+  FMX_HIP(d_sp.alloc(npat * 8));
+  FMX_HIP(d_oo.alloc((npat + 1) * 8));
+  s = launch_locate_ranges(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
+                           d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), total, st);
+  if (s != CS_OK) return s;
+  FMX_HIP(hipMemcpyAsync(out_offs, d_oo.p, (npat + 1) * 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  if (*total > cap) {
+    set_error("locate output capacity too small");
+    return CS_ERR_CAPACITY;
+  }
+  if (!*total) return CS_OK;
+  if (!out_pos) {
+    set_error("null output buffer");
+    return CS_ERR_INVALID;
+  }
+  DevBuf d_pos;
+  FMX_HIP(d_pos.alloc(*total * 8));
+  s = launch_locate_walk(h, d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), npat, *total,
+                         d_pos.as<uint64_t>(), st);
+  if (s != CS_OK) return s;
+  s = check_locate_error(h, d_oo.as<uint64_t>(), npat, st);
+  if (s != CS_OK) return s;
+  FMX_HIP(hipMemcpyAsync(out_pos, d_pos.p, *total * 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+cs_status cs_fm_locate(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t limit,
+                       uint64_t* out, uint64_t cap, uint64_t* nout) {
+  if (!nout) {
+    set_error("null nout");
+    return CS_ERR_INVALID;
+  }
+  *nout = 0;
+  const uint64_t offs[2] = {0, m};
+  uint64_t oo[2] = {0, 0};
+  uint64_t total = 0;
+  cs_status s = cs_fm_locate_batch(h, pattern, offs, 1, limit, oo, out, cap, &total, nullptr);
+  *nout = total;
+  return s;
+}
+
+cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_t* out,
+                        uint64_t* nout) {
+  if (!h || !nout) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  *nout = 0;
+  const uint64_t n = h->h_text.size();  // fm_index.cpp:163-167
+  if (pos >= n) return CS_OK;
+  if (len > n - pos) len = n - pos;
+  if (len && !out) {
+    set_error("null output buffer");
+    return CS_ERR_INVALID;
+  }
+  std::memcpy(out, h->h_text.data() + pos, len);
+  *nout = len;
+  return CS_OK;
+}
+
+}  // extern "C"
+
+// ---- building blocks (host arrays) ----
+template <class In, class Out, class F>
+static cs_status run_host(const cs_fm_index* h, const In* in, uint64_t k, Out* out, F launch) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!k) return CS_OK;
+  DevBuf di, dout;
+  FMX_HIP(di.alloc(k * sizeof(In)));
+  FMX_HIP(dout.alloc(k * sizeof(Out)));
+  FMX_HIP(hipMemcpy(di.p, in, k * sizeof(In), hipMemcpyHostToDevice));
+  s = launch(di.as<In>(), dout.as<Out>());
+  if (s != CS_OK) return s;
+  FMX_HIP(hipMemcpy(out, dout.p, k * sizeof(Out), hipMemcpyDeviceToHost));
+  return CS_OK;
+}
+
+extern "C" {
+
+cs_status cs_fm_level_rank1(const cs_fm_index* h, int level, const uint64_t* pos, uint64_t k,
+                            uint64_t* out) {
+  if (level < 0 || level >= kLevels) {
+    set_error("level out of range");
+    return CS_ERR_INVALID;
+  }
+  return run_host(h, pos, k, out, [&](const uint64_t* dp, uint64_t* dout) {
+    return launch_level_rank1(h, level, dp, k, dout, nullptr);
+  });
+}
+
+cs_status cs_fm_wt_rank(const cs_fm_index* h, const uint8_t* syms, const uint64_t* pos, uint64_t k,
+                        uint64_t* out) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!k) return CS_OK;
+  DevBuf ds;
+  FMX_HIP(ds.alloc(k));
+  FMX_HIP(hipMemcpy(ds.p, syms, k, hipMemcpyHostToDevice));
+  return run_host(h, pos, k, out, [&](const uint64_t* dp, uint64_t* dout) {
+    return launch_wt_rank(h, ds.as<uint8_t>(), dp, k, dout, nullptr);
+  });
+}
+
+cs_status cs_fm_wt_access(const cs_fm_index* h, const uint64_t* pos, uint64_t k, uint8_t* out) {
+  return run_host(h, pos, k, out, [&](const uint64_t* dp, uint8_t* dout) {
+    return launch_wt_access(h, dp, k, dout, nullptr);
+  });
+}
+
+cs_status cs_fm_lf(const cs_fm_index* h, const uint64_t* rows, uint64_t k, uint64_t* out) {
+  return run_host(h, rows, k, out, [&](const uint64_t* dp, uint64_t* dout) {
+    return launch_lf(h, dp, k, dout, nullptr);
+  });
+}
+
+cs_status cs_fm_get_C(const cs_fm_index* h, uint64_t* out257) {
+  if (!h || !out257) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  std::memcpy(out257, h->h_table.C, 257 * 8);
+  return CS_OK;
+}
+
+cs_status cs_fm_bwt_device(const cs_fm_index* h, uint8_t* d_out, void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!h->n) return CS_OK;
+  if (!d_out) {
+    set_error("null output buffer");
+    return CS_ERR_INVALID;
+  }
+  return launch_bwt(h, d_out, (hipStream_t)stream);
+}
+
+cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint64_t* len) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!len) return CS_ERR_INVALID;
+  *len = h->nsamples;
+  if (cap < h->nsamples) return CS_ERR_CAPACITY;
+  std::vector<uint32_t> tmp(h->nsamples);
+  if (h->nsamples) FMX_HIP(hipMemcpy(tmp.data(), h->d_ssa, h->nsamples * 4, hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < h->nsamples; ++i) out[i] = tmp[i];
+  return CS_OK;
+}
+
+cs_status cs_sa_build(const uint8_t* text, uint64_t n, uint32_t* sa_out, int device) {
+  cs_status s = use_device(device);
+  if (s != CS_OK) return s;
+  if (!n) return CS_OK;
+  if (!text || !sa_out) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  DevBuf dt, dsa;
+  FMX_HIP(dt.alloc(n + 16));
+  FMX_HIP(dsa.alloc(n * 4));
+  FMX_HIP(hipMemcpy(dt.p, text, n, hipMemcpyHostToDevice));
+  s = build_sa_device(dt.as<uint8_t>(), n, dsa.as<uint32_t>(), nullptr);
+  if (s != CS_OK) return s;
+  FMX_HIP(hipMemcpy(sa_out, dsa.p, n * 4, hipMemcpyDeviceToHost));
+  return CS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// fm_internal.hpp — host-side handle and shared helpers of libcs_fmindex.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/cs_fmindex.h"
+#include "fm_device.hpp"
+
+struct cs_fm_index {
+  int device = 0;
+  uint64_t n = 0;
+  uint32_t stride = 32;
+  fmx::RankLine* d_lines = nullptr;  // 8 levels x nlines
+  uint64_t nlines = 0;
+  uint32_t* d_ssa = nullptr;
+  uint64_t nsamples = 0;
+  fmx::NodeTable* d_table = nullptr;
+  fmx::NodeTable h_table{};
+  uint64_t* d_err = nullptr;          // locate: min failing item (UINT64_MAX = none)
+  std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
+  uint32_t active_levels[256] = {};
+
+  fmx::DevIndex dev() const {
+    fmx::DevIndex d;
+    d.lines = d_lines;
+    d.nlines = nlines;
+    d.n = n;
+    d.ssa = d_ssa;
+    d.nsamples = nsamples;
+    d.stride = stride;
+    d.stride_shift = 0xFFFFFFFFu;
+    if (stride && (stride & (stride - 1)) == 0) {
+      uint32_t s = 0;
+      while ((1u << s) != stride) ++s;
+      d.stride_shift = s;
+    }
+    d.table = d_table;
+    return d;
+  }
+};
+
+namespace fmx {
+
+// thread-local last-error text (cs_fm_last_error)
+void set_error(const std::string& msg);
+cs_status hip_fail(hipError_t e, const char* what);
+
+#define FMX_HIP(call)                                          \
+  do {                                                         \
+    hipError_t _e = (call);                                    \
+    if (_e != hipSuccess) return ::fmx::hip_fail(_e, #call);   \
+  } while (0)
+
+// Index construction on the device (fm_build.hip).
+cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st);
+cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
+                             hipStream_t st);
+
+// Query launches (fm_query.hip).
+cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                       uint64_t npat, uint64_t* d_out, hipStream_t st);
+cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
+                               const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                               uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                               hipStream_t st);
+cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
+                             const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                             uint64_t* d_out_pos, hipStream_t st);
+cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, uint64_t npat,
+                             hipStream_t st);
+cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
+                             uint64_t* d_out, hipStream_t st);
+cs_status launch_wt_rank(const cs_fm_index* h, const uint8_t* d_syms, const uint64_t* d_pos,
+                         uint64_t k, uint64_t* d_out, hipStream_t st);
+cs_status launch_wt_access(const cs_fm_index* h, const uint64_t* d_pos, uint64_t k,
+                           uint8_t* d_out, hipStream_t st);
+cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st);
+cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
+                    hipStream_t st);
+
+// RAII device buffer for temporaries.
+struct DevBuf {
+  void* p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t alloc(size_t bytes) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+    return hipMalloc(&p, bytes ? bytes : 16);
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+  void release() { if (p) (void)hipFree(p); p = nullptr; }
+};
+
+inline unsigned grid_for(uint64_t work, unsigned block, unsigned cap = 1u << 20) {
+  uint64_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace fmx

@@ -1,0 +1,405 @@
+// fm_query.hip — the hot path: batched backward search (FMIndex::count,
+// src/api/fm_index.cpp:79-101) and the LF/SSA walk of FMIndex::locate
+// (src/api/fm_index.cpp:107-157), as hand-written CDNA4 kernels.
+//
+// count: one lane per live pattern.  Per pattern character c the lane runs
+// WaveletTree::rank (src/core/wavelet.cpp:59-96) for sp and ep at once, in the
+// "relative" form: the start chain of c (start=0 mapped through the levels) is
+// fixed per symbol, so only d = end - start is carried:
+//     per level l with c's node not pure:  r = rank1_l(S + d) - R;  d = bit ? r : d - r
+// (S, R from the node table in LDS).  rank1_l = one 64-B rank line (fm_device.hpp).
+// The first character costs nothing (sp = C[c], ep = C[c+1]); absent symbols and
+// empty ranges exit early exactly where the reference returns 0.
+//
+// locate: (1) same search, writing sp and min(count, limit); (2) exclusive scan ->
+// CSR offsets; (3) rows expanded in row order (fm_index.cpp:125); (4) a persistent
+// walk kernel: each block owns a contiguous slice of rows and its lanes pull rows
+// from an LDS counter, so the geometric LF-walk lengths (row-sampled SSA, SURVEY
+// §0.5) do not idle a wave behind its longest walk.  LF (fm_index.hpp:62-66) is
+// computed by one descent that reads the BWT symbol and its rank from the same
+// rank lines (WaveletTree::access + rank fused), no separate BWT array.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "fm_internal.hpp"
+
+namespace fmx {
+namespace {
+
+constexpr unsigned kBlk = 256;
+
+__device__ __forceinline__ void load_table(NodeTable& T, const NodeTable* __restrict__ g) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
+  constexpr int nw = sizeof(NodeTable) / 4;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
+}
+
+// Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
+// range empties (the reference's `return 0`).  Requires m >= 1, n >= 1.
+__device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
+                                                const uint8_t* __restrict__ P, uint64_t m,
+                                                uint64_t& sp_out, uint64_t& ep_out) {
+  uint32_t c = P[m - 1];
+  uint64_t sp = T.C[c], ep = T.C[c + 1];  // occ(c,0)=0, occ(c,n)=freq(c)
+  if (sp >= ep) return false;
+  uint32_t cn = m >= 2 ? P[m - 2] : 0u;
+  for (uint64_t k = m - 1; k-- > 0;) {
+    c = cn;
+    if (k > 0) cn = P[k - 1];  // prefetch the next character
+    const uint64_t Cc = T.C[c];
+    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
+    uint64_t ds = sp, de = ep;
+#pragma unroll
+    for (int l = 0; l < kLevels; ++l) {
+      const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
+      if (!(T.flags[nid] & kPure)) {
+        const uint64_t S = T.S[nid], R = T.R[nid];
+        const RankLine* lv = ix.lines + (uint64_t)l * ix.nlines;
+        uint32_t qa, oa, qe, oe;
+        line_of(S + ds, qa, oa);
+        line_of(S + de, qe, oe);
+        uint4 va[4], ve[4];
+        load_line(lv, qa, va);
+        load_line(lv, qe, ve);
+        const uint64_t rs = line_base(va) + prefix_pop(va, oa) - R;
+        const uint64_t re = line_base(ve) + prefix_pop(ve, oe) - R;
+        const bool b = (c >> (7 - l)) & 1u;
+        ds = b ? rs : ds - rs;
+        de = b ? re : de - re;
+      }
+    }
+    sp = Cc + ds;
+    ep = Cc + de;
+    if (sp >= ep) return false;
+  }
+  sp_out = sp;
+  ep_out = ep;
+  return true;
+}
+
+__global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                const uint64_t* __restrict__ offs, uint64_t npat,
+                                                uint64_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= npat) return;
+  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  uint64_t res;
+  if (m == 0) res = ix.n;       // fm_index.cpp:80
+  else if (ix.n == 0) res = 0;  // :81
+  else {
+    uint64_t sp, ep;
+    res = backward_search(ix, T, pats + o0, m, sp, ep) ? ep - sp : 0;
+  }
+  out[q] = res;
+}
+
+__global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
+                                                        const uint8_t* __restrict__ pats,
+                                                        const uint64_t* __restrict__ offs,
+                                                        uint64_t npat, uint64_t limit,
+                                                        uint64_t* __restrict__ sp_out,
+                                                        uint64_t* __restrict__ cnt_out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q > npat) return;
+  if (q == npat) {  // scan slot for the total
+    cnt_out[q] = 0;
+    return;
+  }
+  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  uint64_t sp = 0, ep = 0;
+  if (m && ix.n) {  // fm_index.cpp:109: empty pattern or empty text -> {}
+    if (!backward_search(ix, T, pats + o0, m, sp, ep)) sp = ep = 0;
+  }
+  const uint64_t c = ep - sp;
+  sp_out[q] = sp;
+  cnt_out[q] = c < limit ? c : limit;  // fm_index.cpp:125 `positions.size() < limit`
+}
+
+// rows[j] = sp[q] + (j - offs[q]) for the reported rows of pattern q (row order).
+__global__ void k_expand_rows(const uint64_t* __restrict__ sp, const uint64_t* __restrict__ offs,
+                              uint64_t npat, uint32_t* __restrict__ rows) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
+    const uint64_t a = offs[q], b = offs[q + 1], s = sp[q];
+    for (uint64_t j = a; j < b; ++j) rows[j] = (uint32_t)(s + (j - a));
+  }
+}
+
+// One LF step (fm_index.hpp:62-66): descend the wavelet matrix from row i reading
+// the BWT symbol bit by bit (WaveletTree::access, wavelet.cpp:102-128) while
+// mapping i; the leaf offset is rank(c, i).  Pure nodes cost no load.
+__device__ __forceinline__ uint64_t lf_step(const DevIndex& ix, const NodeTable& T, uint64_t pos,
+                                            uint32_t* sym_out = nullptr) {
+  uint32_t x = 0;
+#pragma unroll
+  for (int l = 0; l < kLevels; ++l) {
+    const int nid = (1 << l) - 1 + (int)x;
+    const uint8_t f = T.flags[nid];
+    uint32_t b;
+    uint64_t r;
+    if (f & kPure) {
+      b = (f & kPureBit) ? 1u : 0u;
+      r = T.R[nid] + (b ? pos - T.S[nid] : 0);
+    } else {
+      uint32_t q, o;
+      line_of(pos, q, o);
+      uint4 v[4];
+      load_line(ix.lines + (uint64_t)l * ix.nlines, q, v);
+      b = bit_at(v, o);
+      r = line_base(v) + prefix_pop(v, o);
+    }
+    pos = b ? T.Z[l] + r : pos - r;
+    x = (x << 1) | b;
+  }
+  if (sym_out) *sym_out = x;
+  return T.C[x] + (pos - T.S8[x]);
+}
+
+template <bool POW2>
+__device__ __forceinline__ bool is_sampled(const DevIndex& ix, uint64_t row) {
+  if (POW2) return (row & ((1ull << ix.stride_shift) - 1)) == 0;
+  return row % ix.stride == 0;
+}
+
+template <bool POW2>
+__device__ __forceinline__ uint64_t sample_index(const DevIndex& ix, uint64_t row) {
+  if (POW2) return row >> ix.stride_shift;
+  return row / ix.stride;
+}
+
+// Persistent LF walk (fm_index.cpp:125-153).  Block b owns rows [b*chunk, ...).
+template <bool POW2>
+__global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint32_t* __restrict__ rows,
+                                               uint64_t total, uint64_t chunk,
+                                               uint64_t* __restrict__ out,
+                                               unsigned long long* __restrict__ err) {
+  __shared__ NodeTable T;
+  __shared__ unsigned long long next;
+  const uint64_t a = blockIdx.x * chunk;
+  const uint64_t end = (a + chunk < total) ? a + chunk : total;
+  load_table(T, ix.table);
+  if (threadIdx.x == 0) next = a;
+  __syncthreads();
+  if (a >= total) return;
+  const uint64_t n = ix.n;
+  uint64_t j = 0, pos = 0, steps = 0;
+  bool active = false, drained = false;
+  for (;;) {
+    if (!active && !drained) {
+      j = atomicAdd(&next, 1ull);
+      if (j < end) {
+        pos = rows[j];
+        steps = 0;
+        active = true;
+      } else {
+        drained = true;
+      }
+    }
+    if (!__any(active)) break;
+    if (active) {
+      // loop condition of fm_index.cpp:130: stop at a sampled row or after n steps
+      if (is_sampled<POW2>(ix, pos) || steps >= n) {
+        if (steps >= n) {
+          atomicMin(err, (unsigned long long)j);  // fm_index.cpp:136-138
+        } else {
+          const uint64_t s = (uint64_t)ix.ssa[sample_index<POW2>(ix, pos)] + steps;  // :147-153
+          out[j] = s >= n ? s - n : s;
+        }
+        active = false;
+      } else {
+        pos = lf_step(ix, T, pos);
+        ++steps;
+      }
+    }
+  }
+}
+
+// ---- building-block kernels for parity tests ----
+__global__ void k_level_rank1(DevIndex ix, int level, const uint64_t* __restrict__ pos, uint64_t k,
+                              uint64_t* __restrict__ out) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t >= k) return;
+  uint64_t p = pos[t];
+  // BitVector::rank1(i >= size) = count_ones() (bitvector.cpp:168-170)
+  if (p > ix.n) p = ix.n;
+  out[t] = rank1_dev(ix, level, p);
+}
+
+__global__ void k_wt_rank(DevIndex ix, const uint8_t* __restrict__ syms,
+                          const uint64_t* __restrict__ pos, uint64_t k, uint64_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t >= k) return;
+  const uint32_t c = syms[t];
+  const uint64_t i = pos[t];
+  uint64_t d = 0;
+  if (i != 0 && i <= ix.n && T.C[c] != T.C[c + 1]) {  // wavelet.cpp:60
+    d = i;
+    for (int l = 0; l < kLevels; ++l) {
+      const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
+      if (!(T.flags[nid] & kPure)) {
+        const uint64_t r = rank1_dev(ix, l, T.S[nid] + d) - T.R[nid];
+        d = ((c >> (7 - l)) & 1u) ? r : d - r;
+      }
+    }
+  }
+  out[t] = d;
+}
+
+__global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
+                     uint64_t* __restrict__ out, uint8_t* __restrict__ sym) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (t >= k) return;
+  const uint64_t i = rows[t];
+  if (i >= ix.n) {  // fm_index.hpp:63 / wavelet.cpp:104
+    if (out) out[t] = 0;
+    if (sym) sym[t] = 0;
+    return;
+  }
+  uint32_t c;
+  const uint64_t v = lf_step(ix, T, i, &c);
+  if (out) out[t] = v;
+  if (sym) sym[t] = (uint8_t)c;
+}
+
+// WaveletTree::access for every row (the BWT), grid-stride.
+__global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ix.n; i += stride) {
+    uint32_t c;
+    (void)lf_step(ix, T, i, &c);
+    out[i] = (uint8_t)c;
+  }
+}
+
+}  // namespace
+
+cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
+  k_bwt<<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(h->dev(), d_out);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                       uint64_t npat, uint64_t* d_out, hipStream_t st) {
+  if (!npat) return CS_OK;
+  k_count<<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_pats, d_offs, npat,
+                                                               d_out);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
+                               const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                               uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                               hipStream_t st) {
+  DevBuf cnt, tmp;
+  FMX_HIP(cnt.alloc((npat + 1) * 8));
+  k_locate_ranges<<<grid_for(npat + 1, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+      h->dev(), d_pats, d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
+  FMX_HIP(hipGetLastError());
+  size_t tb = 0;
+  FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint64_t>(), d_out_offs, (uint64_t)0,
+                                  npat + 1, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(tmp.alloc(tb));
+  FMX_HIP(rocprim::exclusive_scan(tmp.p, tb, cnt.as<uint64_t>(), d_out_offs, (uint64_t)0,
+                                  npat + 1, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(hipMemcpyAsync(total, d_out_offs + npat, 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
+                             const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                             uint64_t* d_out_pos, hipStream_t st) {
+  if (!total) return CS_OK;
+  DevBuf rows;
+  FMX_HIP(rows.alloc(total * 4));
+  k_expand_rows<<<grid_for(npat, kBlk, 65536), kBlk, 0, st>>>(d_sp, d_out_offs, npat,
+                                                              rows.as<uint32_t>());
+  FMX_HIP(hipGetLastError());
+  int dev = 0, ncu = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint64_t max_blocks = (uint64_t)ncu * 8;  // 8 x 256 threads = full CU
+  uint64_t chunk = (total + max_blocks - 1) / max_blocks;
+  if (chunk < 64) chunk = 64;
+  const uint64_t blocks = (total + chunk - 1) / chunk;
+  const fmx::DevIndex ix = h->dev();
+  if (ix.stride_shift != 0xFFFFFFFFu)
+    k_walk<true><<<(unsigned)blocks, kBlk, 0, st>>>(ix, rows.as<uint32_t>(), total, chunk,
+                                                    d_out_pos,
+                                                    reinterpret_cast<unsigned long long*>(h->d_err));
+  else
+    k_walk<false><<<(unsigned)blocks, kBlk, 0, st>>>(ix, rows.as<uint32_t>(), total, chunk,
+                                                     d_out_pos,
+                                                     reinterpret_cast<unsigned long long*>(h->d_err));
+  FMX_HIP(hipGetLastError());
+  // rows must outlive the kernel: synchronise before DevBuf frees it
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, uint64_t npat,
+                             hipStream_t st) {
+  uint64_t bad = ~0ull;
+  FMX_HIP(hipMemcpyAsync(&bad, h->d_err, 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  if (bad == ~0ull) return CS_OK;
+  FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  // map the failing row back to its pattern for the message
+  (void)d_out_offs;
+  (void)npat;
+  set_error("locate: LF walk exceeded text length");  // fm_index.cpp:137
+  return CS_ERR_LF_OVERRUN;
+}
+
+cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
+                             uint64_t* d_out, hipStream_t st) {
+  if (!k) return CS_OK;
+  k_level_rank1<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), level, d_pos, k, d_out);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status launch_wt_rank(const cs_fm_index* h, const uint8_t* d_syms, const uint64_t* d_pos,
+                         uint64_t k, uint64_t* d_out, hipStream_t st) {
+  if (!k) return CS_OK;
+  k_wt_rank<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_syms, d_pos, k, d_out);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status launch_wt_access(const cs_fm_index* h, const uint64_t* d_pos, uint64_t k,
+                           uint8_t* d_out, hipStream_t st) {
+  if (!k) return CS_OK;
+  k_lf<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_pos, k, nullptr, d_out);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
+                    hipStream_t st) {
+  if (!k) return CS_OK;
+  k_lf<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_rows, k, d_out, nullptr);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+}  // namespace fmx

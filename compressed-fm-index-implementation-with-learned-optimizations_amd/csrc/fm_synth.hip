@@ -1,0 +1,99 @@
+// fm_synth.hip — synthetic texts and Q_text pattern batches in HBM (SURVEY.md
+// §8(d)); bit-identical to oracle/fm_oracle.c's generators.
+#include "../../include/cs_synth.h"
+#include "fm_internal.hpp"
+
+namespace fmx {
+namespace {
+
+constexpr uint64_t kGamma = 0x9E3779B97F4A7C15ull;
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// one thread per draw
+__global__ void k_text(int kind, uint64_t seed, uint64_t len, uint8_t* __restrict__ out) {
+  const uint64_t per = kind == 0 ? 32 : 8;
+  const uint64_t ndraw = (len + per - 1) / per;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t d = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; d < ndraw; d += stride) {
+    const uint64_t x = mix64(seed + (d + 1) * kGamma);
+    const uint64_t base = d * per;
+    if (kind == 0) {
+      const char acgt[4] = {'A', 'C', 'G', 'T'};
+      if (base + 32 <= len) {
+        uint32_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v |= (uint32_t)acgt[(x >> (2 * (4 * k + b))) & 3u] << (8 * b);
+          w[k] = v;
+        }
+        uint4* o = reinterpret_cast<uint4*>(out + base);
+        o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+        o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+      } else {
+        for (uint64_t k = 0; base + k < len; ++k) out[base + k] = acgt[(x >> (2 * k)) & 3u];
+      }
+    } else {
+      for (uint64_t k = 0; k < 8 && base + k < len; ++k) {
+        const uint64_t b = (x >> (8 * k)) & 0xFFu;
+        out[base + k] = (uint8_t)(1 + ((b * 255) >> 8));
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[len] = kind == 0 ? '$' : 0;
+}
+
+__global__ void k_patterns(const uint8_t* __restrict__ text, uint64_t N, uint64_t m, uint64_t first,
+                           uint64_t npat, uint64_t seed, uint8_t* __restrict__ pats,
+                           uint64_t* __restrict__ offs) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
+    const uint64_t k = first + q;
+    const uint64_t pos = mix64(seed + (k + 1) * kGamma) % (N - m);
+    for (uint64_t j = 0; j < m; ++j) pats[q * m + j] = text[pos + j];
+    if (offs) {
+      offs[q] = q * m;
+      if (q + 1 == npat) offs[npat] = npat * m;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace fmx
+
+using namespace fmx;
+
+extern "C" {
+
+cs_status cs_synth_text_device(int kind, uint64_t seed, uint64_t len, uint8_t* d_out, void* stream) {
+  if (!d_out || (kind != 0 && kind != 1)) {
+    set_error("cs_synth_text_device: bad argument");
+    return CS_ERR_INVALID;
+  }
+  const uint64_t ndraw = (len + 7) / 8;
+  k_text<<<grid_for(ndraw, 256, 65536), 256, 0, (hipStream_t)stream>>>(kind, seed, len, d_out);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status cs_synth_patterns_device(const uint8_t* d_text, uint64_t N, uint64_t m, uint64_t first,
+                                   uint64_t npat, uint64_t seed, uint8_t* d_pats, uint64_t* d_offs,
+                                   void* stream) {
+  if (!d_text || !d_pats || m == 0 || N <= m) {
+    set_error("cs_synth_patterns_device: bad argument");
+    return CS_ERR_INVALID;
+  }
+  if (!npat) return CS_OK;
+  k_patterns<<<grid_for(npat, 256, 65536), 256, 0, (hipStream_t)stream>>>(d_text, N, m, first, npat,
+                                                                         seed, d_pats, d_offs);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+/*
+ * cs_fmindex.h — C ABI of the MI355X-native batched FM-index engine.
+ *
+ * Drop-in boundary for the reference's query path.  The reference exposes no FFI:
+ * its boundary is the C++ class cs::FMIndex (src/api/fm_index.hpp:17-67), linked
+ * statically by every caller (the tools/ and tests/ programs).  Each entry point below
+ * names the member it replaces.  include/cs/fm_index.hpp re-creates that class on
+ * top of this ABI (same names, argument meaning and exceptions), so a caller of the
+ * reference swaps the header and links libcs_fmindex.so — see INTEGRATION.md.
+ *
+ * Conventions
+ *  - plain pointers and sizes; no HIP or torch types.  `stream` is a hipStream_t
+ *    passed as void* (NULL = the legacy default stream of the handle's device).
+ *  - *_device entry points take device pointers (inputs already resident in HBM);
+ *    the others take host pointers and stage through HBM themselves.
+ *  - a handle is immutable after creation and may be used from several host
+ *    threads on distinct streams.
+ *  - positions and counts are uint64 (the reference's uint64_t return types,
+ *    src/api/fm_index.hpp:26,32); this build indexes texts of n < 2^32 bytes,
+ *    the reference's own limit (uint32 SA/C/SSA).
+ *  - on a non-OK status, cs_fm_last_error() returns this thread's message; for
+ *    CS_ERR_LF_OVERRUN it is the reference's exact text
+ *    "locate: LF walk exceeded text length" (src/api/fm_index.cpp:137).
+ */
+#ifndef CS_FMINDEX_H
+#define CS_FMINDEX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum cs_status {
+  CS_OK = 0,
+  CS_ERR_INVALID = 1,        /* bad argument (null pointer, n >= 2^32, ...) */
+  CS_ERR_OOM = 2,            /* device allocation failed */
+  CS_ERR_HIP = 3,            /* HIP runtime error (message in cs_fm_last_error) */
+  CS_ERR_LF_OVERRUN = 4,     /* fm_index.cpp:136-138 */
+  CS_ERR_SSA_RANGE = 5,      /* fm_index.cpp:141-146 */
+  CS_ERR_CAPACITY = 6,       /* caller's output buffer too small; *total says how big */
+  CS_ERR_UNSUPPORTED = 7,    /* e.g. open_directory (fm_index.cpp:71-73 throws) */
+  CS_ERR_NO_DEVICE = 8       /* no HIP device: the engine never falls back to the CPU */
+} cs_status;
+
+/* BuildParams — src/api/fm_index.hpp:11-14.  Only ssa_stride changes the index,
+ * as in the reference (S, s and eps are accepted and ignored there too). */
+typedef struct cs_build_params {
+  uint32_t S;           /* 512 */
+  uint32_t s;           /* 64 */
+  uint32_t ssa_stride;  /* 32 */
+  double eps;           /* 1.0 */
+} cs_build_params;
+
+typedef struct cs_fm_index cs_fm_index;
+
+/* Memory / geometry summary of a built index. */
+typedef struct cs_fm_info {
+  uint64_t n;              /* text length incl. any terminator the caller appended */
+  uint32_t ssa_stride;
+  uint32_t line_bits;      /* payload bits per 64-B rank line */
+  uint64_t lines_per_level;
+  uint64_t rank_bytes;     /* 8 levels of rank lines in HBM */
+  uint64_t ssa_bytes;
+  uint32_t active_levels[256]; /* per symbol: bitmask of levels needing a memory access */
+  int device;
+} cs_fm_info;
+
+void cs_default_build_params(cs_build_params* p);
+
+/* FMIndex::build_from_text — fm_index.hpp:19, fm_index.cpp:16-69.
+ * Builds the whole index on `device` (suffix array by prefix doubling, cyclic BWT,
+ * C[], 8-level wavelet matrix, row-sampled SSA).  `text` is a host pointer. */
+cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_params* p,
+                                int device, cs_fm_index** out);
+/* Same, with the text already in device memory on `device`. */
+cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
+                                       const cs_build_params* p, int device,
+                                       cs_fm_index** out);
+/* FMIndex::open_directory — fm_index.hpp:20, fm_index.cpp:71-73 (throws there):
+ * returns CS_ERR_UNSUPPORTED with the reference's message. */
+cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out);
+void cs_fm_destroy(cs_fm_index* h);
+cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out);
+const char* cs_fm_last_error(void);
+
+/* FMIndex::count — fm_index.hpp:26, fm_index.cpp:79-101 (one pattern, host). */
+cs_status cs_fm_count(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t* out);
+/* FMIndex::locate — fm_index.hpp:32, fm_index.cpp:107-157 (one pattern, host).
+ * Positions in BWT-row order; at most min(limit, cap) written; *nout = number. */
+cs_status cs_fm_locate(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t limit,
+                       uint64_t* out, uint64_t cap, uint64_t* nout);
+/* FMIndex::extract — fm_index.hpp:37, fm_index.cpp:163-167 (clamped substring). */
+cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_t* out,
+                        uint64_t* nout);
+
+/* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers. */
+cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
+                            uint64_t npat, uint64_t* out_counts, void* stream);
+/* Batched locate, host buffers.  out_offs has npat+1 entries (CSR into out_pos).
+ * *total = sum_q min(count_q, limit) (0 for empty patterns, fm_index.cpp:109).
+ * If *total > cap: CS_ERR_CAPACITY, out_offs valid, out_pos untouched. */
+cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
+                             uint64_t npat, uint64_t limit, uint64_t* out_offs, uint64_t* out_pos,
+                             uint64_t cap, uint64_t* total, void* stream);
+
+/* Device-resident batch entry points (no host staging, asynchronous on `stream`
+ * unless stated). */
+cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
+                                   void* stream);
+/* locate phase 1: backward search; d_sp[q] = first row, d_out_offs = exclusive scan
+ * of min(count, limit) (npat+1 entries).  Synchronises `stream` to return *total. */
+cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                     const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                                     uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                                     void* stream);
+/* locate phase 2: LF walk to the sampled rows and SSA lookup for every reported
+ * row.  d_out_pos has `total` entries.  Synchronises `stream` (error check). */
+cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,
+                                   const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                                   uint64_t* d_out_pos, void* stream);
+/* Phase 2 without the final synchronisation, for timing loops: the LF-overrun
+ * flag is checked by the next cs_fm_locate_check call. */
+cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d_sp,
+                                         const uint64_t* d_out_offs, uint64_t npat,
+                                         uint64_t total, uint64_t* d_out_pos, void* stream);
+cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream);
+
+/* Building blocks, for parity tests (host arrays in/out):
+ *   level rank1   — BitVector::rank1 of wavelet level l (src/core/bitvector.cpp:165-230)
+ *   wavelet rank  — WaveletTree::rank (src/core/wavelet.cpp:59-96)
+ *   access        — WaveletTree::access (src/core/wavelet.cpp:102-128) = BWT[i]
+ *   LF            — FMIndex::LF (src/api/fm_index.hpp:62-66) */
+cs_status cs_fm_level_rank1(const cs_fm_index* h, int level, const uint64_t* pos, uint64_t k,
+                            uint64_t* out);
+cs_status cs_fm_wt_rank(const cs_fm_index* h, const uint8_t* syms, const uint64_t* pos,
+                        uint64_t k, uint64_t* out);
+cs_status cs_fm_wt_access(const cs_fm_index* h, const uint64_t* pos, uint64_t k, uint8_t* out);
+cs_status cs_fm_lf(const cs_fm_index* h, const uint64_t* rows, uint64_t k, uint64_t* out);
+cs_status cs_fm_get_C(const cs_fm_index* h, uint64_t* out257);
+/* The whole BWT (WaveletTree::access for every row) into device memory d_out (n
+ * bytes), asynchronous on stream. */
+cs_status cs_fm_bwt_device(const cs_fm_index* h, uint8_t* d_out, void* stream);
+cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint64_t* len);
+
+/* Suffix array of text (host in/out) by the device builder — src/core/sais.hpp:8-16
+ * order (a proper prefix sorts first). */
+cs_status cs_sa_build(const uint8_t* text, uint64_t n, uint32_t* sa_out, int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CS_FMINDEX_H */

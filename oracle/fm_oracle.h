@@ -67,6 +67,7 @@ void orc_bwt_from_sa(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_
 orc_index* orc_build(const uint8_t* text, uint64_t n, uint32_t ssa_stride, int sa_algo);
 /* count-only index from a BWT (no text, no SA): used by the CPU baseline */
 orc_index* orc_build_from_bwt(const uint8_t* bwt, uint64_t n);
+orc_index* orc_build_from_bwt_mt(const uint8_t* bwt, uint64_t n, int nthreads);
 void orc_free(orc_index* idx);
 uint64_t orc_n(const orc_index* idx);
 uint32_t orc_ssa_stride(const orc_index* idx);

@@ -59,6 +59,7 @@ def lib():
         "orc_sa_doubling": (None, [_u8p, C.c_uint64, _u64p]),
         "orc_build": (_vp, [_u8p, C.c_uint64, C.c_uint32, C.c_int]),
         "orc_build_from_bwt": (_vp, [_u8p, C.c_uint64]),
+        "orc_build_from_bwt_mt": (_vp, [_u8p, C.c_uint64, C.c_int]),
         "orc_free": (None, [_vp]),
         "orc_n": (C.c_uint64, [_vp]),
         "orc_ssa_stride": (C.c_uint32, [_vp]),
@@ -182,12 +183,12 @@ class LevelView:
 class Index:
     """cs::FMIndex restated (src/api/fm_index.{hpp,cpp})."""
 
-    def __init__(self, text=None, ssa_stride=32, sa_algo=0, bwt=None):
+    def __init__(self, text=None, ssa_stride=32, sa_algo=0, bwt=None, nthreads=1):
         L = lib()
         if bwt is not None:
             b = as_u8(bwt)
-            self._keep = b
-            self._h = L.orc_build_from_bwt(_u8(b) if len(b) else _u8(np.zeros(1, np.uint8)), len(b))
+            self._h = L.orc_build_from_bwt_mt(_u8(b) if len(b) else _u8(np.zeros(1, np.uint8)),
+                                             len(b), nthreads)
         else:
             t = as_u8(text)
             tt = t if len(t) else np.zeros(1, np.uint8)

@@ -1,0 +1,92 @@
+"""CPU-side checks of the C ABI library (no GPU needed, no compute calls).
+
+- libcs_fmindex.so loads and exports every entry point declared in
+  include/cs_fmindex.h (and the Python mirror binds exactly those);
+- the product fails loudly without a GPU (CS_ERR_NO_DEVICE), never falling back
+  to a CPU path;
+- reference behaviours that need no device (open_directory throws with the
+  reference's message, src/api/fm_index.cpp:71-73).
+"""
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT, load_pkg
+
+HEADERS = sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))
+
+
+def header_symbols():
+    syms = set()
+    for h in HEADERS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        syms |= set(re.findall(r"\b(cs_[A-Za-z0-9_]+)\s*\(", src))
+    return sorted(syms)
+
+
+def test_header_declares_boundary():
+    syms = header_symbols()
+    for s in ["cs_fm_build_from_text", "cs_fm_count", "cs_fm_locate", "cs_fm_extract",
+              "cs_fm_count_batch_device", "cs_fm_locate_ranges_device", "cs_fm_locate_walk_device",
+              "cs_fm_open_directory", "cs_fm_destroy"]:
+        assert s in syms
+
+
+def test_library_exports_every_symbol():
+    pkg = load_pkg()
+    L = pkg.lib()
+    syms = header_symbols()
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert sorted(pkg.SIGNATURES) == syms
+    out = subprocess.run(["nm", "-D", "--defined-only", pkg.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (cs_[A-Za-z0-9_]+)$", out, flags=re.M))
+    assert set(syms) <= exported
+
+
+def test_library_targets_gfx950():
+    pkg = load_pkg()
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", pkg.LIB_PATH],
+                         capture_output=True, text=True).stdout
+    blob = open(pkg.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob or "gfx950" in out
+
+
+def _no_gpu():
+    try:
+        import torch
+        return not torch.cuda.is_available()
+    except Exception:
+        return True
+
+
+@pytest.mark.skipif(not _no_gpu(), reason="checks the no-device failure path")
+def test_fails_loudly_without_gpu():
+    pkg = load_pkg()
+    with pytest.raises(pkg.FMIndexError) as ei:
+        pkg.FMIndex.build_from_text(b"banana$")
+    assert ei.value.status == pkg.CS_ERR_NO_DEVICE
+    assert "GPU" in str(ei.value)
+    with pytest.raises(pkg.FMIndexError):
+        pkg.sa_build(b"banana$")
+
+
+def test_open_directory_throws_like_reference():
+    pkg = load_pkg()
+    with pytest.raises(RuntimeError) as ei:
+        pkg.FMIndex.open_directory("/nonexistent")
+    assert str(ei.value) == "on-disk open not implemented yet"
+
+
+def test_build_params_defaults_match_reference():
+    """src/api/fm_index.hpp:11-14."""
+    pkg = load_pkg()
+    p = pkg.BuildParams()
+    assert (p.S, p.s, p.ssa_stride, p.eps) == (512, 64, 32, 1.0)
+    c = pkg.cs_build_params()
+    pkg.lib().cs_default_build_params(c)
+    assert (c.S, c.s, c.ssa_stride, c.eps) == (512, 64, 32, 1.0)
