@@ -51,9 +51,9 @@ __global__ void k_hist(const uint8_t* __restrict__ t, uint64_t n,
 // Initial key: the first K symbols, dense codes 1..sigma (0 past the end, so a
 // proper prefix sorts first), b bits each.
 __global__ void k_init_keys(const uint8_t* __restrict__ t, uint64_t n,
-                            const uint8_t* __restrict__ code_g, int b, int K,
+                            const uint16_t* __restrict__ code_g, int b, int K,
                             uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
-  __shared__ uint8_t code[256];
+  __shared__ uint16_t code[256];
   for (int i = threadIdx.x; i < 256; i += blockDim.x) code[i] = code_g[i];
   __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -202,15 +202,15 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
   unsigned long long hist[256];
   FMX_HIP(hipMemcpyAsync(hist, d_hist.p, sizeof hist, hipMemcpyDeviceToHost, st));
   FMX_HIP(hipStreamSynchronize(st));
-  uint8_t code[256];
+  uint16_t code[256];  // 1..sigma, sigma <= 256 needs 9 bits
   int sigma = 0;
-  for (int c = 0; c < 256; ++c) code[c] = hist[c] ? (uint8_t)(++sigma) : 0;
+  for (int c = 0; c < 256; ++c) code[c] = hist[c] ? (uint16_t)(++sigma) : 0;
   int b = 1;
   while ((1 << b) <= sigma) ++b;  // codes 0..sigma need b bits
   const int K = 64 / b;
   DevBuf d_code;
-  FMX_HIP(d_code.alloc(256));
-  FMX_HIP(hipMemcpyAsync(d_code.p, code, 256, hipMemcpyHostToDevice, st));
+  FMX_HIP(d_code.alloc(sizeof code));
+  FMX_HIP(hipMemcpyAsync(d_code.p, code, sizeof code, hipMemcpyHostToDevice, st));
 
   DevBuf k0, k1, v1, hp, hp2, rank, d_ng;
   FMX_HIP(k0.alloc(n * 8));
@@ -223,7 +223,7 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
   uint32_t* v0 = d_sa;  // sorted values end up in either buffer; copied to d_sa at the end
 
   const unsigned G = grid_for(n, kBlk, 16384);
-  k_init_keys<<<G, kBlk, 0, st>>>(d_text, n, d_code.as<uint8_t>(), b, K, k0.as<uint64_t>(), v0);
+  k_init_keys<<<G, kBlk, 0, st>>>(d_text, n, d_code.as<uint16_t>(), b, K, k0.as<uint64_t>(), v0);
   FMX_HIP(hipGetLastError());
 
   int B = 1;
