@@ -15,6 +15,9 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "fm_internal.hpp"
@@ -112,68 +115,100 @@ __global__ void k_bwt_ssa(const uint8_t* __restrict__ t, const uint32_t* __restr
   }
 }
 
-// One wave per 64-bit payload word: ballot of the level bit.
+// Payload word w of a level (global word index) lives in line w/7, slot w%7.
+template <class F>
+__device__ __forceinline__ void store_word(void* L, uint64_t w, uint64_t v) {
+  const uint64_t line = w / F::kWords, slot = w % F::kWords;
+  if (F::kWordBits == 32)
+    reinterpret_cast<uint32_t*>(L)[line * 8 + 1 + slot] = (uint32_t)v;
+  else
+    reinterpret_cast<uint64_t*>(L)[line * 8 + 1 + slot] = v;
+}
+
+// One wave per 64 positions: ballot of the level bit (= 1 or 2 payload words).
+template <class F>
 __global__ void k_pack_level(const uint8_t* __restrict__ cur, uint64_t n, int bit,
-                             RankLine* __restrict__ L, uint64_t nwords) {
+                             void* __restrict__ L, uint64_t ngroups) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-  for (uint64_t g = wave; g < nwords; g += nwaves) {
+  for (uint64_t g = wave; g < ngroups; g += nwaves) {
     const uint64_t p = g * 64 + lane;
     const int b = p < n ? (cur[p] >> bit) & 1 : 0;
     const uint64_t w = __ballot(b);
-    if (lane == 0) L[g / kLineWords].w[g % kLineWords] = w;
+    if (F::kWordBits == 64) {
+      if (lane == 0) store_word<F>(L, g, w);
+    } else {
+      if (lane == 0) store_word<F>(L, 2 * g, w & 0xFFFFFFFFull);
+      if (lane == 1) store_word<F>(L, 2 * g + 1, w >> 32);
+    }
   }
 }
 
-__global__ void k_line_counts(const RankLine* __restrict__ L, uint64_t nlines,
+template <class F>
+__global__ void k_line_counts(const void* __restrict__ L, uint64_t nlines,
                               uint64_t* __restrict__ cnt) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nlines; l += stride) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < kLineWords; ++k) c += __popcll(L[l].w[k]);
-    cnt[l] = c;
+    typename F::Raw v;
+    F::load(L, l, v);
+    cnt[l] = F::prefix(v, F::kBits);
   }
 }
 
-__global__ void k_set_base(RankLine* __restrict__ L, const uint64_t* __restrict__ base,
+template <class F>
+__global__ void k_set_base(void* __restrict__ L, const uint64_t* __restrict__ base,
                            uint64_t nlines) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nlines; l += stride)
-    L[l].base = base[l];
+  for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nlines; l += stride) {
+    if (F::kWordBits == 32)
+      reinterpret_cast<uint32_t*>(L)[l * 8] = (uint32_t)base[l];
+    else
+      reinterpret_cast<uint64_t*>(L)[l * 8] = base[l];
+  }
 }
 
 // Stable zeros-then-ones partition (wavelet.cpp:27-30, :47-50) using the level's
 // own rank lines: dst = b ? Z + rank1(p) : p - rank1(p).
+template <class F>
 __global__ void k_partition(const uint8_t* __restrict__ cur, uint64_t n, int bit,
-                            const RankLine* __restrict__ L, uint64_t Z, uint8_t* __restrict__ nxt) {
+                            const void* __restrict__ L, uint64_t Z, uint8_t* __restrict__ nxt) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < n; p += stride) {
     const uint8_t s = cur[p];
-    uint32_t q, o;
-    line_of(p, q, o);
-    uint4 v[4];
-    load_line(L, q, v);
-    const uint64_t r = line_base(v) + prefix_pop(v, o);
+    const uint64_t r = rank1_at<F>(L, p);
     const uint64_t dst = ((s >> bit) & 1) ? Z + r : p - r;
     nxt[dst] = s;
   }
 }
 
-__global__ void k_node_rank(const RankLine* __restrict__ lines, uint64_t nlines,
+template <class F>
+__global__ void k_node_rank(const void* __restrict__ lines, uint64_t nlines,
                             const NodeTable* __restrict__ T, uint64_t* __restrict__ R) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= kNodes) return;
   int level = 0;
   while ((1 << (level + 1)) - 1 <= t) ++level;
-  const uint64_t p = T->S[t];
-  uint32_t q, o;
-  line_of(p, q, o);
-  uint4 v[4];
-  load_line(lines + (uint64_t)level * nlines, q, v);
-  R[t] = line_base(v) + prefix_pop(v, o);
+  const void* lv = reinterpret_cast<const uint8_t*>(lines) + (uint64_t)level * nlines * F::kBytes;
+  R[t] = rank1_at<F>(lv, T->S[t]);
 }
+
+// CS_FM_VERBOSE=1: phase timings of the build on stderr.
+struct PhaseLog {
+  bool on;
+  hipStream_t st;
+  std::chrono::steady_clock::time_point t0;
+  explicit PhaseLog(hipStream_t s) : on(std::getenv("CS_FM_VERBOSE") != nullptr), st(s),
+                                     t0(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    (void)hipStreamSynchronize(st);
+    const auto t = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[cs_fm build] %-28s %9.1f ms\n", what,
+                 std::chrono::duration<double, std::milli>(t - t0).count());
+    t0 = t;
+  }
+};
 
 uint32_t bitrev(uint32_t x, int bits) {
   uint32_t r = 0;
@@ -187,6 +222,48 @@ struct SortTemp {
 };
 
 }  // namespace
+
+// 8 wavelet-matrix levels (wavelet.cpp:14-53) from the BWT in `cur` (consumed).
+template <class F>
+static cs_status build_levels(uint8_t* cur, uint64_t n, cs_fm_index* h, hipStream_t st) {
+  const uint64_t nl = h->nlines;
+  const size_t lbytes = (size_t)kLevels * nl * F::kBytes;
+  FMX_HIP(hipMalloc(&h->d_lines, lbytes));
+  FMX_HIP(hipMemsetAsync(h->d_lines, 0, lbytes, st));
+  NodeTable& T = h->h_table;  // Z[] filled here, the rest by the caller
+  DevBuf nxt, cnt, base, tmp;
+  FMX_HIP(nxt.alloc(n));
+  FMX_HIP(cnt.alloc(nl * 8));
+  FMX_HIP(base.alloc(nl * 8));
+  size_t tmp_bytes = 0;
+  FMX_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.as<uint64_t>(), base.as<uint64_t>(),
+                                  (uint64_t)0, nl, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(tmp.alloc(tmp_bytes));
+  uint8_t* nx = nxt.as<uint8_t>();
+  const uint64_t ngroups = nl * F::kWords * F::kWordBits / 64;
+  for (int l = 0; l < kLevels; ++l) {
+    const int bit = 7 - l;
+    void* L = reinterpret_cast<uint8_t*>(h->d_lines) + (uint64_t)l * nl * F::kBytes;
+    k_pack_level<F><<<grid_for(ngroups * 64, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, ngroups);
+    k_line_counts<F><<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, nl, cnt.as<uint64_t>());
+    size_t tb = tmp_bytes;
+    FMX_HIP(rocprim::exclusive_scan(tmp.p, tb, cnt.as<uint64_t>(), base.as<uint64_t>(), (uint64_t)0,
+                                    nl, rocprim::plus<uint64_t>(), st));
+    k_set_base<F><<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, base.as<uint64_t>(), nl);
+    uint64_t last[2];
+    FMX_HIP(hipMemcpyAsync(&last[0], base.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipMemcpyAsync(&last[1], cnt.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    T.Z[l] = n - (last[0] + last[1]);
+    if (l + 1 < kLevels && n) {
+      k_partition<F><<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, T.Z[l], nx);
+      FMX_HIP(hipGetLastError());
+      std::swap(cur, nx);
+    }
+  }
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
 
 cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st) {
   if (n == 0) return CS_OK;
@@ -222,6 +299,8 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
   FMX_HIP(d_ng.alloc(8));
   uint32_t* v0 = d_sa;  // sorted values end up in either buffer; copied to d_sa at the end
 
+  PhaseLog plog(st);
+  plog.mark("sa: histogram+alloc");
   const unsigned G = grid_for(n, kBlk, 16384);
   k_init_keys<<<G, kBlk, 0, st>>>(d_text, n, d_code.as<uint16_t>(), b, K, k0.as<uint64_t>(), v0);
   FMX_HIP(hipGetLastError());
@@ -241,6 +320,7 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
       tmp.bytes = need;
     }
     FMX_HIP(rocprim::radix_sort_pairs(tmp.buf.p, need, kb, vb, n, 0, end_bit, st));
+    plog.mark("sa: radix sort");
     const uint64_t* skey = kb.current();
     const uint32_t* sval = vb.current();
     FMX_HIP(hipMemsetAsync(d_ng.p, 0, 8, st));
@@ -257,6 +337,9 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
     unsigned long long ng = 0;
     FMX_HIP(hipMemcpyAsync(&ng, d_ng.p, 8, hipMemcpyDeviceToHost, st));
     FMX_HIP(hipStreamSynchronize(st));
+    plog.mark("sa: heads+scan");
+    if (plog.on) std::fprintf(stderr, "[cs_fm build] sa round %d: h=%llu groups=%llu of %llu\n",
+                              iter, (unsigned long long)h, ng, (unsigned long long)n);
     if (ng == n) {  // every suffix has a distinct h-prefix: sval is the SA
       if (sval != d_sa) FMX_HIP(hipMemcpyAsync(d_sa, sval, n * 4, hipMemcpyDeviceToDevice, st));
       FMX_HIP(hipStreamSynchronize(st));
@@ -287,8 +370,9 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   }
   h->n = n;
   h->stride = stride;
-  h->nlines = n / kLineBits + 1;  // + sentinel so rank1(n) is a line read
   h->nsamples = (n + stride - 1) / stride;
+  NodeTable& T = h->h_table;
+  std::memset(&T, 0, sizeof T);
 
   // --- histogram (BWT is a permutation of the text) ---
   unsigned long long hist[256] = {0};
@@ -302,6 +386,8 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     FMX_HIP(hipStreamSynchronize(st));
   }
 
+  PhaseLog plog(st);
+  plog.mark("histogram");
   // --- SA, BWT, SSA ---
   DevBuf bwt;
   FMX_HIP(bwt.alloc(n));
@@ -316,50 +402,19 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipStreamSynchronize(st));
   }
+  plog.mark("suffix array + bwt + ssa");
 
   // --- wavelet matrix levels as rank lines ---
-  const uint64_t nl = h->nlines;
-  FMX_HIP(hipMalloc(&h->d_lines, (size_t)kLevels * nl * sizeof(RankLine)));
-  FMX_HIP(hipMemsetAsync(h->d_lines, 0, (size_t)kLevels * nl * sizeof(RankLine), st));
-  NodeTable& T = h->h_table;
-  std::memset(&T, 0, sizeof T);
-  {
-    DevBuf nxt, cnt, base;
-    FMX_HIP(nxt.alloc(n));
-    FMX_HIP(cnt.alloc(nl * 8));
-    FMX_HIP(base.alloc(nl * 8));
-    DevBuf tmp;
-    size_t tmp_bytes = 0;
-    FMX_HIP(rocprim::exclusive_scan(nullptr, tmp_bytes, cnt.as<uint64_t>(), base.as<uint64_t>(),
-                                    (uint64_t)0, nl, rocprim::plus<uint64_t>(), st));
-    FMX_HIP(tmp.alloc(tmp_bytes));
-    uint8_t* cur = bwt.as<uint8_t>();
-    uint8_t* nx = nxt.as<uint8_t>();
-    const uint64_t nwords = nl * kLineWords;
-    for (int l = 0; l < kLevels; ++l) {
-      const int bit = 7 - l;
-      RankLine* L = h->d_lines + (uint64_t)l * nl;
-      k_pack_level<<<grid_for(nwords * 64, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, nwords);
-      k_line_counts<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, nl, cnt.as<uint64_t>());
-      size_t tb = tmp_bytes;
-      FMX_HIP(rocprim::exclusive_scan(tmp.p, tb, cnt.as<uint64_t>(), base.as<uint64_t>(),
-                                      (uint64_t)0, nl, rocprim::plus<uint64_t>(), st));
-      k_set_base<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, base.as<uint64_t>(), nl);
-      uint64_t last[2];
-      FMX_HIP(hipMemcpyAsync(&last[0], base.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
-      FMX_HIP(hipMemcpyAsync(&last[1], cnt.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
-      FMX_HIP(hipStreamSynchronize(st));
-      const uint64_t ones = last[0] + last[1];
-      T.Z[l] = n - ones;
-      if (l + 1 < kLevels && n) {
-        k_partition<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, T.Z[l], nx);
-        FMX_HIP(hipGetLastError());
-        std::swap(cur, nx);
-      }
-    }
-    FMX_HIP(hipStreamSynchronize(st));
-  }
+  h->line_bytes = n < (1ull << 32) ? 32 : 64;
+  if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force a format
+    if (std::atoi(e) == 64) h->line_bytes = 64;
+  h->line_bits = h->line_bytes == 32 ? Line32::kBits : Line64::kBits;
+  h->nlines = n / h->line_bits + 1;  // + sentinel so rank1(n) is a line read
+  cs_status ws = h->line_bytes == 32 ? build_levels<Line32>(bwt.as<uint8_t>(), n, h, st)
+                                     : build_levels<Line64>(bwt.as<uint8_t>(), n, h, st);
+  if (ws != CS_OK) return ws;
   bwt.release();
+  plog.mark("wavelet levels");
 
   // --- node table from the histogram ---
   uint64_t cum = 0;
@@ -409,7 +464,10 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   {
     DevBuf dR;
     FMX_HIP(dR.alloc(kNodes * 8));
-    k_node_rank<<<1, kBlk, 0, st>>>(h->d_lines, nl, h->d_table, dR.as<uint64_t>());
+    if (h->line_bytes == 32)
+      k_node_rank<Line32><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
+    else
+      k_node_rank<Line64><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipMemcpyAsync(T.R, dR.p, kNodes * 8, hipMemcpyDeviceToHost, st));
     FMX_HIP(hipStreamSynchronize(st));
@@ -418,6 +476,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   FMX_HIP(hipMalloc(&h->d_err, 8));
   FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));
+  plog.mark("node table");
   return CS_OK;
 }
 

@@ -168,9 +168,9 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   std::memset(out, 0, sizeof *out);
   out->n = h->n;
   out->ssa_stride = h->stride;
-  out->line_bits = kLineBits;
+  out->line_bits = h->line_bits;
   out->lines_per_level = h->nlines;
-  out->rank_bytes = (uint64_t)kLevels * h->nlines * sizeof(RankLine);
+  out->rank_bytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
   out->ssa_bytes = h->nsamples * 4;
   std::memcpy(out->active_levels, h->active_levels, sizeof out->active_levels);
   out->device = h->device;

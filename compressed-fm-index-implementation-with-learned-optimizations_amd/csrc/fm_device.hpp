@@ -4,17 +4,20 @@
 // levels, level l holds bit (7-l) of the level-l sequence; the next sequence is the
 // stable zeros-then-ones partition.  Each level's BitVector (src/core/bitvector.hpp:
 // 95-98: bits_ + super_ u32 every 2048 bits + blocks_ u16 every 256 bits) is stored
-// re-laid-out as 64-byte RANK LINES:
+// re-laid-out as RANK LINES, one HBM access per rank1:
 //
-//     struct RankLine { u64 base; u64 w[7]; }   // 64 B, 64-B aligned
+//   Line32  { u32 base; u32 w[7]; }   32 B, 224 payload bits   (n < 2^32)
+//   Line64  { u64 base; u64 w[7]; }   64 B, 448 payload bits   (any n < 2^38)
 //
-// covering 448 bits: base = rank1 at the line's first bit (absolute), w[k] = bits
-// [448L + 64k, +64) LSB-first.  rank1(i) = base + popcount of the bits of line i/448
-// below i — one 64-B HBM granule per rank instead of the reference's three arrays.
-// rank1(i) equals BitVector::rank1(i) for every 0 <= i <= n (tests/test_gpu_parity
-// checks every position against the oracle).  A sentinel line past n makes
-// rank1(n) (the reference's count_ones() special case, bitvector.cpp:168-170) a
-// plain line read.
+// base = rank1 at the line's first bit (absolute), w[] = the bits LSB-first.
+// rank1(i) = base + popcount of the line's bits below i.  MI355X serves random
+// 16/32-B reads at ~50 G/s and 64-B reads at ~26 G/s (profiles/microbench:
+// DRAM access granularity is 32 B), so the 32-B line halves the DRAM cost of a
+// rank; it is used whenever the text fits u32 ranks (the reference's own limit,
+// SURVEY.md §0.6).  rank1(i) equals BitVector::rank1(i) for every 0 <= i <= n
+// (tests/test_gpu_parity.py checks every position against the oracle).  A
+// sentinel line past n makes rank1(n) (the reference's count_ones() special case,
+// bitvector.cpp:168-170) a plain line read.
 //
 // Node table: the wavelet-matrix node of prefix x (top l bits of a symbol) at level
 // l is a contiguous block [S, S+size) of level l.  R = rank1_l(S).  A node is PURE
@@ -29,101 +32,140 @@
 namespace fmx {
 
 constexpr int kLevels = 8;
-constexpr int kLineWords = 7;                 // payload words per line
-constexpr uint32_t kLineBits = 64 * kLineWords;  // 448
-constexpr int kNodes = 255;                   // internal nodes, levels 0..7
+constexpr int kNodes = 255;  // internal nodes, levels 0..7
 constexpr uint8_t kPure = 1, kPureBit = 2;
-
-struct alignas(64) RankLine {
-  uint64_t base;
-  uint64_t w[kLineWords];
-};
-static_assert(sizeof(RankLine) == 64, "rank line must be one 64-B granule");
 
 // Everything the query kernels read besides the rank lines; copied into LDS by
 // every block (8.5 KB).
 struct NodeTable {
-  uint64_t S[kNodes];        // node start in its level
-  uint64_t R[kNodes];        // rank1_l(S)
-  uint64_t Z[kLevels];       // zeros per level (size - ones)
-  uint64_t C[257];           // fm_index.cpp:36-47 (u64)
-  uint64_t S8[256];          // start of each symbol's run after the last level
-  uint8_t flags[256];        // kPure | kPureBit per node
+  uint64_t S[kNodes];   // node start in its level
+  uint64_t R[kNodes];   // rank1_l(S)
+  uint64_t Z[kLevels];  // zeros per level (size - ones)
+  uint64_t C[257];      // fm_index.cpp:36-47 (u64)
+  uint64_t S8[256];     // start of each symbol's run after the last level
+  uint8_t flags[256];   // kPure | kPureBit per node
 };
 
 struct DevIndex {
-  const RankLine* lines;     // kLevels * nlines
-  uint64_t nlines;           // per level = n/448 + 1
+  const void* lines;     // kLevels * nlines rank lines of the handle's format
+  uint64_t nlines;       // per level = n / line_bits + 1
   uint64_t n;
-  const uint32_t* ssa;       // row-sampled SA (fm_index.cpp:57-66), u32 as the reference
+  const uint32_t* ssa;   // row-sampled SA (fm_index.cpp:57-66), u32 as the reference
   uint64_t nsamples;
   uint32_t stride;
-  uint32_t stride_shift;     // log2(stride) when stride is a power of two, else 0xFFFFFFFF
-  const NodeTable* table;    // global copy
+  uint32_t stride_shift; // log2(stride) when stride is a power of two, else 0xFFFFFFFF
+  const NodeTable* table;
 };
 
 __host__ __device__ inline int node_id(int level, uint32_t prefix) {
   return (1 << level) - 1 + (int)prefix;
 }
 
-// Line index / offset of bit position p.  p < 2^38 so p>>6 fits 32 bits and the
-// division by 7 is a 32-bit multiply-high.
-__device__ __forceinline__ void line_of(uint64_t p, uint32_t& q, uint32_t& o) {
-  const uint32_t g = (uint32_t)(p >> 6);
-  q = g / (uint32_t)kLineWords;
-  o = (uint32_t)(p - (uint64_t)q * kLineBits);
-}
-
-// Load one rank line as four 16-B vector loads (global_load_dwordx4).
-__device__ __forceinline__ void load_line(const RankLine* __restrict__ lines, uint64_t idx,
-                                          uint4 (&v)[4]) {
-  const uint4* p = reinterpret_cast<const uint4*>(lines + idx);
-  v[0] = p[0];
-  v[1] = p[1];
-  v[2] = p[2];
-  v[3] = p[3];
-}
-
 __device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// popcount of the first o bits of the 448-bit payload (o in [0, 448]).
-__device__ __forceinline__ uint32_t prefix_pop(const uint4 (&v)[4], uint32_t o) {
-  const uint64_t w[7] = {u64_of(v[0].z, v[0].w), u64_of(v[1].x, v[1].y), u64_of(v[1].z, v[1].w),
-                         u64_of(v[2].x, v[2].y), u64_of(v[2].z, v[2].w), u64_of(v[3].x, v[3].y),
-                         u64_of(v[3].z, v[3].w)};
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int sh = (int)o - 64 * k;
-    const uint64_t m = sh >= 64 ? ~0ull : (sh <= 0 ? 0ull : ((1ull << sh) - 1));
-    r += (uint32_t)__popcll(w[k] & m);
+// ---------------------------------------------------------------------------
+// 32-byte line: dword 0 = base, dwords 1..7 = payload (224 bits)
+struct Line32 {
+  static constexpr uint32_t kBytes = 32;
+  static constexpr uint32_t kWordBits = 32;
+  static constexpr int kWords = 7;
+  static constexpr uint32_t kBits = kWords * kWordBits;  // 224
+  using Raw = uint4[2];
+
+  // p < 2^32 * 32: q = (p/32)/7 in 32-bit arithmetic
+  __device__ static __forceinline__ void locate(uint64_t p, uint32_t& q, uint32_t& o) {
+    const uint32_t g = (uint32_t)(p >> 5);
+    q = g / 7u;
+    o = (uint32_t)(p - (uint64_t)q * kBits);
   }
-  return r;
-}
-
-__device__ __forceinline__ uint32_t bit_at(const uint4 (&v)[4], uint32_t o) {
-  const uint32_t wd = 2 + (o >> 5);  // dword index within the 16-dword line
-  const uint32_t dw[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
-                           v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
-  uint32_t d = 0;
+  __device__ static __forceinline__ void load(const void* lines, uint64_t idx, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + idx * 2;
+    v[0] = p[0];
+    v[1] = p[1];
+  }
+  __device__ static __forceinline__ uint64_t base(const Raw& v) { return v[0].x; }
+  // popcount of the first o payload bits, o in [0, 224]
+  __device__ static __forceinline__ uint32_t prefix(const Raw& v, uint32_t o) {
+    const uint32_t w[7] = {v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    uint32_t r = 0;
 #pragma unroll
-  for (int k = 2; k < 16; ++k) d = (wd == (uint32_t)k) ? dw[k] : d;
-  return (d >> (o & 31)) & 1u;
-}
+    for (int k = 0; k < 7; ++k) {
+      const int sh = (int)o - 32 * k;
+      const uint32_t m = sh >= 32 ? ~0u : (sh <= 0 ? 0u : ((1u << sh) - 1u));
+      r += (uint32_t)__popc(w[k] & m);
+    }
+    return r;
+  }
+  __device__ static __forceinline__ uint32_t bit(const Raw& v, uint32_t o) {
+    const uint32_t w[7] = {v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    const uint32_t k = o >> 5;
+    uint32_t d = w[0];
+#pragma unroll
+    for (int j = 1; j < 7; ++j) d = (k == (uint32_t)j) ? w[j] : d;
+    return (d >> (o & 31)) & 1u;
+  }
+};
 
-__device__ __forceinline__ uint64_t line_base(const uint4 (&v)[4]) {
-  return u64_of(v[0].x, v[0].y);
-}
+// 64-byte line: qword 0 = base, qwords 1..7 = payload (448 bits)
+struct Line64 {
+  static constexpr uint32_t kBytes = 64;
+  static constexpr uint32_t kWordBits = 64;
+  static constexpr int kWords = 7;
+  static constexpr uint32_t kBits = kWords * kWordBits;  // 448
+  using Raw = uint4[4];
 
-// rank1_l(p) with one 64-B line read.
-__device__ __forceinline__ uint64_t rank1_dev(const DevIndex& ix, int level, uint64_t p) {
+  __device__ static __forceinline__ void locate(uint64_t p, uint32_t& q, uint32_t& o) {
+    const uint32_t g = (uint32_t)(p >> 6);
+    q = g / 7u;
+    o = (uint32_t)(p - (uint64_t)q * kBits);
+  }
+  __device__ static __forceinline__ void load(const void* lines, uint64_t idx, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + idx * 4;
+    v[0] = p[0];
+    v[1] = p[1];
+    v[2] = p[2];
+    v[3] = p[3];
+  }
+  __device__ static __forceinline__ uint64_t base(const Raw& v) { return u64_of(v[0].x, v[0].y); }
+  __device__ static __forceinline__ uint32_t prefix(const Raw& v, uint32_t o) {
+    const uint64_t w[7] = {u64_of(v[0].z, v[0].w), u64_of(v[1].x, v[1].y), u64_of(v[1].z, v[1].w),
+                           u64_of(v[2].x, v[2].y), u64_of(v[2].z, v[2].w), u64_of(v[3].x, v[3].y),
+                           u64_of(v[3].z, v[3].w)};
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int sh = (int)o - 64 * k;
+      const uint64_t m = sh >= 64 ? ~0ull : (sh <= 0 ? 0ull : ((1ull << sh) - 1));
+      r += (uint32_t)__popcll(w[k] & m);
+    }
+    return r;
+  }
+  __device__ static __forceinline__ uint32_t bit(const Raw& v, uint32_t o) {
+    const uint32_t dw[14] = {v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w, v[2].x,
+                             v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+    const uint32_t k = o >> 5;
+    uint32_t d = dw[0];
+#pragma unroll
+    for (int j = 1; j < 14; ++j) d = (k == (uint32_t)j) ? dw[j] : d;
+    return (d >> (o & 31)) & 1u;
+  }
+};
+
+// rank1 of level `lv` (pointer to that level's first line) at position p.
+template <class F>
+__device__ __forceinline__ uint64_t rank1_at(const void* lv, uint64_t p) {
   uint32_t q, o;
-  line_of(p, q, o);
-  uint4 v[4];
-  load_line(ix.lines, (uint64_t)level * ix.nlines + q, v);
-  return line_base(v) + prefix_pop(v, o);
+  F::locate(p, q, o);
+  typename F::Raw v;
+  F::load(lv, q, v);
+  return F::base(v) + F::prefix(v, o);
+}
+
+template <class F>
+__device__ __forceinline__ const void* level_ptr(const DevIndex& ix, int level) {
+  return reinterpret_cast<const uint8_t*>(ix.lines) + (uint64_t)level * ix.nlines * F::kBytes;
 }
 
 }  // namespace fmx

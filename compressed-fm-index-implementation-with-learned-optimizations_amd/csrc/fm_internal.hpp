@@ -13,8 +13,10 @@ struct cs_fm_index {
   int device = 0;
   uint64_t n = 0;
   uint32_t stride = 32;
-  fmx::RankLine* d_lines = nullptr;  // 8 levels x nlines
+  void* d_lines = nullptr;            // 8 levels x nlines rank lines
   uint64_t nlines = 0;
+  uint32_t line_bytes = 32;           // 32 (Line32, n < 2^32) or 64 (Line64)
+  uint32_t line_bits = 224;
   uint32_t* d_ssa = nullptr;
   uint64_t nsamples = 0;
   fmx::NodeTable* d_table = nullptr;

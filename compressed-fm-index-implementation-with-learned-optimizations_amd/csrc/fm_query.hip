@@ -7,7 +7,7 @@
 // "relative" form: the start chain of c (start=0 mapped through the levels) is
 // fixed per symbol, so only d = end - start is carried:
 //     per level l with c's node not pure:  r = rank1_l(S + d) - R;  d = bit ? r : d - r
-// (S, R from the node table in LDS).  rank1_l = one 64-B rank line (fm_device.hpp).
+// (S, R from the node table in LDS).  rank1_l = one rank-line read (fm_device.hpp).
 // The first character costs nothing (sp = C[c], ep = C[c+1]); absent symbols and
 // empty ranges exit early exactly where the reference returns 0.
 //
@@ -37,6 +37,7 @@ __device__ __forceinline__ void load_table(NodeTable& T, const NodeTable* __rest
 
 // Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
 // range empties (the reference's `return 0`).  Requires m >= 1, n >= 1.
+template <class F>
 __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
                                                 const uint8_t* __restrict__ P, uint64_t m,
                                                 uint64_t& sp_out, uint64_t& ep_out) {
@@ -55,15 +56,15 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
       const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
       if (!(T.flags[nid] & kPure)) {
         const uint64_t S = T.S[nid], R = T.R[nid];
-        const RankLine* lv = ix.lines + (uint64_t)l * ix.nlines;
+        const void* lv = level_ptr<F>(ix, l);
         uint32_t qa, oa, qe, oe;
-        line_of(S + ds, qa, oa);
-        line_of(S + de, qe, oe);
-        uint4 va[4], ve[4];
-        load_line(lv, qa, va);
-        load_line(lv, qe, ve);
-        const uint64_t rs = line_base(va) + prefix_pop(va, oa) - R;
-        const uint64_t re = line_base(ve) + prefix_pop(ve, oe) - R;
+        F::locate(S + ds, qa, oa);
+        F::locate(S + de, qe, oe);
+        typename F::Raw va, ve;
+        F::load(lv, qa, va);
+        F::load(lv, qe, ve);
+        const uint64_t rs = F::base(va) + F::prefix(va, oa) - R;
+        const uint64_t re = F::base(ve) + F::prefix(ve, oe) - R;
         const bool b = (c >> (7 - l)) & 1u;
         ds = b ? rs : ds - rs;
         de = b ? re : de - re;
@@ -78,6 +79,7 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
   return true;
 }
 
+template <class F>
 __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t npat,
                                                 uint64_t* __restrict__ out) {
@@ -92,11 +94,12 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
   else if (ix.n == 0) res = 0;  // :81
   else {
     uint64_t sp, ep;
-    res = backward_search(ix, T, pats + o0, m, sp, ep) ? ep - sp : 0;
+    res = backward_search<F>(ix, T, pats + o0, m, sp, ep) ? ep - sp : 0;
   }
   out[q] = res;
 }
 
+template <class F>
 __global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
                                                         const uint8_t* __restrict__ pats,
                                                         const uint64_t* __restrict__ offs,
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
   const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
   uint64_t sp = 0, ep = 0;
   if (m && ix.n) {  // fm_index.cpp:109: empty pattern or empty text -> {}
-    if (!backward_search(ix, T, pats + o0, m, sp, ep)) sp = ep = 0;
+    if (!backward_search<F>(ix, T, pats + o0, m, sp, ep)) sp = ep = 0;
   }
   const uint64_t c = ep - sp;
   sp_out[q] = sp;
@@ -135,6 +138,7 @@ __global__ void k_expand_rows(const uint64_t* __restrict__ sp, const uint64_t* _
 // One LF step (fm_index.hpp:62-66): descend the wavelet matrix from row i reading
 // the BWT symbol bit by bit (WaveletTree::access, wavelet.cpp:102-128) while
 // mapping i; the leaf offset is rank(c, i).  Pure nodes cost no load.
+template <class F>
 __device__ __forceinline__ uint64_t lf_step(const DevIndex& ix, const NodeTable& T, uint64_t pos,
                                             uint32_t* sym_out = nullptr) {
   uint32_t x = 0;
@@ -149,11 +153,11 @@ __device__ __forceinline__ uint64_t lf_step(const DevIndex& ix, const NodeTable&
       r = T.R[nid] + (b ? pos - T.S[nid] : 0);
     } else {
       uint32_t q, o;
-      line_of(pos, q, o);
-      uint4 v[4];
-      load_line(ix.lines + (uint64_t)l * ix.nlines, q, v);
-      b = bit_at(v, o);
-      r = line_base(v) + prefix_pop(v, o);
+      F::locate(pos, q, o);
+      typename F::Raw v;
+      F::load(level_ptr<F>(ix, l), q, v);
+      b = F::bit(v, o);
+      r = F::base(v) + F::prefix(v, o);
     }
     pos = b ? T.Z[l] + r : pos - r;
     x = (x << 1) | b;
@@ -175,7 +179,7 @@ __device__ __forceinline__ uint64_t sample_index(const DevIndex& ix, uint64_t ro
 }
 
 // Persistent LF walk (fm_index.cpp:125-153).  Block b owns rows [b*chunk, ...).
-template <bool POW2>
+template <class F, bool POW2>
 __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint32_t* __restrict__ rows,
                                                uint64_t total, uint64_t chunk,
                                                uint64_t* __restrict__ out,
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint32_t* __re
         }
         active = false;
       } else {
-        pos = lf_step(ix, T, pos);
+        pos = lf_step<F>(ix, T, pos);
         ++steps;
       }
     }
@@ -222,6 +226,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint32_t* __re
 }
 
 // ---- building-block kernels for parity tests ----
+template <class F>
 __global__ void k_level_rank1(DevIndex ix, int level, const uint64_t* __restrict__ pos, uint64_t k,
                               uint64_t* __restrict__ out) {
   const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -229,9 +234,10 @@ __global__ void k_level_rank1(DevIndex ix, int level, const uint64_t* __restrict
   uint64_t p = pos[t];
   // BitVector::rank1(i >= size) = count_ones() (bitvector.cpp:168-170)
   if (p > ix.n) p = ix.n;
-  out[t] = rank1_dev(ix, level, p);
+  out[t] = rank1_at<F>(level_ptr<F>(ix, level), p);
 }
 
+template <class F>
 __global__ void k_wt_rank(DevIndex ix, const uint8_t* __restrict__ syms,
                           const uint64_t* __restrict__ pos, uint64_t k, uint64_t* __restrict__ out) {
   __shared__ NodeTable T;
@@ -247,7 +253,7 @@ __global__ void k_wt_rank(DevIndex ix, const uint8_t* __restrict__ syms,
     for (int l = 0; l < kLevels; ++l) {
       const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
       if (!(T.flags[nid] & kPure)) {
-        const uint64_t r = rank1_dev(ix, l, T.S[nid] + d) - T.R[nid];
+        const uint64_t r = rank1_at<F>(level_ptr<F>(ix, l), T.S[nid] + d) - T.R[nid];
         d = ((c >> (7 - l)) & 1u) ? r : d - r;
       }
     }
@@ -255,6 +261,7 @@ __global__ void k_wt_rank(DevIndex ix, const uint8_t* __restrict__ syms,
   out[t] = d;
 }
 
+template <class F>
 __global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
                      uint64_t* __restrict__ out, uint8_t* __restrict__ sym) {
   __shared__ NodeTable T;
@@ -269,12 +276,13 @@ __global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
     return;
   }
   uint32_t c;
-  const uint64_t v = lf_step(ix, T, i, &c);
+  const uint64_t v = lf_step<F>(ix, T, i, &c);
   if (out) out[t] = v;
   if (sym) sym[t] = (uint8_t)c;
 }
 
 // WaveletTree::access for every row (the BWT), grid-stride.
+template <class F>
 __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__ out) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
@@ -282,25 +290,32 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ix.n; i += stride) {
     uint32_t c;
-    (void)lf_step(ix, T, i, &c);
+    (void)lf_step<F>(ix, T, i, &c);
     out[i] = (uint8_t)c;
   }
 }
 
 }  // namespace
 
+// Dispatch on the handle's rank-line format.
+#define FMX_DISPATCH(h, KERNEL, GRID, ...)                                      \
+  do {                                                                          \
+    if ((h)->line_bytes == 32)                                                  \
+      KERNEL<Line32><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
+    else                                                                        \
+      KERNEL<Line64><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
+    FMX_HIP(hipGetLastError());                                                 \
+  } while (0)
+
 cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
-  k_bwt<<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(h->dev(), d_out);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_bwt, grid_for(h->n, kBlk, 65536), h->dev(), d_out);
   return CS_OK;
 }
 
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st) {
   if (!npat) return CS_OK;
-  k_count<<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_pats, d_offs, npat,
-                                                               d_out);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_count, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat, d_out);
   return CS_OK;
 }
 
@@ -310,9 +325,8 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                hipStream_t st) {
   DevBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8));
-  k_locate_ranges<<<grid_for(npat + 1, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-      h->dev(), d_pats, d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,
+               d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
   size_t tb = 0;
   FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint64_t>(), d_out_offs, (uint64_t)0,
                                   npat + 1, rocprim::plus<uint64_t>(), st));
@@ -339,16 +353,18 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   const uint64_t max_blocks = (uint64_t)ncu * 8;  // 8 x 256 threads = full CU
   uint64_t chunk = (total + max_blocks - 1) / max_blocks;
   if (chunk < 64) chunk = 64;
-  const uint64_t blocks = (total + chunk - 1) / chunk;
-  const fmx::DevIndex ix = h->dev();
-  if (ix.stride_shift != 0xFFFFFFFFu)
-    k_walk<true><<<(unsigned)blocks, kBlk, 0, st>>>(ix, rows.as<uint32_t>(), total, chunk,
-                                                    d_out_pos,
-                                                    reinterpret_cast<unsigned long long*>(h->d_err));
-  else
-    k_walk<false><<<(unsigned)blocks, kBlk, 0, st>>>(ix, rows.as<uint32_t>(), total, chunk,
-                                                     d_out_pos,
-                                                     reinterpret_cast<unsigned long long*>(h->d_err));
+  const unsigned blocks = (unsigned)((total + chunk - 1) / chunk);
+  const DevIndex ix = h->dev();
+  unsigned long long* err = reinterpret_cast<unsigned long long*>(h->d_err);
+  const uint32_t* r = rows.as<uint32_t>();
+  const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
+  if (h->line_bytes == 32) {
+    if (pow2) k_walk<Line32, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<Line32, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  } else {
+    if (pow2) k_walk<Line64, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<Line64, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  }
   FMX_HIP(hipGetLastError());
   // rows must outlive the kernel: synchronise before DevBuf frees it
   FMX_HIP(hipStreamSynchronize(st));
@@ -363,7 +379,6 @@ cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, u
   if (bad == ~0ull) return CS_OK;
   FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));
-  // map the failing row back to its pattern for the message
   (void)d_out_offs;
   (void)npat;
   set_error("locate: LF walk exceeded text length");  // fm_index.cpp:137
@@ -373,32 +388,30 @@ cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, u
 cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
                              uint64_t* d_out, hipStream_t st) {
   if (!k) return CS_OK;
-  k_level_rank1<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), level, d_pos, k, d_out);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_level_rank1, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), level, d_pos, k, d_out);
   return CS_OK;
 }
 
 cs_status launch_wt_rank(const cs_fm_index* h, const uint8_t* d_syms, const uint64_t* d_pos,
                          uint64_t k, uint64_t* d_out, hipStream_t st) {
   if (!k) return CS_OK;
-  k_wt_rank<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_syms, d_pos, k, d_out);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_wt_rank, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), d_syms, d_pos, k, d_out);
   return CS_OK;
 }
 
 cs_status launch_wt_access(const cs_fm_index* h, const uint64_t* d_pos, uint64_t k,
                            uint8_t* d_out, hipStream_t st) {
   if (!k) return CS_OK;
-  k_lf<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_pos, k, nullptr, d_out);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_lf, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), d_pos, k, (uint64_t*)nullptr,
+               d_out);
   return CS_OK;
 }
 
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st) {
   if (!k) return CS_OK;
-  k_lf<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(h->dev(), d_rows, k, d_out, nullptr);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_lf, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), d_rows, k, d_out,
+               (uint8_t*)nullptr);
   return CS_OK;
 }
 

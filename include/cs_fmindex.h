@@ -58,7 +58,7 @@ typedef struct cs_fm_index cs_fm_index;
 typedef struct cs_fm_info {
   uint64_t n;              /* text length incl. any terminator the caller appended */
   uint32_t ssa_stride;
-  uint32_t line_bits;      /* payload bits per 64-B rank line */
+  uint32_t line_bits;      /* payload bits per rank line (224 in 32-B lines, 448 in 64-B) */
   uint64_t lines_per_level;
   uint64_t rank_bytes;     /* 8 levels of rank lines in HBM */
   uint64_t ssa_bytes;

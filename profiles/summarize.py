@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""summarize.py <prof_dir> <tag> — condense rocprofv3 CSV output of
+profile_count.sh into <prof_dir>/summary.json:
+
+  kernels: per kernel name, dispatch count and mean/min/max duration (ns) from
+           the --kernel-trace --stats pass;
+  pmc:     per hot kernel, mean FETCH_SIZE (KB per dispatch, as reported) and the
+           L2 hit rate TCC_HIT/(TCC_HIT+TCC_MISS) from their own passes.
+  bench:   the bench JSON line each pass printed (the un-profiled numbers are in
+           BENCH_rNN.json; profiled passes run slower, MI355X_MICROARCH 'DVFS
+           give-back' item 2).
+FETCH_SIZE is reported raw; the gfx950 correction (x2 for wide coalesced streams)
+is NOT applied because this kernel's access is random 64-B lines — the factor for
+that width is calibrated separately (profiles/microbench).
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def short(name):
+    for k in ("k_count", "k_walk", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt",
+              "k_partition", "k_pack_level", "k_init_keys", "k_double_keys", "k_heads",
+              "k_scatter_rank", "k_bwt_ssa", "k_hist", "k_text", "k_patterns", "k_indep", "k_chain"):
+        if k in name:
+            return k
+    return name[:60]
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    res = {"tag": tag, "kernels": {}, "pmc": {}, "bench": {}}
+    kt = rows(os.path.join(d, "trace", "**", "*kernel_trace.csv"))
+    by = {}
+    for r in kt:
+        n = short(r.get("Kernel_Name", ""))
+        dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        by.setdefault(n, []).append(dur)
+    for n, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        res["kernels"][n] = {"dispatches": len(v), "mean_ns": statistics.mean(v), "min_ns": min(v),
+                             "max_ns": max(v), "total_ns": sum(v)}
+    for sub, names in (("pmc_fetch", ["FETCH_SIZE"]), ("pmc_l2", ["TCC_HIT_sum", "TCC_MISS_sum"])):
+        for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv")):
+            n = short(r.get("Kernel_Name", ""))
+            c = r.get("Counter_Name")
+            if c in names:
+                res["pmc"].setdefault(n, {}).setdefault(c, []).append(float(r["Counter_Value"]))
+    for n, cs in res["pmc"].items():
+        for c, v in list(cs.items()):
+            cs[c] = statistics.mean(v)
+        if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
+            tot = cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"]
+            cs["l2_hit_rate"] = cs["TCC_HIT_sum"] / tot if tot else None
+    for f in ("bench_trace.json", "bench_fetch.json", "bench_l2.json"):
+        p = os.path.join(d, f)
+        if os.path.exists(p):
+            try:
+                res["bench"][f] = json.loads(open(p).read().strip().splitlines()[-1])
+            except Exception:
+                pass
+    # stats CSV from pass 1 (copied next to the summary)
+    st = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if st:
+        res["kernel_stats_csv"] = os.path.relpath(st[0], d)
+    with open(os.path.join(d, "summary.json"), "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({"kernels": {k: v["mean_ns"] for k, v in res["kernels"].items()},
+                      "pmc": res["pmc"]}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

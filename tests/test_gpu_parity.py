@@ -3,7 +3,7 @@ golden vectors and the CPU restatement (oracle/), bit for bit.
 
 Layers checked separately, bottom-up:
   suffix array      (device prefix doubling)    vs src/core/sais.hpp:8-16 order
-  level rank1       (64-B rank lines)            vs BitVector::rank1, every position
+  level rank1       (32/64-B rank lines)           vs BitVector::rank1, every position
   wavelet rank      (node-table descent)         vs WaveletTree::rank, every (c, i)
   access / LF       (fused descent)              vs BWT / FMIndex::LF, every row
   count / locate    (batched kernels)            vs golden vectors and the oracle
@@ -17,9 +17,18 @@ from conftest import fm_golden_cases, golden_text, load_golden, load_pkg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def pkg():
-    return load_pkg()
+@pytest.fixture(scope="module", params=["line32", "line64"])
+def pkg(request):
+    """Every test runs on both rank-line formats (32-B default for n < 2^32; the
+    64-B format is forced through the builder's CS_FM_LINE_BYTES test hook)."""
+    import os
+    old = os.environ.get("CS_FM_LINE_BYTES")
+    os.environ["CS_FM_LINE_BYTES"] = "64" if request.param == "line64" else "32"
+    yield load_pkg()
+    if old is None:
+        os.environ.pop("CS_FM_LINE_BYTES", None)
+    else:
+        os.environ["CS_FM_LINE_BYTES"] = old
 
 
 def _texts():
@@ -37,6 +46,8 @@ def _texts():
         "runs": (b"ab" * 700) + (b"a" * 500) + b"$",
         "line_edge_448": bytes(rng.choice(list(b"ACGT"), 447).astype(np.uint8)) + b"$",
         "line_edge_896": bytes(rng.choice(list(b"ACGT"), 896).astype(np.uint8)),
+        "line_edge_224": bytes(rng.choice(list(b"ACGT"), 223).astype(np.uint8)) + b"$",
+        "line_edge_672": bytes(rng.choice(list(b"ACG"), 672).astype(np.uint8)),
     }
     return out
 

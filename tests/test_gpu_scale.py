@@ -1,0 +1,113 @@
+"""Full-size GPU checks (BASELINE.json configs C3/C4) through size-independent
+properties — no CPU index is built at these sizes:
+
+  * every Q_text pattern (a substring sampled at a known position) is found;
+  * every located position p satisfies text[p:p+m] == pattern, positions are
+    distinct, the sampled position is among them, and each list has
+    min(count, limit) entries;
+  * checksum of checksums: sum of count() over ALL k-mers of the alphabet equals
+    the number of k-windows of the text that avoid the terminator, and the sum of
+    count() over all 256 single bytes equals n.
+The oracle comparison at these sizes is on the sample in bench.py's cpu_baseline
+(matches_gpu); bit-exact oracle parity at sizes the oracle builds in seconds is in
+test_gpu_parity.py.
+"""
+import itertools
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _build(pkg, kind, L):
+    dev = torch.device("cuda", 0)
+    N = L + 1
+    text = torch.empty(N + 16, dtype=torch.uint8, device=dev)
+    pkg.synth_text_device(kind, 42, L, text.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N, pkg.BuildParams(), device=0)
+    host = text[:N].cpu().numpy()
+    return idx, text, host, N
+
+
+def _qtext(pkg, text, N, m, npat):
+    dev = text.device
+    pats = torch.empty(npat * m, dtype=torch.uint8, device=dev)
+    pkg.synth_patterns_device(text.data_ptr(), N, m, 0, npat, 4242, pats.data_ptr(), None,
+                              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return pats.cpu().numpy().reshape(npat, m)
+
+
+def _sampled_positions(N, m, npat, seed=4242):
+    g = 0x9E3779B97F4A7C15
+    k = np.arange(1, npat + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + k * np.uint64(g)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z % np.uint64(N - m)
+
+
+def _check_qtext(idx, host, N, P, nloc, limit=1000):
+    npat, m = P.shape
+    buf = np.ascontiguousarray(P).reshape(-1)
+    offs = np.arange(0, (npat + 1) * m, m, dtype=np.uint64)
+    cnt = idx.count_batch(buf=buf, offs=offs)
+    assert (cnt >= 1).all()
+    src = _sampled_positions(N, m, npat)
+    loffs, pos = idx.locate_batch(buf=buf[: nloc * m], offs=offs[: nloc + 1], limit=limit)
+    assert np.array_equal(np.diff(loffs), np.minimum(cnt[:nloc], limit))
+    # every position spells its pattern
+    win = host[pos[:, None].astype(np.int64) + np.arange(m)]
+    owner = np.repeat(np.arange(nloc), np.diff(loffs).astype(np.int64))
+    assert np.array_equal(win, P[owner])
+    for q in range(nloc):
+        seg = pos[loffs[q]:loffs[q + 1]]
+        assert len(np.unique(seg)) == len(seg)
+        if cnt[q] <= limit:
+            assert src[q] in seg
+    return cnt
+
+
+def _kmer_checksum(idx, alphabet, k, N):
+    pats = [bytes(t) for t in itertools.product(alphabet, repeat=k)]
+    tot = int(idx.count_batch(pats).sum())
+    assert tot == N - k  # k-windows of T[0..N-2] (the terminator is unique)
+
+
+@pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C4") == "1", reason="C4 disabled")
+def test_c4_dna_4gb():
+    pkg = load_pkg()
+    idx, text, host, N = _build(pkg, "dna", 3_999_999_999)
+    assert N == 4_000_000_000
+    P = _qtext(pkg, text, N, 20, 200_000)
+    _check_qtext(idx, host, N, P, nloc=20_000)
+    ones = idx.count_batch([bytes([c]) for c in range(256)])
+    assert int(ones.sum()) == N and ones[ord("$")] == 1
+    _kmer_checksum(idx, b"ACGT", 9, N)
+
+
+def test_c3_bytes_1gb():
+    pkg = load_pkg()
+    idx, text, host, N = _build(pkg, "bytes", 999_999_999)
+    P = _qtext(pkg, text, N, 8, 100_000)
+    _check_qtext(idx, host, N, P, nloc=20_000)
+    ones = idx.count_batch([bytes([c]) for c in range(256)])
+    assert int(ones.sum()) == N and ones[0] == 1
+    _kmer_checksum(idx, bytes(range(1, 256)), 2, N)
+
+
+def test_c2_dna_100mb_locate_everything():
+    """100 MB: locate every Q_text hit of 200k 20-mers and 12-mers (limit 100)."""
+    pkg = load_pkg()
+    idx, text, host, N = _build(pkg, "dna", 99_999_999)
+    for m in (20, 12):
+        P = _qtext(pkg, text, N, m, 200_000)
+        _check_qtext(idx, host, N, P, nloc=200_000, limit=100)
