@@ -98,10 +98,13 @@ def main():
     out = torch.empty(B, dtype=torch.int64, device=dev)
     gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
 
-    # algorithmic bytes per launch: 2 lines x 64 B per active level per char after the first
+    # algorithmic bytes per launch: 2 rank-line reads (sp, ep) per non-pure wavelet level
+    # per pattern character after the first (the first comes from C[]); one line = 32 B
+    # (Line32, n < 2^32) or 64 B
+    line_bytes = 32 if info.line_bits == 224 else 64
     act = torch.tensor([bin(info.active_levels[c]).count("1") for c in range(256)],
                        dtype=torch.int64, device=dev)
-    alg_bytes = int(act[pats.view(B, m)[:, :-1].long()].sum().item()) * 2 * 64
+    alg_bytes = int(act[pats.view(B, m)[:, :-1].long()].sum().item()) * 2 * line_bytes
     torch.cuda.synchronize()
 
     def step():
@@ -171,7 +174,7 @@ def main():
                        "index": "replicated per GPU", "workload_key": wl},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,
                          "alg_bytes_per_query": alg_bytes / B,
                          "kernel_ms_mean": kern_avg_s * 1e3,
                          "kernel_ms_min": min(kern_ms)},

@@ -128,7 +128,7 @@ __device__ __forceinline__ void store_word(void* L, uint64_t w, uint64_t v) {
 // One wave per 64 positions: ballot of the level bit (= 1 or 2 payload words).
 template <class F>
 __global__ void k_pack_level(const uint8_t* __restrict__ cur, uint64_t n, int bit,
-                             void* __restrict__ L, uint64_t ngroups) {
+                             void* __restrict__ L, uint64_t ngroups, uint64_t nwords) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -138,9 +138,9 @@ __global__ void k_pack_level(const uint8_t* __restrict__ cur, uint64_t n, int bi
     const uint64_t w = __ballot(b);
     if (F::kWordBits == 64) {
       if (lane == 0) store_word<F>(L, g, w);
-    } else {
+    } else {  // a line holds 7 dwords, so the last group may straddle the end
       if (lane == 0) store_word<F>(L, 2 * g, w & 0xFFFFFFFFull);
-      if (lane == 1) store_word<F>(L, 2 * g + 1, w >> 32);
+      if (lane == 1 && 2 * g + 1 < nwords) store_word<F>(L, 2 * g + 1, w >> 32);
     }
   }
 }
@@ -240,11 +240,12 @@ static cs_status build_levels(uint8_t* cur, uint64_t n, cs_fm_index* h, hipStrea
                                   (uint64_t)0, nl, rocprim::plus<uint64_t>(), st));
   FMX_HIP(tmp.alloc(tmp_bytes));
   uint8_t* nx = nxt.as<uint8_t>();
-  const uint64_t ngroups = nl * F::kWords * F::kWordBits / 64;
+  const uint64_t nwords = nl * F::kWords;
+  const uint64_t ngroups = (nwords * F::kWordBits + 63) / 64;  // 64 positions per wave
   for (int l = 0; l < kLevels; ++l) {
     const int bit = 7 - l;
     void* L = reinterpret_cast<uint8_t*>(h->d_lines) + (uint64_t)l * nl * F::kBytes;
-    k_pack_level<F><<<grid_for(ngroups * 64, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, ngroups);
+    k_pack_level<F><<<grid_for(ngroups * 64, kBlk, 16384), kBlk, 0, st>>>(cur, n, bit, L, ngroups, nwords);
     k_line_counts<F><<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(L, nl, cnt.as<uint64_t>());
     size_t tb = tmp_bytes;
     FMX_HIP(rocprim::exclusive_scan(tmp.p, tb, cnt.as<uint64_t>(), base.as<uint64_t>(), (uint64_t)0,

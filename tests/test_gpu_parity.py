@@ -48,6 +48,9 @@ def _texts():
         "line_edge_896": bytes(rng.choice(list(b"ACGT"), 896).astype(np.uint8)),
         "line_edge_224": bytes(rng.choice(list(b"ACGT"), 223).astype(np.uint8)) + b"$",
         "line_edge_672": bytes(rng.choice(list(b"ACG"), 672).astype(np.uint8)),
+        # 32-B lines hold 224 bits = 3.5 ballot groups: n in the last half group
+        "straddle_201": bytes(rng.choice(list(b"ab"), 200).astype(np.uint8)) + b"$",
+        "straddle_649": bytes(rng.choice(list(b"ACGT"), 648).astype(np.uint8)) + b"$",
     }
     return out
 
