@@ -61,8 +61,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p50-calls", type=int, default=1000)
-    ap.add_argument("--check", type=int, default=0, help="verify this many located Q_text hits")
+    ap.add_argument("--prefix-k", type=int, default=None,
+                    help="prefix-table depth override (0 = off; default automatic)")
     args = ap.parse_args()
+    if args.prefix_k is not None:
+        os.environ["CS_FM_PREFIX_K"] = str(args.prefix_k)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -99,12 +102,26 @@ def main():
     gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     # algorithmic bytes per launch: 2 rank-line reads (sp, ep) per non-pure wavelet level
-    # per pattern character after the first (the first comes from C[]); one line = 32 B
-    # (Line32, n < 2^32) or 64 B
+    # per backward-search step the kernel performs; one line = 32 B (Line32, n < 2^32)
+    # or 64 B.  Steps covered by the prefix table cost one 8-B table read instead
+    # (and the first step without it comes from C[]).
     line_bytes = 32 if info.line_bits == 224 else 64
     act = torch.tensor([bin(info.active_levels[c]).count("1") for c in range(256)],
                        dtype=torch.int64, device=dev)
-    alg_bytes = int(act[pats.view(B, m)[:, :-1].long()].sum().item()) * 2 * line_bytes
+    P2 = pats.view(B, m).long()
+    K = info.prefix_k
+    if K and m >= K:
+        code = torch.tensor(list(info.prefix_code), dtype=torch.int64, device=dev)
+        use = (code[P2[:, m - K:]] != 255).all(dim=1)
+        lines_tab = act[P2[:, : m - K]].sum(dim=1)
+        lines_c = act[P2[:, :-1]].sum(dim=1)
+        per_q = torch.where(use, lines_tab * 2 * line_bytes + 8, lines_c * 2 * line_bytes)
+        alg_bytes = int(per_q.sum().item())
+        table_frac = float(use.float().mean().item())
+    else:
+        alg_bytes = int(act[P2[:, :-1]].sum().item()) * 2 * line_bytes
+        table_frac = 0.0
+    del P2
     torch.cuda.synchronize()
 
     def step():
@@ -175,6 +192,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,
+                         "prefix_k": K, "prefix_table_hit_frac": table_frac,
                          "alg_bytes_per_query": alg_bytes / B,
                          "kernel_ms_mean": kern_avg_s * 1e3,
                          "kernel_ms_min": min(kern_ms)},

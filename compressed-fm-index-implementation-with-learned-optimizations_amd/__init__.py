@@ -39,7 +39,9 @@ class cs_build_params(C.Structure):
 class cs_fm_info(C.Structure):
     _fields_ = [("n", C.c_uint64), ("ssa_stride", C.c_uint32), ("line_bits", C.c_uint32),
                 ("lines_per_level", C.c_uint64), ("rank_bytes", C.c_uint64),
-                ("ssa_bytes", C.c_uint64), ("active_levels", C.c_uint32 * 256), ("device", C.c_int)]
+                ("ssa_bytes", C.c_uint64), ("active_levels", C.c_uint32 * 256), ("device", C.c_int),
+                ("prefix_k", C.c_uint32), ("prefix_sigma", C.c_uint32), ("prefix_bytes", C.c_uint64),
+                ("prefix_code", C.c_uint8 * 256)]
 
 
 # Every entry point of include/cs_fmindex.h with its ctypes signature.

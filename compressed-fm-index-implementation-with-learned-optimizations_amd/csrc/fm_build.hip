@@ -474,6 +474,12 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     FMX_HIP(hipStreamSynchronize(st));
   }
   FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
+  {
+    cs_status ps = build_prefix_table(h, st);
+    if (ps != CS_OK) return ps;
+    FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
+  }
+  plog.mark("prefix table");
   FMX_HIP(hipMalloc(&h->d_err, 8));
   FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));

@@ -71,6 +71,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_ssa) (void)hipFree(h->d_ssa);
   if (h->d_table) (void)hipFree(h->d_table);
   if (h->d_err) (void)hipFree(h->d_err);
+  if (h->d_ptab) (void)hipFree(h->d_ptab);
   delete h;
 }
 
@@ -174,6 +175,14 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->ssa_bytes = h->nsamples * 4;
   std::memcpy(out->active_levels, h->active_levels, sizeof out->active_levels);
   out->device = h->device;
+  out->prefix_k = h->ptab_k;
+  out->prefix_sigma = h->ptab_sigma;
+  out->prefix_bytes = h->ptab_k ? (uint64_t)sizeof(uint2) * [&] {
+    uint64_t e = 1;
+    for (uint32_t i = 0; i < h->ptab_k; ++i) e *= h->ptab_sigma;
+    return e;
+  }() : 0;
+  for (int c = 0; c < 256; ++c) out->prefix_code[c] = h->h_table.code[c];
   return CS_OK;
 }
 

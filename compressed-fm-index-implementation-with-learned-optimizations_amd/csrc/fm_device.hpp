@@ -44,7 +44,10 @@ struct NodeTable {
   uint64_t C[257];      // fm_index.cpp:36-47 (u64)
   uint64_t S8[256];     // start of each symbol's run after the last level
   uint8_t flags[256];   // kPure | kPureBit per node
+  uint8_t code[256];    // prefix-table digit of each symbol, kNoCode if not in its alphabet
+  uint8_t sym[256];     // digit -> symbol
 };
+constexpr uint8_t kNoCode = 0xFF;
 
 struct DevIndex {
   const void* lines;     // kLevels * nlines rank lines of the handle's format
@@ -55,6 +58,13 @@ struct DevIndex {
   uint32_t stride;
   uint32_t stride_shift; // log2(stride) when stride is a power of two, else 0xFFFFFFFF
   const NodeTable* table;
+  // Prefix table: (sp, ep) of every k-mer over the frequent alphabet (sigma_t
+  // symbols), index = sum_j digit(P[m-1-j]) * sigma_t^j.  The generalisation of
+  // C[] (the k = 1 table, fm_index.cpp:36-47): a count() whose last k characters
+  // are all in the alphabet starts at step k+1.  Empty when ptab_k == 0.
+  const uint2* ptab;
+  uint32_t ptab_k;
+  uint32_t ptab_sigma;
 };
 
 __host__ __device__ inline int node_id(int level, uint32_t prefix) {

@@ -22,6 +22,8 @@ struct cs_fm_index {
   fmx::NodeTable* d_table = nullptr;
   fmx::NodeTable h_table{};
   uint64_t* d_err = nullptr;          // locate: min failing item (UINT64_MAX = none)
+  uint2* d_ptab = nullptr;            // prefix table (DevIndex::ptab)
+  uint32_t ptab_k = 0, ptab_sigma = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
 
@@ -40,6 +42,9 @@ struct cs_fm_index {
       d.stride_shift = s;
     }
     d.table = d_table;
+    d.ptab = d_ptab;
+    d.ptab_k = ptab_k;
+    d.ptab_sigma = ptab_sigma;
     return d;
   }
 };
@@ -80,6 +85,7 @@ cs_status launch_wt_rank(const cs_fm_index* h, const uint8_t* d_syms, const uint
 cs_status launch_wt_access(const cs_fm_index* h, const uint64_t* d_pos, uint64_t k,
                            uint8_t* d_out, hipStream_t st);
 cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st);
+cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st);
 

@@ -21,6 +21,9 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "fm_internal.hpp"
 
 namespace fmx {
@@ -35,48 +38,105 @@ __device__ __forceinline__ void load_table(NodeTable& T, const NodeTable* __rest
   for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
 }
 
+// One backward-search step (fm_index.cpp:90-96) for a symbol c present in the
+// text: [sp, ep) -> [C[c] + occ(c, sp), C[c] + occ(c, ep)).  Returns false when
+// the range empties (the reference's `return 0`).
+template <class F>
+__device__ __forceinline__ bool search_step(const DevIndex& ix, const NodeTable& T, uint32_t c,
+                                            uint64_t& sp, uint64_t& ep) {
+  const uint64_t Cc = T.C[c];
+  if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
+  uint64_t ds = sp, de = ep;
+#pragma unroll
+  for (int l = 0; l < kLevels; ++l) {
+    const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
+    if (!(T.flags[nid] & kPure)) {
+      const uint64_t S = T.S[nid], R = T.R[nid];
+      const void* lv = level_ptr<F>(ix, l);
+      uint32_t qa, oa, qe, oe;
+      F::locate(S + ds, qa, oa);
+      F::locate(S + de, qe, oe);
+      typename F::Raw va, ve;
+      F::load(lv, qa, va);
+      F::load(lv, qe, ve);
+      const uint64_t rs = F::base(va) + F::prefix(va, oa) - R;
+      const uint64_t re = F::base(ve) + F::prefix(ve, oe) - R;
+      const bool b = (c >> (7 - l)) & 1u;
+      ds = b ? rs : ds - rs;
+      de = b ? re : de - re;
+    }
+  }
+  sp = Cc + ds;
+  ep = Cc + de;
+  return sp < ep;
+}
+
 // Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
-// range empties (the reference's `return 0`).  Requires m >= 1, n >= 1.
+// range empties.  Requires m >= 1, n >= 1.  The first step comes from C[]
+// (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
+// pattern's last k characters are all in its alphabet.
 template <class F>
 __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
                                                 const uint8_t* __restrict__ P, uint64_t m,
                                                 uint64_t& sp_out, uint64_t& ep_out) {
-  uint32_t c = P[m - 1];
-  uint64_t sp = T.C[c], ep = T.C[c + 1];  // occ(c,0)=0, occ(c,n)=freq(c)
-  if (sp >= ep) return false;
-  uint32_t cn = m >= 2 ? P[m - 2] : 0u;
-  for (uint64_t k = m - 1; k-- > 0;) {
-    c = cn;
-    if (k > 0) cn = P[k - 1];  // prefetch the next character
-    const uint64_t Cc = T.C[c];
-    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
-    uint64_t ds = sp, de = ep;
-#pragma unroll
-    for (int l = 0; l < kLevels; ++l) {
-      const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
-      if (!(T.flags[nid] & kPure)) {
-        const uint64_t S = T.S[nid], R = T.R[nid];
-        const void* lv = level_ptr<F>(ix, l);
-        uint32_t qa, oa, qe, oe;
-        F::locate(S + ds, qa, oa);
-        F::locate(S + de, qe, oe);
-        typename F::Raw va, ve;
-        F::load(lv, qa, va);
-        F::load(lv, qe, ve);
-        const uint64_t rs = F::base(va) + F::prefix(va, oa) - R;
-        const uint64_t re = F::base(ve) + F::prefix(ve, oe) - R;
-        const bool b = (c >> (7 - l)) & 1u;
-        ds = b ? rs : ds - rs;
-        de = b ? re : de - re;
-      }
+  uint64_t sp, ep, k;  // k = characters still to process, P[k-1] .. P[0]
+  bool from_table = false;
+  if (ix.ptab_k && m >= ix.ptab_k) {
+    uint32_t t = 0;
+    bool ok = true;
+    for (uint32_t i = (uint32_t)(m - ix.ptab_k); i < m; ++i) {
+      const uint32_t d = T.code[P[i]];
+      ok &= d != kNoCode;
+      t = t * ix.ptab_sigma + d;
     }
-    sp = Cc + ds;
-    ep = Cc + de;
-    if (sp >= ep) return false;
+    if (ok) {
+      const uint2 r = ix.ptab[t];
+      sp = r.x;
+      ep = r.y;
+      k = m - ix.ptab_k;
+      from_table = true;
+    }
+  }
+  if (!from_table) {
+    const uint32_t c = P[m - 1];
+    sp = T.C[c];  // occ(c,0)=0, occ(c,n)=freq(c)
+    ep = T.C[c + 1];
+    k = m - 1;
+  }
+  if (sp >= ep) return false;
+  uint32_t cn = k ? P[k - 1] : 0u;
+  while (k-- > 0) {
+    const uint32_t c = cn;
+    if (k > 0) cn = P[k - 1];  // prefetch the next character
+    if (!search_step<F>(ix, T, c, sp, ep)) return false;
   }
   sp_out = sp;
   ep_out = ep;
   return true;
+}
+
+// Prefix table entry t: backward search of the k-mer whose j-th character from
+// the end is sym[digit_j(t)] (same steps as above, from C[]).
+template <class F>
+__global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entries,
+                                                     uint2* __restrict__ tab) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += stride) {
+    uint64_t rest = t;
+    uint32_t c = T.sym[rest % ix.ptab_sigma];
+    rest /= ix.ptab_sigma;
+    uint64_t sp = T.C[c], ep = T.C[c + 1];
+    bool live = sp < ep;
+    for (uint32_t j = 1; j < ix.ptab_k && live; ++j) {
+      c = T.sym[rest % ix.ptab_sigma];
+      rest /= ix.ptab_sigma;
+      live = search_step<F>(ix, T, c, sp, ep);
+    }
+    tab[t] = live ? make_uint2((uint32_t)sp, (uint32_t)ep) : make_uint2(0u, 0u);
+  }
 }
 
 template <class F>
@@ -306,6 +366,63 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
       KERNEL<Line64><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
     FMX_HIP(hipGetLastError());                                                 \
   } while (0)
+
+// Prefix table over the frequent alphabet: symbols with at least n/2^20
+// occurrences (all present symbols for small texts), k = largest with
+// sigma^k <= min(2^24, max(4096, 4n)) entries; none when k < 2.  Entries are
+// (sp, ep) as u32, so only for n < 2^32.  CS_FM_PREFIX_K overrides k (0 = off).
+cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
+  NodeTable& T = h->h_table;
+  std::memset(T.code, kNoCode, sizeof T.code);
+  std::memset(T.sym, 0, sizeof T.sym);
+  h->ptab_k = 0;
+  h->ptab_sigma = 0;
+  const uint64_t n = h->n;
+  if (n == 0 || n >= (1ull << 32)) return CS_OK;
+  uint32_t sigma = 0;
+  for (int c = 0; c < 256; ++c) {
+    const uint64_t f = T.C[c + 1] - T.C[c];
+    if (f && f * (1ull << 20) >= n) {
+      T.code[c] = (uint8_t)sigma;
+      T.sym[sigma++] = (uint8_t)c;
+    }
+  }
+  if (sigma == 0) return CS_OK;
+  uint64_t cap = 4 * n > 4096 ? 4 * n : 4096;
+  if (cap > (1ull << 24)) cap = 1ull << 24;
+  uint32_t k = 0;
+  uint64_t entries = 1;
+  while (k < 32 && entries * sigma <= cap) {
+    entries *= sigma;
+    ++k;
+  }
+  if (const char* e = std::getenv("CS_FM_PREFIX_K")) {
+    const int want = std::atoi(e);
+    k = 0;
+    entries = 1;
+    while ((int)k < want && entries * sigma <= (1ull << 28)) {
+      entries *= sigma;
+      ++k;
+    }
+  }
+  if (k < 2 || sigma < 2) {
+    std::memset(T.code, kNoCode, sizeof T.code);
+    return CS_OK;
+  }
+  FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
+  FMX_HIP(hipMalloc(&h->d_ptab, entries * sizeof(uint2)));
+  h->ptab_sigma = sigma;
+  h->ptab_k = k;
+  DevIndex ix = h->dev();
+  ix.ptab = nullptr;  // the builder itself searches from C[]
+  if (h->line_bytes == 32)
+    k_build_ptab<Line32><<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(ix, entries, h->d_ptab);
+  else
+    k_build_ptab<Line64><<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(ix, entries, h->d_ptab);
+  FMX_HIP(hipGetLastError());
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
 
 cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
   FMX_DISPATCH(h, k_bwt, grid_for(h->n, kBlk, 65536), h->dev(), d_out);

@@ -64,6 +64,10 @@ typedef struct cs_fm_info {
   uint64_t ssa_bytes;
   uint32_t active_levels[256]; /* per symbol: bitmask of levels needing a memory access */
   int device;
+  uint32_t prefix_k;       /* prefix table: k-mers whose (sp, ep) is precomputed (0 = none) */
+  uint32_t prefix_sigma;   /* its alphabet size */
+  uint64_t prefix_bytes;
+  uint8_t prefix_code[256];/* digit of each symbol in the table alphabet, 255 = not in it */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -17,18 +17,33 @@ from conftest import fm_golden_cases, golden_text, load_golden, load_pkg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["line32", "line64"])
+ENGINE_VARIANTS = {
+    # name: (rank-line bytes, prefix-table k override or None = automatic)
+    "line32": ("32", None),
+    "line64": ("64", None),
+    "line32_noprefix": ("32", "0"),
+}
+
+
+@pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
 def pkg(request):
-    """Every test runs on both rank-line formats (32-B default for n < 2^32; the
-    64-B format is forced through the builder's CS_FM_LINE_BYTES test hook)."""
+    """Every test runs on each engine variant: 32-B rank lines (default for
+    n < 2^32), 64-B lines (forced through the builder's CS_FM_LINE_BYTES test
+    hook), and with the prefix table disabled (CS_FM_PREFIX_K=0)."""
     import os
-    old = os.environ.get("CS_FM_LINE_BYTES")
-    os.environ["CS_FM_LINE_BYTES"] = "64" if request.param == "line64" else "32"
-    yield load_pkg()
-    if old is None:
-        os.environ.pop("CS_FM_LINE_BYTES", None)
+    lb, pk = ENGINE_VARIANTS[request.param]
+    saved = {k: os.environ.get(k) for k in ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K")}
+    os.environ["CS_FM_LINE_BYTES"] = lb
+    if pk is None:
+        os.environ.pop("CS_FM_PREFIX_K", None)
     else:
-        os.environ["CS_FM_LINE_BYTES"] = old
+        os.environ["CS_FM_PREFIX_K"] = pk
+    yield load_pkg()
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def _texts():
@@ -195,6 +210,29 @@ def test_ssa_strides_vs_oracle(pkg, stride):
     offs, pos = g.locate_batch(pats, limit=100)
     for q, p in enumerate(pats):
         assert pos[offs[q]:offs[q + 1]].tolist() == o.locate(p, limit=100)
+
+
+def test_prefix_table_sweep(pkg):
+    """Prefix tables of every depth give the same counts (k forced 2..8)."""
+    import os
+    t = O.gen_dna(9, 30000).tobytes()
+    o = O.Index(t)
+    rng = np.random.default_rng(2)
+    pats = [t[i:i + m] for i, m in zip(rng.integers(0, 29000, 400), rng.integers(1, 25, 400))]
+    pats += [bytes(rng.choice(list(b"ACGT$"), int(m)).astype(np.uint8)) for m in rng.integers(1, 12, 100)]
+    want = [o.count(p) for p in pats]
+    saved = os.environ.get("CS_FM_PREFIX_K")
+    try:
+        for k in range(2, 9):
+            os.environ["CS_FM_PREFIX_K"] = str(k)
+            g = pkg.FMIndex.build_from_text(t)
+            assert g.info().prefix_k == k
+            assert g.count_batch(pats).tolist() == want, k
+    finally:
+        if saved is None:
+            os.environ.pop("CS_FM_PREFIX_K", None)
+        else:
+            os.environ["CS_FM_PREFIX_K"] = saved
 
 
 def test_lf_overrun_message(pkg):
