@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p50-calls", type=int, default=1000)
+    ap.add_argument("--locate-batch", type=int, default=1_000_000,
+                    help="patterns of the batch timed through locate() (N=1 only; 0 = skip)")
     ap.add_argument("--prefix-k", type=int, default=None,
                     help="prefix-table depth override (0 = off; default automatic)")
     args = ap.parse_args()
@@ -75,6 +77,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     pkg = _load_pkg()
+    import importlib
+    shard = importlib.import_module("cs_fmindex_amd.shard")
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
 
@@ -94,12 +98,14 @@ def main():
 
     # ---- this rank's query shard (contiguous slice of the Q_text stream) ----
     B, m = args.batch, args.m
+    total = B * world  # weak scaling: B patterns per GPU
+    lo, hi = shard.shard_range(total, rank, world)
+    assert hi - lo == B
     pats = torch.empty(B * m, dtype=torch.uint8, device=dev)
     offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
-    pkg.synth_patterns_device(text.data_ptr(), N, m, rank * B, B, 4242, pats.data_ptr(),
+    pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, pats.data_ptr(),
                               offs.data_ptr(), sh)
     out = torch.empty(B, dtype=torch.int64, device=dev)
-    gather = [torch.empty_like(out) for _ in range(world)] if (world > 1 and rank == 0) else None
 
     # algorithmic bytes per launch: 2 rank-line reads (sp, ep) per non-pure wavelet level
     # per backward-search step the kernel performs; one line = 32 B (Line32, n < 2^32)
@@ -127,7 +133,7 @@ def main():
     def step():
         idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, out.data_ptr(), sh)
         if world > 1:
-            dist.gather(out, gather, dst=0)
+            shard.gather_counts(out, total, world, rank)
 
     for _ in range(args.warmup):
         step()
@@ -143,7 +149,7 @@ def main():
         idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, out.data_ptr(), sh)
         evs[k][1].record(stream)
         if world > 1:
-            dist.gather(out, gather, dst=0)
+            shard.gather_counts(out, total, world, rank)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -199,6 +205,34 @@ def main():
             "build_s": build_s,
             "found_frac": found / B,
         }
+
+    # ---- locate (fm_index.cpp:107-157) on a prefix of the batch, N=1 only ----
+    if rank == 0 and world == 1 and args.locate_batch:
+        Lq = min(args.locate_batch, B)
+        d_sp = torch.empty(Lq, dtype=torch.int64, device=dev)
+        d_oo = torch.empty(Lq + 1, dtype=torch.int64, device=dev)
+        lt = []
+        for it in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            tot = idx.locate_ranges_device(pats.data_ptr(), offs.data_ptr(), Lq, 100000,
+                                           d_sp.data_ptr(), d_oo.data_ptr(), sh)
+            if it == 0:
+                d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+            idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), Lq, tot, d_pos.data_ptr(), sh)
+            torch.cuda.synchronize()
+            lt.append(time.perf_counter() - t1)
+        tl = min(lt)
+        # every reported position spells its pattern (full-size property check)
+        pos = d_pos[:tot]
+        oo = d_oo.cpu().numpy()
+        owner = torch.from_numpy(np.repeat(np.arange(Lq), np.diff(oo).astype(np.int64))).to(dev)
+        win = text[(pos.unsqueeze(1) + torch.arange(m, device=dev)).long()]
+        ok = bool((win == pats.view(B, m)[owner]).all().item())
+        res["locate"] = {"patterns": Lq, "positions": int(tot), "seconds": tl,
+                         "patterns_per_s": Lq / tl, "positions_per_s": tot / tl,
+                         "limit": 100000, "positions_verified": ok}
+        del d_sp, d_oo, d_pos, owner, win
 
     # ---- p50 single-pattern latency through the C ABI (end to end) ----
     if rank == 0 and args.p50_calls:

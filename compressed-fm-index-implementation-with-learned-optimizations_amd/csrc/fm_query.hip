@@ -369,8 +369,9 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^24, max(4096, 4n)) entries; none when k < 2.  Entries are
-// (sp, ep) as u32, so only for n < 2^32.  CS_FM_PREFIX_K overrides k (0 = off).
+// sigma^k <= min(2^26, max(4096, n/32)) entries (8 B each: at most n/4 bytes, the
+// order of the sampled SA); none when k < 2.  Entries are (sp, ep) as u32, so only
+// for n < 2^32.  CS_FM_PREFIX_K overrides k (0 = off).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
   std::memset(T.code, kNoCode, sizeof T.code);
@@ -388,8 +389,8 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     }
   }
   if (sigma == 0) return CS_OK;
-  uint64_t cap = 4 * n > 4096 ? 4 * n : 4096;
-  if (cap > (1ull << 24)) cap = 1ull << 24;
+  uint64_t cap = n / 32 > 4096 ? n / 32 : 4096;
+  if (cap > (1ull << 26)) cap = 1ull << 26;
   uint32_t k = 0;
   uint64_t entries = 1;
   while (k < 32 && entries * sigma <= cap) {

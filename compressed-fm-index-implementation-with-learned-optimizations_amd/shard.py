@@ -1,0 +1,68 @@
+"""Multi-GPU query sharding.
+
+One process per GPU, the index replicated in every GPU's HBM, the query batch
+split into contiguous ranges, per-shard results gathered to rank 0 over the
+process group (RCCL over xGMI on the GPU box; gloo in the CPU tests).  No text
+sharding: a query never needs another GPU's data, so the only collective is the
+final gather.
+
+The helpers are engine-agnostic: `count_fn(lo, hi) -> tensor[hi-lo]` runs the
+local shard (the HIP engine in bench.py; the oracle stand-in in the gloo tests).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous range of ceil(total/world) queries for `rank` (the last shards may
+    be shorter or empty)."""
+    per = (total + world - 1) // world
+    lo = min(total, rank * per)
+    hi = min(total, lo + per)
+    return lo, hi
+
+
+def gather_counts(local: torch.Tensor, total: int, world: int, rank: int, dst: int = 0):
+    """Gather every rank's shard of a length-`total` result vector to `dst`.
+
+    Shards follow shard_range; each is padded to the common shard length so the
+    collective is a plain gather.  Returns the full vector on dst, else None."""
+    per = (total + world - 1) // world
+    buf = torch.zeros(per, dtype=local.dtype, device=local.device)
+    buf[: local.numel()] = local
+    if world == 1:
+        return buf[:total]
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, parts, dst=dst)
+    if rank != dst:
+        return None
+    return torch.cat(parts)[:total]
+
+
+def gather_v(local: torch.Tensor, world: int, rank: int, dst: int = 0):
+    """Gather variable-length 1-D tensors (e.g. located positions) to dst: an
+    all_gather of the lengths, then a padded gather.  Returns the list of per-rank
+    tensors on dst, else None."""
+    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
+    if world == 1:
+        return [local]
+    lens = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(lens, n)
+    lens = [int(x.item()) for x in lens]
+    mx = max(lens) if lens else 0
+    buf = torch.zeros(max(mx, 1), dtype=local.dtype, device=local.device)
+    buf[: local.numel()] = local
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
+    dist.gather(buf, parts, dst=dst)
+    if rank != dst:
+        return None
+    return [p[:l] for p, l in zip(parts, lens)]
+
+
+def sharded_count(count_fn, total: int, world: int, rank: int, device, dst: int = 0):
+    """Run this rank's contiguous shard with count_fn and gather all to dst."""
+    lo, hi = shard_range(total, rank, world)
+    local = count_fn(lo, hi) if hi > lo else torch.zeros(0, dtype=torch.int64, device=device)
+    return gather_counts(local.to(device), total, world, rank, dst)

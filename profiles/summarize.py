@@ -75,6 +75,23 @@ def main():
         res["kernel_stats_csv"] = os.path.relpath(st[0], d)
     with open(os.path.join(d, "summary.json"), "w") as f:
         json.dump(res, f, indent=1)
+    # pmc_count.json for bench.py's roofline.traffic (copy into profiles/ to use)
+    b = res["bench"].get("bench_trace.json") or {}
+    kc = res["pmc"].get("k_count", {})
+    if b and "FETCH_SIZE" in kc:
+        pc = {"workload": b.get("config", {}).get("workload_key"), "kernel": "k_count",
+              "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
+              "hbm_bytes_per_launch": kc["FETCH_SIZE"] * 1024 / 2,
+              "correction": "x1/2: FETCH_SIZE tallies every L2->EA read request at 64 B; the "
+                            "count kernel's requests are 32-B rank lines (calibrated with "
+                            "profiles/microbench/gather_bench: 1 request per random 32-B read, "
+                            "FETCH_SIZE = 64 B per read, throughput = 32-B transfers)",
+              "l2_hit_rate": kc.get("l2_hit_rate"),
+              "tcc_miss_per_launch": kc.get("TCC_MISS_sum"),
+              "kernel_mean_ns_profiled": res["kernels"].get("k_count", {}).get("mean_ns"),
+              "tag": tag}
+        with open(os.path.join(d, "pmc_count.json"), "w") as f:
+            json.dump(pc, f, indent=1)
     print(json.dumps({"kernels": {k: v["mean_ns"] for k, v in res["kernels"].items()},
                       "pmc": res["pmc"]}, indent=1))
 

@@ -1,0 +1,124 @@
+// facade_tests.cpp — the reference's own test programs, re-pointed at the drop-in
+// header: tests/fm_search_tests.cpp and tests/simple_tests.cpp of the reference
+// call cs::FMIndex through "src/api/fm_index.hpp"; here the same calls go through
+// include/cs/fm_index.hpp and libcs_fmindex.so (the GPU engine).  Expected values
+// are the reference's actual outputs (tests/golden/fm_kat.json), which differ from
+// two of its asserts (row-order locate, duplicate '$'), see SURVEY.md §0.5/§0.8.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "cs/fm_index.hpp"
+
+using namespace cs;
+
+static int failures = 0;
+#define CHECK(cond)                                                     \
+  do {                                                                  \
+    if (!(cond)) {                                                      \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++failures;                                                       \
+    }                                                                   \
+  } while (0)
+
+static size_t naive_count(const std::string& t, const std::string& p) {
+  if (p.empty()) return t.size();
+  size_t c = 0;
+  for (size_t i = 0; i + p.size() <= t.size(); ++i) c += t.compare(i, p.size(), p) == 0;
+  return c;
+}
+
+int main() {
+  {  // fm_search_tests.cpp:53-67
+    FMIndex idx = FMIndex::build_from_text("", BuildParams{});
+    CHECK(idx.count("") == 0);
+    CHECK(idx.count("x") == 0);
+    CHECK(idx.locate("x").empty());
+    FMIndex idx2 = FMIndex::build_from_text("hello$", BuildParams{});
+    CHECK(idx2.count("") == 6);
+  }
+  {  // fm_search_tests.cpp:69-113 / simple_tests.cpp:6-13
+    FMIndex idx = FMIndex::build_from_text("banana$", BuildParams{});
+    CHECK(idx.count("banana") == 1);
+    CHECK(idx.count("ana") == 2);
+    CHECK(idx.count("na") == 2);
+    CHECK(idx.count("a") == 3);
+    CHECK(idx.count("b") == 1);
+    CHECK(idx.count("$") == 1);
+    CHECK(idx.count("x") == 0);
+    CHECK(idx.count("anana") == 1);
+    CHECK((idx.locate("ana") == std::vector<uint64_t>{3, 1}));    // BWT-row order
+    CHECK((idx.locate("a") == std::vector<uint64_t>{5, 3, 1}));
+    CHECK((idx.locate("banana") == std::vector<uint64_t>{0}));
+    CHECK(idx.locate("x").empty());
+    CHECK(idx.extract(1, 3) == "ana");
+    CHECK(idx.extract(5, 10) == "a$");
+    CHECK(idx.extract(7, 1).empty());
+    auto cb = idx.count_batch({"ana", "", "nab", "a"});
+    CHECK((cb == std::vector<uint64_t>{2, 7, 0, 3}));
+    auto lb = idx.locate_batch({"ana", "x", "a"}, 2);
+    CHECK((lb[0] == std::vector<uint64_t>{3, 1}) && lb[1].empty() &&
+          (lb[2] == std::vector<uint64_t>{5, 3}));
+  }
+  {  // fm_search_tests.cpp:130-152 (stride 4)
+    BuildParams p;
+    p.ssa_stride = 4;
+    std::string t = "aabaabaa$";
+    FMIndex idx = FMIndex::build_from_text(t, p);
+    for (const char* q : {"a", "aa", "aab"}) CHECK(idx.count(q) == naive_count(t, q));
+  }
+  {  // fm_search_tests.cpp:154-173
+    FMIndex idx = FMIndex::build_from_text("abababab$", BuildParams{});
+    CHECK(idx.count("ab") == 4 && idx.count("aba") == 3 && idx.count("abab") == 3);
+    auto pos = idx.locate("aba");
+    std::sort(pos.begin(), pos.end());
+    CHECK((pos == std::vector<uint64_t>{0, 2, 4}));
+  }
+  {  // fm_search_tests.cpp:175-198: '$' occurs twice -> the reference returns 2
+    std::string t;
+    for (int i = 1; i < 256; ++i) t += static_cast<char>(i);
+    t += '$';
+    FMIndex idx = FMIndex::build_from_text(t, BuildParams{});
+    for (int i = 1; i < 256; ++i) {
+      std::string q(1, static_cast<char>(i));
+      CHECK(idx.count(q) == (i == '$' ? 2u : 1u));
+    }
+  }
+  {  // fm_search_tests.cpp:237-261 vs naive
+    std::string t = "The quick brown fox jumps over the lazy dog. The five boxing wizards jump "
+                    "quickly. Pack my box with five dozen liquor jugs.$";
+    FMIndex idx = FMIndex::build_from_text(t, BuildParams{});
+    for (const char* q : {"The", "the", "quick", "fox", "dog", "jump", "five", "box", "xyz", " ",
+                          ".", "qu", "ing", "ck", "ox"})
+      CHECK(idx.count(q) == naive_count(t, q) && idx.locate(q).size() == naive_count(t, q));
+  }
+  {  // cyclic-BWT quirk without a terminator: the reference throws from locate
+    FMIndex idx = FMIndex::build_from_text("abab", BuildParams{});
+    CHECK(idx.count("ba") == 2);
+    bool threw = false;
+    try {
+      idx.locate("ab");
+    } catch (const std::runtime_error& e) {
+      threw = std::string(e.what()) == "locate: LF walk exceeded text length";
+    }
+    CHECK(threw);
+  }
+  {  // fm_index.cpp:71-73
+    bool threw = false;
+    try {
+      FMIndex::open_directory("/tmp");
+    } catch (const std::runtime_error& e) {
+      threw = std::string(e.what()) == "on-disk open not implemented yet";
+    }
+    CHECK(threw);
+  }
+  if (failures) {
+    std::fprintf(stderr, "%d facade checks failed\n", failures);
+    return 1;
+  }
+  std::printf("facade tests PASSED\n");
+  return 0;
+}

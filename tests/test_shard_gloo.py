@@ -1,0 +1,89 @@
+"""Multi-process (world_size 2 and 3, gloo, CPU) test of the query-sharding path
+used by bench.py on N GPUs: contiguous shards, local count, gather to rank 0, and
+the variable-length gather for located positions.  The per-shard engine here is
+the oracle stand-in (the HIP engine needs a GPU); the collective plumbing is the
+same code (shard.py)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, total, result_path):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import load_pkg
+    import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib
+    load_pkg()
+    shard = importlib.import_module("cs_fmindex_amd.shard")
+    text = O.gen_dna(5, 50_000)
+    idx = O.Index(text.tobytes())  # replicated index (stand-in engine)
+    pats = O.gen_patterns_text(text, 20, total, seed=4242)
+
+    def count_fn(lo, hi):
+        buf = np.ascontiguousarray(pats[lo:hi]).reshape(-1)
+        offs = np.arange(0, (hi - lo + 1) * 20, 20, dtype=np.uint64)
+        return torch.from_numpy(idx.count_batch(buf=buf, offs=offs).astype(np.int64))
+
+    full = shard.sharded_count(count_fn, total, world, rank, torch.device("cpu"))
+    lo, hi = shard.shard_range(total, rank, world)
+    # variable-length gather of located positions of the shard's first patterns
+    pos = []
+    for q in range(lo, min(hi, lo + 5)):
+        pos += idx.locate(pats[q].tobytes())
+    parts = shard.gather_v(torch.tensor(pos, dtype=torch.int64), world, rank)
+    if rank == 0:
+        want = idx.count_batch([bytes(p) for p in pats]).astype(np.int64)
+        ok = bool(np.array_equal(full.numpy(), want))
+        want_pos = []
+        for r in range(world):
+            a, b = shard.shard_range(total, r, world)
+            v = []
+            for q in range(a, min(b, a + 5)):
+                v += idx.locate(pats[q].tobytes())
+            want_pos.append(v)
+        ok &= [p.tolist() for p in parts] == want_pos
+        with open(result_path, "w") as f:
+            f.write("ok" if ok else "mismatch")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,total", [(2, 1000), (3, 1001), (2, 1)])
+def test_sharded_count_gloo(tmp_path, world, total):
+    res = tmp_path / "res.txt"
+    mp.start_processes(_worker, args=(world, _free_port(), total, str(res)), nprocs=world,
+                       join=True, start_method="spawn")
+    assert res.read_text() == "ok"
+
+
+def test_shard_range_partition():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from conftest import load_pkg
+    import importlib
+    load_pkg()
+    shard = importlib.import_module("cs_fmindex_amd.shard")
+    for total in (0, 1, 7, 100, 101):
+        for world in (1, 2, 3, 8):
+            rs = [shard.shard_range(total, r, world) for r in range(world)]
+            cover = [i for a, b in rs for i in range(a, b)]
+            assert cover == list(range(total))
