@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p50-calls", type=int, default=1000)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--locate-batch", type=int, default=1_000_000,
                     help="patterns of the batch timed through locate() (N=1 only; 0 = skip)")
     ap.add_argument("--prefix-k", type=int, default=None,
@@ -72,10 +74,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    local_dev = local % max(ndev, 1)  # identity on an N-GPU node; lets a 1-GPU box rehearse N ranks
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     pkg = _load_pkg()
     import importlib
     shard = importlib.import_module("cs_fmindex_amd.shard")
@@ -90,7 +97,7 @@ def main():
     pkg.synth_text_device(args.kind, 42, L, text.data_ptr(), sh)
     torch.cuda.synchronize()
     idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
-                                             pkg.BuildParams(ssa_stride=args.ssa_stride), device=local)
+                                             pkg.BuildParams(ssa_stride=args.ssa_stride), device=local_dev)
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t0
     info = idx.info()
@@ -105,7 +112,9 @@ def main():
     offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
     pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, pats.data_ptr(),
                               offs.data_ptr(), sh)
-    out = torch.empty(B, dtype=torch.int64, device=dev)
+    # counts land in double-buffered shards; for N > 1 the gather of step k overlaps
+    # the count of step k+1 (shard.PipelinedGather)
+    pg = shard.PipelinedGather(B, world, rank, torch.int64, dev)
 
     # algorithmic bytes per launch: 2 rank-line reads (sp, ep) per non-pure wavelet level
     # per backward-search step the kernel performs; one line = 32 B (Line32, n < 2^32)
@@ -130,13 +139,11 @@ def main():
     del P2
     torch.cuda.synchronize()
 
-    def step():
-        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, out.data_ptr(), sh)
-        if world > 1:
-            shard.gather_counts(out, total, world, rank)
-
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        o = pg.buffer(k)
+        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, o.data_ptr(), sh)
+        pg.submit(k)
+    pg.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -145,11 +152,12 @@ def main():
            for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
+        o = pg.buffer(k)
         evs[k][0].record(stream)
-        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, out.data_ptr(), sh)
+        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, o.data_ptr(), sh)
         evs[k][1].record(stream)
-        if world > 1:
-            shard.gather_counts(out, total, world, rank)
+        pg.submit(k)
+    pg.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,6 +172,7 @@ def main():
     value = total_units / elapsed
     kern_avg_s = statistics.mean(kern_ms) / 1e3
     achieved = alg_bytes / kern_avg_s / 1e9
+    out = pg.local[(args.steps - 1) % pg.depth]
     counts = out.cpu().numpy()
     found = int((counts >= 1).sum())
 

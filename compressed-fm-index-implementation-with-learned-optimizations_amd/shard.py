@@ -61,6 +61,55 @@ def gather_v(local: torch.Tensor, world: int, rank: int, dst: int = 0):
     return [p[:l] for p, l in zip(parts, lens)]
 
 
+class PipelinedGather:
+    """Double-buffered gather of fixed-size shards, overlapped with compute.
+
+    Step k writes its shard into buffer(k) (which first waits for the gather that
+    last used that buffer) and submit(k) starts an asynchronous gather of it to dst.
+    On the GPU the count kernel of step k+1 (compute stream) runs while the gather
+    of step k moves over xGMI (RCCL's stream); finish() waits for every gather.
+    """
+
+    def __init__(self, per: int, world: int, rank: int, dtype, device, dst: int = 0, depth: int = 2):
+        self.world, self.rank, self.dst, self.depth = world, rank, dst, depth
+        self.local = [torch.empty(per, dtype=dtype, device=device) for _ in range(depth)]
+        # gloo gathers host tensors only: stage GPU shards through the host (rehearsal
+        # of the N-rank path on one GPU; the GPU box's N-GPU runs use RCCL directly)
+        self.stage = (world > 1 and torch.device(device).type == "cuda"
+                      and dist.get_backend() == "gloo")
+        rdev = "cpu" if self.stage else device
+        self.recv = ([[torch.empty(per, dtype=dtype, device=rdev) for _ in range(world)]
+                      for _ in range(depth)] if rank == dst else [None] * depth)
+        self.work = [None] * depth
+
+    def buffer(self, k: int) -> torch.Tensor:
+        i = k % self.depth
+        if self.work[i] is not None:
+            self.work[i].wait()
+            self.work[i] = None
+        return self.local[i]
+
+    def submit(self, k: int):
+        i = k % self.depth
+        if self.world == 1:
+            return
+        src = self.local[i].cpu() if self.stage else self.local[i]
+        self.work[i] = dist.gather(src, self.recv[i], dst=self.dst, async_op=True)
+
+    def finish(self):
+        for i, w in enumerate(self.work):
+            if w is not None:
+                w.wait()
+                self.work[i] = None
+
+    def result(self, k: int):
+        """Gathered vector of step k on dst (valid after finish())."""
+        i = k % self.depth
+        if self.world == 1:
+            return self.local[i]
+        return torch.cat(self.recv[i]) if self.rank == self.dst else None
+
+
 def sharded_count(count_fn, total: int, world: int, rank: int, device, dst: int = 0):
     """Run this rank's contiguous shard with count_fn and gather all to dst."""
     lo, hi = shard_range(total, rank, world)

@@ -51,9 +51,29 @@ def _worker(rank, world, port, total, result_path):
     for q in range(lo, min(hi, lo + 5)):
         pos += idx.locate(pats[q].tobytes())
     parts = shard.gather_v(torch.tensor(pos, dtype=torch.int64), world, rank)
+    # pipelined, double-buffered gather over 5 steps of equal shards (bench.py N > 1)
+    per = (total + world - 1) // world
+    pg = shard.PipelinedGather(per, world, rank, torch.int64, torch.device("cpu"))
+    for k in range(5):
+        buf = pg.buffer(k)
+        buf.zero_()
+        v = count_fn(lo, hi) + k
+        buf[: v.numel()] = v
+        pg.submit(k)
+        if k == 2:
+            pg.finish()
+            step2 = pg.result(2)
+            step2 = None if step2 is None else step2.clone()
+    pg.finish()
+    last = pg.result(4)
     if rank == 0:
         want = idx.count_batch([bytes(p) for p in pats]).astype(np.int64)
         ok = bool(np.array_equal(full.numpy(), want))
+        for k, got in ((2, step2), (4, last)):
+            parts_k = [got[r * per:(r + 1) * per][: max(0, shard.shard_range(total, r, world)[1]
+                                                         - shard.shard_range(total, r, world)[0])]
+                       for r in range(world)]
+            ok &= bool(np.array_equal(torch.cat(parts_k).numpy(), want + k))
         want_pos = []
         for r in range(world):
             a, b = shard.shard_range(total, r, world)
