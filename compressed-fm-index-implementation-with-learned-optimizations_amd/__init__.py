@@ -52,12 +52,16 @@ SIGNATURES = {
     "cs_fm_build_from_device_text": (C.c_int, [_vp, C.c_uint64, C.POINTER(cs_build_params), C.c_int,
                                                C.POINTER(_vp)]),
     "cs_fm_open_directory": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
+    "cs_fm_open_directory_on": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
+    "cs_fm_save_directory": (C.c_int, [_vp, C.c_char_p]),
     "cs_fm_destroy": (None, [_vp]),
     "cs_fm_get_info": (C.c_int, [_vp, C.POINTER(cs_fm_info)]),
     "cs_fm_last_error": (C.c_char_p, []),
     "cs_fm_count": (C.c_int, [_vp, _u8p, C.c_uint64, _u64p]),
     "cs_fm_locate": (C.c_int, [_vp, _u8p, C.c_uint64, C.c_uint64, _u64p, C.c_uint64, _u64p]),
     "cs_fm_extract": (C.c_int, [_vp, C.c_uint64, C.c_uint64, _u8p, _u64p]),
+    "cs_fm_extract_batch": (C.c_int, [_vp, _u64p, _u64p, C.c_uint64, _u64p, _u8p, C.c_uint64,
+                                      _u64p]),
     "cs_fm_count_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p, _vp]),
     "cs_fm_locate_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, C.c_uint64, _u64p, _u64p,
                                      C.c_uint64, _u64p, _vp]),
@@ -191,10 +195,19 @@ class FMIndex:
         return FMIndex(h, n)
 
     @staticmethod
-    def open_directory(path: str):
+    def open_directory(path: str, device: int | None = None):
+        """Open an index written by save_directory (the reference's TODO,
+        src/api/fm_index.hpp:20)."""
+        if device is None:
+            device = int(os.environ.get("CS_FM_DEVICE", "0"))
         h = _vp()
-        _check(lib().cs_fm_open_directory(path.encode(), C.byref(h)))
-        return FMIndex(h, 0)
+        _check(lib().cs_fm_open_directory_on(path.encode(), device, C.byref(h)))
+        idx = FMIndex(h, 0)
+        idx.n = idx.info().n
+        return idx
+
+    def save_directory(self, path: str):
+        _check(lib().cs_fm_save_directory(self._h, path.encode()))
 
     # -- queries (fm_index.hpp:26-37) -------------------------------------
     def count(self, pattern) -> int:
@@ -213,6 +226,24 @@ class FMIndex:
         got = C.c_uint64()
         _check(lib().cs_fm_extract(self._h, pos, length, _u8(out), C.byref(got)))
         return out[: got.value].tobytes()
+
+    def extract_batch(self, positions, lengths):
+        """Device extract of many (pos, len) by LF inversion -> list of bytes."""
+        p = np.ascontiguousarray(positions, np.uint64)
+        l = np.ascontiguousarray(lengths, np.uint64)
+        k = len(p)
+        oo = np.zeros(k + 1, np.uint64)
+        tot = C.c_uint64()
+        st = lib().cs_fm_extract_batch(self._h, _u64(p), _u64(l), k, _u64(oo), None, 0,
+                                       C.byref(tot))
+        if st == CS_OK:
+            return [b""] * k
+        if st != CS_ERR_CAPACITY:
+            _check(st)
+        out = np.zeros(tot.value, np.uint8)
+        _check(lib().cs_fm_extract_batch(self._h, _u64(p), _u64(l), k, _u64(oo), _u8(out),
+                                         tot.value, C.byref(tot)))
+        return [out[oo[q]:oo[q + 1]].tobytes() for q in range(k)]
 
     # -- batched ----------------------------------------------------------
     def count_batch(self, patterns=None, buf=None, offs=None) -> np.ndarray:

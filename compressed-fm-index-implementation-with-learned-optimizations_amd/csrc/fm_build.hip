@@ -103,15 +103,17 @@ __global__ void k_double_keys(const uint32_t* __restrict__ rank, uint64_t n, uin
   }
 }
 
-// bwt.hpp:7-15 and fm_index.cpp:57-66 in one pass.
+// bwt.hpp:7-15 and fm_index.cpp:57-66 in one pass, plus the inverse-SA samples
+// (row of every stride-th text position) for extract.
 __global__ void k_bwt_ssa(const uint8_t* __restrict__ t, const uint32_t* __restrict__ sa,
                           uint32_t n, uint32_t stride, uint8_t* __restrict__ bwt,
-                          uint32_t* __restrict__ ssa) {
+                          uint32_t* __restrict__ ssa, uint32_t* __restrict__ isa) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gs) {
     const uint32_t s = sa[j];
     bwt[j] = t[s == 0 ? n - 1 : s - 1];
     if (j % stride == 0) ssa[j / stride] = s;
+    if (s % stride == 0) isa[s / stride] = j;
   }
 }
 
@@ -393,13 +395,16 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   DevBuf bwt;
   FMX_HIP(bwt.alloc(n));
   FMX_HIP(hipMalloc(&h->d_ssa, (h->nsamples ? h->nsamples : 1) * 4));
+  h->nisa = h->nsamples;  // text positions 0, stride, 2*stride, ... < n
+  FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * 4));
   if (n) {
     DevBuf sa;
     FMX_HIP(sa.alloc(n * 4));
     cs_status s = build_sa_device(d_text, n, sa.as<uint32_t>(), st);
     if (s != CS_OK) return s;
     k_bwt_ssa<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(d_text, sa.as<uint32_t>(), (uint32_t)n,
-                                                         stride, bwt.as<uint8_t>(), h->d_ssa);
+                                                         stride, bwt.as<uint8_t>(), h->d_ssa,
+                                                         h->d_isa);
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipStreamSynchronize(st));
   }
@@ -424,6 +429,13 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     cum += hist[c];
   }
   T.C[256] = cum;
+  if (n) {
+    uint8_t last = 0;
+    FMX_HIP(hipMemcpy(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost));
+    int smallest = 0;
+    while (smallest < 256 && hist[smallest] == 0) ++smallest;
+    h->lf_exact = hist[last] == 1 && last == smallest;
+  }
   for (int l = 0; l <= kLevels; ++l) {
     const int np = 1 << l;
     std::vector<uint64_t> cnt(np, 0);

@@ -1,6 +1,7 @@
 // fm_capi.hip — the extern "C" boundary (include/cs_fmindex.h).  Host-buffer entry
 // points stage through HBM; *_device entry points only launch.  No CPU fallback:
 // without a HIP device every call fails with CS_ERR_NO_DEVICE.
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -72,6 +73,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_table) (void)hipFree(h->d_table);
   if (h->d_err) (void)hipFree(h->d_err);
   if (h->d_ptab) (void)hipFree(h->d_ptab);
+  if (h->d_isa) (void)hipFree(h->d_isa);
   delete h;
 }
 
@@ -149,10 +151,9 @@ cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
 }
 
 cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out) {
-  (void)dir;
-  if (out) *out = nullptr;
-  set_error("on-disk open not implemented yet");  // fm_index.cpp:72
-  return CS_ERR_UNSUPPORTED;
+  int dev = 0;
+  if (const char* e = std::getenv("CS_FM_DEVICE")) dev = std::atoi(e);
+  return cs_fm_open_directory_on(dir, dev, out);
 }
 
 void cs_fm_destroy(cs_fm_index* h) {
@@ -327,6 +328,51 @@ cs_status cs_fm_locate(const cs_fm_index* h, const uint8_t* pattern, uint64_t m,
   return s;
 }
 
+cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const uint64_t* len,
+                              uint64_t k, uint64_t* out_offs, uint8_t* out, uint64_t cap,
+                              uint64_t* total) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (!total || !out_offs || (k && (!pos || !len))) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  const uint64_t n = h->n;
+  uint64_t acc = 0;
+  for (uint64_t q = 0; q < k; ++q) {  // fm_index.cpp:164-165 clamping
+    out_offs[q] = acc;
+    if (pos[q] < n) acc += len[q] < n - pos[q] ? len[q] : n - pos[q];
+  }
+  out_offs[k] = acc;
+  *total = acc;
+  if (acc > cap) {
+    set_error("extract output capacity too small");
+    return CS_ERR_CAPACITY;
+  }
+  if (!acc) return CS_OK;
+  if (!h->lf_exact) {
+    set_error("device extract needs a text ending in a unique smallest symbol");
+    return CS_ERR_UNSUPPORTED;
+  }
+  if (!out) {
+    set_error("null output buffer");
+    return CS_ERR_INVALID;
+  }
+  DevBuf dp, dl, doo, dout;
+  FMX_HIP(dp.alloc(k * 8));
+  FMX_HIP(dl.alloc(k * 8));
+  FMX_HIP(doo.alloc((k + 1) * 8));
+  FMX_HIP(dout.alloc(acc));
+  FMX_HIP(hipMemcpy(dp.p, pos, k * 8, hipMemcpyHostToDevice));
+  FMX_HIP(hipMemcpy(dl.p, len, k * 8, hipMemcpyHostToDevice));
+  FMX_HIP(hipMemcpy(doo.p, out_offs, (k + 1) * 8, hipMemcpyHostToDevice));
+  s = launch_extract(h, dp.as<uint64_t>(), dl.as<uint64_t>(), doo.as<uint64_t>(), k,
+                     dout.as<uint8_t>(), nullptr);
+  if (s != CS_OK) return s;
+  FMX_HIP(hipMemcpy(out, dout.p, acc, hipMemcpyDeviceToHost));
+  return CS_OK;
+}
+
 cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_t* out,
                         uint64_t* nout) {
   if (!h || !nout) {
@@ -334,16 +380,22 @@ cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_
     return CS_ERR_INVALID;
   }
   *nout = 0;
-  const uint64_t n = h->h_text.size();  // fm_index.cpp:163-167
+  const uint64_t n = h->n;  // fm_index.cpp:163-167
   if (pos >= n) return CS_OK;
   if (len > n - pos) len = n - pos;
   if (len && !out) {
     set_error("null output buffer");
     return CS_ERR_INVALID;
   }
-  std::memcpy(out, h->h_text.data() + pos, len);
-  *nout = len;
-  return CS_OK;
+  if (h->h_text.size() == n) {  // the text_ copy, as the reference keeps it
+    std::memcpy(out, h->h_text.data() + pos, len);
+    *nout = len;
+    return CS_OK;
+  }
+  uint64_t oo[2], tot = 0;  // no host text: LF inversion on the device
+  cs_status s = cs_fm_extract_batch(h, &pos, &len, 1, oo, out, len, &tot);
+  if (s == CS_OK) *nout = tot;
+  return s;
 }
 
 }  // extern "C"

@@ -65,6 +65,12 @@ struct DevIndex {
   const uint2* ptab;
   uint32_t ptab_k;
   uint32_t ptab_sigma;
+  // Inverse-SA samples: isa[k] = row of the suffix at text position k*stride, for
+  // extract by LF inversion (needs suffix order == rotation order, i.e. a unique
+  // smallest last symbol: lf_exact).
+  const uint32_t* isa;
+  uint64_t nisa;
+  uint32_t lf_exact;
 };
 
 __host__ __device__ inline int node_id(int level, uint32_t prefix) {

@@ -52,11 +52,20 @@ FMIndex FMIndex::build_from_text(const std::string& text, const BuildParams& p) 
 
 FMIndex FMIndex::open_directory(const std::string& dir) {
   cs_fm_index* h = nullptr;
-  cs_status s = cs_fm_open_directory(dir.c_str(), &h);
+  cs_status s = cs_fm_open_directory_on(dir.c_str(), pick_device(), &h);
   if (s != CS_OK) raise(s);
   FMIndex idx;
+  cs_fm_info info;
+  (void)cs_fm_get_info(h, &info);
+  idx.meta_.n = info.n;
   idx.h_ = std::shared_ptr<cs_fm_index>(h, cs_fm_destroy);
   return idx;
+}
+
+void FMIndex::save_directory(const std::string& dir) const {
+  if (!h_) throw std::runtime_error("save_directory: empty index");
+  cs_status s = cs_fm_save_directory(h_.get(), dir.c_str());
+  if (s != CS_OK) raise(s);
 }
 
 uint64_t FMIndex::count(std::string_view pattern) const {

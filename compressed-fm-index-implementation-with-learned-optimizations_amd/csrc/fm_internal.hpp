@@ -23,6 +23,9 @@ struct cs_fm_index {
   fmx::NodeTable h_table{};
   uint64_t* d_err = nullptr;          // locate: min failing item (UINT64_MAX = none)
   uint2* d_ptab = nullptr;            // prefix table (DevIndex::ptab)
+  uint32_t* d_isa = nullptr;          // inverse-SA samples (extract)
+  uint64_t nisa = 0;
+  bool lf_exact = false;              // unique smallest last symbol: LF inverts SA
   uint32_t ptab_k = 0, ptab_sigma = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
@@ -45,6 +48,9 @@ struct cs_fm_index {
     d.ptab = d_ptab;
     d.ptab_k = ptab_k;
     d.ptab_sigma = ptab_sigma;
+    d.isa = d_isa;
+    d.nisa = nisa;
+    d.lf_exact = lf_exact ? 1u : 0u;
     return d;
   }
 };
@@ -85,6 +91,8 @@ cs_status launch_wt_rank(const cs_fm_index* h, const uint8_t* d_syms, const uint
 cs_status launch_wt_access(const cs_fm_index* h, const uint64_t* d_pos, uint64_t k,
                            uint8_t* d_out, hipStream_t st);
 cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st);
+cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
+                         const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st);
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st);

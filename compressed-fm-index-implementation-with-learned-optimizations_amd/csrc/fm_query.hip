@@ -341,6 +341,39 @@ __global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
   if (sym) sym[t] = (uint8_t)c;
 }
 
+// extract(pos, len) (fm_index.cpp:163-167) without the text: start at the
+// inverse-SA sample of the first sampled text position e >= pos+len (position n =
+// suffix 0 cyclically, whose BWT symbol is T[n-1]) and invert LF down to pos; each
+// LF step yields BWT[row] = T[cur-1].  One lane per query; requires lf_exact.
+template <class F>
+__global__ __launch_bounds__(kBlk) void k_extract(DevIndex ix, const uint64_t* __restrict__ pos,
+                                                  const uint64_t* __restrict__ len,
+                                                  const uint64_t* __restrict__ out_offs,
+                                                  uint64_t k, uint8_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= k) return;
+  const uint64_t n = ix.n;
+  const uint64_t p = pos[q];
+  if (p >= n) return;  // fm_index.cpp:164: empty
+  uint64_t L = len[q];
+  if (L > n - p) L = n - p;
+  const uint64_t end = p + L;
+  const uint64_t s = ix.stride;
+  uint64_t e = ((end + s - 1) / s) * s;
+  if (e >= n) e = n;
+  uint64_t row = ix.isa[e == n ? 0 : e / s];
+  uint8_t* o = out + out_offs[q];
+  for (uint64_t cur = e; cur > p; --cur) {
+    uint32_t c;
+    const uint64_t nxt = lf_step<F>(ix, T, row, &c);
+    if (cur - 1 < end) o[cur - 1 - p] = (uint8_t)c;
+    row = nxt;
+  }
+}
+
 // WaveletTree::access for every row (the BWT), grid-stride.
 template <class F>
 __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__ out) {
@@ -422,6 +455,14 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     k_build_ptab<Line64><<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(ix, entries, h->d_ptab);
   FMX_HIP(hipGetLastError());
   FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
+                         const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st) {
+  if (!k) return CS_OK;
+  FMX_DISPATCH(h, k_extract, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), d_pos, d_len, d_out_offs, k,
+               d_out);
   return CS_OK;
 }
 

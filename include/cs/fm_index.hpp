@@ -4,9 +4,9 @@
 // exceptions as cs::FMIndex (src/api/fm_index.hpp:11-67); the work runs on the GPU
 // through the C ABI in cs_fmindex.h (implementation: csrc/fm_facade.cpp inside
 // libcs_fmindex.so).  Additions: count_batch / locate_batch (one launch for many
-// patterns) and handle() for the raw ABI.  Errors are std::runtime_error with the
-// reference's message text ("locate: LF walk exceeded text length",
-// "on-disk open not implemented yet").
+// patterns), save_directory (the on-disk format open_directory reads) and handle()
+// for the raw ABI.  Errors are std::runtime_error with the reference's message text
+// ("locate: LF walk exceeded text length").
 //
 // Semantics kept from the reference: plain suffix order and a
 // cyclic BWT, so callers append their own unique smallest terminator as before;
@@ -37,7 +37,10 @@ class FMIndex {
   FMIndex() = default;
   // Builds on the current HIP device (hipGetDevice), or CS_FM_DEVICE if set.
   static FMIndex build_from_text(const std::string& text, const BuildParams& p);
-  static FMIndex open_directory(const std::string& dir);  // throws, as the reference
+  // Opens an index written by save_directory (the reference's TODO, fm_index.hpp:20;
+  // it throws there).  Throws std::runtime_error("cannot open: ...") otherwise.
+  static FMIndex open_directory(const std::string& dir);
+  void save_directory(const std::string& dir) const;
 
   uint64_t count(std::string_view pattern) const;
   std::vector<uint64_t> locate(std::string_view pattern, size_t limit = 100000) const;

@@ -81,9 +81,14 @@ cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_
 cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
                                        const cs_build_params* p, int device,
                                        cs_fm_index** out);
-/* FMIndex::open_directory — fm_index.hpp:20, fm_index.cpp:71-73 (throws there):
- * returns CS_ERR_UNSUPPORTED with the reference's message. */
+/* FMIndex::open_directory — fm_index.hpp:20 ("TODO: on-disk format"); the reference
+ * throws (fm_index.cpp:71-73).  Here it opens an index written by
+ * cs_fm_save_directory onto device CS_FM_DEVICE (default 0);
+ * a missing or foreign directory fails with CS_ERR_INVALID ("cannot open: <path>"). */
 cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out);
+cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out);
+/* Writes the index (HBM images of every structure, plus the text when kept) to dir. */
+cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir);
 void cs_fm_destroy(cs_fm_index* h);
 cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out);
 const char* cs_fm_last_error(void);
@@ -97,6 +102,15 @@ cs_status cs_fm_locate(const cs_fm_index* h, const uint8_t* pattern, uint64_t m,
 /* FMIndex::extract — fm_index.hpp:37, fm_index.cpp:163-167 (clamped substring). */
 cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_t* out,
                         uint64_t* nout);
+
+/* Batched extract on the device (fm_index.cpp:163-167 semantics: pos >= n gives
+ * "", len clamped to n - pos) by LF inversion from inverse-SA samples — the text
+ * itself is not needed.  Requires a text whose last symbol is unique and the
+ * smallest (the standard terminator; otherwise CS_ERR_UNSUPPORTED).  out_offs has
+ * k+1 entries (CSR into out); if *total > cap: CS_ERR_CAPACITY, out_offs valid. */
+cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const uint64_t* len,
+                              uint64_t k, uint64_t* out_offs, uint8_t* out, uint64_t cap,
+                              uint64_t* total);
 
 /* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers. */
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,

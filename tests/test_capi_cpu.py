@@ -75,11 +75,13 @@ def test_fails_loudly_without_gpu():
         pkg.sa_build(b"banana$")
 
 
-def test_open_directory_throws_like_reference():
+def test_open_directory_missing():
+    """The reference throws from open_directory (src/api/fm_index.cpp:71-73); here it
+    opens saved indexes and throws for anything else (no GPU needed to fail)."""
     pkg = load_pkg()
     with pytest.raises(RuntimeError) as ei:
         pkg.FMIndex.open_directory("/nonexistent")
-    assert str(ei.value) == "on-disk open not implemented yet"
+    assert "cannot open: /nonexistent/cs_fmindex.meta" in str(ei.value)
 
 
 def test_build_params_defaults_match_reference():

@@ -24,6 +24,7 @@ def test_facade_compiles_and_links(tmp_path):
 def test_facade_runs_reference_tests(tmp_path):
     exe = str(tmp_path / "facade_tests")
     _compile(exe)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    env = dict(os.environ, FACADE_TMPDIR=str(tmp_path / "idx"))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr
     assert "PASSED" in r.stdout

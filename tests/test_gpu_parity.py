@@ -8,6 +8,8 @@ Layers checked separately, bottom-up:
   access / LF       (fused descent)              vs BWT / FMIndex::LF, every row
   count / locate    (batched kernels)            vs golden vectors and the oracle
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -246,3 +248,43 @@ def test_lf_overrun_message(pkg):
         assert str(ei.value) == loc["error"]
     # the engine stays usable after the error
     assert g.count(b"ab") == 2
+
+
+def test_save_open_directory_roundtrip(pkg, tmp_path):
+    """On-disk format (the reference's open_directory TODO): the reopened index
+    answers identically; an index without its text extracts on the device."""
+    t = O.gen_dna(21, 40000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    d = str(tmp_path / "idx")
+    g.save_directory(d)
+    h = pkg.FMIndex.open_directory(d)
+    assert h.n == len(t)
+    rng = np.random.default_rng(4)
+    pats = [t[i:i + m] for i, m in zip(rng.integers(0, 39000, 300), rng.integers(1, 30, 300))]
+    assert h.count_batch(pats).tolist() == g.count_batch(pats).tolist()
+    a = g.locate_batch(pats, limit=20)
+    b = h.locate_batch(pats, limit=20)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert h.extract(100, 50) == t[100:150]
+    os.remove(os.path.join(d, "text.bin"))
+    meta = open(os.path.join(d, "cs_fmindex.meta")).read().replace("has_text 1", "has_text 0")
+    open(os.path.join(d, "cs_fmindex.meta"), "w").write(meta)
+    k = pkg.FMIndex.open_directory(d)
+    assert k.extract(100, 50) == t[100:150]  # device LF inversion
+    assert k.extract(len(t) - 5, 10) == t[-5:]
+
+
+def test_device_extract(pkg):
+    """Batched extract by LF inversion from inverse-SA samples == text slices
+    (fm_index.cpp:163-167 clamping), for every start position of a small text."""
+    for stride in (1, 5, 32):
+        t = O.gen_dna(stride, 3000).tobytes()
+        g = pkg.FMIndex.build_from_text(t, pkg.BuildParams(ssa_stride=stride))
+        pos = list(range(0, len(t) + 3))
+        lens = [(p * 7) % 45 for p in pos]
+        got = g.extract_batch(pos, lens)
+        assert got == [t[p:p + l] for p, l in zip(pos, lens)]
+    g = pkg.FMIndex.build_from_text(b"abab")  # no unique smallest terminator
+    with pytest.raises(RuntimeError):
+        g.extract_batch([0], [2])
+    assert g.extract(0, 2) == b"ab"  # host text copy, as the reference
