@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 
 #include "fm_internal.hpp"
 
@@ -105,9 +106,10 @@ __global__ void k_double_keys(const uint32_t* __restrict__ rank, uint64_t n, uin
 
 // bwt.hpp:7-15 and fm_index.cpp:57-66 in one pass, plus the inverse-SA samples
 // (row of every stride-th text position) for extract.
+template <class SampleT>
 __global__ void k_bwt_ssa(const uint8_t* __restrict__ t, const uint32_t* __restrict__ sa,
                           uint32_t n, uint32_t stride, uint8_t* __restrict__ bwt,
-                          uint32_t* __restrict__ ssa, uint32_t* __restrict__ isa) {
+                          SampleT* __restrict__ ssa, SampleT* __restrict__ isa) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gs) {
     const uint32_t s = sa[j];
@@ -367,12 +369,17 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     set_error("ssa_stride must be > 0");
     return CS_ERR_INVALID;
   }
-  if (n >= (1ull << 32)) {
-    set_error("text length must be < 2^32 (uint32 suffix array, src/core/sais.hpp:9)");
+  if (n >= (1ull << 38)) {
+    set_error("text length must be < 2^38");
     return CS_ERR_INVALID;
   }
   h->n = n;
   h->stride = stride;
+  // wide index: u64 samples / table entries and 64-B lines (n >= 2^32, or forced
+  // by the CS_FM_WIDE test hook)
+  h->wide = n >= (1ull << 32);
+  if (const char* e = std::getenv("CS_FM_WIDE"))
+    if (std::atoi(e) == 1) h->wide = true;
   h->nsamples = (n + stride - 1) / stride;
   NodeTable& T = h->h_table;
   std::memset(&T, 0, sizeof T);
@@ -394,24 +401,36 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   // --- SA, BWT, SSA ---
   DevBuf bwt;
   FMX_HIP(bwt.alloc(n));
-  FMX_HIP(hipMalloc(&h->d_ssa, (h->nsamples ? h->nsamples : 1) * 4));
+  FMX_HIP(hipMalloc(&h->d_ssa, (h->nsamples ? h->nsamples : 1) * h->sample_bytes()));
   h->nisa = h->nsamples;  // text positions 0, stride, 2*stride, ... < n
-  FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * 4));
-  if (n) {
+  FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
+  bool bucketed = n >= (1ull << 32);
+  if (const char* e = std::getenv("CS_FM_SA_BUILDER"))
+    if (std::string(e) == "bucketed") bucketed = true;
+  if (n && bucketed) {  // BWT + samples pass by pass, no full SA (fm_bwt_bucketed.hip)
+    cs_status s = build_bwt_bucketed(d_text, n, stride, h->wide, bwt.as<uint8_t>(), h->d_ssa,
+                                     h->d_isa, st);
+    if (s != CS_OK) return s;
+  } else if (n) {  // prefix doubling over the full u32 SA
     DevBuf sa;
     FMX_HIP(sa.alloc(n * 4));
     cs_status s = build_sa_device(d_text, n, sa.as<uint32_t>(), st);
     if (s != CS_OK) return s;
-    k_bwt_ssa<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(d_text, sa.as<uint32_t>(), (uint32_t)n,
-                                                         stride, bwt.as<uint8_t>(), h->d_ssa,
-                                                         h->d_isa);
+    if (h->wide)
+      k_bwt_ssa<uint64_t><<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(
+          d_text, sa.as<uint32_t>(), (uint32_t)n, stride, bwt.as<uint8_t>(),
+          static_cast<uint64_t*>(h->d_ssa), static_cast<uint64_t*>(h->d_isa));
+    else
+      k_bwt_ssa<uint32_t><<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(
+          d_text, sa.as<uint32_t>(), (uint32_t)n, stride, bwt.as<uint8_t>(),
+          static_cast<uint32_t*>(h->d_ssa), static_cast<uint32_t*>(h->d_isa));
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipStreamSynchronize(st));
   }
   plog.mark("suffix array + bwt + ssa");
 
   // --- wavelet matrix levels as rank lines ---
-  h->line_bytes = n < (1ull << 32) ? 32 : 64;
+  h->line_bytes = h->wide ? 64 : 32;  // Line32 bases are u32
   if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force a format
     if (std::atoi(e) == 64) h->line_bytes = 64;
   h->line_bits = h->line_bytes == 32 ? Line32::kBits : Line64::kBits;

@@ -173,16 +173,12 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->line_bits = h->line_bits;
   out->lines_per_level = h->nlines;
   out->rank_bytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
-  out->ssa_bytes = h->nsamples * 4;
+  out->ssa_bytes = h->nsamples * h->sample_bytes();
   std::memcpy(out->active_levels, h->active_levels, sizeof out->active_levels);
   out->device = h->device;
   out->prefix_k = h->ptab_k;
   out->prefix_sigma = h->ptab_sigma;
-  out->prefix_bytes = h->ptab_k ? (uint64_t)sizeof(uint2) * [&] {
-    uint64_t e = 1;
-    for (uint32_t i = 0; i < h->ptab_k; ++i) e *= h->ptab_sigma;
-    return e;
-  }() : 0;
+  out->prefix_bytes = h->ptab_entries() * h->ptab_entry_bytes();
   for (int c = 0; c < 256; ++c) out->prefix_code[c] = h->h_table.code[c];
   return CS_OK;
 }
@@ -480,9 +476,13 @@ cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint6
   if (!len) return CS_ERR_INVALID;
   *len = h->nsamples;
   if (cap < h->nsamples) return CS_ERR_CAPACITY;
-  std::vector<uint32_t> tmp(h->nsamples);
-  if (h->nsamples) FMX_HIP(hipMemcpy(tmp.data(), h->d_ssa, h->nsamples * 4, hipMemcpyDeviceToHost));
-  for (uint64_t i = 0; i < h->nsamples; ++i) out[i] = tmp[i];
+  if (h->wide) {
+    if (h->nsamples) FMX_HIP(hipMemcpy(out, h->d_ssa, h->nsamples * 8, hipMemcpyDeviceToHost));
+  } else {
+    std::vector<uint32_t> tmp(h->nsamples);
+    if (h->nsamples) FMX_HIP(hipMemcpy(tmp.data(), h->d_ssa, h->nsamples * 4, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < h->nsamples; ++i) out[i] = tmp[i];
+  }
   return CS_OK;
 }
 

@@ -53,7 +53,11 @@ struct DevIndex {
   const void* lines;     // kLevels * nlines rank lines of the handle's format
   uint64_t nlines;       // per level = n / line_bits + 1
   uint64_t n;
-  const uint32_t* ssa;   // row-sampled SA (fm_index.cpp:57-66), u32 as the reference
+  // Row-sampled SA (fm_index.cpp:57-66): u32 as the reference when the index is not
+  // wide, u64 for wide indexes (n >= 2^32).  Same widths for isa and the prefix
+  // table entries (2 x u32 / 2 x u64).
+  uint32_t wide;
+  const void* ssa;
   uint64_t nsamples;
   uint32_t stride;
   uint32_t stride_shift; // log2(stride) when stride is a power of two, else 0xFFFFFFFF
@@ -62,16 +66,34 @@ struct DevIndex {
   // symbols), index = sum_j digit(P[m-1-j]) * sigma_t^j.  The generalisation of
   // C[] (the k = 1 table, fm_index.cpp:36-47): a count() whose last k characters
   // are all in the alphabet starts at step k+1.  Empty when ptab_k == 0.
-  const uint2* ptab;
+  const void* ptab;
   uint32_t ptab_k;
   uint32_t ptab_sigma;
   // Inverse-SA samples: isa[k] = row of the suffix at text position k*stride, for
   // extract by LF inversion (needs suffix order == rotation order, i.e. a unique
   // smallest last symbol: lf_exact).
-  const uint32_t* isa;
+  const void* isa;
   uint64_t nisa;
   uint32_t lf_exact;
 };
+
+__device__ __forceinline__ uint64_t ssa_at(const DevIndex& ix, uint64_t k) {
+  return ix.wide ? static_cast<const uint64_t*>(ix.ssa)[k] : static_cast<const uint32_t*>(ix.ssa)[k];
+}
+__device__ __forceinline__ uint64_t isa_at(const DevIndex& ix, uint64_t k) {
+  return ix.wide ? static_cast<const uint64_t*>(ix.isa)[k] : static_cast<const uint32_t*>(ix.isa)[k];
+}
+__device__ __forceinline__ void ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
+  if (ix.wide) {
+    const ulonglong2 r = static_cast<const ulonglong2*>(ix.ptab)[t];
+    sp = r.x;
+    ep = r.y;
+  } else {
+    const uint2 r = static_cast<const uint2*>(ix.ptab)[t];
+    sp = r.x;
+    ep = r.y;
+  }
+}
 
 __host__ __device__ inline int node_id(int level, uint32_t prefix) {
   return (1 << level) - 1 + (int)prefix;

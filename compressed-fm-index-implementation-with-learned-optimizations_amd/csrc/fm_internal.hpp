@@ -17,24 +17,35 @@ struct cs_fm_index {
   uint64_t nlines = 0;
   uint32_t line_bytes = 32;           // 32 (Line32, n < 2^32) or 64 (Line64)
   uint32_t line_bits = 224;
-  uint32_t* d_ssa = nullptr;
+  bool wide = false;                  // n >= 2^32 (or forced): u64 samples and table entries
+  void* d_ssa = nullptr;
   uint64_t nsamples = 0;
   fmx::NodeTable* d_table = nullptr;
   fmx::NodeTable h_table{};
   uint64_t* d_err = nullptr;          // locate: min failing item (UINT64_MAX = none)
-  uint2* d_ptab = nullptr;            // prefix table (DevIndex::ptab)
-  uint32_t* d_isa = nullptr;          // inverse-SA samples (extract)
+  void* d_ptab = nullptr;             // prefix table (DevIndex::ptab)
+  void* d_isa = nullptr;              // inverse-SA samples (extract)
   uint64_t nisa = 0;
   bool lf_exact = false;              // unique smallest last symbol: LF inverts SA
   uint32_t ptab_k = 0, ptab_sigma = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
 
+  uint32_t sample_bytes() const { return wide ? 8 : 4; }
+  uint32_t ptab_entry_bytes() const { return wide ? 16 : 8; }
+  uint64_t ptab_entries() const {
+    if (!ptab_k) return 0;
+    uint64_t e = 1;
+    for (uint32_t i = 0; i < ptab_k; ++i) e *= ptab_sigma;
+    return e;
+  }
+
   fmx::DevIndex dev() const {
     fmx::DevIndex d;
     d.lines = d_lines;
     d.nlines = nlines;
     d.n = n;
+    d.wide = wide ? 1u : 0u;
     d.ssa = d_ssa;
     d.nsamples = nsamples;
     d.stride = stride;
@@ -69,6 +80,8 @@ cs_status hip_fail(hipError_t e, const char* what);
 
 // Index construction on the device (fm_build.hip).
 cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st);
+cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, bool wide,
+                             uint8_t* d_bwt, void* d_ssa, void* d_isa, hipStream_t st);
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
                              hipStream_t st);
 

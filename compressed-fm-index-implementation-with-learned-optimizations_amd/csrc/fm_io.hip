@@ -101,13 +101,12 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   cs_status s;
   const uint64_t lbytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
   if ((s = dump_dev(join(d, "lines.bin"), h->d_lines, lbytes, pin.p)) != CS_OK) return s;
-  if ((s = dump_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * 4, pin.p)) != CS_OK) return s;
-  if ((s = dump_dev(join(d, "isa.bin"), h->d_isa, h->nisa * 4, pin.p)) != CS_OK) return s;
-  uint64_t pent = 0;
+  const uint64_t sb = h->sample_bytes();
+  if ((s = dump_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * sb, pin.p)) != CS_OK) return s;
+  if ((s = dump_dev(join(d, "isa.bin"), h->d_isa, h->nisa * sb, pin.p)) != CS_OK) return s;
   if (h->ptab_k) {
-    pent = 1;
-    for (uint32_t i = 0; i < h->ptab_k; ++i) pent *= h->ptab_sigma;
-    if ((s = dump_dev(join(d, "ptab.bin"), h->d_ptab, pent * sizeof(uint2), pin.p)) != CS_OK) return s;
+    const uint64_t pb = h->ptab_entries() * h->ptab_entry_bytes();
+    if ((s = dump_dev(join(d, "ptab.bin"), h->d_ptab, pb, pin.p)) != CS_OK) return s;
   }
   {
     FILE* f = std::fopen(join(d, "table.bin").c_str(), "wb");
@@ -129,11 +128,12 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   FILE* f = std::fopen(join(d, "cs_fmindex.meta").c_str(), "w");
   if (!f) return io_fail("cannot write: " + join(d, "cs_fmindex.meta"));
   std::fprintf(f, "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
-                  "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n",
+                  "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
+                  "wide %d\n",
                kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
-               has_text ? 1 : 0);
+               has_text ? 1 : 0, h->wide ? 1 : 0);
   for (int c = 0; c < 256; ++c) std::fprintf(f, "active %d %u\n", c, h->active_levels[c]);
   std::fclose(f);
   return CS_OK;
@@ -188,6 +188,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
   h->ptab_k = (uint32_t)kv["ptab_k"];
   h->ptab_sigma = (uint32_t)kv["ptab_sigma"];
   h->lf_exact = kv["lf_exact"] != 0;
+  h->wide = kv["wide"] != 0;
   auto fail = [&](cs_status s) {
     cs_fm_destroy(h);
     return s;
@@ -206,22 +207,21 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     return fail(hip_fail(hipGetLastError(), "hipHostMalloc"));
   const uint64_t lbytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
   if (hipMalloc(&h->d_lines, lbytes ? lbytes : 16) != hipSuccess ||
-      hipMalloc(&h->d_ssa, h->nsamples ? h->nsamples * 4 : 16) != hipSuccess ||
-      hipMalloc(&h->d_isa, h->nisa ? h->nisa * 4 : 16) != hipSuccess ||
+      hipMalloc(&h->d_ssa, h->nsamples ? h->nsamples * h->sample_bytes() : 16) != hipSuccess ||
+      hipMalloc(&h->d_isa, h->nisa ? h->nisa * h->sample_bytes() : 16) != hipSuccess ||
       hipMalloc(&h->d_table, sizeof(NodeTable)) != hipSuccess ||
       hipMalloc(&h->d_err, 8) != hipSuccess)
     return fail(hip_fail(hipGetLastError(), "hipMalloc (open)"));
   cs_status s;
   if ((s = load_dev(join(d, "lines.bin"), h->d_lines, lbytes, pin.p)) != CS_OK) return fail(s);
-  if ((s = load_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * 4, pin.p)) != CS_OK) return fail(s);
-  if ((s = load_dev(join(d, "isa.bin"), h->d_isa, h->nisa * 4, pin.p)) != CS_OK) return fail(s);
+  const uint64_t sb = h->sample_bytes();
+  if ((s = load_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * sb, pin.p)) != CS_OK) return fail(s);
+  if ((s = load_dev(join(d, "isa.bin"), h->d_isa, h->nisa * sb, pin.p)) != CS_OK) return fail(s);
   if (h->ptab_k) {
-    uint64_t pent = 1;
-    for (uint32_t i = 0; i < h->ptab_k; ++i) pent *= h->ptab_sigma;
-    if (hipMalloc(&h->d_ptab, pent * sizeof(uint2)) != hipSuccess)
+    const uint64_t pb = h->ptab_entries() * h->ptab_entry_bytes();
+    if (hipMalloc(&h->d_ptab, pb) != hipSuccess)
       return fail(hip_fail(hipGetLastError(), "hipMalloc (ptab)"));
-    if ((s = load_dev(join(d, "ptab.bin"), h->d_ptab, pent * sizeof(uint2), pin.p)) != CS_OK)
-      return fail(s);
+    if ((s = load_dev(join(d, "ptab.bin"), h->d_ptab, pb, pin.p)) != CS_OK) return fail(s);
   }
   if (hipMemcpy(h->d_table, &h->h_table, sizeof(NodeTable), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->d_err, 0xFF, 8) != hipSuccess)

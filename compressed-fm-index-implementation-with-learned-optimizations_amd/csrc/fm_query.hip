@@ -90,9 +90,7 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
       t = t * ix.ptab_sigma + d;
     }
     if (ok) {
-      const uint2 r = ix.ptab[t];
-      sp = r.x;
-      ep = r.y;
+      ptab_at(ix, t, sp, ep);
       k = m - ix.ptab_k;
       from_table = true;
     }
@@ -119,7 +117,7 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
 // the end is sym[digit_j(t)] (same steps as above, from C[]).
 template <class F>
 __global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entries,
-                                                     uint2* __restrict__ tab) {
+                                                     void* __restrict__ tab) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
@@ -135,7 +133,11 @@ __global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entri
       rest /= ix.ptab_sigma;
       live = search_step<F>(ix, T, c, sp, ep);
     }
-    tab[t] = live ? make_uint2((uint32_t)sp, (uint32_t)ep) : make_uint2(0u, 0u);
+    if (!live) sp = ep = 0;
+    if (ix.wide)
+      static_cast<ulonglong2*>(tab)[t] = make_ulonglong2(sp, ep);
+    else
+      static_cast<uint2*>(tab)[t] = make_uint2((uint32_t)sp, (uint32_t)ep);
   }
 }
 
@@ -187,11 +189,11 @@ __global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
 
 // rows[j] = sp[q] + (j - offs[q]) for the reported rows of pattern q (row order).
 __global__ void k_expand_rows(const uint64_t* __restrict__ sp, const uint64_t* __restrict__ offs,
-                              uint64_t npat, uint32_t* __restrict__ rows) {
+                              uint64_t npat, uint64_t* __restrict__ rows) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
     const uint64_t a = offs[q], b = offs[q + 1], s = sp[q];
-    for (uint64_t j = a; j < b; ++j) rows[j] = (uint32_t)(s + (j - a));
+    for (uint64_t j = a; j < b; ++j) rows[j] = s + (j - a);
   }
 }
 
@@ -240,7 +242,7 @@ __device__ __forceinline__ uint64_t sample_index(const DevIndex& ix, uint64_t ro
 
 // Persistent LF walk (fm_index.cpp:125-153).  Block b owns rows [b*chunk, ...).
 template <class F, bool POW2>
-__global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint32_t* __restrict__ rows,
+__global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __restrict__ rows,
                                                uint64_t total, uint64_t chunk,
                                                uint64_t* __restrict__ out,
                                                unsigned long long* __restrict__ err) {
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint32_t* __re
         if (steps >= n) {
           atomicMin(err, (unsigned long long)j);  // fm_index.cpp:136-138
         } else {
-          const uint64_t s = (uint64_t)ix.ssa[sample_index<POW2>(ix, pos)] + steps;  // :147-153
+          const uint64_t s = ssa_at(ix, sample_index<POW2>(ix, pos)) + steps;  // :147-153
           out[j] = s >= n ? s - n : s;
         }
         active = false;
@@ -364,7 +366,7 @@ __global__ __launch_bounds__(kBlk) void k_extract(DevIndex ix, const uint64_t* _
   const uint64_t s = ix.stride;
   uint64_t e = ((end + s - 1) / s) * s;
   if (e >= n) e = n;
-  uint64_t row = ix.isa[e == n ? 0 : e / s];
+  uint64_t row = isa_at(ix, e == n ? 0 : e / s);
   uint8_t* o = out + out_offs[q];
   for (uint64_t cur = e; cur > p; --cur) {
     uint32_t c;
@@ -403,8 +405,8 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
 // sigma^k <= min(2^26, max(4096, n/32)) entries (8 B each: at most n/4 bytes, the
-// order of the sampled SA); none when k < 2.  Entries are (sp, ep) as u32, so only
-// for n < 2^32.  CS_FM_PREFIX_K overrides k (0 = off).
+// order of the sampled SA); none when k < 2.  Entries are (sp, ep) as 2 x u32, or
+// 2 x u64 in wide indexes.  CS_FM_PREFIX_K overrides k (0 = off).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
   std::memset(T.code, kNoCode, sizeof T.code);
@@ -412,7 +414,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   h->ptab_k = 0;
   h->ptab_sigma = 0;
   const uint64_t n = h->n;
-  if (n == 0 || n >= (1ull << 32)) return CS_OK;
+  if (n == 0) return CS_OK;
   uint32_t sigma = 0;
   for (int c = 0; c < 256; ++c) {
     const uint64_t f = T.C[c + 1] - T.C[c];
@@ -444,7 +446,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     return CS_OK;
   }
   FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
-  FMX_HIP(hipMalloc(&h->d_ptab, entries * sizeof(uint2)));
+  FMX_HIP(hipMalloc(&h->d_ptab, entries * h->ptab_entry_bytes()));
   h->ptab_sigma = sigma;
   h->ptab_k = k;
   DevIndex ix = h->dev();
@@ -502,9 +504,9 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              uint64_t* d_out_pos, hipStream_t st) {
   if (!total) return CS_OK;
   DevBuf rows;
-  FMX_HIP(rows.alloc(total * 4));
+  FMX_HIP(rows.alloc(total * 8));
   k_expand_rows<<<grid_for(npat, kBlk, 65536), kBlk, 0, st>>>(d_sp, d_out_offs, npat,
-                                                              rows.as<uint32_t>());
+                                                              rows.as<uint64_t>());
   FMX_HIP(hipGetLastError());
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
@@ -515,7 +517,7 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   const unsigned blocks = (unsigned)((total + chunk - 1) / chunk);
   const DevIndex ix = h->dev();
   unsigned long long* err = reinterpret_cast<unsigned long long*>(h->d_err);
-  const uint32_t* r = rows.as<uint32_t>();
+  const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
   if (h->line_bytes == 32) {
     if (pow2) k_walk<Line32, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);

@@ -20,26 +20,23 @@ pytestmark = pytest.mark.gpu
 
 
 ENGINE_VARIANTS = {
-    # name: (rank-line bytes, prefix-table k override or None = automatic)
-    "line32": ("32", None),
-    "line64": ("64", None),
-    "line32_noprefix": ("32", "0"),
+    # name: environment of the builder (test hooks in csrc/fm_build.hip / fm_query.hip)
+    "line32": {},                                   # default for n < 2^32
+    "line64": {"CS_FM_LINE_BYTES": "64"},           # 64-B rank lines
+    "line32_noprefix": {"CS_FM_PREFIX_K": "0"},     # prefix table off
+    # the n >= 2^32 engine at small n: u64 samples/table, 64-B lines, bucketed sorter
+    "wide_bucketed": {"CS_FM_WIDE": "1", "CS_FM_SA_BUILDER": "bucketed"},
 }
+_HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
 def pkg(request):
-    """Every test runs on each engine variant: 32-B rank lines (default for
-    n < 2^32), 64-B lines (forced through the builder's CS_FM_LINE_BYTES test
-    hook), and with the prefix table disabled (CS_FM_PREFIX_K=0)."""
-    import os
-    lb, pk = ENGINE_VARIANTS[request.param]
-    saved = {k: os.environ.get(k) for k in ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K")}
-    os.environ["CS_FM_LINE_BYTES"] = lb
-    if pk is None:
-        os.environ.pop("CS_FM_PREFIX_K", None)
-    else:
-        os.environ["CS_FM_PREFIX_K"] = pk
+    """Every test runs on each engine variant (see ENGINE_VARIANTS)."""
+    saved = {k: os.environ.get(k) for k in _HOOKS}
+    for k in _HOOKS:
+        os.environ.pop(k, None)
+    os.environ.update(ENGINE_VARIANTS[request.param])
     yield load_pkg()
     for k, v in saved.items():
         if v is None:
@@ -288,3 +285,30 @@ def test_device_extract(pkg):
     with pytest.raises(RuntimeError):
         g.extract_batch([0], [2])
     assert g.extract(0, 2) == b"ab"  # host text copy, as the reference
+
+
+def test_bucketed_multi_pass(pkg):
+    """The bucketed sorter split into many passes (small pass budget) emits the same
+    BWT / SSA / counts / positions as the oracle."""
+    saved = {k: os.environ.get(k) for k in ("CS_FM_SA_BUILDER", "CS_FM_PASS_MAX")}
+    try:
+        os.environ["CS_FM_SA_BUILDER"] = "bucketed"
+        os.environ["CS_FM_PASS_MAX"] = "4000"
+        for t in (O.gen_dna(31, 60000).tobytes(), O.gen_bytes(31, 50000).tobytes(),
+                  (b"ACGTACGTTA" * 3000) + b"$"):
+            g = pkg.FMIndex.build_from_text(t)
+            o = O.Index(t)
+            rows = np.arange(len(t), dtype=np.uint64)
+            assert g.wt_access(rows).tobytes() == o.bwt().tobytes()
+            assert g.ssa().tolist() == o.ssa().tolist()
+            pats = [t[i:i + 12] for i in range(0, len(t) - 12, 997)]
+            assert g.count_batch(pats).tolist() == [o.count(p) for p in pats]
+            offs, pos = g.locate_batch(pats, limit=50)
+            for q, p in enumerate(pats):
+                assert pos[offs[q]:offs[q + 1]].tolist() == o.locate(p, limit=50)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
