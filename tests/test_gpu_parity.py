@@ -293,9 +293,10 @@ def test_bucketed_multi_pass(pkg):
     saved = {k: os.environ.get(k) for k in ("CS_FM_SA_BUILDER", "CS_FM_PASS_MAX")}
     try:
         os.environ["CS_FM_SA_BUILDER"] = "bucketed"
-        os.environ["CS_FM_PASS_MAX"] = "4000"
-        for t in (O.gen_dna(31, 60000).tobytes(), O.gen_bytes(31, 50000).tobytes(),
-                  (b"ACGTACGTTA" * 3000) + b"$"):
+        for t, budget in ((O.gen_dna(31, 60000).tobytes(), 4000),
+                          (O.gen_bytes(31, 50000).tobytes(), 4000),
+                          ((b"ACGTACGTTA" * 3000) + b"$", 7000)):  # 4-mer ACGT: 6000 suffixes
+            os.environ["CS_FM_PASS_MAX"] = str(budget)
             g = pkg.FMIndex.build_from_text(t)
             o = O.Index(t)
             rows = np.arange(len(t), dtype=np.uint64)
