@@ -293,9 +293,12 @@ def test_bucketed_multi_pass(pkg):
     saved = {k: os.environ.get(k) for k in ("CS_FM_SA_BUILDER", "CS_FM_PASS_MAX")}
     try:
         os.environ["CS_FM_SA_BUILDER"] = "bucketed"
+        base = O.gen_dna(32, 30000).tobytes()[:-1]
+        seg = base[1000:1500]  # 500-char repeat copied 6 times: ~24 refinement rounds
+        rep = b"".join(base[i * 5000:(i + 1) * 5000] + seg for i in range(6)) + b"$"
         for t, budget in ((O.gen_dna(31, 60000).tobytes(), 4000),
                           (O.gen_bytes(31, 50000).tobytes(), 4000),
-                          ((b"ACGTACGTTA" * 3000) + b"$", 7000)):  # 4-mer ACGT: 6000 suffixes
+                          (rep, 4000)):
             os.environ["CS_FM_PASS_MAX"] = str(budget)
             g = pkg.FMIndex.build_from_text(t)
             o = O.Index(t)
