@@ -120,7 +120,7 @@ def main():
     # per backward-search step the kernel performs; one line = 32 B (Line32, n < 2^32)
     # or 64 B.  Steps covered by the prefix table cost one 8-B table read instead
     # (and the first step without it comes from C[]).
-    line_bytes = 32 if info.line_bits == 224 else 64
+    line_bytes = 64 if info.line_bits == 448 else 32  # Line32 (224 bits) and Line32W (192) are 32 B
     act = torch.tensor([bin(info.active_levels[c]).count("1") for c in range(256)],
                        dtype=torch.int64, device=dev)
     P2 = pats.view(B, m).long()

@@ -123,10 +123,10 @@ __global__ void k_bwt_ssa(const uint8_t* __restrict__ t, const uint32_t* __restr
 template <class F>
 __device__ __forceinline__ void store_word(void* L, uint64_t w, uint64_t v) {
   const uint64_t line = w / F::kWords, slot = w % F::kWords;
-  if (F::kWordBits == 32)
-    reinterpret_cast<uint32_t*>(L)[line * 8 + 1 + slot] = (uint32_t)v;
+  if (F::kWordBits == 32)  // 32-B lines: 8 dwords
+    reinterpret_cast<uint32_t*>(L)[line * 8 + F::kBaseWords + slot] = (uint32_t)v;
   else
-    reinterpret_cast<uint64_t*>(L)[line * 8 + 1 + slot] = v;
+    reinterpret_cast<uint64_t*>(L)[line * 8 + F::kBaseWords + slot] = v;
 }
 
 // One wave per 64 positions: ballot of the level bit (= 1 or 2 payload words).
@@ -165,10 +165,10 @@ __global__ void k_set_base(void* __restrict__ L, const uint64_t* __restrict__ ba
                            uint64_t nlines) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; l < nlines; l += stride) {
-    if (F::kWordBits == 32)
+    if (F::kBaseWords == 1 && F::kWordBits == 32)  // Line32: u32 base
       reinterpret_cast<uint32_t*>(L)[l * 8] = (uint32_t)base[l];
-    else
-      reinterpret_cast<uint64_t*>(L)[l * 8] = base[l];
+    else  // u64 base at the line start (Line32W: 4 qwords per line, Line64: 8)
+      reinterpret_cast<uint64_t*>(L)[l * (F::kBytes / 8)] = base[l];
   }
 }
 
@@ -430,13 +430,16 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   plog.mark("suffix array + bwt + ssa");
 
   // --- wavelet matrix levels as rank lines ---
-  h->line_bytes = h->wide ? 64 : 32;  // Line32 bases are u32
-  if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force a format
-    if (std::atoi(e) == 64) h->line_bytes = 64;
-  h->line_bits = h->line_bytes == 32 ? Line32::kBits : Line64::kBits;
+  h->line_fmt = h->wide ? kFmtLine32W : kFmtLine32;  // Line32 bases are u32
+  if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force 64-B lines
+    if (std::atoi(e) == 64) h->line_fmt = kFmtLine64;
+  h->line_bytes = h->line_fmt == kFmtLine64 ? 64 : 32;
+  h->line_bits = h->line_fmt == kFmtLine32 ? Line32::kBits
+                 : h->line_fmt == kFmtLine32W ? Line32W::kBits : Line64::kBits;
   h->nlines = n / h->line_bits + 1;  // + sentinel so rank1(n) is a line read
-  cs_status ws = h->line_bytes == 32 ? build_levels<Line32>(bwt.as<uint8_t>(), n, h, st)
-                                     : build_levels<Line64>(bwt.as<uint8_t>(), n, h, st);
+  cs_status ws = h->line_fmt == kFmtLine32    ? build_levels<Line32>(bwt.as<uint8_t>(), n, h, st)
+                 : h->line_fmt == kFmtLine32W ? build_levels<Line32W>(bwt.as<uint8_t>(), n, h, st)
+                                              : build_levels<Line64>(bwt.as<uint8_t>(), n, h, st);
   if (ws != CS_OK) return ws;
   bwt.release();
   plog.mark("wavelet levels");
@@ -496,8 +499,10 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   {
     DevBuf dR;
     FMX_HIP(dR.alloc(kNodes * 8));
-    if (h->line_bytes == 32)
+    if (h->line_fmt == kFmtLine32)
       k_node_rank<Line32><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
+    else if (h->line_fmt == kFmtLine32W)
+      k_node_rank<Line32W><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
     else
       k_node_rank<Line64><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
     FMX_HIP(hipGetLastError());

@@ -6,7 +6,8 @@
 // 95-98: bits_ + super_ u32 every 2048 bits + blocks_ u16 every 256 bits) is stored
 // re-laid-out as RANK LINES, one HBM access per rank1:
 //
-//   Line32  { u32 base; u32 w[7]; }   32 B, 224 payload bits   (n < 2^32)
+//   Line32  { u32 base; u32 w[7]; }   32 B, 224 payload bits   (n < 2^32, default)
+//   Line32W { u64 base; u32 w[6]; }   32 B, 192 payload bits   (wide: n >= 2^32)
 //   Line64  { u64 base; u64 w[7]; }   64 B, 448 payload bits   (any n < 2^38)
 //
 // base = rank1 at the line's first bit (absolute), w[] = the bits LSB-first.
@@ -48,6 +49,9 @@ struct NodeTable {
   uint8_t sym[256];     // digit -> symbol
 };
 constexpr uint8_t kNoCode = 0xFF;
+
+// rank-line formats (cs_fm_index::line_fmt)
+enum LineFmt : uint32_t { kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2 };
 
 struct DevIndex {
   const void* lines;     // kLevels * nlines rank lines of the handle's format
@@ -109,6 +113,7 @@ struct Line32 {
   static constexpr uint32_t kBytes = 32;
   static constexpr uint32_t kWordBits = 32;
   static constexpr int kWords = 7;
+  static constexpr int kBaseWords = 1;  // payload starts at dword 1
   static constexpr uint32_t kBits = kWords * kWordBits;  // 224
   using Raw = uint4[2];
 
@@ -146,11 +151,54 @@ struct Line32 {
   }
 };
 
+// 32-byte wide line: dwords 0-1 = u64 base, dwords 2..7 = payload (192 bits);
+// the 32-B DRAM granule for indexes whose ranks exceed u32 (n >= 2^32).
+struct Line32W {
+  static constexpr uint32_t kBytes = 32;
+  static constexpr uint32_t kWordBits = 32;
+  static constexpr int kWords = 6;
+  static constexpr int kBaseWords = 2;  // payload starts at dword 2
+  static constexpr uint32_t kBits = kWords * kWordBits;  // 192 = 3 x 64
+  using Raw = uint4[2];
+
+  __device__ static __forceinline__ void locate(uint64_t p, uint32_t& q, uint32_t& o) {
+    const uint32_t g = (uint32_t)(p >> 6);  // p < 2^38
+    q = g / 3u;
+    o = (uint32_t)(p - (uint64_t)q * kBits);
+  }
+  __device__ static __forceinline__ void load(const void* lines, uint64_t idx, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + idx * 2;
+    v[0] = p[0];
+    v[1] = p[1];
+  }
+  __device__ static __forceinline__ uint64_t base(const Raw& v) { return u64_of(v[0].x, v[0].y); }
+  __device__ static __forceinline__ uint32_t prefix(const Raw& v, uint32_t o) {
+    const uint32_t w[6] = {v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int sh = (int)o - 32 * k;
+      const uint32_t m = sh >= 32 ? ~0u : (sh <= 0 ? 0u : ((1u << sh) - 1u));
+      r += (uint32_t)__popc(w[k] & m);
+    }
+    return r;
+  }
+  __device__ static __forceinline__ uint32_t bit(const Raw& v, uint32_t o) {
+    const uint32_t w[6] = {v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w};
+    const uint32_t k = o >> 5;
+    uint32_t d = w[0];
+#pragma unroll
+    for (int j = 1; j < 6; ++j) d = (k == (uint32_t)j) ? w[j] : d;
+    return (d >> (o & 31)) & 1u;
+  }
+};
+
 // 64-byte line: qword 0 = base, qwords 1..7 = payload (448 bits)
 struct Line64 {
   static constexpr uint32_t kBytes = 64;
   static constexpr uint32_t kWordBits = 64;
   static constexpr int kWords = 7;
+  static constexpr int kBaseWords = 1;  // payload starts at qword 1
   static constexpr uint32_t kBits = kWords * kWordBits;  // 448
   using Raw = uint4[4];
 

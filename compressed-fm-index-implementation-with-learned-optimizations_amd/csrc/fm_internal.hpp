@@ -15,7 +15,8 @@ struct cs_fm_index {
   uint32_t stride = 32;
   void* d_lines = nullptr;            // 8 levels x nlines rank lines
   uint64_t nlines = 0;
-  uint32_t line_bytes = 32;           // 32 (Line32, n < 2^32) or 64 (Line64)
+  uint32_t line_fmt = fmx::kFmtLine32; // Line32 (n < 2^32), Line32W (wide) or Line64
+  uint32_t line_bytes = 32;
   uint32_t line_bits = 224;
   bool wide = false;                  // n >= 2^32 (or forced): u64 samples and table entries
   void* d_ssa = nullptr;

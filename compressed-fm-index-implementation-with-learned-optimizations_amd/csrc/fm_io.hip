@@ -129,11 +129,11 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   if (!f) return io_fail("cannot write: " + join(d, "cs_fmindex.meta"));
   std::fprintf(f, "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
                   "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
-                  "wide %d\n",
+                  "wide %d\nline_fmt %u\n",
                kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
-               has_text ? 1 : 0, h->wide ? 1 : 0);
+               has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt);
   for (int c = 0; c < 256; ++c) std::fprintf(f, "active %d %u\n", c, h->active_levels[c]);
   std::fclose(f);
   return CS_OK;
@@ -189,6 +189,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
   h->ptab_sigma = (uint32_t)kv["ptab_sigma"];
   h->lf_exact = kv["lf_exact"] != 0;
   h->wide = kv["wide"] != 0;
+  h->line_fmt = (uint32_t)kv["line_fmt"];
   auto fail = [&](cs_status s) {
     cs_fm_destroy(h);
     return s;

@@ -395,8 +395,10 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 // Dispatch on the handle's rank-line format.
 #define FMX_DISPATCH(h, KERNEL, GRID, ...)                                      \
   do {                                                                          \
-    if ((h)->line_bytes == 32)                                                  \
+    if ((h)->line_fmt == kFmtLine32)                                            \
       KERNEL<Line32><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
+    else if ((h)->line_fmt == kFmtLine32W)                                      \
+      KERNEL<Line32W><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                    \
     else                                                                        \
       KERNEL<Line64><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
     FMX_HIP(hipGetLastError());                                                 \
@@ -451,11 +453,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   h->ptab_k = k;
   DevIndex ix = h->dev();
   ix.ptab = nullptr;  // the builder itself searches from C[]
-  if (h->line_bytes == 32)
-    k_build_ptab<Line32><<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(ix, entries, h->d_ptab);
-  else
-    k_build_ptab<Line64><<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(ix, entries, h->d_ptab);
-  FMX_HIP(hipGetLastError());
+  FMX_DISPATCH(h, k_build_ptab, grid_for(entries, kBlk, 65536), ix, entries, h->d_ptab);
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
 }
@@ -519,9 +517,12 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   unsigned long long* err = reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
-  if (h->line_bytes == 32) {
+  if (h->line_fmt == kFmtLine32) {
     if (pow2) k_walk<Line32, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<Line32, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  } else if (h->line_fmt == kFmtLine32W) {
+    if (pow2) k_walk<Line32W, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<Line32W, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else {
     if (pow2) k_walk<Line64, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<Line64, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
