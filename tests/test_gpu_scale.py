@@ -94,6 +94,23 @@ def test_c4_dna_4gb():
     _kmer_checksum(idx, b"ACGT", 9, N)
 
 
+@pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C5") == "1", reason="C5 disabled")
+def test_c5_dna_32gb_wide():
+    """BASELINE configs[4]: 32 GB text (n >= 2^32) — wide index (u64 samples, Line32W
+    rank lines) built by the pass-by-pass bucketed suffix sorter."""
+    pkg = load_pkg()
+    idx, text, host, N = _build(pkg, "dna", 31_999_999_999)
+    info = idx.info()
+    assert N == 32_000_000_000 and info.line_bits == 192
+    P = _qtext(pkg, text, N, 20, 200_000)
+    _check_qtext(idx, host, N, P, nloc=20_000)
+    ones = idx.count_batch([bytes([c]) for c in range(256)])
+    assert int(ones.sum()) == N and ones[ord("$")] == 1
+    _kmer_checksum(idx, b"ACGT", 9, N)
+    assert idx.extract_batch([0, N - 30, 12_345_678_901], [25, 40, 20]) == [
+        host[:25].tobytes(), host[N - 30:].tobytes(), host[12_345_678_901:12_345_678_921].tobytes()]
+
+
 def test_c3_bytes_1gb():
     pkg = load_pkg()
     idx, text, host, N = _build(pkg, "bytes", 999_999_999)
