@@ -116,26 +116,23 @@ def main():
     # the count of step k+1 (shard.PipelinedGather)
     pg = shard.PipelinedGather(B, world, rank, torch.int64, dev)
 
-    # algorithmic bytes per launch: 2 rank-line reads (sp, ep) per non-pure wavelet level
-    # per backward-search step the kernel performs; one line = 32 B (Line32, n < 2^32)
-    # or 64 B.  Steps covered by the prefix table cost one 8-B table read instead
-    # (and the first step without it comes from C[]).
-    line_bytes = 64 if info.line_bits == 448 else 32  # Line32 (224 bits) and Line32W (192) are 32 B
-    act = torch.tensor([bin(info.active_levels[c]).count("1") for c in range(256)],
-                       dtype=torch.int64, device=dev)
+    # algorithmic bytes per launch, counted by the engine's measurement twin of the
+    # count kernel (cs_fm_count_bytes_device): per backward-search step, the distinct
+    # lines its rank pair (sp, ep) needs (one 32-B occurrence line, or one rank line
+    # per non-pure wavelet level; sp and ep in the same line count once) times the
+    # line size, plus the 8-B (16-B wide) prefix-table entry that replaces the first
+    # k steps.
+    line_bytes = info.line_bytes
+    qbytes = torch.empty(B, dtype=torch.int64, device=dev)
+    idx.count_bytes_device(pats.data_ptr(), offs.data_ptr(), B, qbytes.data_ptr(), sh)
+    alg_bytes = int(qbytes.sum().item())
+    del qbytes
     P2 = pats.view(B, m).long()
     K = info.prefix_k
+    table_frac = 0.0
     if K and m >= K:
         code = torch.tensor(list(info.prefix_code), dtype=torch.int64, device=dev)
-        use = (code[P2[:, m - K:]] != 255).all(dim=1)
-        lines_tab = act[P2[:, : m - K]].sum(dim=1)
-        lines_c = act[P2[:, :-1]].sum(dim=1)
-        per_q = torch.where(use, lines_tab * 2 * line_bytes + 8, lines_c * 2 * line_bytes)
-        alg_bytes = int(per_q.sum().item())
-        table_frac = float(use.float().mean().item())
-    else:
-        alg_bytes = int(act[P2[:, :-1]].sum().item()) * 2 * line_bytes
-        table_frac = 0.0
+        table_frac = float((code[P2[:, m - K:]] != 255).all(dim=1).float().mean().item())
     del P2
     torch.cuda.synchronize()
 
@@ -180,7 +177,8 @@ def main():
     if rank == 0:
         traffic = None
         prof = os.path.join(ROOT, "profiles", "pmc_count.json")
-        wl = "%s:%d:m%d:b%d" % (args.kind, N, m, B)
+        engine = "occ" if info.engine == 1 else "wm%d" % info.line_bytes
+        wl = "%s:%d:m%d:b%d:%s" % (args.kind, N, m, B, engine)
         if os.path.exists(prof):
             pj = json.load(open(prof))
             if pj.get("workload") == wl:
@@ -203,7 +201,9 @@ def main():
                        "%s text n=%d, Q_text %d-mers, count()" % (args.kind, N, m),
                        "batch_per_gpu": B, "global_batch": B * world, "m": m,
                        "ssa_stride": args.ssa_stride, "parallelism": "dp%d" % world,
-                       "index": "replicated per GPU", "workload_key": wl},
+                       "index": "replicated per GPU", "workload_key": wl,
+                       "engine": "occurrence lines" if info.engine == 1 else
+                       "wavelet matrix (%d-B rank lines)" % info.line_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,

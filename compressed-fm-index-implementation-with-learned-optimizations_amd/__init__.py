@@ -41,7 +41,8 @@ class cs_fm_info(C.Structure):
                 ("lines_per_level", C.c_uint64), ("rank_bytes", C.c_uint64),
                 ("ssa_bytes", C.c_uint64), ("active_levels", C.c_uint32 * 256), ("device", C.c_int),
                 ("prefix_k", C.c_uint32), ("prefix_sigma", C.c_uint32), ("prefix_bytes", C.c_uint64),
-                ("prefix_code", C.c_uint8 * 256)]
+                ("prefix_code", C.c_uint8 * 256), ("engine", C.c_uint32), ("line_bytes", C.c_uint32),
+                ("levels", C.c_uint32), ("rare_rows", C.c_uint32)]
 
 
 # Every entry point of include/cs_fmindex.h with its ctypes signature.
@@ -66,6 +67,7 @@ SIGNATURES = {
     "cs_fm_locate_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, C.c_uint64, _u64p, _u64p,
                                      C.c_uint64, _u64p, _vp]),
     "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                              _u64p, _vp]),
     "cs_fm_locate_walk_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
@@ -284,6 +286,10 @@ class FMIndex:
     # -- device-resident batches (raw device pointers, e.g. torch data_ptr()) --
     def count_batch_device(self, d_pats: int, d_offs: int, npat: int, d_out: int, stream: int = 0):
         _check(lib().cs_fm_count_batch_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
+
+    def count_bytes_device(self, d_pats, d_offs, npat, d_out, stream=0):
+        """Per-query algorithmic HBM bytes of the search (roofline accounting)."""
+        _check(lib().cs_fm_count_bytes_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
 
     def locate_ranges_device(self, d_pats, d_offs, npat, limit, d_sp, d_out_offs, stream=0) -> int:
         total = C.c_uint64()

@@ -7,8 +7,9 @@
 //   2. cyclic BWT (src/core/bwt.hpp:7-15) and row-sampled SSA (fm_index.cpp:57-66);
 //   3. C[] (fm_index.cpp:36-47) from the symbol histogram (the BWT is a permutation
 //      of the text);
-//   4. the 8-level wavelet matrix (src/core/wavelet.cpp:14-53) as 64-B rank lines
-//      (fm_device.hpp), one stable partition per level;
+//   4. the rank structure: occurrence lines when at most four symbols carry all
+//      but a few rows (DNA), else the 8-level wavelet matrix (src/core/wavelet.cpp:
+//      14-53) as rank lines (fm_device.hpp), one stable partition per level;
 //   5. the node table (starts, ranks, purity) for the query kernels.
 // Index construction is not the timed hot path; it is HBM-streaming work.
 #include <rocprim/device/device_radix_sort.hpp>
@@ -20,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "fm_internal.hpp"
 
@@ -270,6 +272,131 @@ static cs_status build_levels(uint8_t* cur, uint64_t n, cs_fm_index* h, hipStrea
   return CS_OK;
 }
 
+// ---- occurrence lines (fm_device.hpp OccLine) ----
+struct CodeMap {
+  uint8_t c[256];  // 2-bit code per symbol, kNoCode for the rare ones
+};
+
+// One thread per line q: pack the 64 rows' codes (rare symbols as code 0, rows past
+// n as code 0), count codes 0..2 among the rows < n, and list the rare rows.
+__global__ void k_occ_pack(const uint8_t* __restrict__ bwt, uint64_t n, CodeMap map, uint64_t nl,
+                           uint32_t* __restrict__ lines, uint32_t* __restrict__ cnt,
+                           unsigned long long* __restrict__ exc_rows, uint8_t* __restrict__ exc_sym,
+                           unsigned int* __restrict__ exc_n) {
+  __shared__ uint8_t code[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) code[i] = map.c[i];
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nl; q += stride) {
+    const uint64_t a = q << 6;
+    uint32_t w[4] = {0, 0, 0, 0};
+    uint32_t c0 = 0, c1 = 0, c2 = 0;
+    for (int r = 0; r < 64; ++r) {
+      if (a + r >= n) break;
+      const uint32_t sym = bwt[a + r];
+      uint32_t k = code[sym];
+      if (k == kNoCode) {
+        const unsigned int e = atomicAdd(exc_n, 1u);
+        if (e < (unsigned)kMaxExc) {
+          exc_rows[e] = a + r;
+          exc_sym[e] = (uint8_t)sym;
+        }
+        k = 0;
+      }
+      w[r >> 4] |= k << (2 * (r & 15));
+      c0 += k == 0;
+      c1 += k == 1;
+      c2 += k == 2;
+    }
+    uint4* L = reinterpret_cast<uint4*>(lines) + q * 2;
+    L[1] = make_uint4(w[0], w[1], w[2], w[3]);
+    cnt[q] = c0;
+    cnt[nl + q] = c1;
+    cnt[2 * nl + q] = c2;
+  }
+}
+
+// dword j and byte 12+j of each line = scanned occ(code j) (n < 2^40)
+__global__ void k_occ_base(uint32_t* __restrict__ lines, const uint64_t* __restrict__ base,
+                           uint64_t nl, int j) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nl; q += stride) {
+    const uint64_t b = base[q];
+    lines[q * 8 + j] = (uint32_t)b;
+    reinterpret_cast<uint8_t*>(lines)[q * 32 + 12 + j] = (uint8_t)(b >> 32);
+  }
+}
+
+// Occurrence-line engine choice: the (at most) four most frequent symbols get
+// 2-bit codes in symbol order; the rest must hold at most kMaxExc rows.
+bool occ_feasible(const unsigned long long* hist, uint64_t n, CodeMap& map, uint8_t occ_sym[4]) {
+  if (n == 0 || n >= (1ull << 40)) return false;
+  int order[256], np = 0;
+  for (int c = 0; c < 256; ++c)
+    if (hist[c]) order[np++] = c;
+  std::stable_sort(order, order + np, [&](int x, int y) { return hist[x] > hist[y]; });
+  const int nc = np < 4 ? np : 4;
+  uint64_t rare = 0;
+  for (int i = nc; i < np; ++i) rare += hist[order[i]];
+  if (rare > (uint64_t)kMaxExc) return false;
+  std::sort(order, order + nc);
+  std::memset(map.c, kNoCode, sizeof map.c);
+  for (int k = 0; k < 4; ++k) occ_sym[k] = k < nc ? (uint8_t)order[k] : 0;
+  for (int k = 0; k < nc; ++k) map.c[order[k]] = (uint8_t)k;
+  return true;
+}
+
+cs_status build_occ(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
+                    hipStream_t st) {
+  const uint64_t nl = h->nlines;
+  FMX_HIP(hipMalloc(&h->d_lines, nl * OccLine::kBytes));
+  DevBuf cnt, base, tmp, erow, esym, en;
+  FMX_HIP(cnt.alloc(3 * nl * 4));
+  FMX_HIP(base.alloc(nl * 8));
+  FMX_HIP(erow.alloc(kMaxExc * 8));
+  FMX_HIP(esym.alloc(kMaxExc));
+  FMX_HIP(en.alloc(4));
+  FMX_HIP(hipMemsetAsync(en.p, 0, 4, st));
+  k_occ_pack<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(
+      bwt, n, map, nl, static_cast<uint32_t*>(h->d_lines), cnt.as<uint32_t>(),
+      erow.as<unsigned long long>(), esym.as<uint8_t>(), en.as<unsigned int>());
+  FMX_HIP(hipGetLastError());
+  size_t tb = 0;
+  FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint32_t>(), base.as<uint64_t>(), (uint64_t)0,
+                                  nl, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(tmp.alloc(tb));
+  for (int j = 0; j < 3; ++j) {
+    size_t t2 = tb;
+    FMX_HIP(rocprim::exclusive_scan(tmp.p, t2, cnt.as<uint32_t>() + (uint64_t)j * nl,
+                                    base.as<uint64_t>(), (uint64_t)0, nl,
+                                    rocprim::plus<uint64_t>(), st));
+    k_occ_base<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(static_cast<uint32_t*>(h->d_lines),
+                                                          base.as<uint64_t>(), nl, j);
+    FMX_HIP(hipGetLastError());
+  }
+  unsigned int ne = 0;
+  uint64_t rows[kMaxExc];
+  uint8_t syms[kMaxExc];
+  FMX_HIP(hipMemcpyAsync(&ne, en.p, 4, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(rows, erow.p, sizeof rows, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(syms, esym.p, sizeof syms, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  if (ne > (unsigned)kMaxExc) {
+    set_error("occurrence lines: rare-symbol rows exceed the table");
+    return CS_ERR_INVALID;
+  }
+  std::vector<int> idx(ne);
+  for (unsigned i = 0; i < ne; ++i) idx[i] = (int)i;
+  std::sort(idx.begin(), idx.end(), [&](int x, int y) { return rows[x] < rows[y]; });
+  NodeTable& T = h->h_table;
+  T.exc_n = ne;
+  for (unsigned i = 0; i < ne; ++i) {
+    T.exc_row[i] = rows[idx[i]];
+    T.exc_sym[i] = syms[idx[i]];
+  }
+  return CS_OK;
+}
+
 cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st) {
   if (n == 0) return CS_OK;
   if (n >= (1ull << 32)) {
@@ -429,18 +556,39 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   }
   plog.mark("suffix array + bwt + ssa");
 
-  // --- wavelet matrix levels as rank lines ---
-  h->line_fmt = h->wide ? kFmtLine32W : kFmtLine32;  // Line32 bases are u32
-  if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force 64-B lines
-    if (std::atoi(e) == 64) h->line_fmt = kFmtLine64;
-  h->line_bytes = h->line_fmt == kFmtLine64 ? 64 : 32;
-  h->line_bits = h->line_fmt == kFmtLine32 ? Line32::kBits
-                 : h->line_fmt == kFmtLine32W ? Line32W::kBits : Line64::kBits;
-  h->nlines = n / h->line_bits + 1;  // + sentinel so rank1(n) is a line read
-  cs_status ws = h->line_fmt == kFmtLine32    ? build_levels<Line32>(bwt.as<uint8_t>(), n, h, st)
-                 : h->line_fmt == kFmtLine32W ? build_levels<Line32W>(bwt.as<uint8_t>(), n, h, st)
-                                              : build_levels<Line64>(bwt.as<uint8_t>(), n, h, st);
-  if (ws != CS_OK) return ws;
+  // --- rank structure: occurrence lines (<= 4 frequent symbols) or the wavelet
+  //     matrix levels as rank lines ---
+  CodeMap occ_map;
+  uint8_t occ_sym[4] = {0, 0, 0, 0};
+  bool occ = occ_feasible(hist, n, occ_map, occ_sym);
+  if (const char* e = std::getenv("CS_FM_ENGINE"))  // "wavelet" forces the wavelet matrix
+    if (std::string(e) == "wavelet") occ = false;
+  if (occ) {
+    h->line_fmt = kFmtOcc;
+    h->line_bytes = OccLine::kBytes;
+    h->line_bits = OccLine::kRows;
+    h->nlevels = 1;
+    h->nlines = (n >> 6) + 1;  // + the line holding row n, so occ(c, n) is a line read
+    std::memcpy(T.occ_code, occ_map.c, sizeof T.occ_code);
+    std::memcpy(T.occ_sym, occ_sym, sizeof T.occ_sym);
+    cs_status os = build_occ(bwt.as<uint8_t>(), n, occ_map, h, st);
+    if (os != CS_OK) return os;
+  } else {
+    std::memset(T.occ_code, kNoCode, sizeof T.occ_code);
+    h->line_fmt = h->wide ? kFmtLine32W : kFmtLine32;  // Line32 bases are u32
+    if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force 64-B lines
+      if (std::atoi(e) == 64) h->line_fmt = kFmtLine64;
+    h->line_bytes = h->line_fmt == kFmtLine64 ? 64 : 32;
+    h->line_bits = h->line_fmt == kFmtLine32 ? Line32::kBits
+                   : h->line_fmt == kFmtLine32W ? Line32W::kBits : Line64::kBits;
+    h->nlevels = kLevels;
+    h->nlines = n / h->line_bits + 1;  // + sentinel so rank1(n) is a line read
+    cs_status ws = h->line_fmt == kFmtLine32    ? build_levels<Line32>(bwt.as<uint8_t>(), n, h, st)
+                   : h->line_fmt == kFmtLine32W ? build_levels<Line32W>(bwt.as<uint8_t>(), n, h, st)
+                                                : build_levels<Line64>(bwt.as<uint8_t>(), n, h, st);
+    if (ws != CS_OK) return ws;
+  }
+  FMX_HIP(hipStreamSynchronize(st));
   bwt.release();
   plog.mark("wavelet levels");
 
@@ -492,6 +640,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     uint32_t m = 0;
     for (int l = 0; l < kLevels; ++l)
       if (!(T.flags[node_id(l, l ? (c >> (8 - l)) : 0)] & kPure)) m |= 1u << l;
+    if (occ) m = T.occ_code[c] != kNoCode ? 1u : 0u;  // one line per occ, none for rare symbols
     h->active_levels[c] = hist[c] ? m : 0;
   }
   FMX_HIP(hipMalloc(&h->d_table, sizeof(NodeTable)));
@@ -499,7 +648,9 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   {
     DevBuf dR;
     FMX_HIP(dR.alloc(kNodes * 8));
-    if (h->line_fmt == kFmtLine32)
+    if (h->line_fmt == kFmtOcc)
+      FMX_HIP(hipMemsetAsync(dR.p, 0, kNodes * 8, st));  // wavelet node ranks unused
+    else if (h->line_fmt == kFmtLine32)
       k_node_rank<Line32><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
     else if (h->line_fmt == kFmtLine32W)
       k_node_rank<Line32W><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());

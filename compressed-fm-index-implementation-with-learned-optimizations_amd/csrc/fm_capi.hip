@@ -3,6 +3,7 @@
 // without a HIP device every call fails with CS_ERR_NO_DEVICE.
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 
@@ -46,6 +47,21 @@ cs_status check_handle(const cs_fm_index* h) {
   return use_device(h->device);
 }
 
+// Lazily allocate the handle's small-batch arena (caller holds scratch.mu).
+cs_status scratch_ready(const cs_fm_index* h) {
+  if (h->scratch.h) return CS_OK;
+  void *hp = nullptr, *dp = nullptr;
+  FMX_HIP(hipHostMalloc(&hp, cs_fm_index::kScratchBytes, hipHostMallocDefault));
+  hipError_t e = hipMalloc(&dp, cs_fm_index::kScratchBytes);
+  if (e != hipSuccess) {
+    (void)hipHostFree(hp);
+    return hip_fail(e, "hipMalloc (scratch)");
+  }
+  h->scratch.h = static_cast<uint8_t*>(hp);
+  h->scratch.d = static_cast<uint8_t*>(dp);
+  return CS_OK;
+}
+
 // Stage a host pattern batch into HBM.
 struct StagedBatch {
   DevBuf pats, offs;
@@ -74,6 +90,8 @@ void free_index(cs_fm_index* h) {
   if (h->d_err) (void)hipFree(h->d_err);
   if (h->d_ptab) (void)hipFree(h->d_ptab);
   if (h->d_isa) (void)hipFree(h->d_isa);
+  if (h->scratch.h) (void)hipHostFree(h->scratch.h);
+  if (h->scratch.d) (void)hipFree(h->scratch.d);
   delete h;
 }
 
@@ -172,7 +190,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->ssa_stride = h->stride;
   out->line_bits = h->line_bits;
   out->lines_per_level = h->nlines;
-  out->rank_bytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
+  out->rank_bytes = (uint64_t)h->nlevels * h->nlines * h->line_bytes;
   out->ssa_bytes = h->nsamples * h->sample_bytes();
   std::memcpy(out->active_levels, h->active_levels, sizeof out->active_levels);
   out->device = h->device;
@@ -180,6 +198,10 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->prefix_sigma = h->ptab_sigma;
   out->prefix_bytes = h->ptab_entries() * h->ptab_entry_bytes();
   for (int c = 0; c < 256; ++c) out->prefix_code[c] = h->h_table.code[c];
+  out->engine = h->line_fmt == kFmtOcc ? 1u : 0u;
+  out->line_bytes = h->line_bytes;
+  out->levels = h->nlevels;
+  out->rare_rows = h->line_fmt == kFmtOcc ? h->h_table.exc_n : 0u;
   return CS_OK;
 }
 
@@ -195,6 +217,18 @@ cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
   return launch_count(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
 }
 
+cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
+                                   void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (npat && (!d_offs || !d_out)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_count_bytes(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
+}
+
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
                             uint64_t npat, uint64_t* out_counts, void* stream) {
   cs_status s = check_handle(h);
@@ -205,6 +239,27 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     return CS_ERR_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;
+  const uint64_t bytes = offs[npat] - offs[0];
+  const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
+  if (o_pats + bytes + 16 <= cs_fm_index::kScratchBytes) {
+    // small batch: one pinned H2D copy, the search, one D2H copy
+    std::unique_lock<std::mutex> lk(h->scratch.mu);
+    if ((s = scratch_ready(h)) != CS_OK) return s;
+    uint8_t* hp = h->scratch.h;
+    uint8_t* dp = h->scratch.d;
+    uint64_t* ho = reinterpret_cast<uint64_t*>(hp);
+    for (uint64_t q = 0; q <= npat; ++q) ho[q] = offs[q] - offs[0];
+    if (bytes) std::memcpy(hp + o_pats, pats + offs[0], bytes);
+    FMX_HIP(hipMemcpyAsync(dp, hp, o_out, hipMemcpyHostToDevice, st));
+    if (bytes) FMX_HIP(hipMemcpyAsync(dp + o_pats, hp + o_pats, bytes, hipMemcpyHostToDevice, st));
+    s = launch_count(h, dp + o_pats, reinterpret_cast<const uint64_t*>(dp), npat,
+                     reinterpret_cast<uint64_t*>(dp + o_out), st);
+    if (s != CS_OK) return s;
+    FMX_HIP(hipMemcpyAsync(hp + o_out, dp + o_out, npat * 8, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    std::memcpy(out_counts, hp + o_out, npat * 8);
+    return CS_OK;
+  }
   StagedBatch b;
   s = b.load(pats, offs, npat, st);
   if (s != CS_OK) return s;

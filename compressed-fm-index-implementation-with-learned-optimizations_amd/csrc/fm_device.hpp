@@ -35,6 +35,7 @@ namespace fmx {
 constexpr int kLevels = 8;
 constexpr int kNodes = 255;  // internal nodes, levels 0..7
 constexpr uint8_t kPure = 1, kPureBit = 2;
+constexpr int kMaxExc = 128;  // occurrence-line engine: rare-symbol rows kept in LDS
 
 // Everything the query kernels read besides the rank lines; copied into LDS by
 // every block (8.5 KB).
@@ -47,11 +48,19 @@ struct NodeTable {
   uint8_t flags[256];   // kPure | kPureBit per node
   uint8_t code[256];    // prefix-table digit of each symbol, kNoCode if not in its alphabet
   uint8_t sym[256];     // digit -> symbol
+  // occurrence-line engine (OccLine below): 2-bit code of each coded symbol
+  // (kNoCode: rare or absent), code -> symbol, and the BWT rows holding a rare
+  // symbol (ascending; stored as code 0 in the lines and corrected here)
+  uint8_t occ_code[256];
+  uint8_t occ_sym[4];
+  uint32_t exc_n;
+  uint64_t exc_row[kMaxExc];
+  uint8_t exc_sym[kMaxExc];
 };
 constexpr uint8_t kNoCode = 0xFF;
 
 // rank-line formats (cs_fm_index::line_fmt)
-enum LineFmt : uint32_t { kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2 };
+enum LineFmt : uint32_t { kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2, kFmtOcc = 3 };
 
 struct DevIndex {
   const void* lines;     // kLevels * nlines rank lines of the handle's format
@@ -236,6 +245,49 @@ struct Line64 {
 #pragma unroll
     for (int j = 1; j < 14; ++j) d = (k == (uint32_t)j) ? dw[j] : d;
     return (d >> (o & 31)) & 1u;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Occurrence line (small-alphabet engine): the whole BWT in one sequence of 32-B
+// lines, 64 rows each, one HBM access per rank of ANY symbol:
+//   dwords 0-2  low 32 bits of occ(code 0..2) at the line's first row
+//   dword 3     bits 8j..8j+7 = bits 32..39 of occ(code j)        (n < 2^40)
+//   dwords 4-7  the 64 rows' 2-bit codes, row r at bits 2r of the 128-bit payload
+// occ(code 3) = 64 q - occ0 - occ1 - occ2.  Used when at most four symbols carry
+// all but kMaxExc rows (DNA + terminator): a wavelet matrix then needs 2-4 line
+// reads per rank (one per non-pure level), this needs one.  Rows of the remaining
+// (rare) symbols are stored as code 0 and listed in NodeTable::exc_row.
+struct OccLine {
+  static constexpr uint32_t kBytes = 32;
+  static constexpr uint32_t kRows = 64;
+  using Raw = uint4[2];
+  __device__ static __forceinline__ void load(const void* lines, uint64_t q, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + q * 2;
+    v[0] = p[0];
+    v[1] = p[1];
+  }
+  // occ(code c) at the first row of line q
+  __device__ static __forceinline__ uint64_t base(const Raw& v, uint32_t c, uint64_t q) {
+    const uint64_t o0 = u64_of(v[0].x, v[0].w & 0xFFu);
+    const uint64_t o1 = u64_of(v[0].y, (v[0].w >> 8) & 0xFFu);
+    const uint64_t o2 = u64_of(v[0].z, (v[0].w >> 16) & 0xFFu);
+    return c == 0 ? o0 : c == 1 ? o1 : c == 2 ? o2 : (q << 6) - o0 - o1 - o2;
+  }
+  // rows among the first o (0..64) of the line whose code is c
+  __device__ static __forceinline__ uint32_t prefix(const Raw& v, uint32_t c, uint32_t o) {
+    constexpr uint64_t k55 = 0x5555555555555555ull;
+    const uint64_t pat = k55 * c;
+    const uint64_t x0 = u64_of(v[1].x, v[1].y) ^ pat, x1 = u64_of(v[1].z, v[1].w) ^ pat;
+    const uint64_t e0 = ~(x0 | (x0 >> 1)) & k55, e1 = ~(x1 | (x1 >> 1)) & k55;
+    const uint64_t m0 = o >= 32 ? ~0ull : ((1ull << (2 * o)) - 1);
+    const uint64_t m1 = o <= 32 ? 0ull : (o >= 64 ? ~0ull : ((1ull << (2 * (o - 32))) - 1));
+    return (uint32_t)(__popcll(e0 & m0) + __popcll(e1 & m1));
+  }
+  // code of row o (0..63)
+  __device__ static __forceinline__ uint32_t code(const Raw& v, uint32_t o) {
+    const uint64_t lo = u64_of(v[1].x, v[1].y), hi = u64_of(v[1].z, v[1].w);
+    return (uint32_t)(((o < 32 ? lo : hi) >> (2 * (o & 31))) & 3u);
   }
 };
 

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <string>
+#include <mutex>
 #include <vector>
 
 #include "../../include/cs_fmindex.h"
@@ -15,9 +16,10 @@ struct cs_fm_index {
   uint32_t stride = 32;
   void* d_lines = nullptr;            // 8 levels x nlines rank lines
   uint64_t nlines = 0;
-  uint32_t line_fmt = fmx::kFmtLine32; // Line32 (n < 2^32), Line32W (wide) or Line64
+  uint32_t line_fmt = fmx::kFmtLine32; // Line32 (n < 2^32), Line32W (wide), Line64 or Occ
   uint32_t line_bytes = 32;
   uint32_t line_bits = 224;
+  uint32_t nlevels = fmx::kLevels;     // rank-line sequences (1 for occurrence lines)
   bool wide = false;                  // n >= 2^32 (or forced): u64 samples and table entries
   void* d_ssa = nullptr;
   uint64_t nsamples = 0;
@@ -31,6 +33,17 @@ struct cs_fm_index {
   uint32_t ptab_k = 0, ptab_sigma = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
+
+  // Small host batches (single-pattern queries, p50 latency) stage through a
+  // per-handle pinned + HBM arena instead of per-call hipMalloc/hipFree and
+  // pageable copies; the lock serialises calls that share it.
+  struct Scratch {
+    std::mutex mu;
+    uint8_t* h = nullptr;  // pinned host
+    uint8_t* d = nullptr;  // HBM
+  };
+  static constexpr size_t kScratchBytes = 1u << 20;
+  mutable Scratch scratch;
 
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
   uint32_t ptab_entry_bytes() const { return wide ? 16 : 8; }
@@ -89,6 +102,8 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
 // Query launches (fm_query.hip).
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st);
+cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                             uint64_t npat, uint64_t* d_out, hipStream_t st);
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,

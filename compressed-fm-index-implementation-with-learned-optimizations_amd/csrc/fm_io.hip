@@ -8,10 +8,11 @@
 //
 // Directory layout (all little-endian raw arrays, exactly the HBM images):
 //   cs_fmindex.meta  "key value" lines: format, n, stride, line_bytes, line_bits,
-//                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text
+//                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
+//                    wide, line_fmt, levels, active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
-//   lines.bin        8 levels of rank lines
-//   ssa.bin          u32 sampled SA          isa.bin   u32 inverse-SA samples
+//   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
+//   ssa.bin          sampled SA              isa.bin   inverse-SA samples (u32; u64 if wide)
 //   ptab.bin         prefix table (if k > 0) text.bin  the text (if kept, for extract)
 #include <cerrno>
 #include <cstdio>
@@ -25,7 +26,7 @@
 namespace fmx {
 namespace {
 
-constexpr const char* kFormat = "cs_fmindex/1";
+constexpr const char* kFormat = "cs_fmindex/2";
 constexpr size_t kChunk = 256ull << 20;
 
 std::string join(const std::string& dir, const char* f) { return dir + "/" + f; }
@@ -99,7 +100,7 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   Pinned pin;
   FMX_HIP(hipHostMalloc(&pin.p, kChunk, hipHostMallocDefault));
   cs_status s;
-  const uint64_t lbytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
+  const uint64_t lbytes = (uint64_t)h->nlevels * h->nlines * h->line_bytes;
   if ((s = dump_dev(join(d, "lines.bin"), h->d_lines, lbytes, pin.p)) != CS_OK) return s;
   const uint64_t sb = h->sample_bytes();
   if ((s = dump_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * sb, pin.p)) != CS_OK) return s;
@@ -129,11 +130,11 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   if (!f) return io_fail("cannot write: " + join(d, "cs_fmindex.meta"));
   std::fprintf(f, "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
                   "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
-                  "wide %d\nline_fmt %u\n",
+                  "wide %d\nline_fmt %u\nlevels %u\n",
                kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
-               has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt);
+               has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels);
   for (int c = 0; c < 256; ++c) std::fprintf(f, "active %d %u\n", c, h->active_levels[c]);
   std::fclose(f);
   return CS_OK;
@@ -190,6 +191,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
   h->lf_exact = kv["lf_exact"] != 0;
   h->wide = kv["wide"] != 0;
   h->line_fmt = (uint32_t)kv["line_fmt"];
+  h->nlevels = (uint32_t)kv["levels"];
   auto fail = [&](cs_status s) {
     cs_fm_destroy(h);
     return s;
@@ -206,7 +208,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
   Pinned pin;
   if (hipHostMalloc(&pin.p, kChunk, hipHostMallocDefault) != hipSuccess)
     return fail(hip_fail(hipGetLastError(), "hipHostMalloc"));
-  const uint64_t lbytes = (uint64_t)kLevels * h->nlines * h->line_bytes;
+  const uint64_t lbytes = (uint64_t)h->nlevels * h->nlines * h->line_bytes;
   if (hipMalloc(&h->d_lines, lbytes ? lbytes : 16) != hipSuccess ||
       hipMalloc(&h->d_ssa, h->nsamples ? h->nsamples * h->sample_bytes() : 16) != hipSuccess ||
       hipMalloc(&h->d_isa, h->nisa ? h->nisa * h->sample_bytes() : 16) != hipSuccess ||

@@ -43,7 +43,8 @@ __device__ __forceinline__ void load_table(NodeTable& T, const NodeTable* __rest
 // the range empties (the reference's `return 0`).
 template <class F>
 __device__ __forceinline__ bool search_step(const DevIndex& ix, const NodeTable& T, uint32_t c,
-                                            uint64_t& sp, uint64_t& ep) {
+                                            uint64_t& sp, uint64_t& ep,
+                                            uint64_t* bytes = nullptr) {
   const uint64_t Cc = T.C[c];
   if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
   uint64_t ds = sp, de = ep;
@@ -56,6 +57,7 @@ __device__ __forceinline__ bool search_step(const DevIndex& ix, const NodeTable&
       uint32_t qa, oa, qe, oe;
       F::locate(S + ds, qa, oa);
       F::locate(S + de, qe, oe);
+      if (bytes) *bytes += (qa == qe ? 1u : 2u) * F::kBytes;  // distinct lines (measurement)
       typename F::Raw va, ve;
       F::load(lv, qa, va);
       F::load(lv, qe, ve);
@@ -69,132 +71,6 @@ __device__ __forceinline__ bool search_step(const DevIndex& ix, const NodeTable&
   sp = Cc + ds;
   ep = Cc + de;
   return sp < ep;
-}
-
-// Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
-// range empties.  Requires m >= 1, n >= 1.  The first step comes from C[]
-// (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
-// pattern's last k characters are all in its alphabet.
-template <class F>
-__device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
-                                                const uint8_t* __restrict__ P, uint64_t m,
-                                                uint64_t& sp_out, uint64_t& ep_out) {
-  uint64_t sp, ep, k;  // k = characters still to process, P[k-1] .. P[0]
-  bool from_table = false;
-  if (ix.ptab_k && m >= ix.ptab_k) {
-    uint32_t t = 0;
-    bool ok = true;
-    for (uint32_t i = (uint32_t)(m - ix.ptab_k); i < m; ++i) {
-      const uint32_t d = T.code[P[i]];
-      ok &= d != kNoCode;
-      t = t * ix.ptab_sigma + d;
-    }
-    if (ok) {
-      ptab_at(ix, t, sp, ep);
-      k = m - ix.ptab_k;
-      from_table = true;
-    }
-  }
-  if (!from_table) {
-    const uint32_t c = P[m - 1];
-    sp = T.C[c];  // occ(c,0)=0, occ(c,n)=freq(c)
-    ep = T.C[c + 1];
-    k = m - 1;
-  }
-  if (sp >= ep) return false;
-  uint32_t cn = k ? P[k - 1] : 0u;
-  while (k-- > 0) {
-    const uint32_t c = cn;
-    if (k > 0) cn = P[k - 1];  // prefetch the next character
-    if (!search_step<F>(ix, T, c, sp, ep)) return false;
-  }
-  sp_out = sp;
-  ep_out = ep;
-  return true;
-}
-
-// Prefix table entry t: backward search of the k-mer whose j-th character from
-// the end is sym[digit_j(t)] (same steps as above, from C[]).
-template <class F>
-__global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entries,
-                                                     void* __restrict__ tab) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
-  __syncthreads();
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += stride) {
-    uint64_t rest = t;
-    uint32_t c = T.sym[rest % ix.ptab_sigma];
-    rest /= ix.ptab_sigma;
-    uint64_t sp = T.C[c], ep = T.C[c + 1];
-    bool live = sp < ep;
-    for (uint32_t j = 1; j < ix.ptab_k && live; ++j) {
-      c = T.sym[rest % ix.ptab_sigma];
-      rest /= ix.ptab_sigma;
-      live = search_step<F>(ix, T, c, sp, ep);
-    }
-    if (!live) sp = ep = 0;
-    if (ix.wide)
-      static_cast<ulonglong2*>(tab)[t] = make_ulonglong2(sp, ep);
-    else
-      static_cast<uint2*>(tab)[t] = make_uint2((uint32_t)sp, (uint32_t)ep);
-  }
-}
-
-template <class F>
-__global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
-                                                const uint64_t* __restrict__ offs, uint64_t npat,
-                                                uint64_t* __restrict__ out) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
-  __syncthreads();
-  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (q >= npat) return;
-  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
-  uint64_t res;
-  if (m == 0) res = ix.n;       // fm_index.cpp:80
-  else if (ix.n == 0) res = 0;  // :81
-  else {
-    uint64_t sp, ep;
-    res = backward_search<F>(ix, T, pats + o0, m, sp, ep) ? ep - sp : 0;
-  }
-  out[q] = res;
-}
-
-template <class F>
-__global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
-                                                        const uint8_t* __restrict__ pats,
-                                                        const uint64_t* __restrict__ offs,
-                                                        uint64_t npat, uint64_t limit,
-                                                        uint64_t* __restrict__ sp_out,
-                                                        uint64_t* __restrict__ cnt_out) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
-  __syncthreads();
-  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (q > npat) return;
-  if (q == npat) {  // scan slot for the total
-    cnt_out[q] = 0;
-    return;
-  }
-  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
-  uint64_t sp = 0, ep = 0;
-  if (m && ix.n) {  // fm_index.cpp:109: empty pattern or empty text -> {}
-    if (!backward_search<F>(ix, T, pats + o0, m, sp, ep)) sp = ep = 0;
-  }
-  const uint64_t c = ep - sp;
-  sp_out[q] = sp;
-  cnt_out[q] = c < limit ? c : limit;  // fm_index.cpp:125 `positions.size() < limit`
-}
-
-// rows[j] = sp[q] + (j - offs[q]) for the reported rows of pattern q (row order).
-__global__ void k_expand_rows(const uint64_t* __restrict__ sp, const uint64_t* __restrict__ offs,
-                              uint64_t npat, uint64_t* __restrict__ rows) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
-    const uint64_t a = offs[q], b = offs[q + 1], s = sp[q];
-    for (uint64_t j = a; j < b; ++j) rows[j] = s + (j - a);
-  }
 }
 
 // One LF step (fm_index.hpp:62-66): descend the wavelet matrix from row i reading
@@ -228,6 +104,270 @@ __device__ __forceinline__ uint64_t lf_step(const DevIndex& ix, const NodeTable&
   return T.C[x] + (pos - T.S8[x]);
 }
 
+// ---- rare-symbol rows of the occurrence-line engine (NodeTable::exc_*) ----
+// number of exception rows < i (lower bound in the ascending list)
+__device__ __forceinline__ uint32_t exc_before(const NodeTable& T, uint64_t i) {
+  uint32_t lo = 0, hi = T.exc_n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (T.exc_row[mid] < i) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// occ(c, i) of a rare symbol c
+__device__ __forceinline__ uint64_t exc_rank(const NodeTable& T, uint32_t c, uint64_t i) {
+  uint64_t r = 0;
+  for (uint32_t j = 0; j < T.exc_n && T.exc_row[j] < i; ++j) r += T.exc_sym[j] == c;
+  return r;
+}
+
+// ---- engines: what the kernels call per backward-search step / LF step / rank ----
+// WM<F>: the 8-level wavelet matrix (the reference's WaveletTree) in rank lines F.
+template <class F>
+struct WM {
+  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
+                                              uint64_t& sp, uint64_t& ep,
+                                              uint64_t* bytes = nullptr) {
+    return search_step<F>(ix, T, c, sp, ep, bytes);
+  }
+  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
+                                                uint64_t pos, uint32_t* sym = nullptr) {
+    return lf_step<F>(ix, T, pos, sym);
+  }
+  // WaveletTree::rank(c, i) (wavelet.cpp:59-96) for 0 < i <= n, c present
+  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
+                                                  uint32_t c, uint64_t i) {
+    uint64_t d = i;
+    for (int l = 0; l < kLevels; ++l) {
+      const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
+      if (!(T.flags[nid] & kPure)) {
+        const uint64_t r = rank1_at<F>(level_ptr<F>(ix, l), T.S[nid] + d) - T.R[nid];
+        d = ((c >> (7 - l)) & 1u) ? r : d - r;
+      }
+    }
+    return d;
+  }
+};
+
+// OccE: occurrence lines (fm_device.hpp OccLine).  occ(c, i) = one line read:
+// base(code) + rows of that code before i in the line, minus the rare-symbol rows
+// below i when c has code 0 (they are stored as code 0); rare symbols are counted
+// from the LDS list.  sp and ep in the same line share one read.
+struct OccE {
+  __device__ static __forceinline__ uint64_t occ_line(const OccLine::Raw& v, uint32_t code,
+                                                      uint64_t i) {
+    return OccLine::base(v, code, i >> 6) + OccLine::prefix(v, code, (uint32_t)(i & 63));
+  }
+  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
+                                              uint64_t& sp, uint64_t& ep,
+                                              uint64_t* bytes = nullptr) {
+    const uint64_t Cc = T.C[c];
+    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
+    const uint32_t code = T.occ_code[c];
+    uint64_t rs, re;
+    if (code == kNoCode) {
+      rs = exc_rank(T, c, sp);
+      re = exc_rank(T, c, ep);
+    } else {
+      const uint64_t qa = sp >> 6, qe = ep >> 6;
+      if (bytes) *bytes += (qa == qe ? 1u : 2u) * OccLine::kBytes;
+      OccLine::Raw va;
+      OccLine::load(ix.lines, qa, va);
+      OccLine::Raw ve = {va[0], va[1]};
+      if (qe != qa) OccLine::load(ix.lines, qe, ve);
+      rs = occ_line(va, code, sp);
+      re = occ_line(ve, code, ep);
+      if (code == 0 && T.exc_n) {
+        rs -= exc_before(T, sp);
+        re -= exc_before(T, ep);
+      }
+    }
+    sp = Cc + rs;
+    ep = Cc + re;
+    return sp < ep;
+  }
+  // LF(i) = C[BWT[i]] + occ(BWT[i], i), symbol and occ from the same line
+  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
+                                                uint64_t pos, uint32_t* sym_out = nullptr) {
+    OccLine::Raw v;
+    OccLine::load(ix.lines, pos >> 6, v);
+    const uint32_t code = OccLine::code(v, (uint32_t)(pos & 63));
+    uint32_t c = T.occ_sym[code];
+    uint64_t r = occ_line(v, code, pos);
+    if (code == 0 && T.exc_n) {
+      const uint32_t e = exc_before(T, pos);
+      if (e < T.exc_n && T.exc_row[e] == pos) {
+        c = T.exc_sym[e];
+        r = exc_rank(T, c, pos);
+      } else {
+        r -= e;
+      }
+    }
+    if (sym_out) *sym_out = c;
+    return T.C[c] + r;
+  }
+  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
+                                                  uint32_t c, uint64_t i) {
+    const uint32_t code = T.occ_code[c];
+    if (code == kNoCode) return exc_rank(T, c, i);
+    OccLine::Raw v;
+    OccLine::load(ix.lines, i >> 6, v);
+    uint64_t r = occ_line(v, code, i);
+    if (code == 0) r -= exc_before(T, i);
+    return r;
+  }
+};
+
+// Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
+// range empties.  Requires m >= 1, n >= 1.  The first step comes from C[]
+// (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
+// pattern's last k characters are all in its alphabet.
+template <class E>
+__device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
+                                                const uint8_t* __restrict__ P, uint64_t m,
+                                                uint64_t& sp_out, uint64_t& ep_out,
+                                                uint64_t* bytes = nullptr) {
+  uint64_t sp, ep, k;  // k = characters still to process, P[k-1] .. P[0]
+  bool from_table = false;
+  if (ix.ptab_k && m >= ix.ptab_k) {
+    uint32_t t = 0;
+    bool ok = true;
+    for (uint32_t i = (uint32_t)(m - ix.ptab_k); i < m; ++i) {
+      const uint32_t d = T.code[P[i]];
+      ok &= d != kNoCode;
+      t = t * ix.ptab_sigma + d;
+    }
+    if (ok) {
+      ptab_at(ix, t, sp, ep);
+      if (bytes) *bytes += ix.wide ? 16u : 8u;
+      k = m - ix.ptab_k;
+      from_table = true;
+    }
+  }
+  if (!from_table) {
+    const uint32_t c = P[m - 1];
+    sp = T.C[c];  // occ(c,0)=0, occ(c,n)=freq(c)
+    ep = T.C[c + 1];
+    k = m - 1;
+  }
+  if (sp >= ep) return false;
+  uint32_t cn = k ? P[k - 1] : 0u;
+  while (k-- > 0) {
+    const uint32_t c = cn;
+    if (k > 0) cn = P[k - 1];  // prefetch the next character
+    if (!E::step(ix, T, c, sp, ep, bytes)) return false;
+  }
+  sp_out = sp;
+  ep_out = ep;
+  return true;
+}
+
+// Prefix table entry t: backward search of the k-mer whose j-th character from
+// the end is sym[digit_j(t)] (same steps as above, from C[]).
+template <class E>
+__global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entries,
+                                                     void* __restrict__ tab) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += stride) {
+    uint64_t rest = t;
+    uint32_t c = T.sym[rest % ix.ptab_sigma];
+    rest /= ix.ptab_sigma;
+    uint64_t sp = T.C[c], ep = T.C[c + 1];
+    bool live = sp < ep;
+    for (uint32_t j = 1; j < ix.ptab_k && live; ++j) {
+      c = T.sym[rest % ix.ptab_sigma];
+      rest /= ix.ptab_sigma;
+      live = E::step(ix, T, c, sp, ep);
+    }
+    if (!live) sp = ep = 0;
+    if (ix.wide)
+      static_cast<ulonglong2*>(tab)[t] = make_ulonglong2(sp, ep);
+    else
+      static_cast<uint2*>(tab)[t] = make_uint2((uint32_t)sp, (uint32_t)ep);
+  }
+}
+
+template <class E>
+__global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                const uint64_t* __restrict__ offs, uint64_t npat,
+                                                uint64_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= npat) return;
+  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  uint64_t res;
+  if (m == 0) res = ix.n;       // fm_index.cpp:80
+  else if (ix.n == 0) res = 0;  // :81
+  else {
+    uint64_t sp, ep;
+    res = backward_search<E>(ix, T, pats + o0, m, sp, ep) ? ep - sp : 0;
+  }
+  out[q] = res;
+}
+
+// Measurement twin of k_count: the algorithmic bytes of each query's search —
+// distinct lines per rank pair (sp and ep in one line read once) times the line
+// size, plus the prefix-table entry — for the roofline in bench.py.
+template <class E>
+__global__ __launch_bounds__(kBlk) void k_count_bytes(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                      const uint64_t* __restrict__ offs,
+                                                      uint64_t npat, uint64_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= npat) return;
+  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  uint64_t bytes = 0;
+  if (m && ix.n) {
+    uint64_t sp, ep;
+    (void)backward_search<E>(ix, T, pats + o0, m, sp, ep, &bytes);
+  }
+  out[q] = bytes;
+}
+
+template <class E>
+__global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
+                                                        const uint8_t* __restrict__ pats,
+                                                        const uint64_t* __restrict__ offs,
+                                                        uint64_t npat, uint64_t limit,
+                                                        uint64_t* __restrict__ sp_out,
+                                                        uint64_t* __restrict__ cnt_out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q > npat) return;
+  if (q == npat) {  // scan slot for the total
+    cnt_out[q] = 0;
+    return;
+  }
+  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  uint64_t sp = 0, ep = 0;
+  if (m && ix.n) {  // fm_index.cpp:109: empty pattern or empty text -> {}
+    if (!backward_search<E>(ix, T, pats + o0, m, sp, ep)) sp = ep = 0;
+  }
+  const uint64_t c = ep - sp;
+  sp_out[q] = sp;
+  cnt_out[q] = c < limit ? c : limit;  // fm_index.cpp:125 `positions.size() < limit`
+}
+
+// rows[j] = sp[q] + (j - offs[q]) for the reported rows of pattern q (row order).
+__global__ void k_expand_rows(const uint64_t* __restrict__ sp, const uint64_t* __restrict__ offs,
+                              uint64_t npat, uint64_t* __restrict__ rows) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
+    const uint64_t a = offs[q], b = offs[q + 1], s = sp[q];
+    for (uint64_t j = a; j < b; ++j) rows[j] = s + (j - a);
+  }
+}
+
 template <bool POW2>
 __device__ __forceinline__ bool is_sampled(const DevIndex& ix, uint64_t row) {
   if (POW2) return (row & ((1ull << ix.stride_shift) - 1)) == 0;
@@ -241,7 +381,7 @@ __device__ __forceinline__ uint64_t sample_index(const DevIndex& ix, uint64_t ro
 }
 
 // Persistent LF walk (fm_index.cpp:125-153).  Block b owns rows [b*chunk, ...).
-template <class F, bool POW2>
+template <class E, bool POW2>
 __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __restrict__ rows,
                                                uint64_t total, uint64_t chunk,
                                                uint64_t* __restrict__ out,
@@ -280,7 +420,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
         }
         active = false;
       } else {
-        pos = lf_step<F>(ix, T, pos);
+        pos = E::lf(ix, T, pos);
         ++steps;
       }
     }
@@ -299,7 +439,7 @@ __global__ void k_level_rank1(DevIndex ix, int level, const uint64_t* __restrict
   out[t] = rank1_at<F>(level_ptr<F>(ix, level), p);
 }
 
-template <class F>
+template <class E>
 __global__ void k_wt_rank(DevIndex ix, const uint8_t* __restrict__ syms,
                           const uint64_t* __restrict__ pos, uint64_t k, uint64_t* __restrict__ out) {
   __shared__ NodeTable T;
@@ -310,20 +450,11 @@ __global__ void k_wt_rank(DevIndex ix, const uint8_t* __restrict__ syms,
   const uint32_t c = syms[t];
   const uint64_t i = pos[t];
   uint64_t d = 0;
-  if (i != 0 && i <= ix.n && T.C[c] != T.C[c + 1]) {  // wavelet.cpp:60
-    d = i;
-    for (int l = 0; l < kLevels; ++l) {
-      const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
-      if (!(T.flags[nid] & kPure)) {
-        const uint64_t r = rank1_at<F>(level_ptr<F>(ix, l), T.S[nid] + d) - T.R[nid];
-        d = ((c >> (7 - l)) & 1u) ? r : d - r;
-      }
-    }
-  }
+  if (i != 0 && i <= ix.n && T.C[c] != T.C[c + 1]) d = E::rank(ix, T, c, i);  // wavelet.cpp:60
   out[t] = d;
 }
 
-template <class F>
+template <class E>
 __global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
                      uint64_t* __restrict__ out, uint8_t* __restrict__ sym) {
   __shared__ NodeTable T;
@@ -338,7 +469,7 @@ __global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
     return;
   }
   uint32_t c;
-  const uint64_t v = lf_step<F>(ix, T, i, &c);
+  const uint64_t v = E::lf(ix, T, i, &c);
   if (out) out[t] = v;
   if (sym) sym[t] = (uint8_t)c;
 }
@@ -347,7 +478,7 @@ __global__ void k_lf(DevIndex ix, const uint64_t* __restrict__ rows, uint64_t k,
 // inverse-SA sample of the first sampled text position e >= pos+len (position n =
 // suffix 0 cyclically, whose BWT symbol is T[n-1]) and invert LF down to pos; each
 // LF step yields BWT[row] = T[cur-1].  One lane per query; requires lf_exact.
-template <class F>
+template <class E>
 __global__ __launch_bounds__(kBlk) void k_extract(DevIndex ix, const uint64_t* __restrict__ pos,
                                                   const uint64_t* __restrict__ len,
                                                   const uint64_t* __restrict__ out_offs,
@@ -370,14 +501,14 @@ __global__ __launch_bounds__(kBlk) void k_extract(DevIndex ix, const uint64_t* _
   uint8_t* o = out + out_offs[q];
   for (uint64_t cur = e; cur > p; --cur) {
     uint32_t c;
-    const uint64_t nxt = lf_step<F>(ix, T, row, &c);
+    const uint64_t nxt = E::lf(ix, T, row, &c);
     if (cur - 1 < end) o[cur - 1 - p] = (uint8_t)c;
     row = nxt;
   }
 }
 
 // WaveletTree::access for every row (the BWT), grid-stride.
-template <class F>
+template <class E>
 __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__ out) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
@@ -385,29 +516,32 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ix.n; i += stride) {
     uint32_t c;
-    (void)lf_step<F>(ix, T, i, &c);
+    (void)E::lf(ix, T, i, &c);
     out[i] = (uint8_t)c;
   }
 }
 
 }  // namespace
 
-// Dispatch on the handle's rank-line format.
+// Dispatch on the handle's engine / rank-line format.
 #define FMX_DISPATCH(h, KERNEL, GRID, ...)                                      \
   do {                                                                          \
-    if ((h)->line_fmt == kFmtLine32)                                            \
-      KERNEL<Line32><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
+    if ((h)->line_fmt == kFmtOcc)                                               \
+      KERNEL<OccE><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                       \
+    else if ((h)->line_fmt == kFmtLine32)                                       \
+      KERNEL<WM<Line32>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
     else if ((h)->line_fmt == kFmtLine32W)                                      \
-      KERNEL<Line32W><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                    \
+      KERNEL<WM<Line32W>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                \
     else                                                                        \
-      KERNEL<Line64><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                     \
+      KERNEL<WM<Line64>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
     FMX_HIP(hipGetLastError());                                                 \
   } while (0)
 
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^26, max(4096, n/32)) entries (8 B each: at most n/4 bytes, the
-// order of the sampled SA); none when k < 2.  Entries are (sp, ep) as 2 x u32, or
+// sigma^k <= min(2^28, max(4096, n/32)) entries (8 B each, 16 B in wide indexes:
+// at most n/4 resp. n/2 bytes, the order of the sampled SA); none when k < 2.
+// DNA: k = 13 at 4 GB, k = 14 from 8.6 GB on.  Entries are (sp, ep) as 2 x u32, or
 // 2 x u64 in wide indexes.  CS_FM_PREFIX_K overrides k (0 = off).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
@@ -427,7 +561,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   }
   if (sigma == 0) return CS_OK;
   uint64_t cap = n / 32 > 4096 ? n / 32 : 4096;
-  if (cap > (1ull << 26)) cap = 1ull << 26;
+  if (cap > (1ull << 28)) cap = 1ull << 28;
   uint32_t k = 0;
   uint64_t entries = 1;
   while (k < 32 && entries * sigma <= cap) {
@@ -478,6 +612,14 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
   return CS_OK;
 }
 
+cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                             uint64_t npat, uint64_t* d_out, hipStream_t st) {
+  if (!npat) return CS_OK;
+  FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat,
+               d_out);
+  return CS_OK;
+}
+
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
@@ -517,15 +659,18 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   unsigned long long* err = reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
-  if (h->line_fmt == kFmtLine32) {
-    if (pow2) k_walk<Line32, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<Line32, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  if (h->line_fmt == kFmtOcc) {
+    if (pow2) k_walk<OccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<OccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  } else if (h->line_fmt == kFmtLine32) {
+    if (pow2) k_walk<WM<Line32>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<WM<Line32>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else if (h->line_fmt == kFmtLine32W) {
-    if (pow2) k_walk<Line32W, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<Line32W, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<WM<Line32W>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<WM<Line32W>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else {
-    if (pow2) k_walk<Line64, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<Line64, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<WM<Line64>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<WM<Line64>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   }
   FMX_HIP(hipGetLastError());
   // rows must outlive the kernel: synchronise before DevBuf frees it
@@ -549,8 +694,19 @@ cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, u
 
 cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
                              uint64_t* d_out, hipStream_t st) {
+  if (h->line_fmt == kFmtOcc) {
+    set_error("level rank1: this index uses occurrence lines, not a wavelet matrix");
+    return CS_ERR_UNSUPPORTED;
+  }
   if (!k) return CS_OK;
-  FMX_DISPATCH(h, k_level_rank1, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), level, d_pos, k, d_out);
+  const unsigned g = grid_for(k, kBlk, 0xFFFFFFFFu);
+  if (h->line_fmt == kFmtLine32)
+    k_level_rank1<Line32><<<g, kBlk, 0, st>>>(h->dev(), level, d_pos, k, d_out);
+  else if (h->line_fmt == kFmtLine32W)
+    k_level_rank1<Line32W><<<g, kBlk, 0, st>>>(h->dev(), level, d_pos, k, d_out);
+  else
+    k_level_rank1<Line64><<<g, kBlk, 0, st>>>(h->dev(), level, d_pos, k, d_out);
+  FMX_HIP(hipGetLastError());
   return CS_OK;
 }
 

@@ -58,9 +58,9 @@ typedef struct cs_fm_index cs_fm_index;
 typedef struct cs_fm_info {
   uint64_t n;              /* text length incl. any terminator the caller appended */
   uint32_t ssa_stride;
-  uint32_t line_bits;      /* payload bits per rank line (224 in 32-B lines, 448 in 64-B) */
+  uint32_t line_bits;      /* positions per line (224 / 192 / 448 bits; 64 rows in occurrence lines) */
   uint64_t lines_per_level;
-  uint64_t rank_bytes;     /* 8 levels of rank lines in HBM */
+  uint64_t rank_bytes;     /* all rank lines in HBM */
   uint64_t ssa_bytes;
   uint32_t active_levels[256]; /* per symbol: bitmask of levels needing a memory access */
   int device;
@@ -68,13 +68,19 @@ typedef struct cs_fm_info {
   uint32_t prefix_sigma;   /* its alphabet size */
   uint64_t prefix_bytes;
   uint8_t prefix_code[256];/* digit of each symbol in the table alphabet, 255 = not in it */
+  uint32_t engine;         /* 0 = wavelet matrix in rank lines, 1 = occurrence lines */
+  uint32_t line_bytes;     /* bytes per rank / occurrence line (32 or 64) */
+  uint32_t levels;         /* rank-line sequences: 8 wavelet levels, or 1 */
+  uint32_t rare_rows;      /* occurrence lines: BWT rows of rare symbols kept in the table */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);
 
 /* FMIndex::build_from_text — fm_index.hpp:19, fm_index.cpp:16-69.
  * Builds the whole index on `device` (suffix array by prefix doubling, cyclic BWT,
- * C[], 8-level wavelet matrix, row-sampled SSA).  `text` is a host pointer. */
+ * C[], row-sampled SSA, and the rank structure: occurrence lines when at most four
+ * symbols hold all but 128 BWT rows, else the 8-level wavelet matrix; environment
+ * CS_FM_ENGINE=wavelet forces the latter).  `text` is a host pointer. */
 cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_params* p,
                                 int device, cs_fm_index** out);
 /* Same, with the text already in device memory on `device`. */
@@ -127,6 +133,12 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
 cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream);
+/* Measurement twin of cs_fm_count_batch_device: d_out[q] = the algorithmic HBM
+ * bytes of query q's search (distinct rank/occurrence lines per rank pair x line
+ * size + the prefix-table entry), for roofline accounting (bench.py). */
+cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
+                                   void* stream);
 /* locate phase 1: backward search; d_sp[q] = first row, d_out_offs = exclusive scan
  * of min(count, limit) (npat+1 entries).  Synchronises `stream` to return *total. */
 cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
@@ -146,7 +158,8 @@ cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d
 cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream);
 
 /* Building blocks, for parity tests (host arrays in/out):
- *   level rank1   — BitVector::rank1 of wavelet level l (src/core/bitvector.cpp:165-230)
+ *   level rank1   — BitVector::rank1 of wavelet level l (src/core/bitvector.cpp:165-230);
+ *                   CS_ERR_UNSUPPORTED on an occurrence-line index (no levels)
  *   wavelet rank  — WaveletTree::rank (src/core/wavelet.cpp:59-96)
  *   access        — WaveletTree::access (src/core/wavelet.cpp:102-128) = BWT[i]
  *   LF            — FMIndex::LF (src/api/fm_index.hpp:62-66) */

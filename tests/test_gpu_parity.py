@@ -4,7 +4,8 @@ golden vectors and the CPU restatement (oracle/), bit for bit.
 Layers checked separately, bottom-up:
   suffix array      (device prefix doubling)    vs src/core/sais.hpp:8-16 order
   level rank1       (32/64-B rank lines)           vs BitVector::rank1, every position
-  wavelet rank      (node-table descent)         vs WaveletTree::rank, every (c, i)
+  wavelet rank      (node-table descent, or one occurrence-line read)
+                                                 vs WaveletTree::rank, every (c, i)
   access / LF       (fused descent)              vs BWT / FMIndex::LF, every row
   count / locate    (batched kernels)            vs golden vectors and the oracle
 """
@@ -21,13 +22,19 @@ pytestmark = pytest.mark.gpu
 
 ENGINE_VARIANTS = {
     # name: environment of the builder (test hooks in csrc/fm_build.hip / fm_query.hip)
-    "line32": {},                                   # default for n < 2^32
-    "line64": {"CS_FM_LINE_BYTES": "64"},           # 64-B rank lines
-    "line32_noprefix": {"CS_FM_PREFIX_K": "0"},     # prefix table off
-    # the n >= 2^32 engine at small n: u64 samples/table, 64-B lines, bucketed sorter
+    # default: occurrence lines when <= 4 symbols hold all but 128 BWT rows, else
+    # the wavelet matrix in 32-B lines (Line32)
+    "auto": {},
+    "auto_noprefix": {"CS_FM_PREFIX_K": "0"},       # prefix table off
+    "wavelet": {"CS_FM_ENGINE": "wavelet"},         # wavelet matrix for every text
+    "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
+    # the n >= 2^32 engines at small n: u64 samples/table, bucketed sorter, and
+    # occurrence lines or 32-B wide rank lines (Line32W)
     "wide_bucketed": {"CS_FM_WIDE": "1", "CS_FM_SA_BUILDER": "bucketed"},
+    "wide_wavelet": {"CS_FM_WIDE": "1", "CS_FM_ENGINE": "wavelet"},
 }
-_HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX")
+_HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
+          "CS_FM_ENGINE")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -65,8 +72,27 @@ def _texts():
         # 32-B lines hold 224 bits = 3.5 ballot groups: n in the last half group
         "straddle_201": bytes(rng.choice(list(b"ab"), 200).astype(np.uint8)) + b"$",
         "straddle_649": bytes(rng.choice(list(b"ACGT"), 648).astype(np.uint8)) + b"$",
+        # occurrence lines hold 64 rows: n around line edges
+        "occ_edge_63": bytes(rng.choice(list(b"ACGT"), 62).astype(np.uint8)) + b"$",
+        "occ_edge_64": bytes(rng.choice(list(b"ACGT"), 63).astype(np.uint8)) + b"$",
+        "occ_edge_65": bytes(rng.choice(list(b"ACGT"), 64).astype(np.uint8)) + b"$",
+        "occ_edge_128": bytes(rng.choice(list(b"ACGT"), 128).astype(np.uint8)),
+        # rare symbols (stored as code 0 and listed in the node table)
+        "rare_N_41": _sprinkle(rng, 3000, b"N" * 40) + b"$",
+        "rare_128": _sprinkle(rng, 5000, b"N" * 127) + b"$",        # the table's capacity
+        "rare_129": _sprinkle(rng, 5000, b"N" * 128) + b"$",        # one more: wavelet matrix
+        "rare_both_ends": _sprinkle(rng, 2000, b"!!~~~\x00\xff") + b"$",  # below and above ACGT
+        "rare_runs": b"ACGT" * 200 + b"N" * 60 + b"TTGCA" * 100 + b"$",
     }
     return out
+
+
+def _sprinkle(rng, n, rare):
+    """n random ACGT bytes with the `rare` bytes written at distinct random places."""
+    t = rng.choice(list(b"ACGT"), n).astype(np.uint8)
+    at = rng.choice(n, len(rare), replace=False)
+    t[at] = np.frombuffer(rare, np.uint8)
+    return t.tobytes()
 
 
 TEXTS = _texts()
@@ -103,14 +129,33 @@ def test_suffix_array_random_sweep(pkg):
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))
-def test_level_rank1_every_position(built, name):
+def test_level_rank1_every_position(built, pkg, name):
     g, o = built(name)
     n = len(TEXTS[name])
+    if g.info().engine == 1:  # occurrence lines: no wavelet levels to query
+        with pytest.raises(pkg.FMIndexError):
+            g.level_rank1(0, np.arange(4, dtype=np.uint64))
+        return
     pos = np.arange(n + 3, dtype=np.uint64)  # includes i >= size (count_ones path)
     for l in range(8):
         lv = o.level(l)
         want = np.array([lv.rank1(int(i)) for i in pos], np.uint64)
         assert g.level_rank1(l, pos).tolist() == want.tolist(), (name, l)
+
+
+def test_engine_choice(built):
+    """Occurrence lines iff <= 4 symbols hold all but at most 128 BWT rows (and the
+    wavelet matrix is not forced); rare rows are listed in the node table."""
+    forced = os.environ.get("CS_FM_ENGINE") == "wavelet"
+    want = {"dna_5k": (1, 1), "banana": (1, 0), "single": (1, 0), "rare_N_41": (1, 41),
+            "rare_128": (1, 128), "rare_129": (0, 0), "bytes_5k": (0, 0),
+            "rare_both_ends": (1, 8)}
+    for name, (engine, rare) in want.items():
+        info = built(name)[0].info()
+        if forced:
+            engine, rare = 0, 0
+        assert (info.engine, info.rare_rows) == (engine, rare), name
+        assert info.levels == (1 if engine else 8) and info.line_bytes in (32, 64)
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))

@@ -1,4 +1,4 @@
-"""Full-size GPU checks (BASELINE.json configs C3/C4) through size-independent
+"""Full-size GPU checks (BASELINE.json configs C2-C5) through size-independent
 properties — no CPU index is built at these sizes:
 
   * every Q_text pattern (a substring sampled at a known position) is found;
@@ -95,13 +95,21 @@ def test_c4_dna_4gb():
 
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C5") == "1", reason="C5 disabled")
-def test_c5_dna_32gb_wide():
-    """BASELINE configs[4]: 32 GB text (n >= 2^32) — wide index (u64 samples, Line32W
-    rank lines) built by the pass-by-pass bucketed suffix sorter."""
+@pytest.mark.parametrize("engine", ["auto", "wavelet"])
+def test_c5_dna_32gb_wide(engine, monkeypatch):
+    """BASELINE configs[4]: 32 GB text (n >= 2^32) — wide index (u64 samples) built by
+    the pass-by-pass bucketed suffix sorter, with occurrence lines (default for
+    DNA) or the wavelet matrix in 32-B wide rank lines (Line32W)."""
+    if engine == "wavelet":
+        monkeypatch.setenv("CS_FM_ENGINE", "wavelet")
     pkg = load_pkg()
     idx, text, host, N = _build(pkg, "dna", 31_999_999_999)
     info = idx.info()
-    assert N == 32_000_000_000 and info.line_bits == 192
+    assert N == 32_000_000_000
+    if engine == "wavelet":
+        assert info.engine == 0 and info.line_bits == 192
+    else:
+        assert info.engine == 1 and info.rare_rows == 1
     P = _qtext(pkg, text, N, 20, 200_000)
     _check_qtext(idx, host, N, P, nloc=20_000)
     ones = idx.count_batch([bytes([c]) for c in range(256)])
