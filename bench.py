@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--p50-calls", type=int, default=1000)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--locate-batch", type=int, default=1_000_000,
+    ap.add_argument("--locate-batch", type=int, default=12_500_000,
                     help="patterns of the batch timed through locate() (N=1 only; 0 = skip)")
     ap.add_argument("--prefix-k", type=int, default=None,
                     help="prefix-table depth override (0 = off; default automatic)")
@@ -178,7 +178,7 @@ def main():
         traffic = None
         prof = os.path.join(ROOT, "profiles", "pmc_count.json")
         engine = "occ" if info.engine == 1 else "wm%d" % info.line_bytes
-        wl = "%s:%d:m%d:b%d:%s" % (args.kind, N, m, B, engine)
+        wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
         if os.path.exists(prof):
             pj = json.load(open(prof))
             if pj.get("workload") == wl:

@@ -241,6 +241,21 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   hipStream_t st = (hipStream_t)stream;
   const uint64_t bytes = offs[npat] - offs[0];
   const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
+  if (npat == 1 && bytes <= OnePattern::kMax) {
+    // single pattern (the p50 path): pattern in the kernel arguments, count written
+    // into the pinned arena by the kernel; one launch + one synchronisation
+    std::unique_lock<std::mutex> lk(h->scratch.mu);
+    if ((s = scratch_ready(h)) != CS_OK) return s;
+    OnePattern p;
+    p.m = (uint32_t)bytes;
+    if (bytes) std::memcpy(p.b, pats + offs[0], bytes);
+    uint64_t* res = reinterpret_cast<uint64_t*>(h->scratch.h);
+    s = launch_count_one(h, p, res, st);
+    if (s != CS_OK) return s;
+    FMX_HIP(hipStreamSynchronize(st));
+    out_counts[0] = *reinterpret_cast<volatile uint64_t*>(res);
+    return CS_OK;
+  }
   if (o_pats + bytes + 16 <= cs_fm_index::kScratchBytes) {
     // small batch: one pinned H2D copy, the search, one D2H copy
     std::unique_lock<std::mutex> lk(h->scratch.mu);

@@ -90,6 +90,13 @@ struct DevIndex {
   uint32_t lf_exact;
 };
 
+// A single pattern passed by value in kernel arguments (k_count_one).
+struct OnePattern {
+  static constexpr uint32_t kMax = 128;
+  uint8_t b[kMax];
+  uint32_t m;
+};
+
 __device__ __forceinline__ uint64_t ssa_at(const DevIndex& ix, uint64_t k) {
   return ix.wide ? static_cast<const uint64_t*>(ix.ssa)[k] : static_cast<const uint32_t*>(ix.ssa)[k];
 }

@@ -102,6 +102,8 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
 // Query launches (fm_query.hip).
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st);
+cs_status launch_count_one(const cs_fm_index* h, const fmx::OnePattern& p, uint64_t* out_host,
+                           hipStream_t st);
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                              uint64_t npat, uint64_t* d_out, hipStream_t st);
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,

@@ -311,6 +311,24 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
   out[q] = res;
 }
 
+// Single-pattern count (FMIndex::count, the p50 path): the pattern travels in the
+// kernel arguments and the count is stored straight into pinned host memory, so a
+// call is one launch and one synchronisation.  One lane; the node table is read
+// through the cache hierarchy instead of being staged into LDS.
+template <class E>
+__global__ void k_count_one(DevIndex ix, OnePattern p, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const NodeTable& T = *ix.table;
+  uint64_t res;
+  if (p.m == 0) res = ix.n;       // fm_index.cpp:80
+  else if (ix.n == 0) res = 0;    // :81
+  else {
+    uint64_t sp, ep;
+    res = backward_search<E>(ix, T, p.b, p.m, sp, ep) ? ep - sp : 0;
+  }
+  *out = res;
+}
+
 // Measurement twin of k_count: the algorithmic bytes of each query's search —
 // distinct lines per rank pair (sp and ep in one line read once) times the line
 // size, plus the prefix-table entry — for the roofline in bench.py.
@@ -537,11 +555,25 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
     FMX_HIP(hipGetLastError());                                                 \
   } while (0)
 
+// Same, one 64-lane block.
+#define FMX_DISPATCH1(h, KERNEL, ...)                                           \
+  do {                                                                          \
+    if ((h)->line_fmt == kFmtOcc)                                               \
+      KERNEL<OccE><<<1, 64, 0, st>>>(__VA_ARGS__);                              \
+    else if ((h)->line_fmt == kFmtLine32)                                       \
+      KERNEL<WM<Line32>><<<1, 64, 0, st>>>(__VA_ARGS__);                        \
+    else if ((h)->line_fmt == kFmtLine32W)                                      \
+      KERNEL<WM<Line32W>><<<1, 64, 0, st>>>(__VA_ARGS__);                       \
+    else                                                                        \
+      KERNEL<WM<Line64>><<<1, 64, 0, st>>>(__VA_ARGS__);                        \
+    FMX_HIP(hipGetLastError());                                                 \
+  } while (0)
+
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^28, max(4096, n/32)) entries (8 B each, 16 B in wide indexes:
-// at most n/4 resp. n/2 bytes, the order of the sampled SA); none when k < 2.
-// DNA: k = 13 at 4 GB, k = 14 from 8.6 GB on.  Entries are (sp, ep) as 2 x u32, or
+// sigma^k <= min(2^28, max(4096, n/8)) entries (8 B each, 16 B in wide indexes:
+// at most n resp. 2n bytes, capped at 2 resp. 4 GiB); none when k < 2.
+// DNA: k = 11 at 100 MB, k = 14 from 2.1 GB on.  Entries are (sp, ep) as 2 x u32, or
 // 2 x u64 in wide indexes.  CS_FM_PREFIX_K overrides k (0 = off).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
@@ -560,7 +592,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     }
   }
   if (sigma == 0) return CS_OK;
-  uint64_t cap = n / 32 > 4096 ? n / 32 : 4096;
+  uint64_t cap = n / 8 > 4096 ? n / 8 : 4096;
   if (cap > (1ull << 28)) cap = 1ull << 28;
   uint32_t k = 0;
   uint64_t entries = 1;
@@ -609,6 +641,12 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
                        uint64_t npat, uint64_t* d_out, hipStream_t st) {
   if (!npat) return CS_OK;
   FMX_DISPATCH(h, k_count, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat, d_out);
+  return CS_OK;
+}
+
+cs_status launch_count_one(const cs_fm_index* h, const OnePattern& p, uint64_t* out_host,
+                           hipStream_t st) {
+  FMX_DISPATCH1(h, k_count_one, h->dev(), p, out_host);
   return CS_OK;
 }
 
