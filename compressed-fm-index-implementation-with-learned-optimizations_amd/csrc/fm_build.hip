@@ -397,6 +397,155 @@ cs_status build_occ(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_in
   return CS_OK;
 }
 
+// ---- walk lines (fm_device.hpp WalkLine / WalkLineW) ----
+// position marks: bit isa[k] for every sampled text position k*stride
+__global__ void k_mark_positions(const void* __restrict__ isa, uint64_t nisa, uint32_t wide,
+                                 unsigned int* __restrict__ bits) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nisa; k += stride) {
+    const uint64_t r = wide ? static_cast<const uint64_t*>(isa)[k] : static_cast<const uint32_t*>(isa)[k];
+    atomicOr(&bits[r >> 5], 1u << (r & 31));
+  }
+}
+
+// One thread per walk line: codes (rare symbols as code 0), marks (from the bitmap,
+// or row % stride == 0 when bits == null), per-line counts of codes 0..2 and marks.
+template <class W>
+__global__ void k_walk_pack(const uint8_t* __restrict__ bwt, uint64_t n, CodeMap map, uint64_t nw,
+                            const unsigned int* __restrict__ bits, uint32_t stride,
+                            uint32_t* __restrict__ lines, uint8_t* __restrict__ cnt) {
+  __shared__ uint8_t code[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) code[i] = map.c[i];
+  __syncthreads();
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nw; q += gs) {
+    const uint64_t a = q * W::kRows;
+    uint64_t codes0 = 0, codes1 = 0, marks = 0;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, cm = 0;
+    for (uint32_t r = 0; r < W::kRows && a + r < n; ++r) {
+      const uint64_t row = a + r;
+      uint32_t k = code[bwt[row]];
+      if (k == kNoCode) k = 0;
+      const bool mk = bits ? ((bits[row >> 5] >> (row & 31)) & 1u) : (row % stride == 0);
+      if (r < 32) codes0 |= (uint64_t)k << (2 * r);
+      else codes1 |= (uint64_t)k << (2 * (r - 32));
+      marks |= (uint64_t)mk << r;
+      c0 += k == 0;
+      c1 += k == 1;
+      c2 += k == 2;
+      cm += mk;
+    }
+    uint32_t* L = lines + q * 8;
+    if (W::kRows == 42) {  // WalkLine
+      const uint64_t hi = codes1 | (marks << 20);
+      L[4] = (uint32_t)codes0;
+      L[5] = (uint32_t)(codes0 >> 32);
+      L[6] = (uint32_t)hi;
+      L[7] = (uint32_t)(hi >> 32);
+    } else {  // WalkLineW
+      L[4] = 0;
+      L[5] = (uint32_t)codes0;
+      L[6] = (uint32_t)(codes0 >> 32);
+      L[7] = (uint32_t)marks;
+    }
+    cnt[q] = (uint8_t)c0;
+    cnt[nw + q] = (uint8_t)c1;
+    cnt[2 * nw + q] = (uint8_t)c2;
+    cnt[3 * nw + q] = (uint8_t)cm;
+  }
+}
+
+// field j (occ of code 0..2, 3 = marks) of every walk line = base[q]
+template <class W>
+__global__ void k_walk_base(uint32_t* __restrict__ lines, const uint64_t* __restrict__ base,
+                            uint64_t nw, int j) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nw; q += gs) {
+    const uint64_t b = base[q];
+    lines[q * 8 + j] = (uint32_t)b;
+    if (W::kRows != 42) reinterpret_cast<uint8_t*>(lines)[q * 32 + 16 + j] = (uint8_t)(b >> 32);
+  }
+}
+
+// position samples in mark order: wssa[mark_rank(isa[k])] = k * stride
+template <class W, class SampleT>
+__global__ void k_walk_samples(const SampleT* __restrict__ isa, uint64_t nisa, uint32_t stride,
+                               const void* __restrict__ lines, SampleT* __restrict__ wssa) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nisa; k += gs) {
+    uint64_t q;
+    uint32_t o;
+    W::locate((uint64_t)isa[k], q, o);
+    typename W::Raw v;
+    W::load(lines, q, v);
+    wssa[W::mark_rank(v, o)] = (SampleT)(k * stride);
+  }
+}
+
+template <class W>
+cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool pos_marks,
+                       cs_fm_index* h, hipStream_t st) {
+  const uint64_t nw = n / W::kRows + 1;
+  h->nwalk = nw;
+  FMX_HIP(hipMalloc(&h->d_walk, nw * W::kBytes));
+  FMX_HIP(hipMemsetAsync(h->d_walk, 0, nw * W::kBytes, st));
+  DevBuf bits, cnt, base, tmp;
+  if (pos_marks) {
+    const uint64_t words = (n >> 5) + 1;
+    FMX_HIP(bits.alloc(words * 4));
+    FMX_HIP(hipMemsetAsync(bits.p, 0, words * 4, st));
+    k_mark_positions<<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
+        h->d_isa, h->nisa, h->wide ? 1u : 0u, bits.as<unsigned int>());
+    FMX_HIP(hipGetLastError());
+  }
+  FMX_HIP(cnt.alloc(4 * nw));
+  FMX_HIP(base.alloc(nw * 8));
+  k_walk_pack<W><<<grid_for(nw, kBlk, 16384), kBlk, 0, st>>>(
+      bwt, n, map, nw, pos_marks ? bits.as<unsigned int>() : nullptr, h->stride,
+      static_cast<uint32_t*>(h->d_walk), cnt.as<uint8_t>());
+  FMX_HIP(hipGetLastError());
+  size_t tb = 0;
+  FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint8_t>(), base.as<uint64_t>(), (uint64_t)0,
+                                  nw, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(tmp.alloc(tb));
+  for (int j = 0; j < 4; ++j) {
+    size_t t2 = tb;
+    FMX_HIP(rocprim::exclusive_scan(tmp.p, t2, cnt.as<uint8_t>() + (uint64_t)j * nw,
+                                    base.as<uint64_t>(), (uint64_t)0, nw,
+                                    rocprim::plus<uint64_t>(), st));
+    k_walk_base<W><<<grid_for(nw, kBlk, 16384), kBlk, 0, st>>>(static_cast<uint32_t*>(h->d_walk),
+                                                              base.as<uint64_t>(), nw, j);
+    FMX_HIP(hipGetLastError());
+  }
+  if (pos_marks) {
+    FMX_HIP(hipMalloc(&h->d_wssa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
+    if (h->wide)
+      k_walk_samples<W, uint64_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
+          static_cast<const uint64_t*>(h->d_isa), h->nisa, h->stride, h->d_walk,
+          static_cast<uint64_t*>(h->d_wssa));
+    else
+      k_walk_samples<W, uint32_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
+          static_cast<const uint32_t*>(h->d_isa), h->nisa, h->stride, h->d_walk,
+          static_cast<uint32_t*>(h->d_wssa));
+    FMX_HIP(hipGetLastError());
+  }
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+// Walk lines for the occurrence engine.  Position marks need LF to be one n-cycle
+// (lf_exact) so that every walk ends at a sampled text position; otherwise the
+// reference's row marks (row % stride == 0) keep its overrun behaviour.
+cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
+                     hipStream_t st) {
+  bool pos_marks = h->lf_exact;
+  if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
+    if (std::string(e) == "row") pos_marks = false;
+  h->walk_marks = pos_marks ? 2u : 1u;
+  return h->wide ? build_walk_t<WalkLineW>(bwt, n, map, pos_marks, h, st)
+                 : build_walk_t<WalkLine>(bwt, n, map, pos_marks, h, st);
+}
+
 cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st) {
   if (n == 0) return CS_OK;
   if (n >= (1ull << 32)) {
@@ -556,6 +705,14 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   }
   plog.mark("suffix array + bwt + ssa");
 
+  if (n) {  // unique smallest last symbol: LF is one n-cycle, suffix order = rotation order
+    uint8_t last = 0;
+    FMX_HIP(hipMemcpy(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost));
+    int smallest = 0;
+    while (smallest < 256 && hist[smallest] == 0) ++smallest;
+    h->lf_exact = hist[last] == 1 && last == smallest;
+  }
+
   // --- rank structure: occurrence lines (<= 4 frequent symbols) or the wavelet
   //     matrix levels as rank lines ---
   CodeMap occ_map;
@@ -573,6 +730,13 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     std::memcpy(T.occ_sym, occ_sym, sizeof T.occ_sym);
     cs_status os = build_occ(bwt.as<uint8_t>(), n, occ_map, h, st);
     if (os != CS_OK) return os;
+    bool walk = true;
+    if (const char* e = std::getenv("CS_FM_WALK"))  // "0": walk over the occurrence lines
+      walk = std::atoi(e) != 0;
+    if (walk) {
+      os = build_walk(bwt.as<uint8_t>(), n, occ_map, h, st);
+      if (os != CS_OK) return os;
+    }
   } else {
     std::memset(T.occ_code, kNoCode, sizeof T.occ_code);
     h->line_fmt = h->wide ? kFmtLine32W : kFmtLine32;  // Line32 bases are u32
@@ -599,13 +763,6 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     cum += hist[c];
   }
   T.C[256] = cum;
-  if (n) {
-    uint8_t last = 0;
-    FMX_HIP(hipMemcpy(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost));
-    int smallest = 0;
-    while (smallest < 256 && hist[smallest] == 0) ++smallest;
-    h->lf_exact = hist[last] == 1 && last == smallest;
-  }
   for (int l = 0; l <= kLevels; ++l) {
     const int np = 1 << l;
     std::vector<uint64_t> cnt(np, 0);

@@ -90,6 +90,8 @@ void free_index(cs_fm_index* h) {
   if (h->d_err) (void)hipFree(h->d_err);
   if (h->d_ptab) (void)hipFree(h->d_ptab);
   if (h->d_isa) (void)hipFree(h->d_isa);
+  if (h->d_walk) (void)hipFree(h->d_walk);
+  if (h->d_wssa) (void)hipFree(h->d_wssa);
   if (h->scratch.h) (void)hipHostFree(h->scratch.h);
   if (h->scratch.d) (void)hipFree(h->scratch.d);
   delete h;
@@ -202,6 +204,8 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->line_bytes = h->line_bytes;
   out->levels = h->nlevels;
   out->rare_rows = h->line_fmt == kFmtOcc ? h->h_table.exc_n : 0u;
+  out->walk_marks = h->d_walk ? h->walk_marks : 0u;
+  out->walk_bytes = h->d_walk ? h->nwalk * 32 : 0u;
   return CS_OK;
 }
 

@@ -88,6 +88,9 @@ struct DevIndex {
   const void* isa;
   uint64_t nisa;
   uint32_t lf_exact;
+  // Walk lines and the samples they index (WalkLine above); null when absent.
+  const void* walk;
+  const void* wssa;      // sample of each mark, in row order (u32, u64 wide)
 };
 
 // A single pattern passed by value in kernel arguments (k_count_one).
@@ -295,6 +298,94 @@ struct OccLine {
   __device__ static __forceinline__ uint32_t code(const Raw& v, uint32_t o) {
     const uint64_t lo = u64_of(v[1].x, v[1].y), hi = u64_of(v[1].z, v[1].w);
     return (uint32_t)(((o < 32 ? lo : hi) >> (2 * (o & 31))) & 3u);
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Walk lines (locate's LF walk, occurrence engine): one 32-B line gives, for a
+// row, its BWT code, occ(code) at the row (so LF), whether the row holds an SA
+// sample ("mark") and the sample's index (marks before it).  The walk reads one
+// line per step and stops at a mark.  Marks are the rows whose suffix starts at a
+// text position that is a multiple of the stride when LF is one n-cycle
+// (lf_exact: the walk then takes SA[row] mod stride < stride steps, mean
+// (stride-1)/2), else the rows i with i % stride == 0, as the reference's SSA
+// (fm_index.cpp:57-66, 125-153).  Positions are SA values either way, so results
+// are identical.
+//   WalkLine  (n < 2^32): 42 rows.  dwords 0-3 occ(code 0..2), marks before the
+//     line (u32); dwords 4-5 codes of rows 0-31; dwords 6-7 bits 0-19 codes of
+//     rows 32-41, bits 20-61 the 42 marks.
+//   WalkLineW (wide): 32 rows.  dwords 0-3 low 32 bits of occ(code 0..2), marks;
+//     dword 4 their bits 32-39 (byte j); dwords 5-6 codes; dword 7 marks.
+__device__ __forceinline__ uint64_t eq2(uint64_t x, uint32_t c) {  // rows whose code == c
+  constexpr uint64_t k55 = 0x5555555555555555ull;
+  const uint64_t y = x ^ (k55 * c);
+  return ~(y | (y >> 1)) & k55;
+}
+__device__ __forceinline__ uint64_t low_mask(uint32_t bits) {  // bits in [0, 64]
+  return bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+}
+
+struct WalkLine {
+  static constexpr uint32_t kBytes = 32, kRows = 42;
+  using Raw = uint4[2];
+  __device__ static __forceinline__ void locate(uint64_t r, uint64_t& q, uint32_t& o) {
+    const uint32_t r32 = (uint32_t)r;  // r < 2^32
+    const uint32_t qq = r32 / kRows;
+    q = qq;
+    o = r32 - qq * kRows;
+  }
+  __device__ static __forceinline__ void load(const void* lines, uint64_t q, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + q * 2;
+    v[0] = p[0];
+    v[1] = p[1];
+  }
+  __device__ static __forceinline__ uint32_t code(const Raw& v, uint32_t o) {
+    const uint64_t lo = u64_of(v[1].x, v[1].y), hi = u64_of(v[1].z, v[1].w);
+    return (uint32_t)(((o < 32 ? lo : hi) >> (2 * (o & 31))) & 3u);
+  }
+  // occ(code c) at row q*42 + o
+  __device__ static __forceinline__ uint64_t occ(const Raw& v, uint32_t c, uint64_t q, uint32_t o) {
+    const uint64_t lo = u64_of(v[1].x, v[1].y), hi = u64_of(v[1].z, v[1].w) & 0xFFFFFull;
+    const uint32_t in = (uint32_t)(__popcll(eq2(lo, c) & low_mask(2 * (o < 32 ? o : 32))) +
+                                   __popcll(eq2(hi, c) & 0x55555ull & low_mask(o > 32 ? 2 * (o - 32) : 0)));
+    const uint64_t b0 = v[0].x, b1 = v[0].y, b2 = v[0].z;
+    const uint64_t base = c == 0 ? b0 : c == 1 ? b1 : c == 2 ? b2 : q * kRows - b0 - b1 - b2;
+    return base + in;
+  }
+  __device__ static __forceinline__ bool mark(const Raw& v, uint32_t o) {
+    return (u64_of(v[1].z, v[1].w) >> (20 + o)) & 1u;
+  }
+  __device__ static __forceinline__ uint64_t mark_rank(const Raw& v, uint32_t o) {
+    return (uint64_t)v[0].w + __popcll((u64_of(v[1].z, v[1].w) >> 20) & low_mask(o));
+  }
+};
+
+struct WalkLineW {
+  static constexpr uint32_t kBytes = 32, kRows = 32;
+  using Raw = uint4[2];
+  __device__ static __forceinline__ void locate(uint64_t r, uint64_t& q, uint32_t& o) {
+    q = r >> 5;
+    o = (uint32_t)(r & 31);
+  }
+  __device__ static __forceinline__ void load(const void* lines, uint64_t q, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + q * 2;
+    v[0] = p[0];
+    v[1] = p[1];
+  }
+  __device__ static __forceinline__ uint32_t code(const Raw& v, uint32_t o) {
+    return (uint32_t)((u64_of(v[1].y, v[1].z) >> (2 * o)) & 3u);
+  }
+  __device__ static __forceinline__ uint64_t occ(const Raw& v, uint32_t c, uint64_t q, uint32_t o) {
+    const uint32_t in = (uint32_t)__popcll(eq2(u64_of(v[1].y, v[1].z), c) & low_mask(2 * o));
+    const uint32_t hb = v[1].x;
+    const uint64_t b0 = u64_of(v[0].x, hb & 0xFFu), b1 = u64_of(v[0].y, (hb >> 8) & 0xFFu),
+                   b2 = u64_of(v[0].z, (hb >> 16) & 0xFFu);
+    const uint64_t base = c == 0 ? b0 : c == 1 ? b1 : c == 2 ? b2 : q * kRows - b0 - b1 - b2;
+    return base + in;
+  }
+  __device__ static __forceinline__ bool mark(const Raw& v, uint32_t o) { return (v[1].w >> o) & 1u; }
+  __device__ static __forceinline__ uint64_t mark_rank(const Raw& v, uint32_t o) {
+    return u64_of(v[0].w, v[1].x >> 24) + __popc(v[1].w & (uint32_t)low_mask(o));
   }
 };
 

@@ -30,6 +30,10 @@ struct cs_fm_index {
   void* d_isa = nullptr;              // inverse-SA samples (extract)
   uint64_t nisa = 0;
   bool lf_exact = false;              // unique smallest last symbol: LF inverts SA
+  void* d_walk = nullptr;             // walk lines (occurrence engine; WalkLine / WalkLineW)
+  uint64_t nwalk = 0;
+  void* d_wssa = nullptr;             // position samples by mark (lf_exact), else d_ssa is used
+  uint32_t walk_marks = 0;            // 0 no walk lines, 1 row marks, 2 text-position marks
   uint32_t ptab_k = 0, ptab_sigma = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
@@ -76,6 +80,8 @@ struct cs_fm_index {
     d.isa = d_isa;
     d.nisa = nisa;
     d.lf_exact = lf_exact ? 1u : 0u;
+    d.walk = d_walk;
+    d.wssa = d_wssa ? d_wssa : d_ssa;
     return d;
   }
 };

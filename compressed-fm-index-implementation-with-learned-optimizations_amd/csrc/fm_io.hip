@@ -9,11 +9,13 @@
 // Directory layout (all little-endian raw arrays, exactly the HBM images):
 //   cs_fmindex.meta  "key value" lines: format, n, stride, line_bytes, line_bits,
 //                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
-//                    wide, line_fmt, levels, active <symbol> <mask>
+//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa,
+//                    active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
 //   ssa.bin          sampled SA              isa.bin   inverse-SA samples (u32; u64 if wide)
 //   ptab.bin         prefix table (if k > 0) text.bin  the text (if kept, for extract)
+//   walk.bin         walk lines (occurrence engine)  wssa.bin  their position samples
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
@@ -109,6 +111,10 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
     const uint64_t pb = h->ptab_entries() * h->ptab_entry_bytes();
     if ((s = dump_dev(join(d, "ptab.bin"), h->d_ptab, pb, pin.p)) != CS_OK) return s;
   }
+  if (h->d_walk && (s = dump_dev(join(d, "walk.bin"), h->d_walk, h->nwalk * 32, pin.p)) != CS_OK)
+    return s;
+  if (h->d_wssa && (s = dump_dev(join(d, "wssa.bin"), h->d_wssa, h->nisa * sb, pin.p)) != CS_OK)
+    return s;
   {
     FILE* f = std::fopen(join(d, "table.bin").c_str(), "wb");
     if (!f || std::fwrite(&h->h_table, sizeof h->h_table, 1, f) != 1) {
@@ -130,11 +136,12 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   if (!f) return io_fail("cannot write: " + join(d, "cs_fmindex.meta"));
   std::fprintf(f, "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
                   "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
-                  "wide %d\nline_fmt %u\nlevels %u\n",
+                  "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n",
                kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
-               has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels);
+               has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
+               (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0);
   for (int c = 0; c < 256; ++c) std::fprintf(f, "active %d %u\n", c, h->active_levels[c]);
   std::fclose(f);
   return CS_OK;
@@ -225,6 +232,18 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     if (hipMalloc(&h->d_ptab, pb) != hipSuccess)
       return fail(hip_fail(hipGetLastError(), "hipMalloc (ptab)"));
     if ((s = load_dev(join(d, "ptab.bin"), h->d_ptab, pb, pin.p)) != CS_OK) return fail(s);
+  }
+  if (kv["nwalk"]) {
+    h->nwalk = kv["nwalk"];
+    h->walk_marks = (uint32_t)kv["walk_marks"];
+    if (hipMalloc(&h->d_walk, h->nwalk * 32) != hipSuccess)
+      return fail(hip_fail(hipGetLastError(), "hipMalloc (walk)"));
+    if ((s = load_dev(join(d, "walk.bin"), h->d_walk, h->nwalk * 32, pin.p)) != CS_OK) return fail(s);
+  }
+  if (kv["has_wssa"]) {
+    if (hipMalloc(&h->d_wssa, (h->nisa ? h->nisa : 1) * sb) != hipSuccess)
+      return fail(hip_fail(hipGetLastError(), "hipMalloc (wssa)"));
+    if ((s = load_dev(join(d, "wssa.bin"), h->d_wssa, h->nisa * sb, pin.p)) != CS_OK) return fail(s);
   }
   if (hipMemcpy(h->d_table, &h->h_table, sizeof(NodeTable), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(h->d_err, 0xFF, 8) != hipSuccess)

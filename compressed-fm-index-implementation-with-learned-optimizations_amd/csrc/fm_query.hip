@@ -445,6 +445,75 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
   }
 }
 
+// The same walk over walk lines (occurrence engine, fm_device.hpp WalkLine): one
+// line per step gives the mark, the sample index and LF.
+__device__ __forceinline__ uint64_t wssa_at(const DevIndex& ix, uint64_t k) {
+  return ix.wide ? static_cast<const uint64_t*>(ix.wssa)[k] : static_cast<const uint32_t*>(ix.wssa)[k];
+}
+
+template <class W>
+__global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t* __restrict__ rows,
+                                                     uint64_t total, uint64_t chunk,
+                                                     uint64_t* __restrict__ out,
+                                                     unsigned long long* __restrict__ err) {
+  __shared__ NodeTable T;
+  __shared__ unsigned long long next;
+  const uint64_t a = blockIdx.x * chunk;
+  const uint64_t end = (a + chunk < total) ? a + chunk : total;
+  load_table(T, ix.table);
+  if (threadIdx.x == 0) next = a;
+  __syncthreads();
+  if (a >= total) return;
+  const uint64_t n = ix.n;
+  uint64_t j = 0, pos = 0, steps = 0;
+  bool active = false, drained = false;
+  for (;;) {
+    if (!active && !drained) {
+      j = atomicAdd(&next, 1ull);
+      if (j < end) {
+        pos = rows[j];
+        steps = 0;
+        active = true;
+      } else {
+        drained = true;
+      }
+    }
+    if (!__any(active)) break;
+    if (active) {
+      uint64_t q;
+      uint32_t o;
+      W::locate(pos, q, o);
+      typename W::Raw v;
+      W::load(ix.walk, q, v);
+      const bool mk = W::mark(v, o);
+      if (mk || steps >= n) {  // fm_index.cpp:130 loop condition, :136-138 overrun first
+        if (steps >= n) {
+          atomicMin(err, (unsigned long long)j);
+        } else {
+          const uint64_t s = wssa_at(ix, W::mark_rank(v, o)) + steps;  // :147-153
+          out[j] = s >= n ? s - n : s;
+        }
+        active = false;
+      } else {  // LF = C[c] + occ(c, pos) from the same line (OccE::lf)
+        const uint32_t code = W::code(v, o);
+        uint32_t c = T.occ_sym[code];
+        uint64_t r = W::occ(v, code, q, o);
+        if (code == 0 && T.exc_n) {
+          const uint32_t e = exc_before(T, pos);
+          if (e < T.exc_n && T.exc_row[e] == pos) {
+            c = T.exc_sym[e];
+            r = exc_rank(T, c, pos);
+          } else {
+            r -= e;
+          }
+        }
+        pos = T.C[c] + r;
+        ++steps;
+      }
+    }
+  }
+}
+
 // ---- building-block kernels for parity tests ----
 template <class F>
 __global__ void k_level_rank1(DevIndex ix, int level, const uint64_t* __restrict__ pos, uint64_t k,
@@ -697,7 +766,10 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   unsigned long long* err = reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
-  if (h->line_fmt == kFmtOcc) {
+  if (h->d_walk) {
+    if (h->wide) k_walk_lines<WalkLineW><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk_lines<WalkLine><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  } else if (h->line_fmt == kFmtOcc) {
     if (pow2) k_walk<OccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<OccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else if (h->line_fmt == kFmtLine32) {

@@ -72,6 +72,9 @@ typedef struct cs_fm_info {
   uint32_t line_bytes;     /* bytes per rank / occurrence line (32 or 64) */
   uint32_t levels;         /* rank-line sequences: 8 wavelet levels, or 1 */
   uint32_t rare_rows;      /* occurrence lines: BWT rows of rare symbols kept in the table */
+  uint32_t walk_marks;     /* locate walk lines: 0 none, 1 sampled rows (row % stride == 0),
+                              2 sampled text positions (needs a unique smallest terminator) */
+  uint64_t walk_bytes;
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -26,6 +26,8 @@ ENGINE_VARIANTS = {
     # the wavelet matrix in 32-B lines (Line32)
     "auto": {},
     "auto_noprefix": {"CS_FM_PREFIX_K": "0"},       # prefix table off
+    "auto_rowmarks": {"CS_FM_WALK_MARKS": "row"},   # walk lines with the reference's row samples
+    "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # wavelet matrix for every text
     "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
     # the n >= 2^32 engines at small n: u64 samples/table, bucketed sorter, and
@@ -34,7 +36,7 @@ ENGINE_VARIANTS = {
     "wide_wavelet": {"CS_FM_WIDE": "1", "CS_FM_ENGINE": "wavelet"},
 }
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
-          "CS_FM_ENGINE")
+          "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -147,14 +149,20 @@ def test_engine_choice(built):
     """Occurrence lines iff <= 4 symbols hold all but at most 128 BWT rows (and the
     wavelet matrix is not forced); rare rows are listed in the node table."""
     forced = os.environ.get("CS_FM_ENGINE") == "wavelet"
-    want = {"dna_5k": (1, 1), "banana": (1, 0), "single": (1, 0), "rare_N_41": (1, 41),
-            "rare_128": (1, 128), "rare_129": (0, 0), "bytes_5k": (0, 0),
-            "rare_both_ends": (1, 8)}
-    for name, (engine, rare) in want.items():
+    # (engine, rare rows, walk marks: 2 = text positions when the text ends in a unique
+    # smallest symbol, 1 = the reference's sampled rows)
+    want = {"dna_5k": (1, 1, 2), "banana": (1, 0, 2), "single": (1, 0, 2),
+            "rare_N_41": (1, 41, 2), "rare_128": (1, 128, 2), "rare_129": (0, 0, 0),
+            "bytes_5k": (0, 0, 0), "rare_both_ends": (1, 8, 1), "abab_noterm": (1, 0, 1)}
+    for name, (engine, rare, marks) in want.items():
         info = built(name)[0].info()
         if forced:
-            engine, rare = 0, 0
-        assert (info.engine, info.rare_rows) == (engine, rare), name
+            engine, rare, marks = 0, 0, 0
+        if os.environ.get("CS_FM_WALK") == "0":
+            marks = 0
+        elif os.environ.get("CS_FM_WALK_MARKS") == "row" and marks:
+            marks = 1
+        assert (info.engine, info.rare_rows, info.walk_marks) == (engine, rare, marks), name
         assert info.levels == (1 if engine else 8) and info.line_bytes in (32, 64)
 
 
