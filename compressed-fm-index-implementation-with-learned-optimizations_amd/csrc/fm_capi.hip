@@ -64,11 +64,11 @@ cs_status scratch_ready(const cs_fm_index* h) {
 
 // Stage a host pattern batch into HBM.
 struct StagedBatch {
-  DevBuf pats, offs;
+  StreamBuf pats, offs;
   cs_status load(const uint8_t* p, const uint64_t* o, uint64_t npat, hipStream_t st) {
     const uint64_t bytes = o[npat] - o[0];
-    FMX_HIP(pats.alloc(bytes + 16));
-    FMX_HIP(offs.alloc((npat + 1) * 8));
+    FMX_HIP(pats.alloc(bytes + 16, st));
+    FMX_HIP(offs.alloc((npat + 1) * 8, st));
     if (bytes) FMX_HIP(hipMemcpyAsync(pats.p, p + o[0], bytes, hipMemcpyHostToDevice, st));
     if (o[0] == 0) {
       FMX_HIP(hipMemcpyAsync(offs.p, o, (npat + 1) * 8, hipMemcpyHostToDevice, st));
@@ -282,8 +282,8 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   StagedBatch b;
   s = b.load(pats, offs, npat, st);
   if (s != CS_OK) return s;
-  DevBuf d_out;
-  FMX_HIP(d_out.alloc(npat * 8));
+  StreamBuf d_out;
+  FMX_HIP(d_out.alloc(npat * 8, st));
   s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
   if (s != CS_OK) return s;
   FMX_HIP(hipMemcpyAsync(out_counts, d_out.p, npat * 8, hipMemcpyDeviceToHost, st));
@@ -354,9 +354,9 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
   StagedBatch b;
   s = b.load(pats, offs, npat, st);
   if (s != CS_OK) return s;
-  DevBuf d_sp, d_oo;
-  FMX_HIP(d_sp.alloc(npat * 8));
-  FMX_HIP(d_oo.alloc((npat + 1) * 8));
+  StreamBuf d_sp, d_oo;
+  FMX_HIP(d_sp.alloc(npat * 8, st));
+  FMX_HIP(d_oo.alloc((npat + 1) * 8, st));
   s = launch_locate_ranges(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
                            d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), total, st);
   if (s != CS_OK) return s;
@@ -371,8 +371,8 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
     set_error("null output buffer");
     return CS_ERR_INVALID;
   }
-  DevBuf d_pos;
-  FMX_HIP(d_pos.alloc(*total * 8));
+  StreamBuf d_pos;
+  FMX_HIP(d_pos.alloc(*total * 8, st));
   s = launch_locate_walk(h, d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), npat, *total,
                          d_pos.as<uint64_t>(), st);
   if (s != CS_OK) return s;

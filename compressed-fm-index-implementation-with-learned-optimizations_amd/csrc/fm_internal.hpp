@@ -149,6 +149,28 @@ struct DevBuf {
   void release() { if (p) (void)hipFree(p); p = nullptr; }
 };
 
+// Stream-ordered scratch for the query paths: hipMallocAsync / hipFreeAsync on the
+// launch stream, so a call allocates and frees without a device synchronisation
+// and the device's default pool keeps the memory cached between calls.
+void keep_pool(int device);
+struct StreamBuf {
+  void* p = nullptr;
+  hipStream_t st = nullptr;
+  StreamBuf() = default;
+  StreamBuf(const StreamBuf&) = delete;
+  StreamBuf& operator=(const StreamBuf&) = delete;
+  ~StreamBuf() { if (p) (void)hipFreeAsync(p, st); }
+  hipError_t alloc(size_t bytes, hipStream_t s) {
+    if (p) (void)hipFreeAsync(p, st);
+    p = nullptr;
+    st = s;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) keep_pool(dev);
+    return hipMallocAsync(&p, bytes ? bytes : 16, s);
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
 inline unsigned grid_for(uint64_t work, unsigned block, unsigned cap = 1u << 20) {
   uint64_t g = (work + block - 1) / block;
   if (g < 1) g = 1;

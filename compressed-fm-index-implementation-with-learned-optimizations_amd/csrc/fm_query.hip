@@ -23,6 +23,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "fm_internal.hpp"
 
@@ -398,12 +399,16 @@ __device__ __forceinline__ uint64_t sample_index(const DevIndex& ix, uint64_t ro
   return row / ix.stride;
 }
 
-// Persistent LF walk (fm_index.cpp:125-153).  Block b owns rows [b*chunk, ...).
+// Persistent LF walk (fm_index.cpp:125-153).  Block b owns rows [b*chunk, ...);
+// lanes pull rows from an LDS counter and cycle FETCH -> WALK -> SAMPLE as in
+// k_walk_lines below (the SSA read of a finishing lane does not add a round trip
+// to its wave's LF step).
 template <class E, bool POW2>
 __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __restrict__ rows,
                                                uint64_t total, uint64_t chunk,
                                                uint64_t* __restrict__ out,
                                                unsigned long long* __restrict__ err) {
+  enum : uint32_t { kFetch = 0, kWalk = 1, kSample = 2, kDone = 3 };
   __shared__ NodeTable T;
   __shared__ unsigned long long next;
   const uint64_t a = blockIdx.x * chunk;
@@ -414,29 +419,33 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
   if (a >= total) return;
   const uint64_t n = ix.n;
   uint64_t j = 0, pos = 0, steps = 0;
-  bool active = false, drained = false;
+  uint32_t phase = kFetch;
   for (;;) {
-    if (!active && !drained) {
+    if (phase == kFetch) {
       j = atomicAdd(&next, 1ull);
-      if (j < end) {
-        pos = rows[j];
-        steps = 0;
-        active = true;
-      } else {
-        drained = true;
-      }
+      if (j >= end) phase = kDone;
     }
-    if (!__any(active)) break;
-    if (active) {
+    if (!__any(phase != kDone)) break;
+    uint64_t row = 0, smp = 0;
+    if (phase == kFetch) row = rows[j];
+    if (phase == kSample) smp = ssa_at(ix, sample_index<POW2>(ix, pos));
+    if (phase == kFetch) {
+      pos = row;
+      steps = 0;
+      phase = kWalk;
+    } else if (phase == kSample) {
+      const uint64_t s = smp + steps;  // :147-153
+      out[j] = s >= n ? s - n : s;
+      phase = kFetch;
+    } else if (phase == kWalk) {
       // loop condition of fm_index.cpp:130: stop at a sampled row or after n steps
       if (is_sampled<POW2>(ix, pos) || steps >= n) {
         if (steps >= n) {
           atomicMin(err, (unsigned long long)j);  // fm_index.cpp:136-138
+          phase = kFetch;
         } else {
-          const uint64_t s = ssa_at(ix, sample_index<POW2>(ix, pos)) + steps;  // :147-153
-          out[j] = s >= n ? s - n : s;
+          phase = kSample;
         }
-        active = false;
       } else {
         pos = E::lf(ix, T, pos);
         ++steps;
@@ -456,6 +465,12 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
                                                      uint64_t total, uint64_t chunk,
                                                      uint64_t* __restrict__ out,
                                                      unsigned long long* __restrict__ err) {
+  // Each lane cycles FETCH (row from the block's slice) -> WALK (one line per LF
+  // step) -> SAMPLE (the mark's SA sample) -> FETCH.  Every loop iteration issues
+  // at most ONE dependent load per lane, whatever its phase, so a wave waits one
+  // memory round trip per iteration even when some of its lanes are starting or
+  // finishing a walk.
+  enum : uint32_t { kFetch = 0, kWalk = 1, kSample = 2, kDone = 3 };
   __shared__ NodeTable T;
   __shared__ unsigned long long next;
   const uint64_t a = blockIdx.x * chunk;
@@ -465,35 +480,38 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
   __syncthreads();
   if (a >= total) return;
   const uint64_t n = ix.n;
-  uint64_t j = 0, pos = 0, steps = 0;
-  bool active = false, drained = false;
+  uint64_t j = 0, pos = 0, steps = 0, sidx = 0;
+  uint32_t phase = kFetch;
   for (;;) {
-    if (!active && !drained) {
+    if (phase == kFetch) {
       j = atomicAdd(&next, 1ull);
-      if (j < end) {
-        pos = rows[j];
-        steps = 0;
-        active = true;
-      } else {
-        drained = true;
-      }
+      if (j >= end) phase = kDone;
     }
-    if (!__any(active)) break;
-    if (active) {
-      uint64_t q;
-      uint32_t o;
+    if (!__any(phase != kDone)) break;
+    // ---- issue this iteration's load ----
+    uint64_t row = 0, smp = 0, q = 0;
+    uint32_t o = 0;
+    typename W::Raw v;
+    if (phase == kFetch) row = rows[j];
+    if (phase == kWalk) {
       W::locate(pos, q, o);
-      typename W::Raw v;
       W::load(ix.walk, q, v);
-      const bool mk = W::mark(v, o);
-      if (mk || steps >= n) {  // fm_index.cpp:130 loop condition, :136-138 overrun first
-        if (steps >= n) {
+    }
+    if (phase == kSample) smp = wssa_at(ix, sidx);
+    // ---- consume ----
+    if (phase == kFetch) {
+      pos = row;
+      steps = 0;
+      phase = kWalk;
+    } else if (phase == kWalk) {
+      if (W::mark(v, o) || steps >= n) {  // fm_index.cpp:130 loop condition
+        if (steps >= n) {                  // :136-138, checked first
           atomicMin(err, (unsigned long long)j);
+          phase = kFetch;
         } else {
-          const uint64_t s = wssa_at(ix, W::mark_rank(v, o)) + steps;  // :147-153
-          out[j] = s >= n ? s - n : s;
+          sidx = W::mark_rank(v, o);
+          phase = kSample;
         }
-        active = false;
       } else {  // LF = C[c] + occ(c, pos) from the same line (OccE::lf)
         const uint32_t code = W::code(v, o);
         uint32_t c = T.occ_sym[code];
@@ -510,6 +528,10 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
         pos = T.C[c] + r;
         ++steps;
       }
+    } else if (phase == kSample) {
+      const uint64_t s = smp + steps;  // :147-153
+      out[j] = s >= n ? s - n : s;
+      phase = kFetch;
     }
   }
 }
@@ -731,14 +753,14 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
                                hipStream_t st) {
-  DevBuf cnt, tmp;
-  FMX_HIP(cnt.alloc((npat + 1) * 8));
+  StreamBuf cnt, tmp;
+  FMX_HIP(cnt.alloc((npat + 1) * 8, st));
   FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,
                d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
   size_t tb = 0;
   FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint64_t>(), d_out_offs, (uint64_t)0,
                                   npat + 1, rocprim::plus<uint64_t>(), st));
-  FMX_HIP(tmp.alloc(tb));
+  FMX_HIP(tmp.alloc(tb, st));
   FMX_HIP(rocprim::exclusive_scan(tmp.p, tb, cnt.as<uint64_t>(), d_out_offs, (uint64_t)0,
                                   npat + 1, rocprim::plus<uint64_t>(), st));
   FMX_HIP(hipMemcpyAsync(total, d_out_offs + npat, 8, hipMemcpyDeviceToHost, st));
@@ -750,8 +772,8 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st) {
   if (!total) return CS_OK;
-  DevBuf rows;
-  FMX_HIP(rows.alloc(total * 8));
+  StreamBuf rows;
+  FMX_HIP(rows.alloc(total * 8, st));
   k_expand_rows<<<grid_for(npat, kBlk, 65536), kBlk, 0, st>>>(d_sp, d_out_offs, npat,
                                                               rows.as<uint64_t>());
   FMX_HIP(hipGetLastError());
@@ -783,9 +805,22 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
     else k_walk<WM<Line64>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   }
   FMX_HIP(hipGetLastError());
-  // rows must outlive the kernel: synchronise before DevBuf frees it
-  FMX_HIP(hipStreamSynchronize(st));
-  return CS_OK;
+  return CS_OK;  // rows are freed in stream order after the walk
+}
+
+void keep_pool(int device) {
+  static std::once_flag once[64];
+  if (device < 0 || device >= 64) return;
+  std::call_once(once[device], [device] {
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    uint64_t keep = ~0ull;  // never trim the pool back on synchronisation
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    (void)hipGetLastError();
+  });
 }
 
 cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, uint64_t npat,

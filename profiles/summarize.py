@@ -30,7 +30,8 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("k_count_bytes", "k_count", "k_walk", "k_occ_pack", "k_occ_base", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt_ssa", "k_bwt",
+    for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_lines", "k_walk_pack",
+              "k_walk_base", "k_walk_samples", "k_walk", "k_occ_pack", "k_occ_base", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt_ssa", "k_bwt",
               "k_build_ptab",
               "k_partition", "k_pack_level", "k_init_keys", "k_double_keys", "k_heads",
               "k_scatter_rank", "k_bwt_ssa", "k_hist", "k_text", "k_patterns", "k_indep", "k_chain"):
