@@ -7,8 +7,10 @@ terminator, SURVEY.md §8(d): splitmix64 seed 42), Q_text 20-mers (substrings at
 splitmix64(4242) positions).  One step = one batched count() launch over a batch
 of --batch patterns per GPU, inputs resident in HBM.  Multi-GPU: one process per
 GPU, index replicated (built per GPU), query stream sharded in contiguous ranges
-(weak scaling: --batch per GPU), per-shard counts gathered to rank 0 over RCCL
-inside the timed step.
+(weak scaling: --batch per GPU).  Queries are independent, so the timed step has
+no data-path collective: each rank's counts stay with its shard (barrier + max
+over ranks around the K steps).  --gather adds SURVEY §8(e)'s gather of the
+counts to rank 0 over RCCL, double-buffered behind the next step's count.
 
 Extra fields on the JSON line:
   roofline     the count kernel against HBM: achieved = algorithmic bytes per
@@ -65,6 +67,8 @@ def main():
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--locate-batch", type=int, default=12_500_000,
                     help="patterns of the batch timed through locate() (N=1 only; 0 = skip)")
+    ap.add_argument("--gather", action="store_true",
+                    help="gather every step's counts to rank 0 (RCCL), overlapped with the next count")
     ap.add_argument("--prefix-k", type=int, default=None,
                     help="prefix-table depth override (0 = off; default automatic)")
     args = ap.parse_args()
@@ -112,9 +116,11 @@ def main():
     offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
     pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, pats.data_ptr(),
                               offs.data_ptr(), sh)
-    # counts land in double-buffered shards; for N > 1 the gather of step k overlaps
-    # the count of step k+1 (shard.PipelinedGather)
-    pg = shard.PipelinedGather(B, world, rank, torch.int64, dev)
+    # counts land in double-buffered shards; with --gather (N > 1) the gather of step
+    # k to rank 0 overlaps the count of step k+1 (shard.PipelinedGather), otherwise
+    # each rank keeps its shard's counts (no collective in the data path)
+    coll = args.gather and world > 1
+    pg = shard.PipelinedGather(B, world if coll else 1, rank if coll else 0, torch.int64, dev)
 
     # algorithmic bytes per launch, counted by the engine's measurement twin of the
     # count kernel (cs_fm_count_bytes_device): per backward-search step, the distinct
@@ -202,6 +208,9 @@ def main():
                        "batch_per_gpu": B, "global_batch": B * world, "m": m,
                        "ssa_stride": args.ssa_stride, "parallelism": "dp%d" % world,
                        "index": "replicated per GPU", "workload_key": wl,
+                       "collective": "gather of counts to rank 0 (%s), overlapped"
+                       % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) if coll
+                       else "none (independent query shards)",
                        "engine": "occurrence lines" if info.engine == 1 else
                        "wavelet matrix (%d-B rank lines)" % info.line_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
