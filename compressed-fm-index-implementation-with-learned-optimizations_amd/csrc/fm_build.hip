@@ -327,6 +327,184 @@ __global__ void k_occ_base(uint32_t* __restrict__ lines, const uint64_t* __restr
   }
 }
 
+// ---- quaternary wavelet matrix (fm_query.hip QWM) ----
+__global__ void k_qcodes(const uint8_t* __restrict__ bwt, uint64_t n, CodeMap map,
+                         uint8_t* __restrict__ out) {
+  __shared__ uint8_t code[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) code[i] = map.c[i];
+  __syncthreads();
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += gs)
+    out[i] = code[bwt[i]];
+}
+
+// One thread per occurrence line of a level: digit (cur >> shift) & 3 of 64 rows,
+// per-line counts of digits 0..2.
+__global__ void k_qwm_pack(const uint8_t* __restrict__ cur, uint64_t n, int shift, uint64_t nl,
+                           uint32_t* __restrict__ lines, uint8_t* __restrict__ cnt) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nl; q += gs) {
+    const uint64_t a = q << 6;
+    uint32_t w[4] = {0, 0, 0, 0};
+    uint32_t c0 = 0, c1 = 0, c2 = 0;
+    for (int r = 0; r < 64 && a + r < n; ++r) {
+      const uint32_t d = (cur[a + r] >> shift) & 3u;
+      w[r >> 4] |= d << (2 * (r & 15));
+      c0 += d == 0;
+      c1 += d == 1;
+      c2 += d == 2;
+    }
+    reinterpret_cast<uint4*>(lines)[q * 2 + 1] = make_uint4(w[0], w[1], w[2], w[3]);
+    cnt[q] = (uint8_t)c0;
+    cnt[nl + q] = (uint8_t)c1;
+    cnt[2 * nl + q] = (uint8_t)c2;
+  }
+}
+
+struct QZ {
+  uint64_t z[4];
+};
+
+// stable 4-way partition by the level's digit: nxt[Z[d] + occ(d, i)] = cur[i]
+__global__ void k_qwm_partition(const uint8_t* __restrict__ cur, uint64_t n, int shift,
+                                const void* __restrict__ lines, QZ Z, uint8_t* __restrict__ nxt) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += gs) {
+    const uint8_t v = cur[i];
+    const uint32_t d = (v >> shift) & 3u;
+    OccLine::Raw L;
+    const uint64_t q = i >> 6;
+    OccLine::load(lines, q, L);
+    nxt[Z.z[d] + OccLine::base(L, d, q) + OccLine::prefix(L, d, (uint32_t)(i & 63))] = v;
+  }
+}
+
+// R of every pure node: occ_l(d, S) at its start
+__global__ void k_qnode_rank(const void* __restrict__ lines, uint64_t nl,
+                             const NodeTable* __restrict__ T, uint64_t* __restrict__ R) {
+  for (int l = 0; l < (int)T->qlevels; ++l) {
+    const int np = 1 << (2 * l);
+    for (int x = threadIdx.x; x < np; x += blockDim.x) {
+      const int nid = qnode_id(l, (uint32_t)x);
+      uint64_t r = 0;
+      if (T->flags[nid] & kPure) {
+        const uint32_t d = (T->flags[nid] >> 2) & 3u;
+        const uint64_t S = T->S[nid], q = S >> 6;
+        OccLine::Raw v;
+        OccLine::load(static_cast<const uint8_t*>(lines) + (uint64_t)l * nl * OccLine::kBytes, q, v);
+        r = OccLine::base(v, d, q) + OccLine::prefix(v, d, (uint32_t)(S & 63));
+      }
+      R[nid] = r;
+    }
+  }
+}
+
+cs_status build_qwm(const uint8_t* bwt, uint64_t n, const unsigned long long* hist, cs_fm_index* h,
+                    hipStream_t st) {
+  NodeTable& T = h->h_table;
+  CodeMap map;
+  std::memset(map.c, 0, sizeof map.c);
+  uint32_t sigma = 0;
+  std::vector<uint64_t> hc;
+  for (int c = 0; c < 256; ++c)
+    if (hist[c]) {
+      map.c[c] = (uint8_t)sigma;
+      T.qsym[sigma] = (uint8_t)c;
+      hc.push_back(hist[c]);
+      ++sigma;
+    }
+  std::memcpy(T.occ_code, map.c, sizeof T.occ_code);
+  int L = 1;
+  while ((1u << (2 * L)) < sigma) ++L;
+  T.qlevels = (uint32_t)L;
+  h->nlevels = (uint32_t)L;
+  const uint64_t nl = h->nlines;
+  FMX_HIP(hipMalloc(&h->d_lines, (uint64_t)L * nl * OccLine::kBytes));
+  FMX_HIP(hipMemsetAsync(h->d_lines, 0, (uint64_t)L * nl * OccLine::kBytes, st));
+  DevBuf cur, nxt, cnt, base, tmp;
+  FMX_HIP(cur.alloc(n));
+  FMX_HIP(nxt.alloc(n));
+  FMX_HIP(cnt.alloc(3 * nl));
+  FMX_HIP(base.alloc(nl * 8));
+  k_qcodes<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(bwt, n, map, cur.as<uint8_t>());
+  FMX_HIP(hipGetLastError());
+  size_t tb = 0;
+  FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint8_t>(), base.as<uint64_t>(), (uint64_t)0,
+                                  nl, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(tmp.alloc(tb));
+  for (int l = 0; l < L; ++l) {
+    const int shift = 2 * (L - 1 - l);
+    uint32_t* lv = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(h->d_lines) +
+                                               (uint64_t)l * nl * OccLine::kBytes);
+    k_qwm_pack<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(cur.as<uint8_t>(), n, shift, nl, lv,
+                                                          cnt.as<uint8_t>());
+    FMX_HIP(hipGetLastError());
+    uint64_t tot[3];
+    for (int j = 0; j < 3; ++j) {
+      size_t t2 = tb;
+      FMX_HIP(rocprim::exclusive_scan(tmp.p, t2, cnt.as<uint8_t>() + (uint64_t)j * nl,
+                                      base.as<uint64_t>(), (uint64_t)0, nl,
+                                      rocprim::plus<uint64_t>(), st));
+      k_occ_base<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(lv, base.as<uint64_t>(), nl, j);
+      FMX_HIP(hipGetLastError());
+      uint64_t last = 0;
+      uint8_t lc = 0;
+      FMX_HIP(hipMemcpyAsync(&last, base.as<uint64_t>() + nl - 1, 8, hipMemcpyDeviceToHost, st));
+      FMX_HIP(hipMemcpyAsync(&lc, cnt.as<uint8_t>() + (uint64_t)j * nl + nl - 1, 1,
+                             hipMemcpyDeviceToHost, st));
+      FMX_HIP(hipStreamSynchronize(st));
+      tot[j] = last + lc;
+    }
+    QZ Z;
+    Z.z[0] = 0;
+    Z.z[1] = tot[0];
+    Z.z[2] = tot[0] + tot[1];
+    Z.z[3] = tot[0] + tot[1] + tot[2];
+    for (int d = 0; d < 4; ++d) T.qZ[l][d] = Z.z[d];
+    if (l + 1 < L) {
+      k_qwm_partition<<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(cur.as<uint8_t>(), n, shift, lv, Z,
+                                                                nxt.as<uint8_t>());
+      FMX_HIP(hipGetLastError());
+      std::swap(cur.p, nxt.p);
+    }
+  }
+  // node starts (digit-reversed prefix order, as the stable partitions leave them),
+  // purity and leaf starts from the code histogram
+  for (int l = 0; l <= L; ++l) {
+    const int np = 1 << (2 * l);
+    std::vector<uint64_t> cntx(np, 0);
+    for (uint32_t y = 0; y < sigma; ++y) cntx[l ? (y >> (2 * (L - l))) : 0] += hc[y];
+    std::vector<std::pair<uint32_t, int>> ord;
+    for (int x = 0; x < np; ++x) {
+      uint32_t rev = 0;
+      for (int k = 0; k < l; ++k) rev |= ((x >> (2 * k)) & 3u) << (2 * (l - 1 - k));
+      ord.push_back({rev, x});
+    }
+    std::sort(ord.begin(), ord.end());
+    uint64_t sacc = 0;
+    for (auto& e : ord) {
+      const int x = e.second;
+      if (l < L) T.S[qnode_id(l, (uint32_t)x)] = sacc;
+      else T.S8[x] = sacc;
+      sacc += cntx[x];
+    }
+    if (l == L) break;
+    for (int x = 0; x < np; ++x) {
+      int d0 = -1;
+      bool pure = true;
+      for (uint32_t y = 0; y < sigma; ++y) {
+        if ((l ? (y >> (2 * (L - l))) : 0u) != (uint32_t)x) continue;
+        const int d = (int)((y >> (2 * (L - 1 - l))) & 3u);
+        if (d0 < 0) d0 = d;
+        else if (d != d0) pure = false;
+      }
+      T.flags[qnode_id(l, (uint32_t)x)] = pure ? (uint8_t)(kPure | ((d0 < 0 ? 0 : d0) << 2)) : 0;
+    }
+  }
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
 // Occurrence-line engine choice: the (at most) four most frequent symbols get
 // 2-bit codes in symbol order; the rest must hold at most kMaxExc rows.
 bool occ_feasible(const unsigned long long* hist, uint64_t n, CodeMap& map, uint8_t occ_sym[4]) {
@@ -718,9 +896,23 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   CodeMap occ_map;
   uint8_t occ_sym[4] = {0, 0, 0, 0};
   bool occ = occ_feasible(hist, n, occ_map, occ_sym);
-  if (const char* e = std::getenv("CS_FM_ENGINE"))  // "wavelet" forces the wavelet matrix
-    if (std::string(e) == "wavelet") occ = false;
-  if (occ) {
+  bool qwm = !occ && n > 0 && n < (1ull << 40);
+  if (const char* e = std::getenv("CS_FM_ENGINE")) {  // test hooks: force an engine
+    const std::string want(e);
+    if (want == "wavelet") occ = qwm = false;
+    if (want == "qwm" && n > 0 && n < (1ull << 40)) {
+      occ = false;
+      qwm = true;
+    }
+  }
+  if (qwm) {
+    h->line_fmt = kFmtQwm;
+    h->line_bytes = OccLine::kBytes;
+    h->line_bits = OccLine::kRows;
+    h->nlines = (n >> 6) + 1;
+    cs_status qs = build_qwm(bwt.as<uint8_t>(), n, hist, h, st);
+    if (qs != CS_OK) return qs;
+  } else if (occ) {
     h->line_fmt = kFmtOcc;
     h->line_bytes = OccLine::kBytes;
     h->line_bits = OccLine::kRows;
@@ -763,7 +955,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     cum += hist[c];
   }
   T.C[256] = cum;
-  for (int l = 0; l <= kLevels; ++l) {
+  for (int l = 0; l <= kLevels && !qwm; ++l) {  // binary wavelet nodes (QWM set its own)
     const int np = 1 << l;
     std::vector<uint64_t> cnt(np, 0);
     for (int c = 0; c < 256; ++c) cnt[l ? (c >> (8 - l)) : 0] += hist[c];
@@ -795,9 +987,16 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   }
   for (int c = 0; c < 256; ++c) {
     uint32_t m = 0;
-    for (int l = 0; l < kLevels; ++l)
+    for (int l = 0; l < kLevels && !qwm; ++l)
       if (!(T.flags[node_id(l, l ? (c >> (8 - l)) : 0)] & kPure)) m |= 1u << l;
     if (occ) m = T.occ_code[c] != kNoCode ? 1u : 0u;  // one line per occ, none for rare symbols
+    if (qwm) {
+      m = 0;
+      const int L = (int)T.qlevels;
+      const uint32_t x = T.occ_code[c];
+      for (int l = 0; l < L; ++l)
+        if (!(T.flags[qnode_id(l, x >> (2 * (L - l)))] & kPure)) m |= 1u << l;
+    }
     h->active_levels[c] = hist[c] ? m : 0;
   }
   FMX_HIP(hipMalloc(&h->d_table, sizeof(NodeTable)));
@@ -807,6 +1006,10 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     FMX_HIP(dR.alloc(kNodes * 8));
     if (h->line_fmt == kFmtOcc)
       FMX_HIP(hipMemsetAsync(dR.p, 0, kNodes * 8, st));  // wavelet node ranks unused
+    else if (h->line_fmt == kFmtQwm) {
+      FMX_HIP(hipMemsetAsync(dR.p, 0, kNodes * 8, st));
+      k_qnode_rank<<<1, 128, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
+    }
     else if (h->line_fmt == kFmtLine32)
       k_node_rank<Line32><<<1, kBlk, 0, st>>>(h->d_lines, h->nlines, h->d_table, dR.as<uint64_t>());
     else if (h->line_fmt == kFmtLine32W)

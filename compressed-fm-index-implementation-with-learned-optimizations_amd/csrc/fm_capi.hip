@@ -200,7 +200,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->prefix_sigma = h->ptab_sigma;
   out->prefix_bytes = h->ptab_entries() * h->ptab_entry_bytes();
   for (int c = 0; c < 256; ++c) out->prefix_code[c] = h->h_table.code[c];
-  out->engine = h->line_fmt == kFmtOcc ? 1u : 0u;
+  out->engine = h->line_fmt == kFmtOcc ? 1u : h->line_fmt == kFmtQwm ? 2u : 0u;
   out->line_bytes = h->line_bytes;
   out->levels = h->nlevels;
   out->rare_rows = h->line_fmt == kFmtOcc ? h->h_table.exc_n : 0u;

@@ -56,11 +56,23 @@ struct NodeTable {
   uint32_t exc_n;
   uint64_t exc_row[kMaxExc];
   uint8_t exc_sym[kMaxExc];
+  // quaternary wavelet matrix engine (QWM below): occ_code holds each present
+  // symbol's dense code, qsym the inverse; levels; per level the start of each
+  // digit's block in the next level; the node arrays S / R / flags (kPure |
+  // digit << 2) are indexed by qnode_id, S8 by code (leaf starts).
+  uint32_t qlevels;
+  uint64_t qZ[4][4];
+  uint8_t qsym[256];
 };
 constexpr uint8_t kNoCode = 0xFF;
 
 // rank-line formats (cs_fm_index::line_fmt)
-enum LineFmt : uint32_t { kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2, kFmtOcc = 3 };
+enum LineFmt : uint32_t { kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2, kFmtOcc = 3, kFmtQwm = 4 };
+
+// Quaternary wavelet matrix: node of the l-digit code prefix x at level l.
+__host__ __device__ inline int qnode_id(int level, uint32_t prefix) {
+  return ((1 << (2 * level)) - 1) / 3 + (int)prefix;
+}
 
 struct DevIndex {
   const void* lines;     // kLevels * nlines rank lines of the handle's format

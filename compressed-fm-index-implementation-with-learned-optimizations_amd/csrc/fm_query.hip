@@ -220,6 +220,86 @@ struct OccE {
   }
 };
 
+// QWM: quaternary wavelet matrix over dense symbol codes, for alphabets beyond the
+// occurrence engine (e.g. sigma = 256: 4 levels instead of 8).  Level l holds digit
+// l (2 bits, most significant first) of the level-l sequence as occurrence lines
+// (OccLine, 64 rows per 32-B line); the next sequence is the stable 4-way
+// partition by that digit.  A position p maps to the next level as
+// p' = qZ[l][d] + occ_l(d, p) — one line read — or affinely inside a pure node
+// (all its symbols share digit d): p' = qZ[l][d] + R + (p - S).  After the last
+// level, occ(c, i) = p_L(i) - S8[code(c)] (the WaveletTree::rank identity,
+// wavelet.cpp:59-96, in base 4).
+struct QWM {
+  __device__ static __forceinline__ const void* level(const DevIndex& ix, int l) {
+    return static_cast<const uint8_t*>(ix.lines) + (uint64_t)l * ix.nlines * OccLine::kBytes;
+  }
+  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
+                                              uint64_t& sp, uint64_t& ep,
+                                              uint64_t* bytes = nullptr) {
+    const uint64_t Cc = T.C[c];
+    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
+    const uint32_t x = T.occ_code[c];
+    const int L = (int)T.qlevels;
+    uint64_t ps = sp, pe = ep;
+    for (int l = 0; l < L; ++l) {
+      const int nid = qnode_id(l, x >> (2 * (L - l)));
+      const uint32_t d = (x >> (2 * (L - 1 - l))) & 3u;
+      const uint8_t f = T.flags[nid];
+      if (f & kPure) {
+        const uint64_t off = T.qZ[l][d] + T.R[nid] - T.S[nid];
+        ps += off;
+        pe += off;
+      } else {
+        const void* lv = level(ix, l);
+        const uint64_t qa = ps >> 6, qe = pe >> 6;
+        if (bytes) *bytes += (qa == qe ? 1u : 2u) * OccLine::kBytes;
+        OccLine::Raw va;
+        OccLine::load(lv, qa, va);
+        OccLine::Raw ve = {va[0], va[1]};
+        if (qe != qa) OccLine::load(lv, qe, ve);
+        ps = T.qZ[l][d] + OccLine::base(va, d, qa) + OccLine::prefix(va, d, (uint32_t)(ps & 63));
+        pe = T.qZ[l][d] + OccLine::base(ve, d, qe) + OccLine::prefix(ve, d, (uint32_t)(pe & 63));
+      }
+    }
+    sp = Cc + (ps - T.S8[x]);
+    ep = Cc + (pe - T.S8[x]);
+    return sp < ep;
+  }
+  // LF(i): the digits of BWT[i] and its mapped position, one line per level
+  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
+                                                uint64_t pos, uint32_t* sym_out = nullptr) {
+    const int L = (int)T.qlevels;
+    uint32_t x = 0;
+    uint64_t p = pos;
+    for (int l = 0; l < L; ++l) {
+      const int nid = qnode_id(l, x);
+      const uint8_t f = T.flags[nid];
+      uint32_t d;
+      if (f & kPure) {
+        d = (f >> 2) & 3u;
+        p = T.qZ[l][d] + T.R[nid] + (p - T.S[nid]);
+      } else {
+        OccLine::Raw v;
+        const uint64_t q = p >> 6;
+        OccLine::load(level(ix, l), q, v);
+        const uint32_t o = (uint32_t)(p & 63);
+        d = OccLine::code(v, o);
+        p = T.qZ[l][d] + OccLine::base(v, d, q) + OccLine::prefix(v, d, o);
+      }
+      x = (x << 2) | d;
+    }
+    const uint32_t c = T.qsym[x];
+    if (sym_out) *sym_out = c;
+    return T.C[c] + (p - T.S8[x]);
+  }
+  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
+                                                  uint32_t c, uint64_t i) {
+    uint64_t sp = 0, ep = i;
+    (void)step(ix, T, c, sp, ep);
+    return ep - sp;
+  }
+};
+
 // Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
 // range empties.  Requires m >= 1, n >= 1.  The first step comes from C[]
 // (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
@@ -637,6 +717,8 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
   do {                                                                          \
     if ((h)->line_fmt == kFmtOcc)                                               \
       KERNEL<OccE><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                       \
+    else if ((h)->line_fmt == kFmtQwm)                                          \
+      KERNEL<QWM><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                        \
     else if ((h)->line_fmt == kFmtLine32)                                       \
       KERNEL<WM<Line32>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
     else if ((h)->line_fmt == kFmtLine32W)                                      \
@@ -651,6 +733,8 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
   do {                                                                          \
     if ((h)->line_fmt == kFmtOcc)                                               \
       KERNEL<OccE><<<1, 64, 0, st>>>(__VA_ARGS__);                              \
+    else if ((h)->line_fmt == kFmtQwm)                                          \
+      KERNEL<QWM><<<1, 64, 0, st>>>(__VA_ARGS__);                               \
     else if ((h)->line_fmt == kFmtLine32)                                       \
       KERNEL<WM<Line32>><<<1, 64, 0, st>>>(__VA_ARGS__);                        \
     else if ((h)->line_fmt == kFmtLine32W)                                      \
@@ -791,6 +875,9 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   if (h->d_walk) {
     if (h->wide) k_walk_lines<WalkLineW><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk_lines<WalkLine><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  } else if (h->line_fmt == kFmtQwm) {
+    if (pow2) k_walk<QWM, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<QWM, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else if (h->line_fmt == kFmtOcc) {
     if (pow2) k_walk<OccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<OccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
@@ -839,8 +926,8 @@ cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, u
 
 cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
                              uint64_t* d_out, hipStream_t st) {
-  if (h->line_fmt == kFmtOcc) {
-    set_error("level rank1: this index uses occurrence lines, not a wavelet matrix");
+  if (h->line_fmt == kFmtOcc || h->line_fmt == kFmtQwm) {
+    set_error("level rank1: this index has no binary wavelet levels (occurrence lines)");
     return CS_ERR_UNSUPPORTED;
   }
   if (!k) return CS_OK;

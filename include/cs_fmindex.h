@@ -68,9 +68,10 @@ typedef struct cs_fm_info {
   uint32_t prefix_sigma;   /* its alphabet size */
   uint64_t prefix_bytes;
   uint8_t prefix_code[256];/* digit of each symbol in the table alphabet, 255 = not in it */
-  uint32_t engine;         /* 0 = wavelet matrix in rank lines, 1 = occurrence lines */
+  uint32_t engine;         /* 0 = binary wavelet matrix in rank lines, 1 = occurrence lines,
+                              2 = quaternary wavelet matrix of occurrence lines */
   uint32_t line_bytes;     /* bytes per rank / occurrence line (32 or 64) */
-  uint32_t levels;         /* rank-line sequences: 8 wavelet levels, or 1 */
+  uint32_t levels;         /* rank-line sequences: 8 binary levels, 1..4 quaternary, or 1 */
   uint32_t rare_rows;      /* occurrence lines: BWT rows of rare symbols kept in the table */
   uint32_t walk_marks;     /* locate walk lines: 0 none, 1 sampled rows (row % stride == 0),
                               2 sampled text positions (needs a unique smallest terminator) */
@@ -82,8 +83,9 @@ void cs_default_build_params(cs_build_params* p);
 /* FMIndex::build_from_text — fm_index.hpp:19, fm_index.cpp:16-69.
  * Builds the whole index on `device` (suffix array by prefix doubling, cyclic BWT,
  * C[], row-sampled SSA, and the rank structure: occurrence lines when at most four
- * symbols hold all but 128 BWT rows, else the 8-level wavelet matrix; environment
- * CS_FM_ENGINE=wavelet forces the latter).  `text` is a host pointer. */
+ * symbols hold all but 128 BWT rows, else a quaternary wavelet matrix of occurrence
+ * lines; environment CS_FM_ENGINE=wavelet selects the reference's binary 8-level
+ * wavelet matrix instead).  `text` is a host pointer. */
 cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_params* p,
                                 int device, cs_fm_index** out);
 /* Same, with the text already in device memory on `device`. */

@@ -28,7 +28,8 @@ ENGINE_VARIANTS = {
     "auto_noprefix": {"CS_FM_PREFIX_K": "0"},       # prefix table off
     "auto_rowmarks": {"CS_FM_WALK_MARKS": "row"},   # walk lines with the reference's row samples
     "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
-    "wavelet": {"CS_FM_ENGINE": "wavelet"},         # wavelet matrix for every text
+    "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
+    "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
     "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
     # the n >= 2^32 engines at small n: u64 samples/table, bucketed sorter, and
     # occurrence lines or 32-B wide rank lines (Line32W)
@@ -134,7 +135,7 @@ def test_suffix_array_random_sweep(pkg):
 def test_level_rank1_every_position(built, pkg, name):
     g, o = built(name)
     n = len(TEXTS[name])
-    if g.info().engine == 1:  # occurrence lines: no wavelet levels to query
+    if g.info().engine != 0:  # occurrence lines / quaternary matrix: no binary levels
         with pytest.raises(pkg.FMIndexError):
             g.level_rank1(0, np.arange(4, dtype=np.uint64))
         return
@@ -148,22 +149,27 @@ def test_level_rank1_every_position(built, pkg, name):
 def test_engine_choice(built):
     """Occurrence lines iff <= 4 symbols hold all but at most 128 BWT rows (and the
     wavelet matrix is not forced); rare rows are listed in the node table."""
-    forced = os.environ.get("CS_FM_ENGINE") == "wavelet"
+    forced = os.environ.get("CS_FM_ENGINE")
     # (engine, rare rows, walk marks: 2 = text positions when the text ends in a unique
     # smallest symbol, 1 = the reference's sampled rows)
     want = {"dna_5k": (1, 1, 2), "banana": (1, 0, 2), "single": (1, 0, 2),
-            "rare_N_41": (1, 41, 2), "rare_128": (1, 128, 2), "rare_129": (0, 0, 0),
-            "bytes_5k": (0, 0, 0), "rare_both_ends": (1, 8, 1), "abab_noterm": (1, 0, 1)}
+            "rare_N_41": (1, 41, 2), "rare_128": (1, 128, 2), "rare_129": (2, 0, 0),
+            "bytes_5k": (2, 0, 0), "rare_both_ends": (1, 8, 1), "abab_noterm": (1, 0, 1)}
+    levels = {"rare_129": 2, "bytes_5k": 4, "dna_5k": 2, "banana": 1, "single": 1,
+              "rare_N_41": 2, "rare_128": 2, "rare_both_ends": 2, "abab_noterm": 1}
     for name, (engine, rare, marks) in want.items():
         info = built(name)[0].info()
-        if forced:
+        if forced == "wavelet":
             engine, rare, marks = 0, 0, 0
+        elif forced == "qwm":
+            engine, rare, marks = 2, 0, 0
         if os.environ.get("CS_FM_WALK") == "0":
             marks = 0
         elif os.environ.get("CS_FM_WALK_MARKS") == "row" and marks:
             marks = 1
         assert (info.engine, info.rare_rows, info.walk_marks) == (engine, rare, marks), name
-        assert info.levels == (1 if engine else 8) and info.line_bytes in (32, 64)
+        want_levels = {0: 8, 1: 1, 2: levels[name]}[engine]
+        assert info.levels == want_levels and info.line_bytes in (32, 64), name
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))
