@@ -171,6 +171,13 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
+    # DRAM accesses per launch (each distinct line and each table entry is one random
+    # access) against the measured random-access ceiling of MI355X:
+    # profiles/microbench/gather_bench.hip, 8..32-B random reads over a 4 GB table run
+    # at 49-52 G accesses/s (profiles/r01/gather_bench*.txt)
+    eb = info.prefix_bytes // (info.prefix_sigma ** K) if K else 0
+    hits = int(round(B * table_frac)) if K else 0
+    accesses = (alg_bytes - eb * hits) / info.line_bytes + hits
     total_units = B * world * args.steps
     value = total_units / elapsed
     kern_avg_s = statistics.mean(kern_ms) / 1e3
@@ -218,6 +225,10 @@ def main():
                          "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,
                          "prefix_k": K, "prefix_table_hit_frac": table_frac,
                          "alg_bytes_per_query": alg_bytes / B,
+                         "random_accesses_per_launch": accesses,
+                         "random_accesses_per_s": accesses / kern_avg_s,
+                         "random_access_ceiling_per_s": 5.0e10,
+                         "frac_of_random_access_ceiling": accesses / kern_avg_s / 5.0e10,
                          "kernel_ms_mean": kern_avg_s * 1e3,
                          "kernel_ms_min": min(kern_ms)},
             "build_s": build_s,

@@ -46,6 +46,36 @@ __global__ void k_indep(const uint4* __restrict__ tab, uint64_t ngran, uint64_t 
   if (acc == 0x12345678u) sink[t & 1023] = acc;
 }
 
+// independent 32-B reads with the non-temporal hint (no L2/MALL allocation)
+__global__ void k_indep_nt(const uint4* __restrict__ tab, uint64_t ngran, uint64_t reads,
+                           uint32_t* __restrict__ sink) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t r = t; r < reads; r += nt) {
+    const uint64_t g = mix(r * 0x9E3779B97F4A7C15ull + 17) % ngran;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* p = reinterpret_cast<const u32x4*>(tab + g * 2);
+    const u32x4 v0 = __builtin_nontemporal_load(p);
+    const u32x4 v1 = __builtin_nontemporal_load(p + 1);
+    acc ^= v0.x ^ v0.y ^ v0.z ^ v0.w ^ v1.x ^ v1.y ^ v1.z ^ v1.w;
+  }
+  if (acc == 0x12345678u) sink[t & 1023] = acc;
+}
+
+// independent 8-B reads
+__global__ void k_indep8(const uint2* __restrict__ tab, uint64_t ngran, uint64_t reads,
+                         uint32_t* __restrict__ sink) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (uint64_t r = t; r < reads; r += nt) {
+    const uint2 v = tab[mix(r * 0x9E3779B97F4A7C15ull + 17) % ngran];
+    acc ^= v.x ^ v.y;
+  }
+  if (acc == 0x12345678u) sink[t & 1023] = acc;
+}
+
 // dependent chains: each lane does `depth` reads, next address from the data
 template <int W>
 __global__ void k_chain(const uint4* __restrict__ tab, uint64_t ngran, uint64_t lanes, int depth,
@@ -117,6 +147,28 @@ int main(int argc, char** argv) {
   k_fill<<<8192, 256>>>(reinterpret_cast<uint64_t*>(tab), bytes / 8);
   CK(hipDeviceSynchronize());
   std::printf("table %.2f GB, %llu reads per run\n", bytes / 1e9, (unsigned long long)reads);
+  {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int grid : {8192, 32768}) {
+      float ms = 0;
+      k_indep_nt<<<grid, 256>>>(tab, bytes / 32, reads / 4, sink);
+      CK(hipEventRecord(a));
+      k_indep_nt<<<grid, 256>>>(tab, bytes / 32, reads, sink);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      CK(hipEventElapsedTime(&ms, a, b));
+      std::printf("indep-nt W= 32 grid=%6d: %8.3f ms  %7.2f Greads/s\n", grid, ms, reads / ms / 1e6);
+      k_indep8<<<grid, 256>>>(reinterpret_cast<const uint2*>(tab), bytes / 8, reads / 4, sink);
+      CK(hipEventRecord(a));
+      k_indep8<<<grid, 256>>>(reinterpret_cast<const uint2*>(tab), bytes / 8, reads, sink);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      CK(hipEventElapsedTime(&ms, a, b));
+      std::printf("indep    W=  8 grid=%6d: %8.3f ms  %7.2f Greads/s\n", grid, ms, reads / ms / 1e6);
+    }
+  }
   run<16>(tab, bytes, reads, sink);
   run<32>(tab, bytes, reads, sink);
   run<64>(tab, bytes, reads, sink);
