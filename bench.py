@@ -67,6 +67,10 @@ def main():
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--locate-batch", type=int, default=12_500_000,
                     help="patterns of the batch timed through locate() (N=1 only; 0 = skip)")
+    ap.add_argument("--queries", default="text", choices=["text", "unif"],
+                    help="Q_text (substrings of the text, the headline) or Q_unif (uniform random)")
+    ap.add_argument("--cpu-fast-queries", type=int, default=1_000_000,
+                    help="patterns timed through the oracle's fast (precomputed) count, all threads")
     ap.add_argument("--gather", action="store_true",
                     help="gather every step's counts to rank 0 (RCCL), overlapped with the next count")
     ap.add_argument("--prefix-k", type=int, default=None,
@@ -114,8 +118,12 @@ def main():
     assert hi - lo == B
     pats = torch.empty(B * m, dtype=torch.uint8, device=dev)
     offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
-    pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, pats.data_ptr(),
-                              offs.data_ptr(), sh)
+    if args.queries == "text":
+        pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, pats.data_ptr(),
+                                  offs.data_ptr(), sh)
+    else:  # SURVEY §8(d) secondary batch Q_unif
+        pkg.synth_random_patterns_device(args.kind, m, lo, B, 4242, pats.data_ptr(),
+                                         offs.data_ptr(), sh)
     # counts land in double-buffered shards; with --gather (N > 1) the gather of step
     # k to rank 0 overlaps the count of step k+1 (shard.PipelinedGather), otherwise
     # each rank keeps its shard's counts (no collective in the data path)
@@ -192,6 +200,8 @@ def main():
         prof = os.path.join(ROOT, "profiles", "pmc_count.json")
         engine = "occ" if info.engine == 1 else "wm%d" % info.line_bytes
         wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
+        if args.queries != "text":
+            wl += ":" + args.queries
         if os.path.exists(prof):
             pj = json.load(open(prof))
             if pj.get("workload") == wl:
@@ -209,9 +219,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
-            "config": {"workload": "C4: %s text n=%d (incl. terminator), Q_text %d-mers, count()"
-                       % (args.kind.upper(), N, m) if L == 3_999_999_999 else
-                       "%s text n=%d, Q_text %d-mers, count()" % (args.kind, N, m),
+            "config": {"workload": "C4: %s text n=%d (incl. terminator), Q_%s %d-mers, count()"
+                       % (args.kind.upper(), N, args.queries, m) if L == 3_999_999_999 else
+                       "%s text n=%d, Q_%s %d-mers, count()" % (args.kind, N, args.queries, m),
                        "batch_per_gpu": B, "global_batch": B * world, "m": m,
                        "ssa_stride": args.ssa_stride, "parallelism": "dp%d" % world,
                        "index": "replicated per GPU", "workload_key": wl,
@@ -303,6 +313,20 @@ def main():
                       "(oracle/fm_oracle.c faithful=1), %d host threads" % (Q, min(threads, Q)),
             "p50_us": float(np.median(lat) / 1e3), "seconds": cpu_s, "prep_s": prep_s,
             "matches_gpu": match}
+        # also the restatement's fast multi-threaded path (precomputed
+        # count_ones totals, the same wavelet rank) over a larger slice of the batch
+        Qf = min(args.cpu_fast_queries, B)
+        if Qf > 0:
+            fs = pats[: Qf * m].cpu().numpy()
+            foffs = np.arange(0, (Qf + 1) * m, m, dtype=np.uint64)
+            t1 = time.perf_counter()
+            fcnt = ref.count_batch(buf=fs, offs=foffs, nthreads=threads, faithful=False)
+            fast_s = time.perf_counter() - t1
+            res["cpu_fast"] = {
+                "value": Qf / fast_s, "unit": "patterns/s", "cores": threads, "kind": "port",
+                "sample": "first %d patterns of the batch, oracle count() with precomputed "
+                          "totals (not the reference's cost model), %d host threads" % (Qf, threads),
+                "seconds": fast_s, "matches_gpu": bool(np.array_equal(fcnt, counts[:Qf].astype(np.uint64)))}
         del ref
 
     if rank == 0:

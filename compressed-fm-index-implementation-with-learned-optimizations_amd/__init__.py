@@ -86,6 +86,8 @@ SIGNATURES = {
     "cs_synth_text_device": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, _vp, _vp]),
     "cs_synth_patterns_device": (C.c_int, [_vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                            C.c_uint64, _vp, _vp, _vp]),
+    "cs_synth_random_patterns_device": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
+                                                   C.c_uint64, _vp, _vp, _vp]),
 }
 
 _lib = None
@@ -362,6 +364,14 @@ def synth_patterns_device(d_text: int, N: int, m: int, first: int, npat: int, se
     """Q_text patterns [first, first+npat) of stream `seed`, fixed stride m."""
     _check(lib().cs_synth_patterns_device(d_text, N, m, first, npat, seed, d_pats, d_offs,
                                           stream or None))
+
+
+def synth_random_patterns_device(kind: str, m: int, first: int, npat: int, seed: int,
+                                 d_pats: int, d_offs: int | None, stream: int = 0):
+    """Q_unif patterns [first, first+npat): uniform random symbols ("dna" / "bytes")."""
+    k = {"dna": 0, "bytes": 1}[kind]
+    _check(lib().cs_synth_random_patterns_device(k, m, first, npat, seed, d_pats, d_offs,
+                                                 stream or None))
 
 
 def sa_build(text, device: int = 0) -> np.ndarray:

@@ -64,6 +64,29 @@ __global__ void k_patterns(const uint8_t* __restrict__ text, uint64_t N, uint64_
   }
 }
 
+// Q_unif pattern k: m symbols from the draws x_0 = mix(seed + (k+1)*gamma),
+// x_{i+1} = mix(x_i + gamma); DNA takes 2 bits per symbol (32 per draw) -> "ACGT",
+// bytes take 8 bits per symbol (8 per draw) -> 1 + ((b*255)>>8), LSB first.
+__global__ void k_patterns_unif(int kind, uint64_t m, uint64_t first, uint64_t npat, uint64_t seed,
+                                uint8_t* __restrict__ pats, uint64_t* __restrict__ offs) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const char* acgt = "ACGT";
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
+    uint64_t x = mix64(seed + (first + q + 1) * kGamma);
+    const uint32_t per = kind == 0 ? 32u : 8u;
+    for (uint64_t j = 0; j < m; ++j) {
+      if (j && j % per == 0) x = mix64(x + kGamma);
+      const uint32_t sh = (uint32_t)(j % per);
+      pats[q * m + j] = kind == 0 ? (uint8_t)acgt[(x >> (2 * sh)) & 3u]
+                                  : (uint8_t)(1u + ((((x >> (8 * sh)) & 0xFFu) * 255u) >> 8));
+    }
+    if (offs) {
+      offs[q] = q * m;
+      if (q + 1 == npat) offs[npat] = npat * m;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace fmx
 
@@ -92,6 +115,20 @@ cs_status cs_synth_patterns_device(const uint8_t* d_text, uint64_t N, uint64_t m
   if (!npat) return CS_OK;
   k_patterns<<<grid_for(npat, 256, 65536), 256, 0, (hipStream_t)stream>>>(d_text, N, m, first, npat,
                                                                          seed, d_pats, d_offs);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+cs_status cs_synth_random_patterns_device(int kind, uint64_t m, uint64_t first, uint64_t npat,
+                                          uint64_t seed, uint8_t* d_pats, uint64_t* d_offs,
+                                          void* stream) {
+  if ((kind != 0 && kind != 1) || (npat && !d_pats)) {
+    set_error("cs_synth_random_patterns_device: bad argument");
+    return CS_ERR_INVALID;
+  }
+  if (!npat) return CS_OK;
+  k_patterns_unif<<<grid_for(npat, 256, 65536), 256, 0, (hipStream_t)stream>>>(
+      kind, m, first, npat, seed, d_pats, d_offs);
   FMX_HIP(hipGetLastError());
   return CS_OK;
 }

@@ -30,6 +30,15 @@ cs_status cs_synth_patterns_device(const uint8_t* d_text, uint64_t N, uint64_t m
                                    uint64_t npat, uint64_t seed, uint8_t* d_pats, uint64_t* d_offs,
                                    void* stream);
 
+/* Q_unif patterns first..first+npat-1 (SURVEY.md §8(d) secondary batch): uniform
+ * random symbols, kind 0 ACGT (2 bits per symbol, 32 per draw), kind 1 the σ=256
+ * text alphabet (8 bits per symbol, b -> 1 + ((b*255)>>8)); draws x_0 =
+ * splitmix64(seed + (k+1)*0x9E3779B97F4A7C15), x_{i+1} = splitmix64(x_i + that
+ * constant), symbols LSB first.  Same output layout as cs_synth_patterns_device. */
+cs_status cs_synth_random_patterns_device(int kind, uint64_t m, uint64_t first, uint64_t npat,
+                                          uint64_t seed, uint8_t* d_pats, uint64_t* d_offs,
+                                          void* stream);
+
 #ifdef __cplusplus
 }
 #endif

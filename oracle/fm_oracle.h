@@ -112,6 +112,9 @@ void orc_gen_bytes(uint64_t seed, uint64_t len, uint8_t* out);
 /* Q_text: pattern k = T[x_k % (N-m), +m) with x_k the k-th splitmix64 draw. */
 void orc_gen_patterns_text(const uint8_t* text, uint64_t N, uint64_t m, uint64_t npat,
                            uint64_t seed, uint8_t* out);
+/* Q_unif: pattern k from draws x_0 = splitmix64 draw k+1 of `seed`, x_{i+1} =
+ * splitmix64 step of x_i; kind 0 ACGT (2 bits/symbol), kind 1 bytes 1 + ((b*255)>>8). */
+void orc_gen_patterns_unif(int kind, uint64_t m, uint64_t npat, uint64_t seed, uint8_t* out);
 
 #ifdef __cplusplus
 }

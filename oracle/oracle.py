@@ -81,6 +81,7 @@ def lib():
                                        C.c_uint64, C.c_int, C.c_int]),
         "orc_gen_dna": (None, [C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_bytes": (None, [C.c_uint64, C.c_uint64, _u8p]),
+        "orc_gen_patterns_unif": (None, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_patterns_text": (None, [_u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                          _u8p]),
     }
@@ -340,6 +341,14 @@ def gen_patterns_text(text: np.ndarray, m: int, npat: int, seed: int = 4242) -> 
     t = np.ascontiguousarray(text, np.uint8)
     out = np.zeros((max(npat, 1), m), np.uint8)
     lib().orc_gen_patterns_text(_u8(t), len(t), m, npat, seed, _u8(out))
+    return out[:npat]
+
+
+def gen_patterns_unif(kind: str, m: int, npat: int, seed: int = 4242) -> np.ndarray:
+    """Q_unif as cs_synth_random_patterns_device: npat x m uniform random ACGT ("dna")
+    or sigma=256-alphabet ("bytes") symbols from splitmix64."""
+    out = np.zeros((max(npat, 1), m), np.uint8)
+    lib().orc_gen_patterns_unif({"dna": 0, "bytes": 1}[kind], m, npat, seed, _u8(out))
     return out[:npat]
 
 
