@@ -235,6 +235,11 @@ def main():
                          "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,
                          "prefix_k": K, "prefix_table_hit_frac": table_frac,
                          "alg_bytes_per_query": alg_bytes / B,
+                         # SURVEY.md §8(d)'s per-query figure for the reference's
+                         # structure (64 B x 8 levels x 2 ranks x (m-1) steps), for
+                         # comparison only: this engine reads alg_bytes_per_query
+                         "survey_alg_bytes_per_query": 64 * 8 * 2 * (m - 1),
+                         "survey_equivalent_GBs": 64 * 8 * 2 * (m - 1) * B / kern_avg_s / 1e9,
                          "random_accesses_per_launch": accesses,
                          "random_accesses_per_s": accesses / kern_avg_s,
                          "random_access_ceiling_per_s": 5.0e10,
