@@ -278,17 +278,32 @@ def main():
                          "limit": 100000, "positions_verified": ok}
         del d_sp, d_oo, d_pos, owner, win
 
-    # ---- p50 single-pattern latency through the C ABI (end to end) ----
+    # ---- p50 single-pattern latency (>= 1000 single-pattern calls
+    #      through the C++ facade, end to end, as tools/benchmark.cpp:154-166) ----
     if rank == 0 and args.p50_calls:
-        hp = pats[: args.p50_calls * m].cpu().numpy().reshape(-1, m)
-        lat = []
-        for q in range(hp.shape[0]):
-            b = hp[q].tobytes()
-            t1 = time.perf_counter()
-            idx.count(b)
-            lat.append((time.perf_counter() - t1) * 1e6)
+        import ctypes as C
+        hp = np.ascontiguousarray(pats[: args.p50_calls * m].cpu().numpy())
+        nq = hp.size // m
+        blib = C.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libcs_bench.so"))
+        fn = blib.cs_bench_facade_count_latency
+        fn.restype = C.c_int
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
+        cnt1 = np.zeros(nq, np.uint64)
+        lat = np.zeros(nq, np.float64)
+        if fn(idx._h, hp.ctypes.data, m, nq, cnt1.ctypes.data, lat.ctypes.data) != 0:
+            raise RuntimeError("p50 facade loop failed: " + pkg.lib().cs_fm_last_error().decode())
+        assert np.array_equal(cnt1, counts[:nq].astype(np.uint64))
         res["p50_us"] = float(np.median(lat))
         res["p95_us"] = float(np.percentile(lat, 95))
+        res["p50_method"] = "cs::FMIndex::count via the C++ facade, %d calls, steady_clock" % nq
+        # the same through the Python mirror (ctypes), for reference
+        lat_py = []
+        for q in range(min(nq, 1000)):
+            b = hp[q * m:(q + 1) * m].tobytes()
+            t1 = time.perf_counter()
+            idx.count(b)
+            lat_py.append((time.perf_counter() - t1) * 1e6)
+        res["p50_python_us"] = float(np.median(lat_py))
         res["in_batch_us_per_query"] = elapsed / args.steps / B * 1e6
 
     # ---- CPU baseline: reference-faithful restatement on host cores (rank 0, N=1) ----

@@ -59,7 +59,7 @@ SIGNATURES = {
     "cs_fm_destroy": (None, [_vp]),
     "cs_fm_get_info": (C.c_int, [_vp, C.POINTER(cs_fm_info)]),
     "cs_fm_last_error": (C.c_char_p, []),
-    "cs_fm_count": (C.c_int, [_vp, _u8p, C.c_uint64, _u64p]),
+    "cs_fm_count": (C.c_int, [_vp, C.c_char_p, C.c_uint64, _u64p]),
     "cs_fm_locate": (C.c_int, [_vp, _u8p, C.c_uint64, C.c_uint64, _u64p, C.c_uint64, _u64p]),
     "cs_fm_extract": (C.c_int, [_vp, C.c_uint64, C.c_uint64, _u8p, _u64p]),
     "cs_fm_extract_batch": (C.c_int, [_vp, _u64p, _u64p, C.c_uint64, _u64p, _u8p, C.c_uint64,
@@ -216,9 +216,9 @@ class FMIndex:
 
     # -- queries (fm_index.hpp:26-37) -------------------------------------
     def count(self, pattern) -> int:
-        p = np.frombuffer(_bytes(pattern) + b"\0", np.uint8)
+        b = _bytes(pattern)
         out = C.c_uint64()
-        _check(lib().cs_fm_count(self._h, _u8(p), len(p) - 1, C.byref(out)))
+        _check(lib().cs_fm_count(self._h, b, len(b), C.byref(out)))
         return out.value
 
     def locate(self, pattern, limit: int = 100000) -> list:

@@ -1,6 +1,7 @@
 // fm_capi.hip — the extern "C" boundary (include/cs_fmindex.h).  Host-buffer entry
 // points stage through HBM; *_device entry points only launch.  No CPU fallback:
 // without a HIP device every call fails with CS_ERR_NO_DEVICE.
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -253,11 +254,28 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     OnePattern p;
     p.m = (uint32_t)bytes;
     if (bytes) std::memcpy(p.b, pats + offs[0], bytes);
+    // The kernel stores the count (never ~0: counts are < 2^40) into the pinned word
+    // with a system-scope release; the host polls it for up to 1 ms before falling
+    // back to a stream synchronisation (queued work ahead of it, or an error).
+    constexpr uint64_t kPending = ~0ull;
     uint64_t* res = reinterpret_cast<uint64_t*>(h->scratch.h);
+    __atomic_store_n(res, kPending, __ATOMIC_RELAXED);
     s = launch_count_one(h, p, res, st);
     if (s != CS_OK) return s;
-    FMX_HIP(hipStreamSynchronize(st));
-    out_counts[0] = *reinterpret_cast<volatile uint64_t*>(res);
+    uint64_t v = kPending;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; ++spin) {
+      v = __atomic_load_n(res, __ATOMIC_ACQUIRE);
+      if (v != kPending) break;
+      if ((spin & 255) == 255 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1))
+        break;
+    }
+    if (v == kPending) {
+      FMX_HIP(hipStreamSynchronize(st));
+      v = __atomic_load_n(res, __ATOMIC_ACQUIRE);
+    }
+    out_counts[0] = v;
     return CS_OK;
   }
   if (o_pats + bytes + 16 <= cs_fm_index::kScratchBytes) {

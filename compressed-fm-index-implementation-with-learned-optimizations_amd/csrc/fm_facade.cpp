@@ -62,6 +62,16 @@ FMIndex FMIndex::open_directory(const std::string& dir) {
   return idx;
 }
 
+FMIndex FMIndex::borrow(cs_fm_index* h) {
+  if (!h) throw std::runtime_error("borrow: null handle");
+  FMIndex idx;
+  cs_fm_info info;
+  if (cs_fm_get_info(h, &info) != CS_OK) throw std::runtime_error(cs_fm_last_error());
+  idx.meta_.n = info.n;
+  idx.h_ = std::shared_ptr<cs_fm_index>(h, [](cs_fm_index*) {});
+  return idx;
+}
+
 void FMIndex::save_directory(const std::string& dir) const {
   if (!h_) throw std::runtime_error("save_directory: empty index");
   cs_status s = cs_fm_save_directory(h_.get(), dir.c_str());

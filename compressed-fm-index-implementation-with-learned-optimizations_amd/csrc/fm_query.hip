@@ -407,7 +407,8 @@ __global__ void k_count_one(DevIndex ix, OnePattern p, uint64_t* __restrict__ ou
     uint64_t sp, ep;
     res = backward_search<E>(ix, T, p.b, p.m, sp, ep) ? ep - sp : 0;
   }
-  *out = res;
+  // system-scope store: the host polls this word instead of waiting for the stream
+  __hip_atomic_store(out, res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Measurement twin of k_count: the algorithmic bytes of each query's search —

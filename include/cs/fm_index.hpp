@@ -4,9 +4,10 @@
 // exceptions as cs::FMIndex (src/api/fm_index.hpp:11-67); the work runs on the GPU
 // through the C ABI in cs_fmindex.h (implementation: csrc/fm_facade.cpp inside
 // libcs_fmindex.so).  Additions: count_batch / locate_batch (one launch for many
-// patterns), save_directory (the on-disk format open_directory reads) and handle()
-// for the raw ABI.  Errors are std::runtime_error with the reference's message text
-// ("locate: LF walk exceeded text length").
+// patterns), save_directory (the on-disk format open_directory reads), handle()
+// for the raw ABI and borrow() to wrap an ABI handle.  Errors are
+// std::runtime_error with the reference's message text ("locate: LF walk exceeded
+// text length").
 //
 // Semantics kept from the reference: plain suffix order and a
 // cyclic BWT, so callers append their own unique smallest terminator as before;
@@ -53,6 +54,9 @@ class FMIndex {
 
   uint64_t size() const { return meta_.n; }
   const cs_fm_index* handle() const { return h_.get(); }
+  // Wraps an index built or opened through the C ABI without taking ownership
+  // (the caller keeps it alive and destroys it).
+  static FMIndex borrow(cs_fm_index* h);
 
  private:
   IndexMeta meta_;
