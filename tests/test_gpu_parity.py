@@ -87,6 +87,14 @@ def _texts():
         "rare_both_ends": _sprinkle(rng, 2000, b"!!~~~\x00\xff") + b"$",  # below and above ACGT
         "rare_runs": b"ACGT" * 200 + b"N" * 60 + b"TTGCA" * 100 + b"$",
     }
+    # quaternary-matrix level boundaries (k symbols + the terminator): 6 / 16 symbols ->
+    # 2 levels, 17 / 64 -> 3, 65 / 201 -> 4
+    for k in (5, 15, 16, 63, 64, 200):
+        alpha = np.arange(40, 40 + k, dtype=np.uint8)
+        out["alpha_%d" % k] = bytes(rng.choice(alpha, 3000).astype(np.uint8)) + b"\x01"
+    # skewed histogram: one dominant symbol, many rare ones (pure nodes at every level)
+    sk = np.where(rng.random(4000) < 0.97, 65, rng.integers(66, 120, 4000)).astype(np.uint8)
+    out["skewed_55"] = bytes(sk) + b"$"
     return out
 
 
