@@ -51,8 +51,8 @@ def log(rank, *a):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--kind", default="dna", choices=["dna", "bytes"])
     ap.add_argument("--text-bytes", type=int, default=3_999_999_999,
                     help="text length before the terminator (C4: 3,999,999,999)")
