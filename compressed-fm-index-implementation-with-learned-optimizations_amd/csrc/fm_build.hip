@@ -711,7 +711,8 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
   return CS_OK;
 }
 
-// Walk lines for the occurrence engine.  Position marks need LF to be one n-cycle
+// Walk lines for the occurrence engine (codes) or the quaternary matrix (level-0
+// digits; `map` gives each symbol's 2-bit value).  Position marks need LF to be one n-cycle
 // (lf_exact) so that every walk ends at a sampled text position; otherwise the
 // reference's row marks (row % stride == 0) keep its overrun behaviour.
 cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
@@ -912,6 +913,18 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     h->nlines = (n >> 6) + 1;
     cs_status qs = build_qwm(bwt.as<uint8_t>(), n, hist, h, st);
     if (qs != CS_OK) return qs;
+    bool walk = true;
+    if (const char* e = std::getenv("CS_FM_WALK"))  // "0": walk over the matrix levels
+      walk = std::atoi(e) != 0;
+    if (walk) {  // walk lines carry level 0: each symbol's first base-4 digit
+      CodeMap d0;
+      std::memset(d0.c, 0, sizeof d0.c);
+      const int L = (int)T.qlevels;
+      for (int c = 0; c < 256; ++c)
+        if (hist[c]) d0.c[c] = (uint8_t)((T.occ_code[c] >> (2 * (L - 1))) & 3u);
+      qs = build_walk(bwt.as<uint8_t>(), n, d0, h, st);
+      if (qs != CS_OK) return qs;
+    }
   } else if (occ) {
     h->line_fmt = kFmtOcc;
     h->line_bytes = OccLine::kBytes;

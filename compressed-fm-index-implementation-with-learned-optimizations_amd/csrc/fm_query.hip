@@ -541,7 +541,7 @@ __device__ __forceinline__ uint64_t wssa_at(const DevIndex& ix, uint64_t k) {
   return ix.wide ? static_cast<const uint64_t*>(ix.wssa)[k] : static_cast<const uint32_t*>(ix.wssa)[k];
 }
 
-template <class W>
+template <class W, bool kQ>
 __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t* __restrict__ rows,
                                                      uint64_t total, uint64_t chunk,
                                                      uint64_t* __restrict__ out,
@@ -593,7 +593,7 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
           sidx = W::mark_rank(v, o);
           phase = kSample;
         }
-      } else {  // LF = C[c] + occ(c, pos) from the same line (OccE::lf)
+      } else if (!kQ) {  // LF = C[c] + occ(c, pos) from the same line (OccE::lf)
         const uint32_t code = W::code(v, o);
         uint32_t c = T.occ_sym[code];
         uint64_t r = W::occ(v, code, q, o);
@@ -607,6 +607,30 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
           }
         }
         pos = T.C[c] + r;
+        ++steps;
+      } else {  // quaternary matrix: level 0 from the walk line, levels 1.. as QWM::lf
+        const uint32_t d0 = W::code(v, o);
+        uint64_t p = T.qZ[0][d0] + W::occ(v, d0, q, o);
+        uint32_t x = d0;
+        const int L = (int)T.qlevels;
+        for (int l = 1; l < L; ++l) {
+          const int nid = qnode_id(l, x);
+          const uint8_t f = T.flags[nid];
+          uint32_t d;
+          if (f & kPure) {
+            d = (f >> 2) & 3u;
+            p = T.qZ[l][d] + T.R[nid] + (p - T.S[nid]);
+          } else {
+            OccLine::Raw lv;
+            const uint64_t lq = p >> 6;
+            OccLine::load(QWM::level(ix, l), lq, lv);
+            const uint32_t lo = (uint32_t)(p & 63);
+            d = OccLine::code(lv, lo);
+            p = T.qZ[l][d] + OccLine::base(lv, d, lq) + OccLine::prefix(lv, d, lo);
+          }
+          x = (x << 2) | d;
+        }
+        pos = T.C[T.qsym[x]] + (p - T.S8[x]);
         ++steps;
       }
     } else if (phase == kSample) {
@@ -874,8 +898,15 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
   if (h->d_walk) {
-    if (h->wide) k_walk_lines<WalkLineW><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk_lines<WalkLine><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    const bool q = h->line_fmt == kFmtQwm;
+    if (h->wide && q)
+      k_walk_lines<WalkLineW, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else if (h->wide)
+      k_walk_lines<WalkLineW, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else if (q)
+      k_walk_lines<WalkLine, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else
+      k_walk_lines<WalkLine, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else if (h->line_fmt == kFmtQwm) {
     if (pow2) k_walk<QWM, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<QWM, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);

@@ -155,22 +155,25 @@ def test_level_rank1_every_position(built, pkg, name):
 
 
 def test_engine_choice(built):
-    """Occurrence lines iff <= 4 symbols hold all but at most 128 BWT rows (and the
-    wavelet matrix is not forced); rare rows are listed in the node table."""
+    """Occurrence lines iff <= 4 symbols hold all but at most 128 BWT rows, else the
+    quaternary matrix (unless an engine is forced); rare rows are listed in the node
+    table; both get walk lines for locate."""
     forced = os.environ.get("CS_FM_ENGINE")
-    # (engine, rare rows, walk marks: 2 = text positions when the text ends in a unique
-    # smallest symbol, 1 = the reference's sampled rows)
-    want = {"dna_5k": (1, 1, 2), "banana": (1, 0, 2), "single": (1, 0, 2),
-            "rare_N_41": (1, 41, 2), "rare_128": (1, 128, 2), "rare_129": (2, 0, 0),
-            "bytes_5k": (2, 0, 0), "rare_both_ends": (1, 8, 1), "abab_noterm": (1, 0, 1)}
+    # (engine, rare rows, LF one cycle: the text ends in a unique smallest symbol, so the
+    # walk lines mark sampled text positions (2) instead of the reference's rows (1))
+    want = {"dna_5k": (1, 1, True), "banana": (1, 0, True), "single": (1, 0, True),
+            "rare_N_41": (1, 41, True), "rare_128": (1, 128, True), "rare_129": (2, 0, True),
+            "bytes_5k": (2, 0, True), "rare_both_ends": (1, 8, False),
+            "abab_noterm": (1, 0, False)}
     levels = {"rare_129": 2, "bytes_5k": 4, "dna_5k": 2, "banana": 1, "single": 1,
               "rare_N_41": 2, "rare_128": 2, "rare_both_ends": 2, "abab_noterm": 1}
-    for name, (engine, rare, marks) in want.items():
+    for name, (engine, rare, cyc) in want.items():
         info = built(name)[0].info()
         if forced == "wavelet":
-            engine, rare, marks = 0, 0, 0
+            engine, rare = 0, 0
         elif forced == "qwm":
-            engine, rare, marks = 2, 0, 0
+            engine, rare = 2, 0
+        marks = 0 if engine == 0 else (2 if cyc else 1)
         if os.environ.get("CS_FM_WALK") == "0":
             marks = 0
         elif os.environ.get("CS_FM_WALK_MARKS") == "row" and marks:
