@@ -67,6 +67,8 @@ SIGNATURES = {
     "cs_fm_count_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p, _vp]),
     "cs_fm_locate_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, C.c_uint64, _u64p, _u64p,
                                      C.c_uint64, _u64p, _vp]),
+    "cs_fm_create": (C.c_int, [_u8p, C.c_uint64, _u32p, C.c_uint64, C.c_uint32, _u8p, C.c_int,
+                               C.POINTER(_vp)]),
     "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
@@ -197,6 +199,24 @@ class FMIndex:
         p = (params or BuildParams())._c()
         h = _vp()
         _check(lib().cs_fm_build_from_device_text(d_text_ptr, n, C.byref(p), device, C.byref(h)))
+        return FMIndex(h, n)
+
+    @staticmethod
+    def create(bwt, ssa, ssa_stride: int = 32, text=None, device: int | None = None):
+        """From host index arrays built elsewhere: the cyclic BWT and the row-sampled
+        u32 SSA the reference's build_from_text leaves in bwt_ / ssa_
+        (src/api/fm_index.cpp:49-66); `text` optional (kept for extract)."""
+        if device is None:
+            device = int(os.environ.get("CS_FM_DEVICE", "0"))
+        b = np.frombuffer(_bytes(bwt) + b"\0", np.uint8)
+        n = len(b) - 1
+        sa = np.ascontiguousarray(ssa, np.uint32)
+        if len(sa) == 0:
+            sa = np.zeros(1, np.uint32)
+        t = np.frombuffer(_bytes(text) + b"\0", np.uint8) if text is not None else None
+        h = _vp()
+        _check(lib().cs_fm_create(_u8(b), n, sa.ctypes.data_as(_u32p), len(ssa), ssa_stride,
+                                  _u8(t) if t is not None else None, device, C.byref(h)))
         return FMIndex(h, n)
 
     @staticmethod

@@ -717,7 +717,7 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
 // reference's row marks (row % stride == 0) keep its overrun behaviour.
 cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
                      hipStream_t st) {
-  bool pos_marks = h->lf_exact;
+  bool pos_marks = h->lf_exact && h->d_isa && h->nisa == h->nsamples;
   if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
     if (std::string(e) == "row") pos_marks = false;
   h->walk_marks = pos_marks ? 2u : 1u;
@@ -818,6 +818,9 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
   }
 }
 
+static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm_index* h,
+                              hipStream_t st, PhaseLog& plog);
+
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
                              hipStream_t st) {
   if (stride == 0) {
@@ -891,7 +894,15 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     while (smallest < 256 && hist[smallest] == 0) ++smallest;
     h->lf_exact = hist[last] == 1 && last == smallest;
   }
+  return finish_index(bwt, hist, h, st, plog);
+}
 
+// Everything after the BWT and the samples: rank structure, C[], node table, prefix
+// table, walk lines.  Shared by the text builder and cs_fm_create.
+static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm_index* h,
+                              hipStream_t st, PhaseLog& plog) {
+  const uint64_t n = h->n;
+  NodeTable& T = h->h_table;
   // --- rank structure: occurrence lines (<= 4 frequent symbols) or the wavelet
   //     matrix levels as rank lines ---
   CodeMap occ_map;
@@ -1045,6 +1056,57 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   FMX_HIP(hipStreamSynchronize(st));
   plog.mark("node table");
   return CS_OK;
+}
+
+// cs_fm_create: the index from a BWT and the reference's row-sampled SSA built
+// elsewhere (the members FMIndex::build_from_text leaves in bwt_ and ssa_,
+// src/api/fm_index.cpp:49-66).  No suffix sorting; no inverse-SA samples, so the
+// walk uses the given row samples and extract needs the caller's text.
+cs_status build_index_from_bwt(const uint8_t* bwt_host, uint64_t n, const uint32_t* ssa_host,
+                               uint64_t nsamples, uint32_t stride, cs_fm_index* h, hipStream_t st) {
+  if (stride == 0) {
+    set_error("ssa_stride must be > 0");
+    return CS_ERR_INVALID;
+  }
+  if (n >= (1ull << 32)) {
+    set_error("cs_fm_create: u32 samples need n < 2^32");
+    return CS_ERR_INVALID;
+  }
+  if (nsamples != (n + stride - 1) / stride) {
+    set_error("cs_fm_create: ssa must hold ceil(n / stride) samples");
+    return CS_ERR_INVALID;
+  }
+  h->n = n;
+  h->stride = stride;
+  h->wide = false;
+  h->nsamples = nsamples;
+  h->nisa = 0;
+  NodeTable& T = h->h_table;
+  std::memset(&T, 0, sizeof T);
+  PhaseLog plog(st);
+  DevBuf bwt;
+  FMX_HIP(bwt.alloc(n));
+  FMX_HIP(hipMalloc(&h->d_ssa, (nsamples ? nsamples : 1) * 4));
+  if (n) {
+    FMX_HIP(hipMemcpyAsync(bwt.p, bwt_host, n, hipMemcpyHostToDevice, st));
+    FMX_HIP(hipMemcpyAsync(h->d_ssa, ssa_host, nsamples * 4, hipMemcpyHostToDevice, st));
+  }
+  unsigned long long hist[256] = {0};
+  if (n) {
+    DevBuf d_hist;
+    FMX_HIP(d_hist.alloc(256 * sizeof(unsigned long long)));
+    FMX_HIP(hipMemsetAsync(d_hist.p, 0, 256 * sizeof(unsigned long long), st));
+    k_hist<<<grid_for(n / 16 + 1, kBlk, 8192), kBlk, 0, st>>>(bwt.as<uint8_t>(), n,
+                                                              d_hist.as<unsigned long long>());
+    FMX_HIP(hipMemcpyAsync(hist, d_hist.p, sizeof hist, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    // LF is one n-cycle when the unique smallest symbol ends the text: then the
+    // smallest suffix is the last one, SA[0] = n - 1
+    int smallest = 0;
+    while (smallest < 256 && hist[smallest] == 0) ++smallest;
+    h->lf_exact = hist[smallest] == 1 && ssa_host[0] == n - 1;
+  }
+  return finish_index(bwt, hist, h, st, plog);
 }
 
 }  // namespace fmx

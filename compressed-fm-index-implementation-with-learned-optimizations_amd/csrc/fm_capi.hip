@@ -171,6 +171,35 @@ cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
   return build_common(d_text, n, p, device, out, nullptr);
 }
 
+cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint64_t nsamples,
+                       uint32_t ssa_stride, const uint8_t* text, int device, cs_fm_index** out) {
+  if (!out || (n && (!bwt || !ssa))) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  *out = nullptr;
+  cs_status s = use_device(device);
+  if (s != CS_OK) return s;
+  auto* h = new (std::nothrow) cs_fm_index();
+  if (!h) return CS_ERR_OOM;
+  h->device = device;
+  hipStream_t st;
+  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    delete h;
+    return hip_fail(hipGetLastError(), "hipStreamCreate");
+  }
+  s = build_index_from_bwt(bwt, n, ssa, nsamples, ssa_stride, h, st);
+  (void)hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  if (s != CS_OK) {
+    free_index(h);
+    return s;
+  }
+  if (text) h->h_text.assign(text, text + n);
+  *out = h;
+  return CS_OK;
+}
+
 cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out) {
   int dev = 0;
   if (const char* e = std::getenv("CS_FM_DEVICE")) dev = std::atoi(e);
@@ -438,13 +467,19 @@ cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const u
     return CS_ERR_CAPACITY;
   }
   if (!acc) return CS_OK;
-  if (!h->lf_exact) {
-    set_error("device extract needs a text ending in a unique smallest symbol");
-    return CS_ERR_UNSUPPORTED;
-  }
   if (!out) {
     set_error("null output buffer");
     return CS_ERR_INVALID;
+  }
+  if (!h->lf_exact || !h->nisa) {
+    if (h->h_text.size() == n) {  // the text_ copy, as the reference keeps it
+      for (uint64_t q = 0; q < k; ++q)
+        if (pos[q] < n) std::memcpy(out + out_offs[q], h->h_text.data() + pos[q], out_offs[q + 1] - out_offs[q]);
+      return CS_OK;
+    }
+    set_error("device extract needs a text ending in a unique smallest symbol and "
+              "inverse-SA samples");
+    return CS_ERR_UNSUPPORTED;
   }
   DevBuf dp, dl, doo, dout;
   FMX_HIP(dp.alloc(k * 8));

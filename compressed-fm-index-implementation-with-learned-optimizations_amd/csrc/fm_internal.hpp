@@ -100,6 +100,8 @@ cs_status hip_fail(hipError_t e, const char* what);
 
 // Index construction on the device (fm_build.hip).
 cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st);
+cs_status build_index_from_bwt(const uint8_t* bwt_host, uint64_t n, const uint32_t* ssa_host,
+                               uint64_t nsamples, uint32_t stride, cs_fm_index* h, hipStream_t st);
 cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, bool wide,
                              uint8_t* d_bwt, void* d_ssa, void* d_isa, hipStream_t st);
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,

@@ -92,6 +92,14 @@ cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_
 cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
                                        const cs_build_params* p, int device,
                                        cs_fm_index** out);
+/* Create from host index arrays built elsewhere — the members the reference's
+ * build_from_text leaves in bwt_ (the cyclic BWT, n bytes) and ssa_ (u32 samples
+ * SA[k * ssa_stride], ceil(n / ssa_stride) of them), src/api/fm_index.cpp:49-66 —
+ * without suffix sorting.  `text` (n bytes, optional, may be NULL) is kept on the
+ * host for extract, as text_; without it extract returns CS_ERR_UNSUPPORTED
+ * (the arrays carry no inverse-SA samples).  n < 2^32. */
+cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint64_t nsamples,
+                       uint32_t ssa_stride, const uint8_t* text, int device, cs_fm_index** out);
 /* FMIndex::open_directory — fm_index.hpp:20 ("TODO: on-disk format"); the reference
  * throws (fm_index.cpp:71-73).  Here it opens an index written by
  * cs_fm_save_directory onto device CS_FM_DEVICE (default 0);

@@ -386,3 +386,33 @@ def test_bucketed_multi_pass(pkg):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+@pytest.mark.parametrize("name", ["banana", "dna_5k", "bytes_5k", "abab_noterm", "rare_N_41",
+                                  "alpha_16", "runs"])
+def test_create_from_arrays(pkg, name):
+    """cs_fm_create: the index from the reference's own members (bwt_, ssa_), no suffix
+    sort on the device; same counts / positions as the oracle, extract from the text
+    when given, CS_ERR_UNSUPPORTED without it."""
+    t = TEXTS[name]
+    o = O.Index(t, ssa_stride=16)
+    g = pkg.FMIndex.create(o.bwt().tobytes(), o.ssa(), 16)
+    gt = pkg.FMIndex.create(o.bwt().tobytes(), o.ssa(), 16, text=t)
+    rng = np.random.default_rng(len(t))
+    pats = [t[i:i + k] for i, k in zip(rng.integers(0, len(t) - 8, 300), rng.integers(1, 9, 300))]
+    pats += [b"", b"\xfe\xfd", t[:3]]
+    want = [o.count(p) for p in pats]
+    assert g.count_batch(pats).tolist() == want
+    assert [g.count(p) for p in pats[:20]] == want[:20]
+    for p in pats[:60]:
+        try:
+            w = o.locate(p, limit=50)
+        except RuntimeError as e:
+            with pytest.raises(RuntimeError) as ei:
+                g.locate(p, limit=50)
+            assert str(ei.value) == str(e)
+            continue
+        assert g.locate(p, limit=50) == w
+    assert gt.extract(1, 7) == t[1:8]
+    with pytest.raises(RuntimeError):
+        g.extract(1, 7)
