@@ -169,6 +169,12 @@ class LevelView:
     def size(self):
         return lib().orc_bv_size(self._h)
 
+    def words_ptr(self):
+        """(address, count) of the packed words, borrowed from the owning index."""
+        n = C.c_uint64()
+        w = lib().orc_bv_words(self._h, C.byref(n))
+        return C.cast(w, C.c_void_p).value, n.value
+
     def tables(self):
         L = lib()
         n = C.c_uint64()
@@ -357,3 +363,59 @@ def gen_patterns_uniform(alphabet: bytes, m: int, npat: int, seed: int = 4243) -
     rng = np.random.Generator(np.random.PCG64(seed))
     a = np.frombuffer(alphabet, np.uint8)
     return a[rng.integers(0, len(a), size=(npat, m))]
+
+
+# ---- the GENUINE reference (oracle/_ref/libcs_ref.so, built by `make -C oracle ref`
+#      from the reference's own sources; test infrastructure / CPU baseline only) ----
+_ref = None
+REF_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libcs_ref.so")
+
+
+def ref_lib():
+    """The reference shim (oracle/ref/ref_shim.cpp), or None when it is not built."""
+    global _ref
+    if _ref is None and os.path.exists(REF_LIB):
+        R = C.CDLL(REF_LIB)
+        R.ref_build_count_only.restype = C.c_void_p
+        R.ref_build_count_only.argtypes = [C.POINTER(C.c_void_p), C.c_uint64, C.c_uint64, _u64p]
+        R.ref_count_batch.restype = None
+        R.ref_count_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_int, _u64p, _u64p]
+        R.ref_free.restype = None
+        R.ref_free.argtypes = [C.c_void_p]
+        _ref = R
+    return _ref
+
+
+class RefCountIndex:
+    """The reference's own FMIndex::count over this oracle index's wavelet levels
+    (ref_build_count_only: genuine BitVector tables and count loop)."""
+
+    def __init__(self, idx: "Index"):
+        R = ref_lib()
+        if R is None:
+            raise FileNotFoundError(REF_LIB)
+        ptrs = (C.c_void_p * 8)()
+        nw = 0
+        for l in range(8):
+            ptrs[l], nw = idx.level(l).words_ptr()
+        Cv = np.ascontiguousarray(idx.C(), np.uint64)
+        self._h = R.ref_build_count_only(ptrs, nw, idx.n, _u64(Cv))
+        self.n = idx.n
+
+    def count_batch(self, buf, offs, nthreads=1, latencies=False):
+        R = ref_lib()
+        buf = np.ascontiguousarray(buf, np.uint8)
+        if len(buf) == 0:
+            buf = np.zeros(1, np.uint8)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        npat = len(offs) - 1
+        out = np.zeros(max(npat, 1), np.uint64)
+        lat = np.zeros(max(npat, 1), np.uint64)
+        R.ref_count_batch(self._h, _u8(buf), _u64(offs), npat, nthreads, _u64(out), _u64(lat))
+        return (out[:npat], lat[:npat]) if latencies else out[:npat]
+
+    def __del__(self):
+        R = _ref
+        if R is not None and getattr(self, "_h", None):
+            R.ref_free(self._h)
+            self._h = None

@@ -10,6 +10,8 @@
 // by tests/test_oracle_golden.py).  Technique per SURVEY.md §7 step 1.
 #include <algorithm>
 #include <array>
+#include <chrono>
+#include <thread>
 #include <cstdint>
 #include <cstring>
 #include <filesystem>
@@ -76,6 +78,49 @@ int64_t ref_locate(void* h, const uint8_t* p, uint64_t m, uint64_t limit, uint64
   } catch (...) {
     return -1;
   }
+}
+
+// Count-only reference index at sizes where the reference's own build (naive suffix
+// sort, single-threaded wavelet partitions) cannot run: the eight wavelet levels'
+// packed words (e.g. the oracle's levels of the same BWT, checked bit-equal by
+// tests/test_oracle_golden.py) go through the genuine BitVector::build_from_words
+// (src/core/bitvector.cpp:98-159), C_ as build_from_text computes it
+// (src/api/fm_index.cpp:36-47); FMIndex::count (:79-101) then runs unmodified.
+void* ref_build_count_only(const uint64_t* const* level_words, uint64_t nwords, uint64_t n,
+                           const uint64_t* C257) {
+  auto* idx = new cs::FMIndex();
+  idx->meta_.n = n;
+  idx->wavelet_.n_ = n;
+  for (int l = 0; l < 8; ++l) {
+    std::vector<uint64_t> w(level_words[l], level_words[l] + nwords);
+    idx->wavelet_.levels_[l].build_from_words(w, n);
+  }
+  idx->C_.assign(257, 0u);
+  for (int c = 0; c < 257; ++c) idx->C_[c] = static_cast<uint32_t>(C257[c]);
+  return idx;
+}
+
+// count() of npat patterns on nthreads host threads (disjoint contiguous slices; the
+// reference's count is const and re-entrant), per-call latency in ns.
+void ref_count_batch(void* h, const uint8_t* pats, const uint64_t* offs, uint64_t npat,
+                     int nthreads, uint64_t* out, uint64_t* lat_ns) {
+  const auto* idx = static_cast<const cs::FMIndex*>(h);
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([=] {
+      const uint64_t a = npat * t / nthreads, b = npat * (t + 1) / nthreads;
+      for (uint64_t q = a; q < b; ++q) {
+        const auto t0 = std::chrono::steady_clock::now();
+        out[q] = idx->count(std::string_view(reinterpret_cast<const char*>(pats + offs[q]),
+                                             offs[q + 1] - offs[q]));
+        const auto t1 = std::chrono::steady_clock::now();
+        if (lat_ns)
+          lat_ns[q] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
 }
 
 uint64_t ref_wt_rank(void* h, uint8_t c, uint64_t i) {

@@ -115,3 +115,19 @@ def test_synthetic_generators():
     q = O.gen_patterns_text(d, 20, 50, seed=4242)
     s = d.tobytes()
     assert all(bytes(p) in s for p in q)
+
+
+@pytest.mark.parametrize("case", fm_golden_cases("fm_100k.json", "fm_1m.json"))
+def test_reference_count_only_index(case):
+    """bench.py's cpu_baseline of kind "reference": the reference's own
+    FMIndex::count over BitVector tables built by the reference
+    (oracle/ref/ref_shim.cpp ref_build_count_only) from the oracle's levels of the
+    same BWT reproduces the golden counts of the genuine reference."""
+    if O.ref_lib() is None:
+        pytest.skip("oracle/_ref/libcs_ref.so not built (needs /root/reference)")
+    text = golden_text(case["text"])
+    idx = O.Index(text, ssa_stride=case["ssa_stride"])
+    ref = O.RefCountIndex(O.Index(bwt=idx.bwt(), nthreads=2))
+    pats = [bytes.fromhex(h) for h in case["patterns_hex"]]
+    buf, offs = O.pack_patterns(pats)
+    assert ref.count_batch(buf, offs, nthreads=4).tolist() == case["count"]
