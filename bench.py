@@ -73,6 +73,8 @@ def main():
                     help="Q_text (substrings of the text, the headline) or Q_unif (uniform random)")
     ap.add_argument("--cpu-fast-queries", type=int, default=1_000_000,
                     help="patterns timed through the oracle's fast (precomputed) count, all threads")
+    ap.add_argument("--extract-batch", type=int, default=1_000_000,
+                    help="random 20-byte extracts timed on the device (N=1 only; 0 = skip)")
     ap.add_argument("--gather", action="store_true",
                     help="gather every step's counts to rank 0 (RCCL), overlapped with the next count")
     ap.add_argument("--prefix-k", type=int, default=None,
@@ -279,6 +281,28 @@ def main():
                          "patterns_per_s": Lq / tl, "positions_per_s": tot / tl,
                          "limit": 100000, "positions_verified": ok}
         del d_sp, d_oo, d_pos, owner, win
+
+    # ---- extract (fm_index.cpp:163-167) on the device, N=1 ----
+    if rank == 0 and world == 1 and args.extract_batch:
+        K_, XL = args.extract_batch, 20
+        g = torch.Generator(device="cpu").manual_seed(7)
+        xpos = torch.randint(0, N - XL, (K_,), generator=g, dtype=torch.int64).to(dev)
+        xlen = torch.full((K_,), XL, dtype=torch.int64, device=dev)
+        xoff = torch.arange(0, (K_ + 1) * XL, XL, dtype=torch.int64, device=dev)
+        xout = torch.empty(K_ * XL, dtype=torch.uint8, device=dev)
+        xt = []
+        for it in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            idx.extract_device(xpos.data_ptr(), xlen.data_ptr(), xoff.data_ptr(), K_,
+                               xout.data_ptr(), sh)
+            torch.cuda.synchronize()
+            xt.append(time.perf_counter() - t1)
+        want = text[(xpos.unsqueeze(1) + torch.arange(XL, device=dev)).long()].reshape(-1)
+        res["extract"] = {"queries": K_, "len": XL, "seconds": min(xt),
+                          "queries_per_s": K_ / min(xt), "bytes_per_s": K_ * XL / min(xt),
+                          "verified": bool(torch.equal(want, xout))}
+        del xpos, xlen, xoff, xout, want
 
     # ---- p50 single-pattern latency (>= 1000 single-pattern calls
     #      through the C++ facade, end to end, as tools/benchmark.cpp:154-166) ----

@@ -70,6 +70,7 @@ SIGNATURES = {
     "cs_fm_create": (C.c_int, [_u8p, C.c_uint64, _u32p, C.c_uint64, C.c_uint32, _u8p, C.c_int,
                                C.POINTER(_vp)]),
     "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "cs_fm_extract_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                              _u64p, _vp]),
@@ -309,6 +310,11 @@ class FMIndex:
     # -- device-resident batches (raw device pointers, e.g. torch data_ptr()) --
     def count_batch_device(self, d_pats: int, d_offs: int, npat: int, d_out: int, stream: int = 0):
         _check(lib().cs_fm_count_batch_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
+
+    def extract_device(self, d_pos, d_len, d_out_offs, k, d_out, stream=0):
+        """Batched extract with device buffers (d_out_offs = scan of clamped lengths)."""
+        _check(lib().cs_fm_extract_device(self._h, d_pos, d_len, d_out_offs, k, d_out,
+                                          stream or None))
 
     def count_bytes_device(self, d_pats, d_offs, npat, d_out, stream=0):
         """Per-query algorithmic HBM bytes of the search (roofline accounting)."""

@@ -496,6 +496,23 @@ cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const u
   return CS_OK;
 }
 
+cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
+                               const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out,
+                               void* stream) {
+  cs_status s = check_handle(h);
+  if (s != CS_OK) return s;
+  if (k && (!d_pos || !d_len || !d_out_offs || !d_out)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  if (!h->lf_exact || !h->nisa) {
+    set_error("device extract needs a text ending in a unique smallest symbol and "
+              "inverse-SA samples");
+    return CS_ERR_UNSUPPORTED;
+  }
+  return launch_extract(h, d_pos, d_len, d_out_offs, k, d_out, (hipStream_t)stream);
+}
+
 cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_t* out,
                         uint64_t* nout) {
   if (!h || !nout) {

@@ -125,11 +125,18 @@ cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_
 /* Batched extract on the device (fm_index.cpp:163-167 semantics: pos >= n gives
  * "", len clamped to n - pos) by LF inversion from inverse-SA samples — the text
  * itself is not needed.  Requires a text whose last symbol is unique and the
- * smallest (the standard terminator; otherwise CS_ERR_UNSUPPORTED).  out_offs has
+ * smallest (the standard terminator) and inverse-SA samples; otherwise the host
+ * copy of the text (as text_) serves, else CS_ERR_UNSUPPORTED.  out_offs has
  * k+1 entries (CSR into out); if *total > cap: CS_ERR_CAPACITY, out_offs valid. */
 cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const uint64_t* len,
                               uint64_t k, uint64_t* out_offs, uint8_t* out, uint64_t cap,
                               uint64_t* total);
+/* Same with device buffers, asynchronous on `stream`: d_out_offs (k+1 entries) must
+ * already hold the clamped lengths' exclusive scan (d_out_offs[q] = sum over r < q of
+ * min(len[r], n - pos[r]) for pos[r] < n, else 0); d_out receives the bytes. */
+cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
+                               const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out,
+                               void* stream);
 
 /* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers. */
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,

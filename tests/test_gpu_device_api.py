@@ -1,0 +1,57 @@
+"""Device-pointer entry points (the *_device forms of include/cs_fmindex.h) against
+their host-buffer twins and the text: count, locate ranges + walk, extract."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from conftest import load_pkg
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, dtype):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dtype).cuda()
+
+
+@pytest.mark.parametrize("kind", ["dna", "bytes"])
+def test_device_forms_match_host(kind):
+    pkg = load_pkg()
+    st = torch.cuda.current_stream().cuda_stream
+    t = (O.gen_dna(5, 100_000) if kind == "dna" else O.gen_bytes(5, 100_000)).tobytes()
+    n = len(t)
+    g = pkg.FMIndex.build_from_text(t)
+    m = 12 if kind == "dna" else 4
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), m, 3000)
+    buf = P.reshape(-1)
+    offs = np.arange(0, (len(P) + 1) * m, m, dtype=np.uint64)
+    want = g.count_batch(buf=buf, offs=offs)
+    d_p, d_o = _dev(buf, torch.uint8), _dev(offs.astype(np.int64), torch.int64)
+    d_c = torch.empty(len(P), dtype=torch.int64, device="cuda")
+    g.count_batch_device(d_p.data_ptr(), d_o.data_ptr(), len(P), d_c.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert d_c.cpu().numpy().astype(np.uint64).tolist() == want.tolist()
+    # locate: ranges + walk == host locate_batch
+    lo, lp = g.locate_batch(buf=buf, offs=offs, limit=7)
+    d_sp = torch.empty(len(P), dtype=torch.int64, device="cuda")
+    d_oo = torch.empty(len(P) + 1, dtype=torch.int64, device="cuda")
+    tot = g.locate_ranges_device(d_p.data_ptr(), d_o.data_ptr(), len(P), 7, d_sp.data_ptr(),
+                                 d_oo.data_ptr(), st)
+    d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device="cuda")
+    g.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), len(P), tot, d_pos.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert d_oo.cpu().numpy().astype(np.uint64).tolist() == np.asarray(lo).tolist()
+    assert d_pos[:tot].cpu().numpy().astype(np.uint64).tolist() == np.asarray(lp).tolist()
+    # extract: clamped slices, including pos >= n and tails
+    rng = np.random.default_rng(3)
+    pos = np.concatenate([rng.integers(0, n, 2000), [n - 1, n - 5, n, n + 3, 0]]).astype(np.int64)
+    ln = np.concatenate([rng.integers(0, 60, 2000), [10, 10, 4, 4, 0]]).astype(np.int64)
+    clamped = np.where(pos < n, np.minimum(ln, n - np.minimum(pos, n)), 0)
+    oo = np.concatenate([[0], np.cumsum(clamped)]).astype(np.int64)
+    d_out = torch.empty(max(int(oo[-1]), 1), dtype=torch.uint8, device="cuda")
+    g.extract_device(_dev(pos, torch.int64).data_ptr(), _dev(ln, torch.int64).data_ptr(),
+                     _dev(oo, torch.int64).data_ptr(), len(pos), d_out.data_ptr(), st)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy().tobytes()
+    for q in range(len(pos)):
+        assert out[oo[q]:oo[q + 1]] == t[pos[q]:pos[q] + ln[q]], q
