@@ -49,8 +49,10 @@ def test_device_forms_match_host(kind):
     clamped = np.where(pos < n, np.minimum(ln, n - np.minimum(pos, n)), 0)
     oo = np.concatenate([[0], np.cumsum(clamped)]).astype(np.int64)
     d_out = torch.empty(max(int(oo[-1]), 1), dtype=torch.uint8, device="cuda")
-    g.extract_device(_dev(pos, torch.int64).data_ptr(), _dev(ln, torch.int64).data_ptr(),
-                     _dev(oo, torch.int64).data_ptr(), len(pos), d_out.data_ptr(), st)
+    d_pos_x, d_len_x, d_oo_x = (_dev(pos, torch.int64), _dev(ln, torch.int64),
+                                _dev(oo, torch.int64))  # kept alive across the launch
+    g.extract_device(d_pos_x.data_ptr(), d_len_x.data_ptr(), d_oo_x.data_ptr(), len(pos),
+                     d_out.data_ptr(), st)
     torch.cuda.synchronize()
     out = d_out.cpu().numpy().tobytes()
     for q in range(len(pos)):
