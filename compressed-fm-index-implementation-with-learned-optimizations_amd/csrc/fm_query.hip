@@ -771,9 +771,9 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^28, max(4096, n/8)) entries (8 B each, 16 B in wide indexes:
-// at most n resp. 2n bytes, capped at 2 resp. 4 GiB); none when k < 2.
-// DNA: k = 11 at 100 MB, k = 14 from 2.1 GB on.  Entries are (sp, ep) as 2 x u32, or
+// sigma^k <= min(2^30, max(4096, n/8)) entries (8 B each, 16 B in wide indexes:
+// at most n resp. 2n bytes, capped at 8 resp. 16 GiB); none when k < 2.
+// DNA: k = 11 at 100 MB, k = 14 at 4 GB, k = 15 at 32 GB.  Entries are (sp, ep) as 2 x u32, or
 // 2 x u64 in wide indexes.  CS_FM_PREFIX_K overrides k (0 = off).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
@@ -793,7 +793,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   }
   if (sigma == 0) return CS_OK;
   uint64_t cap = n / 8 > 4096 ? n / 8 : 4096;
-  if (cap > (1ull << 28)) cap = 1ull << 28;
+  if (cap > (1ull << 30)) cap = 1ull << 30;
   uint32_t k = 0;
   uint64_t entries = 1;
   while (k < 32 && entries * sigma <= cap) {
@@ -804,7 +804,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     const int want = std::atoi(e);
     k = 0;
     entries = 1;
-    while ((int)k < want && entries * sigma <= (1ull << 28)) {
+    while ((int)k < want && entries * sigma <= (1ull << 30)) {
       entries *= sigma;
       ++k;
     }

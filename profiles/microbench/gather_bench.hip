@@ -5,7 +5,7 @@
 // "Other access widths are uncalibrated: calibrate on a known byte count").
 //
 //   hipcc -O3 --offload-arch=gfx950 gather_bench.hip -o gather_bench
-//   ./gather_bench [table_GB=4] [reads_M=256]
+//   ./gather_bench [table_GB=4] [reads_M=256] [contiguous=0]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -140,9 +140,14 @@ int main(int argc, char** argv) {
   const double gb = argc > 1 ? std::atof(argv[1]) : 4.0;
   const uint64_t reads = (uint64_t)((argc > 2 ? std::atof(argv[2]) : 256.0) * 1e6);
   const uint64_t bytes = (uint64_t)(gb * 1e9) & ~(uint64_t)127;
+  const int contiguous = argc > 3 ? std::atoi(argv[3]) : 0;  // hipDeviceMallocContiguous
   uint4* tab;
   uint32_t* sink;
-  CK(hipMalloc(&tab, bytes));
+  if (contiguous)
+    CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&tab), bytes, hipDeviceMallocContiguous));
+  else
+    CK(hipMalloc(&tab, bytes));
+  std::printf("allocation: %s\n", contiguous ? "hipDeviceMallocContiguous" : "hipMalloc");
   CK(hipMalloc(&sink, 4096));
   k_fill<<<8192, 256>>>(reinterpret_cast<uint64_t*>(tab), bytes / 8);
   CK(hipDeviceSynchronize());
