@@ -1,4 +1,7 @@
-// fm_device.hpp — HBM layout of the index and the device-side rank primitives.
+// fm_device.hpp — HBM layout of the index and the device-side rank primitives:
+// the binary wavelet matrix's rank lines (Line32 / Line32W / Line64, below), the
+// occurrence lines shared by the occurrence engine and the quaternary wavelet
+// matrix (OccLine), and the locate walk lines (WalkLine / WalkLineW).
 //
 // Wavelet matrix (the reference's "WaveletTree", src/core/wavelet.cpp:14-53): 8
 // levels, level l holds bit (7-l) of the level-l sequence; the next sequence is the
@@ -37,8 +40,8 @@ constexpr int kNodes = 255;  // internal nodes, levels 0..7
 constexpr uint8_t kPure = 1, kPureBit = 2;
 constexpr int kMaxExc = 128;  // occurrence-line engine: rare-symbol rows kept in LDS
 
-// Everything the query kernels read besides the rank lines; copied into LDS by
-// every block (8.5 KB).
+// Everything the query kernels read besides the lines; copied into LDS by every
+// block (10.3 KB).
 struct NodeTable {
   uint64_t S[kNodes];   // node start in its level
   uint64_t R[kNodes];   // rank1_l(S)

@@ -2,22 +2,27 @@
 // src/api/fm_index.cpp:79-101) and the LF/SSA walk of FMIndex::locate
 // (src/api/fm_index.cpp:107-157), as hand-written CDNA4 kernels.
 //
-// count: one lane per live pattern.  Per pattern character c the lane runs
-// WaveletTree::rank (src/core/wavelet.cpp:59-96) for sp and ep at once, in the
-// "relative" form: the start chain of c (start=0 mapped through the levels) is
-// fixed per symbol, so only d = end - start is carried:
-//     per level l with c's node not pure:  r = rank1_l(S + d) - R;  d = bit ? r : d - r
-// (S, R from the node table in LDS).  rank1_l = one rank-line read (fm_device.hpp).
-// The first character costs nothing (sp = C[c], ep = C[c+1]); absent symbols and
-// empty ranges exit early exactly where the reference returns 0.
+// Every kernel is a template over a rank ENGINE (occ(c, i) for a search step, and
+// LF with the BWT symbol), dispatched on the index's format (FMX_DISPATCH):
+//   OccE        occurrence lines: one 32-B line per rank of any symbol (<= 4
+//               frequent symbols, rare rows listed in the node table);
+//   QWM         quaternary wavelet matrix of occurrence lines: one line per base-4
+//               level (any alphabet; 4 levels for sigma = 256);
+//   WM<F>       the reference's binary wavelet matrix (WaveletTree::rank,
+//               src/core/wavelet.cpp:59-96) in rank lines F, in the "relative"
+//               form: per level l with c's node not pure
+//                   r = rank1_l(S + d) - R;  d = bit ? r : d - r.
+// The node table (C[], node starts/ranks, code maps, rare rows) is staged in LDS per
+// block.  The first k characters come from the prefix table (a k-mer -> (sp, ep)
+// generalisation of C[]); absent symbols and empty ranges exit early exactly where
+// the reference returns 0.
 //
-// locate: (1) same search, writing sp and min(count, limit); (2) exclusive scan ->
+// locate: (1) the same search writes sp and min(count, limit); (2) exclusive scan ->
 // CSR offsets; (3) rows expanded in row order (fm_index.cpp:125); (4) a persistent
-// walk kernel: each block owns a contiguous slice of rows and its lanes pull rows
-// from an LDS counter, so the geometric LF-walk lengths (row-sampled SSA, SURVEY
-// §0.5) do not idle a wave behind its longest walk.  LF (fm_index.hpp:62-66) is
-// computed by one descent that reads the BWT symbol and its rank from the same
-// rank lines (WaveletTree::access + rank fused), no separate BWT array.
+// walk kernel: each block owns a contiguous slice of rows, its lanes pull rows from
+// an LDS counter and cycle fetch -> walk -> sample with one dependent load per loop
+// iteration.  With walk lines (fm_device.hpp WalkLine) one 32-B read per step gives
+// the symbol, its occ and the sample mark; no separate BWT array is kept.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
