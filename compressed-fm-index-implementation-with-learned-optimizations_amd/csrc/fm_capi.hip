@@ -25,7 +25,7 @@ cs_status hip_fail(hipError_t e, const char* what) {
 
 namespace {
 
-cs_status use_device(int dev) {
+cs_status use_device(int dev, DeviceScope& ds) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
     (void)hipGetLastError();
@@ -36,16 +36,16 @@ cs_status use_device(int dev) {
     set_error("device ordinal out of range");
     return CS_ERR_INVALID;
   }
-  FMX_HIP(hipSetDevice(dev));
+  FMX_HIP(ds.enter(dev));
   return CS_OK;
 }
 
-cs_status check_handle(const cs_fm_index* h) {
+cs_status check_handle(const cs_fm_index* h, DeviceScope& ds) {
   if (!h) {
     set_error("null index handle");
     return CS_ERR_INVALID;
   }
-  return use_device(h->device);
+  return use_device(h->device, ds);
 }
 
 // Lazily allocate the handle's small-batch arena (caller holds scratch.mu).
@@ -108,7 +108,8 @@ cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params*
   cs_build_params dp;
   cs_default_build_params(&dp);
   if (!p) p = &dp;
-  cs_status s = use_device(device);
+  DeviceScope dscope;
+  cs_status s = use_device(device, dscope);
   if (s != CS_OK) return s;
   auto* h = new (std::nothrow) cs_fm_index();
   if (!h) return CS_ERR_OOM;
@@ -153,7 +154,8 @@ cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_
     set_error("null text");
     return CS_ERR_INVALID;
   }
-  cs_status s = use_device(device);
+  DeviceScope dscope;
+  cs_status s = use_device(device, dscope);
   if (s != CS_OK) return s;
   DevBuf d;
   FMX_HIP(d.alloc(n + 16));
@@ -178,7 +180,8 @@ cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint
     return CS_ERR_INVALID;
   }
   *out = nullptr;
-  cs_status s = use_device(device);
+  DeviceScope dscope;
+  cs_status s = use_device(device, dscope);
   if (s != CS_OK) return s;
   auto* h = new (std::nothrow) cs_fm_index();
   if (!h) return CS_ERR_OOM;
@@ -208,7 +211,8 @@ cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out) {
 
 void cs_fm_destroy(cs_fm_index* h) {
   if (!h) return;
-  (void)hipSetDevice(h->device);
+  DeviceScope dscope;
+  (void)dscope.enter(h->device);
   free_index(h);
 }
 
@@ -242,7 +246,8 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
 cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (npat && (!d_offs || !d_out)) {
     set_error("null batch pointer");
@@ -254,7 +259,8 @@ cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
 cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (npat && (!d_offs || !d_out)) {
     set_error("null batch pointer");
@@ -265,7 +271,8 @@ cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
 
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
                             uint64_t npat, uint64_t* out_counts, void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!npat) return CS_OK;
   if (!offs || !out_counts || (!pats && offs[npat] != offs[0])) {
@@ -347,7 +354,8 @@ cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats
                                      const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                      uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
                                      void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!total || !d_out_offs || (npat && (!d_offs || !d_sp))) {
     set_error("null batch pointer");
@@ -360,7 +368,8 @@ cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats
 cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d_sp,
                                          const uint64_t* d_out_offs, uint64_t npat,
                                          uint64_t total, uint64_t* d_out_pos, void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
     set_error("null batch pointer");
@@ -370,23 +379,44 @@ cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d
 }
 
 cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
-  return check_locate_error(h, nullptr, 0, (hipStream_t)stream);
+  return check_locate_error(h, nullptr, (hipStream_t)stream);
+}
+
+// Per-call overrun word: concurrent synchronous locates on distinct streams do not
+// share the handle's flag (the handle is immutable after creation).
+static cs_status walk_checked(const cs_fm_index* h, const uint64_t* d_sp,
+                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                              uint64_t* d_out_pos, hipStream_t st) {
+  StreamBuf err;
+  FMX_HIP(err.alloc(8, st));
+  FMX_HIP(hipMemsetAsync(err.p, 0xFF, 8, st));
+  unsigned long long* e = err.as<unsigned long long>();
+  cs_status s = launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, st, e);
+  if (s != CS_OK) return s;
+  return check_locate_error(h, e, st);
 }
 
 cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,
                                    const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                                    uint64_t* d_out_pos, void* stream) {
-  cs_status s = cs_fm_locate_walk_device_async(h, d_sp, d_out_offs, npat, total, d_out_pos, stream);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
-  return check_locate_error(h, d_out_offs, npat, (hipStream_t)stream);
+  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return walk_checked(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream);
 }
 
 cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
                              uint64_t npat, uint64_t limit, uint64_t* out_offs, uint64_t* out_pos,
                              uint64_t cap, uint64_t* total, void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!total || !out_offs) {
     set_error("null batch pointer");
@@ -420,10 +450,8 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
   }
   StreamBuf d_pos;
   FMX_HIP(d_pos.alloc(*total * 8, st));
-  s = launch_locate_walk(h, d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), npat, *total,
-                         d_pos.as<uint64_t>(), st);
-  if (s != CS_OK) return s;
-  s = check_locate_error(h, d_oo.as<uint64_t>(), npat, st);
+  s = walk_checked(h, d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), npat, *total,
+                   d_pos.as<uint64_t>(), st);
   if (s != CS_OK) return s;
   FMX_HIP(hipMemcpyAsync(out_pos, d_pos.p, *total * 8, hipMemcpyDeviceToHost, st));
   FMX_HIP(hipStreamSynchronize(st));
@@ -448,7 +476,8 @@ cs_status cs_fm_locate(const cs_fm_index* h, const uint8_t* pattern, uint64_t m,
 cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const uint64_t* len,
                               uint64_t k, uint64_t* out_offs, uint8_t* out, uint64_t cap,
                               uint64_t* total) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!total || !out_offs || (k && (!pos || !len))) {
     set_error("null argument");
@@ -499,7 +528,8 @@ cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const u
 cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
                                const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out,
                                void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (k && (!d_pos || !d_len || !d_out_offs || !d_out)) {
     set_error("null batch pointer");
@@ -543,7 +573,8 @@ cs_status cs_fm_extract(const cs_fm_index* h, uint64_t pos, uint64_t len, uint8_
 // ---- building blocks (host arrays) ----
 template <class In, class Out, class F>
 static cs_status run_host(const cs_fm_index* h, const In* in, uint64_t k, Out* out, F launch) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!k) return CS_OK;
   DevBuf di, dout;
@@ -571,7 +602,8 @@ cs_status cs_fm_level_rank1(const cs_fm_index* h, int level, const uint64_t* pos
 
 cs_status cs_fm_wt_rank(const cs_fm_index* h, const uint8_t* syms, const uint64_t* pos, uint64_t k,
                         uint64_t* out) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!k) return CS_OK;
   DevBuf ds;
@@ -604,7 +636,8 @@ cs_status cs_fm_get_C(const cs_fm_index* h, uint64_t* out257) {
 }
 
 cs_status cs_fm_bwt_device(const cs_fm_index* h, uint8_t* d_out, void* stream) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!h->n) return CS_OK;
   if (!d_out) {
@@ -615,7 +648,8 @@ cs_status cs_fm_bwt_device(const cs_fm_index* h, uint8_t* d_out, void* stream) {
 }
 
 cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint64_t* len) {
-  cs_status s = check_handle(h);
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   if (!len) return CS_ERR_INVALID;
   *len = h->nsamples;
@@ -631,7 +665,8 @@ cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint6
 }
 
 cs_status cs_sa_build(const uint8_t* text, uint64_t n, uint32_t* sa_out, int device) {
-  cs_status s = use_device(device);
+  DeviceScope dscope;
+  cs_status s = use_device(device, dscope);
   if (s != CS_OK) return s;
   if (!n) return CS_OK;
   if (!text || !sa_out) {

@@ -118,11 +118,14 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
                                hipStream_t st);
+// err: device word receiving the smallest overrunning row index (UINT64_MAX = none);
+// null = the handle's shared flag (the asynchronous API, cs_fm_locate_check)
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                             uint64_t* d_out_pos, hipStream_t st);
-cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, uint64_t npat,
-                             hipStream_t st);
+                             uint64_t* d_out_pos, hipStream_t st,
+                             unsigned long long* err = nullptr);
+// reads (and re-arms) the overrun word `err` (null = the handle's shared flag)
+cs_status check_locate_error(const cs_fm_index* h, unsigned long long* err, hipStream_t st);
 cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
                              uint64_t* d_out, hipStream_t st);
 cs_status launch_wt_rank(const cs_fm_index* h, const uint8_t* d_syms, const uint64_t* d_pos,
@@ -149,6 +152,27 @@ struct DevBuf {
   }
   template <class T> T* as() const { return static_cast<T*>(p); }
   void release() { if (p) (void)hipFree(p); p = nullptr; }
+};
+
+// Entry points select the index's device and restore the caller's current device on
+// return, so a process driving several GPUs keeps its own device selection.
+struct DeviceScope {
+  int prev = -1;
+  DeviceScope() = default;
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+  hipError_t enter(int dev) {
+    int cur = 0;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) return e;
+    if (cur == dev) return hipSuccess;
+    e = hipSetDevice(dev);
+    if (e == hipSuccess) prev = cur;
+    return e;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
 };
 
 // Stream-ordered scratch for the query paths: hipMallocAsync / hipFreeAsync on the

@@ -94,7 +94,8 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
     set_error("null argument");
     return CS_ERR_INVALID;
   }
-  FMX_HIP(hipSetDevice(h->device));
+  DeviceScope ds;
+  FMX_HIP(ds.enter(h->device));
   errno = 0;
   if (mkdir(dir, 0755) != 0 && errno != EEXIST) return io_fail(std::string("cannot create: ") + dir);
   errno = 0;
@@ -203,7 +204,8 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     cs_fm_destroy(h);
     return s;
   };
-  if (hipSetDevice(device) != hipSuccess) return fail(hip_fail(hipGetLastError(), "hipSetDevice"));
+  DeviceScope ds;
+  if (ds.enter(device) != hipSuccess) return fail(hip_fail(hipGetLastError(), "hipSetDevice"));
   {
     FILE* t = std::fopen(join(d, "table.bin").c_str(), "rb");
     if (!t || std::fread(&h->h_table, sizeof h->h_table, 1, t) != 1) {

@@ -884,7 +884,7 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
 
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                             uint64_t* d_out_pos, hipStream_t st) {
+                             uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word) {
   if (!total) return CS_OK;
   StreamBuf rows;
   FMX_HIP(rows.alloc(total * 8, st));
@@ -899,7 +899,8 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   if (chunk < 64) chunk = 64;
   const unsigned blocks = (unsigned)((total + chunk - 1) / chunk);
   const DevIndex ix = h->dev();
-  unsigned long long* err = reinterpret_cast<unsigned long long*>(h->d_err);
+  unsigned long long* err =
+      err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
   if (h->d_walk) {
@@ -947,16 +948,14 @@ void keep_pool(int device) {
   });
 }
 
-cs_status check_locate_error(const cs_fm_index* h, const uint64_t* d_out_offs, uint64_t npat,
-                             hipStream_t st) {
+cs_status check_locate_error(const cs_fm_index* h, unsigned long long* err, hipStream_t st) {
+  if (!err) err = reinterpret_cast<unsigned long long*>(h->d_err);
   uint64_t bad = ~0ull;
-  FMX_HIP(hipMemcpyAsync(&bad, h->d_err, 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(&bad, err, 8, hipMemcpyDeviceToHost, st));
   FMX_HIP(hipStreamSynchronize(st));
   if (bad == ~0ull) return CS_OK;
-  FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
+  FMX_HIP(hipMemsetAsync(err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));
-  (void)d_out_offs;
-  (void)npat;
   set_error("locate: LF walk exceeded text length");  // fm_index.cpp:137
   return CS_ERR_LF_OVERRUN;
 }

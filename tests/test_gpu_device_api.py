@@ -57,3 +57,46 @@ def test_device_forms_match_host(kind):
     out = d_out.cpu().numpy().tobytes()
     for q in range(len(pos)):
         assert out[oo[q]:oo[q + 1]] == t[pos[q]:pos[q] + ln[q]], q
+
+
+def test_concurrent_calls_share_nothing_mutable():
+    """The handle is immutable after creation and safe from several host threads
+    (SURVEY §8(b)): count / locate from 8 threads at once, on an index whose LF walk
+    overruns for some patterns (no terminator) and not for others, give each call its
+    serial result or its own overrun error."""
+    import threading
+    pkg = load_pkg()
+    t = b"abcab" * 60 + b"ab" * 40  # no unique terminator: some walks cycle
+    g = pkg.FMIndex.build_from_text(t, pkg.BuildParams(ssa_stride=8))
+    o = O.Index(t, ssa_stride=8)
+    pats = sorted({t[i:i + k] for i in range(0, 200, 7) for k in (1, 2, 3, 5)})
+    serial = {}
+    for p in pats:
+        try:
+            serial[p] = ("ok", o.locate(p, limit=20), o.count(p))
+        except RuntimeError as e:
+            serial[p] = ("err", str(e), o.count(p))
+    assert any(v[0] == "err" for v in serial.values()) and any(v[0] == "ok" for v in serial.values())
+    bad = []
+
+    def worker(seed):
+        rng = np.random.default_rng(seed)
+        for _ in range(60):
+            p = pats[rng.integers(len(pats))]
+            kind, want, cnt = serial[p]
+            if g.count(p) != cnt:
+                bad.append(("count", p))
+            try:
+                got = g.locate(p, limit=20)
+                if kind != "ok" or got != want:
+                    bad.append(("locate", p))
+            except RuntimeError as e:
+                if kind != "err" or str(e) != want:
+                    bad.append(("error", p))
+
+    th = [threading.Thread(target=worker, args=(s,)) for s in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad, bad[:5]
