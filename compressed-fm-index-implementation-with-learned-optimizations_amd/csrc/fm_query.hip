@@ -66,7 +66,9 @@ __device__ __forceinline__ bool search_step(const DevIndex& ix, const NodeTable&
       if (bytes) *bytes += (qa == qe ? 1u : 2u) * F::kBytes;  // distinct lines (measurement)
       typename F::Raw va, ve;
       F::load(lv, qa, va);
-      F::load(lv, qe, ve);
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(va) / sizeof(va[0])); ++k) ve[k] = va[k];
+      if (qe != qa) F::load(lv, qe, ve);  // sp and ep in one line: one read
       const uint64_t rs = F::base(va) + F::prefix(va, oa) - R;
       const uint64_t re = F::base(ve) + F::prefix(ve, oe) - R;
       const bool b = (c >> (7 - l)) & 1u;
