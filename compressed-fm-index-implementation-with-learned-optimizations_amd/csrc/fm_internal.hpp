@@ -100,6 +100,20 @@ cs_status hip_fail(hipError_t e, const char* what);
 
 // Index construction on the device (fm_build.hip).
 cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t st);
+
+// Rank structures from a BWT in HBM (fm_build_rank.hip).
+struct CodeMap {
+  uint8_t c[256];  // 2-bit code per symbol, kNoCode for the rare ones
+};
+cs_status build_wm_levels(uint8_t* bwt, uint64_t n, cs_fm_index* h, hipStream_t st);
+bool occ_feasible(const unsigned long long* hist, uint64_t n, CodeMap& map, uint8_t occ_sym[4]);
+cs_status build_occ(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
+                    hipStream_t st);
+cs_status build_qwm(const uint8_t* bwt, uint64_t n, const unsigned long long* hist,
+                    cs_fm_index* h, hipStream_t st);
+cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
+                     hipStream_t st);
+cs_status launch_node_ranks(const cs_fm_index* h, uint64_t* d_R, hipStream_t st);
 cs_status build_index_from_bwt(const uint8_t* bwt_host, uint64_t n, const uint32_t* ssa_host,
                                uint64_t nsamples, uint32_t stride, cs_fm_index* h, hipStream_t st);
 cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, bool wide,
