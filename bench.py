@@ -61,7 +61,9 @@ def main():
     ap.add_argument("--m", type=int, default=20)
     ap.add_argument("--batch", type=int, default=12_500_000, help="patterns per GPU per step")
     ap.add_argument("--ssa-stride", type=int, default=32)
-    ap.add_argument("--cpu-queries", type=int, default=16)
+    ap.add_argument("--cpu-queries", type=int, default=None,
+                    help="patterns timed on the CPU (default SURVEY §8(d): 256 at C2-size texts, "
+                         "32 at C3, 16 at C4 and above)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p50-calls", type=int, default=1000)
@@ -333,6 +335,8 @@ def main():
         res["in_batch_us_per_query"] = elapsed / args.steps / B * 1e6
 
     # ---- CPU baseline: reference-faithful restatement on host cores (rank 0, N=1) ----
+    if args.cpu_queries is None:
+        args.cpu_queries = 256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_queries > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline / checker only
