@@ -48,6 +48,17 @@ cs_status check_handle(const cs_fm_index* h, DeviceScope& ds) {
   return use_device(h->device, ds);
 }
 
+// Host batches: offsets must be non-decreasing (pattern q = [offs[q], offs[q+1])),
+// else a kernel would read past the staged bytes.
+cs_status check_offsets(const uint64_t* offs, uint64_t npat) {
+  for (uint64_t q = 0; q < npat; ++q)
+    if (offs[q + 1] < offs[q]) {
+      set_error("pattern offsets must be non-decreasing");
+      return CS_ERR_INVALID;
+    }
+  return CS_OK;
+}
+
 // Lazily allocate the handle's small-batch arena (caller holds scratch.mu).
 cs_status scratch_ready(const cs_fm_index* h) {
   if (h->scratch.h) return CS_OK;
@@ -279,6 +290,7 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
+  if ((s = check_offsets(offs, npat)) != CS_OK) return s;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t bytes = offs[npat] - offs[0];
   const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
@@ -427,6 +439,11 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
     out_offs[0] = 0;
     return CS_OK;
   }
+  if (!offs || (!pats && offs[npat] != offs[0])) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  if ((s = check_offsets(offs, npat)) != CS_OK) return s;
   hipStream_t st = (hipStream_t)stream;
   StagedBatch b;
   s = b.load(pats, offs, npat, st);

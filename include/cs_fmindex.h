@@ -138,7 +138,9 @@ cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, cons
                                const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out,
                                void* stream);
 
-/* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers. */
+/* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers; offsets must
+ * be non-decreasing (checked: CS_ERR_INVALID).  The *_device forms take the same
+ * layout in device memory, unchecked. */
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
                             uint64_t npat, uint64_t* out_counts, void* stream);
 /* Batched locate, host buffers.  out_offs has npat+1 entries (CSR into out_pos).

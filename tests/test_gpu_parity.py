@@ -229,6 +229,15 @@ def test_fm_golden(pkg, case):
     _check_fm_case(pkg, case)
 
 
+def test_bad_offsets_rejected(pkg):
+    g = pkg.FMIndex.build_from_text(b"banana$")
+    buf = np.frombuffer(b"anaban", np.uint8)
+    with pytest.raises(pkg.FMIndexError, match="non-decreasing"):
+        g.count_batch(buf=buf, offs=np.array([0, 3, 1, 6], np.uint64))
+    with pytest.raises(pkg.FMIndexError, match="non-decreasing"):
+        g.locate_batch(buf=buf, offs=np.array([0, 4, 2], np.uint64))
+
+
 def test_batch_edge_cases(pkg):
     t = O.gen_dna(7, 20000).tobytes()
     g = pkg.FMIndex.build_from_text(t)
