@@ -109,16 +109,15 @@ void free_index(cs_fm_index* h) {
   delete h;
 }
 
-cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params* p, int device,
-                       cs_fm_index** out, const uint8_t* host_text) {
+// A new handle on `device`, filled by body(h, stream) on a private stream; freed
+// again if the body fails.
+template <class Body>
+cs_status build_handle(int device, cs_fm_index** out, Body&& body) {
   if (!out) {
     set_error("null output handle");
     return CS_ERR_INVALID;
   }
   *out = nullptr;
-  cs_build_params dp;
-  cs_default_build_params(&dp);
-  if (!p) p = &dp;
   DeviceScope dscope;
   cs_status s = use_device(device, dscope);
   if (s != CS_OK) return s;
@@ -130,16 +129,27 @@ cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params*
     delete h;
     return hip_fail(hipGetLastError(), "hipStreamCreate");
   }
-  s = build_index_device(d_text, n, p->ssa_stride, h, st);
+  s = body(h, st);
   (void)hipStreamSynchronize(st);
   (void)hipStreamDestroy(st);
   if (s != CS_OK) {
     free_index(h);
     return s;
   }
-  if (host_text) h->h_text.assign(host_text, host_text + n);
   *out = h;
   return CS_OK;
+}
+
+cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params* p, int device,
+                       cs_fm_index** out, const uint8_t* host_text) {
+  cs_build_params dp;
+  cs_default_build_params(&dp);
+  if (!p) p = &dp;
+  return build_handle(device, out, [&](cs_fm_index* h, hipStream_t st) {
+    cs_status s = build_index_device(d_text, n, p->ssa_stride, h, st);
+    if (s == CS_OK && host_text) h->h_text.assign(host_text, host_text + n);
+    return s;
+  });
 }
 
 }  // namespace
@@ -186,32 +196,15 @@ cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
 
 cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint64_t nsamples,
                        uint32_t ssa_stride, const uint8_t* text, int device, cs_fm_index** out) {
-  if (!out || (n && (!bwt || !ssa))) {
+  if (n && (!bwt || !ssa)) {
     set_error("null argument");
     return CS_ERR_INVALID;
   }
-  *out = nullptr;
-  DeviceScope dscope;
-  cs_status s = use_device(device, dscope);
-  if (s != CS_OK) return s;
-  auto* h = new (std::nothrow) cs_fm_index();
-  if (!h) return CS_ERR_OOM;
-  h->device = device;
-  hipStream_t st;
-  if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
-    delete h;
-    return hip_fail(hipGetLastError(), "hipStreamCreate");
-  }
-  s = build_index_from_bwt(bwt, n, ssa, nsamples, ssa_stride, h, st);
-  (void)hipStreamSynchronize(st);
-  (void)hipStreamDestroy(st);
-  if (s != CS_OK) {
-    free_index(h);
+  return build_handle(device, out, [&](cs_fm_index* h, hipStream_t st) {
+    cs_status s = build_index_from_bwt(bwt, n, ssa, nsamples, ssa_stride, h, st);
+    if (s == CS_OK && text) h->h_text.assign(text, text + n);
     return s;
-  }
-  if (text) h->h_text.assign(text, text + n);
-  *out = h;
-  return CS_OK;
+  });
 }
 
 cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out) {
