@@ -254,6 +254,12 @@ def test_batch_edge_cases(pkg):
     assert g.count_batch([]).tolist() == []
     assert g.count(b"") == len(t)
     assert g.locate(b"") == []
+    # each host path: single pattern in the kernel arguments (<= 128 B), through the
+    # pinned arena (longer, or small batches), and staged through HBM (> 1 MiB)
+    for p in (t[5:133], t[5:134], t[100:1100]):
+        assert g.count(p) == o.count(p)
+    big = [t[i:i + 30] for i in rng.integers(0, 19900, 40000)]  # 1.2 MB of patterns
+    assert g.count_batch(big).tolist() == [o.count(p) for p in big]
 
 
 @pytest.mark.parametrize("gen,m", [("dna", 20), ("bytes", 8)])
