@@ -77,6 +77,8 @@ def main():
                     help="patterns timed through the oracle's fast (precomputed) count, all threads")
     ap.add_argument("--extract-batch", type=int, default=1_000_000,
                     help="random 20-byte extracts timed on the device (N=1 only; 0 = skip)")
+    ap.add_argument("--host-batch", type=int, default=1,
+                    help="also time the batch handed over in host memory (PCIe-inclusive; 0 = skip)")
     ap.add_argument("--gather", action="store_true",
                     help="gather every step's counts to rank 0 (RCCL), overlapped with the next count")
     ap.add_argument("--prefix-k", type=int, default=None,
@@ -283,6 +285,21 @@ def main():
                          "patterns_per_s": Lq / tl, "positions_per_s": tot / tl,
                          "limit": 100000, "positions_verified": ok}
         del d_sp, d_oo, d_pos, owner, win
+
+    # ---- the same batch handed over in host memory (cs_fm_count_batch: PCIe in and out
+    #      inside the call), N=1 only: reported beside value, never as value ----
+    if rank == 0 and world == 1 and args.host_batch:
+        hbuf = pats.cpu().numpy()
+        hoffs = offs.cpu().numpy().astype(np.uint64)
+        ht = []
+        for it in range(3):
+            t1 = time.perf_counter()
+            hc = idx.count_batch(buf=hbuf, offs=hoffs)
+            ht.append(time.perf_counter() - t1)
+        res["host_batch"] = {"patterns": B, "seconds": min(ht), "patterns_per_s": B / min(ht),
+                             "h2d_bytes": int(hbuf.nbytes + hoffs.nbytes),
+                             "matches_device_batch": bool(np.array_equal(hc, counts.astype(np.uint64)))}
+        del hbuf, hoffs, hc
 
     # ---- extract (fm_index.cpp:163-167) on the device, N=1 ----
     if rank == 0 and world == 1 and args.extract_batch:
