@@ -74,15 +74,46 @@ cs_status scratch_ready(const cs_fm_index* h) {
   return CS_OK;
 }
 
+// Page-locks a large caller buffer for the duration of a call, so its copies run as
+// DMA at PCIe rate instead of through the runtime's pageable staging; small buffers
+// and buffers that cannot be registered (e.g. already pinned) are left alone.
+struct HostPin {
+  static constexpr uint64_t kMinBytes = 16ull << 20;
+  void* base = nullptr;
+  hipStream_t st = nullptr;
+  HostPin() = default;
+  HostPin(const HostPin&) = delete;
+  HostPin& operator=(const HostPin&) = delete;
+  void pin(const void* p, uint64_t bytes, hipStream_t s) {
+    if (bytes < kMinBytes || base) return;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
+    const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095);
+    if (hipHostRegister(reinterpret_cast<void*>(a), e - a, hipHostRegisterDefault) == hipSuccess) {
+      base = reinterpret_cast<void*>(a);
+      st = s;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
+  ~HostPin() {
+    if (!base) return;
+    (void)hipStreamSynchronize(st);  // no copy may still read the pages
+    (void)hipHostUnregister(base);
+  }
+};
+
 // Stage a host pattern batch into HBM.
 struct StagedBatch {
+  HostPin pin_pats, pin_offs;
   StreamBuf pats, offs;
   cs_status load(const uint8_t* p, const uint64_t* o, uint64_t npat, hipStream_t st) {
     const uint64_t bytes = o[npat] - o[0];
     FMX_HIP(pats.alloc(bytes + 16, st));
     FMX_HIP(offs.alloc((npat + 1) * 8, st));
+    pin_pats.pin(p + o[0], bytes, st);
     if (bytes) FMX_HIP(hipMemcpyAsync(pats.p, p + o[0], bytes, hipMemcpyHostToDevice, st));
     if (o[0] == 0) {
+      pin_offs.pin(o, (npat + 1) * 8, st);
       FMX_HIP(hipMemcpyAsync(offs.p, o, (npat + 1) * 8, hipMemcpyHostToDevice, st));
     } else {  // rebase so offsets index the staged bytes
       std::vector<uint64_t> r(npat + 1);
@@ -338,11 +369,13 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     std::memcpy(out_counts, hp + o_out, npat * 8);
     return CS_OK;
   }
+  HostPin pin_out;
   StagedBatch b;
   s = b.load(pats, offs, npat, st);
   if (s != CS_OK) return s;
   StreamBuf d_out;
   FMX_HIP(d_out.alloc(npat * 8, st));
+  pin_out.pin(out_counts, npat * 8, st);
   s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
   if (s != CS_OK) return s;
   FMX_HIP(hipMemcpyAsync(out_counts, d_out.p, npat * 8, hipMemcpyDeviceToHost, st));
