@@ -570,6 +570,8 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
   const uint64_t n = ix.n;
   uint64_t j = 0, pos = 0, steps = 0, sidx = 0;
   uint32_t phase = kFetch;
+  bool from_ssa = false;  // the stop row is one of the reference's sampled rows
+  const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
   for (;;) {
     if (phase == kFetch) {
       j = atomicAdd(&next, 1ull);
@@ -585,19 +587,25 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
       W::locate(pos, q, o);
       W::load(ix.walk, q, v);
     }
-    if (phase == kSample) smp = wssa_at(ix, sidx);
+    if (phase == kSample) smp = from_ssa ? ssa_at(ix, sidx) : wssa_at(ix, sidx);
     // ---- consume ----
     if (phase == kFetch) {
       pos = row;
       steps = 0;
       phase = kWalk;
     } else if (phase == kWalk) {
-      if (W::mark(v, o) || steps >= n) {  // fm_index.cpp:130 loop condition
-        if (steps >= n) {                  // :136-138, checked first
+      // a walk may stop at a marked row or at a row the reference samples
+      // (row % stride == 0, SSA): both give SA[start] = sample + steps, and the
+      // first of the two comes sooner (mean 11 steps at stride 32 instead of 15.5)
+      const bool mk = W::mark(v, o);
+      const bool rs = row_mask ? (pos & row_mask) == 0 : pos % ix.stride == 0;
+      if (mk || rs || steps >= n) {  // fm_index.cpp:130 loop condition
+        if (steps >= n) {            // :136-138, checked first
           atomicMin(err, (unsigned long long)j);
           phase = kFetch;
         } else {
-          sidx = W::mark_rank(v, o);
+          from_ssa = !mk;
+          sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
           phase = kSample;
         }
       } else if (!kQ) {  // LF = C[c] + occ(c, pos) from the same line (OccE::lf)
