@@ -79,6 +79,9 @@ def main():
                     help="random 20-byte extracts timed on the device (N=1 only; 0 = skip)")
     ap.add_argument("--host-batch", type=int, default=1,
                     help="also time the batch handed over in host memory (PCIe-inclusive; 0 = skip)")
+    ap.add_argument("--replicate", default="build", choices=["build", "broadcast"],
+                    help="N > 1: every rank builds its replica, or rank 0 builds and broadcasts "
+                         "the device image (RCCL)")
     ap.add_argument("--gather", action="store_true",
                     help="gather every step's counts to rank 0 (RCCL), overlapped with the next count")
     ap.add_argument("--prefix-k", type=int, default=None,
@@ -112,8 +115,20 @@ def main():
     text = torch.empty(N + 16, dtype=torch.uint8, device=dev)
     pkg.synth_text_device(args.kind, 42, L, text.data_ptr(), sh)
     torch.cuda.synchronize()
-    idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
-                                             pkg.BuildParams(ssa_stride=args.ssa_stride), device=local_dev)
+    replicate_s = None
+    if args.replicate == "broadcast" and world > 1:
+        # rank 0 builds; the device image goes to every rank (shard.replicate_index)
+        idx = (pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
+                                                  pkg.BuildParams(ssa_stride=args.ssa_stride),
+                                                  device=local_dev) if rank == 0 else None)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        idx = shard.replicate_index(pkg, idx, 0, rank, world, dev)
+        replicate_s = time.perf_counter() - t1
+    else:
+        idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
+                                                 pkg.BuildParams(ssa_stride=args.ssa_stride),
+                                                 device=local_dev)
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t0
     info = idx.info()
@@ -255,6 +270,8 @@ def main():
                          "kernel_ms_mean": kern_avg_s * 1e3,
                          "kernel_ms_min": min(kern_ms)},
             "build_s": build_s,
+            "replicate": args.replicate if world > 1 else "single",
+            "replicate_s": replicate_s,
             "found_frac": found / B,
         }
 

@@ -69,6 +69,10 @@ SIGNATURES = {
                                      C.c_uint64, _u64p, _vp]),
     "cs_fm_create": (C.c_int, [_u8p, C.c_uint64, _u32p, C.c_uint64, C.c_uint32, _u8p, C.c_int,
                                C.POINTER(_vp)]),
+    "cs_fm_export_meta": (C.c_int, [_vp, C.c_char_p, C.c_uint64, _u64p, _u64p, _u32p]),
+    "cs_fm_export_parts": (C.c_int, [_vp, C.POINTER(_vp), _vp]),
+    "cs_fm_import": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(_vp), C.c_uint32, C.c_int,
+                               C.POINTER(_vp)]),
     "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_extract_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
@@ -218,6 +222,33 @@ class FMIndex:
         h = _vp()
         _check(lib().cs_fm_create(_u8(b), n, sa.ctypes.data_as(_u32p), len(ssa), ssa_stride,
                                   _u8(t) if t is not None else None, device, C.byref(h)))
+        return FMIndex(h, n)
+
+    # -- device image (replication across GPUs, shard.replicate_index) -----
+    def export_meta(self):
+        """-> (meta text bytes, [part sizes in bytes]) of the device image."""
+        L = lib()
+        ml, npart = C.c_uint64(), C.c_uint32()
+        st = L.cs_fm_export_meta(self._h, None, 0, C.byref(ml), None, C.byref(npart))
+        if st not in (CS_OK, CS_ERR_CAPACITY):
+            _check(st)
+        buf = C.create_string_buffer(ml.value)
+        sizes = (C.c_uint64 * max(npart.value, 1))()
+        _check(L.cs_fm_export_meta(self._h, buf, ml.value, C.byref(ml), sizes, C.byref(npart)))
+        return buf.raw[: ml.value], [int(sizes[i]) for i in range(npart.value)]
+
+    def export_parts(self, d_ptrs, stream=0):
+        """Copy the image parts into device buffers d_ptrs (asynchronous on stream)."""
+        arr = (_vp * len(d_ptrs))(*d_ptrs)
+        _check(lib().cs_fm_export_parts(self._h, arr, stream or None))
+
+    @staticmethod
+    def import_image(meta: bytes, d_ptrs, device: int = 0):
+        """An index on `device` from a meta text and device buffers holding the parts."""
+        arr = (_vp * len(d_ptrs))(*d_ptrs)
+        h = _vp()
+        _check(lib().cs_fm_import(meta, len(meta), arr, len(d_ptrs), device, C.byref(h)))
+        n = int(dict(l.split(" ", 1) for l in meta.decode().splitlines() if " " in l)["n"])
         return FMIndex(h, n)
 
     @staticmethod

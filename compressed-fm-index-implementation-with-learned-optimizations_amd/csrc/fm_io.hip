@@ -1,4 +1,5 @@
-// fm_io.hip — on-disk index format and FMIndex::open_directory.
+// fm_io.hip — on-disk index format and FMIndex::open_directory, and the same image
+// exported to / imported from device buffers (index replication across GPUs).
 //
 // The reference declares open_directory (src/api/fm_index.hpp:20, "TODO: on-disk
 // format") and throws (src/api/fm_index.cpp:71-73); its CSIDX serializer
@@ -15,12 +16,16 @@
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
 //   ssa.bin          sampled SA              isa.bin   inverse-SA samples (u32; u64 if wide)
 //   ptab.bin         prefix table (if k > 0) text.bin  the text (if kept, for extract)
-//   walk.bin         walk lines (occurrence engine)  wssa.bin  their position samples
+//   walk.bin         walk lines                      wssa.bin  their position samples
+// The device image (cs_fm_export_* / cs_fm_import) is the same meta text plus the
+// parts table, lines, ssa, isa[, ptab][, walk][, wssa] as device buffers.
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <sstream>
 #include <string>
+#include <vector>
 #include <sys/stat.h>
 
 #include "fm_internal.hpp"
@@ -82,6 +87,105 @@ struct Pinned {
   ~Pinned() { if (p) (void)hipHostFree(p); }
 };
 
+// One device array of the index image.
+struct Part {
+  const char* file;
+  void** dptr;
+  uint64_t bytes;
+};
+
+// The index's device arrays in image order; sizes from the geometry fields, so the
+// exporting and the importing side derive the same list from the same meta.
+std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa) {
+  std::vector<Part> v;
+  const uint64_t sb = h->sample_bytes();
+  if (with_table) v.push_back({"table.bin", reinterpret_cast<void**>(&h->d_table), sizeof(NodeTable)});
+  v.push_back({"lines.bin", &h->d_lines, (uint64_t)h->nlevels * h->nlines * h->line_bytes});
+  v.push_back({"ssa.bin", &h->d_ssa, h->nsamples * sb});
+  v.push_back({"isa.bin", &h->d_isa, h->nisa * sb});
+  if (h->ptab_k) v.push_back({"ptab.bin", &h->d_ptab, h->ptab_entries() * h->ptab_entry_bytes()});
+  if (h->nwalk) v.push_back({"walk.bin", &h->d_walk, h->nwalk * 32});
+  if (has_wssa) v.push_back({"wssa.bin", &h->d_wssa, h->nisa * sb});
+  return v;
+}
+
+std::string meta_text(const cs_fm_index* h, bool has_text) {
+  char buf[1024];
+  std::snprintf(buf, sizeof buf,
+                "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
+                "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
+                "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n",
+                kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
+                (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
+                (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
+                has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
+                (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0);
+  std::string m(buf);
+  for (int c = 0; c < 256; ++c) {
+    std::snprintf(buf, sizeof buf, "active %d %u\n", c, h->active_levels[c]);
+    m += buf;
+  }
+  return m;
+}
+
+// Fills h's geometry from a meta text; kv receives the flags (has_text, has_wssa).
+cs_status meta_parse(const std::string& text, cs_fm_index* h,
+                     std::map<std::string, unsigned long long>& kv, const std::string& what) {
+  std::istringstream in(text);
+  std::string key, val, format;
+  while (in >> key >> val) {
+    if (key == "format") {
+      format = val;
+    } else if (key == "active") {
+      const int c = std::atoi(val.c_str());
+      unsigned m = 0;
+      if ((in >> m) && c >= 0 && c < 256) h->active_levels[c] = m;
+    } else {
+      kv[key] = std::strtoull(val.c_str(), nullptr, 10);
+    }
+  }
+  if (format != kFormat) {
+    set_error("not a " + std::string(kFormat) + " index: " + what);
+    return CS_ERR_INVALID;
+  }
+  h->n = kv["n"];
+  h->stride = (uint32_t)kv["stride"];
+  h->line_bytes = (uint32_t)kv["line_bytes"];
+  h->line_bits = (uint32_t)kv["line_bits"];
+  h->nlines = kv["nlines"];
+  h->nsamples = kv["nsamples"];
+  h->nisa = kv["nisa"];
+  h->ptab_k = (uint32_t)kv["ptab_k"];
+  h->ptab_sigma = (uint32_t)kv["ptab_sigma"];
+  h->lf_exact = kv["lf_exact"] != 0;
+  h->wide = kv["wide"] != 0;
+  h->line_fmt = (uint32_t)kv["line_fmt"];
+  h->nlevels = (uint32_t)kv["levels"];
+  h->nwalk = kv["nwalk"];
+  h->walk_marks = (uint32_t)kv["walk_marks"];
+  return CS_OK;
+}
+
+cs_status need_device() {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    (void)hipGetLastError();
+    set_error("no HIP device: the FM-index engine runs only on the GPU");
+    return CS_ERR_NO_DEVICE;
+  }
+  return CS_OK;
+}
+
+// allocate every part (and the overrun flag) of a handle whose geometry is set
+cs_status alloc_parts(cs_fm_index* h, const std::vector<Part>& parts) {
+  for (const Part& p : parts)
+    if (hipMalloc(p.dptr, p.bytes ? p.bytes : 16) != hipSuccess)
+      return hip_fail(hipGetLastError(), "hipMalloc (index image)");
+  if (hipMalloc(&h->d_err, 8) != hipSuccess || hipMemset(h->d_err, 0xFF, 8) != hipSuccess)
+    return hip_fail(hipGetLastError(), "hipMalloc (index image)");
+  return CS_OK;
+}
+
 }  // namespace
 }  // namespace fmx
 
@@ -89,11 +193,12 @@ using namespace fmx;
 
 extern "C" {
 
-cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
-  if (!h || !dir) {
+cs_status cs_fm_save_directory(const cs_fm_index* hc, const char* dir) {
+  if (!hc || !dir) {
     set_error("null argument");
     return CS_ERR_INVALID;
   }
+  cs_fm_index* h = const_cast<cs_fm_index*>(hc);  // parts are only read
   DeviceScope ds;
   FMX_HIP(ds.enter(h->device));
   errno = 0;
@@ -103,19 +208,8 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
   Pinned pin;
   FMX_HIP(hipHostMalloc(&pin.p, kChunk, hipHostMallocDefault));
   cs_status s;
-  const uint64_t lbytes = (uint64_t)h->nlevels * h->nlines * h->line_bytes;
-  if ((s = dump_dev(join(d, "lines.bin"), h->d_lines, lbytes, pin.p)) != CS_OK) return s;
-  const uint64_t sb = h->sample_bytes();
-  if ((s = dump_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * sb, pin.p)) != CS_OK) return s;
-  if ((s = dump_dev(join(d, "isa.bin"), h->d_isa, h->nisa * sb, pin.p)) != CS_OK) return s;
-  if (h->ptab_k) {
-    const uint64_t pb = h->ptab_entries() * h->ptab_entry_bytes();
-    if ((s = dump_dev(join(d, "ptab.bin"), h->d_ptab, pb, pin.p)) != CS_OK) return s;
-  }
-  if (h->d_walk && (s = dump_dev(join(d, "walk.bin"), h->d_walk, h->nwalk * 32, pin.p)) != CS_OK)
-    return s;
-  if (h->d_wssa && (s = dump_dev(join(d, "wssa.bin"), h->d_wssa, h->nisa * sb, pin.p)) != CS_OK)
-    return s;
+  for (const Part& p : index_parts(h, false, h->d_wssa != nullptr))
+    if ((s = dump_dev(join(d, p.file), *p.dptr, p.bytes, pin.p)) != CS_OK) return s;
   {
     FILE* f = std::fopen(join(d, "table.bin").c_str(), "wb");
     if (!f || std::fwrite(&h->h_table, sizeof h->h_table, 1, f) != 1) {
@@ -133,17 +227,12 @@ cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir) {
     }
     std::fclose(f);
   }
+  const std::string meta = meta_text(h, has_text);
   FILE* f = std::fopen(join(d, "cs_fmindex.meta").c_str(), "w");
-  if (!f) return io_fail("cannot write: " + join(d, "cs_fmindex.meta"));
-  std::fprintf(f, "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
-                  "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
-                  "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n",
-               kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
-               (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
-               (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
-               has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
-               (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0);
-  for (int c = 0; c < 256; ++c) std::fprintf(f, "active %d %u\n", c, h->active_levels[c]);
+  if (!f || std::fwrite(meta.data(), 1, meta.size(), f) != meta.size()) {
+    if (f) std::fclose(f);
+    return io_fail("cannot write: " + join(d, "cs_fmindex.meta"));
+  }
   std::fclose(f);
   return CS_OK;
 }
@@ -156,53 +245,27 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
   *out = nullptr;
   const std::string d(dir);
   errno = 0;
-  FILE* f = std::fopen(join(d, "cs_fmindex.meta").c_str(), "r");
-  if (!f) return io_fail("cannot open: " + join(d, "cs_fmindex.meta"));
-  std::map<std::string, unsigned long long> kv;
-  std::string format;
+  std::string meta;
+  {
+    FILE* f = std::fopen(join(d, "cs_fmindex.meta").c_str(), "r");
+    if (!f) return io_fail("cannot open: " + join(d, "cs_fmindex.meta"));
+    char buf[4096];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) meta.append(buf, k);
+    std::fclose(f);
+  }
   auto* h = new cs_fm_index();
-  char key[64], val[128];
-  while (std::fscanf(f, "%63s %127s", key, val) == 2) {
-    if (!std::strcmp(key, "format")) {
-      format = val;
-    } else if (!std::strcmp(key, "active")) {
-      const int c = std::atoi(val);
-      unsigned m = 0;
-      if (std::fscanf(f, "%u", &m) == 1 && c >= 0 && c < 256) h->active_levels[c] = m;
-    } else {
-      kv[key] = std::strtoull(val, nullptr, 10);
-    }
-  }
-  std::fclose(f);
-  if (format != kFormat) {
+  std::map<std::string, unsigned long long> kv;
+  cs_status s = meta_parse(meta, h, kv, d);
+  if (s == CS_OK) s = need_device();
+  if (s != CS_OK) {
     delete h;
-    set_error("not a " + std::string(kFormat) + " index: " + d);
-    return CS_ERR_INVALID;
-  }
-  int count = 0;
-  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
-    delete h;
-    (void)hipGetLastError();
-    set_error("no HIP device: the FM-index engine runs only on the GPU");
-    return CS_ERR_NO_DEVICE;
+    return s;
   }
   h->device = device;
-  h->n = kv["n"];
-  h->stride = (uint32_t)kv["stride"];
-  h->line_bytes = (uint32_t)kv["line_bytes"];
-  h->line_bits = (uint32_t)kv["line_bits"];
-  h->nlines = kv["nlines"];
-  h->nsamples = kv["nsamples"];
-  h->nisa = kv["nisa"];
-  h->ptab_k = (uint32_t)kv["ptab_k"];
-  h->ptab_sigma = (uint32_t)kv["ptab_sigma"];
-  h->lf_exact = kv["lf_exact"] != 0;
-  h->wide = kv["wide"] != 0;
-  h->line_fmt = (uint32_t)kv["line_fmt"];
-  h->nlevels = (uint32_t)kv["levels"];
-  auto fail = [&](cs_status s) {
+  auto fail = [&](cs_status st) {
     cs_fm_destroy(h);
-    return s;
+    return st;
   };
   DeviceScope ds;
   if (ds.enter(device) != hipSuccess) return fail(hip_fail(hipGetLastError(), "hipSetDevice"));
@@ -214,41 +277,16 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     }
     std::fclose(t);
   }
+  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0);
+  if ((s = alloc_parts(h, parts)) != CS_OK) return fail(s);
   Pinned pin;
   if (hipHostMalloc(&pin.p, kChunk, hipHostMallocDefault) != hipSuccess)
     return fail(hip_fail(hipGetLastError(), "hipHostMalloc"));
-  const uint64_t lbytes = (uint64_t)h->nlevels * h->nlines * h->line_bytes;
-  if (hipMalloc(&h->d_lines, lbytes ? lbytes : 16) != hipSuccess ||
-      hipMalloc(&h->d_ssa, h->nsamples ? h->nsamples * h->sample_bytes() : 16) != hipSuccess ||
-      hipMalloc(&h->d_isa, h->nisa ? h->nisa * h->sample_bytes() : 16) != hipSuccess ||
-      hipMalloc(&h->d_table, sizeof(NodeTable)) != hipSuccess ||
-      hipMalloc(&h->d_err, 8) != hipSuccess)
-    return fail(hip_fail(hipGetLastError(), "hipMalloc (open)"));
-  cs_status s;
-  if ((s = load_dev(join(d, "lines.bin"), h->d_lines, lbytes, pin.p)) != CS_OK) return fail(s);
-  const uint64_t sb = h->sample_bytes();
-  if ((s = load_dev(join(d, "ssa.bin"), h->d_ssa, h->nsamples * sb, pin.p)) != CS_OK) return fail(s);
-  if ((s = load_dev(join(d, "isa.bin"), h->d_isa, h->nisa * sb, pin.p)) != CS_OK) return fail(s);
-  if (h->ptab_k) {
-    const uint64_t pb = h->ptab_entries() * h->ptab_entry_bytes();
-    if (hipMalloc(&h->d_ptab, pb) != hipSuccess)
-      return fail(hip_fail(hipGetLastError(), "hipMalloc (ptab)"));
-    if ((s = load_dev(join(d, "ptab.bin"), h->d_ptab, pb, pin.p)) != CS_OK) return fail(s);
+  for (const Part& p : parts) {
+    if (p.dptr == reinterpret_cast<void**>(&h->d_table)) continue;  // from the host copy below
+    if ((s = load_dev(join(d, p.file), *p.dptr, p.bytes, pin.p)) != CS_OK) return fail(s);
   }
-  if (kv["nwalk"]) {
-    h->nwalk = kv["nwalk"];
-    h->walk_marks = (uint32_t)kv["walk_marks"];
-    if (hipMalloc(&h->d_walk, h->nwalk * 32) != hipSuccess)
-      return fail(hip_fail(hipGetLastError(), "hipMalloc (walk)"));
-    if ((s = load_dev(join(d, "walk.bin"), h->d_walk, h->nwalk * 32, pin.p)) != CS_OK) return fail(s);
-  }
-  if (kv["has_wssa"]) {
-    if (hipMalloc(&h->d_wssa, (h->nisa ? h->nisa : 1) * sb) != hipSuccess)
-      return fail(hip_fail(hipGetLastError(), "hipMalloc (wssa)"));
-    if ((s = load_dev(join(d, "wssa.bin"), h->d_wssa, h->nisa * sb, pin.p)) != CS_OK) return fail(s);
-  }
-  if (hipMemcpy(h->d_table, &h->h_table, sizeof(NodeTable), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(h->d_err, 0xFF, 8) != hipSuccess)
+  if (hipMemcpy(h->d_table, &h->h_table, sizeof(NodeTable), hipMemcpyHostToDevice) != hipSuccess)
     return fail(hip_fail(hipGetLastError(), "hipMemcpy (open)"));
   if (kv["has_text"]) {
     FILE* t = std::fopen(join(d, "text.bin").c_str(), "rb");
@@ -259,6 +297,80 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     }
     std::fclose(t);
   }
+  *out = h;
+  return CS_OK;
+}
+
+cs_status cs_fm_export_meta(const cs_fm_index* hc, char* meta, uint64_t cap, uint64_t* meta_len,
+                            uint64_t* part_bytes, uint32_t* nparts) {
+  if (!hc || !meta_len || !nparts) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  cs_fm_index* h = const_cast<cs_fm_index*>(hc);
+  const std::string m = meta_text(h, false);
+  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr);
+  *meta_len = m.size();
+  *nparts = (uint32_t)parts.size();
+  if (!meta || cap < m.size() || !part_bytes) {
+    set_error("export: meta buffer too small");
+    return CS_ERR_CAPACITY;
+  }
+  std::memcpy(meta, m.data(), m.size());
+  for (size_t i = 0; i < parts.size(); ++i) part_bytes[i] = parts[i].bytes;
+  return CS_OK;
+}
+
+cs_status cs_fm_export_parts(const cs_fm_index* hc, void* const* d_dst, void* stream) {
+  if (!hc || !d_dst) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  cs_fm_index* h = const_cast<cs_fm_index*>(hc);
+  DeviceScope ds;
+  FMX_HIP(ds.enter(h->device));
+  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr);
+  for (size_t i = 0; i < parts.size(); ++i)
+    if (parts[i].bytes)
+      FMX_HIP(hipMemcpyAsync(d_dst[i], *parts[i].dptr, parts[i].bytes, hipMemcpyDeviceToDevice,
+                             (hipStream_t)stream));
+  return CS_OK;
+}
+
+cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d_src,
+                       uint32_t nparts, int device, cs_fm_index** out) {
+  if (!meta || !d_src || !out) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  *out = nullptr;
+  auto* h = new cs_fm_index();
+  std::map<std::string, unsigned long long> kv;
+  cs_status s = meta_parse(std::string(meta, meta_len), h, kv, "device image");
+  if (s == CS_OK) s = need_device();
+  if (s != CS_OK) {
+    delete h;
+    return s;
+  }
+  h->device = device;
+  auto fail = [&](cs_status st) {
+    cs_fm_destroy(h);
+    return st;
+  };
+  DeviceScope ds;
+  if (ds.enter(device) != hipSuccess) return fail(hip_fail(hipGetLastError(), "hipSetDevice"));
+  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0);
+  if (parts.size() != nparts) {
+    set_error("import: the image has a different number of parts than its meta");
+    return fail(CS_ERR_INVALID);
+  }
+  if ((s = alloc_parts(h, parts)) != CS_OK) return fail(s);
+  for (size_t i = 0; i < parts.size(); ++i)
+    if (parts[i].bytes &&
+        hipMemcpy(*parts[i].dptr, d_src[i], parts[i].bytes, hipMemcpyDeviceToDevice) != hipSuccess)
+      return fail(hip_fail(hipGetLastError(), "hipMemcpy (import)"));
+  if (hipMemcpy(&h->h_table, h->d_table, sizeof(NodeTable), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(hip_fail(hipGetLastError(), "hipMemcpy (import table)"));
   *out = h;
   return CS_OK;
 }

@@ -115,3 +115,49 @@ def sharded_count(count_fn, total: int, world: int, rank: int, device, dst: int 
     lo, hi = shard_range(total, rank, world)
     local = count_fn(lo, hi) if hi > lo else torch.zeros(0, dtype=torch.int64, device=device)
     return gather_counts(local.to(device), total, world, rank, dst)
+
+
+def replicate_index(fm, idx, src: int, rank: int, world: int, device):
+    """The index built (or opened) on rank `src` on every rank's `device`: its device
+    image (cs_fm_export_meta / cs_fm_export_parts) is broadcast part by part — over
+    RCCL/xGMI with the nccl backend, staged through host memory with gloo — and
+    imported (cs_fm_import).  `fm` is the package, `idx` the FMIndex on src (None on
+    the other ranks).  SURVEY §8(e): replicate by broadcast instead of building on
+    every GPU."""
+    if world == 1:
+        return idx
+    stage = dist.get_backend() == "gloo"
+    bdev = torch.device("cpu") if stage else torch.device(device)
+    if rank == src:
+        meta, sizes = idx.export_meta()
+        hdr = torch.tensor([len(meta), len(sizes)], dtype=torch.int64, device=bdev)
+    else:
+        hdr = torch.zeros(2, dtype=torch.int64, device=bdev)
+    dist.broadcast(hdr, src)
+    meta_len, nparts = int(hdr[0]), int(hdr[1])
+    szt = (torch.tensor(sizes, dtype=torch.int64, device=bdev) if rank == src
+           else torch.zeros(nparts, dtype=torch.int64, device=bdev))
+    dist.broadcast(szt, src)
+    sizes = [int(v) for v in szt.tolist()]
+    mt = (torch.frombuffer(bytearray(meta), dtype=torch.uint8).to(bdev) if rank == src
+          else torch.zeros(meta_len, dtype=torch.uint8, device=bdev))
+    dist.broadcast(mt, src)
+    meta = bytes(mt.cpu().numpy().tobytes())
+    parts = [torch.empty(max(b, 1), dtype=torch.uint8, device=device) for b in sizes]
+    if rank == src:
+        idx.export_parts([p.data_ptr() for p in parts], torch.cuda.current_stream(device).cuda_stream)
+        torch.cuda.synchronize(device)
+    for i, p in enumerate(parts):
+        if stage:  # gloo moves host tensors only
+            h = p.cpu() if rank == src else torch.empty(p.numel(), dtype=torch.uint8)
+            dist.broadcast(h, src)
+            if rank != src:
+                p.copy_(h)
+        else:
+            dist.broadcast(p, src)
+    torch.cuda.synchronize(device)
+    if rank == src:
+        return idx
+    out = fm.FMIndex.import_image(meta, [p.data_ptr() for p in parts], torch.device(device).index)
+    del parts
+    return out

@@ -108,6 +108,18 @@ cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out);
 cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out);
 /* Writes the index (HBM images of every structure, plus the text when kept) to dir. */
 cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir);
+/* The index as a device image, for replication across GPUs (e.g. a broadcast over
+ * RCCL instead of building on every GPU): export_meta returns the meta text (the
+ * directory format's cs_fmindex.meta) and the byte size of each part; export_parts
+ * copies the parts into caller device buffers (asynchronous on stream); import
+ * creates an index on `device` from a meta and device buffers holding the parts
+ * (copied; the buffers may be freed after the call).  The host text is not part of
+ * the image. */
+cs_status cs_fm_export_meta(const cs_fm_index* h, char* meta, uint64_t cap, uint64_t* meta_len,
+                            uint64_t* part_bytes, uint32_t* nparts);
+cs_status cs_fm_export_parts(const cs_fm_index* h, void* const* d_dst, void* stream);
+cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d_src,
+                       uint32_t nparts, int device, cs_fm_index** out);
 void cs_fm_destroy(cs_fm_index* h);
 cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out);
 const char* cs_fm_last_error(void);

@@ -101,3 +101,29 @@ def test_concurrent_calls_share_nothing_mutable():
     for x in th:
         x.join()
     assert not bad, bad[:5]
+
+
+@pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet"])
+def test_export_import_image(engine, monkeypatch):
+    """The device image (cs_fm_export_meta/_parts -> cs_fm_import): the copy answers
+    count / locate / extract exactly as the original."""
+    if engine != "auto":
+        monkeypatch.setenv("CS_FM_ENGINE", engine)
+    pkg = load_pkg()
+    t = O.gen_dna(9, 50_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    meta, sizes = g.export_meta()
+    assert meta.startswith(b"format cs_fmindex/") and len(sizes) >= 4
+    parts = [torch.empty(max(b, 1), dtype=torch.uint8, device="cuda") for b in sizes]
+    g.export_parts([p.data_ptr() for p in parts])
+    torch.cuda.synchronize()
+    c = pkg.FMIndex.import_image(meta, [p.data_ptr() for p in parts], 0)
+    del parts
+    assert c.info().engine == g.info().engine and c.info().walk_marks == g.info().walk_marks
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 14, 500)
+    pats = [bytes(r) for r in P] + [b"ACGTACGTAC", b"$", b""]
+    assert c.count_batch(pats).tolist() == g.count_batch(pats).tolist()
+    lo1, lp1 = g.locate_batch(pats, limit=9)
+    lo2, lp2 = c.locate_batch(pats, limit=9)
+    assert lo1.tolist() == lo2.tolist() and lp1.tolist() == lp2.tolist()
+    assert c.extract_batch([0, 100, len(t) - 3], [10, 25, 10]) == [t[0:10], t[100:125], t[-3:]]
