@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "cs/fm_index.hpp"
+#include "cs_fmindex.h"
 
 using namespace cs;
 
@@ -122,6 +123,23 @@ int main() {
     for (const char* q : {"ssi", "i", "issi", "p", "x", ""})
       CHECK(back.count(q) == idx.count(q) && back.locate(q) == idx.locate(q));
     CHECK(back.extract(2, 4) == "ssis");
+  }
+  {  // borrow(): the facade over an index created through the C ABI (cs_fm_create from
+     // the reference's own bwt_ / ssa_ members of "banana$", stride 2)
+    const std::string bwt = "annb$aa";                      // cyclic BWT of banana$
+    const uint32_t ssa[4] = {6, 3, 0, 2};                    // SA[0], SA[2], SA[4], SA[6]
+    cs_fm_index* h = nullptr;
+    CHECK(cs_fm_create(reinterpret_cast<const uint8_t*>(bwt.data()), bwt.size(), ssa, 4, 2,
+                       reinterpret_cast<const uint8_t*>("banana$"), 0, &h) == CS_OK);
+    if (h) {
+      {
+        const FMIndex b = FMIndex::borrow(h);
+        CHECK(b.size() == 7 && b.count("ana") == 2 && b.count("") == 7);
+        CHECK((b.locate("ana") == std::vector<uint64_t>{3, 1}));
+        CHECK(b.extract(1, 3) == "ana");
+      }
+      cs_fm_destroy(h);  // the borrowed view never owned it
+    }
   }
   if (failures) {
     std::fprintf(stderr, "%d facade checks failed\n", failures);
