@@ -10,8 +10,10 @@
 //     whose suffix count fits the memory budget (rows of a pass are contiguous);
 //   * per pass: select its positions (rocPRIM select over a counting iterator with
 //     the bin predicate), sort (key chunk 0, position) by radix sort, then resolve
-//     groups of equal keys with the next chunks (stable sorts by chunk then group),
-//     until every suffix is alone — for random DNA one or two extra chunks;
+//     groups of equal keys with the next chunks (stable sorts by chunk then group)
+//     over the compacted set of still-tied suffixes only, until every suffix is
+//     alone — for random DNA one or two extra chunks, for an exact repeat of length
+//     R about R/K rounds of a few launches over the repeat's suffixes;
 //   * emit BWT bytes, SSA samples (row % stride == 0) and ISA samples
 //     (position % stride == 0) for the pass's rows.
 #include <rocprim/device/device_radix_sort.hpp>
@@ -21,6 +23,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #include "fm_internal.hpp"
@@ -124,18 +127,26 @@ __global__ void k_tied(const uint8_t* __restrict__ bound, uint64_t P, uint32_t* 
   if ((threadIdx.x & 63) == 0 && local) atomicAdd(ntied, local);
 }
 
-// For the compacted tied slots S: their group id, the next key chunk, and iota.
-__global__ void k_tied_keys(const uint8_t* __restrict__ t, uint64_t n,
-                            const uint16_t* __restrict__ code, int b, int K,
-                            const uint64_t* __restrict__ S, uint64_t T,
-                            const uint32_t* __restrict__ gid_scan, const uint64_t* __restrict__ pos,
-                            uint64_t chunk, uint32_t* __restrict__ tg, uint64_t* __restrict__ tkey,
-                            uint32_t* __restrict__ iota) {
+// Entering the compacted refinement: tied slot S[i] -> its group (slot of the group's
+// first member) and its text position.
+__global__ void k_init_compact(const uint64_t* __restrict__ S, uint64_t T,
+                               const uint32_t* __restrict__ gid_scan, const uint64_t* __restrict__ pos,
+                               uint32_t* __restrict__ cg, uint64_t* __restrict__ cpos) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < T; i += stride) {
     const uint64_t j = S[i];
-    tg[i] = gid_scan[j];
-    tkey[i] = key_chunk(t, n, code, b, K, pos[j], chunk);
+    cg[i] = gid_scan[j];
+    cpos[i] = pos[j];
+  }
+}
+
+// Next key chunk of every still-tied suffix, plus iota for the permutation.
+__global__ void k_ckeys(const uint8_t* __restrict__ t, uint64_t n, const uint16_t* __restrict__ code,
+                        int b, int K, const uint64_t* __restrict__ cpos, uint64_t T, uint64_t chunk,
+                        uint64_t* __restrict__ ckey, uint32_t* __restrict__ iota) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < T; i += stride) {
+    ckey[i] = key_chunk(t, n, code, b, K, cpos[i], chunk);
     iota[i] = (uint32_t)i;
   }
 }
@@ -147,31 +158,49 @@ __global__ void k_gather_gid(const uint32_t* __restrict__ tg, const uint32_t* __
     out[i] = tg[idx[i]];
 }
 
-// Sorted tied element i (source index idx[i] in S order) goes to slot S[i]: groups
-// keep their slot ranges, ordered inside by the new key.  New boundaries where the
-// group or the key changes.
-__global__ void k_writeback(const uint64_t* __restrict__ S, const uint32_t* __restrict__ idx,
-                            const uint32_t* __restrict__ tg, const uint64_t* __restrict__ tkey,
-                            const uint64_t* __restrict__ pos_in, uint64_t T,
-                            uint64_t* __restrict__ pos_out, uint8_t* __restrict__ bound) {
+// Sorted tied element i (source idx[i]) goes to slot S[i]: groups keep their slot
+// ranges, ordered inside by the new key.  A new group starts where the group or the
+// key changes (startv = i there, for the max-scan).
+__global__ void k_round_writeback(const uint64_t* __restrict__ S, const uint32_t* __restrict__ idx,
+                                  const uint32_t* __restrict__ cg, const uint64_t* __restrict__ ckey,
+                                  const uint64_t* __restrict__ cpos, uint64_t T,
+                                  uint64_t* __restrict__ pos, uint32_t* __restrict__ startv,
+                                  uint8_t* __restrict__ nbf) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < T; i += stride) {
     const uint32_t src = idx[i];
-    pos_out[S[i]] = pos_in[S[src]];
-    bool newb = i == 0;
-    if (!newb) {
+    pos[S[i]] = cpos[src];
+    bool nb = i == 0;
+    if (!nb) {
       const uint32_t prv = idx[i - 1];
-      newb = tg[src] != tg[prv] || tkey[src] != tkey[prv];
+      nb = cg[src] != cg[prv] || ckey[src] != ckey[prv];
     }
-    if (newb) bound[S[i]] = 1;
+    startv[i] = nb ? (uint32_t)i : 0u;
+    nbf[i] = nb ? 1 : 0;
   }
 }
 
-__global__ void k_copy_slots(const uint64_t* __restrict__ S, uint64_t T,
-                             const uint64_t* __restrict__ from, uint64_t* __restrict__ to) {
+// still tied = not alone in its new group
+__global__ void k_round_flags(const uint8_t* __restrict__ nbf, uint64_t T, uint8_t* __restrict__ tf) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < T; i += stride)
-    to[S[i]] = from[S[i]];
+    tf[i] = (nbf[i] && (i + 1 == T || nbf[i + 1])) ? 0 : 1;
+}
+
+// Keep the still-tied elements (sel: their sorted indices, increasing), so the slot
+// list stays increasing and the group id is the slot of the group's first member.
+__global__ void k_round_compact(const uint32_t* __restrict__ sel, uint64_t T2,
+                                const uint64_t* __restrict__ S, const uint32_t* __restrict__ start,
+                                const uint32_t* __restrict__ idx, const uint64_t* __restrict__ cpos,
+                                uint64_t* __restrict__ S2, uint32_t* __restrict__ cg2,
+                                uint64_t* __restrict__ cpos2) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < T2; j += stride) {
+    const uint32_t i = sel[j];
+    S2[j] = S[i];
+    cg2[j] = (uint32_t)S[start[i]];
+    cpos2[j] = cpos[idx[i]];
+  }
 }
 
 template <class SampleT>
@@ -269,8 +298,7 @@ cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride,
     std::fprintf(stderr, "[cs_fm bucketed] sigma=%d b=%d K=%d L=%d passes=%zu max_pass=%llu\n", sigma,
                  cd.b, cd.K, L, passes.size(), (unsigned long long)pbig);
 
-  DevBuf pos0, pos1, key0, key1, bound, gid_in, gid_scan, tied, S, tg, tg2, tkey, tkey2, tidx, tidx2,
-      d_cnt, tmp;  // t*: the tied elements of one refinement round
+  DevBuf pos0, pos1, key0, key1, bound, gid_in, gid_scan, tied, d_cnt, tmp;
   size_t tmp_bytes = 0;
   FMX_HIP(pos0.alloc(pbig * 8));
   FMX_HIP(pos1.alloc(pbig * 8));
@@ -304,66 +332,114 @@ cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride,
     uint64_t* pos = vb.current();
     uint64_t* pos_alt = vb.alternate();
     k_bounds<<<G, kBlk, 0, st>>>(kb.current(), P, bound.as<uint8_t>());
-    // 3. refine groups of equal keys with further chunks
-    for (uint64_t chunk = 1;; ++chunk) {
-      FMX_HIP(hipMemsetAsync(d_cnt.p, 0, 16, st));
-      k_tied<<<G, kBlk, 0, st>>>(bound.as<uint8_t>(), P, gid_in.as<uint32_t>(), tied.as<uint8_t>(),
-                                 d_cnt.as<unsigned long long>() + 1);
-      unsigned long long ntied = 0;
-      FMX_HIP(hipMemcpyAsync(&ntied, d_cnt.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, st));
-      FMX_HIP(hipStreamSynchronize(st));
-      if (verbose && chunk <= 3)
-        std::fprintf(stderr, "[cs_fm bucketed] pass bins [%u,%u) P=%llu chunk %llu: %llu tied\n",
-                     ps.lo, ps.hi, (unsigned long long)P, (unsigned long long)chunk, ntied);
-      if (!ntied) break;
-      if (chunk > 256) {
-        set_error("bucketed suffix sort: repeats longer than the refinement cap");
-        return CS_ERR_INVALID;
-      }
-      const uint64_t T = ntied;
+    // 3. refine groups of equal keys with further chunks.  One full-pass sweep finds
+    // the tied slots; from then on every round works on the compacted tied set only
+    // (cost O(tied), not O(P)), so a long exact repeat costs rounds of a few small
+    // launches each.  Suffixes of one group differ at the latest where the shorter
+    // one ends (past-the-end code 0), so at most n/K + 1 rounds are needed.
+    FMX_HIP(hipMemsetAsync(d_cnt.p, 0, 16, st));
+    k_tied<<<G, kBlk, 0, st>>>(bound.as<uint8_t>(), P, gid_in.as<uint32_t>(), tied.as<uint8_t>(),
+                               d_cnt.as<unsigned long long>() + 1);
+    unsigned long long ntied = 0;
+    FMX_HIP(hipMemcpyAsync(&ntied, d_cnt.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    if (verbose)
+      std::fprintf(stderr, "[cs_fm bucketed] pass bins [%u,%u) P=%llu: %llu tied after chunk 0\n",
+                   ps.lo, ps.hi, (unsigned long long)P, ntied);
+    if (ntied) {
+      uint64_t T = ntied;
       s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
         return rocprim::inclusive_scan(p, b, gid_in.as<uint32_t>(), gid_scan.as<uint32_t>(), (size_t)P,
                                        rocprim::maximum<uint32_t>(), st);
       });
       if (s != CS_OK) return s;
-      FMX_HIP(S.alloc(T * 8));
-      FMX_HIP(tg.alloc(T * 4));
-      FMX_HIP(tg2.alloc(T * 4));
-      FMX_HIP(tkey.alloc(T * 8));
-      FMX_HIP(tkey2.alloc(T * 8));
-      FMX_HIP(tidx.alloc(T * 4));
-      FMX_HIP(tidx2.alloc(T * 4));
-      DevBuf idx1, gscr;
-      FMX_HIP(idx1.alloc(T * 4));
+      // compact arrays, sized once for the first tied set (it only shrinks); the
+      // pass-sized key/pos/flag buffers are free from here on and are reused
+      DevBuf S0, S1, cpos1, cg1, cgs, gscr, iota, idx1, start, sel;
+      FMX_HIP(S0.alloc(T * 8));
+      FMX_HIP(S1.alloc(T * 8));
+      FMX_HIP(cpos1.alloc(T * 8));
+      FMX_HIP(cg1.alloc(T * 4));
+      FMX_HIP(cgs.alloc(T * 4));
       FMX_HIP(gscr.alloc(T * 4));
-      const uint8_t* tf = tied.as<uint8_t>();
+      FMX_HIP(iota.alloc(T * 4));
+      FMX_HIP(idx1.alloc(T * 4));
+      FMX_HIP(start.alloc(T * 4));
+      FMX_HIP(sel.alloc(T * 4));
+      uint64_t* cS = S0.as<uint64_t>();
+      uint64_t* nS = S1.as<uint64_t>();
+      uint64_t* cpos = pos_alt;
+      uint64_t* npos = cpos1.as<uint64_t>();
+      uint32_t* cg = gid_in.as<uint32_t>();
+      uint32_t* ncg = cg1.as<uint32_t>();
+      uint64_t* ckey = key0.as<uint64_t>();
+      uint64_t* ckey2 = key1.as<uint64_t>();
+      uint32_t* startv = gid_scan.as<uint32_t>();
+      uint8_t* nbf = bound.as<uint8_t>();
+      uint8_t* tf = tied.as<uint8_t>();
+      const uint8_t* tied_all = tied.as<uint8_t>();
       s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
-        return rocprim::select(p, b, rocprim::counting_iterator<uint64_t>(0), tf, S.as<uint64_t>(),
+        return rocprim::select(p, b, rocprim::counting_iterator<uint64_t>(0), tied_all, cS,
                                d_cnt.as<uint64_t>(), (size_t)P, st);
       });
       if (s != CS_OK) return s;
-      const unsigned GT = grid_for(T, kBlk, 16384);
-      // tg/tkey: group id and chunk key in S order (kept unsorted); tidx2 = iota
-      k_tied_keys<<<GT, kBlk, 0, st>>>(d_text, n, code, cd.b, cd.K, S.as<uint64_t>(), T,
-                                       gid_scan.as<uint32_t>(), pos, chunk, tg.as<uint32_t>(),
-                                       tkey.as<uint64_t>(), tidx2.as<uint32_t>());
-      // stable by key, then stable by group -> (group, key) order in tidx
-      s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
-        return rocprim::radix_sort_pairs(p, b, tkey.as<uint64_t>(), tkey2.as<uint64_t>(),
-                                         tidx2.as<uint32_t>(), idx1.as<uint32_t>(), T, 0,
-                                         cd.b * cd.K, st);
-      });
-      if (s != CS_OK) return s;
-      k_gather_gid<<<GT, kBlk, 0, st>>>(tg.as<uint32_t>(), idx1.as<uint32_t>(), T, tg2.as<uint32_t>());
-      s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
-        return rocprim::radix_sort_pairs(p, b, tg2.as<uint32_t>(), gscr.as<uint32_t>(),
-                                         idx1.as<uint32_t>(), tidx.as<uint32_t>(), T, 0, 32, st);
-      });
-      if (s != CS_OK) return s;
-      k_writeback<<<GT, kBlk, 0, st>>>(S.as<uint64_t>(), tidx.as<uint32_t>(), tg.as<uint32_t>(),
-                                       tkey.as<uint64_t>(), pos, T, pos_alt, bound.as<uint8_t>());
-      k_copy_slots<<<GT, kBlk, 0, st>>>(S.as<uint64_t>(), T, pos_alt, pos);
+      // gid_scan is read here before its buffer becomes startv
+      k_init_compact<<<grid_for(T, kBlk, 16384), kBlk, 0, st>>>(cS, T, gid_scan.as<uint32_t>(), pos,
+                                                                 cg, cpos);
       FMX_HIP(hipGetLastError());
+      int gbits = 1;
+      while (gbits < 32 && (1ull << gbits) < P) ++gbits;
+      const uint64_t max_chunk = n / (uint64_t)cd.K + 2;
+      uint64_t chunk = 1;
+      for (;; ++chunk) {
+        if (chunk > max_chunk) {
+          set_error("bucketed suffix sort: refinement did not converge (internal error)");
+          return CS_ERR_INVALID;
+        }
+        const unsigned GT = grid_for(T, kBlk, 16384);
+        k_ckeys<<<GT, kBlk, 0, st>>>(d_text, n, code, cd.b, cd.K, cpos, T, chunk, ckey,
+                                     iota.as<uint32_t>());
+        // stable by key, then stable by group -> (group, key) order in iota
+        s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
+          return rocprim::radix_sort_pairs(p, b, ckey, ckey2, iota.as<uint32_t>(), idx1.as<uint32_t>(),
+                                           T, 0, cd.b * cd.K, st);
+        });
+        if (s != CS_OK) return s;
+        k_gather_gid<<<GT, kBlk, 0, st>>>(cg, idx1.as<uint32_t>(), T, cgs.as<uint32_t>());
+        s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
+          return rocprim::radix_sort_pairs(p, b, cgs.as<uint32_t>(), gscr.as<uint32_t>(),
+                                           idx1.as<uint32_t>(), iota.as<uint32_t>(), T, 0, gbits, st);
+        });
+        if (s != CS_OK) return s;
+        const uint32_t* idx = iota.as<uint32_t>();
+        k_round_writeback<<<GT, kBlk, 0, st>>>(cS, idx, cg, ckey, cpos, T, pos, startv, nbf);
+        k_round_flags<<<GT, kBlk, 0, st>>>(nbf, T, tf);
+        FMX_HIP(hipGetLastError());
+        s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
+          return rocprim::inclusive_scan(p, b, startv, start.as<uint32_t>(), (size_t)T,
+                                         rocprim::maximum<uint32_t>(), st);
+        });
+        if (s != CS_OK) return s;
+        s = tmp_call(tmp, tmp_bytes, [&](void* p, size_t& b) {
+          return rocprim::select(p, b, rocprim::counting_iterator<uint32_t>(0), (const uint8_t*)tf,
+                                 sel.as<uint32_t>(), d_cnt.as<uint64_t>(), (size_t)T, st);
+        });
+        if (s != CS_OK) return s;
+        uint64_t T2 = 0;
+        FMX_HIP(hipMemcpyAsync(&T2, d_cnt.p, 8, hipMemcpyDeviceToHost, st));
+        FMX_HIP(hipStreamSynchronize(st));
+        if (verbose && (chunk <= 3 || (chunk & (chunk - 1)) == 0))
+          std::fprintf(stderr, "[cs_fm bucketed]   chunk %llu: %llu tied\n", (unsigned long long)chunk,
+                       (unsigned long long)T2);
+        if (!T2) break;
+        k_round_compact<<<grid_for(T2, kBlk, 16384), kBlk, 0, st>>>(
+            sel.as<uint32_t>(), T2, cS, start.as<uint32_t>(), idx, cpos, nS, ncg, npos);
+        FMX_HIP(hipGetLastError());
+        std::swap(cS, nS);
+        std::swap(cg, ncg);
+        std::swap(cpos, npos);
+        T = T2;
+      }
     }
     // 4. emit the pass's rows
     if (wide)

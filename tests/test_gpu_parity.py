@@ -402,6 +402,35 @@ def test_bucketed_multi_pass(pkg):
                 os.environ[k] = v
 
 
+def test_bucketed_long_repeats(pkg):
+    """Exact repeats far longer than one key chunk (20 000-char copies, a 12 000-char
+    run of one symbol, a period-3 stretch): the bucketed sorter refines only the
+    still-tied suffixes, round after round, and emits the oracle's BWT / SSA."""
+    saved = os.environ.get("CS_FM_SA_BUILDER")
+    try:
+        os.environ["CS_FM_SA_BUILDER"] = "bucketed"
+        base = O.gen_dna(33, 60000).tobytes()[:-1]
+        seg = base[:20000]
+        texts = [
+            base[20000:25000] + seg + base[25000:30000] + seg + base[30000:31000] + seg + b"$",
+            base[:3000] + b"A" * 12000 + base[3000:6000] + b"$",
+            base[:2000] + b"ACG" * 5000 + base[2000:4000] + b"ACG" * 4000 + b"$",
+        ]
+        for t in texts:
+            g = pkg.FMIndex.build_from_text(t)
+            o = O.Index(t)
+            rows = np.arange(len(t), dtype=np.uint64)
+            assert g.wt_access(rows).tobytes() == o.bwt().tobytes()
+            assert g.ssa().tolist() == o.ssa().tolist()
+            pats = [t[i:i + 30] for i in range(0, len(t) - 30, 1999)]
+            assert g.count_batch(pats).tolist() == [o.count(p) for p in pats]
+    finally:
+        if saved is None:
+            os.environ.pop("CS_FM_SA_BUILDER", None)
+        else:
+            os.environ["CS_FM_SA_BUILDER"] = saved
+
+
 @pytest.mark.parametrize("name", ["banana", "dna_5k", "bytes_5k", "abab_noterm", "rare_N_41",
                                   "alpha_16", "runs"])
 def test_create_from_arrays(pkg, name):
