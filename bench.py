@@ -23,8 +23,11 @@ Extra fields on the JSON line:
                reference-faithful count() (kind "port"; O(n) count_ones scans, as
                src/core/bitvector.cpp:168-170), on a bounded sample of the same
                batch, rank 0, N=1 only, all host threads.
-  p50_us       median end-to-end latency of single-pattern count() calls through
-               the C ABI (host pattern in, count out), as tools/benchmark.cpp:154-166.
+  p50_us       median end-to-end latency of single-pattern cs::FMIndex::count() calls
+               through the C++ facade (host pattern in, count out), as
+               tools/benchmark.cpp:154-166, with the index in serving mode (a resident
+               wave answers from a pinned mailbox); p50_launch_us: the same calls with
+               one kernel launch each.
 """
 import argparse
 import json
@@ -349,15 +352,27 @@ def main():
         blib = C.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libcs_bench.so"))
         fn = blib.cs_bench_facade_count_latency
         fn.restype = C.c_int
-        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p]
-        cnt1 = np.zeros(nq, np.uint64)
-        lat = np.zeros(nq, np.float64)
-        if fn(idx._h, hp.ctypes.data, m, nq, cnt1.ctypes.data, lat.ctypes.data) != 0:
-            raise RuntimeError("p50 facade loop failed: " + pkg.lib().cs_fm_last_error().decode())
-        assert np.array_equal(cnt1, counts[:nq].astype(np.uint64))
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
+                       C.c_int]
+
+        def facade_p50(serve):
+            cnt1 = np.zeros(nq, np.uint64)
+            lat = np.zeros(nq, np.float64)
+            if fn(idx._h, hp.ctypes.data, m, nq, cnt1.ctypes.data, lat.ctypes.data, serve) != 0:
+                raise RuntimeError("p50 facade loop failed: " + pkg.lib().cs_fm_last_error().decode())
+            assert np.array_equal(cnt1, counts[:nq].astype(np.uint64))
+            return lat
+
+        # serving mode (FMIndex::serve: a resident wave answers from a pinned mailbox)
+        # is the headline p50; the one-launch-per-call path is reported beside it
+        lat = facade_p50(1)
+        lat_launch = facade_p50(0)
         res["p50_us"] = float(np.median(lat))
         res["p95_us"] = float(np.percentile(lat, 95))
-        res["p50_method"] = "cs::FMIndex::count via the C++ facade, %d calls, steady_clock" % nq
+        res["p50_method"] = ("cs::FMIndex::count via the C++ facade in serving mode "
+                             "(FMIndex::serve), %d calls, steady_clock" % nq)
+        res["p50_launch_us"] = float(np.median(lat_launch))
+        res["p95_launch_us"] = float(np.percentile(lat_launch, 95))
         # the same through the Python mirror (ctypes), for reference
         lat_py = []
         for q in range(min(nq, 1000)):

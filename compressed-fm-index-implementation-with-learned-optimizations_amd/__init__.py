@@ -60,6 +60,8 @@ SIGNATURES = {
     "cs_fm_get_info": (C.c_int, [_vp, C.POINTER(cs_fm_info)]),
     "cs_fm_last_error": (C.c_char_p, []),
     "cs_fm_count": (C.c_int, [_vp, C.c_char_p, C.c_uint64, _u64p]),
+    "cs_fm_serve_start": (C.c_int, [_vp, C.c_uint32]),
+    "cs_fm_serve_stop": (C.c_int, [_vp]),
     "cs_fm_locate": (C.c_int, [_vp, _u8p, C.c_uint64, C.c_uint64, _u64p, C.c_uint64, _u64p]),
     "cs_fm_extract": (C.c_int, [_vp, C.c_uint64, C.c_uint64, _u8p, _u64p]),
     "cs_fm_extract_batch": (C.c_int, [_vp, _u64p, _u64p, C.c_uint64, _u64p, _u8p, C.c_uint64,
@@ -272,6 +274,15 @@ class FMIndex:
         out = C.c_uint64()
         _check(lib().cs_fm_count(self._h, b, len(b), C.byref(out)))
         return out.value
+
+    def serve(self, on: bool = True, idle_us: int = 0):
+        """Serving mode for single-pattern count(): a resident wave answers requests
+        from a pinned mailbox instead of one kernel launch per call (cs_fm_serve_start;
+        idle_us = idle exit, 0 = 10 ms).  serve(False) shuts it down."""
+        if on:
+            _check(lib().cs_fm_serve_start(self._h, idle_us))
+        else:
+            _check(lib().cs_fm_serve_stop(self._h))
 
     def locate(self, pattern, limit: int = 100000) -> list:
         offs, pos = self.locate_batch([pattern], limit)

@@ -125,8 +125,92 @@ struct StagedBatch {
   }
 };
 
+// ---- resident single-pattern server (cs_fm_serve_start) ----
+// All of these run with server.mu held.
+constexpr uint64_t kServeLifeUs = 10ull * 1000 * 1000;  // relaunched after 10 s busy
+
+bool server_exited(const cs_fm_index* h) {
+  return (__atomic_load_n(h->server.resp + 2, __ATOMIC_ACQUIRE) >> 63) != 0;
+}
+
+cs_status server_launch(const cs_fm_index* h, uint32_t seq_done) {
+  auto& S = h->server;
+  __atomic_store_n(S.resp + 2, 0ull, __ATOMIC_RELEASE);
+  const uint64_t tpu = S.ticks_per_us;
+  cs_status s = launch_count_server(h, seq_done, (uint64_t)S.idle_us * tpu, kServeLifeUs * tpu);
+  if (s != CS_OK) return s;
+  S.launched = true;
+  return CS_OK;
+}
+
+// Shut the kernel down (stop request, then wait for the stream) and free the
+// server's stream and mailbox.
+cs_status server_shutdown(const cs_fm_index* h) {
+  auto& S = h->server;
+  cs_status s = CS_OK;
+  if (S.launched) {
+    if (!server_exited(h)) {
+      const uint32_t tag = ++S.seq;
+      __atomic_store_n(S.mbox, ((uint64_t)tag << 32) | kServeStop, __ATOMIC_RELEASE);
+    }
+    hipError_t e = hipStreamSynchronize(S.st);
+    if (e != hipSuccess) s = hip_fail(e, "server stream");
+    S.launched = false;
+  }
+  if (S.st) (void)hipStreamDestroy(S.st);
+  if (S.mbox) (void)hipHostFree(S.mbox);
+  S.st = nullptr;
+  S.mbox = S.resp = nullptr;
+  S.enabled = false;
+  return s;
+}
+
+// One request: tag the words the pattern needs, then poll the answer.  A kernel that
+// exited (idle / lifetime) before taking the request is relaunched expecting it.
+cs_status serve_count(const cs_fm_index* h, const uint8_t* pat, uint32_t m, uint64_t* out) {
+  auto& S = h->server;
+  cs_status s;
+  if (!S.launched || server_exited(h)) {
+    if (S.launched) (void)hipStreamSynchronize(S.st);  // exited: reap it
+    if ((s = server_launch(h, S.seq)) != CS_OK) return s;
+  }
+  uint32_t tag = ++S.seq;
+  const uint64_t t = (uint64_t)tag << 32;
+  const uint32_t nw = 1 + (m + 3) / 4;
+  for (uint32_t w = 1; w < nw; ++w) {
+    uint32_t v = 0;
+    const uint32_t o = 4 * (w - 1);
+    std::memcpy(&v, pat + o, m - o < 4 ? m - o : 4);
+    __atomic_store_n(S.mbox + w, t | v, __ATOMIC_RELAXED);
+  }
+  __atomic_store_n(S.mbox, t | m, __ATOMIC_SEQ_CST);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 1;; ++spin) {
+    if ((uint32_t)__atomic_load_n(S.resp + 1, __ATOMIC_ACQUIRE) == tag) {
+      *out = __atomic_load_n(S.resp, __ATOMIC_RELAXED);
+      return CS_OK;
+    }
+    if ((spin & 255) == 0) {
+      if (server_exited(h)) {
+        if ((uint32_t)__atomic_load_n(S.resp + 1, __ATOMIC_ACQUIRE) == tag) continue;
+        FMX_HIP(hipStreamSynchronize(S.st));  // surfaces a kernel fault
+        if ((s = server_launch(h, tag - 1)) != CS_OK) return s;
+      } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        hipError_t e = hipStreamQuery(S.st);
+        if (e != hipSuccess && e != hipErrorNotReady) return hip_fail(e, "server kernel");
+        set_error("serve: no answer from the server kernel within 5 s");
+        return CS_ERR_HIP;
+      }
+    }
+  }
+}
+
 void free_index(cs_fm_index* h) {
   if (!h) return;
+  {
+    std::lock_guard<std::mutex> lk(h->server.mu);
+    (void)server_shutdown(h);
+  }
   if (h->d_lines) (void)hipFree(h->d_lines);
   if (h->d_ssa) (void)hipFree(h->d_ssa);
   if (h->d_table) (void)hipFree(h->d_table);
@@ -318,6 +402,10 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   hipStream_t st = (hipStream_t)stream;
   const uint64_t bytes = offs[npat] - offs[0];
   const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
+  if (npat == 1 && bytes <= kServeMax && h->server.enabled) {
+    std::unique_lock<std::mutex> lk(h->server.mu);
+    if (h->server.enabled) return serve_count(h, pats + offs[0], (uint32_t)bytes, out_counts);
+  }
   if (npat == 1 && bytes <= OnePattern::kMax) {
     // single pattern (the p50 path): pattern in the kernel arguments, count written
     // into the pinned arena by the kernel; one launch + one synchronisation
@@ -381,6 +469,47 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   FMX_HIP(hipMemcpyAsync(out_counts, d_out.p, npat * 8, hipMemcpyDeviceToHost, st));
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
+}
+
+cs_status cs_fm_serve_start(const cs_fm_index* h, uint32_t idle_us) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  auto& S = h->server;
+  std::lock_guard<std::mutex> lk(S.mu);
+  S.idle_us = idle_us ? idle_us : 10000;
+  if (S.enabled) return CS_OK;
+  int khz = 100000;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess ||
+      khz <= 0)
+    khz = 100000;
+  S.ticks_per_us = (uint64_t)khz / 1000 ? (uint64_t)khz / 1000 : 1;
+  void* p = nullptr;
+  FMX_HIP(hipHostMalloc(&p, 512, hipHostMallocCoherent));
+  std::memset(p, 0, 512);
+  S.mbox = static_cast<uint64_t*>(p);
+  S.resp = S.mbox + kServeWords;
+  S.seq = 0;
+  hipError_t e = hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    (void)server_shutdown(h);
+    return hip_fail(e, "hipStreamCreateWithFlags (server)");
+  }
+  S.enabled = true;
+  if ((s = server_launch(h, 0)) != CS_OK) (void)server_shutdown(h);
+  return s;
+}
+
+cs_status cs_fm_serve_stop(const cs_fm_index* h) {
+  if (!h) {
+    set_error("null index handle");
+    return CS_ERR_INVALID;
+  }
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  std::lock_guard<std::mutex> lk(h->server.mu);
+  return server_shutdown(h);
 }
 
 cs_status cs_fm_count(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t* out) {

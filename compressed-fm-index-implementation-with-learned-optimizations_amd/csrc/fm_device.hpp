@@ -115,6 +115,15 @@ struct OnePattern {
   uint32_t m;
 };
 
+// Resident single-pattern server (cs_fm_serve_start): the request mailbox is
+// kServeWords 8-byte words in fine-grained pinned host memory, each (tag << 32 |
+// payload) — word 0 carries the pattern length (kServeStop = shut down), words 1..
+// four pattern bytes each.  Aligned 8-byte stores and loads are single-copy atomic on
+// both sides, so a request is complete when every word it uses carries its tag.
+constexpr uint32_t kServeWords = 32;
+constexpr uint32_t kServeMax = (kServeWords - 1) * 4;  // 124 bytes
+constexpr uint32_t kServeStop = 0xFFFFFFFFu;
+
 __device__ __forceinline__ uint64_t ssa_at(const DevIndex& ix, uint64_t k) {
   return ix.wide ? static_cast<const uint64_t*>(ix.ssa)[k] : static_cast<const uint32_t*>(ix.ssa)[k];
 }

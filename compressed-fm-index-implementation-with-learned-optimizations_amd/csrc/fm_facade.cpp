@@ -87,6 +87,12 @@ uint64_t FMIndex::count(std::string_view pattern) const {
   return c;
 }
 
+void FMIndex::serve(bool on, uint32_t idle_us) const {
+  if (!h_) return;
+  cs_status s = on ? cs_fm_serve_start(h_.get(), idle_us) : cs_fm_serve_stop(h_.get());
+  if (s != CS_OK) raise(s);
+}
+
 std::vector<uint64_t> FMIndex::locate(std::string_view pattern, size_t limit) const {
   std::vector<uint64_t> out;
   if (!h_ || pattern.empty()) return out;  // fm_index.cpp:109

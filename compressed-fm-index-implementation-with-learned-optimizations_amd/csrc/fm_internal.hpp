@@ -49,6 +49,23 @@ struct cs_fm_index {
   static constexpr size_t kScratchBytes = 1u << 20;
   mutable Scratch scratch;
 
+  // Resident single-pattern server (cs_fm_serve_start): one wave on a private
+  // stream polls `mbox` and answers into `resp`; single-pattern counts go through it
+  // while `enabled`.  The kernel exits on a stop request, after idle_us without
+  // requests, or after a lifetime cap; the next request relaunches it.
+  struct Server {
+    std::mutex mu;
+    hipStream_t st = nullptr;
+    uint64_t* mbox = nullptr;  // pinned, fine-grained: kServeWords request words
+    uint64_t* resp = nullptr;  // pinned, fine-grained: [0] count, [1] tag served, [2] exit mark
+    uint32_t seq = 0;          // tag of the last request written
+    uint32_t idle_us = 0;
+    uint64_t ticks_per_us = 100;
+    bool enabled = false;
+    bool launched = false;     // a kernel was launched and its exit not yet observed
+  };
+  mutable Server server;
+
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
   uint32_t ptab_entry_bytes() const { return wide ? 16 : 8; }
   uint64_t ptab_entries() const {
@@ -128,6 +145,9 @@ cs_status launch_count_one(const cs_fm_index* h, const fmx::OnePattern& p, uint6
                            hipStream_t st);
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                              uint64_t npat, uint64_t* d_out, hipStream_t st);
+// the resident server kernel (one wave) on the handle's server stream
+cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t idle_ticks,
+                              uint64_t life_ticks);
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,

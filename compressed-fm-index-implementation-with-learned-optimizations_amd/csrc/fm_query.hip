@@ -418,6 +418,67 @@ __global__ void k_count_one(DevIndex ix, OnePattern p, uint64_t* __restrict__ ou
   __hip_atomic_store(out, res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Resident single-pattern server (cs_fm_serve_start; the p50 path without a launch
+// per query).  One wave: lanes 0..31 poll the request words in fine-grained pinned
+// host memory with system-scope loads; a request is taken when word 0 carries the
+// expected tag and so does every word its length uses.  Lane 0 runs the same
+// backward search as k_count_one over the LDS copy of the pattern and the node
+// table, stores the count and then (release) the tag it answers.  Exits on a stop
+// request, after idle_ticks without one, or after life_ticks in total — every exit
+// test is wave-uniform (wall clock, shuffled word 0, wave vote), so the wave always
+// drains; the exit mark (bit 63 | last tag served) is stored after the last answer.
+template <class E>
+__global__ __launch_bounds__(64) void k_count_server(DevIndex ix, const uint64_t* mbox,
+                                                     uint64_t* resp, uint32_t seq_done,
+                                                     uint64_t idle_ticks, uint64_t life_ticks) {
+  __shared__ NodeTable T;
+  __shared__ __attribute__((aligned(16))) uint8_t pat[kServeWords * 4];
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x;
+  uint32_t want = seq_done + 1;
+  const uint64_t t0 = (uint64_t)wall_clock64();
+  uint64_t t_last = t0;
+  for (;;) {
+    const uint64_t w =
+        lane < kServeWords
+            ? __hip_atomic_load(mbox + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+            : 0ull;
+    const uint64_t w0 = __shfl(w, 0);
+    if ((uint32_t)(w0 >> 32) == want) {
+      const uint32_t m = (uint32_t)w0;
+      const uint32_t nw = m == kServeStop ? 1u : 1u + (m + 3) / 4;
+      const bool ok = lane >= nw || (uint32_t)(w >> 32) == want;
+      if (__all(ok)) {
+        if (m == kServeStop) break;
+        if (lane >= 1 && lane < nw)
+          *reinterpret_cast<uint32_t*>(pat + 4 * (lane - 1)) = (uint32_t)w;
+        __syncthreads();
+        if (lane == 0) {
+          uint64_t res;
+          if (m == 0) res = ix.n;        // fm_index.cpp:80
+          else if (ix.n == 0) res = 0;   // :81
+          else {
+            uint64_t sp, ep;
+            res = backward_search<E>(ix, T, pat, m, sp, ep) ? ep - sp : 0;
+          }
+          __hip_atomic_store(resp, res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(resp + 1, (uint64_t)want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        ++want;
+        t_last = (uint64_t)wall_clock64();
+        continue;
+      }
+    }
+    const uint64_t now = (uint64_t)wall_clock64();
+    if (now - t_last > idle_ticks || now - t0 > life_ticks) break;
+  }
+  if (lane == 0)
+    __hip_atomic_store(resp + 2, (1ull << 63) | (uint64_t)(want - 1), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Measurement twin of k_count: the algorithmic bytes of each query's search —
 // distinct lines per rank pair (sp and ep in one line read once) times the line
 // size, plus the prefix-table entry — for the roofline in bench.py.
@@ -862,6 +923,14 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
 cs_status launch_count_one(const cs_fm_index* h, const OnePattern& p, uint64_t* out_host,
                            hipStream_t st) {
   FMX_DISPATCH1(h, k_count_one, h->dev(), p, out_host);
+  return CS_OK;
+}
+
+cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t idle_ticks,
+                              uint64_t life_ticks) {
+  hipStream_t st = h->server.st;
+  FMX_DISPATCH1(h, k_count_server, h->dev(), h->server.mbox, h->server.resp, seq_done, idle_ticks,
+                life_ticks);
   return CS_OK;
 }
 

@@ -5,7 +5,8 @@
 // through the C ABI in cs_fmindex.h (implementation: csrc/fm_facade.cpp inside
 // libcs_fmindex.so).  Additions: count_batch / locate_batch (one launch for many
 // patterns), save_directory (the on-disk format open_directory reads), handle()
-// for the raw ABI and borrow() to wrap an ABI handle.  Errors are
+// for the raw ABI, borrow() to wrap an ABI handle and serve() (resident
+// single-pattern server).  Errors are
 // std::runtime_error with the reference's message text ("locate: LF walk exceeded
 // text length").
 //
@@ -51,6 +52,10 @@ class FMIndex {
   std::vector<uint64_t> count_batch(const std::vector<std::string_view>& patterns) const;
   std::vector<std::vector<uint64_t>> locate_batch(const std::vector<std::string_view>& patterns,
                                                   size_t limit = 100000) const;
+
+  // Serving mode for single-pattern count(): a resident wave answers from a pinned
+  // mailbox instead of one kernel launch per call (cs_fm_serve_start / _stop).
+  void serve(bool on = true, uint32_t idle_us = 0) const;
 
   uint64_t size() const { return meta_.n; }
   const cs_fm_index* handle() const { return h_.get(); }

@@ -126,6 +126,18 @@ const char* cs_fm_last_error(void);
 
 /* FMIndex::count — fm_index.hpp:26, fm_index.cpp:79-101 (one pattern, host). */
 cs_status cs_fm_count(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t* out);
+/* Serving mode for single-pattern count (the p50 path; no reference counterpart —
+ * it replaces the per-query kernel launch behind FMIndex::count, fm_index.cpp:79-101).
+ * cs_fm_serve_start keeps one wave resident on a private non-blocking stream that
+ * polls a request mailbox in pinned host memory; while it is on, cs_fm_count and
+ * single-pattern cs_fm_count_batch calls with m <= 124 are answered by it (same
+ * results), longer patterns take the launch path.  The wave exits after idle_us
+ * without requests (0 = 10 ms) and is relaunched by the next request.  While it is
+ * resident, device-wide synchronisation (hipDeviceSynchronize, hipFree, …) waits
+ * for it to go idle.  cs_fm_serve_stop shuts it down and waits; cs_fm_destroy
+ * does it too.  Calls on one handle are serialised. */
+cs_status cs_fm_serve_start(const cs_fm_index* h, uint32_t idle_us);
+cs_status cs_fm_serve_stop(const cs_fm_index* h);
 /* FMIndex::locate — fm_index.hpp:32, fm_index.cpp:107-157 (one pattern, host).
  * Positions in BWT-row order; at most min(limit, cap) written; *nout = number. */
 cs_status cs_fm_locate(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, uint64_t limit,

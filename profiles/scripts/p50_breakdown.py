@@ -1,6 +1,7 @@
 """p50_breakdown.py — single-pattern count() latency on C4 by pattern shape:
 empty pattern (launch + result round trip only), 14-mer (prefix table only),
-16/18/20-mers (table + 2/4/6 rank steps), and the same through count_batch of 1."""
+16/18/20-mers (table + 2/4/6 rank steps); launch path (one kernel per call) and
+serving mode (FMIndex.serve: a resident wave answers from a pinned mailbox)."""
 import json
 import os
 import statistics
@@ -31,14 +32,19 @@ def main():
     torch.cuda.synchronize()
     hp = pats.cpu().numpy().reshape(npat, 20)
     res = {}
-    for m in (0, 14, 16, 18, 20):
-        lat = []
-        for q in range(npat):
-            b = hp[q, 20 - m:].tobytes()
-            t0 = time.perf_counter()
-            idx.count(b)
-            lat.append((time.perf_counter() - t0) * 1e6)
-        res["m%d_p50_us" % m] = statistics.median(lat[100:])
+    for mode in ("launch", "serve"):
+        if mode == "serve":
+            idx.serve(True)
+        for m in (0, 14, 16, 18, 20):
+            lat = []
+            for q in range(npat):
+                b = hp[q, 20 - m:].tobytes()
+                t0 = time.perf_counter()
+                idx.count(b)
+                lat.append((time.perf_counter() - t0) * 1e6)
+            res["%s_m%d_p50_us" % (mode, m)] = statistics.median(lat[100:])
+        if mode == "serve":
+            idx.serve(False)
     print(json.dumps(res))
 
 

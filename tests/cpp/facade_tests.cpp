@@ -141,6 +141,18 @@ int main() {
       cs_fm_destroy(h);  // the borrowed view never owned it
     }
   }
+  {  // serve(): single-pattern count() from the resident wave, same answers
+    std::string t = "mississippi$";
+    FMIndex idx = FMIndex::build_from_text(t, BuildParams{});
+    const char* qs[] = {"ssi", "i", "issi", "p", "x", "", "mississippi$", "pp", "s"};
+    std::vector<uint64_t> want;
+    for (const char* q : qs) want.push_back(idx.count(q));
+    idx.serve(true);
+    for (size_t k = 0; k < want.size(); ++k) CHECK(idx.count(qs[k]) == want[k]);
+    CHECK(idx.count(std::string(200, 's')) == 0);  // longer than the mailbox: launch path
+    idx.serve(false);
+    for (size_t k = 0; k < want.size(); ++k) CHECK(idx.count(qs[k]) == want[k]);
+  }
   if (failures) {
     std::fprintf(stderr, "%d facade checks failed\n", failures);
     return 1;
