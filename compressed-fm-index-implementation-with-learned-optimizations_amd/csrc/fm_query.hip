@@ -847,9 +847,11 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^30, max(4096, n/8)) entries (8 B each, 16 B in wide indexes:
-// at most n resp. 2n bytes, capped at 8 resp. 16 GiB); none when k < 2.
-// DNA: k = 11 at 100 MB, k = 14 at 4 GB, k = 15 at 32 GB.  Entries are (sp, ep) as 2 x u32, or
+// sigma^k <= min(2^30, max(4096, n/2)) entries (8 B each, 16 B in wide indexes:
+// at most 4n resp. 8n bytes, capped at 8 resp. 16 GiB); none when k < 2.  Each
+// character in the table saves one dependent random line read per query, and
+// HBM (288 GB) is not the constraint: C4 k = 14 -> 15 is +14 % count rate.
+// DNA: k = 12 at 100 MB, k = 15 at 4 GB and at 32 GB.  Entries are (sp, ep) as 2 x u32, or
 // 2 x u64 in wide indexes.  CS_FM_PREFIX_K overrides k (0 = off).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
@@ -868,7 +870,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     }
   }
   if (sigma == 0) return CS_OK;
-  uint64_t cap = n / 8 > 4096 ? n / 8 : 4096;
+  uint64_t cap = n / 2 > 4096 ? n / 2 : 4096;
   if (cap > (1ull << 30)) cap = 1ull << 30;
   uint32_t k = 0;
   uint64_t entries = 1;
