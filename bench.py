@@ -224,8 +224,10 @@ def main():
     if rank == 0:
         traffic = None
         prof = os.path.join(ROOT, "profiles", "pmc_count.json")
-        engine = "occ" if info.engine == 1 else "wm%d" % info.line_bytes
+        engine = {1: "occ", 2: "qwm"}.get(info.engine, "wm%d" % info.line_bytes)
         wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
+        if info.context_q:
+            wl += ":ctx%d" % info.context_q
         if args.queries != "text":
             wl += ":" + args.queries
         if os.path.exists(prof):
@@ -254,12 +256,16 @@ def main():
                        "collective": "gather of counts to rank 0 (%s), overlapped"
                        % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) if coll
                        else "none (independent query shards)",
-                       "engine": "occurrence lines" if info.engine == 1 else
+                       "engine": ("occurrence lines + left contexts (q=%d)" % info.context_q
+                                  if info.context_q else "occurrence lines") if info.engine == 1 else
+                       "quaternary wavelet matrix (%d levels of occurrence lines)" % info.levels
+                       if info.engine == 2 else
                        "wavelet matrix (%d-B rank lines)" % info.line_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,
                          "prefix_k": K, "prefix_table_hit_frac": table_frac,
+                         "context_q": info.context_q,
                          "alg_bytes_per_query": alg_bytes / B,
                          # SURVEY.md §8(d)'s per-query figure for the reference's
                          # structure (64 B x 8 levels x 2 ranks x (m-1) steps), for

@@ -465,6 +465,11 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
     FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
   }
   plog.mark("prefix table");
+  {
+    cs_status cs = build_left_contexts(h, st);
+    if (cs != CS_OK) return cs;
+  }
+  plog.mark("left contexts");
   FMX_HIP(hipMalloc(&h->d_err, 8));
   FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));

@@ -219,6 +219,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_isa) (void)hipFree(h->d_isa);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
+  if (h->d_lctx) (void)hipFree(h->d_lctx);
   if (h->scratch.h) (void)hipHostFree(h->scratch.h);
   if (h->scratch.d) (void)hipFree(h->scratch.d);
   delete h;
@@ -359,6 +360,8 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->rare_rows = h->line_fmt == kFmtOcc ? h->h_table.exc_n : 0u;
   out->walk_marks = h->d_walk ? h->walk_marks : 0u;
   out->walk_bytes = h->d_walk ? h->nwalk * 32 : 0u;
+  out->context_q = h->d_lctx ? kCtxQ : 0u;
+  out->context_bytes = h->d_lctx ? h->nlctx * 2 : 0u;
   return CS_OK;
 }
 

@@ -106,7 +106,20 @@ struct DevIndex {
   // Walk lines and the samples they index (WalkLine above); null when absent.
   const void* walk;
   const void* wssa;      // sample of each mark, in row order (u32, u64 wide)
+  // Left contexts (occurrence engine; null when absent): per BWT row the codes of the
+  // kCtxQ symbols its LF chain meets (see kCtxQ below).
+  const uint16_t* lctx;
 };
+
+// Left context of BWT row r: lctx[r] bits [2t, 2t+2) = 2-bit code of BWT[LF^t(r)],
+// t = 0..kCtxQ-1 — the kCtxQ characters preceding the row's rotation — and bit 15
+// (kCtxEsc) when one of them is a rare symbol.  A backward search with k <= kCtxQ
+// characters left and its range [sp, ep) inside two 32-B sectors of lctx counts
+// the rows whose context matches those characters in one read: the rows surviving
+// the remaining steps are exactly the rows whose chain spells them (each step keeps
+// {LF(r) : BWT[r] = c}, fm_index.cpp:90-96, monotone in r).
+constexpr uint32_t kCtxQ = 7;
+constexpr uint32_t kCtxEsc = 0x8000u;
 
 // A single pattern passed by value in kernel arguments (k_count_one).
 struct OnePattern {

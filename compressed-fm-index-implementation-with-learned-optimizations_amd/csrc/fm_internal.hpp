@@ -35,6 +35,8 @@ struct cs_fm_index {
   void* d_wssa = nullptr;             // position samples by mark (lf_exact), else d_ssa is used
   uint32_t walk_marks = 0;            // 0 no walk lines, 1 row marks, 2 text-position marks
   uint32_t ptab_k = 0, ptab_sigma = 0;
+  void* d_lctx = nullptr;             // left contexts (occurrence engine; DevIndex::lctx)
+  uint64_t nlctx = 0;                 // u16 entries allocated (rows rounded up + a pad sector)
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
 
@@ -99,6 +101,7 @@ struct cs_fm_index {
     d.lf_exact = lf_exact ? 1u : 0u;
     d.walk = d_walk;
     d.wssa = d_wssa ? d_wssa : d_ssa;
+    d.lctx = static_cast<const uint16_t*>(d_lctx);
     return d;
   }
 };
@@ -170,6 +173,7 @@ cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st);
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
                          const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st);
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
+cs_status build_left_contexts(cs_fm_index* h, hipStream_t st);
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st);
 

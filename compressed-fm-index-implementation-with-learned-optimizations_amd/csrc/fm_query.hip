@@ -134,6 +134,7 @@ __device__ __forceinline__ uint64_t exc_rank(const NodeTable& T, uint32_t c, uin
 // WM<F>: the 8-level wavelet matrix (the reference's WaveletTree) in rank lines F.
 template <class F>
 struct WM {
+  static constexpr bool kCtx = false;  // no left contexts
   __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
                                               uint64_t& sp, uint64_t& ep,
                                               uint64_t* bytes = nullptr) {
@@ -163,6 +164,7 @@ struct WM {
 // below i when c has code 0 (they are stored as code 0); rare symbols are counted
 // from the LDS list.  sp and ep in the same line share one read.
 struct OccE {
+  static constexpr bool kCtx = true;  // left contexts (DevIndex::lctx) when built
   __device__ static __forceinline__ uint64_t occ_line(const OccLine::Raw& v, uint32_t code,
                                                       uint64_t i) {
     return OccLine::base(v, code, i >> 6) + OccLine::prefix(v, code, (uint32_t)(i & 63));
@@ -237,6 +239,7 @@ struct OccE {
 // level, occ(c, i) = p_L(i) - S8[code(c)] (the WaveletTree::rank identity,
 // wavelet.cpp:59-96, in base 4).
 struct QWM {
+  static constexpr bool kCtx = false;
   __device__ static __forceinline__ const void* level(const DevIndex& ix, int l) {
     return static_cast<const uint8_t*>(ix.lines) + (uint64_t)l * ix.nlines * OccLine::kBytes;
   }
@@ -307,17 +310,14 @@ struct QWM {
   }
 };
 
-// Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
-// range empties.  Requires m >= 1, n >= 1.  The first step comes from C[]
+// Start of a backward search (fm_index.cpp:84-89): the first step from C[]
 // (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
-// pattern's last k characters are all in its alphabet.
-template <class E>
-__device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
-                                                const uint8_t* __restrict__ P, uint64_t m,
-                                                uint64_t& sp_out, uint64_t& ep_out,
-                                                uint64_t* bytes = nullptr) {
-  uint64_t sp, ep, k;  // k = characters still to process, P[k-1] .. P[0]
-  bool from_table = false;
+// pattern's last k characters are all in its alphabet.  k receives the characters
+// still to process (P[k-1] .. P[0]).  Requires m >= 1.
+__device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable& T,
+                                             const uint8_t* __restrict__ P, uint64_t m,
+                                             uint64_t& sp, uint64_t& ep, uint64_t& k,
+                                             uint64_t* bytes) {
   if (ix.ptab_k && m >= ix.ptab_k) {
     uint32_t t = 0;
     bool ok = true;
@@ -330,15 +330,24 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
       ptab_at(ix, t, sp, ep);
       if (bytes) *bytes += ix.wide ? 16u : 8u;
       k = m - ix.ptab_k;
-      from_table = true;
+      return;
     }
   }
-  if (!from_table) {
-    const uint32_t c = P[m - 1];
-    sp = T.C[c];  // occ(c,0)=0, occ(c,n)=freq(c)
-    ep = T.C[c + 1];
-    k = m - 1;
-  }
+  const uint32_t c = P[m - 1];
+  sp = T.C[c];  // occ(c,0)=0, occ(c,n)=freq(c)
+  ep = T.C[c + 1];
+  k = m - 1;
+}
+
+// Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
+// range empties.  Requires m >= 1, n >= 1.
+template <class E>
+__device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
+                                                const uint8_t* __restrict__ P, uint64_t m,
+                                                uint64_t& sp_out, uint64_t& ep_out,
+                                                uint64_t* bytes = nullptr) {
+  uint64_t sp, ep, k;
+  search_start(ix, T, P, m, sp, ep, k, bytes);
   if (sp >= ep) return false;
   uint32_t cn = k ? P[k - 1] : 0u;
   while (k-- > 0) {
@@ -349,6 +358,73 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
   sp_out = sp;
   ep_out = ep;
   return true;
+}
+
+// The last k <= kCtxQ characters P[0..k) of a count over the left contexts of the
+// rows [sp, ep) (fm_device.hpp kCtxQ): the rows whose chain spells P[k-1], ...,
+// P[0].  Needs ep - (sp & ~15) <= 32 (two aligned 32-B sectors of 16 rows).
+// Returns false — the caller keeps stepping — when a character is not coded or a
+// row in the range has a rare symbol in its context.
+__device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
+                                          const uint8_t* __restrict__ P, uint32_t k,
+                                          uint64_t sp, uint64_t ep, uint64_t& cnt,
+                                          uint64_t* bytes) {
+  uint32_t want = 0;
+  for (uint32_t t = 0; t < k; ++t) {  // chain symbol t = P[k-1-t]
+    const uint32_t d = T.occ_code[P[k - 1 - t]];
+    if (d == kNoCode) return false;
+    want |= d << (2 * t);
+  }
+  const uint32_t mask = ((1u << (2 * k)) - 1u) | kCtxEsc;
+  const uint64_t base = sp & ~15ull;
+  const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);  // rows [lo, hi) of 32
+  const uint4* p = reinterpret_cast<const uint4*>(ix.lctx + base);
+  const bool two = hi > 16;
+  if (bytes) *bytes += two ? 64u : 32u;
+  uint4 w[4];
+  w[0] = p[0];
+  w[1] = p[1];
+  if (two) {
+    w[2] = p[2];
+    w[3] = p[3];
+  } else {
+    w[2] = w[3] = make_uint4(0, 0, 0, 0);
+  }
+  const uint32_t* dw = reinterpret_cast<const uint32_t*>(w);
+  uint32_t match = 0, esc = 0;  // bit i: row base + i
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+    match |= (uint32_t)((e & mask) == want) << i;
+    esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+  }
+  const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+  if (esc & in) return false;
+  cnt = (uint64_t)__popc(match & in);
+  return true;
+}
+
+// count() of one pattern (fm_index.cpp:84-100), m >= 1, n >= 1: the backward
+// search, finished over the left contexts once at most kCtxQ characters remain and
+// the range is narrow (engines with contexts, when built).
+template <class E>
+__device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const NodeTable& T,
+                                                  const uint8_t* __restrict__ P, uint64_t m,
+                                                  uint64_t* bytes = nullptr) {
+  uint64_t sp, ep, k;
+  search_start(ix, T, P, m, sp, ep, k, bytes);
+  if (sp >= ep) return 0;
+  bool ctx = E::kCtx && ix.lctx != nullptr;
+  while (k > 0) {
+    if (ctx && k <= kCtxQ && ep - (sp & ~15ull) <= 32) {
+      uint64_t cnt;
+      if (ctx_count(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes)) return cnt;
+      ctx = false;
+    }
+    --k;
+    if (!E::step(ix, T, P[k], sp, ep, bytes)) return 0;
+  }
+  return ep - sp;
 }
 
 // Prefix table entry t: backward search of the k-mer whose j-th character from
@@ -379,6 +455,28 @@ __global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entri
   }
 }
 
+// Left contexts (fm_device.hpp kCtxQ): row r follows its LF chain kCtxQ steps
+// (the first line read is shared by neighbouring lanes, the rest are random).
+template <class E>
+__global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix, uint16_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < ix.n; r += stride) {
+    uint64_t p = r;
+    uint32_t v = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kCtxQ; ++t) {
+      uint32_t c;
+      p = E::lf(ix, T, p, &c);
+      const uint32_t d = T.occ_code[c];
+      v |= d == kNoCode ? kCtxEsc : d << (2 * t);
+    }
+    out[r] = (uint16_t)v;
+  }
+}
+
 template <class E>
 __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t npat,
@@ -393,10 +491,151 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
   if (m == 0) res = ix.n;       // fm_index.cpp:80
   else if (ix.n == 0) res = 0;  // :81
   else {
-    uint64_t sp, ep;
-    res = backward_search<E>(ix, T, pats + o0, m, sp, ep) ? ep - sp : 0;
+    res = count_pattern<E>(ix, T, pats + o0, m);
   }
   out[q] = res;
+}
+
+// The batch count over occurrence lines with left contexts, the C4/C5 shape: a
+// pattern of m <= 32 bytes whose last k = ptab_k characters are in the prefix table
+// and whose other m - k <= kCtxQ characters are coded needs two dependent reads —
+// its table entry, then the context sector(s) of its range.  Each lane takes U
+// patterns (q0 + j * kBlk) and runs them in stages so their reads are in flight
+// together: (A) offsets and pattern bytes (realigned dword loads, not byte loads),
+// table index and context key; (B) the U table entries; (C) the U context sectors;
+// (D) counts.  Anything else — longer patterns, symbols outside the table alphabet,
+// wide ranges, escaped contexts — takes count_pattern, the general search.
+constexpr uint32_t kFastM = 32;
+
+// bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
+// (u[i >> 2] >> 8 (i & 3)) & 0xFF.  Reads only the dwords holding pattern bytes.
+__device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats, uint64_t o0,
+                                               uint32_t m, uint32_t u[8]) {
+  const uint32_t* w0 = reinterpret_cast<const uint32_t*>(pats + (o0 & ~3ull));
+  const uint32_t a = (uint32_t)(o0 & 3) * 8;
+  const uint32_t nw = ((uint32_t)(o0 & 3) + m + 3) >> 2;
+  uint32_t w[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) w[j] = (uint32_t)j < nw ? w0[j] : 0u;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                    const uint64_t* __restrict__ offs,
+                                                    uint64_t npat, uint64_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint32_t K = ix.ptab_k;
+  const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
+  uint64_t o0[U], res[U], sp[U], ep[U];
+  uint32_t m[U], t[U], want[U], k[U];
+  uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search
+  // (A)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    st[j] = 0;
+    res[j] = 0;
+    o0[j] = 0;
+    m[j] = 0;
+    t[j] = want[j] = k[j] = 0;
+    if (q >= npat) continue;
+    o0[j] = offs[q];
+    const uint64_t mm = offs[q + 1] - o0[j];
+    m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
+    if (mm == 0) {
+      res[j] = ix.n;  // fm_index.cpp:80
+      continue;
+    }
+    if (ix.n == 0) continue;  // :81
+    st[j] = 3;
+    if (mm > kFastM || mm < K || K == 0) continue;
+    uint32_t u[8];
+    load_pattern32(pats, o0[j], m[j], u);
+    const uint32_t kk = m[j] - K;
+    bool ok = true, cok = kk <= kCtxQ;
+    uint32_t tt = 0, ww = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kFastM; ++i) {
+      const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i >= kk && i < m[j]) {  // table part, most significant first
+        const uint32_t d = T.code[b];
+        ok &= d != kNoCode;
+        tt = tt * ix.ptab_sigma + d;
+      } else if (i < kk && i < kCtxQ) {  // context part: chain symbol kk-1-i
+        const uint32_t d = T.occ_code[b];
+        cok &= d != kNoCode;
+        ww |= (d & 3u) << (2 * (kk - 1 - i));
+      }
+    }
+    if (!ok) continue;
+    st[j] = cok ? 2 : 1;
+    t[j] = tt;
+    want[j] = ww;
+    k[j] = kk;
+  }
+  // (B)
+#pragma unroll
+  for (int j = 0; j < U; ++j)
+    if (st[j] == 1 || st[j] == 2) ptab_at(ix, t[j], sp[j], ep[j]);
+  // (C)
+  uint4 w[U][4];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (st[j] != 1 && st[j] != 2) continue;
+    if (sp[j] >= ep[j]) {
+      st[j] = 0;
+      res[j] = 0;
+    } else if (k[j] == 0) {
+      st[j] = 0;
+      res[j] = ep[j] - sp[j];
+    } else if (st[j] == 2 && ep[j] - (sp[j] & ~15ull) <= 32) {
+      const uint4* p = reinterpret_cast<const uint4*>(ix.lctx + (sp[j] & ~15ull));
+      w[j][0] = p[0];
+      w[j][1] = p[1];
+      if (ep[j] - (sp[j] & ~15ull) > 16) {
+        w[j][2] = p[2];
+        w[j][3] = p[3];
+      } else {
+        w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      st[j] = 3;
+    }
+  }
+  // (D)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (st[j] == 2) {
+      const uint32_t mask = ((1u << (2 * k[j])) - 1u) | kCtxEsc;
+      const uint64_t base = sp[j] & ~15ull;
+      const uint32_t lo = (uint32_t)(sp[j] - base), hi = (uint32_t)(ep[j] - base);
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(w[j]);
+      uint32_t match = 0, esc = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        match |= (uint32_t)((e & mask) == want[j]) << i;
+        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+      }
+      const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      if (esc & in) {
+        st[j] = 3;
+      } else {
+        res[j] = (uint64_t)__popc(match & in);
+        st[j] = 0;
+      }
+    }
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    if (q < npat && st[j] != 3) out[q] = res[j];
+  }
+  // the general search for the rest, with only (o0, m) of each pattern still live
+#pragma unroll
+  for (int j = 0; j < U; ++j)
+    if (st[j] == 3) out[q0 + (uint64_t)j * kBlk] = count_pattern<OccE>(ix, T, pats + o0[j], m[j]);
 }
 
 // Single-pattern count (FMIndex::count, the p50 path): the pattern travels in the
@@ -411,8 +650,7 @@ __global__ void k_count_one(DevIndex ix, OnePattern p, uint64_t* __restrict__ ou
   if (p.m == 0) res = ix.n;       // fm_index.cpp:80
   else if (ix.n == 0) res = 0;    // :81
   else {
-    uint64_t sp, ep;
-    res = backward_search<E>(ix, T, p.b, p.m, sp, ep) ? ep - sp : 0;
+    res = count_pattern<E>(ix, T, p.b, p.m);
   }
   // system-scope store: the host polls this word instead of waiting for the stream
   __hip_atomic_store(out, res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -459,8 +697,7 @@ __global__ __launch_bounds__(64) void k_count_server(DevIndex ix, const uint64_t
           if (m == 0) res = ix.n;        // fm_index.cpp:80
           else if (ix.n == 0) res = 0;   // :81
           else {
-            uint64_t sp, ep;
-            res = backward_search<E>(ix, T, pat, m, sp, ep) ? ep - sp : 0;
+            res = count_pattern<E>(ix, T, pat, m);
           }
           __hip_atomic_store(resp, res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(resp + 1, (uint64_t)want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -493,10 +730,7 @@ __global__ __launch_bounds__(kBlk) void k_count_bytes(DevIndex ix, const uint8_t
   if (q >= npat) return;
   const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
   uint64_t bytes = 0;
-  if (m && ix.n) {
-    uint64_t sp, ep;
-    (void)backward_search<E>(ix, T, pats + o0, m, sp, ep, &bytes);
-  }
+  if (m && ix.n) (void)count_pattern<E>(ix, T, pats + o0, m, &bytes);
   out[q] = bytes;
 }
 
@@ -902,6 +1136,30 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   return CS_OK;
 }
 
+// Left contexts for the occurrence engine: n u16 (2n bytes; C4 8 GB), rows rounded
+// up to whole 32-B sectors plus one pad sector.  Skipped (count steps through the
+// lines instead) for the other engines, when CS_FM_LCTX=0, or when HBM is short:
+// the index must leave a quarter of the device free.
+cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
+  h->d_lctx = nullptr;
+  h->nlctx = 0;
+  if (h->line_fmt != kFmtOcc || h->n == 0) return CS_OK;
+  if (const char* e = std::getenv("CS_FM_LCTX"))
+    if (std::atoi(e) == 0) return CS_OK;
+  const uint64_t rows = ((h->n + 15) & ~15ull) + 16;
+  size_t free_b = 0, total_b = 0;
+  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (rows * 2 + total_b / 4 > free_b) return CS_OK;
+  FMX_HIP(hipMalloc(&h->d_lctx, rows * 2));
+  h->nlctx = rows;
+  FMX_HIP(hipMemsetAsync(static_cast<uint16_t*>(h->d_lctx) + h->n, 0, (rows - h->n) * 2, st));
+  const DevIndex ix = h->dev();
+  k_build_lctx<OccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(ix, static_cast<uint16_t*>(h->d_lctx));
+  FMX_HIP(hipGetLastError());
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
                          const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st) {
   if (!k) return CS_OK;
@@ -918,6 +1176,22 @@ cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st) {
   if (!npat) return CS_OK;
+  if (h->line_fmt == kFmtOcc && h->d_lctx && h->ptab_k) {
+    static const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U)
+      const char* e = std::getenv("CS_FM_COUNT_U");
+      const int u = e ? std::atoi(e) : 2;
+      return u == 1 || u == 4 ? u : 2;
+    }();
+    const DevIndex ix = h->dev();
+    if (U == 1)
+      k_count_ctx<1><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_out);
+    else if (U == 2)
+      k_count_ctx<2><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_out);
+    else
+      k_count_ctx<4><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_out);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
   FMX_DISPATCH(h, k_count, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat, d_out);
   return CS_OK;
 }

@@ -76,6 +76,10 @@ typedef struct cs_fm_info {
   uint32_t walk_marks;     /* locate walk lines: 0 none, 1 sampled rows (row % stride == 0),
                               2 sampled text positions (needs a unique smallest terminator) */
   uint64_t walk_bytes;
+  uint32_t context_q;      /* left contexts: symbols per BWT row a count may finish with
+                              in one read (0 = none; occurrence lines only) */
+  uint32_t reserved;
+  uint64_t context_bytes;
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -9,9 +9,8 @@ profile_count.sh into <prof_dir>/summary.json:
   bench:   the bench JSON line each pass printed (the un-profiled numbers are in
            BENCH_rNN.json; profiled passes run slower, MI355X_MICROARCH 'DVFS
            give-back' item 2).
-FETCH_SIZE is reported raw; the gfx950 correction (x2 for wide coalesced streams)
-is NOT applied because this kernel's access is random 64-B lines — the factor for
-that width is calibrated separately (profiles/microbench).
+FETCH_SIZE is reported raw in `pmc`; pmc_count.json converts it to HBM bytes with
+the request mix of the count kernel (see the correction note written there).
 """
 import csv
 import glob
@@ -30,7 +29,7 @@ def rows(pattern):
 
 
 def short(name):
-    for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_lines", "k_walk_pack",
+    for k in ("k_count_bytes", "k_count_one", "k_count_ctx", "k_count", "k_build_lctx", "k_walk_lines", "k_walk_pack",
               "k_walk_base", "k_walk_samples", "k_walk", "k_occ_pack", "k_occ_base", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt_ssa", "k_bwt",
               "k_build_ptab",
               "k_partition", "k_pack_level", "k_init_keys", "k_double_keys", "k_heads",
@@ -79,18 +78,31 @@ def main():
         json.dump(res, f, indent=1)
     # pmc_count.json for bench.py's roofline.traffic (copy into profiles/ to use)
     b = res["bench"].get("bench_trace.json") or {}
-    kc = res["pmc"].get("k_count", {})
+    kname = "k_count_ctx" if "FETCH_SIZE" in res["pmc"].get("k_count_ctx", {}) else "k_count"
+    kc = res["pmc"].get(kname, {})
     if b and "FETCH_SIZE" in kc:
-        pc = {"workload": b.get("config", {}).get("workload_key"), "kernel": "k_count",
+        # FETCH_SIZE = TCC_EA0_RDREQ x 64 B.  Requests of this kernel: random 32-B
+        # reads (rank lines, context sectors, table entries: one request each, tallied
+        # at 64 B — profiles/microbench/gather_bench calibration) and the coalesced
+        # stream of patterns + offsets (128-B requests tallied at 64 B, the guide's
+        # gfx950 x2).  bytes = stream + (requests - stream / 128) x 32.
+        cfg = b.get("config", {})
+        B, m = cfg.get("batch_per_gpu", 0), cfg.get("m", 0)
+        stream = B * m + (B + 1) * 8
+        req = kc["FETCH_SIZE"] * 1024 / 64
+        pc = {"workload": cfg.get("workload_key"), "kernel": kname,
               "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
-              "hbm_bytes_per_launch": kc["FETCH_SIZE"] * 1024 / 2,
-              "correction": "x1/2: FETCH_SIZE tallies every L2->EA read request at 64 B; the "
-                            "count kernel's requests are 32-B rank lines (calibrated with "
-                            "profiles/microbench/gather_bench: 1 request per random 32-B read, "
-                            "FETCH_SIZE = 64 B per read, throughput = 32-B transfers)",
+              "read_requests_per_launch": req,
+              "stream_bytes_per_launch": stream,
+              "hbm_bytes_per_launch": stream + max(req - stream / 128, 0) * 32,
+              "correction": "FETCH_SIZE/64 B = read requests; the pattern/offset stream "
+                            "(B*m + 8(B+1) bytes, 128-B requests) counted at its byte size, "
+                            "every other request a random 32-B read (calibrated with "
+                            "profiles/microbench/gather_bench: 1 request per random 32-B "
+                            "read, FETCH_SIZE = 64 B per read)",
               "l2_hit_rate": kc.get("l2_hit_rate"),
               "tcc_miss_per_launch": kc.get("TCC_MISS_sum"),
-              "kernel_mean_ns_profiled": res["kernels"].get("k_count", {}).get("mean_ns"),
+              "kernel_mean_ns_profiled": res["kernels"].get(kname, {}).get("mean_ns"),
               "tag": tag}
         with open(os.path.join(d, "pmc_count.json"), "w") as f:
             json.dump(pc, f, indent=1)

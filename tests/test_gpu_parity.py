@@ -28,6 +28,7 @@ ENGINE_VARIANTS = {
     "auto_noprefix": {"CS_FM_PREFIX_K": "0"},       # prefix table off
     "auto_rowmarks": {"CS_FM_WALK_MARKS": "row"},   # walk lines with the reference's row samples
     "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
+    "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
     "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
@@ -37,7 +38,7 @@ ENGINE_VARIANTS = {
     "wide_wavelet": {"CS_FM_WIDE": "1", "CS_FM_ENGINE": "wavelet"},
 }
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
-          "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS")
+          "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -181,6 +182,9 @@ def test_engine_choice(built):
         assert (info.engine, info.rare_rows, info.walk_marks) == (engine, rare, marks), name
         want_levels = {0: 8, 1: 1, 2: levels[name]}[engine]
         assert info.levels == want_levels and info.line_bytes in (32, 64), name
+        ctx = 7 if engine == 1 and os.environ.get("CS_FM_LCTX") != "0" else 0
+        assert info.context_q == ctx, name
+        assert info.context_bytes == (((info.n + 15) // 16 + 1) * 32 if ctx else 0), name
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))
@@ -199,6 +203,28 @@ def test_wavelet_rank_access_lf(built, name):
     assert g.lf(rows).tolist() == [o.lf(int(i)) for i in rows]
     assert g.C().tolist() == o.C().tolist()
     assert g.ssa().tolist() == o.ssa().tolist()
+
+
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_count_every_text_vs_oracle(built, name):
+    """count() of substrings and one-symbol mutants of every test text: ranges of
+    every width around the left contexts' 32-B sectors (one or two, or too wide),
+    chains through rare rows (escaped contexts), patterns the text lacks."""
+    g, o = built(name)
+    t = TEXTS[name]
+    n = len(t)
+    rng = np.random.default_rng(n)
+    pats = []
+    for m in (1, 2, 3, 5, 6, 7, 8, 9, 12, 20):
+        for i in rng.integers(0, max(1, n - m + 1), 40):
+            p = bytearray(t[i:i + m])
+            pats.append(bytes(p))
+            if p:
+                p[rng.integers(0, len(p))] = t[rng.integers(0, n)]
+                pats.append(bytes(p))
+    assert g.count_batch(pats).tolist() == [o.count(p) for p in pats], name
+    for p in pats[::37]:  # single-pattern path (kernel arguments)
+        assert g.count(p) == o.count(p), (name, p)
 
 
 def _check_fm_case(pkg, case):
@@ -341,6 +367,7 @@ def test_save_open_directory_roundtrip(pkg, tmp_path):
     g.save_directory(d)
     h = pkg.FMIndex.open_directory(d)
     assert h.n == len(t)
+    assert (h.info().context_q, h.info().context_bytes) == (g.info().context_q, g.info().context_bytes)
     rng = np.random.default_rng(4)
     pats = [t[i:i + m] for i, m in zip(rng.integers(0, 39000, 300), rng.integers(1, 30, 300))]
     assert h.count_batch(pats).tolist() == g.count_batch(pats).tolist()
