@@ -360,8 +360,8 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->rare_rows = h->line_fmt == kFmtOcc ? h->h_table.exc_n : 0u;
   out->walk_marks = h->d_walk ? h->walk_marks : 0u;
   out->walk_bytes = h->d_walk ? h->nwalk * 32 : 0u;
-  out->context_q = h->d_lctx ? kCtxQ : 0u;
-  out->context_bytes = h->d_lctx ? h->nlctx * 2 : 0u;
+  out->context_q = h->d_lctx ? h->lctx_q : 0u;
+  out->context_bytes = h->d_lctx ? h->nlctx * h->lctx_eb : 0u;
   return CS_OK;
 }
 

@@ -106,18 +106,23 @@ struct DevIndex {
   // Walk lines and the samples they index (WalkLine above); null when absent.
   const void* walk;
   const void* wssa;      // sample of each mark, in row order (u32, u64 wide)
-  // Left contexts (occurrence engine; null when absent): per BWT row the codes of the
-  // kCtxQ symbols its LF chain meets (see kCtxQ below).
-  const uint16_t* lctx;
+  // Left contexts (null when absent): per BWT row the codes of the lctx_q symbols
+  // its LF chain meets, lctx_sb bits each (see kCtxQ below).
+  const void* lctx;
+  uint32_t lctx_q;
+  uint32_t lctx_sb;
 };
 
-// Left context of BWT row r: lctx[r] bits [2t, 2t+2) = 2-bit code of BWT[LF^t(r)],
-// t = 0..kCtxQ-1 — the kCtxQ characters preceding the row's rotation — and bit 15
-// (kCtxEsc) when one of them is a rare symbol.  A backward search with k <= kCtxQ
-// characters left and its range [sp, ep) inside two 32-B sectors of lctx counts
-// the rows whose context matches those characters in one read: the rows surviving
-// the remaining steps are exactly the rows whose chain spells them (each step keeps
-// {LF(r) : BWT[r] = c}, fm_index.cpp:90-96, monotone in r).
+// Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q
+// characters preceding the row's rotation — symbol t in bits [sb t, sb (t+1)).
+// Occurrence engine: u16 entries, 2-bit codes, q = kCtxQ = 7, and bit 15 (kCtxEsc)
+// when one of the symbols is a rare one.  Quaternary matrix: u32 entries, the dense
+// symbol code (sb = 2 x levels bits: 8 for sigma = 256), q = 32 / sb (4 for sigma =
+// 256), no escapes (every present symbol has a code).  A backward search with
+// k <= q characters left and its range [sp, ep) inside two 32-B sectors of lctx
+// counts the rows whose context matches those characters in one read: the rows
+// surviving the remaining steps are exactly the rows whose chain spells them (each
+// step keeps {LF(r) : BWT[r] = c}, fm_index.cpp:90-96, monotone in r).
 constexpr uint32_t kCtxQ = 7;
 constexpr uint32_t kCtxEsc = 0x8000u;
 

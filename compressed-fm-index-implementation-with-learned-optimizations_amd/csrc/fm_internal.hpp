@@ -35,8 +35,10 @@ struct cs_fm_index {
   void* d_wssa = nullptr;             // position samples by mark (lf_exact), else d_ssa is used
   uint32_t walk_marks = 0;            // 0 no walk lines, 1 row marks, 2 text-position marks
   uint32_t ptab_k = 0, ptab_sigma = 0;
-  void* d_lctx = nullptr;             // left contexts (occurrence engine; DevIndex::lctx)
-  uint64_t nlctx = 0;                 // u16 entries allocated (rows rounded up + a pad sector)
+  void* d_lctx = nullptr;             // left contexts (DevIndex::lctx)
+  uint64_t nlctx = 0;                 // entries allocated (rows rounded up + a pad sector)
+  uint32_t lctx_q = 0, lctx_sb = 0;   // symbols per entry, bits per symbol
+  uint32_t lctx_eb = 0;               // bytes per entry (2 occurrence lines, 4 quaternary matrix)
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
 
@@ -101,7 +103,9 @@ struct cs_fm_index {
     d.lf_exact = lf_exact ? 1u : 0u;
     d.walk = d_walk;
     d.wssa = d_wssa ? d_wssa : d_ssa;
-    d.lctx = static_cast<const uint16_t*>(d_lctx);
+    d.lctx = d_lctx;
+    d.lctx_q = d_lctx ? lctx_q : 0u;
+    d.lctx_sb = lctx_sb;
     return d;
   }
 };

@@ -10,14 +10,14 @@
 // Directory layout (all little-endian raw arrays, exactly the HBM images):
 //   cs_fmindex.meta  "key value" lines: format, n, stride, line_bytes, line_bits,
 //                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
-//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx,
+//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb,
 //                    active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
 //   ssa.bin          sampled SA              isa.bin   inverse-SA samples (u32; u64 if wide)
 //   ptab.bin         prefix table (if k > 0) text.bin  the text (if kept, for extract)
 //   walk.bin         walk lines                      wssa.bin  their position samples
-//   lctx.bin         left contexts (occurrence engine, if built)
+//   lctx.bin         left contexts (if built)
 // The device image (cs_fm_export_* / cs_fm_import) is the same meta text plus the
 // parts table, lines, ssa, isa[, ptab][, walk][, wssa][, lctx] as device buffers.
 #include <cerrno>
@@ -107,7 +107,7 @@ std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa) {
   if (h->ptab_k) v.push_back({"ptab.bin", &h->d_ptab, h->ptab_entries() * h->ptab_entry_bytes()});
   if (h->nwalk) v.push_back({"walk.bin", &h->d_walk, h->nwalk * 32});
   if (has_wssa) v.push_back({"wssa.bin", &h->d_wssa, h->nisa * sb});
-  if (h->nlctx) v.push_back({"lctx.bin", &h->d_lctx, h->nlctx * 2});
+  if (h->nlctx) v.push_back({"lctx.bin", &h->d_lctx, h->nlctx * h->lctx_eb});
   return v;
 }
 
@@ -117,13 +117,13 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
                 "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
                 "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n"
-                "nlctx %llu\n",
+                "nlctx %llu\nlctx_q %u\nlctx_sb %u\nlctx_eb %u\n",
                 kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                 (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                 (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
                 has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
                 (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0,
-                (unsigned long long)(h->d_lctx ? h->nlctx : 0));
+                (unsigned long long)(h->d_lctx ? h->nlctx : 0), h->lctx_q, h->lctx_sb, h->lctx_eb);
   std::string m(buf);
   for (int c = 0; c < 256; ++c) {
     std::snprintf(buf, sizeof buf, "active %d %u\n", c, h->active_levels[c]);
@@ -168,6 +168,9 @@ cs_status meta_parse(const std::string& text, cs_fm_index* h,
   h->nwalk = kv["nwalk"];
   h->walk_marks = (uint32_t)kv["walk_marks"];
   h->nlctx = kv["nlctx"];  // absent in indexes saved before left contexts: none
+  h->lctx_q = (uint32_t)kv["lctx_q"];
+  h->lctx_sb = (uint32_t)kv["lctx_sb"];
+  h->lctx_eb = (uint32_t)kv["lctx_eb"];
   return CS_OK;
 }
 

@@ -135,6 +135,7 @@ __device__ __forceinline__ uint64_t exc_rank(const NodeTable& T, uint32_t c, uin
 template <class F>
 struct WM {
   static constexpr bool kCtx = false;  // no left contexts
+  using CtxEnt = uint32_t;
   __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
                                               uint64_t& sp, uint64_t& ep,
                                               uint64_t* bytes = nullptr) {
@@ -165,6 +166,7 @@ struct WM {
 // from the LDS list.  sp and ep in the same line share one read.
 struct OccE {
   static constexpr bool kCtx = true;  // left contexts (DevIndex::lctx) when built
+  using CtxEnt = uint16_t;
   __device__ static __forceinline__ uint64_t occ_line(const OccLine::Raw& v, uint32_t code,
                                                       uint64_t i) {
     return OccLine::base(v, code, i >> 6) + OccLine::prefix(v, code, (uint32_t)(i & 63));
@@ -239,7 +241,8 @@ struct OccE {
 // level, occ(c, i) = p_L(i) - S8[code(c)] (the WaveletTree::rank identity,
 // wavelet.cpp:59-96, in base 4).
 struct QWM {
-  static constexpr bool kCtx = false;
+  static constexpr bool kCtx = true;
+  using CtxEnt = uint32_t;
   __device__ static __forceinline__ const void* level(const DevIndex& ix, int l) {
     return static_cast<const uint8_t*>(ix.lines) + (uint64_t)l * ix.nlines * OccLine::kBytes;
   }
@@ -360,26 +363,37 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
   return true;
 }
 
-// The last k <= kCtxQ characters P[0..k) of a count over the left contexts of the
+// The last k <= lctx_q characters P[0..k) of a count over the left contexts of the
 // rows [sp, ep) (fm_device.hpp kCtxQ): the rows whose chain spells P[k-1], ...,
-// P[0].  Needs ep - (sp & ~15) <= 32 (two aligned 32-B sectors of 16 rows).
-// Returns false — the caller keeps stepping — when a character is not coded or a
-// row in the range has a rare symbol in its context.
+// P[0].  Needs ep - (sp & ~(R-1)) <= 2R, R = rows per 32-B sector (16 for u16
+// entries, 8 for u32).  Returns false — the caller keeps stepping — when a character
+// has no code (a rare symbol) or a row in the range has an escaped context; a
+// character absent from the text gives 0, as the reference's step would.
+template <class Ent>
 __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
                                           const uint8_t* __restrict__ P, uint32_t k,
                                           uint64_t sp, uint64_t ep, uint64_t& cnt,
                                           uint64_t* bytes) {
+  constexpr uint32_t R = 32 / sizeof(Ent);
+  constexpr bool kEsc = sizeof(Ent) == 2;
+  const uint32_t sb = kEsc ? 2u : ix.lctx_sb;
   uint32_t want = 0;
   for (uint32_t t = 0; t < k; ++t) {  // chain symbol t = P[k-1-t]
-    const uint32_t d = T.occ_code[P[k - 1 - t]];
+    const uint32_t c = P[k - 1 - t];
+    if (T.C[c] == T.C[c + 1]) {  // absent: the reference's step returns 0
+      cnt = 0;
+      return true;
+    }
+    const uint32_t d = T.occ_code[c];
     if (d == kNoCode) return false;
-    want |= d << (2 * t);
+    want |= d << (sb * t);
   }
-  const uint32_t mask = ((1u << (2 * k)) - 1u) | kCtxEsc;
-  const uint64_t base = sp & ~15ull;
-  const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);  // rows [lo, hi) of 32
-  const uint4* p = reinterpret_cast<const uint4*>(ix.lctx + base);
-  const bool two = hi > 16;
+  const uint32_t kb = sb * k;
+  const uint32_t mask = (kb >= 32 ? ~0u : ((1u << kb) - 1u)) | (kEsc ? kCtxEsc : 0u);
+  const uint64_t base = sp & ~(uint64_t)(R - 1);
+  const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);  // rows [lo, hi) of 2R
+  const uint4* p = reinterpret_cast<const uint4*>(static_cast<const Ent*>(ix.lctx) + base);
+  const bool two = hi > R;
   if (bytes) *bytes += two ? 64u : 32u;
   uint4 w[4];
   w[0] = p[0];
@@ -393,10 +407,10 @@ __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(w);
   uint32_t match = 0, esc = 0;  // bit i: row base + i
 #pragma unroll
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+  for (int i = 0; i < (int)(2 * R); ++i) {
+    const uint32_t e = kEsc ? (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu : dw[i];
     match |= (uint32_t)((e & mask) == want) << i;
-    esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+    if (kEsc) esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
   }
   const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
   if (esc & in) return false;
@@ -414,11 +428,12 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
   uint64_t sp, ep, k;
   search_start(ix, T, P, m, sp, ep, k, bytes);
   if (sp >= ep) return 0;
+  constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
   bool ctx = E::kCtx && ix.lctx != nullptr;
   while (k > 0) {
-    if (ctx && k <= kCtxQ && ep - (sp & ~15ull) <= 32) {
+    if (ctx && k <= ix.lctx_q && ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R) {
       uint64_t cnt;
-      if (ctx_count(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes)) return cnt;
+      if (ctx_count<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes)) return cnt;
       ctx = false;
     }
     --k;
@@ -455,25 +470,27 @@ __global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entri
   }
 }
 
-// Left contexts (fm_device.hpp kCtxQ): row r follows its LF chain kCtxQ steps
-// (the first line read is shared by neighbouring lanes, the rest are random).
+// Left contexts (fm_device.hpp kCtxQ): row r follows its LF chain q steps (the
+// first line read is shared by neighbouring lanes, the rest are random).
 template <class E>
-__global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix, uint16_t* __restrict__ out) {
+__global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix,
+                                                     typename E::CtxEnt* __restrict__ out) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
+  constexpr bool kEsc = sizeof(typename E::CtxEnt) == 2;
+  const uint32_t q = ix.lctx_q, sb = ix.lctx_sb;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < ix.n; r += stride) {
     uint64_t p = r;
     uint32_t v = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < kCtxQ; ++t) {
+    for (uint32_t t = 0; t < q; ++t) {
       uint32_t c;
       p = E::lf(ix, T, p, &c);
       const uint32_t d = T.occ_code[c];
-      v |= d == kNoCode ? kCtxEsc : d << (2 * t);
+      v |= (kEsc && d == kNoCode) ? kCtxEsc : d << (sb * t);
     }
-    out[r] = (uint16_t)v;
+    out[r] = (typename E::CtxEnt)v;
   }
 }
 
@@ -593,7 +610,8 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
       st[j] = 0;
       res[j] = ep[j] - sp[j];
     } else if (st[j] == 2 && ep[j] - (sp[j] & ~15ull) <= 32) {
-      const uint4* p = reinterpret_cast<const uint4*>(ix.lctx + (sp[j] & ~15ull));
+      const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
+                                                      (sp[j] & ~15ull));
       w[j][0] = p[0];
       w[j][1] = p[1];
       if (ep[j] - (sp[j] & ~15ull) > 16) {
@@ -1136,25 +1154,39 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   return CS_OK;
 }
 
-// Left contexts for the occurrence engine: n u16 (2n bytes; C4 8 GB), rows rounded
-// up to whole 32-B sectors plus one pad sector.  Skipped (count steps through the
-// lines instead) for the other engines, when CS_FM_LCTX=0, or when HBM is short:
-// the index must leave a quarter of the device free.
+// Left contexts: u16 per row over occurrence lines (2n bytes; C4 8 GB), u32 over the
+// quaternary matrix (4n bytes; C3 4 GB); rows rounded up to whole 32-B sectors plus
+// one pad sector.  Skipped (count steps through the rank structure instead) for the
+// binary wavelet matrix, when CS_FM_LCTX=0, or when HBM is short: the index must
+// leave a quarter of the device free.
 cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   h->d_lctx = nullptr;
   h->nlctx = 0;
-  if (h->line_fmt != kFmtOcc || h->n == 0) return CS_OK;
+  h->lctx_q = h->lctx_sb = h->lctx_eb = 0;
+  const bool occ = h->line_fmt == kFmtOcc, qwm = h->line_fmt == kFmtQwm;
+  if (!(occ || qwm) || h->n == 0) return CS_OK;
   if (const char* e = std::getenv("CS_FM_LCTX"))
     if (std::atoi(e) == 0) return CS_OK;
-  const uint64_t rows = ((h->n + 15) & ~15ull) + 16;
+  const uint32_t eb = occ ? 2 : 4, R = 32 / eb;
+  const uint32_t sb = occ ? 2 : 2 * h->h_table.qlevels;
+  const uint32_t q = occ ? kCtxQ : (32 / sb < 16 ? 32 / sb : 16);
+  const uint64_t rows = ((h->n + R - 1) & ~(uint64_t)(R - 1)) + R;
   size_t free_b = 0, total_b = 0;
   FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (rows * 2 + total_b / 4 > free_b) return CS_OK;
-  FMX_HIP(hipMalloc(&h->d_lctx, rows * 2));
+  if (rows * eb + total_b / 4 > free_b) return CS_OK;
+  FMX_HIP(hipMalloc(&h->d_lctx, rows * eb));
   h->nlctx = rows;
-  FMX_HIP(hipMemsetAsync(static_cast<uint16_t*>(h->d_lctx) + h->n, 0, (rows - h->n) * 2, st));
+  h->lctx_q = q;
+  h->lctx_sb = sb;
+  h->lctx_eb = eb;
+  FMX_HIP(hipMemsetAsync(static_cast<uint8_t*>(h->d_lctx) + h->n * eb, 0, (rows - h->n) * eb, st));
   const DevIndex ix = h->dev();
-  k_build_lctx<OccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(ix, static_cast<uint16_t*>(h->d_lctx));
+  if (occ)
+    k_build_lctx<OccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
+        ix, static_cast<uint16_t*>(h->d_lctx));
+  else
+    k_build_lctx<QWM><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
+        ix, static_cast<uint32_t*>(h->d_lctx));
   FMX_HIP(hipGetLastError());
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;

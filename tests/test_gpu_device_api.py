@@ -120,7 +120,7 @@ def test_export_import_image(engine, monkeypatch):
     c = pkg.FMIndex.import_image(meta, [p.data_ptr() for p in parts], 0)
     del parts
     assert c.info().engine == g.info().engine and c.info().walk_marks == g.info().walk_marks
-    assert c.info().context_q == g.info().context_q == (7 if engine == "auto" else 0)
+    assert c.info().context_q == g.info().context_q == {"auto": 7, "qwm": 8, "wavelet": 0}[engine]
     P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 14, 500)
     pats = [bytes(r) for r in P] + [b"ACGTACGTAC", b"$", b""]
     assert c.count_batch(pats).tolist() == g.count_batch(pats).tolist()

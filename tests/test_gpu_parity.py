@@ -182,9 +182,13 @@ def test_engine_choice(built):
         assert (info.engine, info.rare_rows, info.walk_marks) == (engine, rare, marks), name
         want_levels = {0: 8, 1: 1, 2: levels[name]}[engine]
         assert info.levels == want_levels and info.line_bytes in (32, 64), name
-        ctx = 7 if engine == 1 and os.environ.get("CS_FM_LCTX") != "0" else 0
+        # left contexts: occurrence lines 7 x 2-bit codes in u16 (16 rows per 32-B
+        # sector), quaternary matrix 32 / (2 x levels) dense codes in u32 (8 rows)
+        ctx, R = {1: (7, 16), 2: (min(16, 32 // (2 * info.levels)), 8)}.get(engine, (0, 1))
+        if os.environ.get("CS_FM_LCTX") == "0":
+            ctx = 0
         assert info.context_q == ctx, name
-        assert info.context_bytes == (((info.n + 15) // 16 + 1) * 32 if ctx else 0), name
+        assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))
