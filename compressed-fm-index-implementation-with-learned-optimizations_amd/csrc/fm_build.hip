@@ -108,17 +108,17 @@ __global__ void k_double_keys(const uint32_t* __restrict__ rank, uint64_t n, uin
 }
 
 // bwt.hpp:7-15 and fm_index.cpp:57-66 in one pass, plus the inverse-SA samples
-// (row of every stride-th text position) for extract.
+// (row of every pstride-th text position) for extract and the walk-line marks.
 template <class SampleT>
 __global__ void k_bwt_ssa(const uint8_t* __restrict__ t, const uint32_t* __restrict__ sa,
-                          uint32_t n, uint32_t stride, uint8_t* __restrict__ bwt,
+                          uint32_t n, uint32_t stride, uint32_t pstride, uint8_t* __restrict__ bwt,
                           SampleT* __restrict__ ssa, SampleT* __restrict__ isa) {
   const uint32_t gs = gridDim.x * blockDim.x;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gs) {
     const uint32_t s = sa[j];
     bwt[j] = t[s == 0 ? n - 1 : s - 1];
     if (j % stride == 0) ssa[j / stride] = s;
-    if (s % stride == 0) isa[s / stride] = j;
+    if (s % pstride == 0) isa[s / pstride] = j;
   }
 }
 
@@ -248,6 +248,18 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
 static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm_index* h,
                               hipStream_t st, PhaseLog& plog);
 
+// Text-position sample stride (inverse-SA samples for extract; walk-line marks and
+// their position samples for locate): a quarter of the SSA stride, half for wide
+// indexes (n >= 2^32, u64 samples), at least 1.  A locate walk then averages about
+// pstride / 2 steps instead of stride / 2, an extract stride / 2 fewer; the
+// reference's row-sampled SSA (fm_index.cpp:57-66) is kept as is.  The samples cost
+// 2 x sample bytes x n / pstride (C4: 2 GB, C5: 32 GB).  CS_FM_PSTRIDE overrides.
+static uint32_t position_stride(uint32_t stride, bool wide) {
+  uint32_t p = stride / (wide ? 2u : 4u);
+  if (const char* e = std::getenv("CS_FM_PSTRIDE")) p = (uint32_t)std::atoi(e);
+  return p ? p : 1u;
+}
+
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
                              hipStream_t st) {
   if (stride == 0) {
@@ -287,13 +299,14 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   DevBuf bwt;
   FMX_HIP(bwt.alloc(n));
   FMX_HIP(hipMalloc(&h->d_ssa, (h->nsamples ? h->nsamples : 1) * h->sample_bytes()));
-  h->nisa = h->nsamples;  // text positions 0, stride, 2*stride, ... < n
+  h->pstride = position_stride(stride, h->wide);
+  h->nisa = (n + h->pstride - 1) / h->pstride;  // text positions 0, pstride, ... < n
   FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
   bool bucketed = n >= (1ull << 32);
   if (const char* e = std::getenv("CS_FM_SA_BUILDER"))
     if (std::string(e) == "bucketed") bucketed = true;
   if (n && bucketed) {  // BWT + samples pass by pass, no full SA (fm_bwt_bucketed.hip)
-    cs_status s = build_bwt_bucketed(d_text, n, stride, h->wide, bwt.as<uint8_t>(), h->d_ssa,
+    cs_status s = build_bwt_bucketed(d_text, n, stride, h->pstride, h->wide, bwt.as<uint8_t>(), h->d_ssa,
                                      h->d_isa, st);
     if (s != CS_OK) return s;
   } else if (n) {  // prefix doubling over the full u32 SA
@@ -303,11 +316,11 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     if (s != CS_OK) return s;
     if (h->wide)
       k_bwt_ssa<uint64_t><<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(
-          d_text, sa.as<uint32_t>(), (uint32_t)n, stride, bwt.as<uint8_t>(),
+          d_text, sa.as<uint32_t>(), (uint32_t)n, stride, h->pstride, bwt.as<uint8_t>(),
           static_cast<uint64_t*>(h->d_ssa), static_cast<uint64_t*>(h->d_isa));
     else
       k_bwt_ssa<uint32_t><<<grid_for(n, kBlk, 16384), kBlk, 0, st>>>(
-          d_text, sa.as<uint32_t>(), (uint32_t)n, stride, bwt.as<uint8_t>(),
+          d_text, sa.as<uint32_t>(), (uint32_t)n, stride, h->pstride, bwt.as<uint8_t>(),
           static_cast<uint32_t*>(h->d_ssa), static_cast<uint32_t*>(h->d_isa));
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipStreamSynchronize(st));
@@ -497,6 +510,7 @@ cs_status build_index_from_bwt(const uint8_t* bwt_host, uint64_t n, const uint32
   }
   h->n = n;
   h->stride = stride;
+  h->pstride = stride;
   h->wide = false;
   h->nsamples = nsamples;
   h->nisa = 0;

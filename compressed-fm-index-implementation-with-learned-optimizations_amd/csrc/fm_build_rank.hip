@@ -454,7 +454,7 @@ cs_status build_occ(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_in
 }
 
 // ---- walk lines (fm_device.hpp WalkLine / WalkLineW) ----
-// position marks: bit isa[k] for every sampled text position k*stride
+// position marks: bit isa[k] for every sampled text position k*pstride
 __global__ void k_mark_positions(const void* __restrict__ isa, uint64_t nisa, uint32_t wide,
                                  unsigned int* __restrict__ bits) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -523,9 +523,9 @@ __global__ void k_walk_base(uint32_t* __restrict__ lines, const uint64_t* __rest
   }
 }
 
-// position samples in mark order: wssa[mark_rank(isa[k])] = k * stride
+// position samples in mark order: wssa[mark_rank(isa[k])] = k * pstride
 template <class W, class SampleT>
-__global__ void k_walk_samples(const SampleT* __restrict__ isa, uint64_t nisa, uint32_t stride,
+__global__ void k_walk_samples(const SampleT* __restrict__ isa, uint64_t nisa, uint32_t pstride,
                                const void* __restrict__ lines, SampleT* __restrict__ wssa) {
   const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nisa; k += gs) {
@@ -534,7 +534,7 @@ __global__ void k_walk_samples(const SampleT* __restrict__ isa, uint64_t nisa, u
     W::locate((uint64_t)isa[k], q, o);
     typename W::Raw v;
     W::load(lines, q, v);
-    wssa[W::mark_rank(v, o)] = (SampleT)(k * stride);
+    wssa[W::mark_rank(v, o)] = (SampleT)(k * pstride);
   }
 }
 
@@ -577,11 +577,11 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
     FMX_HIP(hipMalloc(&h->d_wssa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
     if (h->wide)
       k_walk_samples<W, uint64_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
-          static_cast<const uint64_t*>(h->d_isa), h->nisa, h->stride, h->d_walk,
+          static_cast<const uint64_t*>(h->d_isa), h->nisa, h->pstride, h->d_walk,
           static_cast<uint64_t*>(h->d_wssa));
     else
       k_walk_samples<W, uint32_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
-          static_cast<const uint32_t*>(h->d_isa), h->nisa, h->stride, h->d_walk,
+          static_cast<const uint32_t*>(h->d_isa), h->nisa, h->pstride, h->d_walk,
           static_cast<uint32_t*>(h->d_wssa));
     FMX_HIP(hipGetLastError());
   }
@@ -595,7 +595,7 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
 // reference's row marks (row % stride == 0) keep its overrun behaviour.
 cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
                      hipStream_t st) {
-  bool pos_marks = h->lf_exact && h->d_isa && h->nisa == h->nsamples;
+  bool pos_marks = h->lf_exact && h->d_isa && h->nisa == (n + h->pstride - 1) / h->pstride;
   if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
     if (std::string(e) == "row") pos_marks = false;
   h->walk_marks = pos_marks ? 2u : 1u;

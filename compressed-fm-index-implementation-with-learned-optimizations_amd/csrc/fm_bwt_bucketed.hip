@@ -15,7 +15,7 @@
 //     alone — for random DNA one or two extra chunks, for an exact repeat of length
 //     R about R/K rounds of a few launches over the repeat's suffixes;
 //   * emit BWT bytes, SSA samples (row % stride == 0) and ISA samples
-//     (position % stride == 0) for the pass's rows.
+//     (position % pstride == 0) for the pass's rows.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
@@ -204,7 +204,7 @@ __global__ void k_round_compact(const uint32_t* __restrict__ sel, uint64_t T2,
 }
 
 template <class SampleT>
-__global__ void k_emit(const uint8_t* __restrict__ t, uint64_t n, uint32_t stride,
+__global__ void k_emit(const uint8_t* __restrict__ t, uint64_t n, uint32_t stride, uint32_t pstride,
                        const uint64_t* __restrict__ pos, uint64_t P, uint64_t row0,
                        uint8_t* __restrict__ bwt, SampleT* __restrict__ ssa, SampleT* __restrict__ isa) {
   const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
@@ -212,7 +212,7 @@ __global__ void k_emit(const uint8_t* __restrict__ t, uint64_t n, uint32_t strid
     const uint64_t row = row0 + j, s = pos[j];
     bwt[row] = t[s == 0 ? n - 1 : s - 1];
     if (row % stride == 0) ssa[row / stride] = (SampleT)s;
-    if (s % stride == 0) isa[s / stride] = (SampleT)row;
+    if (s % pstride == 0) isa[s / pstride] = (SampleT)row;
   }
 }
 
@@ -230,7 +230,8 @@ cs_status tmp_call(DevBuf& tmp, size_t& tmp_bytes, F f) {
 
 }  // namespace
 
-cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, bool wide,
+cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, uint32_t pstride,
+                             bool wide,
                              uint8_t* d_bwt, void* d_ssa, void* d_isa, hipStream_t st) {
   if (n == 0) return CS_OK;
   const bool verbose = std::getenv("CS_FM_VERBOSE") != nullptr;
@@ -443,10 +444,10 @@ cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride,
     }
     // 4. emit the pass's rows
     if (wide)
-      k_emit<uint64_t><<<G, kBlk, 0, st>>>(d_text, n, stride, pos, P, ps.row0, d_bwt,
+      k_emit<uint64_t><<<G, kBlk, 0, st>>>(d_text, n, stride, pstride, pos, P, ps.row0, d_bwt,
                                            static_cast<uint64_t*>(d_ssa), static_cast<uint64_t*>(d_isa));
     else
-      k_emit<uint32_t><<<G, kBlk, 0, st>>>(d_text, n, stride, pos, P, ps.row0, d_bwt,
+      k_emit<uint32_t><<<G, kBlk, 0, st>>>(d_text, n, stride, pstride, pos, P, ps.row0, d_bwt,
                                            static_cast<uint32_t*>(d_ssa), static_cast<uint32_t*>(d_isa));
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipStreamSynchronize(st));

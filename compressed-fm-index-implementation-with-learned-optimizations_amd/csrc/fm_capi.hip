@@ -362,6 +362,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->walk_bytes = h->d_walk ? h->nwalk * 32 : 0u;
   out->context_q = h->d_lctx ? h->lctx_q : 0u;
   out->context_bytes = h->d_lctx ? h->nlctx * h->lctx_eb : 0u;
+  out->position_stride = h->pstride;
   return CS_OK;
 }
 

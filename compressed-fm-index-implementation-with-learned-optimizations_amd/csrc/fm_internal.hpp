@@ -27,8 +27,9 @@ struct cs_fm_index {
   fmx::NodeTable h_table{};
   uint64_t* d_err = nullptr;          // locate: min failing item (UINT64_MAX = none)
   void* d_ptab = nullptr;             // prefix table (DevIndex::ptab)
-  void* d_isa = nullptr;              // inverse-SA samples (extract)
+  void* d_isa = nullptr;              // inverse-SA samples (extract, walk-line marks)
   uint64_t nisa = 0;
+  uint32_t pstride = 32;              // their text-position stride (position_stride())
   bool lf_exact = false;              // unique smallest last symbol: LF inverts SA
   void* d_walk = nullptr;             // walk lines (occurrence engine; WalkLine / WalkLineW)
   uint64_t nwalk = 0;
@@ -100,6 +101,7 @@ struct cs_fm_index {
     d.ptab_sigma = ptab_sigma;
     d.isa = d_isa;
     d.nisa = nisa;
+    d.pstride = pstride;
     d.lf_exact = lf_exact ? 1u : 0u;
     d.walk = d_walk;
     d.wssa = d_wssa ? d_wssa : d_ssa;
@@ -140,7 +142,8 @@ cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_i
 cs_status launch_node_ranks(const cs_fm_index* h, uint64_t* d_R, hipStream_t st);
 cs_status build_index_from_bwt(const uint8_t* bwt_host, uint64_t n, const uint32_t* ssa_host,
                                uint64_t nsamples, uint32_t stride, cs_fm_index* h, hipStream_t st);
-cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, bool wide,
+cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride, uint32_t pstride,
+                             bool wide,
                              uint8_t* d_bwt, void* d_ssa, void* d_isa, hipStream_t st);
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
                              hipStream_t st);

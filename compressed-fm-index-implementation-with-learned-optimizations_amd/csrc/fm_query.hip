@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(kBlk) void k_extract(DevIndex ix, const uint64_t* _
   uint64_t L = len[q];
   if (L > n - p) L = n - p;
   const uint64_t end = p + L;
-  const uint64_t s = ix.stride;
+  const uint64_t s = ix.pstride;
   uint64_t e = ((end + s - 1) / s) * s;
   if (e >= n) e = n;
   uint64_t row = isa_at(ix, e == n ? 0 : e / s);

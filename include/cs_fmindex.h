@@ -78,7 +78,8 @@ typedef struct cs_fm_info {
   uint64_t walk_bytes;
   uint32_t context_q;      /* left contexts: symbols per BWT row a count may finish with
                               in one read (0 = none; occurrence lines only) */
-  uint32_t reserved;
+  uint32_t position_stride; /* text-position samples (extract, locate walk marks) every
+                              position_stride positions; the SSA keeps ssa_stride */
   uint64_t context_bytes;
 } cs_fm_info;
 

@@ -29,6 +29,7 @@ ENGINE_VARIANTS = {
     "auto_rowmarks": {"CS_FM_WALK_MARKS": "row"},   # walk lines with the reference's row samples
     "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
+    "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
     "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
@@ -38,7 +39,8 @@ ENGINE_VARIANTS = {
     "wide_wavelet": {"CS_FM_WIDE": "1", "CS_FM_ENGINE": "wavelet"},
 }
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
-          "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX")
+          "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
+          "CS_FM_PSTRIDE")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -188,6 +190,9 @@ def test_engine_choice(built):
         if os.environ.get("CS_FM_LCTX") == "0":
             ctx = 0
         assert info.context_q == ctx, name
+        wide = os.environ.get("CS_FM_WIDE") == "1"
+        assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or
+                                        (16 if wide else 8)), name
         assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
 
 
