@@ -363,34 +363,33 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
   return true;
 }
 
-// The last k <= lctx_q characters P[0..k) of a count over the left contexts of the
-// rows [sp, ep) (fm_device.hpp kCtxQ): the rows whose chain spells P[k-1], ...,
-// P[0].  Needs ep - (sp & ~(R-1)) <= 2R, R = rows per 32-B sector (16 for u16
-// entries, 8 for u32).  Returns false — the caller keeps stepping — when a character
-// has no code (a rare symbol) or a row in the range has an escaped context; a
-// character absent from the text gives 0, as the reference's step would.
+// The last k <= lctx_q characters P[0..k) over the left contexts of the rows
+// [sp, ep) (fm_device.hpp kCtxQ): the rows whose chain spells P[k-1], ..., P[0].
+// Needs ep - (sp & ~(R-1)) <= 2R, R = rows per 32-B sector (16 for u16 entries, 8
+// for u32).  Returns kCtxNone — the caller keeps stepping — when a character has no
+// code (a rare symbol) or a row in the range has an escaped context; kCtxAbsent when
+// a character does not occur in the text (count 0, as the reference's step);
+// otherwise kCtxOk with bit i of `mm` set when row base + i matches.
+enum : uint32_t { kCtxNone = 0, kCtxAbsent = 1, kCtxOk = 2 };
 template <class Ent>
-__device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
-                                          const uint8_t* __restrict__ P, uint32_t k,
-                                          uint64_t sp, uint64_t ep, uint64_t& cnt,
-                                          uint64_t* bytes) {
+__device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTable& T,
+                                              const uint8_t* __restrict__ P, uint32_t k,
+                                              uint64_t sp, uint64_t ep, uint32_t& mm,
+                                              uint64_t& base, uint64_t* bytes) {
   constexpr uint32_t R = 32 / sizeof(Ent);
   constexpr bool kEsc = sizeof(Ent) == 2;
   const uint32_t sb = kEsc ? 2u : ix.lctx_sb;
   uint32_t want = 0;
   for (uint32_t t = 0; t < k; ++t) {  // chain symbol t = P[k-1-t]
     const uint32_t c = P[k - 1 - t];
-    if (T.C[c] == T.C[c + 1]) {  // absent: the reference's step returns 0
-      cnt = 0;
-      return true;
-    }
+    if (T.C[c] == T.C[c + 1]) return kCtxAbsent;
     const uint32_t d = T.occ_code[c];
-    if (d == kNoCode) return false;
+    if (d == kNoCode) return kCtxNone;
     want |= d << (sb * t);
   }
   const uint32_t kb = sb * k;
   const uint32_t mask = (kb >= 32 ? ~0u : ((1u << kb) - 1u)) | (kEsc ? kCtxEsc : 0u);
-  const uint64_t base = sp & ~(uint64_t)(R - 1);
+  base = sp & ~(uint64_t)(R - 1);
   const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);  // rows [lo, hi) of 2R
   const uint4* p = reinterpret_cast<const uint4*>(static_cast<const Ent*>(ix.lctx) + base);
   const bool two = hi > R;
@@ -413,8 +412,21 @@ __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T
     if (kEsc) esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
   }
   const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-  if (esc & in) return false;
-  cnt = (uint64_t)__popc(match & in);
+  if (esc & in) return kCtxNone;
+  mm = match & in;
+  return kCtxOk;
+}
+
+template <class Ent>
+__device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
+                                          const uint8_t* __restrict__ P, uint32_t k,
+                                          uint64_t sp, uint64_t ep, uint64_t& cnt,
+                                          uint64_t* bytes) {
+  uint32_t mm = 0;
+  uint64_t base;
+  const uint32_t r = ctx_match<Ent>(ix, T, P, k, sp, ep, mm, base, bytes);
+  if (r == kCtxNone) return false;
+  cnt = r == kCtxOk ? (uint64_t)__popc(mm) : 0;
   return true;
 }
 
@@ -439,6 +451,54 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
     --k;
     if (!E::step(ix, T, P[k], sp, ep, bytes)) return 0;
   }
+  return ep - sp;
+}
+
+// Locate records (phase 1 -> phase 2, cs_fm_locate_ranges_device's d_sp): the
+// first row of the range [sp, ep), or — for a search finished over the left
+// contexts (lf_exact indexes only) — the window of matching rows r at k characters
+// before the end: bit 63 set, bits 60-62 k, bits 38-59 the matches relative to the
+// first one (bit i: row r0 + i), bits 0-37 r0.  The final rows are LF^k(r), in the
+// same order (LF keeps the order of rows with equal chains), and with LF one n-cycle
+// SA[LF^k(r)] = SA[r] - k (mod n), so phase 2 walks from r and subtracts k.
+constexpr uint64_t kLocCtx = 1ull << 63;
+constexpr uint64_t kLocRowMask = (1ull << 38) - 1;
+constexpr uint32_t kLocSpanBits = 22;
+// rows handed to the walk: row | k << kWalkAdjShift (k = positions to subtract)
+constexpr int kWalkAdjShift = 56;
+constexpr uint64_t kWalkRowMask = (1ull << kWalkAdjShift) - 1;
+
+template <class E>
+__device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const NodeTable& T,
+                                                  const uint8_t* __restrict__ P, uint64_t m,
+                                                  uint64_t& rec) {
+  uint64_t sp, ep, k;
+  rec = 0;
+  search_start(ix, T, P, m, sp, ep, k, nullptr);
+  if (sp >= ep) return 0;
+  constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);
+  bool ctx = E::kCtx && ix.lctx != nullptr && ix.lf_exact;
+  while (k > 0) {
+    if (ctx && k <= ix.lctx_q && k <= 7 && ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R) {
+      uint32_t mm = 0;
+      uint64_t base;
+      const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, mm, base,
+                                                       nullptr);
+      if (r == kCtxAbsent || (r == kCtxOk && mm == 0)) return 0;
+      if (r == kCtxOk) {
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u;
+        const uint32_t rel = mm >> f;
+        if ((rel >> kLocSpanBits) == 0) {
+          rec = kLocCtx | (k << 60) | ((uint64_t)rel << 38) | (base + f);
+          return (uint64_t)__popc(mm);
+        }
+      }
+      ctx = false;
+    }
+    --k;
+    if (!E::step(ix, T, P[k], sp, ep, nullptr)) return 0;
+  }
+  rec = sp;
   return ep - sp;
 }
 
@@ -769,22 +829,30 @@ __global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
     return;
   }
   const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
-  uint64_t sp = 0, ep = 0;
-  if (m && ix.n) {  // fm_index.cpp:109: empty pattern or empty text -> {}
-    if (!backward_search<E>(ix, T, pats + o0, m, sp, ep)) sp = ep = 0;
-  }
-  const uint64_t c = ep - sp;
-  sp_out[q] = sp;
+  uint64_t rec = 0, c = 0;
+  if (m && ix.n) c = locate_search<E>(ix, T, pats + o0, m, rec);  // fm_index.cpp:109: empty -> {}
+  sp_out[q] = rec;
   cnt_out[q] = c < limit ? c : limit;  // fm_index.cpp:125 `positions.size() < limit`
 }
 
-// rows[j] = sp[q] + (j - offs[q]) for the reported rows of pattern q (row order).
+// The reported rows of pattern q in row order (fm_index.cpp:125): sp[q] + (j -
+// offs[q]) for a plain record, else the window's matching rows, tagged with k.
 __global__ void k_expand_rows(const uint64_t* __restrict__ sp, const uint64_t* __restrict__ offs,
                               uint64_t npat, uint64_t* __restrict__ rows) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += stride) {
     const uint64_t a = offs[q], b = offs[q + 1], s = sp[q];
-    for (uint64_t j = a; j < b; ++j) rows[j] = s + (j - a);
+    if (s & kLocCtx) {
+      const uint64_t r0 = s & kLocRowMask, tag = ((s >> 60) & 7u) << kWalkAdjShift;
+      uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+      for (uint64_t j = a; j < b; ++j) {
+        const uint32_t f = (uint32_t)__ffs(rel) - 1u;
+        rows[j] = (r0 + f) | tag;
+        rel &= rel - 1u;
+      }
+    } else {
+      for (uint64_t j = a; j < b; ++j) rows[j] = s + (j - a);
+    }
   }
 }
 
@@ -819,7 +887,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
   __syncthreads();
   if (a >= total) return;
   const uint64_t n = ix.n;
-  uint64_t j = 0, pos = 0, steps = 0;
+  uint64_t j = 0, pos = 0, steps = 0, adj = 0;
   uint32_t phase = kFetch;
   for (;;) {
     if (phase == kFetch) {
@@ -831,12 +899,14 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
     if (phase == kFetch) row = rows[j];
     if (phase == kSample) smp = ssa_at(ix, sample_index<POW2>(ix, pos));
     if (phase == kFetch) {
-      pos = row;
+      pos = row & kWalkRowMask;
+      adj = row >> kWalkAdjShift;
       steps = 0;
       phase = kWalk;
     } else if (phase == kSample) {
-      const uint64_t s = smp + steps;  // :147-153
-      out[j] = s >= n ? s - n : s;
+      uint64_t s = smp + steps;  // :147-153
+      s = s >= n ? s - n : s;
+      out[j] = s >= adj ? s - adj : s + n - adj;
       phase = kFetch;
     } else if (phase == kWalk) {
       // loop condition of fm_index.cpp:130: stop at a sampled row or after n steps
@@ -881,7 +951,7 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
   __syncthreads();
   if (a >= total) return;
   const uint64_t n = ix.n;
-  uint64_t j = 0, pos = 0, steps = 0, sidx = 0;
+  uint64_t j = 0, pos = 0, steps = 0, sidx = 0, adj = 0;
   uint32_t phase = kFetch;
   bool from_ssa = false;  // the stop row is one of the reference's sampled rows
   const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
@@ -903,7 +973,8 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
     if (phase == kSample) smp = from_ssa ? ssa_at(ix, sidx) : wssa_at(ix, sidx);
     // ---- consume ----
     if (phase == kFetch) {
-      pos = row;
+      pos = row & kWalkRowMask;
+      adj = row >> kWalkAdjShift;
       steps = 0;
       phase = kWalk;
     } else if (phase == kWalk) {
@@ -962,8 +1033,9 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
         ++steps;
       }
     } else if (phase == kSample) {
-      const uint64_t s = smp + steps;  // :147-153
-      out[j] = s >= n ? s - n : s;
+      uint64_t s = smp + steps;  // :147-153
+      s = s >= n ? s - n : s;
+      out[j] = s >= adj ? s - adj : s + n - adj;
       phase = kFetch;
     }
   }

@@ -190,7 +190,9 @@ cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
 cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream);
-/* locate phase 1: backward search; d_sp[q] = first row, d_out_offs = exclusive scan
+/* locate phase 1: backward search; d_sp[q] = the pattern's record for phase 2 (the
+ * first row of its range, or an encoded window of matching rows when the search
+ * finished over the left contexts — treat it as opaque), d_out_offs = exclusive scan
  * of min(count, limit) (npat+1 entries).  Synchronises `stream` to return *total. */
 cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
                                      const uint64_t* d_offs, uint64_t npat, uint64_t limit,

@@ -234,6 +234,38 @@ def test_count_every_text_vs_oracle(built, name):
     assert g.count_batch(pats).tolist() == [o.count(p) for p in pats], name
     for p in pats[::37]:  # single-pattern path (kernel arguments)
         assert g.count(p) == o.count(p), (name, p)
+    # locate of the same patterns: ranges finished over the contexts hand windows of
+    # matching rows to the walk (lf_exact texts), limits cutting inside a window
+    for lim in (3, 1000):
+        for p in pats[::3]:
+            try:
+                want = o.locate(p, limit=lim)
+            except RuntimeError as e:
+                with pytest.raises(RuntimeError, match=str(e)):
+                    g.locate(p, limit=lim)
+                continue
+            assert g.locate(p, limit=lim) == want, (name, p, lim)
+
+
+def test_locate_context_windows(pkg):
+    """Locate over context windows (phase-1 records): patterns with up to 40 hits in
+    one window (repeats: the window's match span exceeds the record's 22 bits and the
+    search steps on), and hits separated by non-matching rows."""
+    rng = np.random.default_rng(8)
+    rnd = lambda k: bytes(rng.choice(list(b"ACGT"), k).astype(np.uint8))
+    core = rnd(14)
+    parts = []
+    for i in range(40):  # 40 copies of core, each after a different 6-mer
+        parts += [rnd(30), rnd(6), core]
+    t = b"".join(parts) + rnd(200) + b"$"
+    g = pkg.FMIndex.build_from_text(t)
+    o = O.Index(t)
+    pats = [core, core[1:], core[:10], core[3:]] + [t[i:i + 20] for i in range(0, len(t) - 20, 13)]
+    pats += [t[i:i + 17] for i in range(0, len(t) - 17, 29)]
+    for lim in (1, 5, 21, 22, 23, 100000):
+        offs, pos = g.locate_batch(pats, limit=lim)
+        for q, p in enumerate(pats):
+            assert pos[offs[q]:offs[q + 1]].tolist() == o.locate(p, limit=lim), (p, lim)
 
 
 def _check_fm_case(pkg, case):
