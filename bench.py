@@ -14,10 +14,12 @@ counts to rank 0 over RCCL, double-buffered behind the next step's count.
 
 Extra fields on the JSON line:
   roofline     the count kernel against HBM: achieved = algorithmic bytes per
-               launch (64 B per rank-line read the algorithm needs: 2 per
-               non-pure wavelet level per pattern character after the first) /
-               mean kernel time (HIP events on the launch stream); traffic from
-               the committed rocprofv3 PMC summary for this workload, if present.
+               launch / mean kernel time (HIP events on the launch stream).
+               Algorithmic bytes = the random reads the search needs (prefix-table
+               entry, one 32-B line per rank step, the 32-B context sector(s);
+               counted per query by cs_fm_count_bytes_device) + the stream every
+               launch moves (patterns, offsets, counts).  traffic = HBM bytes per
+               launch from the committed rocprofv3 PMC summary for this workload.
   cpu_baseline the reference's own FMIndex::count (oracle/_ref/libcs_ref.so, built
                from its sources; kind "reference"), else the oracle's
                reference-faithful count() (kind "port"; O(n) count_ones scans, as
@@ -165,7 +167,11 @@ def main():
     line_bytes = info.line_bytes
     qbytes = torch.empty(B, dtype=torch.int64, device=dev)
     idx.count_bytes_device(pats.data_ptr(), offs.data_ptr(), B, qbytes.data_ptr(), sh)
-    alg_bytes = int(qbytes.sum().item())
+    alg_random = int(qbytes.sum().item())
+    # plus the streamed bytes every launch must move: the patterns, their offsets and
+    # the counts written back
+    alg_stream = B * m + (B + 1) * 8 + B * 8
+    alg_bytes = alg_random + alg_stream
     del qbytes
     P2 = pats.view(B, m).long()
     K = info.prefix_k
@@ -211,7 +217,7 @@ def main():
     # at 49-52 G accesses/s (profiles/r01/gather_bench*.txt)
     eb = info.prefix_bytes // (info.prefix_sigma ** K) if K else 0
     hits = int(round(B * table_frac)) if K else 0
-    accesses = (alg_bytes - eb * hits) / info.line_bytes + hits
+    accesses = (alg_random - eb * hits) / info.line_bytes + hits
     total_units = B * world * args.steps
     value = total_units / elapsed
     kern_avg_s = statistics.mean(kern_ms) / 1e3
@@ -263,7 +269,8 @@ def main():
                        "wavelet matrix (%d-B rank lines)" % info.line_bytes},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "line_bytes": line_bytes,
+                         "alg_bytes_per_launch": alg_bytes, "alg_random_bytes_per_launch": alg_random,
+                         "alg_stream_bytes_per_launch": alg_stream, "line_bytes": line_bytes,
                          "prefix_k": K, "prefix_table_hit_frac": table_frac,
                          "context_q": info.context_q,
                          "alg_bytes_per_query": alg_bytes / B,

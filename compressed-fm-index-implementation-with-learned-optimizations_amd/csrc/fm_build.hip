@@ -249,13 +249,16 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
                               hipStream_t st, PhaseLog& plog);
 
 // Text-position sample stride (inverse-SA samples for extract; walk-line marks and
-// their position samples for locate): a quarter of the SSA stride, half for wide
-// indexes (n >= 2^32, u64 samples), at least 1.  A locate walk then averages about
-// pstride / 2 steps instead of stride / 2, an extract stride / 2 fewer; the
-// reference's row-sampled SSA (fm_index.cpp:57-66) is kept as is.  The samples cost
-// 2 x sample bytes x n / pstride (C4: 2 GB, C5: 32 GB).  CS_FM_PSTRIDE overrides.
+// their position samples for locate): an eighth of the SSA stride, half for wide
+// indexes (n >= 2^32, u64 samples: their HBM goes to the left contexts first), at
+// least 1.  A locate walk then averages about pstride / 2 steps instead of
+// stride / 2, an extract (stride - pstride) / 2 fewer; the reference's row-sampled
+// SSA (fm_index.cpp:57-66) is kept as is.  The samples cost 2 x sample bytes x
+// n / pstride (C4: 4 GB, C5: 32 GB).  C4 walk of 12.5 M positions: 1.8 ms at
+// pstride 8, 1.3 ms at 4 (profiles/r01/locate_phases_c4_p*.json).  CS_FM_PSTRIDE
+// overrides.
 static uint32_t position_stride(uint32_t stride, bool wide) {
-  uint32_t p = stride / (wide ? 2u : 4u);
+  uint32_t p = stride / (wide ? 2u : 8u);
   if (const char* e = std::getenv("CS_FM_PSTRIDE")) p = (uint32_t)std::atoi(e);
   return p ? p : 1u;
 }

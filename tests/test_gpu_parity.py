@@ -192,7 +192,7 @@ def test_engine_choice(built):
         assert info.context_q == ctx, name
         wide = os.environ.get("CS_FM_WIDE") == "1"
         assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or
-                                        (16 if wide else 8)), name
+                                        (16 if wide else 4)), name
         assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
 
 
