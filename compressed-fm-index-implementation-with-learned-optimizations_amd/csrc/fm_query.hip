@@ -582,6 +582,9 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
 // table index and context key; (B) the U table entries; (C) the U context sectors;
 // (D) counts.  Anything else — longer patterns, symbols outside the table alphabet,
 // wide ranges, escaped contexts — takes count_pattern, the general search.
+// kLoc: the same stages for locate's phase 1 (k_locate_ranges): out = min(count,
+// limit), rec = the pattern's locate record (locate_search), context windows only
+// when LF is one n-cycle (lf_exact).
 constexpr uint32_t kFastM = 32;
 
 // bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
@@ -598,24 +601,27 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
-template <int U>
+template <int U, bool kLoc>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
-                                                    uint64_t npat, uint64_t* __restrict__ out) {
+                                                    uint64_t npat, uint64_t* __restrict__ out,
+                                                    uint64_t limit, uint64_t* __restrict__ rec) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
   const uint32_t K = ix.ptab_k;
   const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
-  uint64_t o0[U], res[U], sp[U], ep[U];
+  uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U];
   uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search
+  if (kLoc && q0 == 0) out[npat] = 0;  // scan slot for the total
   // (A)
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     st[j] = 0;
     res[j] = 0;
+    rv[j] = 0;
     o0[j] = 0;
     m[j] = 0;
     t[j] = want[j] = k[j] = 0;
@@ -624,7 +630,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     const uint64_t mm = offs[q + 1] - o0[j];
     m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
     if (mm == 0) {
-      res[j] = ix.n;  // fm_index.cpp:80
+      res[j] = kLoc ? 0 : ix.n;  // fm_index.cpp:80; locate: :109
       continue;
     }
     if (ix.n == 0) continue;  // :81
@@ -633,7 +639,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     uint32_t u[8];
     load_pattern32(pats, o0[j], m[j], u);
     const uint32_t kk = m[j] - K;
-    bool ok = true, cok = kk <= kCtxQ;
+    bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
     uint32_t tt = 0, ww = 0;
 #pragma unroll
     for (uint32_t i = 0; i < kFastM; ++i) {
@@ -669,6 +675,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     } else if (k[j] == 0) {
       st[j] = 0;
       res[j] = ep[j] - sp[j];
+      rv[j] = sp[j];
     } else if (st[j] == 2 && ep[j] - (sp[j] & ~15ull) <= 32) {
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
                                                       (sp[j] & ~15ull));
@@ -700,20 +707,48 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
         esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
       }
       const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      const uint32_t mm = match & in;
       if (esc & in) {
         st[j] = 3;
-      } else {
-        res[j] = (uint64_t)__popc(match & in);
+      } else if (!kLoc || mm == 0) {
+        res[j] = (uint64_t)__popc(mm);
         st[j] = 0;
+      } else {  // the window record (locate_search)
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u;
+        const uint32_t rel = mm >> f;
+        if (rel >> kLocSpanBits) {
+          st[j] = 3;
+        } else {
+          rv[j] = kLocCtx | ((uint64_t)k[j] << 60) | ((uint64_t)rel << 38) | (base + f);
+          res[j] = (uint64_t)__popc(mm);
+          st[j] = 0;
+        }
       }
     }
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if (q < npat && st[j] != 3) out[q] = res[j];
+    if (q < npat && st[j] != 3) {
+      if (kLoc) {
+        out[q] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
+        rec[q] = rv[j];
+      } else {
+        out[q] = res[j];
+      }
+    }
   }
   // the general search for the rest, with only (o0, m) of each pattern still live
 #pragma unroll
-  for (int j = 0; j < U; ++j)
-    if (st[j] == 3) out[q0 + (uint64_t)j * kBlk] = count_pattern<OccE>(ix, T, pats + o0[j], m[j]);
+  for (int j = 0; j < U; ++j) {
+    if (st[j] != 3) continue;
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    if (kLoc) {
+      uint64_t r;
+      const uint64_t c = locate_search<OccE>(ix, T, pats + o0[j], m[j], r);
+      out[q] = c < limit ? c : limit;
+      rec[q] = r;
+    } else {
+      out[q] = count_pattern<OccE>(ix, T, pats + o0[j], m[j]);
+    }
+  }
 }
 
 // Single-pattern count (FMIndex::count, the p50 path): the pattern travels in the
@@ -1303,11 +1338,14 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
     }();
     const DevIndex ix = h->dev();
     if (U == 1)
-      k_count_ctx<1><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_out);
+      k_count_ctx<1, false><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
     else if (U == 2)
-      k_count_ctx<2><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_out);
+      k_count_ctx<2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
     else
-      k_count_ctx<4><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_out);
+      k_count_ctx<4, false><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
@@ -1343,8 +1381,14 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                hipStream_t st) {
   StreamBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8, st));
-  FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,
-               d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
+  if (h->line_fmt == kFmtOcc && h->d_lctx && h->ptab_k) {  // staged, two patterns per lane
+    k_count_ctx<2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp);
+    FMX_HIP(hipGetLastError());
+  } else {
+    FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,
+                 d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
+  }
   size_t tb = 0;
   FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint64_t>(), d_out_offs, (uint64_t)0,
                                   npat + 1, rocprim::plus<uint64_t>(), st));

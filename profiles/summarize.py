@@ -29,6 +29,8 @@ def rows(pattern):
 
 
 def short(name):
+    if "k_count_ctx" in name:  # template <int U, bool kLoc>: count or locate phase 1
+        return "k_count_ctx_loc" if "Lb1E" in name else "k_count_ctx"
     for k in ("k_count_bytes", "k_count_one", "k_count_ctx", "k_count", "k_build_lctx", "k_walk_lines", "k_walk_pack",
               "k_walk_base", "k_walk_samples", "k_walk", "k_occ_pack", "k_occ_base", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt_ssa", "k_bwt",
               "k_build_ptab",
