@@ -966,6 +966,93 @@ __device__ __forceinline__ uint64_t wssa_at(const DevIndex& ix, uint64_t k) {
   return ix.wide ? static_cast<const uint64_t*>(ix.wssa)[k] : static_cast<const uint32_t*>(ix.wssa)[k];
 }
 
+// LF(pos) from pos's walk line v (line q, offset o): C[c] + occ(c, pos) from the same
+// line (OccE::lf), or for the quaternary matrix level 0 from the walk line and levels
+// 1.. as QWM::lf.
+template <class W, bool kQ>
+__device__ __forceinline__ uint64_t walk_lf(const DevIndex& ix, const NodeTable& T,
+                                            const typename W::Raw& v, uint64_t q, uint32_t o,
+                                            uint64_t pos) {
+  if (!kQ) {
+    const uint32_t code = W::code(v, o);
+    uint32_t c = T.occ_sym[code];
+    uint64_t r = W::occ(v, code, q, o);
+    if (code == 0 && T.exc_n) {
+      const uint32_t e = exc_before(T, pos);
+      if (e < T.exc_n && T.exc_row[e] == pos) {
+        c = T.exc_sym[e];
+        r = exc_rank(T, c, pos);
+      } else {
+        r -= e;
+      }
+    }
+    return T.C[c] + r;
+  }
+  const uint32_t d0 = W::code(v, o);
+  uint64_t p = T.qZ[0][d0] + W::occ(v, d0, q, o);
+  uint32_t x = d0;
+  const int L = (int)T.qlevels;
+  for (int l = 1; l < L; ++l) {
+    const int nid = qnode_id(l, x);
+    const uint8_t f = T.flags[nid];
+    uint32_t d;
+    if (f & kPure) {
+      d = (f >> 2) & 3u;
+      p = T.qZ[l][d] + T.R[nid] + (p - T.S[nid]);
+    } else {
+      OccLine::Raw lv;
+      const uint64_t lq = p >> 6;
+      OccLine::load(QWM::level(ix, l), lq, lv);
+      const uint32_t lo = (uint32_t)(p & 63);
+      d = OccLine::code(lv, lo);
+      p = T.qZ[l][d] + OccLine::base(lv, d, lq) + OccLine::prefix(lv, d, lo);
+    }
+    x = (x << 2) | d;
+  }
+  return T.C[T.qsym[x]] + (p - T.S8[x]);
+}
+
+// Short walks (walk lines with text-position marks, lf_exact): every walk ends within
+// pstride - 1 steps, so one lane per reported row — coalesced row reads, no work
+// queue — and finished waves make room for new ones, as in the count kernels.
+template <class W, bool kQ>
+__global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t* __restrict__ rows,
+                                                     uint64_t total, uint64_t* __restrict__ out,
+                                                     unsigned long long* __restrict__ err) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const uint64_t n = ix.n;
+  const uint64_t row = rows[j];
+  uint64_t pos = row & kWalkRowMask, steps = 0;
+  const uint64_t adj = row >> kWalkAdjShift;
+  const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
+  for (;;) {
+    uint64_t q;
+    uint32_t o;
+    typename W::Raw v;
+    W::locate(pos, q, o);
+    W::load(ix.walk, q, v);
+    const bool mk = W::mark(v, o);
+    const bool rs = row_mask ? (pos & row_mask) == 0 : pos % ix.stride == 0;
+    if (mk || rs || steps >= n) {  // fm_index.cpp:130 loop condition
+      if (steps >= n) {            // :136-138
+        atomicMin(err, (unsigned long long)j);
+        return;
+      }
+      const uint64_t sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
+      uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps;  // :147-153
+      s = s >= n ? s - n : s;
+      out[j] = s >= adj ? s - adj : s + n - adj;
+      return;
+    }
+    pos = walk_lf<W, kQ>(ix, T, v, q, o, pos);
+    ++steps;
+  }
+}
+
 template <class W, bool kQ>
 __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t* __restrict__ rows,
                                                      uint64_t total, uint64_t chunk,
@@ -1034,44 +1121,8 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
           sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
           phase = kSample;
         }
-      } else if (!kQ) {  // LF = C[c] + occ(c, pos) from the same line (OccE::lf)
-        const uint32_t code = W::code(v, o);
-        uint32_t c = T.occ_sym[code];
-        uint64_t r = W::occ(v, code, q, o);
-        if (code == 0 && T.exc_n) {
-          const uint32_t e = exc_before(T, pos);
-          if (e < T.exc_n && T.exc_row[e] == pos) {
-            c = T.exc_sym[e];
-            r = exc_rank(T, c, pos);
-          } else {
-            r -= e;
-          }
-        }
-        pos = T.C[c] + r;
-        ++steps;
-      } else {  // quaternary matrix: level 0 from the walk line, levels 1.. as QWM::lf
-        const uint32_t d0 = W::code(v, o);
-        uint64_t p = T.qZ[0][d0] + W::occ(v, d0, q, o);
-        uint32_t x = d0;
-        const int L = (int)T.qlevels;
-        for (int l = 1; l < L; ++l) {
-          const int nid = qnode_id(l, x);
-          const uint8_t f = T.flags[nid];
-          uint32_t d;
-          if (f & kPure) {
-            d = (f >> 2) & 3u;
-            p = T.qZ[l][d] + T.R[nid] + (p - T.S[nid]);
-          } else {
-            OccLine::Raw lv;
-            const uint64_t lq = p >> 6;
-            OccLine::load(QWM::level(ix, l), lq, lv);
-            const uint32_t lo = (uint32_t)(p & 63);
-            d = OccLine::code(lv, lo);
-            p = T.qZ[l][d] + OccLine::base(lv, d, lq) + OccLine::prefix(lv, d, lo);
-          }
-          x = (x << 2) | d;
-        }
-        pos = T.C[T.qsym[x]] + (p - T.S8[x]);
+      } else {
+        pos = walk_lf<W, kQ>(ix, T, v, q, o, pos);
         ++steps;
       }
     } else if (phase == kSample) {
@@ -1421,7 +1472,22 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
       err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
-  if (h->d_walk) {
+  static const bool persistent = [] {  // tuning hook: CS_FM_WALK_PERSISTENT=1
+    const char* e = std::getenv("CS_FM_WALK_PERSISTENT");
+    return e && std::atoi(e) == 1;
+  }();
+  if (h->d_walk && h->walk_marks == 2 && !persistent) {
+    const bool q = h->line_fmt == kFmtQwm;
+    const unsigned g = grid_for(total, kBlk, 0xFFFFFFFFu);
+    if (h->wide && q)
+      k_walk_short<WalkLineW, true><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+    else if (h->wide)
+      k_walk_short<WalkLineW, false><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+    else if (q)
+      k_walk_short<WalkLine, true><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+    else
+      k_walk_short<WalkLine, false><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+  } else if (h->d_walk) {
     const bool q = h->line_fmt == kFmtQwm;
     if (h->wide && q)
       k_walk_lines<WalkLineW, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
