@@ -230,7 +230,7 @@ def main():
     if rank == 0:
         traffic = None
         prof = os.path.join(ROOT, "profiles", "pmc_count.json")
-        engine = {1: "occ", 2: "qwm"}.get(info.engine, "wm%d" % info.line_bytes)
+        engine = {1: "occ", 2: "qwm", 3: "locc"}.get(info.engine, "wm%d" % info.line_bytes)
         wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
         if info.context_q:
             wl += ":ctx%d" % info.context_q
@@ -262,8 +262,9 @@ def main():
                        "collective": "gather of counts to rank 0 (%s), overlapped"
                        % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) if coll
                        else "none (independent query shards)",
-                       "engine": ("occurrence lines + left contexts (q=%d)" % info.context_q
-                                  if info.context_q else "occurrence lines") if info.engine == 1 else
+                       "engine": ("%s + left contexts (q=%d)" % (
+                                  "learned occurrence lines" if info.engine == 3 else "occurrence lines",
+                                  info.context_q)) if info.engine in (1, 3) else
                        "quaternary wavelet matrix (%d levels of occurrence lines)" % info.levels
                        if info.engine == 2 else
                        "wavelet matrix (%d-B rank lines)" % info.line_bytes},

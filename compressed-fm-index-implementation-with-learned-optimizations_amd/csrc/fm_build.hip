@@ -352,8 +352,10 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   uint8_t occ_sym[4] = {0, 0, 0, 0};
   bool occ = occ_feasible(hist, n, occ_map, occ_sym);
   bool qwm = !occ && n > 0 && n < (1ull << 40);
+  bool learned = false;  // learned occurrence lines instead of occurrence lines
   if (const char* e = std::getenv("CS_FM_ENGINE")) {  // test hooks: force an engine
     const std::string want(e);
+    if (want == "learned") learned = occ;
     if (want == "wavelet") occ = qwm = false;
     if (want == "qwm" && n > 0 && n < (1ull << 40)) {
       occ = false;
@@ -380,14 +382,16 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
       if (qs != CS_OK) return qs;
     }
   } else if (occ) {
-    h->line_fmt = kFmtOcc;
+    h->line_fmt = learned ? kFmtLOcc : kFmtOcc;
     h->line_bytes = OccLine::kBytes;
-    h->line_bits = OccLine::kRows;
+    h->line_bits = learned ? LOccLine::kRows : OccLine::kRows;
     h->nlevels = 1;
-    h->nlines = (n >> 6) + 1;  // + the line holding row n, so occ(c, n) is a line read
+    // + the line holding row n, so occ(c, n) is a line read
+    h->nlines = learned ? n / LOccLine::kRows + 1 : (n >> 6) + 1;
     std::memcpy(T.occ_code, occ_map.c, sizeof T.occ_code);
     std::memcpy(T.occ_sym, occ_sym, sizeof T.occ_sym);
-    cs_status os = build_occ(bwt.as<uint8_t>(), n, occ_map, h, st);
+    cs_status os = learned ? build_locc(bwt.as<uint8_t>(), n, occ_map, h, st)
+                           : build_occ(bwt.as<uint8_t>(), n, occ_map, h, st);
     if (os != CS_OK) return os;
     bool walk = true;
     if (const char* e = std::getenv("CS_FM_WALK"))  // "0": walk over the occurrence lines

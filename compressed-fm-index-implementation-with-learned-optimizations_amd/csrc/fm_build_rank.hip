@@ -205,6 +205,78 @@ __global__ void k_occ_base(uint32_t* __restrict__ lines, const uint64_t* __restr
   }
 }
 
+// ---- learned occurrence lines (fm_device.hpp LOccLine) ----
+// One thread per line: the 104 rows' codes (rare symbols as code 0, listed), and the
+// line's count of codes 0..2.
+__global__ void k_locc_pack(const uint8_t* __restrict__ bwt, uint64_t n, CodeMap map, uint64_t nl,
+                            uint32_t* __restrict__ lines, uint32_t* __restrict__ cnt,
+                            unsigned long long* __restrict__ exc_rows, uint8_t* __restrict__ exc_sym,
+                            unsigned int* __restrict__ exc_n) {
+  __shared__ uint8_t code[256];
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) code[i] = map.c[i];
+  __syncthreads();
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nl; q += stride) {
+    const uint64_t a = q * LOccLine::kRows;
+    uint32_t w[7] = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t c0 = 0, c1 = 0, c2 = 0;
+    for (uint32_t r = 0; r < LOccLine::kRows; ++r) {
+      if (a + r >= n) break;
+      const uint32_t sym = bwt[a + r];
+      uint32_t k = code[sym];
+      if (k == kNoCode) {
+        const unsigned int e = atomicAdd(exc_n, 1u);
+        if (e < (unsigned)kMaxExc) {
+          exc_rows[e] = a + r;
+          exc_sym[e] = (uint8_t)sym;
+        }
+        k = 0;
+      }
+      w[r >> 4] |= k << (2 * (r & 15));
+      c0 += k == 0;
+      c1 += k == 1;
+      c2 += k == 2;
+    }
+    uint4* L = reinterpret_cast<uint4*>(lines) + q * 2;
+    L[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    L[1] = make_uint4(w[4], w[5], w[6], 0u);  // residuals are filled in per code
+    cnt[q] = c0;
+    cnt[nl + q] = c1;
+    cnt[2 * nl + q] = c2;
+  }
+}
+
+// One thread per superblock: the model of code j through the occ values at the
+// superblock's first and last line starts (base[] = exclusive scan of the counts).
+__global__ void k_locc_model(const uint64_t* __restrict__ base, uint64_t nl, uint32_t shift,
+                             uint64_t nsb, int j, LOccModel* __restrict__ models) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < nsb; b += gs) {
+    const uint64_t q0 = b << shift;
+    uint64_t q1 = q0 + (1ull << shift) - 1;
+    if (q1 >= nl) q1 = nl - 1;
+    const uint64_t b0 = base[q0], b1 = base[q1];
+    const uint64_t rows = 104ull * (q1 - q0);
+    models[b].base[j] = b0;
+    models[b].slope[j] = rows ? ((b1 - b0) << 32) / rows : 0;
+  }
+}
+
+// One thread per line: residual of code j against its superblock's model; flags any
+// residual outside int16.
+__global__ void k_locc_resid(uint32_t* __restrict__ lines, const uint64_t* __restrict__ base,
+                             uint64_t nl, uint32_t shift, const LOccModel* __restrict__ models,
+                             int j, unsigned int* __restrict__ bad) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nl; q += gs) {
+    const LOccModel m = models[q >> shift];
+    const int64_t r = (int64_t)base[q] - (int64_t)locc_pred(m, (uint32_t)j, q - ((q >> shift) << shift));
+    if (r < -32768 || r > 32767) atomicOr(bad, 1u);
+    uint16_t* h16 = reinterpret_cast<uint16_t*>(lines + q * 8 + 6);  // w3 bits 16.. (dwords 6, 7)
+    h16[1 + j] = (uint16_t)(int16_t)r;
+  }
+}
+
 // ---- quaternary wavelet matrix (fm_query.hip QWM) ----
 __global__ void k_qcodes(const uint8_t* __restrict__ bwt, uint64_t n, CodeMap map,
                          uint8_t* __restrict__ out) {
@@ -400,6 +472,86 @@ bool occ_feasible(const unsigned long long* hist, uint64_t n, CodeMap& map, uint
   for (int k = 0; k < 4; ++k) occ_sym[k] = k < nc ? (uint8_t)order[k] : 0;
   for (int k = 0; k < nc; ++k) map.c[order[k]] = (uint8_t)k;
   return true;
+}
+
+// Learned occurrence lines (LOccLine): codes and residuals per line, models per
+// superblock of 2^14 lines (2^8 when a residual of the first try overflows int16:
+// then every residual fits, fm_device.hpp).  Rare rows as build_occ.
+cs_status build_locc(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
+                     hipStream_t st) {
+  const uint64_t nl = h->nlines;
+  FMX_HIP(hipMalloc(&h->d_lines, nl * LOccLine::kBytes));
+  DevBuf cnt, base, tmp, erow, esym, en, bad;
+  FMX_HIP(cnt.alloc(3 * nl * 4));
+  FMX_HIP(base.alloc(3 * nl * 8));
+  FMX_HIP(erow.alloc(kMaxExc * 8));
+  FMX_HIP(esym.alloc(kMaxExc));
+  FMX_HIP(en.alloc(4));
+  FMX_HIP(bad.alloc(4));
+  FMX_HIP(hipMemsetAsync(en.p, 0, 4, st));
+  k_locc_pack<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(
+      bwt, n, map, nl, static_cast<uint32_t*>(h->d_lines), cnt.as<uint32_t>(),
+      erow.as<unsigned long long>(), esym.as<uint8_t>(), en.as<unsigned int>());
+  FMX_HIP(hipGetLastError());
+  size_t tb = 0;
+  FMX_HIP(rocprim::exclusive_scan(nullptr, tb, cnt.as<uint32_t>(), base.as<uint64_t>(), (uint64_t)0,
+                                  nl, rocprim::plus<uint64_t>(), st));
+  FMX_HIP(tmp.alloc(tb));
+  for (int j = 0; j < 3; ++j) {
+    size_t t2 = tb;
+    FMX_HIP(rocprim::exclusive_scan(tmp.p, t2, cnt.as<uint32_t>() + (uint64_t)j * nl,
+                                    base.as<uint64_t>() + (uint64_t)j * nl, (uint64_t)0, nl,
+                                    rocprim::plus<uint64_t>(), st));
+  }
+  uint32_t shift = 14;
+  if (const char* e = std::getenv("CS_FM_LEARNED_SHIFT")) shift = (uint32_t)std::atoi(e);
+  for (;;) {
+    const uint64_t nsb = ((nl - 1) >> shift) + 1;
+    if (h->d_lmodel) (void)hipFree(h->d_lmodel);
+    FMX_HIP(hipMalloc(&h->d_lmodel, nsb * sizeof(LOccModel)));
+    FMX_HIP(hipMemsetAsync(bad.p, 0, 4, st));
+    for (int j = 0; j < 3; ++j) {
+      const uint64_t* bj = base.as<uint64_t>() + (uint64_t)j * nl;
+      k_locc_model<<<grid_for(nsb, kBlk, 16384), kBlk, 0, st>>>(
+          bj, nl, shift, nsb, j, static_cast<LOccModel*>(h->d_lmodel));
+      k_locc_resid<<<grid_for(nl, kBlk, 16384), kBlk, 0, st>>>(
+          static_cast<uint32_t*>(h->d_lines), bj, nl, shift,
+          static_cast<const LOccModel*>(h->d_lmodel), j, bad.as<unsigned int>());
+      FMX_HIP(hipGetLastError());
+    }
+    unsigned int b = 0;
+    FMX_HIP(hipMemcpyAsync(&b, bad.p, 4, hipMemcpyDeviceToHost, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    h->nlmodel = nsb;
+    h->lmodel_shift = shift;
+    if (!b) break;
+    if (shift <= 8) {
+      set_error("learned occurrence lines: residual overflow");
+      return CS_ERR_INVALID;
+    }
+    shift = 8;
+  }
+  unsigned int ne = 0;
+  uint64_t rows[kMaxExc];
+  uint8_t syms[kMaxExc];
+  FMX_HIP(hipMemcpyAsync(&ne, en.p, 4, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(rows, erow.p, sizeof rows, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(syms, esym.p, sizeof syms, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  if (ne > (unsigned)kMaxExc) {
+    set_error("occurrence lines: rare-symbol rows exceed the table");
+    return CS_ERR_INVALID;
+  }
+  std::vector<int> idx(ne);
+  for (unsigned i = 0; i < ne; ++i) idx[i] = (int)i;
+  std::sort(idx.begin(), idx.end(), [&](int x, int y) { return rows[x] < rows[y]; });
+  NodeTable& T = h->h_table;
+  T.exc_n = ne;
+  for (unsigned i = 0; i < ne; ++i) {
+    T.exc_row[i] = rows[idx[i]];
+    T.exc_sym[i] = syms[idx[i]];
+  }
+  return CS_OK;
 }
 
 cs_status build_occ(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
@@ -607,7 +759,7 @@ cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_i
 // quaternary matrix's occ of the pure digit at its pure nodes' starts.
 cs_status launch_node_ranks(const cs_fm_index* h, uint64_t* d_R, hipStream_t st) {
   FMX_HIP(hipMemsetAsync(d_R, 0, kNodes * 8, st));
-  if (h->line_fmt == kFmtOcc) return CS_OK;  // no wavelet nodes
+  if (h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) return CS_OK;  // no wavelet nodes
   if (h->line_fmt == kFmtQwm)
     k_qnode_rank<<<1, 128, 0, st>>>(h->d_lines, h->nlines, h->d_table, d_R);
   else if (h->line_fmt == kFmtLine32)

@@ -220,6 +220,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
   if (h->d_lctx) (void)hipFree(h->d_lctx);
+  if (h->d_lmodel) (void)hipFree(h->d_lmodel);
   if (h->scratch.h) (void)hipHostFree(h->scratch.h);
   if (h->scratch.d) (void)hipFree(h->scratch.d);
   delete h;
@@ -354,10 +355,11 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->prefix_sigma = h->ptab_sigma;
   out->prefix_bytes = h->ptab_entries() * h->ptab_entry_bytes();
   for (int c = 0; c < 256; ++c) out->prefix_code[c] = h->h_table.code[c];
-  out->engine = h->line_fmt == kFmtOcc ? 1u : h->line_fmt == kFmtQwm ? 2u : 0u;
+  out->engine = h->line_fmt == kFmtOcc ? 1u : h->line_fmt == kFmtQwm ? 2u
+               : h->line_fmt == kFmtLOcc ? 3u : 0u;
   out->line_bytes = h->line_bytes;
   out->levels = h->nlevels;
-  out->rare_rows = h->line_fmt == kFmtOcc ? h->h_table.exc_n : 0u;
+  out->rare_rows = (h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) ? h->h_table.exc_n : 0u;
   out->walk_marks = h->d_walk ? h->walk_marks : 0u;
   out->walk_bytes = h->d_walk ? h->nwalk * 32 : 0u;
   out->context_q = h->d_lctx ? h->lctx_q : 0u;

@@ -70,7 +70,9 @@ struct NodeTable {
 constexpr uint8_t kNoCode = 0xFF;
 
 // rank-line formats (cs_fm_index::line_fmt)
-enum LineFmt : uint32_t { kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2, kFmtOcc = 3, kFmtQwm = 4 };
+enum LineFmt : uint32_t {
+  kFmtLine32 = 0, kFmtLine32W = 1, kFmtLine64 = 2, kFmtOcc = 3, kFmtQwm = 4, kFmtLOcc = 5
+};
 
 // Quaternary wavelet matrix: node of the l-digit code prefix x at level l.
 __host__ __device__ inline int qnode_id(int level, uint32_t prefix) {
@@ -112,6 +114,10 @@ struct DevIndex {
   const void* lctx;
   uint32_t lctx_q;
   uint32_t lctx_sb;
+  // Learned occurrence lines (LOccLine below): one LOccModel per superblock of
+  // 2^lmodel_shift lines.
+  const void* lmodel;
+  uint32_t lmodel_shift;
 };
 
 // Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q
@@ -343,6 +349,68 @@ struct OccLine {
     return (uint32_t)(((o < 32 ? lo : hi) >> (2 * (o & 31))) & 3u);
   }
 };
+
+// ---------------------------------------------------------------------------
+// Learned occurrence lines (LOccE; SURVEY.md §8(f) item 4 — the reference's learned
+// occ, src/core/bitvector_learned.cpp:114-203: rank = coarse model prediction + micro
+// residual + tail popcount, with the model of src/learned/pgm.hpp:31-79).  The
+// occurrence line's three absolute 40-bit counts become three int16 residuals against a
+// linear model of occ(c, .) per superblock of 2^sb lines, fitted through the
+// superblock's end points, so a 32-B line holds 104 rows instead of 64:
+//   occ(c, 104 q) = pred_c(q) + r_c(q),
+//   pred_c(q) = base_c + (slope_c * 104 (q - q0)) >> 32,  q0 = first line of q's superblock
+// (integers only: the builder and the queries evaluate the same expression).  A rank is
+// still one line read; the 48-B models of all superblocks (C4: 28 KB) stay in L2 and
+// are read beside the line.  Residuals are bounded by the superblock's rows, so a
+// superblock of 2^8 lines (26,624 rows) always fits int16; the builder tries 2^14 first.
+//   words (u64): w0 rows 0-31, w1 rows 32-63, w2 rows 64-95 (2-bit codes), w3 bits 0-15
+//   rows 96-103, bits 16-31 r_0, 32-47 r_1, 48-63 r_2.
+struct LOccModel {
+  uint64_t base[3];   // occ(c, 104 q0)
+  uint64_t slope[3];  // 2^32 x (occ(c) at the superblock's last line start - base) / rows
+};
+struct LOccLine {
+  static constexpr uint32_t kBytes = 32, kRows = 104;
+  using Raw = uint4[2];
+  __device__ static __forceinline__ void load(const void* lines, uint64_t q, Raw& v) {
+    const uint4* p = reinterpret_cast<const uint4*>(lines) + q * 2;
+    v[0] = p[0];
+    v[1] = p[1];
+  }
+  // rows among the first o (0..104) of the line whose code is c
+  __device__ static __forceinline__ uint32_t prefix(const Raw& v, uint32_t c, uint32_t o) {
+    constexpr uint64_t k55 = 0x5555555555555555ull;
+    const uint64_t pat = k55 * c;
+    const uint64_t w[4] = {u64_of(v[0].x, v[0].y), u64_of(v[0].z, v[0].w), u64_of(v[1].x, v[1].y),
+                           (uint64_t)(v[1].z & 0xFFFFu)};
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t x = w[k] ^ pat;
+      const uint64_t e = ~(x | (x >> 1)) & k55;
+      const int rows = (int)o - 32 * k;
+      const uint64_t m = rows >= 32 ? ~0ull : (rows <= 0 ? 0ull : ((1ull << (2 * rows)) - 1));
+      r += (uint32_t)__popcll(e & m);
+    }
+    return r;
+  }
+  __device__ static __forceinline__ uint32_t code(const Raw& v, uint32_t o) {
+    const uint32_t k = o >> 4;  // dword holding row o
+    const uint32_t d[7] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z};
+    uint32_t x = d[0];
+#pragma unroll
+    for (int j = 1; j < 7; ++j) x = k == (uint32_t)j ? d[j] : x;
+    return (x >> (2 * (o & 15))) & 3u;
+  }
+  __device__ static __forceinline__ int32_t resid(const Raw& v, uint32_t c) {
+    const uint32_t h = c == 0 ? (v[1].z >> 16) : c == 1 ? (v[1].w & 0xFFFFu) : (v[1].w >> 16);
+    return (int32_t)(int16_t)(uint16_t)h;
+  }
+};
+
+__host__ __device__ inline uint64_t locc_pred(const LOccModel& m, uint32_t c, uint64_t dq) {
+  return m.base[c] + ((m.slope[c] * (104ull * dq)) >> 32);
+}
 
 // ---------------------------------------------------------------------------
 // Walk lines (locate's LF walk, occurrence engine): one 32-B line gives, for a

@@ -40,6 +40,9 @@ struct cs_fm_index {
   uint64_t nlctx = 0;                 // entries allocated (rows rounded up + a pad sector)
   uint32_t lctx_q = 0, lctx_sb = 0;   // symbols per entry, bits per symbol
   uint32_t lctx_eb = 0;               // bytes per entry (2 occurrence lines, 4 quaternary matrix)
+  void* d_lmodel = nullptr;           // learned occurrence lines: superblock models
+  uint64_t nlmodel = 0;
+  uint32_t lmodel_shift = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   uint32_t active_levels[256] = {};
 
@@ -108,6 +111,8 @@ struct cs_fm_index {
     d.lctx = d_lctx;
     d.lctx_q = d_lctx ? lctx_q : 0u;
     d.lctx_sb = lctx_sb;
+    d.lmodel = d_lmodel;
+    d.lmodel_shift = lmodel_shift;
     return d;
   }
 };
@@ -135,6 +140,8 @@ cs_status build_wm_levels(uint8_t* bwt, uint64_t n, cs_fm_index* h, hipStream_t 
 bool occ_feasible(const unsigned long long* hist, uint64_t n, CodeMap& map, uint8_t occ_sym[4]);
 cs_status build_occ(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
                     hipStream_t st);
+cs_status build_locc(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
+                     hipStream_t st);
 cs_status build_qwm(const uint8_t* bwt, uint64_t n, const unsigned long long* hist,
                     cs_fm_index* h, hipStream_t st);
 cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,

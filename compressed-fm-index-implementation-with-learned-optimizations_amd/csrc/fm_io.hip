@@ -10,14 +10,14 @@
 // Directory layout (all little-endian raw arrays, exactly the HBM images):
 //   cs_fmindex.meta  "key value" lines: format, n, stride, line_bytes, line_bits,
 //                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
-//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride,
+//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride, nlmodel, lmodel_shift,
 //                    active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
 //   ssa.bin          sampled SA              isa.bin   inverse-SA samples (u32; u64 if wide)
 //   ptab.bin         prefix table (if k > 0) text.bin  the text (if kept, for extract)
 //   walk.bin         walk lines                      wssa.bin  their position samples
-//   lctx.bin         left contexts (if built)
+//   lctx.bin         left contexts (if built)    lmodel.bin  learned-line models
 // The device image (cs_fm_export_* / cs_fm_import) is the same meta text plus the
 // parts table, lines, ssa, isa[, ptab][, walk][, wssa][, lctx] as device buffers.
 #include <cerrno>
@@ -108,6 +108,7 @@ std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa) {
   if (h->nwalk) v.push_back({"walk.bin", &h->d_walk, h->nwalk * 32});
   if (has_wssa) v.push_back({"wssa.bin", &h->d_wssa, h->nisa * sb});
   if (h->nlctx) v.push_back({"lctx.bin", &h->d_lctx, h->nlctx * h->lctx_eb});
+  if (h->nlmodel) v.push_back({"lmodel.bin", &h->d_lmodel, h->nlmodel * sizeof(LOccModel)});
   return v;
 }
 
@@ -117,14 +118,15 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 "format %s\nn %llu\nstride %u\nline_bytes %u\nline_bits %u\nnlines %llu\n"
                 "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
                 "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n"
-                "nlctx %llu\nlctx_q %u\nlctx_sb %u\nlctx_eb %u\npstride %u\n",
+                "nlctx %llu\nlctx_q %u\nlctx_sb %u\nlctx_eb %u\npstride %u\nnlmodel %llu\n"
+                "lmodel_shift %u\n",
                 kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                 (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                 (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
                 has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
                 (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0,
                 (unsigned long long)(h->d_lctx ? h->nlctx : 0), h->lctx_q, h->lctx_sb, h->lctx_eb,
-                h->pstride);
+                h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift);
   std::string m(buf);
   for (int c = 0; c < 256; ++c) {
     std::snprintf(buf, sizeof buf, "active %d %u\n", c, h->active_levels[c]);
@@ -173,6 +175,8 @@ cs_status meta_parse(const std::string& text, cs_fm_index* h,
   h->lctx_sb = (uint32_t)kv["lctx_sb"];
   h->lctx_eb = (uint32_t)kv["lctx_eb"];
   h->pstride = kv["pstride"] ? (uint32_t)kv["pstride"] : h->stride;  // older images: the SSA's
+  h->nlmodel = kv["nlmodel"];
+  h->lmodel_shift = (uint32_t)kv["lmodel_shift"];
   return CS_OK;
 }
 

@@ -231,6 +231,92 @@ struct OccE {
   }
 };
 
+// LOccE: learned occurrence lines (fm_device.hpp LOccLine), the occurrence engine
+// with 104 rows per line.  occ(c, i) = the model's prediction at the line start + the
+// line's residual + rows of code c before i in the line (bitvector_learned.cpp:152-203:
+// coarse prediction + micro correction + tail popcount); the superblock model is an
+// L2-resident read beside the line.  Rare rows as OccE.
+struct LOccE {
+  static constexpr bool kCtx = true;
+  using CtxEnt = uint16_t;
+  __device__ static __forceinline__ uint64_t line_of(uint64_t i) { return i / LOccLine::kRows; }
+  // occ(code, i) with i in line q
+  __device__ static __forceinline__ uint64_t occ_line(const DevIndex& ix, const LOccLine::Raw& v,
+                                                      uint32_t code, uint64_t q, uint64_t i) {
+    const uint64_t b = q >> ix.lmodel_shift, dq = q - (b << ix.lmodel_shift);
+    const LOccModel* m = static_cast<const LOccModel*>(ix.lmodel) + b;
+    uint64_t start;
+    if (code < 3) {
+      start = m->base[code] + ((m->slope[code] * (104ull * dq)) >> 32) + (int64_t)LOccLine::resid(v, code);
+    } else {
+      start = 104ull * q;
+#pragma unroll
+      for (uint32_t c = 0; c < 3; ++c)
+        start -= m->base[c] + ((m->slope[c] * (104ull * dq)) >> 32) + (int64_t)LOccLine::resid(v, c);
+    }
+    return start + LOccLine::prefix(v, code, (uint32_t)(i - q * LOccLine::kRows));
+  }
+  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
+                                              uint64_t& sp, uint64_t& ep,
+                                              uint64_t* bytes = nullptr) {
+    const uint64_t Cc = T.C[c];
+    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
+    const uint32_t code = T.occ_code[c];
+    uint64_t rs, re;
+    if (code == kNoCode) {
+      rs = exc_rank(T, c, sp);
+      re = exc_rank(T, c, ep);
+    } else {
+      const uint64_t qa = line_of(sp), qe = line_of(ep);
+      if (bytes) *bytes += (qa == qe ? 1u : 2u) * LOccLine::kBytes;
+      LOccLine::Raw va;
+      LOccLine::load(ix.lines, qa, va);
+      LOccLine::Raw ve = {va[0], va[1]};
+      if (qe != qa) LOccLine::load(ix.lines, qe, ve);
+      rs = occ_line(ix, va, code, qa, sp);
+      re = occ_line(ix, ve, code, qe, ep);
+      if (code == 0 && T.exc_n) {
+        rs -= exc_before(T, sp);
+        re -= exc_before(T, ep);
+      }
+    }
+    sp = Cc + rs;
+    ep = Cc + re;
+    return sp < ep;
+  }
+  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
+                                                uint64_t pos, uint32_t* sym_out = nullptr) {
+    const uint64_t q = line_of(pos);
+    LOccLine::Raw v;
+    LOccLine::load(ix.lines, q, v);
+    const uint32_t code = LOccLine::code(v, (uint32_t)(pos - q * LOccLine::kRows));
+    uint32_t c = T.occ_sym[code];
+    uint64_t r = occ_line(ix, v, code, q, pos);
+    if (code == 0 && T.exc_n) {
+      const uint32_t e = exc_before(T, pos);
+      if (e < T.exc_n && T.exc_row[e] == pos) {
+        c = T.exc_sym[e];
+        r = exc_rank(T, c, pos);
+      } else {
+        r -= e;
+      }
+    }
+    if (sym_out) *sym_out = c;
+    return T.C[c] + r;
+  }
+  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
+                                                  uint32_t c, uint64_t i) {
+    const uint32_t code = T.occ_code[c];
+    if (code == kNoCode) return exc_rank(T, c, i);
+    const uint64_t q = line_of(i);
+    LOccLine::Raw v;
+    LOccLine::load(ix.lines, q, v);
+    uint64_t r = occ_line(ix, v, code, q, i);
+    if (code == 0) r -= exc_before(T, i);
+    return r;
+  }
+};
+
 // QWM: quaternary wavelet matrix over dense symbol codes, for alphabets beyond the
 // occurrence engine (e.g. sigma = 256: 4 levels instead of 8).  Level l holds digit
 // l (2 bits, most significant first) of the level-l sequence as occurrence lines
@@ -601,7 +687,7 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
-template <int U, bool kLoc>
+template <class E, int U, bool kLoc>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, uint64_t* __restrict__ out,
@@ -742,11 +828,11 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (kLoc) {
       uint64_t r;
-      const uint64_t c = locate_search<OccE>(ix, T, pats + o0[j], m[j], r);
+      const uint64_t c = locate_search<E>(ix, T, pats + o0[j], m[j], r);
       out[q] = c < limit ? c : limit;
       rec[q] = r;
     } else {
-      out[q] = count_pattern<OccE>(ix, T, pats + o0[j], m[j]);
+      out[q] = count_pattern<E>(ix, T, pats + o0[j], m[j]);
     }
   }
 }
@@ -1243,6 +1329,8 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
   do {                                                                          \
     if ((h)->line_fmt == kFmtOcc)                                               \
       KERNEL<OccE><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                       \
+    else if ((h)->line_fmt == kFmtLOcc)                                         \
+      KERNEL<LOccE><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                      \
     else if ((h)->line_fmt == kFmtQwm)                                          \
       KERNEL<QWM><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                        \
     else if ((h)->line_fmt == kFmtLine32)                                       \
@@ -1259,6 +1347,8 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
   do {                                                                          \
     if ((h)->line_fmt == kFmtOcc)                                               \
       KERNEL<OccE><<<1, 64, 0, st>>>(__VA_ARGS__);                              \
+    else if ((h)->line_fmt == kFmtLOcc)                                         \
+      KERNEL<LOccE><<<1, 64, 0, st>>>(__VA_ARGS__);                             \
     else if ((h)->line_fmt == kFmtQwm)                                          \
       KERNEL<QWM><<<1, 64, 0, st>>>(__VA_ARGS__);                               \
     else if ((h)->line_fmt == kFmtLine32)                                       \
@@ -1336,7 +1426,7 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   h->d_lctx = nullptr;
   h->nlctx = 0;
   h->lctx_q = h->lctx_sb = h->lctx_eb = 0;
-  const bool occ = h->line_fmt == kFmtOcc, qwm = h->line_fmt == kFmtQwm;
+  const bool occ = h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc, qwm = h->line_fmt == kFmtQwm;
   if (!(occ || qwm) || h->n == 0) return CS_OK;
   if (const char* e = std::getenv("CS_FM_LCTX"))
     if (std::atoi(e) == 0) return CS_OK;
@@ -1354,7 +1444,10 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   h->lctx_eb = eb;
   FMX_HIP(hipMemsetAsync(static_cast<uint8_t*>(h->d_lctx) + h->n * eb, 0, (rows - h->n) * eb, st));
   const DevIndex ix = h->dev();
-  if (occ)
+  if (h->line_fmt == kFmtLOcc)
+    k_build_lctx<LOccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
+        ix, static_cast<uint16_t*>(h->d_lctx));
+  else if (occ)
     k_build_lctx<OccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
         ix, static_cast<uint16_t*>(h->d_lctx));
   else
@@ -1381,21 +1474,24 @@ cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st) {
   if (!npat) return CS_OK;
-  if (h->line_fmt == kFmtOcc && h->d_lctx && h->ptab_k) {
+  if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
     static const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U)
       const char* e = std::getenv("CS_FM_COUNT_U");
       const int u = e ? std::atoi(e) : 2;
       return u == 1 || u == 4 ? u : 2;
     }();
     const DevIndex ix = h->dev();
-    if (U == 1)
-      k_count_ctx<1, false><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+    if (h->line_fmt == kFmtLOcc)
+      k_count_ctx<LOccE, 2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
+    else if (U == 1)
+      k_count_ctx<OccE, 1, false><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, d_out, 0, nullptr);
     else if (U == 2)
-      k_count_ctx<2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+      k_count_ctx<OccE, 2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, d_out, 0, nullptr);
     else
-      k_count_ctx<4, false><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+      k_count_ctx<OccE, 4, false><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, d_out, 0, nullptr);
     FMX_HIP(hipGetLastError());
     return CS_OK;
@@ -1432,9 +1528,13 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                hipStream_t st) {
   StreamBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8, st));
-  if (h->line_fmt == kFmtOcc && h->d_lctx && h->ptab_k) {  // staged, two patterns per lane
-    k_count_ctx<2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp);
+  if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
+    if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
+      k_count_ctx<OccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp);
+    else
+      k_count_ctx<LOccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp);
     FMX_HIP(hipGetLastError());
   } else {
     FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,
@@ -1503,6 +1603,9 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   } else if (h->line_fmt == kFmtOcc) {
     if (pow2) k_walk<OccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<OccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+  } else if (h->line_fmt == kFmtLOcc) {
+    if (pow2) k_walk<LOccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    else k_walk<LOccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
   } else if (h->line_fmt == kFmtLine32) {
     if (pow2) k_walk<WM<Line32>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
     else k_walk<WM<Line32>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
@@ -1546,7 +1649,7 @@ cs_status check_locate_error(const cs_fm_index* h, unsigned long long* err, hipS
 
 cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,
                              uint64_t* d_out, hipStream_t st) {
-  if (h->line_fmt == kFmtOcc || h->line_fmt == kFmtQwm) {
+  if (h->line_fmt == kFmtOcc || h->line_fmt == kFmtQwm || h->line_fmt == kFmtLOcc) {
     set_error("level rank1: this index has no binary wavelet levels (occurrence lines)");
     return CS_ERR_UNSUPPORTED;
   }

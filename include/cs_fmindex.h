@@ -69,7 +69,8 @@ typedef struct cs_fm_info {
   uint64_t prefix_bytes;
   uint8_t prefix_code[256];/* digit of each symbol in the table alphabet, 255 = not in it */
   uint32_t engine;         /* 0 = binary wavelet matrix in rank lines, 1 = occurrence lines,
-                              2 = quaternary wavelet matrix of occurrence lines */
+                              2 = quaternary wavelet matrix of occurrence lines,
+                              3 = learned occurrence lines (model + residual counters) */
   uint32_t line_bytes;     /* bytes per rank / occurrence line (32 or 64) */
   uint32_t levels;         /* rank-line sequences: 8 binary levels, 1..4 quaternary, or 1 */
   uint32_t rare_rows;      /* occurrence lines: BWT rows of rare symbols kept in the table */

@@ -103,7 +103,7 @@ def test_concurrent_calls_share_nothing_mutable():
     assert not bad, bad[:5]
 
 
-@pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet"])
+@pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "learned"])
 def test_export_import_image(engine, monkeypatch):
     """The device image (cs_fm_export_meta/_parts -> cs_fm_import): the copy answers
     count / locate / extract exactly as the original."""
@@ -120,7 +120,7 @@ def test_export_import_image(engine, monkeypatch):
     c = pkg.FMIndex.import_image(meta, [p.data_ptr() for p in parts], 0)
     del parts
     assert c.info().engine == g.info().engine and c.info().walk_marks == g.info().walk_marks
-    assert c.info().context_q == g.info().context_q == {"auto": 7, "qwm": 8, "wavelet": 0}[engine]
+    assert c.info().context_q == g.info().context_q == {"auto": 7, "qwm": 8, "wavelet": 0, "learned": 7}[engine]
     P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 14, 500)
     pats = [bytes(r) for r in P] + [b"ACGTACGTAC", b"$", b""]
     assert c.count_batch(pats).tolist() == g.count_batch(pats).tolist()

@@ -31,6 +31,8 @@ ENGINE_VARIANTS = {
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
+    "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
+    "learned_sb4": {"CS_FM_ENGINE": "learned", "CS_FM_LEARNED_SHIFT": "2"},  # 4-line superblocks
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
     "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
     # the n >= 2^32 engines at small n: u64 samples/table, bucketed sorter, and
@@ -40,7 +42,7 @@ ENGINE_VARIANTS = {
 }
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
           "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
-          "CS_FM_PSTRIDE")
+          "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -176,17 +178,19 @@ def test_engine_choice(built):
             engine, rare = 0, 0
         elif forced == "qwm":
             engine, rare = 2, 0
+        elif forced == "learned" and engine == 1:
+            engine = 3
         marks = 0 if engine == 0 else (2 if cyc else 1)
         if os.environ.get("CS_FM_WALK") == "0":
             marks = 0
         elif os.environ.get("CS_FM_WALK_MARKS") == "row" and marks:
             marks = 1
         assert (info.engine, info.rare_rows, info.walk_marks) == (engine, rare, marks), name
-        want_levels = {0: 8, 1: 1, 2: levels[name]}[engine]
+        want_levels = {0: 8, 1: 1, 2: levels[name], 3: 1}[engine]
         assert info.levels == want_levels and info.line_bytes in (32, 64), name
         # left contexts: occurrence lines 7 x 2-bit codes in u16 (16 rows per 32-B
         # sector), quaternary matrix 32 / (2 x levels) dense codes in u32 (8 rows)
-        ctx, R = {1: (7, 16), 2: (min(16, 32 // (2 * info.levels)), 8)}.get(engine, (0, 1))
+        ctx, R = {1: (7, 16), 3: (7, 16), 2: (min(16, 32 // (2 * info.levels)), 8)}.get(engine, (0, 1))
         if os.environ.get("CS_FM_LCTX") == "0":
             ctx = 0
         assert info.context_q == ctx, name

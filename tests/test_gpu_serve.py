@@ -26,7 +26,7 @@ def _patterns(t, rng, n):
     return pats
 
 
-@pytest.mark.parametrize("engine", ["auto", "wavelet", "qwm"])
+@pytest.mark.parametrize("engine", ["auto", "wavelet", "qwm", "learned"])
 @pytest.mark.parametrize("kind", ["dna", "bytes"])
 def test_serve_matches_oracle(kind, engine, monkeypatch):
     if engine != "auto":
