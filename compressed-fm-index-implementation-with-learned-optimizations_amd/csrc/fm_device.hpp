@@ -155,16 +155,23 @@ __device__ __forceinline__ uint64_t ssa_at(const DevIndex& ix, uint64_t k) {
 __device__ __forceinline__ uint64_t isa_at(const DevIndex& ix, uint64_t k) {
   return ix.wide ? static_cast<const uint64_t*>(ix.isa)[k] : static_cast<const uint32_t*>(ix.isa)[k];
 }
-__device__ __forceinline__ void ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
+// Prefix-table entries: 2 x u32 (sp, ep); in wide indexes (n >= 2^32) one u64 packing
+// sp (38 bits, n < 2^38) and the range width (26 bits), so the table keeps 8 B per
+// k-mer.  A width >= kPtabEsc is stored as kPtabEsc: that k-mer's search starts from
+// C[] instead (ptab_at returns false).
+constexpr uint64_t kPtabEsc = (1ull << 26) - 1;
+__device__ __forceinline__ bool ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
   if (ix.wide) {
-    const ulonglong2 r = static_cast<const ulonglong2*>(ix.ptab)[t];
-    sp = r.x;
-    ep = r.y;
-  } else {
-    const uint2 r = static_cast<const uint2*>(ix.ptab)[t];
-    sp = r.x;
-    ep = r.y;
+    const uint64_t e = static_cast<const uint64_t*>(ix.ptab)[t];
+    const uint64_t w = e >> 38;
+    sp = e & ((1ull << 38) - 1);
+    ep = sp + w;
+    return w != kPtabEsc;
   }
+  const uint2 r = static_cast<const uint2*>(ix.ptab)[t];
+  sp = r.x;
+  ep = r.y;
+  return true;
 }
 
 __host__ __device__ inline int node_id(int level, uint32_t prefix) {

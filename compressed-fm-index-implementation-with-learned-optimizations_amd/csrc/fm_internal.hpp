@@ -75,7 +75,7 @@ struct cs_fm_index {
   mutable Server server;
 
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
-  uint32_t ptab_entry_bytes() const { return wide ? 16 : 8; }
+  uint32_t ptab_entry_bytes() const { return 8; }  // 2 x u32, or packed (sp, width) when wide
   uint64_t ptab_entries() const {
     if (!ptab_k) return 0;
     uint64_t e = 1;

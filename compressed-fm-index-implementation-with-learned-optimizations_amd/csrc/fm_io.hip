@@ -34,7 +34,7 @@
 namespace fmx {
 namespace {
 
-constexpr const char* kFormat = "cs_fmindex/2";
+constexpr const char* kFormat = "cs_fmindex/3";  // 3: packed wide prefix-table entries
 constexpr size_t kChunk = 256ull << 20;
 
 std::string join(const std::string& dir, const char* f) { return dir + "/" + f; }

@@ -415,9 +415,8 @@ __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable
       ok &= d != kNoCode;
       t = t * ix.ptab_sigma + d;
     }
-    if (ok) {
-      ptab_at(ix, t, sp, ep);
-      if (bytes) *bytes += ix.wide ? 16u : 8u;
+    if (ok && ptab_at(ix, t, sp, ep)) {
+      if (bytes) *bytes += 8u;
       k = m - ix.ptab_k;
       return;
     }
@@ -592,7 +591,7 @@ __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const Node
 // the end is sym[digit_j(t)] (same steps as above, from C[]).
 template <class E>
 __global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entries,
-                                                     void* __restrict__ tab) {
+                                                     void* __restrict__ tab, uint64_t wmax) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
@@ -609,8 +608,8 @@ __global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entri
       live = E::step(ix, T, c, sp, ep);
     }
     if (!live) sp = ep = 0;
-    if (ix.wide)
-      static_cast<ulonglong2*>(tab)[t] = make_ulonglong2(sp, ep);
+    if (ix.wide)  // packed (sp, width), widths >= wmax escaped (fm_device.hpp ptab_at)
+      static_cast<uint64_t*>(tab)[t] = ep - sp >= wmax ? kPtabEsc << 38 : sp | ((ep - sp) << 38);
     else
       static_cast<uint2*>(tab)[t] = make_uint2((uint32_t)sp, (uint32_t)ep);
   }
@@ -749,7 +748,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   // (B)
 #pragma unroll
   for (int j = 0; j < U; ++j)
-    if (st[j] == 1 || st[j] == 2) ptab_at(ix, t[j], sp[j], ep[j]);
+    if ((st[j] == 1 || st[j] == 2) && !ptab_at(ix, t[j], sp[j], ep[j])) st[j] = 3;
   // (C)
   uint4 w[U][4];
 #pragma unroll
@@ -1362,12 +1361,14 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 
 // Prefix table over the frequent alphabet: symbols with at least n/2^20
 // occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^30, max(4096, n/2)) entries (8 B each, 16 B in wide indexes:
-// at most 4n resp. 8n bytes, capped at 8 resp. 16 GiB); none when k < 2.  Each
-// character in the table saves one dependent random line read per query, and
-// HBM (288 GB) is not the constraint: C4 k = 14 -> 15 is +14 % count rate.
-// DNA: k = 12 at 100 MB, k = 15 at 4 GB and at 32 GB.  Entries are (sp, ep) as 2 x u32, or
-// 2 x u64 in wide indexes.  CS_FM_PREFIX_K overrides k (0 = off).
+// sigma^k <= min(2^32, max(4096, n/2)) entries of 8 B (at most 4n bytes, capped at
+// 32 GiB); none when k < 2.  Each character in the table saves one dependent random
+// line read per query, and HBM (288 GB) is not the constraint: C4 k = 14 -> 15 is
+// +14 % count rate; C5 k = 15 -> 16 leaves a range of ~7 rows instead of ~30 for the
+// left contexts.  DNA: k = 12 at 100 MB, 15 at 4 GB, 16 at 32 GB.  Entries are (sp, ep)
+// as 2 x u32, or packed (sp, width) in wide indexes (fm_device.hpp ptab_at).
+// CS_FM_PREFIX_K overrides k (0 = off); CS_FM_PTAB_WMAX lowers the escape width (test
+// hook).
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   NodeTable& T = h->h_table;
   std::memset(T.code, kNoCode, sizeof T.code);
@@ -1386,7 +1387,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   }
   if (sigma == 0) return CS_OK;
   uint64_t cap = n / 2 > 4096 ? n / 2 : 4096;
-  if (cap > (1ull << 30)) cap = 1ull << 30;
+  if (cap > (1ull << 32)) cap = 1ull << 32;
   uint32_t k = 0;
   uint64_t entries = 1;
   while (k < 32 && entries * sigma <= cap) {
@@ -1397,7 +1398,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     const int want = std::atoi(e);
     k = 0;
     entries = 1;
-    while ((int)k < want && entries * sigma <= (1ull << 30)) {
+    while ((int)k < want && entries * sigma <= (1ull << 32)) {
       entries *= sigma;
       ++k;
     }
@@ -1412,7 +1413,9 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   h->ptab_k = k;
   DevIndex ix = h->dev();
   ix.ptab = nullptr;  // the builder itself searches from C[]
-  FMX_DISPATCH(h, k_build_ptab, grid_for(entries, kBlk, 65536), ix, entries, h->d_ptab);
+  uint64_t wmax = kPtabEsc;
+  if (const char* e = std::getenv("CS_FM_PTAB_WMAX")) wmax = std::strtoull(e, nullptr, 10);
+  FMX_DISPATCH(h, k_build_ptab, grid_for(entries, kBlk, 65536), ix, entries, h->d_ptab, wmax);
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
 }
@@ -1421,7 +1424,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
 // quaternary matrix (4n bytes; C3 4 GB); rows rounded up to whole 32-B sectors plus
 // one pad sector.  Skipped (count steps through the rank structure instead) for the
 // binary wavelet matrix, when CS_FM_LCTX=0, or when HBM is short: the index must
-// leave a quarter of the device free.
+// leave an eighth of the device free (36 GB on MI355X) for the query buffers.
 cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   h->d_lctx = nullptr;
   h->nlctx = 0;
@@ -1436,7 +1439,7 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   const uint64_t rows = ((h->n + R - 1) & ~(uint64_t)(R - 1)) + R;
   size_t free_b = 0, total_b = 0;
   FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (rows * eb + total_b / 4 > free_b) return CS_OK;
+  if (rows * eb + total_b / 8 > free_b) return CS_OK;
   FMX_HIP(hipMalloc(&h->d_lctx, rows * eb));
   h->nlctx = rows;
   h->lctx_q = q;

@@ -39,10 +39,12 @@ ENGINE_VARIANTS = {
     # occurrence lines or 32-B wide rank lines (Line32W)
     "wide_bucketed": {"CS_FM_WIDE": "1", "CS_FM_SA_BUILDER": "bucketed"},
     "wide_wavelet": {"CS_FM_WIDE": "1", "CS_FM_ENGINE": "wavelet"},
+    # packed wide prefix-table entries with every range of 3+ rows escaped (C[] start)
+    "wide_ptab_esc": {"CS_FM_WIDE": "1", "CS_FM_PTAB_WMAX": "3"},
 }
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
           "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
-          "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT")
+          "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT", "CS_FM_PTAB_WMAX")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
