@@ -691,9 +691,15 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, uint64_t* __restrict__ out,
                                                     uint64_t limit, uint64_t* __restrict__ rec) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
+  // the stages need only the symbol -> (table digit, occurrence code) map in LDS (512 B
+  // instead of the 10.8-KB node table: a shorter block prologue); the general search
+  // of the few remaining patterns reads the node table through the caches
+  __shared__ uint16_t cmap[256];
+  static_assert(kBlk >= 256, "one map entry per thread");
+  if (threadIdx.x < 256)
+    cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   __syncthreads();
+  const NodeTable& T = *ix.table;
   const uint32_t K = ix.ptab_k;
   const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
@@ -730,11 +736,11 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     for (uint32_t i = 0; i < kFastM; ++i) {
       const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
       if (i >= kk && i < m[j]) {  // table part, most significant first
-        const uint32_t d = T.code[b];
+        const uint32_t d = cmap[b] & 0xFFu;
         ok &= d != kNoCode;
         tt = tt * ix.ptab_sigma + d;
       } else if (i < kk && i < kCtxQ) {  // context part: chain symbol kk-1-i
-        const uint32_t d = T.occ_code[b];
+        const uint32_t d = cmap[b] >> 8;
         cok &= d != kNoCode;
         ww |= (d & 3u) << (2 * (kk - 1 - i));
       }
