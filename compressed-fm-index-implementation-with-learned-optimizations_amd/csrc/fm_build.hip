@@ -490,6 +490,11 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
     if (cs != CS_OK) return cs;
   }
   plog.mark("left contexts");
+  {
+    cs_status cs = build_context_records(h, st);
+    if (cs != CS_OK) return cs;
+  }
+  plog.mark("context records");
   FMX_HIP(hipMalloc(&h->d_err, 8));
   FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));

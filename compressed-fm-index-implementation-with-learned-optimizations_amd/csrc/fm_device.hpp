@@ -99,6 +99,7 @@ struct DevIndex {
   const void* ptab;
   uint32_t ptab_k;
   uint32_t ptab_sigma;
+  uint32_t ptab_rec;     // entries are 32-B context records (kRecCtx below)
   // Inverse-SA samples: isa[k] = row of the suffix at text position k*stride, for
   // extract by LF inversion (needs suffix order == rotation order, i.e. a unique
   // smallest last symbol: lf_exact).
@@ -160,7 +161,19 @@ __device__ __forceinline__ uint64_t isa_at(const DevIndex& ix, uint64_t k) {
 // k-mer.  A width >= kPtabEsc is stored as kPtabEsc: that k-mer's search starts from
 // C[] instead (ptab_at returns false).
 constexpr uint64_t kPtabEsc = (1ull << 26) - 1;
+// Context records (narrow occurrence-engine indexes with left contexts): each entry
+// is 32 B — sp (u32), width (u32) and the left contexts (u16) of the range's first
+// kRecCtx rows — so a search whose range after the table is at most kRecCtx rows
+// wide and has at most kCtxQ characters left is answered by the ONE random read of its
+// table entry (the contexts are the rows' lctx entries, fm_device.hpp kCtxQ).
+constexpr uint32_t kRecCtx = 12;
 __device__ __forceinline__ bool ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
+  if (ix.ptab_rec) {
+    const uint2 r = static_cast<const uint2*>(ix.ptab)[t * 4];
+    sp = r.x;
+    ep = (uint64_t)r.x + r.y;
+    return true;
+  }
   if (ix.wide) {
     const uint64_t e = static_cast<const uint64_t*>(ix.ptab)[t];
     const uint64_t w = e >> 38;

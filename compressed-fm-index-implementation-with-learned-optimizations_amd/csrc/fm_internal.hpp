@@ -75,7 +75,8 @@ struct cs_fm_index {
   mutable Server server;
 
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
-  uint32_t ptab_entry_bytes() const { return 8; }  // 2 x u32, or packed (sp, width) when wide
+  bool ptab_rec = false;             // prefix-table entries are 32-B context records
+  uint32_t ptab_entry_bytes() const { return ptab_rec ? 32 : 8; }  // else 2 x u32 / packed wide
   uint64_t ptab_entries() const {
     if (!ptab_k) return 0;
     uint64_t e = 1;
@@ -102,6 +103,7 @@ struct cs_fm_index {
     d.ptab = d_ptab;
     d.ptab_k = ptab_k;
     d.ptab_sigma = ptab_sigma;
+    d.ptab_rec = ptab_rec ? 1u : 0u;
     d.isa = d_isa;
     d.nisa = nisa;
     d.pstride = pstride;
@@ -188,6 +190,7 @@ cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint
                          const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st);
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
 cs_status build_left_contexts(cs_fm_index* h, hipStream_t st);
+cs_status build_context_records(cs_fm_index* h, hipStream_t st);
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st);
 

@@ -10,7 +10,7 @@
 // Directory layout (all little-endian raw arrays, exactly the HBM images):
 //   cs_fmindex.meta  "key value" lines: format, n, stride, line_bytes, line_bits,
 //                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
-//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride, nlmodel, lmodel_shift,
+//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride, nlmodel, lmodel_shift, ptab_rec,
 //                    active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
@@ -119,14 +119,14 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
                 "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n"
                 "nlctx %llu\nlctx_q %u\nlctx_sb %u\nlctx_eb %u\npstride %u\nnlmodel %llu\n"
-                "lmodel_shift %u\n",
+                "lmodel_shift %u\nptab_rec %d\n",
                 kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                 (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                 (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
                 has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
                 (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0,
                 (unsigned long long)(h->d_lctx ? h->nlctx : 0), h->lctx_q, h->lctx_sb, h->lctx_eb,
-                h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift);
+                h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift, h->ptab_rec ? 1 : 0);
   std::string m(buf);
   for (int c = 0; c < 256; ++c) {
     std::snprintf(buf, sizeof buf, "active %d %u\n", c, h->active_levels[c]);
@@ -177,6 +177,7 @@ cs_status meta_parse(const std::string& text, cs_fm_index* h,
   h->pstride = kv["pstride"] ? (uint32_t)kv["pstride"] : h->stride;  // older images: the SSA's
   h->nlmodel = kv["nlmodel"];
   h->lmodel_shift = (uint32_t)kv["lmodel_shift"];
+  h->ptab_rec = kv["ptab_rec"] != 0;
   return CS_OK;
 }
 

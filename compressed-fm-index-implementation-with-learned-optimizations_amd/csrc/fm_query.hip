@@ -403,10 +403,12 @@ struct QWM {
 // (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
 // pattern's last k characters are all in its alphabet.  k receives the characters
 // still to process (P[k-1] .. P[0]).  Requires m >= 1.
+// With context records, *inl receives the entry's contexts (kRecCtx u16 in 6 dwords).
 __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable& T,
                                              const uint8_t* __restrict__ P, uint64_t m,
                                              uint64_t& sp, uint64_t& ep, uint64_t& k,
-                                             uint64_t* bytes) {
+                                             uint64_t* bytes, const uint32_t** inl = nullptr) {
+  if (inl) *inl = nullptr;
   if (ix.ptab_k && m >= ix.ptab_k) {
     uint32_t t = 0;
     bool ok = true;
@@ -416,7 +418,8 @@ __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable
       t = t * ix.ptab_sigma + d;
     }
     if (ok && ptab_at(ix, t, sp, ep)) {
-      if (bytes) *bytes += 8u;
+      if (bytes) *bytes += ix.ptab_rec ? 32u : 8u;
+      if (inl && ix.ptab_rec) *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 8 + 2;
       k = m - ix.ptab_k;
       return;
     }
@@ -456,11 +459,14 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
 // a character does not occur in the text (count 0, as the reference's step);
 // otherwise kCtxOk with bit i of `mm` set when row base + i matches.
 enum : uint32_t { kCtxNone = 0, kCtxAbsent = 1, kCtxOk = 2 };
+// inl: the contexts of a context record whose range [sp, ep) is at most kRecCtx rows
+// (already read with the record: no further access), else null.
 template <class Ent>
 __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTable& T,
                                               const uint8_t* __restrict__ P, uint32_t k,
                                               uint64_t sp, uint64_t ep, uint32_t& mm,
-                                              uint64_t& base, uint64_t* bytes) {
+                                              uint64_t& base, uint64_t* bytes,
+                                              const uint32_t* inl = nullptr) {
   constexpr uint32_t R = 32 / sizeof(Ent);
   constexpr bool kEsc = sizeof(Ent) == 2;
   const uint32_t sb = kEsc ? 2u : ix.lctx_sb;
@@ -474,19 +480,30 @@ __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTabl
   }
   const uint32_t kb = sb * k;
   const uint32_t mask = (kb >= 32 ? ~0u : ((1u << kb) - 1u)) | (kEsc ? kCtxEsc : 0u);
-  base = sp & ~(uint64_t)(R - 1);
-  const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);  // rows [lo, hi) of 2R
-  const uint4* p = reinterpret_cast<const uint4*>(static_cast<const Ent*>(ix.lctx) + base);
-  const bool two = hi > R;
-  if (bytes) *bytes += two ? 64u : 32u;
   uint4 w[4];
-  w[0] = p[0];
-  w[1] = p[1];
-  if (two) {
-    w[2] = p[2];
-    w[3] = p[3];
-  } else {
+  uint32_t lo, hi;  // rows [lo, hi) of the 2R from base
+  if (kEsc && inl) {
+    base = sp;
+    lo = 0;
+    hi = (uint32_t)(ep - sp);
+    w[0] = make_uint4(inl[0], inl[1], inl[2], inl[3]);
+    w[1] = make_uint4(inl[4], inl[5], 0, 0);
     w[2] = w[3] = make_uint4(0, 0, 0, 0);
+  } else {
+    base = sp & ~(uint64_t)(R - 1);
+    lo = (uint32_t)(sp - base);
+    hi = (uint32_t)(ep - base);
+    const uint4* p = reinterpret_cast<const uint4*>(static_cast<const Ent*>(ix.lctx) + base);
+    const bool two = hi > R;
+    if (bytes) *bytes += two ? 64u : 32u;
+    w[0] = p[0];
+    w[1] = p[1];
+    if (two) {
+      w[2] = p[2];
+      w[3] = p[3];
+    } else {
+      w[2] = w[3] = make_uint4(0, 0, 0, 0);
+    }
   }
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(w);
   uint32_t match = 0, esc = 0;  // bit i: row base + i
@@ -506,10 +523,10 @@ template <class Ent>
 __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
                                           const uint8_t* __restrict__ P, uint32_t k,
                                           uint64_t sp, uint64_t ep, uint64_t& cnt,
-                                          uint64_t* bytes) {
+                                          uint64_t* bytes, const uint32_t* inl = nullptr) {
   uint32_t mm = 0;
   uint64_t base;
-  const uint32_t r = ctx_match<Ent>(ix, T, P, k, sp, ep, mm, base, bytes);
+  const uint32_t r = ctx_match<Ent>(ix, T, P, k, sp, ep, mm, base, bytes, inl);
   if (r == kCtxNone) return false;
   cnt = r == kCtxOk ? (uint64_t)__popc(mm) : 0;
   return true;
@@ -523,16 +540,19 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
                                                   const uint8_t* __restrict__ P, uint64_t m,
                                                   uint64_t* bytes = nullptr) {
   uint64_t sp, ep, k;
-  search_start(ix, T, P, m, sp, ep, k, bytes);
+  const uint32_t* inl;
+  search_start(ix, T, P, m, sp, ep, k, bytes, &inl);
   if (sp >= ep) return 0;
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
   bool ctx = E::kCtx && ix.lctx != nullptr;
   while (k > 0) {
-    if (ctx && k <= ix.lctx_q && ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R) {
+    if (inl && ep - sp > kRecCtx) inl = nullptr;
+    if (ctx && k <= ix.lctx_q && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
       uint64_t cnt;
-      if (ctx_count<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes)) return cnt;
+      if (ctx_count<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes, inl)) return cnt;
       ctx = false;
     }
+    inl = nullptr;
     --k;
     if (!E::step(ix, T, P[k], sp, ep, bytes)) return 0;
   }
@@ -558,17 +578,19 @@ __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const Node
                                                   const uint8_t* __restrict__ P, uint64_t m,
                                                   uint64_t& rec) {
   uint64_t sp, ep, k;
+  const uint32_t* inl;
   rec = 0;
-  search_start(ix, T, P, m, sp, ep, k, nullptr);
+  search_start(ix, T, P, m, sp, ep, k, nullptr, &inl);
   if (sp >= ep) return 0;
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);
   bool ctx = E::kCtx && ix.lctx != nullptr && ix.lf_exact;
   while (k > 0) {
-    if (ctx && k <= ix.lctx_q && k <= 7 && ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R) {
+    if (inl && ep - sp > kRecCtx) inl = nullptr;
+    if (ctx && k <= ix.lctx_q && k <= 7 && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
       uint32_t mm = 0;
       uint64_t base;
       const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, mm, base,
-                                                       nullptr);
+                                                       nullptr, inl);
       if (r == kCtxAbsent || (r == kCtxOk && mm == 0)) return 0;
       if (r == kCtxOk) {
         const uint32_t f = (uint32_t)__ffs(mm) - 1u;
@@ -580,6 +602,7 @@ __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const Node
       }
       ctx = false;
     }
+    inl = nullptr;
     --k;
     if (!E::step(ix, T, P[k], sp, ep, nullptr)) return 0;
   }
@@ -751,14 +774,27 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     want[j] = ww;
     k[j] = kk;
   }
-  // (B)
-#pragma unroll
-  for (int j = 0; j < U; ++j)
-    if ((st[j] == 1 || st[j] == 2) && !ptab_at(ix, t[j], sp[j], ep[j])) st[j] = 3;
-  // (C)
+  // (B) the table entries (whole context records: their contexts come with them)
   uint4 w[U][4];
 #pragma unroll
   for (int j = 0; j < U; ++j) {
+    if (st[j] != 1 && st[j] != 2) continue;
+    if (ix.ptab_rec) {
+      const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t[j] * 2;
+      const uint4 a = r[0], b = r[1];
+      sp[j] = a.x;
+      ep[j] = (uint64_t)a.x + a.y;
+      w[j][0] = make_uint4(a.z, a.w, b.x, b.y);
+      w[j][1] = make_uint4(b.z, b.w, 0u, 0u);
+    } else if (!ptab_at(ix, t[j], sp[j], ep[j])) {
+      st[j] = 3;
+    }
+  }
+  // (C) the context sector(s), unless the record holds the range's contexts
+  uint64_t bs[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    bs[j] = 0;
     if (st[j] != 1 && st[j] != 2) continue;
     if (sp[j] >= ep[j]) {
       st[j] = 0;
@@ -767,9 +803,13 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
       st[j] = 0;
       res[j] = ep[j] - sp[j];
       rv[j] = sp[j];
+    } else if (st[j] == 2 && ix.ptab_rec && ep[j] - sp[j] <= kRecCtx) {
+      bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record
+      w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
     } else if (st[j] == 2 && ep[j] - (sp[j] & ~15ull) <= 32) {
+      bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
-                                                      (sp[j] & ~15ull));
+                                                      bs[j]);
       w[j][0] = p[0];
       w[j][1] = p[1];
       if (ep[j] - (sp[j] & ~15ull) > 16) {
@@ -787,7 +827,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   for (int j = 0; j < U; ++j) {
     if (st[j] == 2) {
       const uint32_t mask = ((1u << (2 * k[j])) - 1u) | kCtxEsc;
-      const uint64_t base = sp[j] & ~15ull;
+      const uint64_t base = bs[j];
       const uint32_t lo = (uint32_t)(sp[j] - base), hi = (uint32_t)(ep[j] - base);
       const uint32_t* dw = reinterpret_cast<const uint32_t*>(w[j]);
       uint32_t match = 0, esc = 0;
@@ -1464,6 +1504,53 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
         ix, static_cast<uint32_t*>(h->d_lctx));
   FMX_HIP(hipGetLastError());
   FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
+// Context records (fm_device.hpp kRecCtx) from the 8-B table and the left contexts:
+// one lane per k-mer.
+__global__ __launch_bounds__(kBlk) void k_fill_records(const uint2* __restrict__ tab,
+                                                       uint64_t entries,
+                                                       const uint16_t* __restrict__ lctx,
+                                                       uint32_t* __restrict__ rec) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
+    const uint2 e = tab[t];
+    const uint32_t w = e.y - e.x;
+    uint32_t d[6] = {0, 0, 0, 0, 0, 0};
+    for (uint32_t i = 0; i < kRecCtx && i < w; ++i) d[i >> 1] |= (uint32_t)lctx[e.x + i] << (16 * (i & 1));
+    uint4* r = reinterpret_cast<uint4*>(rec) + t * 2;
+    r[0] = make_uint4(e.x, w, d[0], d[1]);
+    r[1] = make_uint4(d[2], d[3], d[4], d[5]);
+  }
+}
+
+// Replace the 8-B prefix table by 32-B context records (narrow occurrence-engine
+// indexes with left contexts; C4: 34 GB for k = 15) when HBM allows (an eighth of the
+// device stays free); CS_FM_CTX_RECORDS=0 keeps the plain table.
+cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
+  h->ptab_rec = false;
+  if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide || h->lctx_eb != 2) return CS_OK;
+  if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
+    if (std::atoi(e) == 0) return CS_OK;
+  const uint64_t entries = h->ptab_entries();
+  size_t free_b = 0, total_b = 0;
+  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (entries * 32 + total_b / 8 > free_b) return CS_OK;
+  void* rec = nullptr;
+  FMX_HIP(hipMalloc(&rec, entries * 32));
+  k_fill_records<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
+      static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
+      static_cast<uint32_t*>(rec));
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    (void)hipFree(rec);
+    return hip_fail(e, "context records");
+  }
+  FMX_HIP(hipFree(h->d_ptab));
+  h->d_ptab = rec;
+  h->ptab_rec = true;
   return CS_OK;
 }
 
