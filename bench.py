@@ -234,6 +234,8 @@ def main():
         wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
         if info.context_q:
             wl += ":ctx%d" % info.context_q
+        if K and info.prefix_bytes == 32 * info.prefix_sigma ** K:
+            wl += ":rec"  # context records (32-B prefix-table entries)
         if args.queries != "text":
             wl += ":" + args.queries
         if os.path.exists(prof):
@@ -262,9 +264,11 @@ def main():
                        "collective": "gather of counts to rank 0 (%s), overlapped"
                        % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) if coll
                        else "none (independent query shards)",
-                       "engine": ("%s + left contexts (q=%d)" % (
+                       "engine": ("%s + left contexts (q=%d)%s" % (
                                   "learned occurrence lines" if info.engine == 3 else "occurrence lines",
-                                  info.context_q)) if info.engine in (1, 3) else
+                                  info.context_q,
+                                  " + context records" if K and info.prefix_bytes == 32 * info.prefix_sigma ** K
+                                  else "")) if info.engine in (1, 3) else
                        "quaternary wavelet matrix (%d levels of occurrence lines)" % info.levels
                        if info.engine == 2 else
                        "wavelet matrix (%d-B rank lines)" % info.line_bytes},
