@@ -1527,12 +1527,17 @@ __global__ __launch_bounds__(kBlk) void k_fill_records(const uint2* __restrict__
 
 // Replace the 8-B prefix table by 32-B context records (narrow occurrence-engine
 // indexes with left contexts; C4: 34 GB for k = 15) when HBM allows (an eighth of the
-// device stays free); CS_FM_CTX_RECORDS=0 keeps the plain table.
+// device stays free) and the table spans at least 14 characters: records pay for
+// patterns of k+1 .. k+7 characters (the 20-mers of the DNA configs from k = 13 on)
+// and cost 4x the plain table's reads in bytes otherwise (C2, k = 12: 7.9e9 patterns/s
+// with records, 9.1e9 without).  CS_FM_CTX_RECORDS=0 keeps the plain table, =1 forces
+// records for any k (test hook).
 cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   h->ptab_rec = false;
   if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide || h->lctx_eb != 2) return CS_OK;
-  if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
-    if (std::atoi(e) == 0) return CS_OK;
+  bool want = h->ptab_k >= 14;
+  if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) want = std::atoi(e) != 0;
+  if (!want) return CS_OK;
   const uint64_t entries = h->ptab_entries();
   size_t free_b = 0, total_b = 0;
   FMX_HIP(hipMemGetInfo(&free_b, &total_b));

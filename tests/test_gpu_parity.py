@@ -29,7 +29,7 @@ ENGINE_VARIANTS = {
     "auto_rowmarks": {"CS_FM_WALK_MARKS": "row"},   # walk lines with the reference's row samples
     "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
-    "auto_norec": {"CS_FM_CTX_RECORDS": "0"},       # 8-B prefix table (no context records)
+    "auto_rec": {"CS_FM_CTX_RECORDS": "1"},         # context records at any table depth
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
     "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
