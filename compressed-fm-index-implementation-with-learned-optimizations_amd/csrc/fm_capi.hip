@@ -75,30 +75,51 @@ cs_status scratch_ready(const cs_fm_index* h) {
 }
 
 // Page-locks a large caller buffer for the duration of a call, so its copies run as
-// DMA at PCIe rate instead of through the runtime's pageable staging; small buffers
-// and buffers that cannot be registered (e.g. already pinned) are left alone.
+// DMA at PCIe rate instead of through the runtime's pageable staging.  Only the pages
+// lying wholly inside the buffer are registered: a neighbouring allocation sharing the
+// first or last page is never covered (the runtime would then take a copy to or from
+// that neighbour for pinned memory and reject it).  copy() moves the buffer as head
+// (pageable), registered body and tail (pageable).  Small buffers and buffers that
+// cannot be registered (e.g. already pinned) are left alone.
 struct HostPin {
   static constexpr uint64_t kMinBytes = 16ull << 20;
-  void* base = nullptr;
+  uintptr_t a = 0, e = 0;  // registered pages [a, e)
   hipStream_t st = nullptr;
   HostPin() = default;
   HostPin(const HostPin&) = delete;
   HostPin& operator=(const HostPin&) = delete;
   void pin(const void* p, uint64_t bytes, hipStream_t s) {
-    if (bytes < kMinBytes || base) return;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095);
-    const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes + 4095) & ~uintptr_t(4095);
-    if (hipHostRegister(reinterpret_cast<void*>(a), e - a, hipHostRegisterDefault) == hipSuccess) {
-      base = reinterpret_cast<void*>(a);
+    if (bytes < kMinBytes || a) return;
+    const uintptr_t lo = (reinterpret_cast<uintptr_t>(p) + 4095) & ~uintptr_t(4095);
+    const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes) & ~uintptr_t(4095);
+    if (hi <= lo) return;
+    if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault) == hipSuccess) {
+      a = lo;
+      e = hi;
       st = s;
     } else {
       (void)hipGetLastError();
     }
   }
+  // host <-> device copy of the pinned buffer `host` (bytes), split at the registered pages
+  hipError_t copy(void* dst, const void* src, uint64_t bytes, bool h2d, hipStream_t s) const {
+    const uintptr_t h = reinterpret_cast<uintptr_t>(h2d ? src : dst);
+    const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+    if (!a || a < h || e > h + bytes) return hipMemcpyAsync(dst, src, bytes, kind, s);
+    const uint64_t cut[4] = {0, a - h, e - h, bytes};
+    for (int i = 0; i < 3; ++i) {
+      const uint64_t n = cut[i + 1] - cut[i];
+      if (!n) continue;
+      hipError_t r = hipMemcpyAsync(static_cast<uint8_t*>(dst) + cut[i],
+                                    static_cast<const uint8_t*>(src) + cut[i], n, kind, s);
+      if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+  }
   ~HostPin() {
-    if (!base) return;
+    if (!a) return;
     (void)hipStreamSynchronize(st);  // no copy may still read the pages
-    (void)hipHostUnregister(base);
+    (void)hipHostUnregister(reinterpret_cast<void*>(a));
   }
 };
 
@@ -111,10 +132,10 @@ struct StagedBatch {
     FMX_HIP(pats.alloc(bytes + 16, st));
     FMX_HIP(offs.alloc((npat + 1) * 8, st));
     pin_pats.pin(p + o[0], bytes, st);
-    if (bytes) FMX_HIP(hipMemcpyAsync(pats.p, p + o[0], bytes, hipMemcpyHostToDevice, st));
+    if (bytes) FMX_HIP(pin_pats.copy(pats.p, p + o[0], bytes, true, st));
     if (o[0] == 0) {
       pin_offs.pin(o, (npat + 1) * 8, st);
-      FMX_HIP(hipMemcpyAsync(offs.p, o, (npat + 1) * 8, hipMemcpyHostToDevice, st));
+      FMX_HIP(pin_offs.copy(offs.p, o, (npat + 1) * 8, true, st));
     } else {  // rebase so offsets index the staged bytes
       std::vector<uint64_t> r(npat + 1);
       for (uint64_t q = 0; q <= npat; ++q) r[q] = o[q] - o[0];
@@ -472,7 +493,7 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   pin_out.pin(out_counts, npat * 8, st);
   s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
   if (s != CS_OK) return s;
-  FMX_HIP(hipMemcpyAsync(out_counts, d_out.p, npat * 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(pin_out.copy(out_counts, d_out.p, npat * 8, false, st));
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
 }

@@ -715,14 +715,14 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
                                                     uint64_t npat, uint64_t* __restrict__ out,
                                                     uint64_t limit, uint64_t* __restrict__ rec) {
   // the stages need only the symbol -> (table digit, occurrence code) map in LDS (512 B
-  // instead of the 10.8-KB node table: a shorter block prologue); the general search
-  // of the few remaining patterns reads the node table through the caches
+  // instead of the 10.8-KB node table: a shorter block prologue); a block stages the
+  // node table only when one of its patterns needs the general search
   __shared__ uint16_t cmap[256];
+  __shared__ NodeTable T;
   static_assert(kBlk >= 256, "one map entry per thread");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   __syncthreads();
-  const NodeTable& T = *ix.table;
   const uint32_t K = ix.ptab_k;
   const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
@@ -867,6 +867,12 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     }
   }
   // the general search for the rest, with only (o0, m) of each pattern still live
+  bool general = false;
+#pragma unroll
+  for (int j = 0; j < U; ++j) general |= st[j] == 3;
+  if (!__syncthreads_or(general)) return;
+  load_table(T, ix.table);
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     if (st[j] != 3) continue;

@@ -128,3 +128,24 @@ def test_export_import_image(engine, monkeypatch):
     lo2, lp2 = c.locate_batch(pats, limit=9)
     assert lo1.tolist() == lo2.tolist() and lp1.tolist() == lp2.tolist()
     assert c.extract_batch([0, 100, len(t) - 3], [10, 25, 10]) == [t[0:10], t[100:125], t[-3:]]
+
+
+def test_host_batch_buffers_sharing_pages():
+    """A large host batch whose pattern bytes and counts live in one caller arena (the
+    counts start inside the patterns' last page): the pinned-copy path registers only
+    whole inner pages, so neither copy is mistaken for pinned memory of the other."""
+    pkg = load_pkg()
+    t = O.gen_dna(5, 200_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 20, 1_000_000, seed=9)
+    npat = len(P)
+    pb = npat * 20  # 20 MB, not a multiple of the page size
+    start = (pb + 7) // 8 * 8
+    arena = np.zeros(start + 8 * npat, np.uint8)
+    arena[:pb] = P.reshape(-1)
+    out = arena[start:].view(np.uint64)
+    offs = np.arange(0, (npat + 1) * 20, 20, dtype=np.uint64)
+    st = pkg.lib().cs_fm_count_batch(g._h, pkg._u8(arena), pkg._u64(offs), npat, pkg._u64(out), None)
+    assert st == 0, pkg.lib().cs_fm_last_error()
+    assert np.array_equal(out, g.count_batch(buf=P.reshape(-1), offs=offs))
+    assert (out >= 1).all()
