@@ -296,6 +296,13 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     FMX_HIP(hipStreamSynchronize(st));
   }
 
+  if (n) {  // unique smallest last symbol: LF is one n-cycle, suffix order = rotation order
+    uint8_t last = 0;
+    FMX_HIP(hipMemcpy(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost));
+    int smallest = 0;
+    while (smallest < 256 && hist[smallest] == 0) ++smallest;
+    h->lf_exact = hist[last] == 1 && last == smallest;
+  }
   PhaseLog plog(st);
   plog.mark("histogram");
   // --- SA, BWT, SSA ---
@@ -327,16 +334,20 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
           static_cast<uint32_t*>(h->d_ssa), static_cast<uint32_t*>(h->d_isa));
     FMX_HIP(hipGetLastError());
     FMX_HIP(hipStreamSynchronize(st));
+    // Keep the full suffix array (as the reference keeps sa_, fm_index.hpp:43) when LF is
+    // one n-cycle: a located row's position is then SA[row] (what the reference's SSA
+    // walk computes, fm_index.cpp:125-153), one read instead of a walk.  4n bytes (C4:
+    // 16 GB), an eighth of the device left free; CS_FM_FULL_SA=0 keeps only the samples.
+    bool keep = h->lf_exact;
+    if (const char* e = std::getenv("CS_FM_FULL_SA")) keep = keep && std::atoi(e) != 0;
+    size_t free_b = 0, total_b = 0;
+    if (keep && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > total_b / 8 + n * 8) {
+      h->d_sa = sa.p;  // the handle owns it from here
+      sa.p = nullptr;
+    }
   }
   plog.mark("suffix array + bwt + ssa");
 
-  if (n) {  // unique smallest last symbol: LF is one n-cycle, suffix order = rotation order
-    uint8_t last = 0;
-    FMX_HIP(hipMemcpy(&last, d_text + n - 1, 1, hipMemcpyDeviceToHost));
-    int smallest = 0;
-    while (smallest < 256 && hist[smallest] == 0) ++smallest;
-    h->lf_exact = hist[last] == 1 && last == smallest;
-  }
   return finish_index(bwt, hist, h, st, plog);
 }
 

@@ -238,6 +238,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_err) (void)hipFree(h->d_err);
   if (h->d_ptab) (void)hipFree(h->d_ptab);
   if (h->d_isa) (void)hipFree(h->d_isa);
+  if (h->d_sa) (void)hipFree(h->d_sa);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
   if (h->d_lctx) (void)hipFree(h->d_lctx);
@@ -386,6 +387,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->context_q = h->d_lctx ? h->lctx_q : 0u;
   out->context_bytes = h->d_lctx ? h->nlctx * h->lctx_eb : 0u;
   out->position_stride = h->pstride;
+  out->full_sa_bytes = h->d_sa ? h->n * 4 : 0u;
   return CS_OK;
 }
 

@@ -27,6 +27,7 @@ struct cs_fm_index {
   fmx::NodeTable h_table{};
   uint64_t* d_err = nullptr;          // locate: min failing item (UINT64_MAX = none)
   void* d_ptab = nullptr;             // prefix table (DevIndex::ptab)
+  void* d_sa = nullptr;               // full suffix array, u32 (lf_exact prefix-doubling builds)
   void* d_isa = nullptr;              // inverse-SA samples (extract, walk-line marks)
   uint64_t nisa = 0;
   uint32_t pstride = 32;              // their text-position stride (position_stride())

@@ -1658,6 +1658,19 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
   return CS_OK;
 }
 
+// Positions of the reported rows from the full suffix array (lf_exact): SA[row] - k
+// (mod n) for a window row tagged with k (locate records), SA[row] otherwise.
+__global__ __launch_bounds__(kBlk) void k_sa_gather(const uint32_t* __restrict__ sa, uint64_t n,
+                                                    const uint64_t* __restrict__ rows,
+                                                    uint64_t total, uint64_t* __restrict__ out) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < total; j += gs) {
+    const uint64_t row = rows[j];
+    const uint64_t s = sa[row & kWalkRowMask], adj = row >> kWalkAdjShift;
+    out[j] = s >= adj ? s - adj : s + n - adj;
+  }
+}
+
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word) {
@@ -1679,6 +1692,12 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
       err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
+  if (h->d_sa && h->lf_exact) {  // full suffix array: one read per position
+    k_sa_gather<<<grid_for(total, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        static_cast<const uint32_t*>(h->d_sa), h->n, r, total, d_out_pos);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
   static const bool persistent = [] {  // tuning hook: CS_FM_WALK_PERSISTENT=1
     const char* e = std::getenv("CS_FM_WALK_PERSISTENT");
     return e && std::atoi(e) == 1;

@@ -82,6 +82,7 @@ typedef struct cs_fm_info {
   uint32_t position_stride; /* text-position samples (extract, locate walk marks) every
                               position_stride positions; the SSA keeps ssa_stride */
   uint64_t context_bytes;
+  uint64_t full_sa_bytes;  /* full suffix array kept for locate (lf_exact builds), 0 = none */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -30,6 +30,7 @@ ENGINE_VARIANTS = {
     "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "auto_rec": {"CS_FM_CTX_RECORDS": "1"},         # context records at any table depth
+    "auto_nosa": {"CS_FM_FULL_SA": "0"},            # locate walks (no full suffix array kept)
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
     "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
@@ -46,7 +47,7 @@ ENGINE_VARIANTS = {
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
           "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
           "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT", "CS_FM_PTAB_WMAX",
-          "CS_FM_CTX_RECORDS")
+          "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -199,6 +200,9 @@ def test_engine_choice(built):
             ctx = 0
         assert info.context_q == ctx, name
         wide = os.environ.get("CS_FM_WIDE") == "1"
+        full_sa = (cyc and os.environ.get("CS_FM_FULL_SA") != "0"
+                   and os.environ.get("CS_FM_SA_BUILDER") != "bucketed")
+        assert info.full_sa_bytes == (4 * info.n if full_sa else 0), name
         assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or
                                         (16 if wide else 4)), name
         assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
