@@ -747,6 +747,12 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
 // reference's row marks (row % stride == 0) keep its overrun behaviour.
 cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_index* h,
                      hipStream_t st) {
+  // with the full suffix array kept (lf_exact), locate reads SA[row] and never walks:
+  // no walk lines (C4: 3 GB + 4 GB of position samples saved)
+  if (h->d_sa && h->lf_exact && !std::getenv("CS_FM_WALK_MARKS")) {
+    h->walk_marks = 0;
+    return CS_OK;
+  }
   bool pos_marks = h->lf_exact && h->d_isa && h->nisa == (n + h->pstride - 1) / h->pstride;
   if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
     if (std::string(e) == "row") pos_marks = false;

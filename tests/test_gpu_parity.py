@@ -26,8 +26,8 @@ ENGINE_VARIANTS = {
     # the wavelet matrix in 32-B lines (Line32)
     "auto": {},
     "auto_noprefix": {"CS_FM_PREFIX_K": "0"},       # prefix table off
-    "auto_rowmarks": {"CS_FM_WALK_MARKS": "row"},   # walk lines with the reference's row samples
-    "auto_nowalk": {"CS_FM_WALK": "0"},             # locate walks the occurrence lines
+    "auto_rowmarks": {"CS_FM_WALK_MARKS": "row", "CS_FM_FULL_SA": "0"},  # walks over row-marked walk lines
+    "auto_nowalk": {"CS_FM_WALK": "0", "CS_FM_FULL_SA": "0"},  # locate walks the occurrence lines
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "auto_rec": {"CS_FM_CTX_RECORDS": "1"},         # context records at any table depth
     "auto_nosa": {"CS_FM_FULL_SA": "0"},            # locate walks (no full suffix array kept)
@@ -186,10 +186,14 @@ def test_engine_choice(built):
         elif forced == "learned" and engine == 1:
             engine = 3
         marks = 0 if engine == 0 else (2 if cyc else 1)
+        full_sa = (cyc and os.environ.get("CS_FM_FULL_SA") != "0"
+                   and os.environ.get("CS_FM_SA_BUILDER") != "bucketed")
         if os.environ.get("CS_FM_WALK") == "0":
             marks = 0
         elif os.environ.get("CS_FM_WALK_MARKS") == "row" and marks:
             marks = 1
+        elif full_sa:  # locate reads the full suffix array: no walk lines
+            marks = 0
         assert (info.engine, info.rare_rows, info.walk_marks) == (engine, rare, marks), name
         want_levels = {0: 8, 1: 1, 2: levels[name], 3: 1}[engine]
         assert info.levels == want_levels and info.line_bytes in (32, 64), name
@@ -200,8 +204,6 @@ def test_engine_choice(built):
             ctx = 0
         assert info.context_q == ctx, name
         wide = os.environ.get("CS_FM_WIDE") == "1"
-        full_sa = (cyc and os.environ.get("CS_FM_FULL_SA") != "0"
-                   and os.environ.get("CS_FM_SA_BUILDER") != "bucketed")
         assert info.full_sa_bytes == (4 * info.n if full_sa else 0), name
         assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or
                                         (16 if wide else 4)), name
