@@ -83,10 +83,22 @@ def _kmer_checksum(idx, alphabet, k, N):
 
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C4") == "1", reason="C4 disabled")
-def test_c4_dna_4gb():
+@pytest.mark.parametrize("variant", ["auto", "plain_walk", "learned"])
+def test_c4_dna_4gb(variant, monkeypatch):
+    """BASELINE configs[3] at full size: the default index (context records, left
+    contexts, full suffix array), the same without records and full SA (8-B table,
+    context sectors, locate by walk lines), and the learned occurrence lines."""
+    if variant == "plain_walk":
+        monkeypatch.setenv("CS_FM_CTX_RECORDS", "0")
+        monkeypatch.setenv("CS_FM_FULL_SA", "0")
+    elif variant == "learned":
+        monkeypatch.setenv("CS_FM_ENGINE", "learned")
     pkg = load_pkg()
     idx, text, host, N = _build(pkg, "dna", 3_999_999_999)
     assert N == 4_000_000_000
+    info = idx.info()
+    assert (info.full_sa_bytes > 0) == (variant != "plain_walk")
+    assert (info.prefix_bytes == 32 * 4 ** info.prefix_k) == (variant != "plain_walk")
     P = _qtext(pkg, text, N, 20, 200_000)
     _check_qtext(idx, host, N, P, nloc=20_000)
     ones = idx.count_batch([bytes([c]) for c in range(256)])
