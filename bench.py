@@ -234,8 +234,8 @@ def main():
         wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
         if info.context_q:
             wl += ":ctx%d" % info.context_q
-        if K and info.prefix_bytes == 32 * info.prefix_sigma ** K:
-            wl += ":rec"  # context records (32-B prefix-table entries)
+        if info.record_bytes:
+            wl += ":rec%d" % info.record_bytes  # context records (32-/16-B prefix-table entries)
         if args.queries != "text":
             wl += ":" + args.queries
         if os.path.exists(prof):
@@ -267,7 +267,7 @@ def main():
                        "engine": ("%s + left contexts (q=%d)%s" % (
                                   "learned occurrence lines" if info.engine == 3 else "occurrence lines",
                                   info.context_q,
-                                  " + context records" if K and info.prefix_bytes == 32 * info.prefix_sigma ** K
+                                  " + %d-B context records" % info.record_bytes if info.record_bytes
                                   else "")) if info.engine in (1, 3) else
                        "quaternary wavelet matrix (%d levels of occurrence lines)" % info.levels
                        if info.engine == 2 else

@@ -388,6 +388,8 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->context_bytes = h->d_lctx ? h->nlctx * h->lctx_eb : 0u;
   out->position_stride = h->pstride;
   out->full_sa_bytes = h->d_sa ? h->n * 4 : 0u;
+  out->record_bytes = h->ptab_rec ? h->ptab_entry_bytes() : 0u;
+  out->reserved0 = 0;
   return CS_OK;
 }
 

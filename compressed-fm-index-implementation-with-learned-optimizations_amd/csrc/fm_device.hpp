@@ -99,7 +99,7 @@ struct DevIndex {
   const void* ptab;
   uint32_t ptab_k;
   uint32_t ptab_sigma;
-  uint32_t ptab_rec;     // entries are 32-B context records (kRecCtx below)
+  uint32_t ptab_rec;     // 1: entries are 32-B context records, 2: 16-B ones (kRecCtx below)
   // Inverse-SA samples: isa[k] = row of the suffix at text position k*stride, for
   // extract by LF inversion (needs suffix order == rotation order, i.e. a unique
   // smallest last symbol: lf_exact).
@@ -166,12 +166,41 @@ constexpr uint64_t kPtabEsc = (1ull << 26) - 1;
 // kRecCtx rows — so a search whose range after the table is at most kRecCtx rows
 // wide and has at most kCtxQ characters left is answered by the ONE random read of its
 // table entry (the contexts are the rows' lctx entries, fm_device.hpp kCtxQ).
+// Compact records (ptab_rec 2, tables whose mean range is at most 4 rows) are 16 B —
+// half the table, and 16-B random reads run faster than 32-B ones over a multi-GB table
+// (DESIGN.md §2): dword 0 sp; dword 1 bits 0-3 the width w when w <= kRec16Ctx, else
+// kRec16Wide (the width is then dword 2, no contexts: also used when a row of the range
+// has an escaped context); contexts of kRec16Q characters (10 bits, the low bits of the
+// rows' lctx entries) of rows 0-5 at bits 4 + 10i of dwords 1-2, rows 6-8 at bits
+// 10(i-6) of dword 3.
 constexpr uint32_t kRecCtx = 12;
+constexpr uint32_t kRec16Ctx = 9;
+constexpr uint32_t kRec16Q = 5;
+constexpr uint32_t kRec16Wide = 15;
+// the rows' contexts of a compact record, as u16 entries in dw[0..4] (dw[4] bits 0-15)
+__device__ __forceinline__ void rec16_contexts(uint32_t y, uint32_t z, uint32_t w, uint32_t dw[5]) {
+  const uint64_t lo = (uint64_t)y | ((uint64_t)z << 32);
+  uint32_t e[10];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) e[i] = (uint32_t)(lo >> (4 + 10 * i)) & 0x3FFu;
+#pragma unroll
+  for (int i = 6; i < 9; ++i) e[i] = (w >> (10 * (i - 6))) & 0x3FFu;
+  e[9] = 0;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dw[i] = e[2 * i] | (e[2 * i + 1] << 16);
+}
 __device__ __forceinline__ bool ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
-  if (ix.ptab_rec) {
+  if (ix.ptab_rec == 1) {
     const uint2 r = static_cast<const uint2*>(ix.ptab)[t * 4];
     sp = r.x;
     ep = (uint64_t)r.x + r.y;
+    return true;
+  }
+  if (ix.ptab_rec == 2) {
+    const uint4 r = static_cast<const uint4*>(ix.ptab)[t];
+    const uint32_t wc = r.y & 15u;
+    sp = r.x;
+    ep = (uint64_t)r.x + (wc == kRec16Wide ? r.z : wc);
     return true;
   }
   if (ix.wide) {

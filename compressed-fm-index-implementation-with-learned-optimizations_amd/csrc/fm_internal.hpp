@@ -76,8 +76,8 @@ struct cs_fm_index {
   mutable Server server;
 
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
-  bool ptab_rec = false;             // prefix-table entries are 32-B context records
-  uint32_t ptab_entry_bytes() const { return ptab_rec ? 32 : 8; }  // else 2 x u32 / packed wide
+  uint32_t ptab_rec = 0;             // prefix-table entries: 0 plain, 1 32-B / 2 16-B context records
+  uint32_t ptab_entry_bytes() const { return ptab_rec == 1 ? 32 : ptab_rec == 2 ? 16 : 8; }  // plain: 2 x u32 / packed wide
   uint64_t ptab_entries() const {
     if (!ptab_k) return 0;
     uint64_t e = 1;
@@ -104,7 +104,7 @@ struct cs_fm_index {
     d.ptab = d_ptab;
     d.ptab_k = ptab_k;
     d.ptab_sigma = ptab_sigma;
-    d.ptab_rec = ptab_rec ? 1u : 0u;
+    d.ptab_rec = ptab_rec;
     d.isa = d_isa;
     d.nisa = nisa;
     d.pstride = pstride;

@@ -128,7 +128,7 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 has_text ? 1 : 0, h->wide ? 1 : 0, h->line_fmt, h->nlevels,
                 (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0,
                 (unsigned long long)(h->d_lctx ? h->nlctx : 0), h->lctx_q, h->lctx_sb, h->lctx_eb,
-                h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift, h->ptab_rec ? 1 : 0,
+                h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift, (int)h->ptab_rec,
                 h->d_sa ? 1 : 0);
   std::string m(buf);
   for (int c = 0; c < 256; ++c) {
@@ -180,7 +180,11 @@ cs_status meta_parse(const std::string& text, cs_fm_index* h,
   h->pstride = kv["pstride"] ? (uint32_t)kv["pstride"] : h->stride;  // older images: the SSA's
   h->nlmodel = kv["nlmodel"];
   h->lmodel_shift = (uint32_t)kv["lmodel_shift"];
-  h->ptab_rec = kv["ptab_rec"] != 0;
+  h->ptab_rec = (uint32_t)kv["ptab_rec"];
+  if (h->ptab_rec > 2) {
+    set_error("bad ptab_rec in " + what);
+    return CS_ERR_INVALID;
+  }
   return CS_OK;
 }
 

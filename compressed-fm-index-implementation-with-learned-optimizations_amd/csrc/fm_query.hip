@@ -403,7 +403,8 @@ struct QWM {
 // (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
 // pattern's last k characters are all in its alphabet.  k receives the characters
 // still to process (P[k-1] .. P[0]).  Requires m >= 1.
-// With context records, *inl receives the entry's contexts (kRecCtx u16 in 6 dwords).
+// With context records, *inl receives the entry's contexts (kRecCtx u16 in 6 dwords),
+// or the compact record itself (fm_device.hpp kRec16Ctx) when it holds contexts.
 __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable& T,
                                              const uint8_t* __restrict__ P, uint64_t m,
                                              uint64_t& sp, uint64_t& ep, uint64_t& k,
@@ -418,8 +419,12 @@ __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable
       t = t * ix.ptab_sigma + d;
     }
     if (ok && ptab_at(ix, t, sp, ep)) {
-      if (bytes) *bytes += ix.ptab_rec ? 32u : 8u;
-      if (inl && ix.ptab_rec) *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 8 + 2;
+      if (bytes) *bytes += ix.ptab_rec == 1 ? 32u : ix.ptab_rec == 2 ? 16u : 8u;
+      if (inl && ix.ptab_rec == 1) *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 8 + 2;
+      if (inl && ix.ptab_rec == 2) {
+        const uint32_t* r = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4;
+        if ((r[1] & 15u) != kRec16Wide) *inl = r;
+      }
       k = m - ix.ptab_k;
       return;
     }
@@ -459,6 +464,10 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
 // a character does not occur in the text (count 0, as the reference's step);
 // otherwise kCtxOk with bit i of `mm` set when row base + i matches.
 enum : uint32_t { kCtxNone = 0, kCtxAbsent = 1, kCtxOk = 2 };
+// whether a record's inline contexts answer k characters over a w-row range
+__device__ __forceinline__ bool rec_inline(const DevIndex& ix, uint64_t k, uint64_t w) {
+  return ix.ptab_rec == 2 ? k <= kRec16Q : w <= kRecCtx;
+}
 // inl: the contexts of a context record whose range [sp, ep) is at most kRecCtx rows
 // (already read with the record: no further access), else null.
 template <class Ent>
@@ -486,8 +495,15 @@ __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTabl
     base = sp;
     lo = 0;
     hi = (uint32_t)(ep - sp);
-    w[0] = make_uint4(inl[0], inl[1], inl[2], inl[3]);
-    w[1] = make_uint4(inl[4], inl[5], 0, 0);
+    if (ix.ptab_rec == 2) {
+      uint32_t d[5];
+      rec16_contexts(inl[1], inl[2], inl[3], d);
+      w[0] = make_uint4(d[0], d[1], d[2], d[3]);
+      w[1] = make_uint4(d[4], 0, 0, 0);
+    } else {
+      w[0] = make_uint4(inl[0], inl[1], inl[2], inl[3]);
+      w[1] = make_uint4(inl[4], inl[5], 0, 0);
+    }
     w[2] = w[3] = make_uint4(0, 0, 0, 0);
   } else {
     base = sp & ~(uint64_t)(R - 1);
@@ -546,7 +562,7 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
   bool ctx = E::kCtx && ix.lctx != nullptr;
   while (k > 0) {
-    if (inl && ep - sp > kRecCtx) inl = nullptr;
+    if (inl && !rec_inline(ix, k, ep - sp)) inl = nullptr;
     if (ctx && k <= ix.lctx_q && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
       uint64_t cnt;
       if (ctx_count<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes, inl)) return cnt;
@@ -585,7 +601,7 @@ __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const Node
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);
   bool ctx = E::kCtx && ix.lctx != nullptr && ix.lf_exact;
   while (k > 0) {
-    if (inl && ep - sp > kRecCtx) inl = nullptr;
+    if (inl && !rec_inline(ix, k, ep - sp)) inl = nullptr;
     if (ctx && k <= ix.lctx_q && k <= 7 && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
       uint32_t mm = 0;
       uint64_t base;
@@ -776,16 +792,30 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   }
   // (B) the table entries (whole context records: their contexts come with them)
   uint4 w[U][4];
+  bool inl[U];  // the record's contexts answer the rest
+#pragma unroll
+  for (int j = 0; j < U; ++j) inl[j] = false;
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     if (st[j] != 1 && st[j] != 2) continue;
-    if (ix.ptab_rec) {
+    if (ix.ptab_rec == 1) {
       const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t[j] * 2;
       const uint4 a = r[0], b = r[1];
       sp[j] = a.x;
       ep[j] = (uint64_t)a.x + a.y;
       w[j][0] = make_uint4(a.z, a.w, b.x, b.y);
       w[j][1] = make_uint4(b.z, b.w, 0u, 0u);
+      inl[j] = ep[j] - sp[j] <= kRecCtx;
+    } else if (ix.ptab_rec == 2) {
+      const uint4 a = static_cast<const uint4*>(ix.ptab)[t[j]];
+      const uint32_t wc = a.y & 15u;
+      sp[j] = a.x;
+      inl[j] = wc != kRec16Wide && k[j] <= kRec16Q;
+      ep[j] = (uint64_t)a.x + (wc == kRec16Wide ? a.z : wc);
+      uint32_t d[5];
+      rec16_contexts(a.y, a.z, a.w, d);
+      w[j][0] = make_uint4(d[0], d[1], d[2], d[3]);
+      w[j][1] = make_uint4(d[4], 0u, 0u, 0u);
     } else if (!ptab_at(ix, t[j], sp[j], ep[j])) {
       st[j] = 3;
     }
@@ -803,7 +833,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
       st[j] = 0;
       res[j] = ep[j] - sp[j];
       rv[j] = sp[j];
-    } else if (st[j] == 2 && ix.ptab_rec && ep[j] - sp[j] <= kRecCtx) {
+    } else if (st[j] == 2 && inl[j]) {
       bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record
       w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
     } else if (st[j] == 2 && ep[j] - (sp[j] & ~15ull) <= 32) {
@@ -1531,28 +1561,69 @@ __global__ __launch_bounds__(kBlk) void k_fill_records(const uint2* __restrict__
   }
 }
 
+// Compact 16-B records (fm_device.hpp kRec16Ctx): the width inline when at most
+// kRec16Ctx rows and no row's context is escaped, else kRec16Wide and the width.
+__global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict__ tab,
+                                                         uint64_t entries,
+                                                         const uint16_t* __restrict__ lctx,
+                                                         uint4* __restrict__ rec) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
+    const uint2 e = tab[t];
+    const uint32_t w = e.y - e.x;
+    bool esc = false;
+    uint64_t lo = 0;
+    uint32_t hi = 0;
+    for (uint32_t i = 0; i < kRec16Ctx && i < w; ++i) {
+      const uint32_t c = lctx[e.x + i];
+      esc |= (c & kCtxEsc) != 0;
+      if (i < 6)
+        lo |= (uint64_t)(c & 0x3FFu) << (4 + 10 * i);
+      else
+        hi |= (c & 0x3FFu) << (10 * (i - 6));
+    }
+    if (w > kRec16Ctx || esc)
+      rec[t] = make_uint4(e.x, kRec16Wide, w, 0u);
+    else
+      rec[t] = make_uint4(e.x, (uint32_t)lo | w, (uint32_t)(lo >> 32), hi);
+  }
+}
+
 // Replace the 8-B prefix table by 32-B context records (narrow occurrence-engine
 // indexes with left contexts; C4: 34 GB for k = 15) when HBM allows (an eighth of the
 // device stays free) and the table spans at least 14 characters: records pay for
 // patterns of k+1 .. k+7 characters (the 20-mers of the DNA configs from k = 13 on)
 // and cost 4x the plain table's reads in bytes otherwise (C2, k = 12: 7.9e9 patterns/s
 // with records, 9.1e9 without).  CS_FM_CTX_RECORDS=0 keeps the plain table, =1 forces
-// records for any k (test hook).
+// records for any k (test hook), =16 forces the compact 16-B records, which replace the
+// 32-B ones by default when the table's mean range is at most 4 rows (C4: n / 4^15 =
+// 3.7; a range wider than kRec16Ctx rows or a pattern with 6-7 characters left after the
+// table then reads its context sector).
 cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
-  h->ptab_rec = false;
+  h->ptab_rec = 0;
   if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide || h->lctx_eb != 2) return CS_OK;
-  bool want = h->ptab_k >= 14;
-  if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) want = std::atoi(e) != 0;
-  if (!want) return CS_OK;
   const uint64_t entries = h->ptab_entries();
+  bool want = h->ptab_k >= 14;
+  uint32_t fmt = h->n <= 4 * entries ? 2 : 1;
+  if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) {
+    want = std::atoi(e) != 0;
+    fmt = std::atoi(e) == 16 ? 2 : 1;
+  }
+  if (!want) return CS_OK;
+  const uint64_t bytes = entries * (fmt == 2 ? 16 : 32);
   size_t free_b = 0, total_b = 0;
   FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (entries * 32 + total_b / 8 > free_b) return CS_OK;
+  if (bytes + total_b / 8 > free_b) return CS_OK;
   void* rec = nullptr;
-  FMX_HIP(hipMalloc(&rec, entries * 32));
-  k_fill_records<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
-      static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
-      static_cast<uint32_t*>(rec));
+  FMX_HIP(hipMalloc(&rec, bytes));
+  if (fmt == 2)
+    k_fill_records16<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
+        static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
+        static_cast<uint4*>(rec));
+  else
+    k_fill_records<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
+        static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
+        static_cast<uint32_t*>(rec));
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
@@ -1561,7 +1632,7 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   }
   FMX_HIP(hipFree(h->d_ptab));
   h->d_ptab = rec;
-  h->ptab_rec = true;
+  h->ptab_rec = fmt;
   return CS_OK;
 }
 

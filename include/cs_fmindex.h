@@ -83,6 +83,8 @@ typedef struct cs_fm_info {
                               position_stride positions; the SSA keeps ssa_stride */
   uint64_t context_bytes;
   uint64_t full_sa_bytes;  /* full suffix array kept for locate (lf_exact builds), 0 = none */
+  uint32_t record_bytes;   /* prefix-table entries are context records of 32 or 16 B; 0 = plain table */
+  uint32_t reserved0;
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -103,13 +103,13 @@ def test_concurrent_calls_share_nothing_mutable():
     assert not bad, bad[:5]
 
 
-@pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "learned", "records"])
+@pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "learned", "records", "records16"])
 def test_export_import_image(engine, monkeypatch):
     """The device image (cs_fm_export_meta/_parts -> cs_fm_import): the copy answers
     count / locate / extract exactly as the original (context records and the full
     suffix array included)."""
-    if engine == "records":
-        monkeypatch.setenv("CS_FM_CTX_RECORDS", "1")
+    if engine in ("records", "records16"):
+        monkeypatch.setenv("CS_FM_CTX_RECORDS", "1" if engine == "records" else "16")
     elif engine != "auto":
         monkeypatch.setenv("CS_FM_ENGINE", engine)
     pkg = load_pkg()
@@ -124,11 +124,13 @@ def test_export_import_image(engine, monkeypatch):
     del parts
     assert c.info().engine == g.info().engine and c.info().walk_marks == g.info().walk_marks
     assert c.info().context_q == g.info().context_q == {"auto": 7, "qwm": 8, "wavelet": 0, "learned": 7,
-                                                        "records": 7}[engine]
+                                                        "records": 7, "records16": 7}[engine]
     assert c.info().prefix_bytes == g.info().prefix_bytes
     assert c.info().full_sa_bytes == g.info().full_sa_bytes == 4 * len(t)
-    if engine == "records":
-        assert g.info().prefix_bytes == 32 * g.info().prefix_sigma ** g.info().prefix_k
+    if engine in ("records", "records16"):
+        rb = 32 if engine == "records" else 16
+        assert c.info().record_bytes == g.info().record_bytes == rb
+        assert g.info().prefix_bytes == rb * g.info().prefix_sigma ** g.info().prefix_k
     P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 14, 500)
     pats = [bytes(r) for r in P] + [b"ACGTACGTAC", b"$", b""]
     assert c.count_batch(pats).tolist() == g.count_batch(pats).tolist()

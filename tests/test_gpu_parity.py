@@ -30,6 +30,7 @@ ENGINE_VARIANTS = {
     "auto_nowalk": {"CS_FM_WALK": "0", "CS_FM_FULL_SA": "0"},  # locate walks the occurrence lines
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "auto_rec": {"CS_FM_CTX_RECORDS": "1"},         # context records at any table depth
+    "auto_rec16": {"CS_FM_CTX_RECORDS": "16"},      # compact 16-B context records at any table depth
     "auto_nosa": {"CS_FM_FULL_SA": "0"},            # locate walks (no full suffix array kept)
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
@@ -208,6 +209,13 @@ def test_engine_choice(built):
         assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or
                                         (16 if wide else 4)), name
         assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
+        # context records: narrow occurrence-line indexes with contexts and a table of
+        # 14+ characters (none of these texts) or forced; 16 B when forced compact
+        rec = {"1": 32, "16": 16}.get(os.environ.get("CS_FM_CTX_RECORDS", ""), 0)
+        if not (ctx and engine in (1, 3) and not wide and info.prefix_k):
+            rec = 0
+        assert info.record_bytes == rec, name
+        assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))

@@ -98,7 +98,9 @@ def test_c4_dna_4gb(variant, monkeypatch):
     assert N == 4_000_000_000
     info = idx.info()
     assert (info.full_sa_bytes > 0) == (variant != "plain_walk")
-    assert (info.prefix_bytes == 32 * info.prefix_sigma ** info.prefix_k) == (variant != "plain_walk")
+    # C4: n / 4^15 = 3.7 rows per k-mer -> compact 16-B records
+    assert info.record_bytes == (0 if variant == "plain_walk" else 16)
+    assert info.prefix_bytes == max(info.record_bytes, 8) * info.prefix_sigma ** info.prefix_k
     P = _qtext(pkg, text, N, 20, 200_000)
     _check_qtext(idx, host, N, P, nloc=20_000)
     ones = idx.count_batch([bytes([c]) for c in range(256)])
