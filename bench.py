@@ -358,7 +358,9 @@ def main():
         want = text[(xpos.unsqueeze(1) + torch.arange(XL, device=dev)).long()].reshape(-1)
         res["extract"] = {"queries": K_, "len": XL, "seconds": min(xt),
                           "queries_per_s": K_ / min(xt), "bytes_per_s": K_ * XL / min(xt),
-                          "verified": bool(torch.equal(want, xout))}
+                          "verified": bool(torch.equal(want, xout)),
+                          "method": ("copy from the text in HBM (text_.substr)" if info.text_in_hbm
+                                     else "LF inversion from inverse-SA samples")}
         del xpos, xlen, xoff, xout, want
 
     # ---- p50 single-pattern latency (>= 1000 single-pattern calls

@@ -239,6 +239,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_ptab) (void)hipFree(h->d_ptab);
   if (h->d_isa) (void)hipFree(h->d_isa);
   if (h->d_sa) (void)hipFree(h->d_sa);
+  if (h->d_dtext) (void)hipFree(h->d_dtext);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
   if (h->d_lctx) (void)hipFree(h->d_lctx);
@@ -287,6 +288,7 @@ cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params*
   return build_handle(device, out, [&](cs_fm_index* h, hipStream_t st) {
     cs_status s = build_index_device(d_text, n, p->ssa_stride, h, st);
     if (s == CS_OK && host_text) h->h_text.assign(host_text, host_text + n);
+    if (s == CS_OK) s = keep_device_text(h, d_text, true, st);
     return s;
   });
 }
@@ -342,6 +344,7 @@ cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint
   return build_handle(device, out, [&](cs_fm_index* h, hipStream_t st) {
     cs_status s = build_index_from_bwt(bwt, n, ssa, nsamples, ssa_stride, h, st);
     if (s == CS_OK && text) h->h_text.assign(text, text + n);
+    if (s == CS_OK && text) s = keep_device_text(h, text, false, st);
     return s;
   });
 }
@@ -389,7 +392,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->position_stride = h->pstride;
   out->full_sa_bytes = h->d_sa ? h->n * 4 : 0u;
   out->record_bytes = h->ptab_rec ? h->ptab_entry_bytes() : 0u;
-  out->reserved0 = 0;
+  out->text_in_hbm = h->d_dtext ? 1u : 0u;
   return CS_OK;
 }
 
@@ -703,7 +706,7 @@ cs_status cs_fm_extract_batch(const cs_fm_index* h, const uint64_t* pos, const u
     set_error("null output buffer");
     return CS_ERR_INVALID;
   }
-  if (!h->lf_exact || !h->nisa) {
+  if (!h->d_dtext && (!h->lf_exact || !h->nisa)) {
     if (h->h_text.size() == n) {  // the text_ copy, as the reference keeps it
       for (uint64_t q = 0; q < k; ++q)
         if (pos[q] < n) std::memcpy(out + out_offs[q], h->h_text.data() + pos[q], out_offs[q + 1] - out_offs[q]);
@@ -738,9 +741,9 @@ cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, cons
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
-  if (!h->lf_exact || !h->nisa) {
-    set_error("device extract needs a text ending in a unique smallest symbol and "
-              "inverse-SA samples");
+  if (!h->d_dtext && (!h->lf_exact || !h->nisa)) {
+    set_error("device extract needs the text in HBM, or a text ending in a unique smallest "
+              "symbol and inverse-SA samples");
     return CS_ERR_UNSUPPORTED;
   }
   return launch_extract(h, d_pos, d_len, d_out_offs, k, d_out, (hipStream_t)stream);

@@ -45,6 +45,7 @@ struct cs_fm_index {
   uint64_t nlmodel = 0;
   uint32_t lmodel_shift = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
+  void* d_dtext = nullptr;            // the same text in HBM: extract as a copy (fm_index.cpp:163-167)
   uint32_t active_levels[256] = {};
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
@@ -192,6 +193,7 @@ cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint
 cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
 cs_status build_left_contexts(cs_fm_index* h, hipStream_t st);
 cs_status build_context_records(cs_fm_index* h, hipStream_t st);
+cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st);
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st);
 

@@ -10,7 +10,7 @@
 // Directory layout (all little-endian raw arrays, exactly the HBM images):
 //   cs_fmindex.meta  "key value" lines: format, n, stride, line_bytes, line_bits,
 //                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
-//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride, nlmodel, lmodel_shift, ptab_rec, has_sa,
+//                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride, nlmodel, lmodel_shift, ptab_rec, has_sa, has_dtext,
 //                    active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
@@ -18,7 +18,7 @@
 //   ptab.bin         prefix table (if k > 0) text.bin  the text (if kept, for extract)
 //   walk.bin         walk lines                      wssa.bin  their position samples
 //   lctx.bin         left contexts (if built)    lmodel.bin  learned-line models
-//   sa.bin           full suffix array (if kept)
+//   sa.bin           full suffix array (if kept)     dtext.bin  the text in HBM (if kept)
 // The device image (cs_fm_export_* / cs_fm_import) is the same meta text plus the
 // parts table, lines, ssa, isa[, ptab][, walk][, wssa][, lctx] as device buffers.
 #include <cerrno>
@@ -98,7 +98,8 @@ struct Part {
 
 // The index's device arrays in image order; sizes from the geometry fields, so the
 // exporting and the importing side derive the same list from the same meta.
-std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa, bool has_sa) {
+std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa, bool has_sa,
+                              bool has_dtext) {
   std::vector<Part> v;
   const uint64_t sb = h->sample_bytes();
   if (with_table) v.push_back({"table.bin", reinterpret_cast<void**>(&h->d_table), sizeof(NodeTable)});
@@ -111,6 +112,7 @@ std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa, bo
   if (h->nlctx) v.push_back({"lctx.bin", &h->d_lctx, h->nlctx * h->lctx_eb});
   if (h->nlmodel) v.push_back({"lmodel.bin", &h->d_lmodel, h->nlmodel * sizeof(LOccModel)});
   if (has_sa) v.push_back({"sa.bin", &h->d_sa, h->n * 4});
+  if (has_dtext) v.push_back({"dtext.bin", &h->d_dtext, h->n});
   return v;
 }
 
@@ -121,7 +123,7 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
                 "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n"
                 "nlctx %llu\nlctx_q %u\nlctx_sb %u\nlctx_eb %u\npstride %u\nnlmodel %llu\n"
-                "lmodel_shift %u\nptab_rec %d\nhas_sa %d\n",
+                "lmodel_shift %u\nptab_rec %d\nhas_sa %d\nhas_dtext %d\n",
                 kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                 (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                 (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
@@ -129,7 +131,7 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 (unsigned long long)(h->d_walk ? h->nwalk : 0), h->walk_marks, h->d_wssa ? 1 : 0,
                 (unsigned long long)(h->d_lctx ? h->nlctx : 0), h->lctx_q, h->lctx_sb, h->lctx_eb,
                 h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift, (int)h->ptab_rec,
-                h->d_sa ? 1 : 0);
+                h->d_sa ? 1 : 0, h->d_dtext ? 1 : 0);
   std::string m(buf);
   for (int c = 0; c < 256; ++c) {
     std::snprintf(buf, sizeof buf, "active %d %u\n", c, h->active_levels[c]);
@@ -230,7 +232,7 @@ cs_status cs_fm_save_directory(const cs_fm_index* hc, const char* dir) {
   Pinned pin;
   FMX_HIP(hipHostMalloc(&pin.p, kChunk, hipHostMallocDefault));
   cs_status s;
-  for (const Part& p : index_parts(h, false, h->d_wssa != nullptr, h->d_sa != nullptr))
+  for (const Part& p : index_parts(h, false, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr))
     if ((s = dump_dev(join(d, p.file), *p.dptr, p.bytes, pin.p)) != CS_OK) return s;
   {
     FILE* f = std::fopen(join(d, "table.bin").c_str(), "wb");
@@ -240,7 +242,8 @@ cs_status cs_fm_save_directory(const cs_fm_index* hc, const char* dir) {
     }
     std::fclose(f);
   }
-  const bool has_text = h->h_text.size() == h->n && h->n;
+  // the host text_ copy, unless the text travels as the device part dtext.bin
+  const bool has_text = h->h_text.size() == h->n && h->n && !h->d_dtext;
   if (has_text) {
     FILE* f = std::fopen(join(d, "text.bin").c_str(), "wb");
     if (!f || std::fwrite(h->h_text.data(), 1, h->n, f) != h->n) {
@@ -299,7 +302,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     }
     std::fclose(t);
   }
-  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0, kv["has_sa"] != 0);
+  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0, kv["has_sa"] != 0, kv["has_dtext"] != 0);
   if ((s = alloc_parts(h, parts)) != CS_OK) return fail(s);
   Pinned pin;
   if (hipHostMalloc(&pin.p, kChunk, hipHostMallocDefault) != hipSuccess)
@@ -331,7 +334,7 @@ cs_status cs_fm_export_meta(const cs_fm_index* hc, char* meta, uint64_t cap, uin
   }
   cs_fm_index* h = const_cast<cs_fm_index*>(hc);
   const std::string m = meta_text(h, false);
-  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr);
+  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr);
   *meta_len = m.size();
   *nparts = (uint32_t)parts.size();
   if (!meta || cap < m.size() || !part_bytes) {
@@ -351,7 +354,7 @@ cs_status cs_fm_export_parts(const cs_fm_index* hc, void* const* d_dst, void* st
   cs_fm_index* h = const_cast<cs_fm_index*>(hc);
   DeviceScope ds;
   FMX_HIP(ds.enter(h->device));
-  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr);
+  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr);
   for (size_t i = 0; i < parts.size(); ++i)
     if (parts[i].bytes)
       FMX_HIP(hipMemcpyAsync(d_dst[i], *parts[i].dptr, parts[i].bytes, hipMemcpyDeviceToDevice,
@@ -381,7 +384,7 @@ cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d
   };
   DeviceScope ds;
   if (ds.enter(device) != hipSuccess) return fail(hip_fail(hipGetLastError(), "hipSetDevice"));
-  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0, kv["has_sa"] != 0);
+  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0, kv["has_sa"] != 0, kv["has_dtext"] != 0);
   if (parts.size() != nparts) {
     set_error("import: the image has a different number of parts than its meta");
     return fail(CS_ERR_INVALID);

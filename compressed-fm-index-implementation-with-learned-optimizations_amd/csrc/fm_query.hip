@@ -1389,6 +1389,32 @@ __global__ __launch_bounds__(kBlk) void k_extract(DevIndex ix, const uint64_t* _
   }
 }
 
+// extract(pos, len) (fm_index.cpp:163-167) as the reference does it — a copy of
+// text_[pos, pos+len) — from the text kept in HBM (keep_device_text).  One lane per
+// query: the queries' strings are short and start at random positions, so each lane
+// reads its own 1-2 cache lines; dword loads when source and destination line up.
+__global__ __launch_bounds__(kBlk) void k_extract_text(const uint8_t* __restrict__ text, uint64_t n,
+                                                       const uint64_t* __restrict__ pos,
+                                                       const uint64_t* __restrict__ len,
+                                                       const uint64_t* __restrict__ out_offs,
+                                                       uint64_t k, uint8_t* __restrict__ out) {
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= k) return;
+  const uint64_t p = pos[q];
+  if (p >= n) return;  // fm_index.cpp:164: empty
+  uint64_t L = len[q];
+  if (L > n - p) L = n - p;  // :165
+  const uint8_t* s = text + p;
+  uint8_t* o = out + out_offs[q];
+  uint64_t i = 0;
+  if ((((uintptr_t)s ^ (uintptr_t)o) & 3) == 0) {
+    for (; i < L && ((uintptr_t)(s + i) & 3); ++i) o[i] = s[i];
+    for (; i + 4 <= L; i += 4)
+      *reinterpret_cast<uint32_t*>(o + i) = *reinterpret_cast<const uint32_t*>(s + i);
+  }
+  for (; i < L; ++i) o[i] = s[i];
+}
+
 // WaveletTree::access for every row (the BWT), grid-stride.
 template <class E>
 __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__ out) {
@@ -1636,9 +1662,32 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   return CS_OK;
 }
 
+// The text in HBM for extract (the reference keeps text_, fm_index.hpp:41): n bytes
+// (C4: 4 GB, C5: 32 GB), kept when an eighth of the device stays free;
+// CS_FM_DEVICE_TEXT=0 leaves extract to LF inversion from the inverse-SA samples.
+cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st) {
+  if (!src || !h->n || h->d_dtext) return CS_OK;
+  if (const char* e = std::getenv("CS_FM_DEVICE_TEXT"))
+    if (std::atoi(e) == 0) return CS_OK;
+  size_t free_b = 0, total_b = 0;
+  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
+  if (h->n + total_b / 8 > free_b) return CS_OK;
+  FMX_HIP(hipMalloc(&h->d_dtext, h->n));
+  FMX_HIP(hipMemcpyAsync(h->d_dtext, src, h->n,
+                         src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  return CS_OK;
+}
+
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
                          const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st) {
   if (!k) return CS_OK;
+  if (h->d_dtext) {
+    k_extract_text<<<grid_for(k, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        static_cast<const uint8_t*>(h->d_dtext), h->n, d_pos, d_len, d_out_offs, k, d_out);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
   FMX_DISPATCH(h, k_extract, grid_for(k, kBlk, 0xFFFFFFFFu), h->dev(), d_pos, d_len, d_out_offs, k,
                d_out);
   return CS_OK;

@@ -84,7 +84,7 @@ typedef struct cs_fm_info {
   uint64_t context_bytes;
   uint64_t full_sa_bytes;  /* full suffix array kept for locate (lf_exact builds), 0 = none */
   uint32_t record_bytes;   /* prefix-table entries are context records of 32 or 16 B; 0 = plain table */
-  uint32_t reserved0;
+  uint32_t text_in_hbm;    /* 1: the text is kept in HBM and extract copies it (as text_.substr) */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

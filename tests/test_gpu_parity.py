@@ -27,7 +27,8 @@ ENGINE_VARIANTS = {
     "auto": {},
     "auto_noprefix": {"CS_FM_PREFIX_K": "0"},       # prefix table off
     "auto_rowmarks": {"CS_FM_WALK_MARKS": "row", "CS_FM_FULL_SA": "0"},  # walks over row-marked walk lines
-    "auto_nowalk": {"CS_FM_WALK": "0", "CS_FM_FULL_SA": "0"},  # locate walks the occurrence lines
+    # locate walks the occurrence lines; extract by LF inversion (no text in HBM)
+    "auto_nowalk": {"CS_FM_WALK": "0", "CS_FM_FULL_SA": "0", "CS_FM_DEVICE_TEXT": "0"},
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "auto_rec": {"CS_FM_CTX_RECORDS": "1"},         # context records at any table depth
     "auto_rec16": {"CS_FM_CTX_RECORDS": "16"},      # compact 16-B context records at any table depth
@@ -37,10 +38,11 @@ ENGINE_VARIANTS = {
     "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
     "learned_sb4": {"CS_FM_ENGINE": "learned", "CS_FM_LEARNED_SHIFT": "2"},  # 4-line superblocks
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
-    "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64"},  # 64-B rank lines
+    "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64",  # 64-B rank lines,
+                       "CS_FM_DEVICE_TEXT": "0"},                             # LF-inversion extract
     # the n >= 2^32 engines at small n: u64 samples/table, bucketed sorter, and
     # occurrence lines or 32-B wide rank lines (Line32W)
-    "wide_bucketed": {"CS_FM_WIDE": "1", "CS_FM_SA_BUILDER": "bucketed"},
+    "wide_bucketed": {"CS_FM_WIDE": "1", "CS_FM_SA_BUILDER": "bucketed", "CS_FM_DEVICE_TEXT": "0"},
     "wide_wavelet": {"CS_FM_WIDE": "1", "CS_FM_ENGINE": "wavelet"},
     # packed wide prefix-table entries with every range of 3+ rows escaped (C[] start)
     "wide_ptab_esc": {"CS_FM_WIDE": "1", "CS_FM_PTAB_WMAX": "3"},
@@ -48,7 +50,7 @@ ENGINE_VARIANTS = {
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
           "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
           "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT", "CS_FM_PTAB_WMAX",
-          "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA")
+          "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA", "CS_FM_DEVICE_TEXT")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
@@ -215,6 +217,7 @@ def test_engine_choice(built):
         if not (ctx and engine in (1, 3) and not wide and info.prefix_k):
             rec = 0
         assert info.record_bytes == rec, name
+        assert info.text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0"), name
         assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
 
 
@@ -438,24 +441,44 @@ def test_save_open_directory_roundtrip(pkg, tmp_path):
     b = h.locate_batch(pats, limit=20)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
     assert h.extract(100, 50) == t[100:150]
-    os.remove(os.path.join(d, "text.bin"))
-    meta = open(os.path.join(d, "cs_fmindex.meta")).read().replace("has_text 1", "has_text 0")
+    assert h.extract_batch([100, len(t) - 5], [50, 10]) == [t[100:150], t[-5:]]
+    if g.info().text_in_hbm:
+        # the text travels as the device part dtext.bin (no host text.bin beside it)
+        assert h.info().text_in_hbm == 1 and not os.path.exists(os.path.join(d, "text.bin"))
+        part, key = "dtext.bin", "has_dtext"
+    else:  # CS_FM_DEVICE_TEXT=0: the host text_ copy is saved as text.bin
+        assert h.info().text_in_hbm == 0 and os.path.exists(os.path.join(d, "text.bin"))
+        part, key = "text.bin", "has_text"
+    os.remove(os.path.join(d, part))
+    meta = open(os.path.join(d, "cs_fmindex.meta")).read().replace(key + " 1", key + " 0")
     open(os.path.join(d, "cs_fmindex.meta"), "w").write(meta)
     k = pkg.FMIndex.open_directory(d)
+    assert k.info().text_in_hbm == 0
     assert k.extract(100, 50) == t[100:150]  # device LF inversion
     assert k.extract(len(t) - 5, 10) == t[-5:]
 
 
-def test_device_extract(pkg):
-    """Batched extract by LF inversion from inverse-SA samples == text slices
-    (fm_index.cpp:163-167 clamping), for every start position of a small text."""
-    for stride in (1, 5, 32):
-        t = O.gen_dna(stride, 3000).tobytes()
-        g = pkg.FMIndex.build_from_text(t, pkg.BuildParams(ssa_stride=stride))
-        pos = list(range(0, len(t) + 3))
-        lens = [(p * 7) % 45 for p in pos]
-        got = g.extract_batch(pos, lens)
-        assert got == [t[p:p + l] for p, l in zip(pos, lens)]
+@pytest.mark.parametrize("dtext", ["1", "0"])
+def test_device_extract(pkg, dtext):
+    """Batched extract == text slices (fm_index.cpp:163-167 clamping), for every start
+    position of a small text: copied from the text in HBM, or (CS_FM_DEVICE_TEXT=0) by
+    LF inversion from inverse-SA samples."""
+    saved = os.environ.get("CS_FM_DEVICE_TEXT")
+    os.environ["CS_FM_DEVICE_TEXT"] = dtext
+    try:
+        for stride in (1, 5, 32):
+            t = O.gen_dna(stride, 3000).tobytes()
+            g = pkg.FMIndex.build_from_text(t, pkg.BuildParams(ssa_stride=stride))
+            assert g.info().text_in_hbm == int(dtext)
+            pos = list(range(0, len(t) + 3))
+            lens = [(p * 7) % 45 for p in pos]
+            got = g.extract_batch(pos, lens)
+            assert got == [t[p:p + l] for p, l in zip(pos, lens)]
+    finally:
+        if saved is None:
+            del os.environ["CS_FM_DEVICE_TEXT"]
+        else:
+            os.environ["CS_FM_DEVICE_TEXT"] = saved
     g = pkg.FMIndex.build_from_text(b"abab")  # no unique smallest terminator:
     assert g.extract_batch([0, 3], [2, 5]) == [b"ab", b"b"]  # the host text copy, as text_
     assert g.extract(0, 2) == b"ab"
@@ -548,5 +571,8 @@ def test_create_from_arrays(pkg, name):
             continue
         assert g.locate(p, limit=50) == w
     assert gt.extract(1, 7) == t[1:8]
+    assert gt.info().text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0")
+    assert g.info().text_in_hbm == 0
+    assert gt.extract_batch([1, 0, len(t) - 2], [7, 3, 9]) == [t[1:8], t[0:3], t[-2:]]
     with pytest.raises(RuntimeError):
         g.extract(1, 7)
