@@ -324,6 +324,23 @@ def main():
                          "limit": 100000, "positions_verified": ok}
         del d_sp, d_oo, d_pos, owner, win
 
+    # ---- the same batch as one-length k-mers back to back (cs_fm_count_fixed_device: no
+    #      offsets array to read), N=1 only: reported beside value, never as value ----
+    if rank == 0 and world == 1:
+        fo = torch.empty(B, dtype=torch.int64, device=dev)
+        for k in range(max(args.warmup, 1)):
+            idx.count_fixed_device(pats.data_ptr(), m, B, fo.data_ptr(), sh)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(args.steps):
+            idx.count_fixed_device(pats.data_ptr(), m, B, fo.data_ptr(), sh)
+        torch.cuda.synchronize()
+        tf = (time.perf_counter() - t1) / args.steps
+        res["count_fixed"] = {"patterns": B, "m": m, "ms_per_step": tf * 1e3,
+                              "patterns_per_s": B / tf,
+                              "matches_batch": bool(np.array_equal(fo.cpu().numpy(), counts))}
+        del fo
+
     # ---- the same batch handed over in host memory (cs_fm_count_batch: PCIe in and out
     #      inside the call), N=1 only: reported beside value, never as value ----
     if rank == 0 and world == 1 and args.host_batch:

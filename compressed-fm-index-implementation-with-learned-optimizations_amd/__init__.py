@@ -80,6 +80,7 @@ SIGNATURES = {
     "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_extract_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "cs_fm_count_fixed_device": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
     "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                              _u64p, _vp]),
     "cs_fm_locate_walk_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
@@ -354,6 +355,10 @@ class FMIndex:
     # -- device-resident batches (raw device pointers, e.g. torch data_ptr()) --
     def count_batch_device(self, d_pats: int, d_offs: int, npat: int, d_out: int, stream: int = 0):
         _check(lib().cs_fm_count_batch_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
+
+    def count_fixed_device(self, d_pats: int, m: int, npat: int, d_out: int, stream: int = 0):
+        """count of npat patterns of length m laid out back to back (no offsets array)."""
+        _check(lib().cs_fm_count_fixed_device(self._h, d_pats, m, npat, d_out, stream or None))
 
     def extract_device(self, d_pos, d_len, d_out_offs, k, d_out, stream=0):
         """Batched extract with device buffers (d_out_offs = scan of clamped lengths)."""

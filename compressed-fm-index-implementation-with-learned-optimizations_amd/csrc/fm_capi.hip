@@ -409,6 +409,18 @@ cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
   return launch_count(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
 }
 
+cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, uint64_t m,
+                                   uint64_t npat, uint64_t* d_out, void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (npat && (!d_out || (m && !d_pats))) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_count(h, d_pats, nullptr, npat, d_out, (hipStream_t)stream, m);
+}
+
 cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream) {

@@ -160,8 +160,9 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
                              hipStream_t st);
 
 // Query launches (fm_query.hip).
+// d_offs == nullptr: npat patterns of length fixed_m at stride fixed_m
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                       uint64_t npat, uint64_t* d_out, hipStream_t st);
+                       uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m = 0);
 cs_status launch_count_one(const cs_fm_index* h, const fmx::OnePattern& p, uint64_t* out_host,
                            hipStream_t st);
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,

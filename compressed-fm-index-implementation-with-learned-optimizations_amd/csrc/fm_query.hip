@@ -679,15 +679,16 @@ __global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix,
 }
 
 template <class E>
+// offs == nullptr: patterns of one length fixed_m at stride fixed_m (cs_fm_count_fixed_device)
 __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t npat,
-                                                uint64_t* __restrict__ out) {
+                                                uint64_t* __restrict__ out, uint64_t fixed_m) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
   const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (q >= npat) return;
-  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
   uint64_t res;
   if (m == 0) res = ix.n;       // fm_index.cpp:80
   else if (ix.n == 0) res = 0;  // :81
@@ -729,7 +730,9 @@ template <class E, int U, bool kLoc>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, uint64_t* __restrict__ out,
-                                                    uint64_t limit, uint64_t* __restrict__ rec) {
+                                                    uint64_t limit, uint64_t* __restrict__ rec,
+                                                    uint64_t fixed_m) {
+  // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
   // the stages need only the symbol -> (table digit, occurrence code) map in LDS (512 B
   // instead of the 10.8-KB node table: a shorter block prologue); a block stages the
   // node table only when one of its patterns needs the general search
@@ -756,8 +759,8 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     m[j] = 0;
     t[j] = want[j] = k[j] = 0;
     if (q >= npat) continue;
-    o0[j] = offs[q];
-    const uint64_t mm = offs[q + 1] - o0[j];
+    o0[j] = offs ? offs[q] : q * fixed_m;
+    const uint64_t mm = offs ? offs[q + 1] - o0[j] : fixed_m;
     m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
     if (mm == 0) {
       res[j] = kLoc ? 0 : ix.n;  // fm_index.cpp:80; locate: :109
@@ -1699,7 +1702,7 @@ cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
 }
 
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                       uint64_t npat, uint64_t* d_out, hipStream_t st) {
+                       uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m) {
   if (!npat) return CS_OK;
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
     static const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U)
@@ -1710,20 +1713,21 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
     const DevIndex ix = h->dev();
     if (h->line_fmt == kFmtLOcc)
       k_count_ctx<LOccE, 2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
     else if (U == 1)
       k_count_ctx<OccE, 1, false><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
     else if (U == 2)
       k_count_ctx<OccE, 2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
     else
       k_count_ctx<OccE, 4, false><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr);
+          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
-  FMX_DISPATCH(h, k_count, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat, d_out);
+  FMX_DISPATCH(h, k_count, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat, d_out,
+               fixed_m);
   return CS_OK;
 }
 
@@ -1758,10 +1762,10 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
     if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
       k_count_ctx<OccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp);
+          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
     else
       k_count_ctx<LOccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp);
+          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
     FMX_HIP(hipGetLastError());
   } else {
     FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,

@@ -188,6 +188,11 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
 cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream);
+/* The same for npat patterns of one length m laid out back to back (pattern q at
+ * d_pats + q*m; k-mer batches): FMIndex::count (src/api/fm_index.cpp:79-101) of each,
+ * without an offsets array to read. */
+cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, uint64_t m,
+                                   uint64_t npat, uint64_t* d_out, void* stream);
 /* Measurement twin of cs_fm_count_batch_device: d_out[q] = the algorithmic HBM
  * bytes of query q's search (distinct rank/occurrence lines per rank pair x line
  * size + the prefix-table entry), for roofline accounting (bench.py). */

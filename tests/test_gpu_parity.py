@@ -272,6 +272,35 @@ def test_count_every_text_vs_oracle(built, name):
             assert g.locate(p, limit=lim) == want, (name, p, lim)
 
 
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_count_fixed_length(built, name):
+    """cs_fm_count_fixed_device — patterns of one length m back to back, no offsets
+    array — equals the oracle's count for substrings and mutants, and n for m = 0."""
+    import torch
+    g, o = built(name)
+    t = TEXTS[name]
+    n = len(t)
+    rng = np.random.default_rng(n + 1)
+    for m in (1, 3, 7, 13, 20, 33):
+        if m > n:
+            continue
+        pats = []
+        for i in rng.integers(0, n - m + 1, 50):
+            p = bytearray(t[i:i + m])
+            pats.append(bytes(p))
+            p[rng.integers(0, m)] = t[rng.integers(0, n)]
+            pats.append(bytes(p))
+        buf = torch.tensor(list(b"".join(pats)), dtype=torch.uint8, device="cuda")
+        out = torch.empty(len(pats), dtype=torch.int64, device="cuda")
+        g.count_fixed_device(buf.data_ptr(), m, len(pats), out.data_ptr())
+        torch.cuda.synchronize()
+        assert out.tolist() == [o.count(p) for p in pats], (name, m)
+    out = torch.empty(3, dtype=torch.int64, device="cuda")
+    g.count_fixed_device(out.data_ptr(), 0, 3, out.data_ptr())  # fm_index.cpp:80
+    torch.cuda.synchronize()
+    assert out.tolist() == [n] * 3
+
+
 def test_locate_context_windows(pkg):
     """Locate over context windows (phase-1 records): patterns with up to 40 hits in
     one window (repeats: the window's match span exceeds the record's 22 bits and the
