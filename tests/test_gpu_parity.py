@@ -13,6 +13,7 @@ import os
 
 import numpy as np
 import pytest
+import torch  # before the engine's library loads: one HIP runtime in the process
 
 import oracle as O
 from conftest import fm_golden_cases, golden_text, load_golden, load_pkg
@@ -276,7 +277,6 @@ def test_count_every_text_vs_oracle(built, name):
 def test_count_fixed_length(built, name):
     """cs_fm_count_fixed_device — patterns of one length m back to back, no offsets
     array — equals the oracle's count for substrings and mutants, and n for m = 0."""
-    import torch
     g, o = built(name)
     t = TEXTS[name]
     n = len(t)
