@@ -1782,16 +1782,49 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
   return CS_OK;
 }
 
-// Positions of the reported rows from the full suffix array (lf_exact): SA[row] - k
-// (mod n) for a window row tagged with k (locate records), SA[row] otherwise.
-__global__ __launch_bounds__(kBlk) void k_sa_gather(const uint32_t* __restrict__ sa, uint64_t n,
-                                                    const uint64_t* __restrict__ rows,
-                                                    uint64_t total, uint64_t* __restrict__ out) {
+// Phase 2 with the full suffix array, fused (no rows buffer): each pattern's rows come
+// from its record (as k_expand_rows) and go straight through SA: SA[row] - k (mod n) for
+// a window row k characters before the end, SA[row] otherwise.  A lane
+// takes a pattern of at most kLocSmall rows (every context window: <= kLocSpanBits);
+// wider plain ranges are listed for k_locate_sa_wide, a block per range.
+constexpr uint64_t kLocSmall = 32;
+__global__ __launch_bounds__(kBlk) void k_locate_sa(const uint32_t* __restrict__ sa, uint64_t n,
+                                                    const uint64_t* __restrict__ sp,
+                                                    const uint64_t* __restrict__ offs, uint64_t npat,
+                                                    uint64_t* __restrict__ out,
+                                                    uint64_t* __restrict__ wide,
+                                                    unsigned long long* __restrict__ nwide) {
   const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < total; j += gs) {
-    const uint64_t row = rows[j];
-    const uint64_t s = sa[row & kWalkRowMask], adj = row >> kWalkAdjShift;
-    out[j] = s >= adj ? s - adj : s + n - adj;
+  for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < npat; q += gs) {
+    const uint64_t a = offs[q], c = offs[q + 1] - a, s = sp[q];
+    if (!c) continue;
+    if (s & kLocCtx) {
+      const uint64_t r0 = s & kLocRowMask, adj = (s >> 60) & 7u;
+      uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+      for (uint64_t j = 0; j < c; ++j) {
+        const uint32_t f = (uint32_t)__ffs(rel) - 1u;
+        const uint64_t p = sa[r0 + f];
+        out[a + j] = p >= adj ? p - adj : p + n - adj;
+        rel &= rel - 1u;
+      }
+    } else if (c <= kLocSmall) {
+      for (uint64_t j = 0; j < c; ++j) out[a + j] = sa[s + j];
+    } else {
+      wide[atomicAdd(nwide, 1ull)] = q;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlk) void k_locate_sa_wide(const uint32_t* __restrict__ sa,
+                                                         const uint64_t* __restrict__ sp,
+                                                         const uint64_t* __restrict__ offs,
+                                                         uint64_t* __restrict__ out,
+                                                         const uint64_t* __restrict__ wide,
+                                                         const unsigned long long* __restrict__ nwide) {
+  const uint64_t nw = *nwide;
+  for (uint64_t e = blockIdx.x; e < nw; e += gridDim.x) {
+    const uint64_t q = wide[e], a = offs[q], c = offs[q + 1] - a, s = sp[q];
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) out[a + j] = sa[s + j];
   }
 }
 
@@ -1799,6 +1832,20 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word) {
   if (!total) return CS_OK;
+  if (h->d_sa && h->lf_exact) {  // full suffix array: one read per position
+    StreamBuf wide;
+    FMX_HIP(wide.alloc((total / (kLocSmall + 1) + 1) * 8 + 8, st));
+    unsigned long long* nwide = wide.as<unsigned long long>();
+    FMX_HIP(hipMemsetAsync(nwide, 0, 8, st));
+    const uint32_t* sa = static_cast<const uint32_t*>(h->d_sa);
+    k_locate_sa<<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        sa, h->n, d_sp, d_out_offs, npat, d_out_pos, wide.as<uint64_t>() + 1, nwide);
+    FMX_HIP(hipGetLastError());
+    k_locate_sa_wide<<<1024, kBlk, 0, st>>>(sa, d_sp, d_out_offs, d_out_pos,
+                                             wide.as<uint64_t>() + 1, nwide);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
   StreamBuf rows;
   FMX_HIP(rows.alloc(total * 8, st));
   k_expand_rows<<<grid_for(npat, kBlk, 65536), kBlk, 0, st>>>(d_sp, d_out_offs, npat,
@@ -1816,12 +1863,6 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
       err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
-  if (h->d_sa && h->lf_exact) {  // full suffix array: one read per position
-    k_sa_gather<<<grid_for(total, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        static_cast<const uint32_t*>(h->d_sa), h->n, r, total, d_out_pos);
-    FMX_HIP(hipGetLastError());
-    return CS_OK;
-  }
   static const bool persistent = [] {  // tuning hook: CS_FM_WALK_PERSISTENT=1
     const char* e = std::getenv("CS_FM_WALK_PERSISTENT");
     return e && std::atoi(e) == 1;
