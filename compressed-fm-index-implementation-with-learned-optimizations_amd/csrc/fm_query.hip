@@ -1760,7 +1760,14 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
   StreamBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8, st));
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
-    if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
+    static const int U = [] {  // patterns per lane (tuning hook CS_FM_LOCATE_U: 1 or 2)
+      const char* e = std::getenv("CS_FM_LOCATE_U");
+      return e && std::atoi(e) == 1 ? 1 : 2;
+    }();
+    if (h->line_fmt == kFmtOcc && U == 1)
+      k_count_ctx<OccE, 1, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
+    else if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
       k_count_ctx<OccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
           h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
     else
