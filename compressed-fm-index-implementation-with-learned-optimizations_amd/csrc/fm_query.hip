@@ -1705,7 +1705,7 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
                        uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m) {
   if (!npat) return CS_OK;
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
-    static const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U)
+    const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U, read per call)
       const char* e = std::getenv("CS_FM_COUNT_U");
       const int u = e ? std::atoi(e) : 2;
       return u == 1 || u == 4 ? u : 2;
@@ -1760,7 +1760,7 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
   StreamBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8, st));
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
-    static const int U = [] {  // patterns per lane (tuning hook CS_FM_LOCATE_U: 1 or 2)
+    const int U = [] {  // patterns per lane (tuning hook CS_FM_LOCATE_U: 1 or 2, read per call)
       const char* e = std::getenv("CS_FM_LOCATE_U");
       return e && std::atoi(e) == 1 ? 1 : 2;
     }();

@@ -32,7 +32,9 @@ ENGINE_VARIANTS = {
     "auto_nowalk": {"CS_FM_WALK": "0", "CS_FM_FULL_SA": "0", "CS_FM_DEVICE_TEXT": "0"},
     "auto_nolctx": {"CS_FM_LCTX": "0"},             # count steps to the end (no left contexts)
     "auto_rec": {"CS_FM_CTX_RECORDS": "1"},         # context records at any table depth
-    "auto_rec16": {"CS_FM_CTX_RECORDS": "16"},      # compact 16-B context records at any table depth
+    # compact 16-B context records at any table depth; one pattern per lane in the
+    # staged count and locate kernels
+    "auto_rec16": {"CS_FM_CTX_RECORDS": "16", "CS_FM_COUNT_U": "1", "CS_FM_LOCATE_U": "1"},
     "auto_nosa": {"CS_FM_FULL_SA": "0"},            # locate walks (no full suffix array kept)
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
@@ -51,7 +53,7 @@ ENGINE_VARIANTS = {
 _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
           "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
           "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT", "CS_FM_PTAB_WMAX",
-          "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA", "CS_FM_DEVICE_TEXT")
+          "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA", "CS_FM_DEVICE_TEXT", "CS_FM_COUNT_U", "CS_FM_LOCATE_U")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
