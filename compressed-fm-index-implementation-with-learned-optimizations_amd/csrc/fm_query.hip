@@ -1497,8 +1497,17 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     }
   }
   if (sigma == 0) return CS_OK;
-  uint64_t cap = n / 2 > 4096 ? n / 2 : 4096;
+  // Entries: at most n/2 for DNA-like alphabets (sigma <= 4; C4 k = 15), 8n for larger
+  // ones, where a table character saves a multi-level step (C3, sigma = 256: k = 4,
+  // 2^32 entries, 34 GB: 2x the count rate of k = 3); at most 2^32, and the table
+  // leaves an eighth of HBM free.
+  uint64_t cap = sigma <= 4 ? n / 2 : 8 * n;
+  if (cap < 4096) cap = 4096;
   if (cap > (1ull << 32)) cap = 1ull << 32;
+  size_t free_b = 0, total_b = 0;
+  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
+  const uint64_t budget = free_b > total_b / 8 ? (free_b - total_b / 8) / 8 : 0;
+  if (cap > budget && budget >= 4096) cap = budget;
   uint32_t k = 0;
   uint64_t entries = 1;
   while (k < 32 && entries * sigma <= cap) {
