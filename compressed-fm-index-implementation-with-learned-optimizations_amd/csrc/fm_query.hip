@@ -1497,11 +1497,11 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     }
   }
   if (sigma == 0) return CS_OK;
-  // Entries: at most n/2 for DNA-like alphabets (sigma <= 4; C4 k = 15), 8n for larger
-  // ones, where a table character saves a multi-level step (C3, sigma = 256: k = 4,
-  // 2^32 entries, 34 GB: 2x the count rate of k = 3); at most 2^32, and the table
-  // leaves an eighth of HBM free.
-  uint64_t cap = sigma <= 4 ? n / 2 : 8 * n;
+  // Entries: at most n for DNA-like alphabets (sigma <= 4; C2 k = 13, C4 k = 15), 8n for
+  // larger ones, where a table character saves a multi-level step (C3, sigma = 256:
+  // k = 4, 2^32 entries, 34 GB: 2x the count rate of k = 3); at most 2^32, and the
+  // table leaves an eighth of HBM free.
+  uint64_t cap = sigma <= 4 ? n : 8 * n;
   if (cap < 4096) cap = 4096;
   if (cap > (1ull << 32)) cap = 1ull << 32;
   size_t free_b = 0, total_b = 0;
@@ -1629,20 +1629,22 @@ __global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict
 
 // Replace the 8-B prefix table by 32-B context records (narrow occurrence-engine
 // indexes with left contexts; C4: 34 GB for k = 15) when HBM allows (an eighth of the
-// device stays free) and the table spans at least 14 characters: records pay for
-// patterns of k+1 .. k+7 characters (the 20-mers of the DNA configs from k = 13 on)
-// and cost 4x the plain table's reads in bytes otherwise (C2, k = 12: 7.9e9 patterns/s
-// with records, 9.1e9 without).  CS_FM_CTX_RECORDS=0 keeps the plain table, =1 forces
+// device stays free) and the table spans at least 13 characters: records pay for
+// patterns of k+1 .. k+7 characters (the 20-mers of the DNA configs from k = 13 on:
+// C2, k = 13: 2.35e10 patterns/s with records, 1.64e10 without) and cost 4x the plain
+// table's reads in bytes otherwise (C2, k = 12: 7.9e9 with records, 9.1e9 without).  CS_FM_CTX_RECORDS=0 keeps the plain table, =1 forces
 // records for any k (test hook), =16 forces the compact 16-B records, which replace the
-// 32-B ones by default when the table's mean range is at most 4 rows (C4: n / 4^15 =
-// 3.7; a range wider than kRec16Ctx rows or a pattern with 6-7 characters left after the
-// table then reads its context sector).
+// 32-B ones by default from k = 15 when the table's mean range is at most 4 rows (C4:
+// n / 4^15 = 3.7; a range wider than kRec16Ctx rows or a pattern with 6-7 characters
+// left after the table then reads its context sector).
 cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   h->ptab_rec = 0;
   if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide || h->lctx_eb != 2) return CS_OK;
   const uint64_t entries = h->ptab_entries();
-  bool want = h->ptab_k >= 14;
-  uint32_t fmt = h->n <= 4 * entries ? 2 : 1;
+  // a record answers patterns of up to k + q characters: q = 7 (32 B) from k = 13 covers
+  // the 20-mers of the DNA workloads; the compact q = 5 still does from k = 15
+  bool want = h->ptab_k >= 13;
+  uint32_t fmt = h->ptab_k >= 15 && h->n <= 4 * entries ? 2 : 1;
   if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) {
     want = std::atoi(e) != 0;
     fmt = std::atoi(e) == 16 ? 2 : 1;
