@@ -173,6 +173,9 @@ constexpr uint64_t kPtabEsc = (1ull << 26) - 1;
 // has an escaped context); contexts of kRec16Q characters (10 bits, the low bits of the
 // rows' lctx entries) of rows 0-5 at bits 4 + 10i of dwords 1-2, rows 6-8 at bits
 // 10(i-6) of dword 3.
+// Quaternary-matrix records (ptab_rec 3, tables with at most 2 rows per k-mer on
+// average; C3: k = 4, 0.23): 16 B — sp, width, and the u32 contexts of rows 0-1.
+constexpr uint32_t kRecQCtx = 2;
 constexpr uint32_t kRecCtx = 12;
 constexpr uint32_t kRec16Ctx = 9;
 constexpr uint32_t kRec16Q = 5;
@@ -192,6 +195,12 @@ __device__ __forceinline__ void rec16_contexts(uint32_t y, uint32_t z, uint32_t 
 __device__ __forceinline__ bool ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
   if (ix.ptab_rec == 1) {
     const uint2 r = static_cast<const uint2*>(ix.ptab)[t * 4];
+    sp = r.x;
+    ep = (uint64_t)r.x + r.y;
+    return true;
+  }
+  if (ix.ptab_rec == 3) {
+    const uint2 r = static_cast<const uint2*>(ix.ptab)[t * 2];
     sp = r.x;
     ep = (uint64_t)r.x + r.y;
     return true;

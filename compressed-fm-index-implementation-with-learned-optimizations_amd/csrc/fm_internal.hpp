@@ -78,7 +78,7 @@ struct cs_fm_index {
 
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
   uint32_t ptab_rec = 0;             // prefix-table entries: 0 plain, 1 32-B / 2 16-B context records
-  uint32_t ptab_entry_bytes() const { return ptab_rec == 1 ? 32 : ptab_rec == 2 ? 16 : 8; }  // plain: 2 x u32 / packed wide
+  uint32_t ptab_entry_bytes() const { return ptab_rec == 1 ? 32 : ptab_rec >= 2 ? 16 : 8; }  // plain: 2 x u32 / packed wide
   uint64_t ptab_entries() const {
     if (!ptab_k) return 0;
     uint64_t e = 1;

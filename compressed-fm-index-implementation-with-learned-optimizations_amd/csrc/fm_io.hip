@@ -183,7 +183,7 @@ cs_status meta_parse(const std::string& text, cs_fm_index* h,
   h->nlmodel = kv["nlmodel"];
   h->lmodel_shift = (uint32_t)kv["lmodel_shift"];
   h->ptab_rec = (uint32_t)kv["ptab_rec"];
-  if (h->ptab_rec > 2) {
+  if (h->ptab_rec > 3) {
     set_error("bad ptab_rec in " + what);
     return CS_ERR_INVALID;
   }

@@ -419,7 +419,9 @@ __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable
       t = t * ix.ptab_sigma + d;
     }
     if (ok && ptab_at(ix, t, sp, ep)) {
-      if (bytes) *bytes += ix.ptab_rec == 1 ? 32u : ix.ptab_rec == 2 ? 16u : 8u;
+      if (bytes) *bytes += ix.ptab_rec == 1 ? 32u : ix.ptab_rec >= 2 ? 16u : 8u;
+      if (inl && ix.ptab_rec == 3 && ep - sp <= kRecQCtx)
+        *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4 + 2;
       if (inl && ix.ptab_rec == 1) *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 8 + 2;
       if (inl && ix.ptab_rec == 2) {
         const uint32_t* r = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4;
@@ -466,7 +468,7 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
 enum : uint32_t { kCtxNone = 0, kCtxAbsent = 1, kCtxOk = 2 };
 // whether a record's inline contexts answer k characters over a w-row range
 __device__ __forceinline__ bool rec_inline(const DevIndex& ix, uint64_t k, uint64_t w) {
-  return ix.ptab_rec == 2 ? k <= kRec16Q : w <= kRecCtx;
+  return ix.ptab_rec == 2 ? k <= kRec16Q : ix.ptab_rec == 3 ? w <= kRecQCtx : w <= kRecCtx;
 }
 // inl: the contexts of a context record whose range [sp, ep) is at most kRecCtx rows
 // (already read with the record: no further access), else null.
@@ -491,7 +493,13 @@ __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTabl
   const uint32_t mask = (kb >= 32 ? ~0u : ((1u << kb) - 1u)) | (kEsc ? kCtxEsc : 0u);
   uint4 w[4];
   uint32_t lo, hi;  // rows [lo, hi) of the 2R from base
-  if (kEsc && inl) {
+  if (!kEsc && inl) {  // quaternary-matrix record: rows sp, sp+1 (u32 entries)
+    base = sp;
+    lo = 0;
+    hi = (uint32_t)(ep - sp);
+    w[0] = make_uint4(inl[0], inl[1], 0, 0);
+    w[1] = w[2] = w[3] = make_uint4(0, 0, 0, 0);
+  } else if (kEsc && inl) {
     base = sp;
     lo = 0;
     hi = (uint32_t)(ep - sp);
@@ -1627,6 +1635,20 @@ __global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict
   }
 }
 
+// Quaternary-matrix records (fm_device.hpp kRecQCtx): sp, width, contexts of rows 0-1.
+__global__ __launch_bounds__(kBlk) void k_fill_records_q(const uint2* __restrict__ tab,
+                                                         uint64_t entries,
+                                                         const uint32_t* __restrict__ lctx,
+                                                         uint4* __restrict__ rec) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
+    const uint2 e = tab[t];
+    const uint32_t w = e.y - e.x;
+    rec[t] = make_uint4(e.x, w, w > 0 && w <= kRecQCtx ? lctx[e.x] : 0u,
+                        w > 1 && w <= kRecQCtx ? lctx[e.x + 1] : 0u);
+  }
+}
+
 // Replace the 8-B prefix table by 32-B context records (narrow occurrence-engine
 // indexes with left contexts; C4: 34 GB for k = 15) when HBM allows (an eighth of the
 // device stays free) and the table spans at least 13 characters: records pay for
@@ -1639,8 +1661,32 @@ __global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict
 // left after the table then reads its context sector).
 cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   h->ptab_rec = 0;
-  if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide || h->lctx_eb != 2) return CS_OK;
+  if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide) return CS_OK;
   const uint64_t entries = h->ptab_entries();
+  if (h->lctx_eb == 4) {  // quaternary matrix: 16-B records when ranges average <= 2 rows
+    if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
+      if (std::atoi(e) == 0) return CS_OK;
+    if (h->n > kRecQCtx * entries) return CS_OK;
+    size_t free_q = 0, total_q = 0;
+    FMX_HIP(hipMemGetInfo(&free_q, &total_q));
+    if (entries * 16 + total_q / 8 > free_q) return CS_OK;
+    void* rq = nullptr;
+    FMX_HIP(hipMalloc(&rq, entries * 16));
+    k_fill_records_q<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
+        static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint32_t*>(h->d_lctx),
+        static_cast<uint4*>(rq));
+    hipError_t eq = hipGetLastError();
+    if (eq == hipSuccess) eq = hipStreamSynchronize(st);
+    if (eq != hipSuccess) {
+      (void)hipFree(rq);
+      return hip_fail(eq, "context records");
+    }
+    FMX_HIP(hipFree(h->d_ptab));
+    h->d_ptab = rq;
+    h->ptab_rec = 3;
+    return CS_OK;
+  }
+  if (h->lctx_eb != 2) return CS_OK;
   // a record answers patterns of up to k + q characters: q = 7 (32 B) from k = 13 covers
   // the 20-mers of the DNA workloads; the compact q = 5 still does from k = 15
   bool want = h->ptab_k >= 13;

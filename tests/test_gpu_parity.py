@@ -219,6 +219,11 @@ def test_engine_choice(built):
         rec = {"1": 32, "16": 16}.get(os.environ.get("CS_FM_CTX_RECORDS", ""), 0)
         if not (ctx and engine in (1, 3) and not wide and info.prefix_k):
             rec = 0
+        # quaternary matrix: 16-B records (u32 contexts of 2 rows) when the table's
+        # ranges average at most 2 rows
+        if (engine == 2 and ctx and not wide and info.prefix_k and os.environ.get("CS_FM_CTX_RECORDS") != "0"
+                and info.n <= 2 * info.prefix_sigma ** info.prefix_k):
+            rec = 16
         assert info.record_bytes == rec, name
         assert info.text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0"), name
         assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
