@@ -18,6 +18,6 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 BENCH=(python3 "$ROOT/bench.py" --no-cpu --p50-calls 0 "$@")
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${BENCH[@]}" > "$OUT/bench_trace.json" 2> "$OUT/trace.err"
-timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_count|k_walk_lines|k_walk<|k_locate|k_build_lctx" --output-format csv -d "$OUT/pmc_fetch" -o run -- "${BENCH[@]}" > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
-timeout -k 10 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_count|k_walk_lines|k_walk<|k_locate|k_build_lctx" --output-format csv -d "$OUT/pmc_l2" -o run -- "${BENCH[@]}" > "$OUT/bench_l2.json" 2> "$OUT/l2.err"
+timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_count|k_walk_lines|k_walk<|k_locate|k_build_lctx|k_extract" --output-format csv -d "$OUT/pmc_fetch" -o run -- "${BENCH[@]}" > "$OUT/bench_fetch.json" 2> "$OUT/fetch.err"
+timeout -k 10 900 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex "k_count|k_walk_lines|k_walk<|k_locate|k_build_lctx|k_extract" --output-format csv -d "$OUT/pmc_l2" -o run -- "${BENCH[@]}" > "$OUT/bench_l2.json" 2> "$OUT/l2.err"
 python3 "$ROOT/profiles/summarize.py" "$OUT" "$TAG"

@@ -30,10 +30,11 @@ def rows(pattern):
 
 def short(name):
     if "k_count_ctx" in name:  # template <int U, bool kLoc>: count or locate phase 1
-        return "k_count_ctx_loc" if "Lb1E" in name else "k_count_ctx"
+        return "k_count_ctx_loc" if ("Lb1E" in name or ", true>" in name) else "k_count_ctx"
     for k in ("k_count_bytes", "k_count_one", "k_count_ctx", "k_count", "k_build_lctx", "k_walk_lines", "k_walk_pack",
               "k_walk_base", "k_walk_samples", "k_walk", "k_occ_pack", "k_occ_base", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt_ssa", "k_bwt",
-              "k_build_ptab",
+              "k_build_ptab", "k_locate_sa_wide", "k_locate_sa", "k_extract_text", "k_extract",
+              "k_fill_records16", "k_fill_records_q", "k_fill_records",
               "k_partition", "k_pack_level", "k_init_keys", "k_double_keys", "k_heads",
               "k_scatter_rank", "k_bwt_ssa", "k_hist", "k_text", "k_patterns", "k_indep", "k_chain"):
         if k in name:
