@@ -26,6 +26,9 @@ LIB_PATH = os.path.join(_HERE, "libcs_fmindex.so")
 CS_OK, CS_ERR_INVALID, CS_ERR_OOM, CS_ERR_HIP = 0, 1, 2, 3
 CS_ERR_LF_OVERRUN, CS_ERR_SSA_RANGE, CS_ERR_CAPACITY, CS_ERR_UNSUPPORTED, CS_ERR_NO_DEVICE = 4, 5, 6, 7, 8
 
+# query flags (include/cs_fmindex.h CS_Q_*): results unchanged, structures left out
+Q_NO_PREFIX, Q_NO_CONTEXTS, Q_NO_FULL_SA, Q_NO_WALK_LINES = 1, 2, 4, 8
+
 _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)
 _u32p = C.POINTER(C.c_uint32)
@@ -34,6 +37,11 @@ _vp = C.c_void_p
 
 class cs_build_params(C.Structure):
     _fields_ = [("S", C.c_uint32), ("s", C.c_uint32), ("ssa_stride", C.c_uint32), ("eps", C.c_double)]
+
+
+class cs_count_out(C.Structure):
+    _fields_ = [("d_counts", C.c_void_p), ("width", C.c_uint32), ("d_exc", C.c_void_p),
+                ("exc_cap", C.c_uint64), ("d_exc_n", C.c_void_p)]
 
 
 class cs_fm_info(C.Structure):
@@ -77,9 +85,24 @@ SIGNATURES = {
     "cs_fm_export_parts": (C.c_int, [_vp, C.POINTER(_vp), _vp]),
     "cs_fm_import": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(_vp), C.c_uint32, C.c_int,
                                C.POINTER(_vp)]),
+    "cs_fm_export_part_ptrs": (C.c_int, [_vp, C.POINTER(_vp), C.c_uint32]),
+    "cs_fm_import_alloc": (C.c_int, [C.c_char_p, C.c_uint64, C.c_int, C.POINTER(_vp),
+                                     C.POINTER(_vp), C.c_uint32]),
+    "cs_fm_import_commit": (C.c_int, [_vp]),
     "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_extract_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
+    "cs_fm_count_bytes_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, C.c_uint32, _vp]),
+    "cs_fm_count_batch_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64,
+                                              C.POINTER(cs_count_out), C.c_uint32, _vp]),
+    "cs_fm_count_packed_device": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64,
+                                            C.POINTER(cs_count_out), C.c_uint32, _vp]),
+    "cs_fm_locate_ranges_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
+                                                _u64p, C.c_uint32, _vp]),
+    "cs_fm_locate_walk_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp,
+                                              C.c_uint32, _vp]),
+    "cs_fm_locate_walk_steps_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp,
+                                                 C.c_uint32, _vp]),
     "cs_fm_count_fixed_device": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
     "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
                                              _u64p, _vp]),
@@ -94,6 +117,8 @@ SIGNATURES = {
     "cs_fm_bwt_device": (C.c_int, [_vp, _vp, _vp]),
     "cs_fm_get_ssa": (C.c_int, [_vp, _u64p, C.c_uint64, _u64p]),
     "cs_sa_build": (C.c_int, [_u8p, C.c_uint64, _u32p, C.c_int]),
+    "cs_counts_wire_bytes": (C.c_uint64, [C.c_uint64, C.c_uint64]),
+    "cs_counts_pack_wire": (C.c_int, [_vp, C.c_uint64, C.c_uint64, _vp, _vp]),
     # include/cs_synth.h
     "cs_synth_text_device": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, _vp, _vp]),
     "cs_synth_patterns_device": (C.c_int, [_vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
@@ -256,6 +281,25 @@ class FMIndex:
         n = int(dict(l.split(" ", 1) for l in meta.decode().splitlines() if " " in l)["n"])
         return FMIndex(h, n)
 
+    def export_part_ptrs(self, nparts: int):
+        """Device addresses of the index's own image parts (read-only)."""
+        arr = (_vp * max(nparts, 1))()
+        _check(lib().cs_fm_export_part_ptrs(self._h, arr, nparts))
+        return [int(arr[i] or 0) for i in range(nparts)]
+
+    @staticmethod
+    def import_alloc(meta: bytes, nparts: int, device: int = 0):
+        """-> (index, [part addresses]): a handle with its parts allocated for the caller
+        to fill (e.g. receive a broadcast into); call import_commit() afterwards."""
+        arr = (_vp * max(nparts, 1))()
+        h = _vp()
+        _check(lib().cs_fm_import_alloc(meta, len(meta), device, C.byref(h), arr, nparts))
+        n = int(dict(l.split(" ", 1) for l in meta.decode().splitlines() if " " in l)["n"])
+        return FMIndex(h, n), [int(arr[i] or 0) for i in range(nparts)]
+
+    def import_commit(self):
+        _check(lib().cs_fm_import_commit(self._h))
+
     @staticmethod
     def open_directory(path: str, device: int | None = None):
         """Open an index written by save_directory (the reference's TODO,
@@ -365,19 +409,52 @@ class FMIndex:
         _check(lib().cs_fm_extract_device(self._h, d_pos, d_len, d_out_offs, k, d_out,
                                           stream or None))
 
-    def count_bytes_device(self, d_pats, d_offs, npat, d_out, stream=0):
-        """Per-query algorithmic HBM bytes of the search (roofline accounting)."""
-        _check(lib().cs_fm_count_bytes_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
+    def count_device_ex(self, d_pats, d_offs, npat, d_out, width=8, flags=0, fixed_m=0,
+                        d_exc=None, exc_cap=0, d_exc_n=None, stream=0):
+        """count() of a device batch, general form (cs_fm_count_batch_device_ex): d_offs
+        or None for npat patterns of length fixed_m back to back; counts as uint64
+        (width 8), uint32 (4) or uint8 with (index, count) pairs for counts >= 255 (1);
+        flags Q_* leave structures out (same results)."""
+        o = cs_count_out(d_out, width, d_exc, exc_cap, d_exc_n)
+        _check(lib().cs_fm_count_batch_device_ex(self._h, d_pats, d_offs, fixed_m, npat,
+                                                 C.byref(o), flags, stream or None))
 
-    def locate_ranges_device(self, d_pats, d_offs, npat, limit, d_sp, d_out_offs, stream=0) -> int:
+    def count_packed_device(self, d_packed, m, npat, d_out, width=8, flags=0, d_exc=None,
+                            exc_cap=0, d_exc_n=None, stream=0):
+        """count() of 2-bit packed DNA patterns (uint64 each, character i = "ACGT"[(x >> 2i)
+        & 3], m <= 32): cs_fm_count_packed_device."""
+        o = cs_count_out(d_out, width, d_exc, exc_cap, d_exc_n)
+        _check(lib().cs_fm_count_packed_device(self._h, d_packed, m, npat, C.byref(o), flags,
+                                               stream or None))
+
+    def count_bytes_device(self, d_pats, d_offs, npat, d_out, stream=0, flags=0):
+        """Per-query algorithmic HBM bytes of the search (roofline accounting)."""
+        _check(lib().cs_fm_count_bytes_device_ex(self._h, d_pats, d_offs, npat, d_out, flags,
+                                                 stream or None))
+
+    def locate_ranges_device(self, d_pats, d_offs, npat, limit, d_sp, d_out_offs, stream=0,
+                             flags=0) -> int:
         total = C.c_uint64()
-        _check(lib().cs_fm_locate_ranges_device(self._h, d_pats, d_offs, npat, limit, d_sp,
-                                                d_out_offs, C.byref(total), stream or None))
+        _check(lib().cs_fm_locate_ranges_device_ex(self._h, d_pats, d_offs, npat, limit, d_sp,
+                                                   d_out_offs, C.byref(total), flags,
+                                                   stream or None))
         return total.value
 
-    def locate_walk_device(self, d_sp, d_out_offs, npat, total, d_out_pos, stream=0, sync=True):
+    def locate_walk_device(self, d_sp, d_out_offs, npat, total, d_out_pos, stream=0, sync=True,
+                           flags=0):
+        if flags:
+            if not sync:
+                raise ValueError("flags need the synchronous walk")
+            _check(lib().cs_fm_locate_walk_device_ex(self._h, d_sp, d_out_offs, npat, total,
+                                                     d_out_pos, flags, stream or None))
+            return
         f = lib().cs_fm_locate_walk_device if sync else lib().cs_fm_locate_walk_device_async
         _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, stream or None))
+
+    def locate_walk_steps_device(self, d_sp, d_out_offs, npat, total, d_steps, stream=0, flags=0):
+        """LF steps of each reported row's walk (measurement twin of the walk)."""
+        _check(lib().cs_fm_locate_walk_steps_device(self._h, d_sp, d_out_offs, npat, total, d_steps,
+                                                    flags, stream or None))
 
     def locate_check(self, stream=0):
         _check(lib().cs_fm_locate_check(self._h, stream or None))
@@ -429,6 +506,27 @@ class FMIndex:
         return out[: len(p)]
 
 
+def pack_dna(patterns) -> np.ndarray:
+    """Equal-length ACGT patterns (m <= 32) -> one uint64 each, character i in bits 2i..2i+1
+    (A=0, C=1, G=2, T=3): the input of count_packed_device."""
+    pats = [_bytes(p) for p in patterns]
+    lut = np.full(256, 255, np.uint8)
+    for i, c in enumerate(b"ACGT"):
+        lut[c] = i
+    out = np.zeros(len(pats), np.uint64)
+    if not pats:
+        return out
+    a = np.frombuffer(b"".join(pats), np.uint8).reshape(len(pats), -1)
+    if a.shape[1] > 32:
+        raise ValueError("packed DNA patterns hold at most 32 characters")
+    d = lut[a]
+    if (d == 255).any():
+        raise ValueError("packed DNA patterns take A, C, G, T only")
+    for i in range(a.shape[1]):
+        out |= d[:, i].astype(np.uint64) << np.uint64(2 * i)
+    return out
+
+
 def synth_text_device(kind: str, seed: int, length: int, d_out: int, stream: int = 0):
     """SURVEY §8(d) text (kind 'dna' | 'bytes'), length+1 bytes incl. terminator."""
     _check(lib().cs_synth_text_device(0 if kind == "dna" else 1, seed, length, d_out, stream or None))
@@ -447,6 +545,16 @@ def synth_random_patterns_device(kind: str, m: int, first: int, npat: int, seed:
     k = {"dna": 0, "bytes": 1}[kind]
     _check(lib().cs_synth_random_patterns_device(k, m, first, npat, seed, d_pats, d_offs,
                                                  stream or None))
+
+
+def counts_wire_bytes(npat: int, cap: int) -> int:
+    """Size of the gather wire form of npat counts with cap overflow pairs."""
+    return int(lib().cs_counts_wire_bytes(npat, cap))
+
+
+def counts_pack_wire(d_counts: int, npat: int, cap: int, d_wire: int, stream: int = 0):
+    """Pack a device uint64 count vector into its wire form (cs_counts_pack_wire)."""
+    _check(lib().cs_counts_pack_wire(d_counts, npat, cap, d_wire, stream or None))
 
 
 def sa_build(text, device: int = 0) -> np.ndarray:

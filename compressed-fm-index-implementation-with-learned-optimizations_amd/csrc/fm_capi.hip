@@ -434,6 +434,79 @@ cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
   return launch_count_bytes(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
 }
 
+cs_status cs_fm_count_bytes_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
+                                      const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
+                                      uint32_t flags, void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (npat && (!d_offs || !d_out)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_count_bytes(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream, flags);
+}
+
+// cs_count_out -> the kernels' CountOut, validated
+static cs_status count_out(const cs_fm_index* h, const cs_count_out* o, uint64_t npat,
+                           CountOut& co) {
+  if (!o || (npat && !o->d_counts)) {
+    set_error("null count output");
+    return CS_ERR_INVALID;
+  }
+  if (o->width != 8 && o->width != 4 && o->width != 1) {
+    set_error("count width must be 8, 4 or 1");
+    return CS_ERR_INVALID;
+  }
+  if (o->width == 4 && h->n >= (1ull << 32)) {
+    set_error("uint32 counts need n < 2^32");
+    return CS_ERR_INVALID;
+  }
+  if (o->width == 1 && (!o->d_exc_n || (o->exc_cap && !o->d_exc))) {
+    set_error("uint8 counts need an overflow counter (and a pair buffer for exc_cap > 0)");
+    return CS_ERR_INVALID;
+  }
+  co = CountOut{o->d_counts, o->d_exc, reinterpret_cast<unsigned long long*>(o->d_exc_n),
+                o->width == 1 ? o->exc_cap : 0, o->width};
+  return CS_OK;
+}
+
+cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
+                                      const uint64_t* d_offs, uint64_t fixed_m, uint64_t npat,
+                                      const cs_count_out* out, uint32_t flags, void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  CountOut co;
+  if ((s = count_out(h, out, npat, co)) != CS_OK) return s;
+  if (npat && !d_offs && fixed_m && !d_pats) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_count_ex(h, d_pats, d_offs, npat, co, flags, (hipStream_t)stream,
+                         d_offs ? 0 : fixed_m, false);
+}
+
+cs_status cs_fm_count_packed_device(const cs_fm_index* h, const uint64_t* d_packed, uint32_t m,
+                                    uint64_t npat, const cs_count_out* out, uint32_t flags,
+                                    void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  CountOut co;
+  if ((s = count_out(h, out, npat, co)) != CS_OK) return s;
+  if (m > 32) {
+    set_error("packed DNA patterns hold at most 32 characters");
+    return CS_ERR_INVALID;
+  }
+  if (npat && !d_packed) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_count_ex(h, reinterpret_cast<const uint8_t*>(d_packed), nullptr, npat, co, flags,
+                         (hipStream_t)stream, m, true);
+}
+
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
                             uint64_t npat, uint64_t* out_counts, void* stream) {
   DeviceScope dscope;
@@ -602,14 +675,58 @@ cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream) {
 // share the handle's flag (the handle is immutable after creation).
 static cs_status walk_checked(const cs_fm_index* h, const uint64_t* d_sp,
                               const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                              uint64_t* d_out_pos, hipStream_t st) {
+                              uint64_t* d_out_pos, hipStream_t st, uint32_t flags = 0,
+                              uint32_t steps_only = 0) {
   StreamBuf err;
   FMX_HIP(err.alloc(8, st));
   FMX_HIP(hipMemsetAsync(err.p, 0xFF, 8, st));
   unsigned long long* e = err.as<unsigned long long>();
-  cs_status s = launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, st, e);
+  cs_status s = launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, st, e, flags,
+                                   steps_only);
   if (s != CS_OK) return s;
   return check_locate_error(h, e, st);
+}
+
+cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
+                                        const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                                        uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                                        uint32_t flags, void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (!total || !d_out_offs || (npat && (!d_offs || !d_sp))) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_locate_ranges(h, d_pats, d_offs, npat, limit, d_sp, d_out_offs, total,
+                              (hipStream_t)stream, flags);
+}
+
+cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
+                                      const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                                      uint64_t* d_out_pos, uint32_t flags, void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return walk_checked(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream, flags);
+}
+
+cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,
+                                         const uint64_t* d_out_offs, uint64_t npat,
+                                         uint64_t total, uint64_t* d_steps, uint32_t flags,
+                                         void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (total && (!d_sp || !d_out_offs || !d_steps)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return walk_checked(h, d_sp, d_out_offs, npat, total, d_steps, (hipStream_t)stream, flags, 1);
 }
 
 cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,

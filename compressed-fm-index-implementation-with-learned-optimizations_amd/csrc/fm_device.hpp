@@ -134,6 +134,37 @@ struct DevIndex {
 constexpr uint32_t kCtxQ = 7;
 constexpr uint32_t kCtxEsc = 0x8000u;
 
+// Where a batch count writes (cs_count_out): uint64 counts (the reference's type), uint32
+// (exact when n < 2^32, checked by the caller), or uint8 with counts >= 255 stored as 255
+// and listed as (pattern, count) pairs behind an atomic counter (pairs past exc_cap are
+// dropped; the counter still counts them).
+struct CountOut {
+  void* out;
+  uint64_t* exc;
+  unsigned long long* exc_n;
+  uint64_t exc_cap;
+  uint32_t width;
+};
+// W: the width when known at compile time (8, 4, 1), 0 = o.width
+template <int W>
+__device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint64_t v) {
+  const uint32_t w = W ? (uint32_t)W : o.width;
+  if (w == 8) {
+    static_cast<uint64_t*>(o.out)[q] = v;
+  } else if (w == 4) {
+    static_cast<uint32_t*>(o.out)[q] = (uint32_t)v;
+  } else {
+    static_cast<uint8_t*>(o.out)[q] = (uint8_t)(v < 255 ? v : 255);
+    if (v >= 255) {
+      const unsigned long long e = atomicAdd(o.exc_n, 1ull);
+      if (e < o.exc_cap) {
+        o.exc[2 * e] = q;
+        o.exc[2 * e + 1] = v;
+      }
+    }
+  }
+}
+
 // A single pattern passed by value in kernel arguments (k_count_one).
 struct OnePattern {
   static constexpr uint32_t kMax = 128;

@@ -163,23 +163,29 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
 // d_offs == nullptr: npat patterns of length fixed_m at stride fixed_m
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m = 0);
+// the general form: output width (fmx::CountOut), query flags (CS_Q_*), packed DNA input
+// (d_pats = one uint64 per pattern of fixed_m 2-bit characters)
+cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                          uint64_t npat, const fmx::CountOut& co, uint32_t flags, hipStream_t st,
+                          uint64_t fixed_m, bool packed);
 cs_status launch_count_one(const cs_fm_index* h, const fmx::OnePattern& p, uint64_t* out_host,
                            hipStream_t st);
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                             uint64_t npat, uint64_t* d_out, hipStream_t st);
+                             uint64_t npat, uint64_t* d_out, hipStream_t st, uint32_t flags = 0);
 // the resident server kernel (one wave) on the handle's server stream
 cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t idle_ticks,
                               uint64_t life_ticks);
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
-                               hipStream_t st);
+                               hipStream_t st, uint32_t flags = 0);
 // err: device word receiving the smallest overrunning row index (UINT64_MAX = none);
 // null = the handle's shared flag (the asynchronous API, cs_fm_locate_check)
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st,
-                             unsigned long long* err = nullptr);
+                             unsigned long long* err = nullptr, uint32_t flags = 0,
+                             uint32_t steps_only = 0);
 // reads (and re-arms) the overrun word `err` (null = the handle's shared flag)
 cs_status check_locate_error(const cs_fm_index* h, unsigned long long* err, hipStream_t st);
 cs_status launch_level_rank1(const cs_fm_index* h, int level, const uint64_t* d_pos, uint64_t k,

@@ -400,4 +400,64 @@ cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d
   return CS_OK;
 }
 
+cs_status cs_fm_export_part_ptrs(const cs_fm_index* hc, const void** d_parts, uint32_t cap) {
+  if (!hc || !d_parts) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  cs_fm_index* h = const_cast<cs_fm_index*>(hc);  // parts are only read
+  const std::vector<Part> parts = index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr);
+  if (cap < parts.size()) {
+    set_error("export: part pointer array too small");
+    return CS_ERR_CAPACITY;
+  }
+  for (size_t i = 0; i < parts.size(); ++i) d_parts[i] = *parts[i].dptr;
+  return CS_OK;
+}
+
+cs_status cs_fm_import_alloc(const char* meta, uint64_t meta_len, int device, cs_fm_index** out,
+                             void** d_parts, uint32_t nparts) {
+  if (!meta || !out || !d_parts) {
+    set_error("null argument");
+    return CS_ERR_INVALID;
+  }
+  *out = nullptr;
+  auto* h = new cs_fm_index();
+  std::map<std::string, unsigned long long> kv;
+  cs_status s = meta_parse(std::string(meta, meta_len), h, kv, "device image");
+  if (s == CS_OK) s = need_device();
+  if (s != CS_OK) {
+    delete h;
+    return s;
+  }
+  h->device = device;
+  auto fail = [&](cs_status st) {
+    cs_fm_destroy(h);
+    return st;
+  };
+  DeviceScope ds;
+  if (ds.enter(device) != hipSuccess) return fail(hip_fail(hipGetLastError(), "hipSetDevice"));
+  const std::vector<Part> parts = index_parts(h, true, kv["has_wssa"] != 0, kv["has_sa"] != 0, kv["has_dtext"] != 0);
+  if (parts.size() != nparts) {
+    set_error("import: the image has a different number of parts than its meta");
+    return fail(CS_ERR_INVALID);
+  }
+  if ((s = alloc_parts(h, parts)) != CS_OK) return fail(s);
+  for (size_t i = 0; i < parts.size(); ++i) d_parts[i] = *parts[i].dptr;
+  *out = h;
+  return CS_OK;
+}
+
+cs_status cs_fm_import_commit(cs_fm_index* h) {
+  if (!h) {
+    set_error("null index handle");
+    return CS_ERR_INVALID;
+  }
+  DeviceScope ds;
+  FMX_HIP(ds.enter(h->device));
+  FMX_HIP(hipDeviceSynchronize());  // the caller's copies into the parts (any stream)
+  FMX_HIP(hipMemcpy(&h->h_table, h->d_table, sizeof(NodeTable), hipMemcpyDeviceToHost));
+  return CS_OK;
+}
+
 }  // extern "C"

@@ -44,6 +44,18 @@ __device__ __forceinline__ void load_table(NodeTable& T, const NodeTable* __rest
   for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
 }
 
+// A 2-bit packed DNA pattern (cs_fm_count_packed_device): character i is code
+// (x >> 2i) & 3 of "ACGT".  Indexes like the byte pointer of a byte-string pattern,
+// so every search helper takes either (template parameter PT).
+constexpr uint32_t kDnaSyms = 0x54474341u;  // 'A' 'C' 'G' 'T', little-endian
+struct PackedDna {
+  uint64_t x;
+  __device__ __forceinline__ uint32_t operator[](uint64_t i) const {
+    return (kDnaSyms >> (8u * (uint32_t)((x >> (2 * i)) & 3u))) & 0xFFu;
+  }
+};
+
+
 // One backward-search step (fm_index.cpp:90-96) for a symbol c present in the
 // text: [sp, ep) -> [C[c] + occ(c, sp), C[c] + occ(c, ep)).  Returns false when
 // the range empties (the reference's `return 0`).
@@ -405,8 +417,9 @@ struct QWM {
 // still to process (P[k-1] .. P[0]).  Requires m >= 1.
 // With context records, *inl receives the entry's contexts (kRecCtx u16 in 6 dwords),
 // or the compact record itself (fm_device.hpp kRec16Ctx) when it holds contexts.
+template <class PT>
 __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable& T,
-                                             const uint8_t* __restrict__ P, uint64_t m,
+                                             PT P, uint64_t m,
                                              uint64_t& sp, uint64_t& ep, uint64_t& k,
                                              uint64_t* bytes, const uint32_t** inl = nullptr) {
   if (inl) *inl = nullptr;
@@ -439,9 +452,9 @@ __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable
 
 // Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
 // range empties.  Requires m >= 1, n >= 1.
-template <class E>
+template <class E, class PT>
 __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
-                                                const uint8_t* __restrict__ P, uint64_t m,
+                                                PT P, uint64_t m,
                                                 uint64_t& sp_out, uint64_t& ep_out,
                                                 uint64_t* bytes = nullptr) {
   uint64_t sp, ep, k;
@@ -472,9 +485,9 @@ __device__ __forceinline__ bool rec_inline(const DevIndex& ix, uint64_t k, uint6
 }
 // inl: the contexts of a context record whose range [sp, ep) is at most kRecCtx rows
 // (already read with the record: no further access), else null.
-template <class Ent>
+template <class Ent, class PT>
 __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTable& T,
-                                              const uint8_t* __restrict__ P, uint32_t k,
+                                              PT P, uint32_t k,
                                               uint64_t sp, uint64_t ep, uint32_t& mm,
                                               uint64_t& base, uint64_t* bytes,
                                               const uint32_t* inl = nullptr) {
@@ -543,9 +556,9 @@ __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTabl
   return kCtxOk;
 }
 
-template <class Ent>
+template <class Ent, class PT>
 __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
-                                          const uint8_t* __restrict__ P, uint32_t k,
+                                          PT P, uint32_t k,
                                           uint64_t sp, uint64_t ep, uint64_t& cnt,
                                           uint64_t* bytes, const uint32_t* inl = nullptr) {
   uint32_t mm = 0;
@@ -556,17 +569,31 @@ __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T
   return true;
 }
 
+template <class E, class PT>
+__device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTable& T, PT P,
+                                               uint64_t k, uint64_t sp, uint64_t ep,
+                                               uint64_t* bytes, const uint32_t* inl);
+
 // count() of one pattern (fm_index.cpp:84-100), m >= 1, n >= 1: the backward
 // search, finished over the left contexts once at most kCtxQ characters remain and
 // the range is narrow (engines with contexts, when built).
-template <class E>
+template <class E, class PT>
 __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const NodeTable& T,
-                                                  const uint8_t* __restrict__ P, uint64_t m,
+                                                  PT P, uint64_t m,
                                                   uint64_t* bytes = nullptr) {
   uint64_t sp, ep, k;
   const uint32_t* inl;
   search_start(ix, T, P, m, sp, ep, k, bytes, &inl);
   if (sp >= ep) return 0;
+  return count_rest<E>(ix, T, P, k, sp, ep, bytes, inl);
+}
+
+// The rest of a count() from the range [sp, ep) (non-empty) with P[0..k) still to
+// process (fm_index.cpp:90-98); inl as search_start's.
+template <class E, class PT>
+__device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTable& T, PT P,
+                                               uint64_t k, uint64_t sp, uint64_t ep,
+                                               uint64_t* bytes, const uint32_t* inl) {
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
   bool ctx = E::kCtx && ix.lctx != nullptr;
   while (k > 0) {
@@ -597,9 +624,9 @@ constexpr uint32_t kLocSpanBits = 22;
 constexpr int kWalkAdjShift = 56;
 constexpr uint64_t kWalkRowMask = (1ull << kWalkAdjShift) - 1;
 
-template <class E>
+template <class E, class PT>
 __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const NodeTable& T,
-                                                  const uint8_t* __restrict__ P, uint64_t m,
+                                                  PT P, uint64_t m,
                                                   uint64_t& rec) {
   uint64_t sp, ep, k;
   const uint32_t* inl;
@@ -686,38 +713,47 @@ __global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix,
   }
 }
 
-template <class E>
-// offs == nullptr: patterns of one length fixed_m at stride fixed_m (cs_fm_count_fixed_device)
+// offs == nullptr: patterns of one length fixed_m at stride fixed_m (cs_fm_count_fixed_device);
+// kPacked: pats holds one uint64 per pattern, fixed_m <= 32 2-bit DNA characters (PackedDna)
+template <class E, bool kPacked>
 __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t npat,
-                                                uint64_t* __restrict__ out, uint64_t fixed_m) {
+                                                CountOut co, uint64_t fixed_m) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
   const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (q >= npat) return;
-  const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
   uint64_t res;
-  if (m == 0) res = ix.n;       // fm_index.cpp:80
-  else if (ix.n == 0) res = 0;  // :81
-  else {
-    res = count_pattern<E>(ix, T, pats + o0, m);
+  if constexpr (kPacked) {
+    const uint64_t x = reinterpret_cast<const uint64_t*>(pats)[q];
+    if (fixed_m == 0) res = ix.n;  // fm_index.cpp:80
+    else if (ix.n == 0) res = 0;   // :81
+    else res = count_pattern<E>(ix, T, PackedDna{x}, fixed_m);
+  } else {
+    const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
+    if (m == 0) res = ix.n;       // fm_index.cpp:80
+    else if (ix.n == 0) res = 0;  // :81
+    else res = count_pattern<E>(ix, T, pats + o0, m);
   }
-  out[q] = res;
+  store_count<0>(co, q, res);
 }
 
 // The batch count over occurrence lines with left contexts, the C4/C5 shape: a
-// pattern of m <= 32 bytes whose last k = ptab_k characters are in the prefix table
-// and whose other m - k <= kCtxQ characters are coded needs two dependent reads —
-// its table entry, then the context sector(s) of its range.  Each lane takes U
-// patterns (q0 + j * kBlk) and runs them in stages so their reads are in flight
-// together: (A) offsets and pattern bytes (realigned dword loads, not byte loads),
-// table index and context key; (B) the U table entries; (C) the U context sectors;
-// (D) counts.  Anything else — longer patterns, symbols outside the table alphabet,
-// wide ranges, escaped contexts — takes count_pattern, the general search.
-// kLoc: the same stages for locate's phase 1 (k_locate_ranges): out = min(count,
-// limit), rec = the pattern's locate record (locate_search), context windows only
-// when LF is one n-cycle (lf_exact).
+// pattern whose last k = ptab_k characters are in the prefix table and whose other
+// m - k <= kCtxQ characters are coded needs two dependent reads — its table entry,
+// then the context sector(s) of its range (one, when the entry is a context record
+// holding the range).  Each lane takes U patterns (q0 + j * kBlk) and runs them in
+// stages so their reads are in flight together: (A) offsets and pattern bytes
+// (realigned dword loads, not byte loads), table index and context key; (B) the U
+// table entries; (C) the U context sectors; (D) counts.  Anything else — patterns
+// over 32 characters, symbols outside the table alphabet, wide ranges, escaped
+// contexts — takes count_pattern, the general search (which reads the table entry
+// again: carrying the range across would cost the kernel a wave per SIMD).
+// kLoc: the same stages for locate's phase 1 (k_locate_ranges): co.out = min(count,
+// limit) as uint64, rec = the pattern's locate record (locate_search), context windows
+// only when LF is one n-cycle (lf_exact).
+// kPacked: one uint64 of 2-bit DNA per pattern (PackedDna), fixed_m characters.
 constexpr uint32_t kFastM = 32;
 
 // bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
@@ -734,10 +770,10 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
-template <class E, int U, bool kLoc>
+template <class E, int U, bool kLoc, bool kPacked, int W>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
-                                                    uint64_t npat, uint64_t* __restrict__ out,
+                                                    uint64_t npat, CountOut co,
                                                     uint64_t limit, uint64_t* __restrict__ rec,
                                                     uint64_t fixed_m) {
   // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
@@ -750,12 +786,13 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   __syncthreads();
+  uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
   const uint32_t K = ix.ptab_k;
   const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U];
   uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search
-  if (kLoc && q0 == 0) out[npat] = 0;  // scan slot for the total
+  if (kLoc && q0 == 0) cnt_out[npat] = 0;  // scan slot for the total
   // (A)
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -767,8 +804,14 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     m[j] = 0;
     t[j] = want[j] = k[j] = 0;
     if (q >= npat) continue;
-    o0[j] = offs ? offs[q] : q * fixed_m;
-    const uint64_t mm = offs ? offs[q + 1] - o0[j] : fixed_m;
+    uint64_t mm;
+    if constexpr (kPacked) {
+      o0[j] = reinterpret_cast<const uint64_t*>(pats)[q];  // the pattern itself
+      mm = fixed_m;
+    } else {
+      o0[j] = offs ? offs[q] : q * fixed_m;
+      mm = offs ? offs[q + 1] - o0[j] : fixed_m;
+    }
     m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
     if (mm == 0) {
       res[j] = kLoc ? 0 : ix.n;  // fm_index.cpp:80; locate: :109
@@ -776,16 +819,19 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     }
     if (ix.n == 0) continue;  // :81
     st[j] = 3;
-    if (mm > kFastM || mm < K || K == 0) continue;
+    if (mm < K || K == 0 || mm > kFastM) continue;
+    const uint32_t wl = (uint32_t)mm;
     uint32_t u[8];
-    load_pattern32(pats, o0[j], m[j], u);
+    if constexpr (!kPacked) load_pattern32(pats, o0[j], wl, u);
     const uint32_t kk = m[j] - K;
     bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
     uint32_t tt = 0, ww = 0;
 #pragma unroll
     for (uint32_t i = 0; i < kFastM; ++i) {
-      const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-      if (i >= kk && i < m[j]) {  // table part, most significant first
+      uint32_t b;
+      if constexpr (kPacked) b = PackedDna{o0[j]}[i];
+      else b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i >= wl - K && i < wl) {  // table part, most significant first
         const uint32_t d = cmap[b] & 0xFFu;
         ok &= d != kNoCode;
         tt = tt * ix.ptab_sigma + d;
@@ -844,10 +890,10 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
       st[j] = 0;
       res[j] = ep[j] - sp[j];
       rv[j] = sp[j];
-    } else if (st[j] == 2 && inl[j]) {
+    } else if (st[j] == 2 && inl[j] && ix.lctx) {
       bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record
       w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
-    } else if (st[j] == 2 && ep[j] - (sp[j] & ~15ull) <= 32) {
+    } else if (st[j] == 2 && ix.lctx && ep[j] - (sp[j] & ~15ull) <= 32) {
       bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
                                                       bs[j]);
@@ -900,10 +946,10 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (q < npat && st[j] != 3) {
       if (kLoc) {
-        out[q] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
+        cnt_out[q] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
         rec[q] = rv[j];
       } else {
-        out[q] = res[j];
+        store_count<W>(co, q, res[j]);
       }
     }
   }
@@ -918,13 +964,17 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   for (int j = 0; j < U; ++j) {
     if (st[j] != 3) continue;
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if (kLoc) {
+    if constexpr (kLoc) {
       uint64_t r;
       const uint64_t c = locate_search<E>(ix, T, pats + o0[j], m[j], r);
-      out[q] = c < limit ? c : limit;
+      cnt_out[q] = c < limit ? c : limit;
       rec[q] = r;
+    } else if constexpr (kPacked) {
+      const PackedDna P{o0[j]};
+      store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
     } else {
-      out[q] = count_pattern<E>(ix, T, pats + o0[j], m[j]);
+      const uint8_t* P = pats + o0[j];
+      store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
     }
   }
 }
@@ -1089,7 +1139,8 @@ template <class E, bool POW2>
 __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __restrict__ rows,
                                                uint64_t total, uint64_t chunk,
                                                uint64_t* __restrict__ out,
-                                               unsigned long long* __restrict__ err) {
+                                               unsigned long long* __restrict__ err,
+                                               uint32_t steps_only) {
   enum : uint32_t { kFetch = 0, kWalk = 1, kSample = 2, kDone = 3 };
   __shared__ NodeTable T;
   __shared__ unsigned long long next;
@@ -1119,7 +1170,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
     } else if (phase == kSample) {
       uint64_t s = smp + steps;  // :147-153
       s = s >= n ? s - n : s;
-      out[j] = s >= adj ? s - adj : s + n - adj;
+      out[j] = steps_only ? steps : s >= adj ? s - adj : s + n - adj;
       phase = kFetch;
     } else if (phase == kWalk) {
       // loop condition of fm_index.cpp:130: stop at a sampled row or after n steps
@@ -1196,7 +1247,8 @@ __device__ __forceinline__ uint64_t walk_lf(const DevIndex& ix, const NodeTable&
 template <class W, bool kQ>
 __global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t* __restrict__ rows,
                                                      uint64_t total, uint64_t* __restrict__ out,
-                                                     unsigned long long* __restrict__ err) {
+                                                     unsigned long long* __restrict__ err,
+                                                     uint32_t steps_only) {
   __shared__ NodeTable T;
   load_table(T, ix.table);
   __syncthreads();
@@ -1223,7 +1275,7 @@ __global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t
       const uint64_t sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
       uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps;  // :147-153
       s = s >= n ? s - n : s;
-      out[j] = s >= adj ? s - adj : s + n - adj;
+      out[j] = steps_only ? steps : s >= adj ? s - adj : s + n - adj;
       return;
     }
     pos = walk_lf<W, kQ>(ix, T, v, q, o, pos);
@@ -1235,7 +1287,8 @@ template <class W, bool kQ>
 __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t* __restrict__ rows,
                                                      uint64_t total, uint64_t chunk,
                                                      uint64_t* __restrict__ out,
-                                                     unsigned long long* __restrict__ err) {
+                                                     unsigned long long* __restrict__ err,
+                                                     uint32_t steps_only) {
   // Each lane cycles FETCH (row from the block's slice) -> WALK (one line per LF
   // step) -> SAMPLE (the mark's SA sample, with the next row's index) -> WALK ...
   // Every loop iteration issues at most one dependent load per lane and kind,
@@ -1306,7 +1359,7 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
     } else if (phase == kSample) {
       uint64_t s = smp + steps;  // :147-153
       s = s >= n ? s - n : s;
-      out[j] = s >= adj ? s - adj : s + n - adj;
+      out[j] = steps_only ? steps : s >= adj ? s - adj : s + n - adj;
       if (jn < end) {
         j = jn;
         pos = row & kWalkRowMask;
@@ -1457,6 +1510,24 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
       KERNEL<WM<Line32W>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                \
     else                                                                        \
       KERNEL<WM<Line64>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
+    FMX_HIP(hipGetLastError());                                                 \
+  } while (0)
+
+// Same, with a second template argument after the engine.
+#define FMX_DISPATCH2(h, KERNEL, TARG, GRID, ...)                               \
+  do {                                                                          \
+    if ((h)->line_fmt == kFmtOcc)                                               \
+      KERNEL<OccE, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
+    else if ((h)->line_fmt == kFmtLOcc)                                         \
+      KERNEL<LOccE, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                \
+    else if ((h)->line_fmt == kFmtQwm)                                          \
+      KERNEL<QWM, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                  \
+    else if ((h)->line_fmt == kFmtLine32)                                       \
+      KERNEL<WM<Line32>, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);           \
+    else if ((h)->line_fmt == kFmtLine32W)                                      \
+      KERNEL<WM<Line32W>, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);          \
+    else                                                                        \
+      KERNEL<WM<Line64>, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);           \
     FMX_HIP(hipGetLastError());                                                 \
   } while (0)
 
@@ -1758,33 +1829,77 @@ cs_status launch_bwt(const cs_fm_index* h, uint8_t* d_out, hipStream_t st) {
   return CS_OK;
 }
 
+// The index as one query sees it under the caller's query flags (cs_fmindex.h CS_Q_*):
+// the same structures with the prefix table, the left contexts / context records or the
+// walk lines left out, so a search runs the plain backward-search steps of the
+// reference (fm_index.cpp:84-98) and a walk its row-sampled SSA walk (:125-153).
+DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
+  DevIndex d = h->dev();
+  if (flags & CS_Q_NO_PREFIX) d.ptab_k = 0;
+  if (flags & CS_Q_NO_CONTEXTS) {
+    d.lctx = nullptr;
+    d.lctx_q = 0;
+  }
+  if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
+  return d;
+}
+
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                        uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m) {
+  CountOut co{d_out, nullptr, nullptr, 0, 8};
+  return launch_count_ex(h, d_pats, d_offs, npat, co, 0, st, fixed_m, false);
+}
+
+// the staged kernel at count width W: table entries (context records) of U patterns per
+// lane in flight together, then their context sectors or rank steps
+template <int W>
+void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t* d_pats,
+                         const uint64_t* d_offs, uint64_t npat, const CountOut& co,
+                         hipStream_t st, uint64_t fixed_m, bool packed) {
+  const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U, read per call)
+    const char* e = std::getenv("CS_FM_COUNT_U");
+    const int u = e ? std::atoi(e) : 2;
+    return u == 1 || u == 4 ? u : 2;
+  }();
+  const bool lo = h->line_fmt == kFmtLOcc;
+  const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
+  if (packed && lo)
+    k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
+                                                                nullptr, fixed_m);
+  else if (packed)
+    k_count_ctx<OccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
+                                                               nullptr, fixed_m);
+  else if (lo)
+    k_count_ctx<LOccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
+                                                                 nullptr, fixed_m);
+  else if (W == 8 && U == 1)
+    k_count_ctx<OccE, 1, false, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+  else if (W == 8 && U == 4)
+    k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+  else
+    k_count_ctx<OccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
+                                                                nullptr, fixed_m);
+}
+
+cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                          uint64_t npat, const CountOut& co, uint32_t flags, hipStream_t st,
+                          uint64_t fixed_m, bool packed) {
   if (!npat) return CS_OK;
-  if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
-    const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U, read per call)
-      const char* e = std::getenv("CS_FM_COUNT_U");
-      const int u = e ? std::atoi(e) : 2;
-      return u == 1 || u == 4 ? u : 2;
-    }();
-    const DevIndex ix = h->dev();
-    if (h->line_fmt == kFmtLOcc)
-      k_count_ctx<LOccE, 2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
-    else if (U == 1)
-      k_count_ctx<OccE, 1, false><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
-    else if (U == 2)
-      k_count_ctx<OccE, 2, false><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
-    else
-      k_count_ctx<OccE, 4, false><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, d_out, 0, nullptr, fixed_m);
+  const DevIndex ix = query_dev(h, flags);
+  if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.ptab_k) {
+    if (co.width == 8) launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
+    else if (co.width == 4) launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
+    else launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
-  FMX_DISPATCH(h, k_count, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat, d_out,
-               fixed_m);
+  const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
+  if (packed)
+    FMX_DISPATCH2(h, k_count, true, g, ix, d_pats, nullptr, npat, co, fixed_m);
+  else
+    FMX_DISPATCH2(h, k_count, false, g, ix, d_pats, d_offs, npat, co, fixed_m);
   return CS_OK;
 }
 
@@ -1803,36 +1918,38 @@ cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t 
 }
 
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                             uint64_t npat, uint64_t* d_out, hipStream_t st) {
+                             uint64_t npat, uint64_t* d_out, hipStream_t st, uint32_t flags) {
   if (!npat) return CS_OK;
-  FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), h->dev(), d_pats, d_offs, npat,
-               d_out);
+  FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), query_dev(h, flags), d_pats,
+               d_offs, npat, d_out);
   return CS_OK;
 }
 
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
-                               hipStream_t st) {
+                               hipStream_t st, uint32_t flags) {
   StreamBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8, st));
-  if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && h->d_lctx && h->ptab_k) {
+  const DevIndex ix = query_dev(h, flags);
+  if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.lctx && ix.ptab_k) {
     const int U = [] {  // patterns per lane (tuning hook CS_FM_LOCATE_U: 1 or 2, read per call)
       const char* e = std::getenv("CS_FM_LOCATE_U");
       return e && std::atoi(e) == 1 ? 1 : 2;
     }();
+    const CountOut co{cnt.p, nullptr, nullptr, 0, 8};
     if (h->line_fmt == kFmtOcc && U == 1)
-      k_count_ctx<OccE, 1, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
+      k_count_ctx<OccE, 1, true, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
     else if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
-      k_count_ctx<OccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
+      k_count_ctx<OccE, 2, true, false, 8><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
     else
-      k_count_ctx<LOccE, 2, true><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          h->dev(), d_pats, d_offs, npat, cnt.as<uint64_t>(), limit, d_sp, 0);
+      k_count_ctx<LOccE, 2, true, false, 8><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
     FMX_HIP(hipGetLastError());
   } else {
-    FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), h->dev(), d_pats,
+    FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), ix, d_pats,
                  d_offs, npat, limit, d_sp, cnt.as<uint64_t>());
   }
   size_t tb = 0;
@@ -1894,9 +2011,14 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa_wide(const uint32_t* __restr
 
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                             uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word) {
+                             uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word,
+                             uint32_t flags, uint32_t steps_only) {
   if (!total) return CS_OK;
-  if (h->d_sa && h->lf_exact) {  // full suffix array: one read per position
+  if (h->d_sa && h->lf_exact && !(flags & CS_Q_NO_FULL_SA)) {  // full suffix array: one read per position
+    if (steps_only) {  // no LF steps: one SA read per position
+      FMX_HIP(hipMemsetAsync(d_out_pos, 0, total * 8, st));
+      return CS_OK;
+    }
     StreamBuf wide;
     FMX_HIP(wide.alloc((total / (kLocSmall + 1) + 1) * 8 + 8, st));
     unsigned long long* nwide = wide.as<unsigned long long>();
@@ -1922,7 +2044,7 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   uint64_t chunk = (total + max_blocks - 1) / max_blocks;
   if (chunk < 64) chunk = 64;
   const unsigned blocks = (unsigned)((total + chunk - 1) / chunk);
-  const DevIndex ix = h->dev();
+  const DevIndex ix = query_dev(h, flags);
   unsigned long long* err =
       err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
   const uint64_t* r = rows.as<uint64_t>();
@@ -1931,45 +2053,45 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
     const char* e = std::getenv("CS_FM_WALK_PERSISTENT");
     return e && std::atoi(e) == 1;
   }();
-  if (h->d_walk && h->walk_marks == 2 && !persistent) {
+  if (ix.walk && h->walk_marks == 2 && !persistent) {
     const bool q = h->line_fmt == kFmtQwm;
     const unsigned g = grid_for(total, kBlk, 0xFFFFFFFFu);
     if (h->wide && q)
-      k_walk_short<WalkLineW, true><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+      k_walk_short<WalkLineW, true><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err, steps_only);
     else if (h->wide)
-      k_walk_short<WalkLineW, false><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+      k_walk_short<WalkLineW, false><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err, steps_only);
     else if (q)
-      k_walk_short<WalkLine, true><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
+      k_walk_short<WalkLine, true><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err, steps_only);
     else
-      k_walk_short<WalkLine, false><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err);
-  } else if (h->d_walk) {
+      k_walk_short<WalkLine, false><<<g, kBlk, 0, st>>>(ix, r, total, d_out_pos, err, steps_only);
+  } else if (ix.walk) {
     const bool q = h->line_fmt == kFmtQwm;
     if (h->wide && q)
-      k_walk_lines<WalkLineW, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+      k_walk_lines<WalkLineW, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
     else if (h->wide)
-      k_walk_lines<WalkLineW, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+      k_walk_lines<WalkLineW, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
     else if (q)
-      k_walk_lines<WalkLine, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+      k_walk_lines<WalkLine, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
     else
-      k_walk_lines<WalkLine, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+      k_walk_lines<WalkLine, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   } else if (h->line_fmt == kFmtQwm) {
-    if (pow2) k_walk<QWM, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<QWM, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<QWM, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
+    else k_walk<QWM, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   } else if (h->line_fmt == kFmtOcc) {
-    if (pow2) k_walk<OccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<OccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<OccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
+    else k_walk<OccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   } else if (h->line_fmt == kFmtLOcc) {
-    if (pow2) k_walk<LOccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<LOccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<LOccE, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
+    else k_walk<LOccE, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   } else if (h->line_fmt == kFmtLine32) {
-    if (pow2) k_walk<WM<Line32>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<WM<Line32>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<WM<Line32>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
+    else k_walk<WM<Line32>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   } else if (h->line_fmt == kFmtLine32W) {
-    if (pow2) k_walk<WM<Line32W>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<WM<Line32W>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<WM<Line32W>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
+    else k_walk<WM<Line32W>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   } else {
-    if (pow2) k_walk<WM<Line64>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
-    else k_walk<WM<Line64>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err);
+    if (pow2) k_walk<WM<Line64>, true><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
+    else k_walk<WM<Line64>, false><<<blocks, kBlk, 0, st>>>(ix, r, total, chunk, d_out_pos, err, steps_only);
   }
   FMX_HIP(hipGetLastError());
   return CS_OK;  // rows are freed in stream order after the walk

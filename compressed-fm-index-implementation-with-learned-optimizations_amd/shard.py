@@ -117,13 +117,27 @@ def sharded_count(count_fn, total: int, world: int, rank: int, device, dst: int 
     return gather_counts(local.to(device), total, world, rank, dst)
 
 
+def device_bytes(ptr: int, nbytes: int, device) -> torch.Tensor:
+    """A uint8 tensor over nbytes of device memory the engine owns (no copy), through
+    __cuda_array_interface__: lets a collective send from / receive into the index's
+    own parts."""
+    class _Arr:
+        pass
+    a = _Arr()
+    a.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                  "strides": None, "version": 2}
+    return torch.as_tensor(a, device=device)
+
+
 def replicate_index(fm, idx, src: int, rank: int, world: int, device):
-    """The index built (or opened) on rank `src` on every rank's `device`: its device
-    image (cs_fm_export_meta / cs_fm_export_parts) is broadcast part by part — over
-    RCCL/xGMI with the nccl backend, staged through host memory with gloo — and
-    imported (cs_fm_import).  `fm` is the package, `idx` the FMIndex on src (None on
-    the other ranks).  SURVEY §8(e): replicate by broadcast instead of building on
-    every GPU."""
+    """The index built (or opened) on rank `src` on every rank's `device`, at one
+    index's worth of HBM per GPU: rank src broadcasts each part of its device image
+    straight from the index's own memory (cs_fm_export_part_ptrs), and the other ranks
+    receive straight into the parts of a handle allocated for it (cs_fm_import_alloc,
+    then cs_fm_import_commit).  RCCL over xGMI with the nccl backend; gloo moves host
+    tensors, so there each part is staged through host memory.  `fm` is the package,
+    `idx` the FMIndex on src (None on the other ranks).  SURVEY §8(e): replicate by
+    broadcast instead of building on every GPU."""
     if world == 1:
         return idx
     stage = dist.get_backend() == "gloo"
@@ -143,21 +157,58 @@ def replicate_index(fm, idx, src: int, rank: int, world: int, device):
           else torch.zeros(meta_len, dtype=torch.uint8, device=bdev))
     dist.broadcast(mt, src)
     meta = bytes(mt.cpu().numpy().tobytes())
-    parts = [torch.empty(max(b, 1), dtype=torch.uint8, device=device) for b in sizes]
     if rank == src:
-        idx.export_parts([p.data_ptr() for p in parts], torch.cuda.current_stream(device).cuda_stream)
-        torch.cuda.synchronize(device)
-    for i, p in enumerate(parts):
+        out, ptrs = idx, idx.export_part_ptrs(nparts)
+    else:
+        out, ptrs = fm.FMIndex.import_alloc(meta, nparts, torch.device(device).index)
+    for ptr, nb in zip(ptrs, sizes):
+        if nb == 0:
+            continue
+        part = device_bytes(ptr, nb, device)
         if stage:  # gloo moves host tensors only
-            h = p.cpu() if rank == src else torch.empty(p.numel(), dtype=torch.uint8)
+            h = part.cpu() if rank == src else torch.empty(nb, dtype=torch.uint8)
             dist.broadcast(h, src)
             if rank != src:
-                p.copy_(h)
+                part.copy_(h)
         else:
-            dist.broadcast(p, src)
+            dist.broadcast(part, src)
+        del part
     torch.cuda.synchronize(device)
-    if rank == src:
-        return idx
-    out = fm.FMIndex.import_image(meta, [p.data_ptr() for p in parts], torch.device(device).index)
-    del parts
+    if rank != src:
+        out.import_commit()
+    return out
+
+
+# ---- the gathered counts' wire form (cs_counts_pack_wire) -----------------------
+
+WIRE_CAP = 4096  # overflow pairs (counts >= 255) per shard and step
+
+
+def wire_bytes(fm, per: int, cap: int = WIRE_CAP) -> int:
+    return fm.counts_wire_bytes(per, cap)
+
+
+def pack_counts(fm, counts: torch.Tensor, wire: torch.Tensor, cap: int = WIRE_CAP, stream: int = 0):
+    """Pack a device uint64 count vector into `wire` (uint8, wire_bytes long) on the
+    GPU: 1 B per count plus the overflow pairs (include/cs_fmindex.h
+    cs_counts_pack_wire)."""
+    assert counts.is_cuda and wire.is_cuda and counts.dtype == torch.int64
+    assert wire.numel() >= fm.counts_wire_bytes(counts.numel(), cap)
+    fm.counts_pack_wire(counts.data_ptr(), counts.numel(), cap, wire.data_ptr(), stream)
+
+
+def unpack_counts(wire: torch.Tensor, npat: int) -> torch.Tensor:
+    """The exact int64 counts of one shard's wire form.  Raises when the shard had more
+    overflow pairs than its buffer holds (the caller then fetches that shard's counts
+    as uint64)."""
+    w = wire.reshape(-1)
+    hdr = w[:16].view(torch.int64)
+    pairs, cap = int(hdr[0].item()), int(hdr[1].item())
+    if pairs > cap:
+        raise OverflowError("wire: %d counts >= 255, buffer holds %d" % (pairs, cap))
+    u8 = w[16 + 16 * cap: 16 + 16 * cap + npat]
+    out = u8.to(torch.int64)
+    if pairs:
+        pr = w[16: 16 + 16 * pairs].view(torch.int64).view(-1, 2)
+        out[pr[:, 0]] = pr[:, 1]
     return out

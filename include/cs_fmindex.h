@@ -16,8 +16,10 @@
  *  - a handle is immutable after creation and may be used from several host
  *    threads on distinct streams.
  *  - positions and counts are uint64 (the reference's uint64_t return types,
- *    src/api/fm_index.hpp:26,32); this build indexes texts of n < 2^32 bytes,
- *    the reference's own limit (uint32 SA/C/SSA).
+ *    src/api/fm_index.hpp:26,32).  Texts up to n < 2^38 bytes are indexed (the
+ *    reference's uint32 SA/C/SSA stop at 2^32): from n >= 2^32 the
+ *    index is "wide" (u64 samples and packed 8-B prefix-table entries, a bucketed
+ *    suffix sorter); cs_fm_create takes the reference's own u32 arrays, so n < 2^32.
  *  - on a non-OK status, cs_fm_last_error() returns this thread's message; for
  *    CS_ERR_LF_OVERRUN it is the reference's exact text
  *    "locate: LF walk exceeded text length" (src/api/fm_index.cpp:137).
@@ -129,6 +131,17 @@ cs_status cs_fm_export_meta(const cs_fm_index* h, char* meta, uint64_t cap, uint
 cs_status cs_fm_export_parts(const cs_fm_index* h, void* const* d_dst, void* stream);
 cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d_src,
                        uint32_t nparts, int device, cs_fm_index** out);
+/* The same without staging copies (replication at one index's worth of HBM per GPU):
+ * export_part_ptrs gives the device address of each of the index's own parts
+ * (read-only, valid while h lives) so a broadcast can send straight from them;
+ * import_alloc creates a handle on `device` with its parts allocated (contents
+ * undefined) and returns their addresses for the caller to fill, e.g. by receiving the
+ * broadcast into them; import_commit (after those copies, on any stream) completes the
+ * handle — it must not be queried before. */
+cs_status cs_fm_export_part_ptrs(const cs_fm_index* h, const void** d_parts, uint32_t cap);
+cs_status cs_fm_import_alloc(const char* meta, uint64_t meta_len, int device, cs_fm_index** out,
+                             void** d_parts, uint32_t nparts);
+cs_status cs_fm_import_commit(cs_fm_index* h);
 void cs_fm_destroy(cs_fm_index* h);
 cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out);
 const char* cs_fm_last_error(void);
@@ -193,12 +206,58 @@ cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
  * without an offsets array to read. */
 cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, uint64_t m,
                                    uint64_t npat, uint64_t* d_out, void* stream);
+/* Query flags (the *_ex entry points).  Every flag leaves the results unchanged and
+ * only selects which structures a search may read, so the reference's own loop can
+ * be run and timed on any index:
+ *   CS_Q_NO_PREFIX     start every search from C[] (fm_index.cpp:84-89): no prefix table
+ *   CS_Q_NO_CONTEXTS   step every remaining character through the rank structure
+ *                      (fm_index.cpp:90-96): no left contexts, no context records
+ *   CS_Q_NO_FULL_SA    locate phase 2: walk LF to the sampled rows (fm_index.cpp:125-153)
+ *                      even when the full suffix array is kept
+ *   CS_Q_NO_WALK_LINES locate phase 2: walk the rank structure to the reference's row
+ *                      samples (row % ssa_stride == 0) even when walk lines exist */
+#define CS_Q_NO_PREFIX 1u
+#define CS_Q_NO_CONTEXTS 2u
+#define CS_Q_NO_FULL_SA 4u
+#define CS_Q_NO_WALK_LINES 8u
+
+/* Where a batch count writes.  width 8: uint64 counts (the reference's return type,
+ * fm_index.hpp:26).  width 4: uint32, exact while n < 2^32 (CS_ERR_INVALID otherwise).
+ * width 1: uint8 — a count >= 255 is stored as 255 and listed as a (pattern index, count)
+ * pair of uint64 in d_exc (capacity exc_cap pairs); *d_exc_n (device, caller-zeroed)
+ * receives the number of such patterns, which may exceed exc_cap: the pairs past it are
+ * then not stored.  Narrow widths cut the HBM bytes written per pattern and the bytes a
+ * gather of the counts across GPUs moves (bench.py, shard.py). */
+typedef struct cs_count_out {
+  void* d_counts;
+  uint32_t width;
+  uint64_t* d_exc;
+  uint64_t exc_cap;
+  uint64_t* d_exc_n;
+} cs_count_out;
+
+/* FMIndex::count (fm_index.cpp:79-101) of a device batch, general form: d_offs as
+ * cs_fm_count_batch_device, or NULL for npat patterns of one length fixed_m back to back
+ * (cs_fm_count_fixed_device); output as *out; flags CS_Q_*. */
+cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
+                                      const uint64_t* d_offs, uint64_t fixed_m, uint64_t npat,
+                                      const cs_count_out* out, uint32_t flags, void* stream);
+/* The same for 2-bit packed DNA patterns (not a reference form: 8 B per pattern
+ * instead of m bytes plus an 8-B offset): pattern q is d_packed[q], character i is
+ * "ACGT"[(d_packed[q] >> 2i) & 3], i = 0 .. m-1, m <= 32.  Counts equal count() of the
+ * byte string those characters spell. */
+cs_status cs_fm_count_packed_device(const cs_fm_index* h, const uint64_t* d_packed, uint32_t m,
+                                    uint64_t npat, const cs_count_out* out, uint32_t flags,
+                                    void* stream);
 /* Measurement twin of cs_fm_count_batch_device: d_out[q] = the algorithmic HBM
  * bytes of query q's search (distinct rank/occurrence lines per rank pair x line
  * size + the prefix-table entry), for roofline accounting (bench.py). */
 cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream);
+cs_status cs_fm_count_bytes_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
+                                      const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
+                                      uint32_t flags, void* stream);
 /* locate phase 1: backward search; d_sp[q] = the pattern's record for phase 2 (the
  * first row of its range, or an encoded window of matching rows when the search
  * finished over the left contexts — treat it as opaque), d_out_offs = exclusive scan
@@ -218,6 +277,21 @@ cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d
                                          const uint64_t* d_out_offs, uint64_t npat,
                                          uint64_t total, uint64_t* d_out_pos, void* stream);
 cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream);
+/* The two phases under query flags (CS_Q_*; e.g. CS_Q_NO_FULL_SA | CS_Q_NO_WALK_LINES
+ * runs the reference's row-sampled SSA walk, fm_index.cpp:125-153, on any index). */
+cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
+                                        const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                                        uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                                        uint32_t flags, void* stream);
+cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
+                                      const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                                      uint64_t* d_out_pos, uint32_t flags, void* stream);
+/* Measurement twin of phase 2 (bench.py's walk roofline): d_steps[j] = the LF steps the
+ * walk of reported row j takes before its sample (0 with the full suffix array). */
+cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,
+                                         const uint64_t* d_out_offs, uint64_t npat,
+                                         uint64_t total, uint64_t* d_steps, uint32_t flags,
+                                         void* stream);
 
 /* Building blocks, for parity tests (host arrays in/out):
  *   level rank1   — BitVector::rank1 of wavelet level l (src/core/bitvector.cpp:165-230);
@@ -236,6 +310,16 @@ cs_status cs_fm_get_C(const cs_fm_index* h, uint64_t* out257);
  * bytes), asynchronous on stream. */
 cs_status cs_fm_bwt_device(const cs_fm_index* h, uint8_t* d_out, void* stream);
 cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint64_t* len);
+
+/* Wire form of a device count vector for the cross-GPU gather of per-shard counts
+ * (shard.py): exact and 1 B per pattern — min(count, 255) as uint8
+ * plus a (pattern index, count) pair for each count >= 255 — in one fixed-size buffer
+ * of cs_counts_wire_bytes(npat, cap) bytes:
+ *   [u64 pairs][u64 cap][cap x (u64 index, u64 count)][npat x u8]
+ * `pairs` may exceed cap (the pairs past it are not stored).  Asynchronous on stream. */
+uint64_t cs_counts_wire_bytes(uint64_t npat, uint64_t cap);
+cs_status cs_counts_pack_wire(const uint64_t* d_counts, uint64_t npat, uint64_t cap, void* d_wire,
+                              void* stream);
 
 /* Suffix array of text (host in/out) by the device builder — src/core/sais.hpp:8-16
  * order (a proper prefix sorts first). */

@@ -382,6 +382,12 @@ def ref_lib():
         R.ref_count_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_int, _u64p, _u64p]
         R.ref_free.restype = None
         R.ref_free.argtypes = [C.c_void_p]
+        R.ref_attach_locate.restype = None
+        R.ref_attach_locate.argtypes = [C.c_void_p, _u8p, C.c_uint64, C.POINTER(C.c_uint32),
+                                        C.c_uint64, C.c_uint32]
+        R.ref_locate_batch.restype = None
+        R.ref_locate_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint64, C.c_int,
+                                       C.c_uint64, C.POINTER(C.c_int64), _u64p, _u64p]
         _ref = R
     return _ref
 
@@ -413,6 +419,29 @@ class RefCountIndex:
         lat = np.zeros(max(npat, 1), np.uint64)
         R.ref_count_batch(self._h, _u8(buf), _u64(offs), npat, nthreads, _u64(out), _u64(lat))
         return (out[:npat], lat[:npat]) if latencies else out[:npat]
+
+    def attach_locate(self, bwt, ssa, stride):
+        """Give the index the members locate() reads (bwt_, ssa_): the reference's own
+        FMIndex::locate (src/api/fm_index.cpp:107-157) then runs unmodified."""
+        self._bwt = np.ascontiguousarray(bwt, np.uint8)
+        self._ssa = np.ascontiguousarray(ssa, np.uint32)
+        ref_lib().ref_attach_locate(self._h, _u8(self._bwt), len(self._bwt),
+                                    self._ssa.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                    len(self._ssa), stride)
+        del self._bwt, self._ssa  # copied into the reference's members
+
+    def locate_batch(self, buf, offs, limit=100000, nthreads=1, cap=8):
+        """-> (nout[q] (-1: the reference threw), positions[q, :cap], latency ns)."""
+        R = ref_lib()
+        buf = np.ascontiguousarray(buf, np.uint8)
+        offs = np.ascontiguousarray(offs, np.uint64)
+        npat = len(offs) - 1
+        nout = np.zeros(max(npat, 1), np.int64)
+        out = np.zeros((max(npat, 1), cap), np.uint64)
+        lat = np.zeros(max(npat, 1), np.uint64)
+        R.ref_locate_batch(self._h, _u8(buf), _u64(offs), npat, limit, nthreads, cap,
+                           nout.ctypes.data_as(C.POINTER(C.c_int64)), _u64(out), _u64(lat))
+        return nout[:npat], out[:npat], lat[:npat]
 
     def __del__(self):
         R = _ref

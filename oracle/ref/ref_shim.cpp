@@ -100,6 +100,48 @@ void* ref_build_count_only(const uint64_t* const* level_words, uint64_t nwords, 
   return idx;
 }
 
+// locate() on such an index: the members it reads besides the wavelet levels and C_
+// (src/api/fm_index.cpp:107-157) — bwt_ (LF, fm_index.hpp:62-66) and the row-sampled
+// ssa_ (src/core/ssa.hpp:7-13) — taken from arrays of the same BWT.
+void ref_attach_locate(void* h, const uint8_t* bwt, uint64_t n, const uint32_t* ssa,
+                       uint64_t nsamples, uint32_t stride) {
+  auto* idx = static_cast<cs::FMIndex*>(h);
+  idx->bwt_.assign(reinterpret_cast<const char*>(bwt), n);
+  idx->ssa_.stride = stride;
+  idx->ssa_.samples.assign(ssa, ssa + nsamples);
+}
+
+// locate(pattern, limit) of npat patterns on nthreads host threads (disjoint slices):
+// nout[q] = number of positions (-1: the reference threw), the first min(nout, cap)
+// of them at out[q * cap ..], per-call latency in ns.
+void ref_locate_batch(void* h, const uint8_t* pats, const uint64_t* offs, uint64_t npat,
+                      uint64_t limit, int nthreads, uint64_t cap, int64_t* nout, uint64_t* out,
+                      uint64_t* lat_ns) {
+  const auto* idx = static_cast<const cs::FMIndex*>(h);
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([=] {
+      const uint64_t a = npat * t / nthreads, b = npat * (t + 1) / nthreads;
+      for (uint64_t q = a; q < b; ++q) {
+        const auto t0 = std::chrono::steady_clock::now();
+        try {
+          auto v = idx->locate(std::string_view(reinterpret_cast<const char*>(pats + offs[q]),
+                                                offs[q + 1] - offs[q]), limit);
+          nout[q] = (int64_t)v.size();
+          std::memcpy(out + q * cap, v.data(), std::min<uint64_t>(v.size(), cap) * 8);
+        } catch (...) {
+          nout[q] = -1;
+        }
+        const auto t1 = std::chrono::steady_clock::now();
+        if (lat_ns)
+          lat_ns[q] = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
 // count() of npat patterns on nthreads host threads (disjoint contiguous slices; the
 // reference's count is const and re-entrant), per-call latency in ns.
 void ref_count_batch(void* h, const uint8_t* pats, const uint64_t* offs, uint64_t npat,

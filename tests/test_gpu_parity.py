@@ -612,3 +612,152 @@ def test_create_from_arrays(pkg, name):
     assert gt.extract_batch([1, 0, len(t) - 2], [7, 3, 9]) == [t[1:8], t[0:3], t[-2:]]
     with pytest.raises(RuntimeError):
         g.extract(1, 7)
+
+
+# ---- query forms: flags (CS_Q_*), count widths, packed DNA ----------------------
+
+FLAG_SETS = {"none": 0, "no_prefix": 1, "no_contexts": 2, "loop": 3}
+
+
+def _substrings_and_mutants(t, lengths, per, seed):
+    rng = np.random.default_rng(seed)
+    n = len(t)
+    pats = []
+    for m in lengths:
+        for i in rng.integers(0, max(1, n - m + 1), per):
+            p = bytearray(t[i:i + m])
+            pats.append(bytes(p))
+            if p:
+                p[rng.integers(0, len(p))] = t[rng.integers(0, n)]
+                pats.append(bytes(p))
+    return pats
+
+
+def _count_ex(g, pats, width=8, flags=0, exc_cap=1 << 16):
+    """count through cs_fm_count_batch_device_ex -> (counts as uint64, exception pairs)."""
+    buf, offs = O.pack_patterns(pats)
+    d_buf = torch.from_numpy(buf.copy()).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    npat = len(pats)
+    dt = {8: torch.int64, 4: torch.int32, 1: torch.uint8}[width]
+    out = torch.zeros(max(npat, 1), dtype=dt, device="cuda")
+    exc = torch.zeros(2 * max(exc_cap, 1), dtype=torch.int64, device="cuda")
+    exc_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+    g.count_device_ex(d_buf.data_ptr(), d_offs.data_ptr(), npat, out.data_ptr(), width=width,
+                      flags=flags, d_exc=exc.data_ptr(), exc_cap=exc_cap, d_exc_n=exc_n.data_ptr())
+    torch.cuda.synchronize()
+    got = out[:npat].cpu().numpy().astype(np.uint64)
+    pairs = exc[: 2 * min(int(exc_n.item()), exc_cap)].view(-1, 2).cpu().numpy()
+    return got, pairs, int(exc_n.item())
+
+
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_query_flags_count(built, pkg, name):
+    """The same counts with the prefix table, the left contexts / context records, or
+    both left out (CS_Q_NO_PREFIX / CS_Q_NO_CONTEXTS): the plain backward-search loop of
+    fm_index.cpp:84-98 on the same index, and its algorithmic bytes only grow."""
+    g, o = built(name)
+    t = TEXTS[name]
+    pats = _substrings_and_mutants(t, (1, 2, 5, 7, 9, 14, 20, 33), 25, len(t) + 7)
+    want = [o.count(p) for p in pats]
+    buf, offs = O.pack_patterns(pats)
+    d_buf = torch.from_numpy(buf.copy()).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    nb = {}
+    for fname, f in FLAG_SETS.items():
+        got, _, _ = _count_ex(g, pats, flags=f)
+        assert got.tolist() == want, (name, fname)
+        qb = torch.zeros(len(pats), dtype=torch.int64, device="cuda")
+        g.count_bytes_device(d_buf.data_ptr(), d_offs.data_ptr(), len(pats), qb.data_ptr(), flags=f)
+        torch.cuda.synchronize()
+        nb[fname] = int(qb.sum().item())
+    assert nb["loop"] >= nb["no_contexts"] or g.info().prefix_k == 0, nb
+    if g.info().context_q == 0:
+        assert nb["no_contexts"] == nb["none"], nb
+
+
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_query_flags_locate(built, pkg, name):
+    """locate with phase 2 forced onto the LF walk (CS_Q_NO_FULL_SA) and onto the
+    reference's row-sampled SSA walk over the rank structure (CS_Q_NO_WALK_LINES,
+    fm_index.cpp:125-153), with and without the prefix table / contexts in phase 1: the
+    oracle's positions in row order, or its overrun error."""
+    g, o = built(name)
+    t = TEXTS[name]
+    pats = _substrings_and_mutants(t, (1, 3, 6, 9, 20), 12, len(t) + 3)
+    lim = 40
+    for f in (4, 4 | 8, 1 | 2 | 4 | 8, 2 | 8):
+        buf, offs = O.pack_patterns(pats)
+        d_buf = torch.from_numpy(buf.copy()).cuda()
+        d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+        npat = len(pats)
+        d_sp = torch.zeros(npat, dtype=torch.int64, device="cuda")
+        d_oo = torch.zeros(npat + 1, dtype=torch.int64, device="cuda")
+        tot = g.locate_ranges_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim, d_sp.data_ptr(),
+                                     d_oo.data_ptr(), flags=f)
+        d_pos = torch.zeros(max(tot, 1), dtype=torch.int64, device="cuda")
+        try:
+            g.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), npat, tot, d_pos.data_ptr(),
+                                 flags=f)
+        except RuntimeError as e:
+            assert str(e) == "locate: LF walk exceeded text length"
+            with pytest.raises(RuntimeError, match="LF walk exceeded"):
+                for p in pats:
+                    o.locate(p, limit=lim)
+            continue
+        oo = d_oo.cpu().numpy()
+        pos = d_pos[:tot].cpu().numpy()
+        for q, p in enumerate(pats):
+            assert pos[oo[q]:oo[q + 1]].tolist() == o.locate(p, limit=lim), (name, f, p)
+
+
+@pytest.mark.parametrize("name", ["dna_5k", "bytes_5k", "all_same", "runs", "rare_N_41", "banana"])
+def test_count_widths(built, pkg, name):
+    """uint32 counts equal the uint64 ones; uint8 counts saturate at 255 with every
+    larger count listed exactly once as (pattern, count); pairs past the capacity are
+    counted but not stored."""
+    g, o = built(name)
+    t = TEXTS[name]
+    pats = _substrings_and_mutants(t, (1, 2, 3, 8, 20), 30, 9) + [b""]
+    want = np.array([o.count(p) for p in pats], np.uint64)
+    for f in (0, 3):
+        got4, _, _ = _count_ex(g, pats, width=4, flags=f)
+        assert np.array_equal(got4, want), (name, f)
+        got1, pairs, nexc = _count_ex(g, pats, width=1, flags=f)
+        big = np.nonzero(want >= 255)[0]
+        assert nexc == len(big)
+        assert np.array_equal(got1, np.minimum(want, 255))
+        assert sorted(pairs[:, 0].tolist()) == big.tolist()
+        assert all(want[q] == c for q, c in pairs.tolist())
+        if len(big) > 2:
+            _, pairs2, nexc2 = _count_ex(g, pats, width=1, flags=f, exc_cap=2)
+            assert nexc2 == len(big) and len(pairs2) == 2
+            assert all(want[q] == c for q, c in pairs2.tolist())
+
+
+@pytest.mark.parametrize("name", ["dna_5k", "banana", "rare_N_41", "rare_both_ends", "line_edge_896",
+                                  "occ_edge_65", "bytes_5k", "abab_noterm"])
+def test_count_packed(built, pkg, name):
+    """2-bit packed DNA patterns (cs_fm_count_packed_device) count as the byte strings
+    they spell, at every length 0..32, under every flag set and width."""
+    g, o = built(name)
+    t = TEXTS[name]
+    rng = np.random.default_rng(3)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    for m in (0, 1, 4, 7, 12, 15, 16, 19, 20, 21, 27, 32):
+        pats = []
+        # substrings of the text mapped onto ACGT (exact hits on DNA texts) and random ones
+        for i in (rng.integers(0, len(t) - m + 1, 30) if len(t) >= m else []):
+            s = np.frombuffer(t[i:i + m], np.uint8)
+            pats.append(acgt[s % 4].tobytes() if not set(s.tolist()) <= set(b"ACGT") else s.tobytes())
+        pats += [acgt[rng.integers(0, 4, m)].tobytes() for _ in range(20)]
+        want = np.array([o.count(p) for p in pats], np.uint64)
+        packed = torch.from_numpy(pkg.pack_dna(pats).view(np.int64)).cuda()
+        for f in (0, 1, 2, 3):
+            for width in (8, 4):
+                dt = torch.int64 if width == 8 else torch.int32
+                out = torch.zeros(len(pats), dtype=dt, device="cuda")
+                g.count_packed_device(packed.data_ptr(), m, len(pats), out.data_ptr(), width=width,
+                                      flags=f)
+                torch.cuda.synchronize()
+                assert out.cpu().numpy().astype(np.uint64).tolist() == want.tolist(), (name, m, f, width)
