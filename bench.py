@@ -5,31 +5,43 @@ Workload (default = BASELINE.json configs[3], "C4", the config the metric is
 quoted on; it fits one GPU): 4 GB synthetic DNA text (n = 4e9 incl. the '$'
 terminator, SURVEY.md §8(d): splitmix64 seed 42), Q_text 20-mers (substrings at
 splitmix64(4242) positions).  One step = one batched count() launch over a batch
-of --batch patterns per GPU, inputs resident in HBM.  Multi-GPU: one process per
-GPU, index replicated (built per GPU), query stream sharded in contiguous ranges
-(weak scaling: --batch per GPU).  Queries are independent, so the timed step has
-no data-path collective: each rank's counts stay with its shard (barrier + max
-over ranks around the K steps).  --gather adds SURVEY §8(e)'s gather of the
-counts to rank 0 over RCCL, double-buffered behind the next step's count.
+of --batch patterns per GPU, inputs resident in HBM, uint64 counts (the
+reference's FMIndex::count return type).  Multi-GPU: one process per GPU, index
+replicated (built per GPU), query stream sharded in contiguous ranges (weak
+scaling: --batch per GPU); every step's counts are gathered to rank 0 over RCCL
+ in their exact 1-B wire form (cs_counts_pack_wire), the gather of
+step k overlapped with the count of step k+1; the timed region closes after the
+last gather.
 
 Extra fields on the JSON line:
   roofline     the count kernel against HBM: achieved = algorithmic bytes per
                launch / mean kernel time (HIP events on the launch stream).
                Algorithmic bytes = the random reads the search needs (prefix-table
-               entry, one 32-B line per rank step, the 32-B context sector(s);
-               counted per query by cs_fm_count_bytes_device) + the stream every
-               launch moves (patterns, offsets, counts).  traffic = HBM bytes per
+               entry or context record, one 32-B line per rank step, the 32-B context
+               sector(s); counted per query by cs_fm_count_bytes_device) + the stream
+               every launch moves (patterns, offsets, counts).  traffic = HBM bytes per
                launch from the committed rocprofv3 PMC summary for this workload.
+  legs         (N=1) the same batch through the other query forms and structures,
+               each with its own roofline: the reference's plain backward-search loop
+               (CS_Q_NO_CONTEXTS: table + rank steps; CS_Q_NO_PREFIX|NO_CONTEXTS: every
+               step through the occurrence lines), longer patterns (m = 32, 64),
+               uint32 counts, 2-bit packed patterns, the reference's own 8-level
+               binary wavelet matrix (its table + steps and its whole LF loop), and
+               locate with the full SA, the reference's row-sampled SSA walk (stride
+               32) and the walk lines.
   cpu_baseline the reference's own FMIndex::count (oracle/_ref/libcs_ref.so, built
                from its sources; kind "reference"), else the oracle's
                reference-faithful count() (kind "port"; O(n) count_ones scans, as
                src/core/bitvector.cpp:168-170), on a bounded sample of the same
-               batch, rank 0, N=1 only, all host threads.
+               batch, rank 0, N=1 only, on the process's CPU share; cpu_locate: the
+               reference's FMIndex::locate the same way.
   p50_us       median end-to-end latency of single-pattern cs::FMIndex::count() calls
                through the C++ facade (host pattern in, count out), as
                tools/benchmark.cpp:154-166, with the index in serving mode (a resident
                wave answers from a pinned mailbox); p50_launch_us: the same calls with
                one kernel launch each.
+--only LEG runs one leg and nothing else (the rocprofv3 passes of
+profiles/profile_legs.sh); --legs chooses the legs of a full run.
 """
 import argparse
 import json
@@ -48,11 +60,253 @@ from __graft_entry__ import _load_pkg  # noqa: E402
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# measured random-read ceiling of MI355X: profiles/microbench/gather_bench.hip, 8..32-B
+# random reads over a 4 GB table at 49-52 G accesses/s (profiles/r01/gather_bench*.txt)
+RANDOM_CEIL = 5.0e10
+PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
+
+# legs by index: the headline index (occurrence lines + contexts + records + full SA),
+# the reference's binary wavelet matrix, the occurrence engine with walk lines
+LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
+             "count_m64", "count_fixed", "locate", "locate_ssa_rows", "host_batch", "extract"]
+LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
+LEGS_WALK = ["locate_ssa"]
+# repetitive DNA of the same size (cs_synth_text_device kind 2): heavy-tailed ranges
+LEGS_RDNA = ["count_rdna", "locate_rdna"]
+ALL_LEGS = LEGS_MAIN + LEGS_WM + LEGS_WALK + LEGS_RDNA
 
 
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(wl, leg):
+    """HBM bytes per launch of `leg` on workload `wl` from the committed PMC summaries."""
+    if os.path.exists(PMC_LEGS):
+        e = json.load(open(PMC_LEGS)).get("%s|%s" % (wl, leg))
+        if e:
+            return e.get("hbm_bytes_per_launch")
+    if leg == "count":  # round-1 summary of the headline kernel
+        prof = os.path.join(ROOT, "profiles", "pmc_count.json")
+        if os.path.exists(prof):
+            pj = json.load(open(prof))
+            if pj.get("workload") == wl:
+                return pj.get("hbm_bytes_per_launch")
+    return None
+
+
+def time_launches(launch, steps, warmup, stream):
+    """warmup + timed launches -> (wall s per launch, kernel s per launch (HIP events on
+    the launch stream), min kernel ms)."""
+    for _ in range(warmup):
+        launch()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        evs[k][0].record(stream)
+        launch()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    ms = [a.elapsed_time(b) for a, b in evs]
+    return wall, statistics.mean(ms) / 1e3, min(ms)
+
+
+class Workload:
+    """Device batch of B patterns of length m (Q_text or Q_unif) + its accounting."""
+
+    def __init__(self, pkg, text, N, m, lo, B, kind, queries, dev, sh):
+        self.m, self.B = m, B
+        self.pats = torch.empty(B * m, dtype=torch.uint8, device=dev)
+        self.offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
+        if queries == "text":
+            pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, self.pats.data_ptr(),
+                                      self.offs.data_ptr(), sh)
+        else:  # SURVEY §8(d) secondary batch Q_unif
+            pkg.synth_random_patterns_device(kind, m, lo, B, 4242, self.pats.data_ptr(),
+                                             self.offs.data_ptr(), sh)
+
+    def accounting(self, idx, info, flags, sh, dev):
+        """-> (random algorithmic bytes per launch, random accesses per launch, table hit
+        fraction).  Random bytes from the engine's measurement twin
+        (cs_fm_count_bytes_device): per backward-search step the distinct lines its rank
+        pair (sp, ep) needs times the line size, the prefix-table entry / context
+        record, the context sector(s)."""
+        B, m = self.B, self.m
+        qb = torch.empty(B, dtype=torch.int64, device=dev)
+        idx.count_bytes_device(self.pats.data_ptr(), self.offs.data_ptr(), B, qb.data_ptr(), sh,
+                               flags=flags)
+        rnd = int(qb.sum().item())
+        del qb
+        K = 0 if flags & 1 else info.prefix_k
+        frac = 0.0
+        if K and m >= K:
+            code = torch.tensor(list(info.prefix_code), dtype=torch.int64, device=dev)
+            P2 = self.pats.view(B, m).long()
+            frac = float((code[P2[:, m - K:]] != 255).all(dim=1).float().mean().item())
+            del P2
+        eb = info.prefix_bytes // (info.prefix_sigma ** K) if K else 0
+        hits = int(round(B * frac)) if K else 0
+        acc = (rnd - eb * hits) / info.line_bytes + hits
+        return rnd, acc, frac
+
+
+def roofline(alg_random, alg_stream, accesses, kern_s, B, traffic, stream_read=None):
+    alg = alg_random + alg_stream
+    achieved = alg / kern_s / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "alg_bytes_per_launch": alg, "alg_random_bytes_per_launch": alg_random,
+            "alg_stream_bytes_per_launch": alg_stream, "alg_bytes_per_query": alg / B,
+            "stream_read_bytes_per_launch": stream_read,
+            "random_accesses_per_launch": accesses,
+            "random_accesses_per_query": accesses / B,
+            "random_accesses_per_s": accesses / kern_s,
+            "random_access_ceiling_per_s": RANDOM_CEIL,
+            "frac_of_random_access_ceiling": accesses / kern_s / RANDOM_CEIL}
+
+
+def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, steps, warmup,
+              stream, sh, dev, ref_counts, read_counts, stream_read=None):
+    """Time one count form over workload W; check its counts against ref_counts.
+    stream_bytes: the bytes every launch streams (patterns, offsets, counts written);
+    stream_read: the read part of them (default: the patterns and their offsets)."""
+    if stream_read is None:
+        stream_read = W.B * W.m + (W.B + 1) * 8
+    wall, kern_s, kmin = time_launches(launch, steps, warmup, stream)
+    rnd, acc, frac = W.accounting(idx, info, flags, sh, dev)
+    got = read_counts()
+    out = {"what": what, "workload_key": wl_key, "patterns": W.B, "m": W.m, "flags": flags,
+           "ms_per_launch": wall * 1e3, "kernel_ms_mean": kern_s * 1e3, "kernel_ms_min": kmin,
+           "patterns_per_s": W.B / kern_s, "prefix_table_hit_frac": frac,
+           "matches_headline": None if ref_counts is None else bool(np.array_equal(got, ref_counts)),
+           "roofline": roofline(rnd, stream_bytes, acc, kern_s, W.B, pmc_traffic(wl_key, name),
+                                stream_read)}
+    return out, got
+
+
+def walk_step_bytes(info, idx):
+    """HBM bytes of one LF step of the walk: one 32-B occurrence / walk line, or on the
+    binary wavelet matrix one rank line per non-pure level of the row's symbol
+    (cs_fm_info.active_levels), averaged over the BWT's symbol frequencies."""
+    if info.engine != 0:
+        return 32.0
+    C = idx.C().astype(np.float64)
+    f = np.diff(C)
+    lines = np.array([bin(info.active_levels[c]).count("1") for c in range(256)], np.float64)
+    return float((f * lines).sum() / max(f.sum(), 1)) * info.line_bytes
+
+
+def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, limit=100000):
+    """locate (fm_index.cpp:107-157) of the batch: phase 1 (backward search, min(count,
+    limit) per pattern, CSR offsets) and phase 2 (positions: full SA, walk lines or the
+    row-sampled SSA walk, as `flags` select), HIP events around each phase; every
+    position checked to spell its pattern; phase 2's LF steps from its measurement twin."""
+    B, m = W.B, W.m
+    stream = torch.cuda.current_stream()
+    d_sp = torch.empty(B, dtype=torch.int64, device=dev)
+    d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    t1s, t2s, walls = [], [], []
+    d_pos = None
+    for it in range(reps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e[0].record(stream)
+        tot = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, limit,
+                                       d_sp.data_ptr(), d_oo.data_ptr(), sh, flags=flags)
+        e[1].record(stream)
+        if d_pos is None:
+            d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+        idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh,
+                               flags=flags)
+        e[2].record(stream)
+        torch.cuda.synchronize()
+        walls.append(time.perf_counter() - t0)
+        t1s.append(e[0].elapsed_time(e[1]) / 1e3)
+        t2s.append(e[1].elapsed_time(e[2]) / 1e3)
+    tl = min(walls)
+    pos = d_pos[:tot]
+    oo = d_oo.cpu().numpy()
+    owner = torch.from_numpy(np.repeat(np.arange(B), np.diff(oo).astype(np.int64))).to(dev)
+    ok = True
+    for a in range(0, tot, 1 << 24):  # chunks: the window gather is 20 B per position
+        p, w = pos[a:a + (1 << 24)], owner[a:a + (1 << 24)]
+        win = text[(p.unsqueeze(1) + torch.arange(m, device=dev)).long()]
+        ok &= bool((win == W.pats.view(B, m)[w]).all().item())
+    del owner
+    steps = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+    idx.locate_walk_steps_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, steps.data_ptr(), sh,
+                                 flags=flags)
+    st = int(steps[:tot].sum().item()) if tot else 0
+    del steps, d_pos, d_sp, d_oo
+    walk_s = min(t2s)
+    sb = info.ssa_bytes // max(info.n // info.ssa_stride, 1) if info.ssa_bytes else 4
+    step_bytes = walk_step_bytes(info, idx)
+    uses_sa = info.full_sa_bytes and not (flags & 4)
+    # phase 2's algorithmic bytes: the LF steps' lines, one sample (or SA entry) per
+    # position, the record/offsets read and the position written
+    alg = st * step_bytes + tot * ((4 if uses_sa else sb) + 8) + B * 16
+    reads = st * (step_bytes / 32.0) + tot
+    # streamed reads of the phase-2 kernel (PMC correction, profiles/summarize_legs.py): the
+    # records + offsets (full SA) or the expanded rows (walks)
+    stream_rd = 16 * B if uses_sa else 8 * tot
+    return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
+            "patterns_per_s": B / tl, "positions_per_s": tot / tl,
+            "phase1_ms": min(t1s) * 1e3, "phase2_ms": walk_s * 1e3, "limit": limit,
+            "flags": flags, "positions_verified": ok,
+            "walk_lf_steps_per_position": st / max(tot, 1),
+            "phase2_stream_read_bytes": stream_rd, "phase2_alg_bytes": alg,
+            "walk_roofline": {"bound": "hbm", "achieved": alg / walk_s / 1e9, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": alg / walk_s / 1e9 / HBM_PEAK_GBS,
+                              "alg_bytes_per_position": alg / max(tot, 1),
+                              "traffic": pmc_traffic(wl_key, name),
+                              "dependent_reads_per_s": reads / walk_s,
+                              "frac_of_random_access_ceiling": reads / walk_s / RANDOM_CEIL}}
+
+
+def build_index(pkg, text, N, stride, dev_index, env=None):
+    saved = {}
+    for k, v in (env or {}).items():
+        saved[k] = os.environ.get(k)
+        os.environ[k] = v
+    try:
+        t0 = time.perf_counter()
+        idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N, pkg.BuildParams(ssa_stride=stride),
+                                                 device=dev_index)
+        torch.cuda.synchronize()
+        return idx, time.perf_counter() - t0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def workload_key(kind, N, m, B, info, queries):
+    engine = {1: "occ", 2: "qwm", 3: "locc"}.get(info.engine, "wm%d" % info.line_bytes)
+    wl = "%s:%d:m%d:b%d:%s:k%d" % (kind, N, m, B, engine, info.prefix_k)
+    if info.context_q:
+        wl += ":ctx%d" % info.context_q
+    if info.record_bytes:
+        wl += ":rec%d" % info.record_bytes  # context records (32-/16-B prefix-table entries)
+    if queries != "text":
+        wl += ":" + queries
+    return wl
+
+
+def engine_name(info):
+    if info.engine in (1, 3):
+        return "%s + left contexts (q=%d)%s" % (
+            "learned occurrence lines" if info.engine == 3 else "occurrence lines", info.context_q,
+            " + %d-B context records" % info.record_bytes if info.record_bytes else "")
+    if info.engine == 2:
+        return "quaternary wavelet matrix (%d levels of occurrence lines)" % info.levels
+    return "binary wavelet matrix, 8 levels (%d-B rank lines)" % info.line_bytes
 
 
 def main():
@@ -67,33 +321,41 @@ def main():
     ap.add_argument("--batch", type=int, default=12_500_000, help="patterns per GPU per step")
     ap.add_argument("--ssa-stride", type=int, default=32)
     ap.add_argument("--cpu-queries", type=int, default=None,
-                    help="patterns timed on the CPU (default SURVEY §8(d): 256 at C2-size texts, "
-                         "32 at C3, 16 at C4 and above)")
+                    help="patterns timed through the reference's count() on the CPU (default: "
+                         "SURVEY §8(d)'s 256 at C2-size texts, 32 at C3, 16 at C4 and above, and "
+                         "at least two per host thread)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--p50-calls", type=int, default=1000)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on one GPU")
-    ap.add_argument("--locate-batch", type=int, default=12_500_000,
-                    help="patterns of the batch timed through locate() (N=1 only; 0 = skip)")
     ap.add_argument("--queries", default="text", choices=["text", "unif"],
                     help="Q_text (substrings of the text, the headline) or Q_unif (uniform random)")
     ap.add_argument("--cpu-fast-queries", type=int, default=1_000_000,
                     help="patterns timed through the oracle's fast (precomputed) count, all threads")
     ap.add_argument("--extract-batch", type=int, default=1_000_000,
                     help="random 20-byte extracts timed on the device (N=1 only; 0 = skip)")
-    ap.add_argument("--host-batch", type=int, default=1,
-                    help="also time the batch handed over in host memory (PCIe-inclusive; 0 = skip)")
     ap.add_argument("--replicate", default="build", choices=["build", "broadcast"],
                     help="N > 1: every rank builds its replica, or rank 0 builds and broadcasts "
                          "the device image (RCCL)")
-    ap.add_argument("--gather", action="store_true",
-                    help="gather every step's counts to rank 0 (RCCL), overlapped with the next count")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: keep each rank's counts (no gather to rank 0)")
     ap.add_argument("--prefix-k", type=int, default=None,
                     help="prefix-table depth override (0 = off; default automatic)")
+    ap.add_argument("--legs", default="all",
+                    help="comma-separated legs of a full N=1 run (%s), 'all' or 'none'"
+                         % ",".join(ALL_LEGS))
+    ap.add_argument("--only", default=None,
+                    help="run only this leg ('count' = the headline) and print its object "
+                         "(profiling passes)")
     args = ap.parse_args()
     if args.prefix_k is not None:
         os.environ["CS_FM_PREFIX_K"] = str(args.prefix_k)
+    legs = (set(ALL_LEGS) if args.legs == "all" else set() if args.legs == "none"
+            else set(x for x in args.legs.split(",") if x))
+    if args.only:
+        legs = {args.only} - {"count"}
+        args.no_cpu, args.p50_calls = True, 0
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,6 +369,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+        legs = set()  # the N=1 legs; N > 1 runs the headline and the sharded locate
     pkg = _load_pkg()
     import importlib
     shard = importlib.import_module("cs_fmindex_amd.shard")
@@ -121,270 +384,301 @@ def main():
     pkg.synth_text_device(args.kind, 42, L, text.data_ptr(), sh)
     torch.cuda.synchronize()
     replicate_s = None
-    if args.replicate == "broadcast" and world > 1:
-        # rank 0 builds; the device image goes to every rank (shard.replicate_index)
-        idx = (pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
-                                                  pkg.BuildParams(ssa_stride=args.ssa_stride),
-                                                  device=local_dev) if rank == 0 else None)
+    need_main = not (args.only and (args.only in LEGS_WM or args.only in LEGS_WALK
+                                    or args.only in LEGS_RDNA))
+    idx = None
+    if need_main:
+        if args.replicate == "broadcast" and world > 1:
+            # rank 0 builds; the device image goes to every rank (shard.replicate_index)
+            idx = build_index(pkg, text, N, args.ssa_stride, local_dev)[0] if rank == 0 else None
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            idx = shard.replicate_index(pkg, idx, 0, rank, world, dev)
+            replicate_s = time.perf_counter() - t1
+        else:
+            idx = build_index(pkg, text, N, args.ssa_stride, local_dev)[0]
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        idx = shard.replicate_index(pkg, idx, 0, rank, world, dev)
-        replicate_s = time.perf_counter() - t1
-    else:
-        idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N,
-                                                 pkg.BuildParams(ssa_stride=args.ssa_stride),
-                                                 device=local_dev)
-    torch.cuda.synchronize()
     build_s = time.perf_counter() - t0
-    info = idx.info()
-    log(rank, "index built: n=%d in %.1f s, rank lines %.2f GB" % (N, build_s, info.rank_bytes / 1e9))
-
-    # ---- this rank's query shard (contiguous slice of the Q_text stream) ----
     B, m = args.batch, args.m
     total = B * world  # weak scaling: B patterns per GPU
     lo, hi = shard.shard_range(total, rank, world)
     assert hi - lo == B
-    pats = torch.empty(B * m, dtype=torch.uint8, device=dev)
-    offs = torch.empty(B + 1, dtype=torch.int64, device=dev)
-    if args.queries == "text":
-        pkg.synth_patterns_device(text.data_ptr(), N, m, lo, B, 4242, pats.data_ptr(),
-                                  offs.data_ptr(), sh)
-    else:  # SURVEY §8(d) secondary batch Q_unif
-        pkg.synth_random_patterns_device(args.kind, m, lo, B, 4242, pats.data_ptr(),
-                                         offs.data_ptr(), sh)
-    # counts land in double-buffered shards; with --gather (N > 1) the gather of step
-    # k to rank 0 overlaps the count of step k+1 (shard.PipelinedGather), otherwise
-    # each rank keeps its shard's counts (no collective in the data path)
-    coll = args.gather and world > 1
-    pg = shard.PipelinedGather(B, world if coll else 1, rank if coll else 0, torch.int64, dev)
+    W = Workload(pkg, text, N, m, lo, B, args.kind, args.queries, dev, sh)
+    res = {}
+    counts = None
 
-    # algorithmic bytes per launch, counted by the engine's measurement twin of the
-    # count kernel (cs_fm_count_bytes_device): per backward-search step, the distinct
-    # lines its rank pair (sp, ep) needs (one 32-B occurrence line, or one rank line
-    # per non-pure wavelet level; sp and ep in the same line count once) times the
-    # line size, plus the 8-B (16-B wide) prefix-table entry that replaces the first
-    # k steps.
-    line_bytes = info.line_bytes
-    qbytes = torch.empty(B, dtype=torch.int64, device=dev)
-    idx.count_bytes_device(pats.data_ptr(), offs.data_ptr(), B, qbytes.data_ptr(), sh)
-    alg_random = int(qbytes.sum().item())
-    # plus the streamed bytes every launch must move: the patterns, their offsets and
-    # the counts written back
-    alg_stream = B * m + (B + 1) * 8 + B * 8
-    alg_bytes = alg_random + alg_stream
-    del qbytes
-    P2 = pats.view(B, m).long()
-    K = info.prefix_k
-    table_frac = 0.0
-    if K and m >= K:
-        code = torch.tensor(list(info.prefix_code), dtype=torch.int64, device=dev)
-        table_frac = float((code[P2[:, m - K:]] != 255).all(dim=1).float().mean().item())
-    del P2
-    torch.cuda.synchronize()
+    if need_main:
+        info = idx.info()
+        log(rank, "index built: n=%d in %.1f s, rank lines %.2f GB" % (N, build_s, info.rank_bytes / 1e9))
+        wl = workload_key(args.kind, N, m, B, info, args.queries)
+        out = torch.empty(B, dtype=torch.int64, device=dev)
 
-    for k in range(args.warmup):
-        o = pg.buffer(k)
-        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, o.data_ptr(), sh)
-        pg.submit(k)
-    pg.finish()
-    torch.cuda.synchronize()
-    if world > 1:
+        def headline():
+            idx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, out.data_ptr(), sh)
+
+    if need_main and (not args.only or args.only == "count"):
+        # ---- the timed region: K steps of the batch count (+ the gather at N > 1) ----
+        coll = world > 1 and not args.no_gather
+        wire_len = shard.wire_bytes(pkg, B) if coll else 0
+        pg = shard.PipelinedGather(wire_len, world, rank, torch.uint8, dev) if coll else None
+
+        def step(k):
+            headline()
+            if coll:  # exact 1-B wire form, gathered behind the next step's count
+                w = pg.buffer(k)
+                shard.pack_counts(pkg, out, w, stream=sh)
+                pg.submit(k)
+
+        for k in range(args.warmup):
+            step(k)
+        if coll:
+            pg.finish()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            evs[k][0].record(stream)
+            headline()
+            evs[k][1].record(stream)
+            if coll:
+                w = pg.buffer(k)
+                shard.pack_counts(pkg, out, w, stream=sh)
+                pg.submit(k)
+        if coll:
+            pg.finish()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kern_ms = [a.elapsed_time(b) for a, b in evs]
+        if world > 1:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = tt.item()
+        counts = out.cpu().numpy()
+        gather_ok = None
+        if coll:
+            # rank 0 decodes every shard of the last step and checks it against its own
+            # count of the same patterns (the whole global batch, shard by shard)
+            if rank == 0:
+                gather_ok = True
+                parts = pg.result_parts((args.steps - 1))
+                for r in range(world):
+                    got = shard.unpack_counts(parts[r], B)
+                    Wr = W if r == 0 else Workload(pkg, text, N, m, shard.shard_range(total, r, world)[0],
+                                                   B, args.kind, args.queries, dev, sh)
+                    chk = torch.empty(B, dtype=torch.int64, device=dev)
+                    idx.count_batch_device(Wr.pats.data_ptr(), Wr.offs.data_ptr(), B, chk.data_ptr(), sh)
+                    gather_ok &= bool(torch.equal(got.to(dev), chk))
+                    del chk
+            del pg
+        found = int((counts >= 1).sum())
+        kern_avg_s = statistics.mean(kern_ms) / 1e3
+        rnd, acc, frac = W.accounting(idx, info, 0, sh, dev)
+        stream_b = B * m + (B + 1) * 8 + B * 8  # patterns, offsets, uint64 counts
+        if rank == 0:
+            rf = roofline(rnd, stream_b, acc, kern_avg_s, B, pmc_traffic(wl, "count"),
+                          B * m + (B + 1) * 8)
+            rf.update({"line_bytes": info.line_bytes, "prefix_k": info.prefix_k,
+                       "prefix_table_hit_frac": frac, "context_q": info.context_q,
+                       # SURVEY.md §8(d)'s per-query figure for the reference's structure
+                       # (64 B x 8 levels x 2 ranks x (m-1) steps), for comparison only:
+                       # this engine reads alg_bytes_per_query
+                       "survey_alg_bytes_per_query": 64 * 8 * 2 * (m - 1),
+                       "survey_equivalent_GBs": 64 * 8 * 2 * (m - 1) * B / kern_avg_s / 1e9,
+                       "kernel_ms_mean": kern_avg_s * 1e3, "kernel_ms_min": min(kern_ms)})
+            res = {
+                "metric": METRIC,
+                "value": B * world * args.steps / elapsed,
+                "unit": "patterns/s",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": elapsed / args.steps * 1e3,
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": "u64",
+                "data": "synthetic",
+                "config": {"workload": "C4: %s text n=%d (incl. terminator), Q_%s %d-mers, count()"
+                           % (args.kind.upper(), N, args.queries, m) if L == 3_999_999_999 else
+                           "%s text n=%d, Q_%s %d-mers, count()" % (args.kind, N, args.queries, m),
+                           "batch_per_gpu": B, "global_batch": B * world, "m": m,
+                           "ssa_stride": args.ssa_stride, "parallelism": "dp%d" % world,
+                           "index": "replicated per GPU", "workload_key": wl,
+                           "collective": ("gather of every step's counts to rank 0 (%s), exact "
+                                          "1-B wire form, %d B per rank per step, overlapped with "
+                                          "the next step's count" % (
+                                              "RCCL over xGMI" if args.dist_backend == "nccl"
+                                              else args.dist_backend, wire_len)) if coll
+                           else "none (independent query shards)",
+                           "engine": engine_name(info)},
+                "roofline": rf,
+                "build_s": build_s,
+                "replicate": args.replicate if world > 1 else "single",
+                "replicate_s": replicate_s,
+                "found_frac": found / B,
+            }
+            if coll:
+                res["gather_verified"] = gather_ok
+
+    # ---- N > 1: locate of each rank's shard, positions gathered to rank 0 (gather_v) ----
+    if world > 1 and need_main and not args.only:
+        d_sp = torch.empty(B, dtype=torch.int64, device=dev)
+        d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
         dist.barrier()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        o = pg.buffer(k)
-        evs[k][0].record(stream)
-        idx.count_batch_device(pats.data_ptr(), offs.data_ptr(), B, o.data_ptr(), sh)
-        evs[k][1].record(stream)
-        pg.submit(k)
-    pg.finish()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = tt.item()
-    # DRAM accesses per launch (each distinct line and each table entry is one random
-    # access) against the measured random-access ceiling of MI355X:
-    # profiles/microbench/gather_bench.hip, 8..32-B random reads over a 4 GB table run
-    # at 49-52 G accesses/s (profiles/r01/gather_bench*.txt)
-    eb = info.prefix_bytes // (info.prefix_sigma ** K) if K else 0
-    hits = int(round(B * table_frac)) if K else 0
-    accesses = (alg_random - eb * hits) / info.line_bytes + hits
-    total_units = B * world * args.steps
-    value = total_units / elapsed
-    kern_avg_s = statistics.mean(kern_ms) / 1e3
-    achieved = alg_bytes / kern_avg_s / 1e9
-    out = pg.local[(args.steps - 1) % pg.depth]
-    counts = out.cpu().numpy()
-    found = int((counts >= 1).sum())
-
-    res = None
-    if rank == 0:
-        traffic = None
-        prof = os.path.join(ROOT, "profiles", "pmc_count.json")
-        engine = {1: "occ", 2: "qwm", 3: "locc"}.get(info.engine, "wm%d" % info.line_bytes)
-        wl = "%s:%d:m%d:b%d:%s:k%d" % (args.kind, N, m, B, engine, info.prefix_k)
-        if info.context_q:
-            wl += ":ctx%d" % info.context_q
-        if info.record_bytes:
-            wl += ":rec%d" % info.record_bytes  # context records (32-/16-B prefix-table entries)
-        if args.queries != "text":
-            wl += ":" + args.queries
-        if os.path.exists(prof):
-            pj = json.load(open(prof))
-            if pj.get("workload") == wl:
-                traffic = pj.get("hbm_bytes_per_launch")
-        res = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "patterns/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic",
-            "config": {"workload": "C4: %s text n=%d (incl. terminator), Q_%s %d-mers, count()"
-                       % (args.kind.upper(), N, args.queries, m) if L == 3_999_999_999 else
-                       "%s text n=%d, Q_%s %d-mers, count()" % (args.kind, N, args.queries, m),
-                       "batch_per_gpu": B, "global_batch": B * world, "m": m,
-                       "ssa_stride": args.ssa_stride, "parallelism": "dp%d" % world,
-                       "index": "replicated per GPU", "workload_key": wl,
-                       "collective": "gather of counts to rank 0 (%s), overlapped"
-                       % ("RCCL" if args.dist_backend == "nccl" else args.dist_backend) if coll
-                       else "none (independent query shards)",
-                       "engine": ("%s + left contexts (q=%d)%s" % (
-                                  "learned occurrence lines" if info.engine == 3 else "occurrence lines",
-                                  info.context_q,
-                                  " + %d-B context records" % info.record_bytes if info.record_bytes
-                                  else "")) if info.engine in (1, 3) else
-                       "quaternary wavelet matrix (%d levels of occurrence lines)" % info.levels
-                       if info.engine == 2 else
-                       "wavelet matrix (%d-B rank lines)" % info.line_bytes},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "alg_random_bytes_per_launch": alg_random,
-                         "alg_stream_bytes_per_launch": alg_stream, "line_bytes": line_bytes,
-                         "prefix_k": K, "prefix_table_hit_frac": table_frac,
-                         "context_q": info.context_q,
-                         "alg_bytes_per_query": alg_bytes / B,
-                         # SURVEY.md §8(d)'s per-query figure for the reference's
-                         # structure (64 B x 8 levels x 2 ranks x (m-1) steps), for
-                         # comparison only: this engine reads alg_bytes_per_query
-                         "survey_alg_bytes_per_query": 64 * 8 * 2 * (m - 1),
-                         "survey_equivalent_GBs": 64 * 8 * 2 * (m - 1) * B / kern_avg_s / 1e9,
-                         "random_accesses_per_launch": accesses,
-                         "random_accesses_per_s": accesses / kern_avg_s,
-                         "random_access_ceiling_per_s": 5.0e10,
-                         "frac_of_random_access_ceiling": accesses / kern_avg_s / 5.0e10,
-                         "kernel_ms_mean": kern_avg_s * 1e3,
-                         "kernel_ms_min": min(kern_ms)},
-            "build_s": build_s,
-            "replicate": args.replicate if world > 1 else "single",
-            "replicate_s": replicate_s,
-            "found_frac": found / B,
-        }
-
-    # ---- locate (fm_index.cpp:107-157) on a prefix of the batch, N=1 only ----
-    if rank == 0 and world == 1 and args.locate_batch:
-        Lq = min(args.locate_batch, B)
-        d_sp = torch.empty(Lq, dtype=torch.int64, device=dev)
-        d_oo = torch.empty(Lq + 1, dtype=torch.int64, device=dev)
-        lt = []
-        for it in range(3):
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            tot = idx.locate_ranges_device(pats.data_ptr(), offs.data_ptr(), Lq, 100000,
-                                           d_sp.data_ptr(), d_oo.data_ptr(), sh)
-            if it == 0:
-                d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
-            idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), Lq, tot, d_pos.data_ptr(), sh)
-            torch.cuda.synchronize()
-            lt.append(time.perf_counter() - t1)
-        tl = min(lt)
-        # every reported position spells its pattern (full-size property check)
+        t1 = time.perf_counter()
+        tot = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000,
+                                       d_sp.data_ptr(), d_oo.data_ptr(), sh)
+        d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+        idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh)
+        parts = shard.gather_v(d_pos[:tot], world, rank)
+        torch.cuda.synchronize()
+        tl = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
         pos = d_pos[:tot]
         oo = d_oo.cpu().numpy()
-        owner = torch.from_numpy(np.repeat(np.arange(Lq), np.diff(oo).astype(np.int64))).to(dev)
+        owner = torch.from_numpy(np.repeat(np.arange(B), np.diff(oo).astype(np.int64))).to(dev)
         win = text[(pos.unsqueeze(1) + torch.arange(m, device=dev)).long()]
-        ok = bool((win == pats.view(B, m)[owner]).all().item())
-        res["locate"] = {"patterns": Lq, "positions": int(tot), "seconds": tl,
-                         "patterns_per_s": Lq / tl, "positions_per_s": tot / tl,
-                         "limit": 100000, "positions_verified": ok}
-        del d_sp, d_oo, d_pos, owner, win
+        okt = torch.tensor([int(bool((win == W.pats.view(B, m)[owner]).all().item()))],
+                           dtype=torch.int64, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        tt = torch.tensor([tot], dtype=torch.int64, device=dev)
+        dist.all_reduce(tt)
+        if rank == 0:
+            res["locate"] = {"patterns": B * world, "positions": int(tt.item()),
+                             "seconds": tl.item(), "patterns_per_s": B * world / tl.item(),
+                             "positions_per_s": int(tt.item()) / tl.item(), "limit": 100000,
+                             "positions_verified": bool(okt.item()),
+                             "gathered_positions": int(sum(p.numel() for p in parts)),
+                             "collective": "gather_v of every rank's positions to rank 0"}
+        del d_sp, d_oo, d_pos, owner, win, parts
 
-    # ---- the same batch as one-length k-mers back to back (cs_fm_count_fixed_device: no
-    #      offsets array to read), N=1 only: reported beside value, never as value ----
-    if rank == 0 and world == 1:
-        fo = torch.empty(B, dtype=torch.int64, device=dev)
-        for k in range(max(args.warmup, 1)):
-            idx.count_fixed_device(pats.data_ptr(), m, B, fo.data_ptr(), sh)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for k in range(args.steps):
-            idx.count_fixed_device(pats.data_ptr(), m, B, fo.data_ptr(), sh)
-        torch.cuda.synchronize()
-        tf = (time.perf_counter() - t1) / args.steps
-        res["count_fixed"] = {"patterns": B, "m": m, "ms_per_step": tf * 1e3,
-                              "patterns_per_s": B / tf,
-                              "matches_batch": bool(np.array_equal(fo.cpu().numpy(), counts))}
-        del fo
-
-    # ---- the same batch handed over in host memory (cs_fm_count_batch: PCIe in and out
-    #      inside the call), N=1 only: reported beside value, never as value ----
-    if rank == 0 and world == 1 and args.host_batch:
-        hbuf = pats.cpu().numpy()
-        hoffs = offs.cpu().numpy().astype(np.uint64)
-        ht = []
-        for it in range(3):
-            t1 = time.perf_counter()
-            hc = idx.count_batch(buf=hbuf, offs=hoffs)
-            ht.append(time.perf_counter() - t1)
-        res["host_batch"] = {"patterns": B, "seconds": min(ht), "patterns_per_s": B / min(ht),
-                             "h2d_bytes": int(hbuf.nbytes + hoffs.nbytes),
-                             "matches_device_batch": bool(np.array_equal(hc, counts.astype(np.uint64)))}
-        del hbuf, hoffs, hc
-
-    # ---- extract (fm_index.cpp:163-167) on the device, N=1 ----
-    if rank == 0 and world == 1 and args.extract_batch:
-        K_, XL = args.extract_batch, 20
-        g = torch.Generator(device="cpu").manual_seed(7)
-        xpos = torch.randint(0, N - XL, (K_,), generator=g, dtype=torch.int64).to(dev)
-        xlen = torch.full((K_,), XL, dtype=torch.int64, device=dev)
-        xoff = torch.arange(0, (K_ + 1) * XL, XL, dtype=torch.int64, device=dev)
-        xout = torch.empty(K_ * XL, dtype=torch.uint8, device=dev)
-        xt = []
-        for it in range(3):
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            idx.extract_device(xpos.data_ptr(), xlen.data_ptr(), xoff.data_ptr(), K_,
-                               xout.data_ptr(), sh)
-            torch.cuda.synchronize()
-            xt.append(time.perf_counter() - t1)
-        want = text[(xpos.unsqueeze(1) + torch.arange(XL, device=dev)).long()].reshape(-1)
-        res["extract"] = {"queries": K_, "len": XL, "seconds": min(xt),
-                          "queries_per_s": K_ / min(xt), "bytes_per_s": K_ * XL / min(xt),
-                          "verified": bool(torch.equal(want, xout)),
-                          "method": ("copy from the text in HBM (text_.substr)" if info.text_in_hbm
-                                     else "LF inversion from inverse-SA samples")}
-        del xpos, xlen, xoff, xout, want
+    # ---- N = 1 legs on the headline index ----
+    lg = {}
+    stream_m = B * m + (B + 1) * 8
+    if need_main and legs & set(LEGS_MAIN):
+        steps, warm = max(3, args.steps // 2), 2
+        if "count_u32" in legs:
+            o4 = torch.empty(B, dtype=torch.int32, device=dev)
+            lg["count_u32"], _ = count_leg(
+                "count_u32", "the headline batch with uint32 counts (exact, n < 2^32)", idx, info, wl,
+                W, lambda: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B, o4.data_ptr(),
+                                               width=4, stream=sh),
+                0, stream_m + 4 * B, steps, warm, stream, sh, dev, counts,
+                lambda: o4.cpu().numpy().astype(np.int64))
+            del o4
+        if "count_packed" in legs and args.kind == "dna" and m <= 32:
+            # 2-bit packed patterns (8 B each, no offsets) and uint32 counts
+            lut = torch.full((256,), 0, dtype=torch.int64, device=dev)
+            lut[torch.tensor(list(b"ACGT"), device=dev)] = torch.arange(4, device=dev)
+            codes = lut[W.pats.view(B, m).long()]
+            packed = (codes << (2 * torch.arange(m, device=dev))).sum(dim=1)
+            del codes
+            o4 = torch.empty(B, dtype=torch.int32, device=dev)
+            lg["count_packed"], _ = count_leg(
+                "count_packed", "the headline batch as 2-bit packed DNA (8 B per pattern), uint32 "
+                "counts", idx, info, wl, W,
+                lambda: idx.count_packed_device(packed.data_ptr(), m, B, o4.data_ptr(), width=4,
+                                                stream=sh),
+                0, 8 * B + 4 * B, steps, warm, stream, sh, dev, counts,
+                lambda: o4.cpu().numpy().astype(np.int64), stream_read=8 * B)
+            del o4, packed
+        for name, fl, what in (("count_table_steps", 2, "prefix table, then the reference's backward-"
+                                "search steps (fm_index.cpp:90-96), one occurrence line per rank pair: "
+                                "no left contexts / context records (CS_Q_NO_CONTEXTS)"),
+                               ("count_lf_loop", 3, "the reference's whole backward-search loop "
+                                "(fm_index.cpp:84-98) from C[], every character one rank step over "
+                                "the occurrence lines (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS)")):
+            if name in legs:
+                o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                lg[name], _ = count_leg(
+                    name, what, idx, info, wl, W,
+                    lambda fl=fl, o8=o8: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
+                                                             o8.data_ptr(), flags=fl, stream=sh),
+                    fl, stream_m + 8 * B, max(3, steps // 4), 1, stream, sh, dev, counts,
+                    lambda o8=o8: o8.cpu().numpy())
+                del o8
+        for name, mm in (("count_m32", 32), ("count_m64", 64)):
+            if name in legs:
+                Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
+                o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                r, got = count_leg(
+                    name, "Q_text %d-mers through the headline index: prefix table, %d rank steps, "
+                    "then the left contexts" % (mm, mm - info.prefix_k - info.context_q),
+                    idx, info, wl, Wm,
+                    lambda Wm=Wm, o8=o8: idx.count_batch_device(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
+                                                                o8.data_ptr(), sh),
+                    0, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
+                    lambda o8=o8: o8.cpu().numpy())
+                r["found_frac"] = float((got >= 1).mean())
+                lg[name] = r
+                del Wm, o8
+        if "count_fixed" in legs:
+            # one-length k-mers back to back (cs_fm_count_fixed_device: no offsets array)
+            fo = torch.empty(B, dtype=torch.int64, device=dev)
+            lg["count_fixed"], _ = count_leg(
+                "count_fixed", "the headline batch as one-length k-mers (no offsets array)", idx, info,
+                wl, W, lambda: idx.count_fixed_device(W.pats.data_ptr(), m, B, fo.data_ptr(), sh),
+                0, B * m + 8 * B, steps, warm, stream, sh, dev, counts, lambda: fo.cpu().numpy(),
+                stream_read=B * m)
+            del fo
+        if "locate" in legs:
+            lg["locate"] = locate_leg("locate", "locate (fm_index.cpp:107-157), limit 100000: positions "
+                                      "from the full suffix array" if info.full_sa_bytes else
+                                      "locate, limit 100000", idx, info, wl, W, text, 0, dev, sh)
+        if "locate_ssa_rows" in legs:
+            lg["locate_ssa_rows"] = locate_leg(
+                "locate_ssa_rows", "locate with the reference's SSA walk (fm_index.cpp:125-153): LF over the occurrence "
+                "lines to a row with row %% %d == 0, SA sample + steps (CS_Q_NO_FULL_SA | "
+                "CS_Q_NO_WALK_LINES)" % args.ssa_stride, idx, info, wl, W, text, 4 | 8, dev, sh, reps=2)
+        if "host_batch" in legs and counts is not None:
+            # the batch handed over in host memory (PCIe in and out inside the call)
+            hbuf = W.pats.cpu().numpy()
+            hoffs = W.offs.cpu().numpy().astype(np.uint64)
+            ht = []
+            for it in range(3):
+                t1 = time.perf_counter()
+                hc = idx.count_batch(buf=hbuf, offs=hoffs)
+                ht.append(time.perf_counter() - t1)
+            lg["host_batch"] = {"patterns": B, "seconds": min(ht), "patterns_per_s": B / min(ht),
+                                "h2d_bytes": int(hbuf.nbytes + hoffs.nbytes),
+                                "matches_device_batch": bool(np.array_equal(hc, counts.astype(np.uint64)))}
+            del hbuf, hoffs, hc
+        if "extract" in legs and args.extract_batch:
+            K_, XL = args.extract_batch, 20
+            g = torch.Generator(device="cpu").manual_seed(7)
+            xpos = torch.randint(0, N - XL, (K_,), generator=g, dtype=torch.int64).to(dev)
+            xlen = torch.full((K_,), XL, dtype=torch.int64, device=dev)
+            xoff = torch.arange(0, (K_ + 1) * XL, XL, dtype=torch.int64, device=dev)
+            xout = torch.empty(K_ * XL, dtype=torch.uint8, device=dev)
+            xt = []
+            for it in range(3):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                idx.extract_device(xpos.data_ptr(), xlen.data_ptr(), xoff.data_ptr(), K_,
+                                   xout.data_ptr(), sh)
+                torch.cuda.synchronize()
+                xt.append(time.perf_counter() - t1)
+            want = text[(xpos.unsqueeze(1) + torch.arange(XL, device=dev)).long()].reshape(-1)
+            lg["extract"] = {"queries": K_, "len": XL, "seconds": min(xt),
+                             "queries_per_s": K_ / min(xt), "bytes_per_s": K_ * XL / min(xt),
+                             "verified": bool(torch.equal(want, xout)),
+                             "method": ("copy from the text in HBM (text_.substr)" if info.text_in_hbm
+                                        else "LF inversion from inverse-SA samples")}
+            del xpos, xlen, xoff, xout, want
 
     # ---- p50 single-pattern latency (>= 1000 single-pattern calls
     #      through the C++ facade, end to end, as tools/benchmark.cpp:154-166) ----
-    if rank == 0 and args.p50_calls:
+    if rank == 0 and args.p50_calls and counts is not None:
         import ctypes as C
-        hp = np.ascontiguousarray(pats[: args.p50_calls * m].cpu().numpy())
+        hp = np.ascontiguousarray(W.pats[: args.p50_calls * m].cpu().numpy())
         nq = hp.size // m
         blib = C.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libcs_bench.so"))
         fn = blib.cs_bench_facade_count_latency
@@ -410,7 +704,6 @@ def main():
                              "(FMIndex::serve), %d calls, steady_clock" % nq)
         res["p50_launch_us"] = float(np.median(lat_launch))
         res["p95_launch_us"] = float(np.percentile(lat_launch, 95))
-        # the same through the Python mirror (ctypes), for reference
         lat_py = []
         for q in range(min(nq, 1000)):
             b = hp[q * m:(q + 1) * m].tobytes()
@@ -418,62 +711,92 @@ def main():
             idx.count(b)
             lat_py.append((time.perf_counter() - t1) * 1e6)
         res["p50_python_us"] = float(np.median(lat_py))
-        res["in_batch_us_per_query"] = elapsed / args.steps / B * 1e6
+        res["in_batch_us_per_query"] = res["ms_per_step"] * 1e3 / B
 
-    # ---- CPU baseline: reference-faithful restatement on host cores (rank 0, N=1) ----
-    if args.cpu_queries is None:
-        args.cpu_queries = 256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16
-    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_queries > 0:
+    # ---- CPU baseline: the reference's count() and locate() on host cores (rank 0, N=1) ----
+    if rank == 0 and world == 1 and not args.no_cpu and counts is not None:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O  # CPU baseline / checker only
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        # the process's CPU share: OMP_NUM_THREADS on the GPU box (16 per GPU there; the
+        # machine's count is many times that), else the affinity set
+        threads = (args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+                   or len(os.sched_getaffinity(0)))
+        Q = args.cpu_queries
+        if Q is None:
+            Q = max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16, 2 * threads)
         t1 = time.perf_counter()
         d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
         idx.bwt_device(d_bwt.data_ptr(), sh)
         bwt = d_bwt.cpu().numpy()
         del d_bwt
         ref = O.Index(bwt=bwt, nthreads=threads)
-        del bwt
         prep_s = time.perf_counter() - t1
-        Q = args.cpu_queries
-        sample = pats[: Q * m].cpu().numpy()
+        sample = W.pats[: Q * m].cpu().numpy()
         soffs = np.arange(0, (Q + 1) * m, m, dtype=np.uint64)
         nt = min(threads, Q)
+        Qp = min(Q, nt)  # the restatement: one pattern per thread
         t1 = time.perf_counter()
-        cnt, lat = ref.count_batch(buf=sample, offs=soffs, nthreads=nt, faithful=True,
-                                   latencies=True)
+        cnt, lat = ref.count_batch(buf=sample[: Qp * m], offs=soffs[: Qp + 1], nthreads=nt,
+                                   faithful=True, latencies=True)
         cpu_s = time.perf_counter() - t1
         port = {
-            "value": Q / cpu_s, "unit": "patterns/s", "cores": nt, "kind": "port",
+            "value": Qp / cpu_s, "unit": "patterns/s", "cores": nt, "kind": "port",
             "sample": "first %d patterns of the batch, reference-faithful count() "
-                      "(oracle/fm_oracle.c faithful=1), %d host threads" % (Q, nt),
+                      "(oracle/fm_oracle.c faithful=1), %d host threads" % (Qp, nt),
             "p50_us": float(np.median(lat) / 1e3), "seconds": cpu_s, "prep_s": prep_s,
-            "matches_gpu": bool(np.array_equal(cnt, counts[:Q].astype(np.uint64)))}
+            "matches_gpu": bool(np.array_equal(cnt, counts[:Qp].astype(np.uint64)))}
         res["cpu_baseline"] = port
-        # the genuine reference's FMIndex::count (oracle/_ref/libcs_ref.so, built from
-        # the reference's sources) over its own BitVector tables of the same BWT
         if O.ref_lib() is not None:
+            # the genuine reference's FMIndex::count / locate (oracle/_ref/libcs_ref.so,
+            # built from the reference's sources) over its own BitVector tables of the
+            # same BWT, plus its bwt_ and ssa_ members for locate
             t1 = time.perf_counter()
             gref = O.RefCountIndex(ref)
+            ssa = idx.ssa().astype(np.uint32)
+            gref.attach_locate(bwt, ssa, args.ssa_stride)
             rprep = time.perf_counter() - t1
             t1 = time.perf_counter()
             rcnt, rlat = gref.count_batch(sample, soffs, nthreads=nt, latencies=True)
             ref_s = time.perf_counter() - t1
-            del gref
             res["cpu_baseline"] = {
                 "value": Q / ref_s, "unit": "patterns/s", "cores": nt, "kind": "reference",
-                "sample": "first %d patterns of the batch, the reference's own FMIndex::count "
-                          "(src/api/fm_index.cpp:79-101, oracle/_ref/libcs_ref.so) over its "
-                          "BitVector tables of the same BWT, %d host threads" % (Q, nt),
+                "sample": "first %d patterns of the batch (%d per thread), the reference's own "
+                          "FMIndex::count (src/api/fm_index.cpp:79-101, oracle/_ref/libcs_ref.so) "
+                          "over its BitVector tables of the same BWT, %d host threads"
+                          % (Q, Q // nt, nt),
                 "p50_us": float(np.median(rlat) / 1e3), "seconds": ref_s,
                 "prep_s": prep_s + rprep,
                 "matches_gpu": bool(np.array_equal(rcnt, counts[:Q].astype(np.uint64)))}
             res["cpu_port"] = port
-        # also the restatement's fast multi-threaded path (precomputed
-        # count_ones totals, the same wavelet rank) over a larger slice of the batch
+            # locate: one pattern per thread (a C4 locate is the count's search plus ~31
+            # LF steps, each a wavelet rank with the O(n) scans)
+            Ql = nt
+            t1 = time.perf_counter()
+            nout, lpos, llat = gref.locate_batch(sample[: Ql * m], soffs[: Ql + 1], limit=100000,
+                                                 nthreads=nt)
+            loc_s = time.perf_counter() - t1
+            # the GPU's positions of the same patterns
+            d_sp = torch.empty(Ql, dtype=torch.int64, device=dev)
+            d_oo = torch.empty(Ql + 1, dtype=torch.int64, device=dev)
+            gt = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), Ql, 100000,
+                                          d_sp.data_ptr(), d_oo.data_ptr(), sh)
+            d_pos = torch.empty(max(gt, 1), dtype=torch.int64, device=dev)
+            idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), Ql, gt, d_pos.data_ptr(), sh)
+            goo, gpos = d_oo.cpu().numpy(), d_pos[:gt].cpu().numpy()
+            lok = all(nout[q] == goo[q + 1] - goo[q] and
+                      lpos[q, :min(nout[q], lpos.shape[1])].tolist() ==
+                      gpos[goo[q]:goo[q] + min(nout[q], lpos.shape[1])].tolist() for q in range(Ql))
+            res["cpu_locate"] = {
+                "value": Ql / loc_s, "unit": "patterns/s", "cores": nt, "kind": "reference",
+                "sample": "first %d patterns of the batch (one per thread), the reference's own "
+                          "FMIndex::locate (src/api/fm_index.cpp:107-157), limit 100000, row-sampled "
+                          "SSA stride %d, %d host threads" % (Ql, args.ssa_stride, nt),
+                "p50_us": float(np.median(llat) / 1e3), "seconds": loc_s,
+                "positions": int(max(nout.sum(), 0)), "matches_gpu": bool(lok)}
+            del gref, d_sp, d_oo, d_pos
         Qf = min(args.cpu_fast_queries, B)
         if Qf > 0:
-            fs = pats[: Qf * m].cpu().numpy()
+            fs = W.pats[: Qf * m].cpu().numpy()
             foffs = np.arange(0, (Qf + 1) * m, m, dtype=np.uint64)
             t1 = time.perf_counter()
             fcnt = ref.count_batch(buf=fs, offs=foffs, nthreads=threads, faithful=False)
@@ -483,9 +806,112 @@ def main():
                 "sample": "first %d patterns of the batch, oracle count() with precomputed "
                           "totals (not the reference's cost model), %d host threads" % (Qf, threads),
                 "seconds": fast_s, "matches_gpu": bool(np.array_equal(fcnt, counts[:Qf].astype(np.uint64)))}
-        del ref
+        del ref, bwt
+
+    # ---- N = 1 legs on the reference's own structure: the binary wavelet matrix ----
+    if idx is not None and (legs & (set(LEGS_WM) | set(LEGS_WALK) | set(LEGS_RDNA))):
+        del idx
+        idx = None
+        torch.cuda.synchronize()
+    if legs & set(LEGS_WM):
+        wm, bs = build_index(pkg, text, N, args.ssa_stride, local_dev,
+                             {"CS_FM_ENGINE": "wavelet", "CS_FM_FULL_SA": "0"})
+        wi = wm.info()
+        wwl = workload_key(args.kind, N, m, B, wi, args.queries)
+        log(rank, "wavelet index built in %.1f s" % bs)
+        for name, fl, what in (("wm_count", 0, "the reference's 8-level binary wavelet matrix "
+                                "(src/core/wavelet.cpp:59-96 over BitVector::rank1, bitvector.cpp:"
+                                "165-230) in 32-B rank lines: prefix table, then one rank-line pair "
+                                "per non-pure level per step"),
+                               ("wm_lf_loop", 1, "the reference's structure and its whole backward-"
+                                "search loop from C[] (fm_index.cpp:84-98): every character an "
+                                "8-level wavelet rank pair (CS_Q_NO_PREFIX)")):
+            if name in legs:
+                o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                lg[name], _ = count_leg(
+                    name, what, wm, wi, wwl, W,
+                    lambda fl=fl, o8=o8: wm.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
+                                                            o8.data_ptr(), flags=fl, stream=sh),
+                    fl, stream_m + 8 * B, max(3, args.steps // 8), 1, stream, sh, dev, counts,
+                    lambda o8=o8: o8.cpu().numpy())
+                lg[name]["build_s"] = bs
+                del o8
+        if "wm_locate_ssa" in legs:
+            lg["wm_locate_ssa"] = locate_leg(
+                "wm_locate_ssa", "the reference's locate on its own structure: backward search, then the SSA walk "
+                "(fm_index.cpp:125-153) by LF over the 8-level wavelet matrix to a row with row %% "
+                "%d == 0" % args.ssa_stride, wm, wi, wwl, W, text, 0, dev, sh, reps=2)
+        del wm
+        torch.cuda.synchronize()
+    if legs & set(LEGS_WALK):
+        wk, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, {"CS_FM_FULL_SA": "0"})
+        ki = wk.info()
+        log(rank, "walk-line index built in %.1f s" % bs)
+        kwl = workload_key(args.kind, N, m, B, ki, args.queries) + ":walk"
+        lg["locate_ssa"] = locate_leg(
+            "locate_ssa", "locate without the full suffix array (the C5 layout at C4): SSA stride %d, LF walk over "
+            "walk lines (symbol, occ and sample mark in one 32-B line) to the first row the "
+            "reference samples or a text position marked every %d" % (args.ssa_stride, ki.position_stride),
+            wk, ki, kwl, W, text, 0, dev, sh)
+        lg["locate_ssa"]["build_s"] = bs
+        del wk
+        torch.cuda.synchronize()
+
+    if legs & set(LEGS_RDNA) and args.kind == "dna":
+        # repetitive DNA: copies of a 2^20-base seed with ~0.75 % substitutions, so a
+        # text 20-mer occurs in most of the ~3800 copies: ranges thousands of rows wide
+        # step through the rank structure instead of ending in a context record
+        rtext = torch.empty(N + 16, dtype=torch.uint8, device=dev)
+        pkg.synth_text_device("rdna", 42, L, rtext.data_ptr(), sh)
+        torch.cuda.synchronize()
+        rx, bs = build_index(pkg, rtext, N, args.ssa_stride, local_dev)
+        ri = rx.info()
+        rwl = workload_key("rdna", N, m, B, ri, args.queries)
+        log(rank, "repetitive-DNA index built in %.1f s" % bs)
+        RW = Workload(pkg, rtext, N, m, lo, B, args.kind, args.queries, dev, sh)
+        o8 = torch.empty(B, dtype=torch.int64, device=dev)
+        if "count_rdna" in legs:
+            r, got = count_leg(
+                "count_rdna", "Q_text 20-mers of a repetitive DNA text of the same size (copies of a "
+                "2^20-base seed, ~0.75 %% substitutions; cs_synth_text_device kind 2) through the "
+                "headline engine", rx, ri, rwl, RW,
+                lambda: rx.count_batch_device(RW.pats.data_ptr(), RW.offs.data_ptr(), B, o8.data_ptr(), sh),
+                0, stream_m + 8 * B, max(3, args.steps // 4), 1, stream, sh, dev, None,
+                lambda: o8.cpu().numpy())
+            # the search paths taken, from the per-query bytes of the measurement twin:
+            # one 16-B context record alone, or more reads (context sectors, rank steps)
+            qb = torch.empty(B, dtype=torch.int64, device=dev)
+            rx.count_bytes_device(RW.pats.data_ptr(), RW.offs.data_ptr(), B, qb.data_ptr(), sh)
+            eb = ri.prefix_bytes // (ri.prefix_sigma ** ri.prefix_k) if ri.prefix_k else 0
+            r.update({"build_s": bs, "found_frac": float((got >= 1).mean()),
+                      "count_mean": float(got.mean()), "count_p50": float(np.median(got)),
+                      "count_p99": float(np.percentile(got, 99)), "count_max": int(got.max()),
+                      "record_only_frac": float((qb == eb).float().mean().item()),
+                      "fallback_frac": float((qb > eb).float().mean().item())})
+            del qb
+            lg["count_rdna"] = r
+        if "locate_rdna" in legs:
+            # 1/125 of the batch: ~3,300 positions per pattern at limit 100000
+            LB = max(1, B // 125)
+            LW = Workload.__new__(Workload)
+            LW.m, LW.B, LW.pats, LW.offs = m, LB, RW.pats[: LB * m], RW.offs[: LB + 1]
+            lg["locate_rdna"] = locate_leg(
+                "locate_rdna", "locate (limit 100000) of %d repetitive-DNA 20-mers: thousands of "
+                "positions per pattern from the full suffix array" % LB, rx, ri, rwl, LW, rtext, 0,
+                dev, sh, reps=2)
+        del rx, RW, o8, rtext
+        torch.cuda.synchronize()
 
     if rank == 0:
+        if args.only:
+            res = {"only": args.only, "workload_key": wl if need_main else None,
+                   **({"count": res.get("roofline")} if args.only == "count" else {}),
+                   "legs": lg}
+        elif lg:
+            # the locate leg stays at the top level as before
+            if "locate" in lg:
+                res["locate"] = lg["locate"]
+            res["legs"] = lg
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

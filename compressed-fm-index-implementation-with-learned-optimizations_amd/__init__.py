@@ -528,8 +528,10 @@ def pack_dna(patterns) -> np.ndarray:
 
 
 def synth_text_device(kind: str, seed: int, length: int, d_out: int, stream: int = 0):
-    """SURVEY §8(d) text (kind 'dna' | 'bytes'), length+1 bytes incl. terminator."""
-    _check(lib().cs_synth_text_device(0 if kind == "dna" else 1, seed, length, d_out, stream or None))
+    """SURVEY §8(d) text (kind 'dna' | 'bytes'), or 'rdna' (repetitive DNA: copies of a
+    2^20-base seed with ~0.75 % substitutions); length+1 bytes incl. terminator."""
+    k = {"dna": 0, "bytes": 1, "rdna": 2}[kind]
+    _check(lib().cs_synth_text_device(k, seed, length, d_out, stream or None))
 
 
 def synth_patterns_device(d_text: int, N: int, m: int, first: int, npat: int, seed: int,

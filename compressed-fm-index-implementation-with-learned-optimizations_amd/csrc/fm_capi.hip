@@ -3,6 +3,7 @@
 // without a HIP device every call fails with CS_ERR_NO_DEVICE.
 #include <chrono>
 #include <cstdlib>
+#include <map>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -74,44 +75,107 @@ cs_status scratch_ready(const cs_fm_index* h) {
   return CS_OK;
 }
 
-// Page-locks a large caller buffer for the duration of a call, so its copies run as
-// DMA at PCIe rate instead of through the runtime's pageable staging.  Only the pages
-// lying wholly inside the buffer are registered: a neighbouring allocation sharing the
-// first or last page is never covered (the runtime would then take a copy to or from
-// that neighbour for pinned memory and reject it).  copy() moves the buffer as head
-// (pageable), registered body and tail (pageable).  Small buffers and buffers that
-// cannot be registered (e.g. already pinned) are left alone.
+// Page-locked caller pages, shared by concurrent calls: a process-wide registry of
+// registered page ranges with reference counts, so two calls passing the same large
+// buffer share one hipHostRegister and the pages are unregistered only after the last
+// of them has synchronised its copies.
+struct PinRegistry {
+  std::mutex mu;
+  std::map<uintptr_t, std::pair<uintptr_t, int>> m;  // start -> (end, references)
+  // [lo, hi) usable for DMA: inside a registered range (one more reference) or newly
+  // registered; false when it overlaps a registration without lying inside it
+  bool acquire(uintptr_t lo, uintptr_t hi) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.upper_bound(lo);
+    if (it != m.begin()) {
+      auto pv = std::prev(it);
+      if (pv->second.first > lo) {  // overlaps the range starting at or before lo
+        if (pv->second.first >= hi) {
+          ++pv->second.second;
+          return true;
+        }
+        return false;
+      }
+    }
+    if (it != m.end() && it->first < hi) return false;
+    if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    m[lo] = {hi, 1};
+    return true;
+  }
+  void release(uintptr_t lo) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.upper_bound(lo);
+    if (it == m.begin()) return;
+    --it;
+    if (--it->second.second == 0) {
+      (void)hipHostUnregister(reinterpret_cast<void*>(it->first));
+      m.erase(it);
+    }
+  }
+};
+PinRegistry& pin_registry() {
+  static PinRegistry r;
+  return r;
+}
+
+// A large caller buffer for the duration of a call: its whole inner pages are used
+// for DMA at PCIe rate while the registry holds them; the partial first and last pages
+// (and a buffer whose pages cannot be held) go through the handle's pinned arena with
+// synchronous copies, so no copy ever treats pages another call may unregister as
+// pinned.  Small buffers use plain copies.
 struct HostPin {
   static constexpr uint64_t kMinBytes = 16ull << 20;
-  uintptr_t a = 0, e = 0;  // registered pages [a, e)
+  uintptr_t a = 0, e = 0;  // held pages [a, e)
   hipStream_t st = nullptr;
+  const cs_fm_index* h = nullptr;
   HostPin() = default;
   HostPin(const HostPin&) = delete;
   HostPin& operator=(const HostPin&) = delete;
-  void pin(const void* p, uint64_t bytes, hipStream_t s) {
+  void pin(const cs_fm_index* hh, const void* p, uint64_t bytes, hipStream_t s) {
+    h = hh;
     if (bytes < kMinBytes || a) return;
     const uintptr_t lo = (reinterpret_cast<uintptr_t>(p) + 4095) & ~uintptr_t(4095);
     const uintptr_t hi = (reinterpret_cast<uintptr_t>(p) + bytes) & ~uintptr_t(4095);
-    if (hi <= lo) return;
-    if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault) == hipSuccess) {
-      a = lo;
-      e = hi;
-      st = s;
-    } else {
-      (void)hipGetLastError();
-    }
+    if (hi <= lo || !pin_registry().acquire(lo, hi)) return;
+    a = lo;
+    e = hi;
+    st = s;
   }
-  // host <-> device copy of the pinned buffer `host` (bytes), split at the registered pages
+  // synchronous copy of a span the registry does not hold, through the pinned arena
+  hipError_t bounce(void* dst, const void* src, uint64_t n, bool h2d, hipStream_t s) const {
+    std::unique_lock<std::mutex> lk(h->scratch.mu);
+    if (scratch_ready(h) != CS_OK) return hipErrorOutOfMemory;
+    for (uint64_t o = 0; o < n; o += cs_fm_index::kScratchBytes) {
+      const uint64_t k = n - o < cs_fm_index::kScratchBytes ? n - o : cs_fm_index::kScratchBytes;
+      hipError_t r;
+      if (h2d) {
+        std::memcpy(h->scratch.h, static_cast<const uint8_t*>(src) + o, k);
+        r = hipMemcpyAsync(static_cast<uint8_t*>(dst) + o, h->scratch.h, k, hipMemcpyHostToDevice, s);
+      } else {
+        r = hipMemcpyAsync(h->scratch.h, static_cast<const uint8_t*>(src) + o, k, hipMemcpyDeviceToHost, s);
+      }
+      if (r == hipSuccess) r = hipStreamSynchronize(s);
+      if (r != hipSuccess) return r;
+      if (!h2d) std::memcpy(static_cast<uint8_t*>(dst) + o, h->scratch.h, k);
+    }
+    return hipSuccess;
+  }
+  // host <-> device copy of the buffer `host` (bytes), split at the held pages
   hipError_t copy(void* dst, const void* src, uint64_t bytes, bool h2d, hipStream_t s) const {
-    const uintptr_t h = reinterpret_cast<uintptr_t>(h2d ? src : dst);
+    const uintptr_t hb = reinterpret_cast<uintptr_t>(h2d ? src : dst);
     const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
-    if (!a || a < h || e > h + bytes) return hipMemcpyAsync(dst, src, bytes, kind, s);
-    const uint64_t cut[4] = {0, a - h, e - h, bytes};
+    if (bytes < kMinBytes) return hipMemcpyAsync(dst, src, bytes, kind, s);
+    if (!a || a < hb || e > hb + bytes) return bounce(dst, src, bytes, h2d, s);
+    const uint64_t cut[4] = {0, a - hb, e - hb, bytes};
     for (int i = 0; i < 3; ++i) {
       const uint64_t n = cut[i + 1] - cut[i];
       if (!n) continue;
-      hipError_t r = hipMemcpyAsync(static_cast<uint8_t*>(dst) + cut[i],
-                                    static_cast<const uint8_t*>(src) + cut[i], n, kind, s);
+      void* d = static_cast<uint8_t*>(dst) + cut[i];
+      const void* q = static_cast<const uint8_t*>(src) + cut[i];
+      hipError_t r = i == 1 ? hipMemcpyAsync(d, q, n, kind, s) : bounce(d, q, n, h2d, s);
       if (r != hipSuccess) return r;
     }
     return hipSuccess;
@@ -119,7 +183,7 @@ struct HostPin {
   ~HostPin() {
     if (!a) return;
     (void)hipStreamSynchronize(st);  // no copy may still read the pages
-    (void)hipHostUnregister(reinterpret_cast<void*>(a));
+    pin_registry().release(a);
   }
 };
 
@@ -127,14 +191,15 @@ struct HostPin {
 struct StagedBatch {
   HostPin pin_pats, pin_offs;
   StreamBuf pats, offs;
-  cs_status load(const uint8_t* p, const uint64_t* o, uint64_t npat, hipStream_t st) {
+  cs_status load(const cs_fm_index* h, const uint8_t* p, const uint64_t* o, uint64_t npat,
+                 hipStream_t st) {
     const uint64_t bytes = o[npat] - o[0];
     FMX_HIP(pats.alloc(bytes + 16, st));
     FMX_HIP(offs.alloc((npat + 1) * 8, st));
-    pin_pats.pin(p + o[0], bytes, st);
+    pin_pats.pin(h, p + o[0], bytes, st);
     if (bytes) FMX_HIP(pin_pats.copy(pats.p, p + o[0], bytes, true, st));
     if (o[0] == 0) {
-      pin_offs.pin(o, (npat + 1) * 8, st);
+      pin_offs.pin(h, o, (npat + 1) * 8, st);
       FMX_HIP(pin_offs.copy(offs.p, o, (npat + 1) * 8, true, st));
     } else {  // rebase so offsets index the staged bytes
       std::vector<uint64_t> r(npat + 1);
@@ -182,7 +247,7 @@ cs_status server_shutdown(const cs_fm_index* h) {
   if (S.mbox) (void)hipHostFree(S.mbox);
   S.st = nullptr;
   S.mbox = S.resp = nullptr;
-  S.enabled = false;
+  S.enabled.store(false, std::memory_order_release);
   return s;
 }
 
@@ -521,9 +586,9 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   hipStream_t st = (hipStream_t)stream;
   const uint64_t bytes = offs[npat] - offs[0];
   const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
-  if (npat == 1 && bytes <= kServeMax && h->server.enabled) {
+  if (npat == 1 && bytes <= kServeMax && h->server.enabled.load(std::memory_order_acquire)) {
     std::unique_lock<std::mutex> lk(h->server.mu);
-    if (h->server.enabled) return serve_count(h, pats + offs[0], (uint32_t)bytes, out_counts);
+    if (h->server.enabled.load(std::memory_order_acquire)) return serve_count(h, pats + offs[0], (uint32_t)bytes, out_counts);
   }
   if (npat == 1 && bytes <= OnePattern::kMax) {
     // single pattern (the p50 path): pattern in the kernel arguments, count written
@@ -578,11 +643,11 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   }
   HostPin pin_out;
   StagedBatch b;
-  s = b.load(pats, offs, npat, st);
+  s = b.load(h, pats, offs, npat, st);
   if (s != CS_OK) return s;
   StreamBuf d_out;
   FMX_HIP(d_out.alloc(npat * 8, st));
-  pin_out.pin(out_counts, npat * 8, st);
+  pin_out.pin(h, out_counts, npat * 8, st);
   s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
   if (s != CS_OK) return s;
   FMX_HIP(pin_out.copy(out_counts, d_out.p, npat * 8, false, st));
@@ -597,7 +662,7 @@ cs_status cs_fm_serve_start(const cs_fm_index* h, uint32_t idle_us) {
   auto& S = h->server;
   std::lock_guard<std::mutex> lk(S.mu);
   S.idle_us = idle_us ? idle_us : 10000;
-  if (S.enabled) return CS_OK;
+  if (S.enabled.load(std::memory_order_acquire)) return CS_OK;
   int khz = 100000;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device) != hipSuccess ||
       khz <= 0)
@@ -614,7 +679,7 @@ cs_status cs_fm_serve_start(const cs_fm_index* h, uint32_t idle_us) {
     (void)server_shutdown(h);
     return hip_fail(e, "hipStreamCreateWithFlags (server)");
   }
-  S.enabled = true;
+  S.enabled.store(true, std::memory_order_release);
   if ((s = server_launch(h, 0)) != CS_OK) (void)server_shutdown(h);
   return s;
 }
@@ -764,7 +829,7 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
   if ((s = check_offsets(offs, npat)) != CS_OK) return s;
   hipStream_t st = (hipStream_t)stream;
   StagedBatch b;
-  s = b.load(pats, offs, npat, st);
+  s = b.load(h, pats, offs, npat, st);
   if (s != CS_OK) return s;
   StreamBuf d_sp, d_oo;
   FMX_HIP(d_sp.alloc(npat * 8, st));

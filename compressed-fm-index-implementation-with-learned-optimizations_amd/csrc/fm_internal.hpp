@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 #include <mutex>
@@ -71,7 +72,7 @@ struct cs_fm_index {
     uint32_t seq = 0;          // tag of the last request written
     uint32_t idle_us = 0;
     uint64_t ticks_per_us = 100;
-    bool enabled = false;
+    std::atomic<bool> enabled{false};  // read without mu on the count path
     bool launched = false;     // a kernel was launched and its exit not yet observed
   };
   mutable Server server;

@@ -273,7 +273,26 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
   std::string meta;
   {
     FILE* f = std::fopen(join(d, "cs_fmindex.meta").c_str(), "r");
-    if (!f) return io_fail("cannot open: " + join(d, "cs_fmindex.meta"));
+    if (!f) {
+      // a reference-style index directory holding only its source text (the shipped
+      // sample.csidx/text.txt): built here as tools/build_index.cpp does — '$' appended
+      // unless the text ends in '$' or '\0', ssa_stride 32
+      FILE* t = std::fopen(join(d, "text.txt").c_str(), "rb");
+      if (!t) return io_fail("cannot open: " + join(d, "cs_fmindex.meta"));
+      std::vector<uint8_t> text;
+      uint8_t buf[1 << 16];
+      size_t k;
+      while ((k = std::fread(buf, 1, sizeof buf, t)) > 0) text.insert(text.end(), buf, buf + k);
+      std::fclose(t);
+      if (text.empty()) {
+        set_error("empty text: " + join(d, "text.txt"));
+        return CS_ERR_INVALID;
+      }
+      if (text.back() != '$' && text.back() != '\0') text.push_back('$');
+      cs_build_params bp;
+      cs_default_build_params(&bp);
+      return cs_fm_build_from_text(text.data(), text.size(), &bp, device, out);
+    }
     char buf[4096];
     size_t k;
     while ((k = std::fread(buf, 1, sizeof buf, f)) > 0) meta.append(buf, k);

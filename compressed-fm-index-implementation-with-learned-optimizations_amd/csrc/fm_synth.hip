@@ -49,6 +49,37 @@ __global__ void k_text(int kind, uint64_t seed, uint64_t len, uint8_t* __restric
   if (blockIdx.x == 0 && threadIdx.x == 0) out[len] = kind == 0 ? '$' : 0;
 }
 
+// Repetitive DNA (kind 2): copies of a 2^20-base seed sequence — the first 2^20 bases
+// of the kind-0 stream — each base substituted with probability 655/65536 by a
+// uniform one; one thread per 32 positions (they share the seed draw).
+constexpr uint64_t kRdnaSeedBits = 20;
+constexpr uint64_t kRdnaSalt = 0x5DEECE66Dull;
+constexpr uint32_t kRdnaRate = 655;  // of 65536: ~1.0 % drawn, ~0.75 % changed
+__global__ void k_text_rdna(uint64_t seed, uint64_t len, uint8_t* __restrict__ out) {
+  const char acgt[4] = {'A', 'C', 'G', 'T'};
+  const uint64_t ngroup = (len + 31) / 32;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < ngroup; g += stride) {
+    const uint64_t i0 = g * 32, o0 = i0 & ((1ull << kRdnaSeedBits) - 1);
+    const uint64_t x = mix64(seed + (o0 / 32 + 1) * kGamma);
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint64_t h = mix64((seed ^ kRdnaSalt) + (i0 + k + 1) * kGamma);
+      const uint32_t b = (h & 0xFFFFu) < kRdnaRate ? (uint32_t)(h >> 16) & 3u : (uint32_t)(x >> (2 * k)) & 3u;
+      w[k >> 2] |= (uint32_t)acgt[b] << (8 * (k & 3));
+    }
+    if (i0 + 32 <= len) {
+      uint4* o = reinterpret_cast<uint4*>(out + i0);
+      o[0] = make_uint4(w[0], w[1], w[2], w[3]);
+      o[1] = make_uint4(w[4], w[5], w[6], w[7]);
+    } else {
+      for (uint64_t k = 0; i0 + k < len; ++k) out[i0 + k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[len] = '$';
+}
+
 __global__ void k_patterns(const uint8_t* __restrict__ text, uint64_t N, uint64_t m, uint64_t first,
                            uint64_t npat, uint64_t seed, uint8_t* __restrict__ pats,
                            uint64_t* __restrict__ offs) {
@@ -95,9 +126,15 @@ using namespace fmx;
 extern "C" {
 
 cs_status cs_synth_text_device(int kind, uint64_t seed, uint64_t len, uint8_t* d_out, void* stream) {
-  if (!d_out || (kind != 0 && kind != 1)) {
+  if (!d_out || kind < 0 || kind > 2) {
     set_error("cs_synth_text_device: bad argument");
     return CS_ERR_INVALID;
+  }
+  if (kind == 2) {
+    k_text_rdna<<<grid_for((len + 31) / 32 + 1, 256, 65536), 256, 0, (hipStream_t)stream>>>(seed, len,
+                                                                                          d_out);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
   }
   const uint64_t ndraw = (len + 7) / 8;
   k_text<<<grid_for(ndraw, 256, 65536), 256, 0, (hipStream_t)stream>>>(kind, seed, len, d_out);

@@ -45,14 +45,17 @@ def gather_v(local: torch.Tensor, world: int, rank: int, dst: int = 0):
     """Gather variable-length 1-D tensors (e.g. located positions) to dst: an
     all_gather of the lengths, then a padded gather.  Returns the list of per-rank
     tensors on dst, else None."""
-    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
     if world == 1:
         return [local]
+    n = torch.tensor([local.numel()], dtype=torch.int64,
+                     device="cpu" if dist.get_backend() == "gloo" else local.device)
     lens = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(lens, n)
     lens = [int(x.item()) for x in lens]
     mx = max(lens) if lens else 0
-    buf = torch.zeros(max(mx, 1), dtype=local.dtype, device=local.device)
+    # gloo gathers host tensors only (the N-rank rehearsal on one GPU)
+    bdev = "cpu" if dist.get_backend() == "gloo" else local.device
+    buf = torch.zeros(max(mx, 1), dtype=local.dtype, device=bdev)
     buf[: local.numel()] = local
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
     dist.gather(buf, parts, dst=dst)
@@ -108,6 +111,13 @@ class PipelinedGather:
         if self.world == 1:
             return self.local[i]
         return torch.cat(self.recv[i]) if self.rank == self.dst else None
+
+    def result_parts(self, k: int):
+        """The per-rank buffers of step k on dst (valid after finish())."""
+        i = k % self.depth
+        if self.world == 1:
+            return [self.local[i]]
+        return list(self.recv[i]) if self.rank == self.dst else None
 
 
 def sharded_count(count_fn, total: int, world: int, rank: int, device, dst: int = 0):

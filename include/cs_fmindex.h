@@ -113,8 +113,11 @@ cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint
                        uint32_t ssa_stride, const uint8_t* text, int device, cs_fm_index** out);
 /* FMIndex::open_directory — fm_index.hpp:20 ("TODO: on-disk format"); the reference
  * throws (fm_index.cpp:71-73).  Here it opens an index written by
- * cs_fm_save_directory onto device CS_FM_DEVICE (default 0);
- * a missing or foreign directory fails with CS_ERR_INVALID ("cannot open: <path>"). */
+ * cs_fm_save_directory onto device CS_FM_DEVICE (default 0).
+ * A reference-style directory holding only its source text (text.txt, as the shipped
+ * sample.csidx/) is built on the device the way tools/build_index.cpp builds it ('$'
+ * appended unless the text ends in '$' or '\0', ssa_stride 32).  A missing or foreign
+ * directory fails with CS_ERR_INVALID ("cannot open: <path>"). */
 cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out);
 cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out);
 /* Writes the index (HBM images of every structure, plus the text when kept) to dir. */

@@ -20,6 +20,11 @@ extern "C" {
 
 /* kind 0: DNA, 32 bases per draw (2 bits each, LSB first) -> "ACGT", then '$'.
  * kind 1: bytes, 8 per draw, b -> 1 + ((b*255)>>8), then 0x00.
+ * kind 2: repetitive DNA — position i copies base i mod 2^20 of the kind-0 stream (the
+ *         seed sequence), substituted when h_i = splitmix64((seed ^ 0x5DEECE66D) +
+ *         (i+1)*0x9E3779B97F4A7C15) has (h_i & 0xFFFF) < 655 by "ACGT"[(h_i >> 16) & 3]
+ *         (~0.75 % of bases changed); then '$'.  Substrings recur in every copy: ranges
+ *         thousands of rows wide, the heavy-tailed case of genomic text.
  * Writes len+1 bytes to d_out (device).  Asynchronous on stream. */
 cs_status cs_synth_text_device(int kind, uint64_t seed, uint64_t len, uint8_t* d_out, void* stream);
 

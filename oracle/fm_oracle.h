@@ -109,6 +109,9 @@ uint64_t orc_splitmix64(uint64_t* state);
 void orc_gen_dna(uint64_t seed, uint64_t len, uint8_t* out);
 /* bytes: 8 per draw, b -> 1 + ((b*255)>>8), then 0x00.  Writes len+1 bytes. */
 void orc_gen_bytes(uint64_t seed, uint64_t len, uint8_t* out);
+/* repetitive DNA: copies of a 2^20-base seed sequence with ~0.75 % substitutions
+ * (cs_synth_text_device kind 2) */
+void orc_gen_rdna(uint64_t seed, uint64_t len, uint8_t* out);
 /* Q_text: pattern k = T[x_k % (N-m), +m) with x_k the k-th splitmix64 draw. */
 void orc_gen_patterns_text(const uint8_t* text, uint64_t N, uint64_t m, uint64_t npat,
                            uint64_t seed, uint8_t* out);

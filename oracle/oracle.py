@@ -81,6 +81,7 @@ def lib():
                                        C.c_uint64, C.c_int, C.c_int]),
         "orc_gen_dna": (None, [C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_bytes": (None, [C.c_uint64, C.c_uint64, _u8p]),
+        "orc_gen_rdna": (None, [C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_patterns_unif": (None, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_patterns_text": (None, [_u8p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
                                          _u8p]),
@@ -333,6 +334,14 @@ def gen_dna(seed: int, length: int) -> np.ndarray:
     """splitmix64, 32 bases per draw LSB-first, then '$'."""
     out = np.zeros(length + 1, np.uint8)
     lib().orc_gen_dna(seed, length, _u8(out))
+    return out
+
+
+def gen_rdna(seed: int, length: int) -> np.ndarray:
+    """Repetitive DNA (cs_synth_text_device kind 2): copies of a 2^20-base seed sequence
+    with ~0.75 % substitutions, then '$'."""
+    out = np.zeros(length + 1, np.uint8)
+    lib().orc_gen_rdna(seed, length, _u8(out))
     return out
 
 

@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""summarize_legs.py <prof_dir> <tag> — condense profile_legs.sh's rocprofv3 output.
+
+For every leg directory <prof_dir>/<leg>/: the per-kernel durations of the trace pass,
+the mean FETCH_SIZE and L2 hit rate of each profiled kernel, and the leg's own kernel
+(the count kernel of a count leg, the phase-2 kernel of a locate leg).  Writes
+<prof_dir>/stats.json and <prof_dir>/pmc_legs.json — the file bench.py reads as
+profiles/pmc_legs.json:
+
+  "<workload key>|<leg>": {kernel, fetch_size_kb_per_launch, read_requests_per_launch,
+                           stream_read_bytes_per_launch, hbm_bytes_per_launch, ...}
+
+HBM bytes from FETCH_SIZE (= TCC_EA0_RDREQ x 64 B on gfx950, MI355X_MICROARCH.md): the
+kernel's streamed reads (coalesced 128-B requests, tallied at 64 B — the guide's x2)
+count at their byte size, every other request is one random 32-B DRAM read (calibrated
+with profiles/microbench/gather_bench: one request per random read of 16-32 B, tallied
+at 64 B; profiles/r01/fetch_calibration.txt).
+"""
+import csv
+import glob
+import json
+import os
+import re
+import statistics
+import sys
+
+# the kernel that carries each leg's work
+LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
+              "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
+              "count_m64": "count", "count_fixed": "count", "wm_count": "count",
+              "wm_lf_loop": "count", "locate": "k_locate_sa", "locate_ssa_rows": "k_walk",
+              "wm_locate_ssa": "k_walk", "locate_ssa": "k_walk_short"}
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f) as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def short(name):
+    """Readable kernel name: k_count_ctx (count) / k_count_ctx_loc (locate phase 1) with
+    the template's U, packed flag and count width; the others by their base name."""
+    m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)>", name)
+    if m:
+        eng, u, loc, packed, w = m.groups()
+        if loc == "true":
+            return "k_count_ctx_loc"
+        return "k_count_ctx%s_w%s" % ("_packed" if packed == "true" else "", w)
+    m = re.search(r"k_count<[^,]*?(\w+)(<\w+>)?, (true|false)>", name)
+    if m:
+        return "k_count_packed" if m.group(3) == "true" else "k_count"
+    for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk",
+              "k_locate_ranges", "k_locate_sa_wide", "k_locate_sa", "k_expand_rows", "k_pack_wire"):
+        if k in name:
+            return k
+    return name[:48]
+
+
+def last_json(path):
+    try:
+        return json.loads(open(path).read().strip().splitlines()[-1])
+    except Exception:
+        return None
+
+
+def main():
+    d, tag = sys.argv[1], sys.argv[2]
+    stats, pmc_legs = {"tag": tag, "legs": {}}, {}
+    for ld in sorted(glob.glob(os.path.join(d, "*", ""))):
+        leg = os.path.basename(os.path.dirname(ld))
+        res = {"kernels": {}, "pmc": {}}
+        for r in rows(os.path.join(ld, "trace", "**", "*kernel_trace.csv")):
+            n = short(r.get("Kernel_Name", ""))
+            dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+            res["kernels"].setdefault(n, []).append(dur)
+        res["kernels"] = {n: {"dispatches": len(v), "mean_ns": statistics.mean(v), "min_ns": min(v),
+                              "total_ns": sum(v)}
+                          for n, v in sorted(res["kernels"].items(), key=lambda kv: -sum(kv[1]))}
+        for sub, names in (("pmc_fetch", ["FETCH_SIZE"]), ("pmc_l2", ["TCC_HIT_sum", "TCC_MISS_sum"])):
+            for r in rows(os.path.join(ld, sub, "**", "*counter_collection.csv")):
+                n = short(r.get("Kernel_Name", ""))
+                if r.get("Counter_Name") in names:
+                    res["pmc"].setdefault(n, {}).setdefault(r["Counter_Name"], []).append(
+                        float(r["Counter_Value"]))
+        for n, cs in res["pmc"].items():
+            for c, v in list(cs.items()):
+                cs[c] = statistics.mean(v)
+            if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
+                tot = cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"]
+                cs["l2_hit_rate"] = cs["TCC_HIT_sum"] / tot if tot else None
+        b = last_json(os.path.join(ld, "bench_trace.json")) or {}
+        res["bench"] = b
+        # the leg's kernel and its streamed reads
+        want = LEG_KERNEL.get(leg, "count")
+        if want == "count":
+            cands = [n for n in res["pmc"] if n.startswith("k_count_ctx_") or n == "k_count"]
+        else:
+            cands = [n for n in res["pmc"] if n == want]
+        kname = max(cands, key=lambda n: res["kernels"].get(n, {}).get("total_ns", 0)) if cands else None
+        lo = (b.get("legs") or {}).get(leg) or {}
+        if leg == "count":
+            stream_rd = (b.get("count") or {}).get("stream_read_bytes_per_launch")
+        elif "roofline" in lo:
+            stream_rd = lo["roofline"].get("stream_read_bytes_per_launch")
+        else:
+            stream_rd = lo.get("phase2_stream_read_bytes")
+        wl = lo.get("workload_key") or b.get("workload_key")  # the leg's own index
+        kc = res["pmc"].get(kname, {}) if kname else {}
+        if kname and "FETCH_SIZE" in kc and stream_rd is not None:
+            req = kc["FETCH_SIZE"] * 1024 / 64
+            e = {"leg": leg, "kernel": kname, "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
+                 "read_requests_per_launch": req, "stream_read_bytes_per_launch": stream_rd,
+                 "hbm_bytes_per_launch": stream_rd + max(req - stream_rd / 128, 0) * 32,
+                 "l2_hit_rate": kc.get("l2_hit_rate"),
+                 "kernel_mean_ns_profiled": res["kernels"].get(kname, {}).get("mean_ns"),
+                 "tag": tag}
+            e["workload"] = wl
+            pmc_legs["%s|%s" % (wl, leg)] = e
+            res["traffic"] = e
+        stats["legs"][leg] = res
+    with open(os.path.join(d, "stats.json"), "w") as f:
+        json.dump(stats, f, indent=1)
+    with open(os.path.join(d, "pmc_legs.json"), "w") as f:
+        json.dump(pmc_legs, f, indent=1)
+    print(json.dumps({k: {"kernel": v["kernel"], "hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
+                          "l2": v["l2_hit_rate"]} for k, v in pmc_legs.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -159,3 +159,109 @@ def test_host_batch_buffers_sharing_pages():
     assert st == 0, pkg.lib().cs_fm_last_error()
     assert np.array_equal(out, g.count_batch(buf=P.reshape(-1), offs=offs))
     assert (out >= 1).all()
+
+
+@pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "records16"])
+def test_import_alloc_commit(engine, monkeypatch):
+    """Replication without staging copies: the index's own part addresses
+    (cs_fm_export_part_ptrs) copied into the parts of a handle allocated for them
+    (cs_fm_import_alloc, then cs_fm_import_commit), through torch tensors over the raw
+    device memory (shard.device_bytes) — the copy answers as the original."""
+    if engine in ("records", "records16"):
+        monkeypatch.setenv("CS_FM_CTX_RECORDS", "1" if engine == "records" else "16")
+    elif engine != "auto":
+        monkeypatch.setenv("CS_FM_ENGINE", engine)
+    pkg = load_pkg()
+    import importlib
+    shard = importlib.import_module("cs_fmindex_amd.shard")
+    t = O.gen_dna(19, 40_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    meta, sizes = g.export_meta()
+    src = g.export_part_ptrs(len(sizes))
+    c, dst = pkg.FMIndex.import_alloc(meta, len(sizes), 0)
+    assert len(dst) == len(sizes) and all(dst)
+    for s, d, nb in zip(src, dst, sizes):
+        if nb:
+            shard.device_bytes(d, nb, "cuda").copy_(shard.device_bytes(s, nb, "cuda"))
+    c.import_commit()
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 17, 400)
+    pats = [bytes(r) for r in P] + [b"ACGTACGTAC", b"$", b""]
+    assert c.count_batch(pats).tolist() == g.count_batch(pats).tolist()
+    lo1, lp1 = g.locate_batch(pats, limit=9)
+    lo2, lp2 = c.locate_batch(pats, limit=9)
+    assert lo1.tolist() == lo2.tolist() and lp1.tolist() == lp2.tolist()
+
+
+def _wire_reference(counts, cap):
+    """The wire format of include/cs_fmindex.h (cs_counts_pack_wire), in numpy."""
+    counts = np.asarray(counts, np.uint64)
+    big = np.nonzero(counts >= 255)[0]
+    hdr = np.array([len(big), cap], np.uint64)
+    return hdr, set(zip(big.tolist(), counts[big].tolist())), np.minimum(counts, 255).astype(np.uint8)
+
+
+@pytest.mark.parametrize("npat,cap", [(0, 4), (1, 4), (7, 4), (1001, 4), (100_003, 64), (100_003, 0)])
+def test_counts_wire(npat, cap):
+    """cs_counts_pack_wire writes the documented layout (u8 counts, every count >= 255 as
+    one pair, the pair counter even past cap) and shard.unpack_counts restores the exact
+    counts, or raises when the pairs did not fit."""
+    pkg = load_pkg()
+    import importlib
+    shard = importlib.import_module("cs_fmindex_amd.shard")
+    rng = np.random.default_rng(npat + cap)
+    c = rng.integers(0, 300, npat).astype(np.int64)
+    c[rng.random(npat) < 0.9] %= 255  # mostly small, some >= 255
+    if npat > 3:
+        c[3] = 4_000_000_000
+    d = torch.from_numpy(c).cuda()
+    nb = pkg.counts_wire_bytes(npat, cap)
+    assert nb == 16 + 16 * cap + ((npat + 7) // 8) * 8
+    wire = torch.full((nb,), 0xAB, dtype=torch.uint8, device="cuda")
+    shard.pack_counts(pkg, d, wire, cap=cap)
+    torch.cuda.synchronize()
+    w = wire.cpu().numpy()
+    hdr, pairs, u8 = _wire_reference(c, cap)
+    assert w[:16].view(np.uint64).tolist() == hdr.tolist()
+    got_pairs = w[16:16 + 16 * min(int(hdr[0]), cap)].view(np.uint64).reshape(-1, 2)
+    assert set(map(tuple, got_pairs.tolist())) <= pairs and len(got_pairs) == min(int(hdr[0]), cap)
+    assert w[16 + 16 * cap:16 + 16 * cap + npat].tolist() == u8.tolist()
+    if hdr[0] <= cap:
+        assert shard.unpack_counts(wire, npat).cpu().tolist() == c.tolist()
+    else:
+        with pytest.raises(OverflowError):
+            shard.unpack_counts(wire, npat)
+
+
+def test_concurrent_host_batches_share_pages():
+    """Two host threads count batches over the same large buffer at once — one the whole
+    buffer, one a window starting inside it (overlapping registrations) — on distinct
+    streams: the pin registry shares or bounces the pages, and both get the
+    single-thread answer, repeatedly."""
+    import threading
+    pkg = load_pkg()
+    t = O.gen_dna(23, 200_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    m = 24
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), m, 1_200_000)  # 28.8 MB of patterns
+    buf = np.ascontiguousarray(P.reshape(-1))
+    offs = np.arange(0, (len(P) + 1) * m, m, dtype=np.uint64)
+    want = g.count_batch(buf=buf, offs=offs)
+    lo = 700_001  # window: patterns [lo, end) — its first page lies inside the first buffer
+    res, errs = {}, []
+
+    def run(key, o):
+        try:
+            for _ in range(4):
+                res.setdefault(key, []).append(g.count_batch(buf=buf, offs=o).copy())
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=("all", offs)),
+          threading.Thread(target=run, args=("win", offs[lo:]))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    assert all(np.array_equal(r, want) for r in res["all"])
+    assert all(np.array_equal(r, want[lo:]) for r in res["win"])

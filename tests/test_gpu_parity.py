@@ -761,3 +761,50 @@ def test_count_packed(built, pkg, name):
                                       flags=f)
                 torch.cuda.synchronize()
                 assert out.cpu().numpy().astype(np.uint64).tolist() == want.tolist(), (name, m, f, width)
+
+
+def test_repetitive_text_vs_oracle(pkg):
+    """Heavy-tailed ranges (genomic repeats): 500 copies of a 4000-base seed with ~1 %
+    substitutions — 20-mers occur hundreds of times, so searches leave the context
+    records and the left contexts and step through wide ranges, and locate walks many
+    rows per pattern; counts and positions (limit 50 and 5000) equal the oracle's."""
+    rng = np.random.default_rng(12)
+    seed = rng.choice(list(b"ACGT"), 4000).astype(np.uint8)
+    t = np.tile(seed, 500)
+    mut = rng.random(len(t)) < 0.01
+    t[mut] = rng.choice(list(b"ACGT"), int(mut.sum())).astype(np.uint8)
+    t = t.tobytes() + b"$"
+    g = pkg.FMIndex.build_from_text(t)
+    o = O.Index(t)
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), 20, 3000, seed=4)
+    pats = [bytes(p) for p in P] + [bytes(p) for p in O.gen_patterns_text(np.frombuffer(t, np.uint8), 9, 500, seed=5)]
+    buf, offs = O.pack_patterns(pats)
+    want = o.count_batch(buf=buf, offs=offs, nthreads=8)
+    assert np.median(want[:3000]) > 100
+    assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
+    for lim in (50, 5000):
+        sub = pats[::7]
+        b2, o2 = O.pack_patterns(sub)
+        woffs, wpos = o.locate_batch(buf=b2, offs=o2, limit=lim, nthreads=8)
+        goffs, gpos = g.locate_batch(buf=b2, offs=o2, limit=lim)
+        assert np.array_equal(goffs, woffs) and np.array_equal(gpos, wpos), lim
+
+
+def test_open_reference_style_directory(pkg, tmp_path):
+    """open_directory on a directory shaped like the reference's shipped sample.csidx/
+    (only its text.txt; tests/golden/sample_csidx is that file): built as
+    tools/build_index.cpp builds it ('$' appended, stride 32), answers as the oracle."""
+    import shutil
+    d = tmp_path / "sample.csidx"
+    shutil.copytree(os.path.join(os.path.dirname(__file__), "golden", "sample_csidx"), d)
+    t = open(d / "text.txt", "rb").read()
+    g = pkg.FMIndex.open_directory(str(d))
+    o = O.Index(t + b"$")
+    assert g.n == len(t) + 1
+    for p in (b"banana", b"ana", b"band", b"a", b"$", b"nan", b"x"):
+        assert g.count(p) == o.count(p), p
+        assert g.locate(p) == o.locate(p), p
+    empty = tmp_path / "empty"
+    empty.mkdir()
+    with pytest.raises(RuntimeError, match="cannot open"):
+        pkg.FMIndex.open_directory(str(empty))

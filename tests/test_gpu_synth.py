@@ -11,19 +11,19 @@ from conftest import load_pkg
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("kind", ["dna", "bytes"])
+@pytest.mark.parametrize("kind", ["dna", "bytes", "rdna"])
 def test_text_and_patterns(kind):
     pkg = load_pkg()
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream().cuda_stream
-    L = 100_003
+    L = 100_003 if kind != "rdna" else 3_000_017  # rdna: past two copies of its seed sequence
     text = torch.empty(L + 1 + 16, dtype=torch.uint8, device=dev)
     pkg.synth_text_device(kind, 42, L, text.data_ptr(), st)
-    want = O.gen_dna(42, L) if kind == "dna" else O.gen_bytes(42, L)
+    want = {"dna": O.gen_dna, "bytes": O.gen_bytes, "rdna": O.gen_rdna}[kind](42, L)
     torch.cuda.synchronize()
     host = text[: L + 1].cpu().numpy()
     assert np.array_equal(host, want)
-    m, npat, first = 20 if kind == "dna" else 8, 5000, 0
+    m, npat, first = 8 if kind == "bytes" else 20, 5000, 0
     pats = torch.empty(npat * m, dtype=torch.uint8, device=dev)
     offs = torch.empty(npat + 1, dtype=torch.int64, device=dev)
     pkg.synth_patterns_device(text.data_ptr(), L + 1, m, first, npat, 4242, pats.data_ptr(),

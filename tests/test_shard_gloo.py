@@ -66,6 +66,38 @@ def _worker(rank, world, port, total, result_path):
             step2 = None if step2 is None else step2.clone()
     pg.finish()
     last = pg.result(4)
+    # the counts' wire form (cs_counts_pack_wire's layout, packed here by the test since the
+    # packer is a HIP kernel) through the pipelined gather, decoded by shard.unpack_counts;
+    # counts >= 255 travel as pairs
+    cap = 4
+    nbw = 16 + 16 * cap + ((per + 7) // 8) * 8
+    pw = shard.PipelinedGather(nbw, world, rank, torch.uint8, torch.device("cpu"))
+    wire_ok = True
+    for k in range(3):
+        v = np.zeros(per, np.int64)
+        v[: hi - lo] = count_fn(lo, hi).numpy() * (1 + 200 * k) + rank
+        w = pw.buffer(k)
+        w.zero_()
+        big = np.nonzero(v >= 255)[0][:cap]
+        hdr = np.array([len(np.nonzero(v >= 255)[0]), cap], np.uint64)
+        w[:16] = torch.from_numpy(hdr.view(np.uint8))
+        pr = np.stack([big, v[big]], axis=1).astype(np.uint64).reshape(-1)
+        w[16:16 + 16 * len(big)] = torch.from_numpy(pr.view(np.uint8))
+        w[16 + 16 * cap:16 + 16 * cap + per] = torch.from_numpy(np.minimum(v, 255).astype(np.uint8))
+        pw.submit(k)
+        pw.finish()
+        parts_w = pw.result_parts(k)
+        if rank == 0:
+            for r in range(world):
+                a, b = shard.shard_range(total, r, world)
+                want_r = np.zeros(per, np.int64)
+                want_r[: b - a] = np.array([idx.count(bytes(pats[q])) for q in range(a, b)],
+                                           np.int64) * (1 + 200 * k) + r
+                try:
+                    got_r = shard.unpack_counts(parts_w[r], per).numpy()
+                    wire_ok &= bool(np.array_equal(got_r, want_r))
+                except OverflowError:
+                    wire_ok &= int((want_r >= 255).sum()) > cap
     if rank == 0:
         want = idx.count_batch([bytes(p) for p in pats]).astype(np.int64)
         ok = bool(np.array_equal(full.numpy(), want))
@@ -82,6 +114,7 @@ def _worker(rank, world, port, total, result_path):
                 v += idx.locate(pats[q].tobytes())
             want_pos.append(v)
         ok &= [p.tolist() for p in parts] == want_pos
+        ok &= wire_ok
         with open(result_path, "w") as f:
             f.write("ok" if ok else "mismatch")
     dist.barrier()
