@@ -105,6 +105,18 @@ struct PinRegistry {
     m[lo] = {hi, 1};
     return true;
   }
+  // runs f() (a plain copy of pageable caller memory [lo, hi)) only while no registration
+  // overlaps those bytes — else the runtime would take the range for pinned memory that
+  // does not cover it (hipErrorInvalidValue) — holding the lock so none starts meanwhile
+  template <class F>
+  bool unregistered(uintptr_t lo, uintptr_t hi, F&& f) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.upper_bound(lo);
+    if (it != m.begin() && std::prev(it)->second.first > lo) return false;
+    if (it != m.end() && it->first < hi) return false;
+    f();
+    return true;
+  }
   void release(uintptr_t lo) {
     std::lock_guard<std::mutex> lk(mu);
     auto it = m.upper_bound(lo);
@@ -121,11 +133,12 @@ PinRegistry& pin_registry() {
   return r;
 }
 
-// A large caller buffer for the duration of a call: its whole inner pages are used
-// for DMA at PCIe rate while the registry holds them; the partial first and last pages
-// (and a buffer whose pages cannot be held) go through the handle's pinned arena with
-// synchronous copies, so no copy ever treats pages another call may unregister as
-// pinned.  Small buffers use plain copies.
+// A caller buffer for the duration of a call: the whole inner pages of a large one are
+// used for DMA at PCIe rate while the registry holds them; every other span (small
+// buffers, the partial first and last pages, a buffer whose pages cannot be held) is a
+// plain copy when no registration overlaps it and goes through the handle's pinned arena
+// with synchronous copies when one does, so no copy ever takes pages another call
+// registered (and may unregister) for its own.
 struct HostPin {
   static constexpr uint64_t kMinBytes = 16ull << 20;
   uintptr_t a = 0, e = 0;  // held pages [a, e)
@@ -163,19 +176,30 @@ struct HostPin {
     }
     return hipSuccess;
   }
+  // a span of caller memory the registry does not hold for this call: a plain copy when
+  // no registration overlaps it, else through the pinned arena
+  hipError_t plain(void* dst, const void* src, uint64_t n, bool h2d, hipStream_t s) const {
+    const uintptr_t hp = reinterpret_cast<uintptr_t>(h2d ? src : dst);
+    hipError_t r = hipSuccess;
+    if (pin_registry().unregistered(hp, hp + n, [&] {
+          r = hipMemcpyAsync(dst, src, n, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s);
+        }))
+      return r;
+    return bounce(dst, src, n, h2d, s);
+  }
   // host <-> device copy of the buffer `host` (bytes), split at the held pages
   hipError_t copy(void* dst, const void* src, uint64_t bytes, bool h2d, hipStream_t s) const {
     const uintptr_t hb = reinterpret_cast<uintptr_t>(h2d ? src : dst);
-    const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
-    if (bytes < kMinBytes) return hipMemcpyAsync(dst, src, bytes, kind, s);
-    if (!a || a < hb || e > hb + bytes) return bounce(dst, src, bytes, h2d, s);
+    if (!bytes) return hipSuccess;
+    if (!a || a < hb || e > hb + bytes) return plain(dst, src, bytes, h2d, s);
     const uint64_t cut[4] = {0, a - hb, e - hb, bytes};
     for (int i = 0; i < 3; ++i) {
       const uint64_t n = cut[i + 1] - cut[i];
       if (!n) continue;
       void* d = static_cast<uint8_t*>(dst) + cut[i];
       const void* q = static_cast<const uint8_t*>(src) + cut[i];
-      hipError_t r = i == 1 ? hipMemcpyAsync(d, q, n, kind, s) : bounce(d, q, n, h2d, s);
+      hipError_t r = i == 1 ? hipMemcpyAsync(d, q, n, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, s)
+                            : plain(d, q, n, h2d, s);
       if (r != hipSuccess) return r;
     }
     return hipSuccess;
@@ -837,7 +861,11 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
   s = launch_locate_ranges(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
                            d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), total, st);
   if (s != CS_OK) return s;
-  FMX_HIP(hipMemcpyAsync(out_offs, d_oo.p, (npat + 1) * 8, hipMemcpyDeviceToHost, st));
+  {
+    HostPin po;
+    po.pin(h, out_offs, (npat + 1) * 8, st);
+    FMX_HIP(po.copy(out_offs, d_oo.p, (npat + 1) * 8, false, st));
+  }
   FMX_HIP(hipStreamSynchronize(st));
   if (*total > cap) {
     set_error("locate output capacity too small");
@@ -853,7 +881,9 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
   s = walk_checked(h, d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), npat, *total,
                    d_pos.as<uint64_t>(), st);
   if (s != CS_OK) return s;
-  FMX_HIP(hipMemcpyAsync(out_pos, d_pos.p, *total * 8, hipMemcpyDeviceToHost, st));
+  HostPin pp;
+  pp.pin(h, out_pos, *total * 8, st);
+  FMX_HIP(pp.copy(out_pos, d_pos.p, *total * 8, false, st));
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
 }

@@ -620,6 +620,9 @@ __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTab
 constexpr uint64_t kLocCtx = 1ull << 63;
 constexpr uint64_t kLocRowMask = (1ull << 38) - 1;
 constexpr uint32_t kLocSpanBits = 22;
+// locate phase 2 kernels fused with the records: a lane takes a pattern of at most this
+// many rows (every context window: <= kLocSpanBits); wider ranges go a block per range
+constexpr uint64_t kLocSmall = 32;
 // rows handed to the walk: row | k << kWalkAdjShift (k = positions to subtract)
 constexpr int kWalkAdjShift = 56;
 constexpr uint64_t kWalkRowMask = (1ull << kWalkAdjShift) - 1;
@@ -770,13 +773,42 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
+// the patterns of a k_count_ctx lane that need the general search (st == 3)
+template <class E, int U, bool kLoc, bool kPacked, int W>
+__device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable& T,
+                                             const uint8_t* __restrict__ pats, const uint8_t* st,
+                                             const uint64_t* o0, const uint32_t* m, uint64_t q0,
+                                             const CountOut& co, uint64_t limit,
+                                             uint64_t* __restrict__ rec) {
+  uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (st[j] != 3) continue;
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    if constexpr (kLoc) {
+      uint64_t r;
+      const uint64_t c = locate_search<E>(ix, T, pats + o0[j], m[j], r);
+      cnt_out[q] = c < limit ? c : limit;
+      rec[q] = r;
+    } else if constexpr (kPacked) {
+      const PackedDna P{o0[j]};
+      store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
+    } else {
+      const uint8_t* P = pats + o0[j];
+      store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
+    }
+  }
+}
+
 template <class E, int U, bool kLoc, bool kPacked, int W>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, CountOut co,
                                                     uint64_t limit, uint64_t* __restrict__ rec,
-                                                    uint64_t fixed_m) {
+                                                    uint64_t fixed_m, uint32_t nobar) {
   // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
+  // nobar: the general search reads the node table through the caches instead of a
+  // block-wide LDS copy, so no wave waits at a block barrier for the block's slowest
   // the stages need only the symbol -> (table digit, occurrence code) map in LDS (512 B
   // instead of the 10.8-KB node table: a shorter block prologue); a block stages the
   // node table only when one of its patterns needs the general search
@@ -957,26 +989,14 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   bool general = false;
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3;
+  if (nobar) {
+    if (general) general_rest<E, U, kLoc, kPacked, W>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec);
+    return;
+  }
   if (!__syncthreads_or(general)) return;
   load_table(T, ix.table);
   __syncthreads();
-#pragma unroll
-  for (int j = 0; j < U; ++j) {
-    if (st[j] != 3) continue;
-    const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if constexpr (kLoc) {
-      uint64_t r;
-      const uint64_t c = locate_search<E>(ix, T, pats + o0[j], m[j], r);
-      cnt_out[q] = c < limit ? c : limit;
-      rec[q] = r;
-    } else if constexpr (kPacked) {
-      const PackedDna P{o0[j]};
-      store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
-    } else {
-      const uint8_t* P = pats + o0[j];
-      store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
-    }
-  }
+  general_rest<E, U, kLoc, kPacked, W>(ix, T, pats, st, o0, m, q0, co, limit, rec);
 }
 
 // Single-pattern count (FMIndex::count, the p50 path): the pattern travels in the
@@ -1244,21 +1264,17 @@ __device__ __forceinline__ uint64_t walk_lf(const DevIndex& ix, const NodeTable&
 // Short walks (walk lines with text-position marks, lf_exact): every walk ends within
 // pstride - 1 steps, so one lane per reported row — coalesced row reads, no work
 // queue — and finished waves make room for new ones, as in the count kernels.
+// One short walk (walk lines with text-position marks): from BWT row `pos` by LF to the
+// first marked row or row the reference samples; writes out[j] = its text position
+// minus adj (mod n), or the LF steps when steps_only; an overrun records j in err.
 template <class W, bool kQ>
-__global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t* __restrict__ rows,
-                                                     uint64_t total, uint64_t* __restrict__ out,
-                                                     unsigned long long* __restrict__ err,
-                                                     uint32_t steps_only) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
-  __syncthreads();
-  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (j >= total) return;
+__device__ __forceinline__ void walk_short_one(const DevIndex& ix, const NodeTable& T, uint64_t pos,
+                                               uint64_t adj, uint64_t j, uint64_t* __restrict__ out,
+                                               unsigned long long* __restrict__ err,
+                                               uint32_t steps_only) {
   const uint64_t n = ix.n;
-  const uint64_t row = rows[j];
-  uint64_t pos = row & kWalkRowMask, steps = 0;
-  const uint64_t adj = row >> kWalkAdjShift;
   const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
+  uint64_t steps = 0;
   for (;;) {
     uint64_t q;
     uint32_t o;
@@ -1280,6 +1296,74 @@ __global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t
     }
     pos = walk_lf<W, kQ>(ix, T, v, q, o, pos);
     ++steps;
+  }
+}
+
+template <class W, bool kQ>
+__global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t* __restrict__ rows,
+                                                     uint64_t total, uint64_t* __restrict__ out,
+                                                     unsigned long long* __restrict__ err,
+                                                     uint32_t steps_only) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (j >= total) return;
+  const uint64_t row = rows[j];
+  walk_short_one<W, kQ>(ix, T, row & kWalkRowMask, row >> kWalkAdjShift, j, out, err, steps_only);
+}
+
+// Phase 2 over walk lines with text-position marks, fused with the records (no rows
+// buffer, as k_locate_sa for the full SA): a lane takes a pattern's reported rows —
+// a context window's matching rows (subtracting k) or a plain range of at most
+// kLocSmall rows — and walks each; wider ranges are listed for k_walk_fused_wide.
+template <class W, bool kQ>
+__global__ __launch_bounds__(kBlk) void k_walk_fused(DevIndex ix, const uint64_t* __restrict__ sp,
+                                                     const uint64_t* __restrict__ offs, uint64_t npat,
+                                                     uint64_t* __restrict__ out,
+                                                     uint64_t* __restrict__ wide,
+                                                     unsigned long long* __restrict__ nwide,
+                                                     unsigned long long* __restrict__ err,
+                                                     uint32_t steps_only) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= npat) return;
+  const uint64_t a = offs[q], c = offs[q + 1] - a, s = sp[q];
+  if (!c) return;
+  if (s & kLocCtx) {
+    const uint64_t r0 = s & kLocRowMask, adj = (s >> 60) & 7u;
+    uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+    for (uint64_t j = 0; j < c; ++j) {
+      const uint32_t f = (uint32_t)__ffs(rel) - 1u;
+      walk_short_one<W, kQ>(ix, T, r0 + f, adj, a + j, out, err, steps_only);
+      rel &= rel - 1u;
+    }
+  } else if (c <= kLocSmall) {
+    for (uint64_t j = 0; j < c; ++j) walk_short_one<W, kQ>(ix, T, s + j, 0, a + j, out, err, steps_only);
+  } else {
+    wide[atomicAdd(nwide, 1ull)] = q;
+  }
+}
+
+// the listed wide ranges: a block per range, its threads over the rows
+template <class W, bool kQ>
+__global__ __launch_bounds__(kBlk) void k_walk_fused_wide(DevIndex ix, const uint64_t* __restrict__ sp,
+                                                          const uint64_t* __restrict__ offs,
+                                                          uint64_t* __restrict__ out,
+                                                          const uint64_t* __restrict__ wide,
+                                                          const unsigned long long* __restrict__ nwide,
+                                                          unsigned long long* __restrict__ err,
+                                                          uint32_t steps_only) {
+  __shared__ NodeTable T;
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t nw = *nwide;
+  for (uint64_t e = blockIdx.x; e < nw; e += gridDim.x) {
+    const uint64_t q = wide[e], a = offs[q], c = offs[q + 1] - a, s = sp[q];
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x)
+      walk_short_one<W, kQ>(ix, T, s + j, 0, a + j, out, err, steps_only);
   }
 }
 
@@ -1850,6 +1934,14 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
   return launch_count_ex(h, d_pats, d_offs, npat, co, 0, st, fixed_m, false);
 }
 
+// tuning hook CS_FM_COUNT_NOBAR (read per call): 1 = the staged kernels' general
+// search reads the node table through the caches (no block barrier), 0 = a block-wide
+// LDS copy behind a barrier
+uint32_t count_nobar() {
+  const char* e = std::getenv("CS_FM_COUNT_NOBAR");
+  return e && std::atoi(e) == 1 ? 1u : 0u;
+}
+
 // the staged kernel at count width W: table entries (context records) of U patterns per
 // lane in flight together, then their context sectors or rank steps
 template <int W>
@@ -1862,25 +1954,26 @@ void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t
     return u == 1 || u == 4 ? u : 2;
   }();
   const bool lo = h->line_fmt == kFmtLOcc;
+  const uint32_t nobar = count_nobar();
   const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
   if (packed && lo)
     k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
-                                                                nullptr, fixed_m);
+                                                                nullptr, fixed_m, nobar);
   else if (packed)
     k_count_ctx<OccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
-                                                               nullptr, fixed_m);
+                                                               nullptr, fixed_m, nobar);
   else if (lo)
     k_count_ctx<LOccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                 nullptr, fixed_m);
+                                                                 nullptr, fixed_m, nobar);
   else if (W == 8 && U == 1)
     k_count_ctx<OccE, 1, false, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, nobar);
   else if (W == 8 && U == 4)
     k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, nobar);
   else
     k_count_ctx<OccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                nullptr, fixed_m);
+                                                                nullptr, fixed_m, nobar);
 }
 
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
@@ -1940,13 +2033,13 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
     const CountOut co{cnt.p, nullptr, nullptr, 0, 8};
     if (h->line_fmt == kFmtOcc && U == 1)
       k_count_ctx<OccE, 1, true, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0, count_nobar());
     else if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
       k_count_ctx<OccE, 2, true, false, 8><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0, count_nobar());
     else
       k_count_ctx<LOccE, 2, true, false, 8><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0, count_nobar());
     FMX_HIP(hipGetLastError());
   } else {
     FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), ix, d_pats,
@@ -1968,7 +2061,6 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
 // a window row k characters before the end, SA[row] otherwise.  A lane
 // takes a pattern of at most kLocSmall rows (every context window: <= kLocSpanBits);
 // wider plain ranges are listed for k_locate_sa_wide, a block per range.
-constexpr uint64_t kLocSmall = 32;
 __global__ __launch_bounds__(kBlk) void k_locate_sa(const uint32_t* __restrict__ sa, uint64_t n,
                                                     const uint64_t* __restrict__ sp,
                                                     const uint64_t* __restrict__ offs, uint64_t npat,
@@ -2009,6 +2101,13 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa_wide(const uint32_t* __restr
   }
 }
 
+// tuning hook CS_FM_WALK_ROWS=1 (read per call): short walks from an expanded rows
+// buffer (k_expand_rows + k_walk_short) instead of straight from the records
+bool walk_rows_hook() {
+  const char* e = std::getenv("CS_FM_WALK_ROWS");
+  return e && std::atoi(e) == 1;
+}
+
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word,
@@ -2032,11 +2131,6 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
-  StreamBuf rows;
-  FMX_HIP(rows.alloc(total * 8, st));
-  k_expand_rows<<<grid_for(npat, kBlk, 65536), kBlk, 0, st>>>(d_sp, d_out_offs, npat,
-                                                              rows.as<uint64_t>());
-  FMX_HIP(hipGetLastError());
   int dev = 0, ncu = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -2047,12 +2141,42 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   const DevIndex ix = query_dev(h, flags);
   unsigned long long* err =
       err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
-  const uint64_t* r = rows.as<uint64_t>();
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
   static const bool persistent = [] {  // tuning hook: CS_FM_WALK_PERSISTENT=1
     const char* e = std::getenv("CS_FM_WALK_PERSISTENT");
     return e && std::atoi(e) == 1;
   }();
+  if (ix.walk && h->walk_marks == 2 && !persistent && !walk_rows_hook()) {
+    // short walks straight from the records (no rows buffer)
+    StreamBuf wide;
+    FMX_HIP(wide.alloc((total / (kLocSmall + 1) + 1) * 8 + 8, st));
+    unsigned long long* nwide = wide.as<unsigned long long>();
+    FMX_HIP(hipMemsetAsync(nwide, 0, 8, st));
+    uint64_t* wl = wide.as<uint64_t>() + 1;
+    const bool q = h->line_fmt == kFmtQwm;
+    const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
+    if (h->wide && q) {
+      k_walk_fused<WalkLineW, true><<<g, kBlk, 0, st>>>(ix, d_sp, d_out_offs, npat, d_out_pos, wl, nwide, err, steps_only);
+      k_walk_fused_wide<WalkLineW, true><<<1024, kBlk, 0, st>>>(ix, d_sp, d_out_offs, d_out_pos, wl, nwide, err, steps_only);
+    } else if (h->wide) {
+      k_walk_fused<WalkLineW, false><<<g, kBlk, 0, st>>>(ix, d_sp, d_out_offs, npat, d_out_pos, wl, nwide, err, steps_only);
+      k_walk_fused_wide<WalkLineW, false><<<1024, kBlk, 0, st>>>(ix, d_sp, d_out_offs, d_out_pos, wl, nwide, err, steps_only);
+    } else if (q) {
+      k_walk_fused<WalkLine, true><<<g, kBlk, 0, st>>>(ix, d_sp, d_out_offs, npat, d_out_pos, wl, nwide, err, steps_only);
+      k_walk_fused_wide<WalkLine, true><<<1024, kBlk, 0, st>>>(ix, d_sp, d_out_offs, d_out_pos, wl, nwide, err, steps_only);
+    } else {
+      k_walk_fused<WalkLine, false><<<g, kBlk, 0, st>>>(ix, d_sp, d_out_offs, npat, d_out_pos, wl, nwide, err, steps_only);
+      k_walk_fused_wide<WalkLine, false><<<1024, kBlk, 0, st>>>(ix, d_sp, d_out_offs, d_out_pos, wl, nwide, err, steps_only);
+    }
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
+  StreamBuf rows;
+  FMX_HIP(rows.alloc(total * 8, st));
+  k_expand_rows<<<grid_for(npat, kBlk, 65536), kBlk, 0, st>>>(d_sp, d_out_offs, npat,
+                                                              rows.as<uint64_t>());
+  FMX_HIP(hipGetLastError());
+  const uint64_t* r = rows.as<uint64_t>();
   if (ix.walk && h->walk_marks == 2 && !persistent) {
     const bool q = h->line_fmt == kFmtQwm;
     const unsigned g = grid_for(total, kBlk, 0xFFFFFFFFu);

@@ -5,7 +5,7 @@
 // "Other access widths are uncalibrated: calibrate on a known byte count").
 //
 //   hipcc -O3 --offload-arch=gfx950 gather_bench.hip -o gather_bench
-//   ./gather_bench [table_GB=4] [reads_M=256] [contiguous=0]
+//   ./gather_bench [table_GB=4] [reads_M=256] [contiguous=0] [mixed=0]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -74,6 +74,28 @@ __global__ void k_indep8(const uint2* __restrict__ tab, uint64_t ngran, uint64_t
     acc ^= v.x ^ v.y;
   }
   if (acc == 0x12345678u) sink[t & 1023] = acc;
+}
+
+// the count kernel's memory mix: per query a random W-byte read plus a coalesced
+// stream (32 B read: pattern + offset; 8 B written: the count) — does the stream slow
+// the random reads down?
+template <int W>
+__global__ void k_mixed(const uint4* __restrict__ tab, uint64_t ngran, uint64_t reads,
+                        const uint4* __restrict__ stream, uint64_t* __restrict__ out) {
+  const uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t nt = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t r = t; r < reads; r += nt) {
+    const uint4 a = stream[2 * r], b = stream[2 * r + 1];
+    const uint64_t g = mix(r * 0x9E3779B97F4A7C15ull + 17 + (a.x & b.w & 1)) % ngran;
+    const uint4* p = tab + g * (W / 16);
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < W / 16; ++k) {
+      const uint4 v = p[k];
+      x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    out[r] = x;
+  }
 }
 
 // dependent chains: each lane does `depth` reads, next address from the data
@@ -173,6 +195,39 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, a, b));
       std::printf("indep    W=  8 grid=%6d: %8.3f ms  %7.2f Greads/s\n", grid, ms, reads / ms / 1e6);
     }
+  }
+  if (argc > 4 && std::atoi(argv[4]) == 1) {  // the count kernel's mix (k_mixed)
+    uint4* stream;
+    uint64_t* out;
+    CK(hipMalloc(&stream, reads * 32));
+    CK(hipMalloc(&out, reads * 8));
+    CK(hipMemset(stream, 0x5A, reads * 32));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int grid : {8192, 32768, 131072}) {
+      float ms = 0;
+      k_mixed<16><<<grid, 256>>>(tab, bytes / 16, reads / 4, stream, out);
+      CK(hipEventRecord(a));
+      k_mixed<16><<<grid, 256>>>(tab, bytes / 16, reads, stream, out);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      CK(hipEventElapsedTime(&ms, a, b));
+      std::printf("mixed W= 16 + 32 B read + 8 B written per read, grid=%6d: %8.3f ms  %7.2f Greads/s\n",
+                  grid, ms, reads / ms / 1e6);
+      k_indep<16><<<grid, 256>>>(tab, bytes / 16, reads / 4, sink);
+      CK(hipEventRecord(a));
+      k_indep<16><<<grid, 256>>>(tab, bytes / 16, reads, sink);
+      CK(hipEventRecord(b));
+      CK(hipEventSynchronize(b));
+      CK(hipEventElapsedTime(&ms, a, b));
+      std::printf("indep W= 16 (same grid)                             grid=%6d: %8.3f ms  %7.2f Greads/s\n",
+                  grid, ms, reads / ms / 1e6);
+    }
+    CK(hipFree(stream));
+    CK(hipFree(out));
+    CK(hipFree(tab));
+    return 0;
   }
   run<16>(tab, bytes, reads, sink);
   run<32>(tab, bytes, reads, sink);
