@@ -800,14 +800,14 @@ __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable
   }
 }
 
-template <class E, int U, bool kLoc, bool kPacked, int W>
+template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, CountOut co,
                                                     uint64_t limit, uint64_t* __restrict__ rec,
-                                                    uint64_t fixed_m, uint32_t nobar) {
+                                                    uint64_t fixed_m) {
   // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
-  // nobar: the general search reads the node table through the caches instead of a
+  // kNoBar: the general search reads the node table through the caches instead of a
   // block-wide LDS copy, so no wave waits at a block barrier for the block's slowest
   // the stages need only the symbol -> (table digit, occurrence code) map in LDS (512 B
   // instead of the 10.8-KB node table: a shorter block prologue); a block stages the
@@ -989,7 +989,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   bool general = false;
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3;
-  if (nobar) {
+  if constexpr (kNoBar) {
     if (general) general_rest<E, U, kLoc, kPacked, W>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec);
     return;
   }
@@ -1934,12 +1934,15 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
   return launch_count_ex(h, d_pats, d_offs, npat, co, 0, st, fixed_m, false);
 }
 
-// tuning hook CS_FM_COUNT_NOBAR (read per call): 1 = the staged kernels' general
-// search reads the node table through the caches (no block barrier), 0 = a block-wide
-// LDS copy behind a barrier
-uint32_t count_nobar() {
+// tuning hook CS_FM_COUNT_NOBAR (read per call): 1 = the staged kernel's general search
+// reads the node table through the caches (no block barrier), 0 = a block-wide LDS copy
+// behind a barrier.  A template parameter (a runtime flag kept both general searches in
+// one kernel: 100 VGPRs, 4 waves per SIMD instead of 79 / 6), honoured for the
+// headline form (occurrence lines, two patterns per lane, byte-string patterns) and
+// locate's phase 1.
+bool count_nobar() {
   const char* e = std::getenv("CS_FM_COUNT_NOBAR");
-  return e && std::atoi(e) == 1 ? 1u : 0u;
+  return e && std::atoi(e) == 1;
 }
 
 // the staged kernel at count width W: table entries (context records) of U patterns per
@@ -1954,26 +1957,28 @@ void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t
     return u == 1 || u == 4 ? u : 2;
   }();
   const bool lo = h->line_fmt == kFmtLOcc;
-  const uint32_t nobar = count_nobar();
   const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
   if (packed && lo)
     k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
-                                                                nullptr, fixed_m, nobar);
+                                                                nullptr, fixed_m);
   else if (packed)
     k_count_ctx<OccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
-                                                               nullptr, fixed_m, nobar);
+                                                               nullptr, fixed_m);
   else if (lo)
     k_count_ctx<LOccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                 nullptr, fixed_m, nobar);
+                                                                 nullptr, fixed_m);
   else if (W == 8 && U == 1)
     k_count_ctx<OccE, 1, false, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, nobar);
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
   else if (W == 8 && U == 4)
     k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, nobar);
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+  else if (W == 8 && count_nobar())
+    k_count_ctx<OccE, 2, false, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
+                                                                      nullptr, fixed_m);
   else
     k_count_ctx<OccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                nullptr, fixed_m, nobar);
+                                                                nullptr, fixed_m);
 }
 
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
@@ -2031,15 +2036,19 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
       return e && std::atoi(e) == 1 ? 1 : 2;
     }();
     const CountOut co{cnt.p, nullptr, nullptr, 0, 8};
+    const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
     if (h->line_fmt == kFmtOcc && U == 1)
       k_count_ctx<OccE, 1, true, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, d_sp, 0, count_nobar());
+          ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
+    else if (h->line_fmt == kFmtOcc && count_nobar())
+      k_count_ctx<OccE, 2, true, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co,
+                                                                      limit, d_sp, 0);
     else if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
-      k_count_ctx<OccE, 2, true, false, 8><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, d_sp, 0, count_nobar());
+      k_count_ctx<OccE, 2, true, false, 8><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, limit,
+                                                                 d_sp, 0);
     else
-      k_count_ctx<LOccE, 2, true, false, 8><<<grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, d_sp, 0, count_nobar());
+      k_count_ctx<LOccE, 2, true, false, 8><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, limit,
+                                                                  d_sp, 0);
     FMX_HIP(hipGetLastError());
   } else {
     FMX_DISPATCH(h, k_locate_ranges, grid_for(npat + 1, kBlk, 0xFFFFFFFFu), ix, d_pats,

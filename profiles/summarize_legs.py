@@ -29,7 +29,8 @@ LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
               "count_m64": "count", "count_fixed": "count", "wm_count": "count",
               "wm_lf_loop": "count", "locate": "k_locate_sa", "locate_ssa_rows": "k_walk",
-              "wm_locate_ssa": "k_walk", "locate_ssa": "k_walk_short"}
+              "wm_locate_ssa": "k_walk", "locate_ssa": "k_walk_fused", "count_rdna": "count",
+              "locate_rdna": "k_locate_sa"}
 
 
 def rows(pattern):
@@ -43,7 +44,7 @@ def rows(pattern):
 def short(name):
     """Readable kernel name: k_count_ctx (count) / k_count_ctx_loc (locate phase 1) with
     the template's U, packed flag and count width; the others by their base name."""
-    m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)>", name)
+    m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)(?:, (?:true|false))?>", name)
     if m:
         eng, u, loc, packed, w = m.groups()
         if loc == "true":
@@ -52,7 +53,8 @@ def short(name):
     m = re.search(r"k_count<[^,]*?(\w+)(<\w+>)?, (true|false)>", name)
     if m:
         return "k_count_packed" if m.group(3) == "true" else "k_count"
-    for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk",
+    for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk_fused_wide",
+              "k_walk_fused", "k_walk",
               "k_locate_ranges", "k_locate_sa_wide", "k_locate_sa", "k_expand_rows", "k_pack_wire"):
         if k in name:
             return k
