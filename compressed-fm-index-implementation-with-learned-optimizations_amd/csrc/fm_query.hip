@@ -499,7 +499,9 @@ __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTabl
     const uint32_t c = P[k - 1 - t];
     if (T.C[c] == T.C[c + 1]) return kCtxAbsent;
     const uint32_t d = T.occ_code[c];
-    if (d == kNoCode) return kCtxNone;
+    // a rare symbol of the occurrence engine; the quaternary matrix codes every present
+    // symbol densely (with 256 symbols one of them is code 0xFF == kNoCode)
+    if (kEsc && d == kNoCode) return kCtxNone;
     want |= d << (sb * t);
   }
   const uint32_t kb = sb * k;
@@ -997,6 +999,165 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   load_table(T, ix.table);
   __syncthreads();
   general_rest<E, U, kLoc, kPacked, W>(ix, T, pats, st, o0, m, q0, co, limit, rec);
+}
+
+// The batch count over the quaternary wavelet matrix with left contexts (C3: sigma = 256,
+// k = 4 prefix table of 16-B context records, u32 contexts of lctx_q = 4 dense codes):
+// the shape of k_count_ctx for u32 contexts.  (A) the pattern as realigned dword loads,
+// the table index and the context key from a 1-KB LDS map (symbol -> table digit,
+// dense code); (B) the U table entries — a whole 16-B record {sp, width, contexts of
+// rows 0-1} in one load, or the (sp, ep) pair of a plain table; (C) when the record does
+// not hold the range, the u32 context sector(s) of rows [sp, ep) (8 rows per 32 B, at
+// most two sectors); (D) counts.  Anything else — patterns over 32 bytes, symbols
+// outside the table alphabet or without a dense code, wider ranges — takes
+// count_pattern, the general search, behind a block-wide node-table copy.
+// Exact by the same backward-search invariant as the occurrence engine's contexts
+// (count_rest / ctx_match): after the table, the rows r of [sp, ep) whose chain spells
+// P[k-1], ..., P[0] are exactly the rows that survive the reference's remaining k steps
+// (fm_index.cpp:90-96).
+template <int U, int W>
+__global__ __launch_bounds__(kBlk) void k_count_qctx(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                     const uint64_t* __restrict__ offs,
+                                                     uint64_t npat, CountOut co, uint64_t fixed_m) {
+  // bits 0-7 table digit (kNoCode: outside the table alphabet), 8-15 dense code, bit 16 the
+  // symbol occurs (every present symbol has a dense code; with 256 symbols one of them is
+  // 0xFF, so kNoCode cannot mark "no code" here)
+  __shared__ uint32_t cmap[256];
+  __shared__ NodeTable T;
+  if (threadIdx.x < 256) {
+    const NodeTable* g = ix.table;
+    const uint32_t c = threadIdx.x;
+    cmap[c] = g->code[c] | ((uint32_t)g->occ_code[c] << 8) | (g->C[c] != g->C[c + 1] ? 1u << 16 : 0u);
+  }
+  __syncthreads();
+  const uint32_t K = ix.ptab_k, sb = ix.lctx_sb, Q = ix.lctx_q;
+  const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
+  uint64_t o0[U], res[U], sp[U], ep[U];
+  uint32_t m[U], t[U], want[U], k[U], c0[U], c1[U];
+  uint8_t st[U];  // 0 done, 1 table only, 2 table + contexts, 3 general search
+  // (A)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    st[j] = 0;
+    res[j] = 0;
+    o0[j] = 0;
+    m[j] = 0;
+    t[j] = want[j] = k[j] = 0;
+    if (q >= npat) continue;
+    o0[j] = offs ? offs[q] : q * fixed_m;
+    const uint64_t mm = offs ? offs[q + 1] - o0[j] : fixed_m;
+    m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
+    if (mm == 0) {
+      res[j] = ix.n;  // fm_index.cpp:80
+      continue;
+    }
+    if (ix.n == 0) continue;  // :81
+    st[j] = 3;
+    if (mm < K || K == 0 || mm > kFastM) continue;
+    uint32_t u[8];
+    load_pattern32(pats, o0[j], m[j], u);
+    const uint32_t kk = m[j] - K;
+    const bool cq = kk <= Q && sb * kk <= 32;  // the rest fits one context entry
+    bool ok = true, cok = cq;
+    uint32_t tt = 0, ww = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kFastM; ++i) {
+      const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i >= kk && i < m[j]) {  // table part, most significant first
+        const uint32_t d = cmap[b] & 0xFFu;
+        ok &= d != kNoCode;
+        tt = tt * ix.ptab_sigma + d;
+      } else if (cq && i < kk) {  // context part: chain symbol kk-1-i
+        const uint32_t e = cmap[b];
+        cok &= (e >> 16) != 0u;  // an absent symbol: the general search returns 0
+        ww |= ((e >> 8) & 0xFFu) << (sb * (kk - 1 - i));
+      }
+    }
+    if (!ok) continue;
+    st[j] = cok ? 2 : 1;
+    t[j] = tt;
+    want[j] = ww;
+    k[j] = kk;
+  }
+  // (B) the table entries
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    c0[j] = c1[j] = 0;
+    if (st[j] != 1 && st[j] != 2) continue;
+    if (ix.ptab_rec == 3) {
+      const uint4 a = static_cast<const uint4*>(ix.ptab)[t[j]];
+      sp[j] = a.x;
+      ep[j] = (uint64_t)a.x + a.y;
+      c0[j] = a.z;
+      c1[j] = a.w;
+    } else {
+      const uint2 a = static_cast<const uint2*>(ix.ptab)[t[j]];
+      sp[j] = a.x;
+      ep[j] = a.y;
+    }
+  }
+  // (C) the context sector(s), unless the record holds the range's contexts
+  uint4 w[U][4];
+  uint64_t bs[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    bs[j] = 0;
+    if (st[j] != 1 && st[j] != 2) continue;
+    if (sp[j] >= ep[j]) {
+      st[j] = 0;
+      res[j] = 0;
+    } else if (k[j] == 0) {
+      st[j] = 0;
+      res[j] = ep[j] - sp[j];
+    } else if (st[j] == 2 && ix.ptab_rec == 3 && ep[j] - sp[j] <= kRecQCtx) {
+      bs[j] = sp[j];
+      w[j][0] = make_uint4(c0[j], c1[j], 0u, 0u);
+      w[j][1] = w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
+    } else if (st[j] == 2 && ep[j] - (sp[j] & ~7ull) <= 16) {
+      bs[j] = sp[j] & ~7ull;
+      const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint32_t*>(ix.lctx) + bs[j]);
+      w[j][0] = p[0];
+      w[j][1] = p[1];
+      if (ep[j] - bs[j] > 8) {
+        w[j][2] = p[2];
+        w[j][3] = p[3];
+      } else {
+        w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      st[j] = 3;
+    }
+  }
+  // (D)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (st[j] == 2) {
+      const uint32_t kb = sb * k[j];
+      const uint32_t mask = kb >= 32 ? ~0u : ((1u << kb) - 1u);
+      const uint32_t lo = (uint32_t)(sp[j] - bs[j]), hi = (uint32_t)(ep[j] - bs[j]);
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(w[j]);
+      uint32_t match = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) match |= (uint32_t)((dw[i] & mask) == want[j]) << i;
+      const uint32_t in = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+      res[j] = (uint64_t)__popc(match & in);
+      st[j] = 0;
+    }
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    if (q < npat && st[j] != 3) store_count<W>(co, q, res[j]);
+  }
+  bool general = false;
+#pragma unroll
+  for (int j = 0; j < U; ++j) general |= st[j] == 3;
+  if (!__syncthreads_or(general)) return;
+  load_table(T, ix.table);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (st[j] != 3) continue;
+    store_count<W>(co, q0 + (uint64_t)j * kBlk, count_pattern<QWM>(ix, T, pats + o0[j], m[j]));
+  }
 }
 
 // Single-pattern count (FMIndex::count, the p50 path): the pattern travels in the
@@ -1945,6 +2106,13 @@ bool count_nobar() {
   return e && std::atoi(e) == 1;
 }
 
+// test / tuning hook CS_FM_QCTX_STAGED (read per call): 0 = the quaternary matrix counts
+// through k_count (one pattern per lane) instead of the staged k_count_qctx
+bool qctx_staged() {
+  const char* e = std::getenv("CS_FM_QCTX_STAGED");
+  return !(e && std::atoi(e) == 0);
+}
+
 // the staged kernel at count width W: table entries (context records) of U patterns per
 // lane in flight together, then their context sectors or rank steps
 template <int W>
@@ -1986,6 +2154,18 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
                           uint64_t fixed_m, bool packed) {
   if (!npat) return CS_OK;
   const DevIndex ix = query_dev(h, flags);
+  if (h->line_fmt == kFmtQwm && ix.ptab_k && ix.lctx && !ix.wide && !packed && qctx_staged()) {
+    // the staged quaternary-matrix kernel (C3)
+    const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
+    if (co.width == 8)
+      k_count_qctx<2, 8><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
+    else if (co.width == 4)
+      k_count_qctx<2, 4><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
+    else
+      k_count_qctx<2, 1><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.ptab_k) {
     if (co.width == 8) launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
     else if (co.width == 4) launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);

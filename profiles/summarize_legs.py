@@ -50,6 +50,9 @@ def short(name):
         if loc == "true":
             return "k_count_ctx_loc"
         return "k_count_ctx%s_w%s" % ("_packed" if packed == "true" else "", w)
+    m = re.search(r"k_count_qctx<(\d), (\d)>", name)
+    if m:
+        return "k_count_qctx_w%s" % m.group(2)
     m = re.search(r"k_count<[^,]*?(\w+)(<\w+>)?, (true|false)>", name)
     if m:
         return "k_count_packed" if m.group(3) == "true" else "k_count"
@@ -98,7 +101,8 @@ def main():
         # the leg's kernel and its streamed reads
         want = LEG_KERNEL.get(leg, "count")
         if want == "count":
-            cands = [n for n in res["pmc"] if n.startswith("k_count_ctx_") or n == "k_count"]
+            cands = [n for n in res["pmc"] if n.startswith("k_count_ctx_") or n.startswith("k_count_qctx")
+                     or n == "k_count"]
         else:
             cands = [n for n in res["pmc"] if n == want]
         kname = max(cands, key=lambda n: res["kernels"].get(n, {}).get("total_ns", 0)) if cands else None

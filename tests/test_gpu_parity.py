@@ -42,6 +42,7 @@ ENGINE_VARIANTS = {
     "auto_nobar": {"CS_FM_COUNT_NOBAR": "1"},
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
+    "qwm_unstaged": {"CS_FM_ENGINE": "qwm", "CS_FM_QCTX_STAGED": "0"},  # its count one pattern per lane
     "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
     "learned_sb4": {"CS_FM_ENGINE": "learned", "CS_FM_LEARNED_SHIFT": "2"},  # 4-line superblocks
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
@@ -58,7 +59,7 @@ _HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER"
           "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
           "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT", "CS_FM_PTAB_WMAX",
           "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA", "CS_FM_DEVICE_TEXT", "CS_FM_COUNT_U", "CS_FM_LOCATE_U",
-          "CS_FM_WALK_ROWS", "CS_FM_COUNT_NOBAR")
+          "CS_FM_WALK_ROWS", "CS_FM_COUNT_NOBAR", "CS_FM_QCTX_STAGED")
 
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
