@@ -73,7 +73,28 @@ LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
 # repetitive DNA of the same size (cs_synth_text_device kind 2): heavy-tailed ranges
 LEGS_RDNA = ["count_rdna", "locate_rdna"]
-ALL_LEGS = LEGS_MAIN + LEGS_WM + LEGS_WALK + LEGS_RDNA
+# the HBM footprint / throughput trade-off: the same text indexed with the optional
+# structures added one at a time
+LEGS_FOOT = ["footprint"]
+ALL_LEGS = LEGS_MAIN + LEGS_WM + LEGS_WALK + LEGS_RDNA + LEGS_FOOT
+
+# footprint ladder rungs: (name, what the rung adds, build switches)
+_OFF = {"CS_FM_PREFIX_K": "0", "CS_FM_LCTX": "0", "CS_FM_CTX_RECORDS": "0", "CS_FM_FULL_SA": "0",
+        "CS_FM_DEVICE_TEXT": "0", "CS_FM_WALK": "0"}
+FOOT_RUNGS = [
+    ("minimal", "occurrence lines, row-sampled SSA, position samples: the reference's members "
+     "(bwt_ as lines, ssa_)", dict(_OFF)),
+    ("walk_lines", "+ walk lines (locate: LF + mark + sample index in one line)",
+     dict(_OFF, CS_FM_WALK="1")),
+    ("prefix_table", "+ k-mer prefix table (count: the first k steps in one read)",
+     dict(_OFF, CS_FM_WALK="1", CS_FM_PREFIX_K="")),
+    ("left_contexts", "+ left contexts (count: the last <= 7 steps in one read)",
+     dict(_OFF, CS_FM_WALK="1", CS_FM_PREFIX_K="", CS_FM_LCTX="")),
+    ("context_records", "+ context records (count: one read)",
+     dict(_OFF, CS_FM_WALK="1", CS_FM_PREFIX_K="", CS_FM_LCTX="", CS_FM_CTX_RECORDS="")),
+    ("full", "+ full suffix array and the text (the default build: locate one SA read, "
+     "extract a copy)", {}),
+]
 
 
 def log(rank, *a):
@@ -218,12 +239,14 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
         e[0].record(stream)
         tot = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, limit,
                                        d_sp.data_ptr(), d_oo.data_ptr(), sh, flags=flags)
-        e[1].record(stream)
         if d_pos is None:
             d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+        e[1].record(stream)
+        # phase 2 without its own synchronisation (the overrun check follows the event)
         idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh,
-                               flags=flags)
+                               sync=False, flags=flags)
         e[2].record(stream)
+        idx.locate_check(sh)
         torch.cuda.synchronize()
         walls.append(time.perf_counter() - t0)
         t1s.append(e[0].elapsed_time(e[1]) / 1e3)
@@ -247,13 +270,24 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
     sb = info.ssa_bytes // max(info.n // info.ssa_stride, 1) if info.ssa_bytes else 4
     step_bytes = walk_step_bytes(info, idx)
     uses_sa = info.full_sa_bytes and not (flags & 4)
-    # phase 2's algorithmic bytes: the LF steps' lines, one sample (or SA entry) per
-    # position, the record/offsets read and the position written
-    alg = st * step_bytes + tot * ((4 if uses_sa else sb) + 8) + B * 16
-    reads = st * (step_bytes / 32.0) + tot
+    walk_lines = not uses_sa and info.walk_bytes and not (flags & 8)
+    # phase 2's random reads: the full SA one entry per position; walk lines one 32-B
+    # line per visited row (the start row and every LF step: the line holds the row's
+    # mark, symbol and occ) + one sample; the row-sampled walk one LF step's lines per
+    # step (a sampled row is known from its index) + one sample
+    if uses_sa:
+        lines, reads = 0.0, float(tot)
+    elif walk_lines:
+        lines = float(st + tot)
+        reads = lines + tot
+    else:
+        lines = st * (step_bytes / 32.0)
+        reads = lines + tot
+    # algorithmic bytes: those reads, the record/offsets read and the position written
+    alg = lines * 32 + tot * ((4 if uses_sa else sb) + 8) + B * 16
     # streamed reads of the phase-2 kernel (PMC correction, profiles/summarize_legs.py): the
-    # records + offsets (full SA) or the expanded rows (walks)
-    stream_rd = 16 * B if uses_sa else 8 * tot
+    # records + offsets (full SA, fused walk-line walk) or the expanded rows (k_walk)
+    stream_rd = 16 * B if (uses_sa or walk_lines) else 8 * tot
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl,
             "phase1_ms": min(t1s) * 1e3, "phase2_ms": walk_s * 1e3, "limit": limit,
@@ -269,10 +303,14 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
 
 
 def build_index(pkg, text, N, stride, dev_index, env=None):
+    """Build with the engine's environment switches `env` set for the build ("" = unset)."""
     saved = {}
     for k, v in (env or {}).items():
         saved[k] = os.environ.get(k)
-        os.environ[k] = v
+        if v == "":
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     try:
         t0 = time.perf_counter()
         idx = pkg.FMIndex.build_from_device_text(text.data_ptr(), N, pkg.BuildParams(ssa_stride=stride),
@@ -385,7 +423,7 @@ def main():
     torch.cuda.synchronize()
     replicate_s = None
     need_main = not (args.only and (args.only in LEGS_WM or args.only in LEGS_WALK
-                                    or args.only in LEGS_RDNA))
+                                    or args.only in LEGS_RDNA or args.only in LEGS_FOOT))
     idx = None
     if need_main:
         if args.replicate == "broadcast" and world > 1:
@@ -809,7 +847,7 @@ def main():
         del ref, bwt
 
     # ---- N = 1 legs on the reference's own structure: the binary wavelet matrix ----
-    if idx is not None and (legs & (set(LEGS_WM) | set(LEGS_WALK) | set(LEGS_RDNA))):
+    if idx is not None and (legs & (set(LEGS_WM) | set(LEGS_WALK) | set(LEGS_RDNA) | set(LEGS_FOOT))):
         del idx
         idx = None
         torch.cuda.synchronize()
@@ -856,6 +894,48 @@ def main():
         lg["locate_ssa"]["build_s"] = bs
         del wk
         torch.cuda.synchronize()
+
+    if "footprint" in legs:
+        # the throughput each rung of HBM buys: count of the headline batch (kernel time,
+        # HIP events) and locate (both phases, wall) on the same text, one rung at a time
+        ladder = []
+        for rung, what, env in FOOT_RUNGS:
+            fx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, env)
+            fi = fx.info()
+            nbytes = int(sum(fx.export_meta()[1]))
+            o8 = torch.empty(B, dtype=torch.int64, device=dev)
+            wall, kern_s, _ = time_launches(
+                lambda: fx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(), sh),
+                max(3, args.steps // 8), 1, stream)
+            ok = counts is None or bool(np.array_equal(o8.cpu().numpy(), counts))
+            del o8
+            d_sp = torch.empty(B, dtype=torch.int64, device=dev)
+            d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
+            lt = []
+            for it in range(2):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                tot = fx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000,
+                                              d_sp.data_ptr(), d_oo.data_ptr(), sh)
+                d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+                fx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh)
+                torch.cuda.synchronize()
+                lt.append(time.perf_counter() - t1)
+                del d_pos
+            del d_sp, d_oo
+            ladder.append({"rung": rung, "adds": what, "index_bytes": nbytes,
+                           "bytes_per_text_byte": nbytes / N, "build_s": bs,
+                           "engine": engine_name(fi), "prefix_k": fi.prefix_k,
+                           "count_patterns_per_s": B / kern_s, "count_kernel_ms": kern_s * 1e3,
+                           "count_matches_headline": ok,
+                           "locate_patterns_per_s": B / min(lt), "locate_ms": min(lt) * 1e3})
+            log(rank, "footprint %s: %.1f GB, count %.3g/s, locate %.3g/s" % (
+                rung, nbytes / 1e9, B / kern_s, B / min(lt)))
+            del fx
+            torch.cuda.synchronize()
+        lg["footprint"] = {"what": "the same text and batch indexed with the optional structures "
+                                   "added one at a time (HBM footprint vs throughput)",
+                           "rungs": ladder}
 
     if legs & set(LEGS_RDNA) and args.kind == "dna":
         # repetitive DNA: copies of a 2^20-base seed with ~0.75 % substitutions, so a

@@ -108,6 +108,8 @@ SIGNATURES = {
                                              _u64p, _vp]),
     "cs_fm_locate_walk_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
     "cs_fm_locate_walk_device_async": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
+    "cs_fm_locate_walk_device_async_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp,
+                                                    C.c_uint32, _vp]),
     "cs_fm_locate_check": (C.c_int, [_vp, _vp]),
     "cs_fm_level_rank1": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint64, _u64p]),
     "cs_fm_wt_rank": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p]),
@@ -443,10 +445,8 @@ class FMIndex:
     def locate_walk_device(self, d_sp, d_out_offs, npat, total, d_out_pos, stream=0, sync=True,
                            flags=0):
         if flags:
-            if not sync:
-                raise ValueError("flags need the synchronous walk")
-            _check(lib().cs_fm_locate_walk_device_ex(self._h, d_sp, d_out_offs, npat, total,
-                                                     d_out_pos, flags, stream or None))
+            f = lib().cs_fm_locate_walk_device_ex if sync else lib().cs_fm_locate_walk_device_async_ex
+            _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, flags, stream or None))
             return
         f = lib().cs_fm_locate_walk_device if sync else lib().cs_fm_locate_walk_device_async
         _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, stream or None))

@@ -753,6 +753,21 @@ cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d
   return launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream);
 }
 
+cs_status cs_fm_locate_walk_device_async_ex(const cs_fm_index* h, const uint64_t* d_sp,
+                                            const uint64_t* d_out_offs, uint64_t npat,
+                                            uint64_t total, uint64_t* d_out_pos, uint32_t flags,
+                                            void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream,
+                            nullptr, flags);
+}
+
 cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);

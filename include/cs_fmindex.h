@@ -289,6 +289,12 @@ cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_p
 cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
                                       const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                                       uint64_t* d_out_pos, uint32_t flags, void* stream);
+/* Phase 2 under query flags without the final synchronisation (as
+ * cs_fm_locate_walk_device_async; the overrun flag goes to the next cs_fm_locate_check). */
+cs_status cs_fm_locate_walk_device_async_ex(const cs_fm_index* h, const uint64_t* d_sp,
+                                            const uint64_t* d_out_offs, uint64_t npat,
+                                            uint64_t total, uint64_t* d_out_pos, uint32_t flags,
+                                            void* stream);
 /* Measurement twin of phase 2 (bench.py's walk roofline): d_steps[j] = the LF steps the
  * walk of reported row j takes before its sample (0 with the full suffix array). */
 cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,
