@@ -75,15 +75,17 @@ LEGS_WALK = ["locate_ssa"]
 LEGS_RDNA = ["count_rdna", "locate_rdna"]
 # the HBM footprint / throughput trade-off: the same text indexed with the optional
 # structures added one at a time
-LEGS_FOOT = ["footprint"]
+LEGS_FOOT = ["footprint", "budget"]
+# CS_FM_HBM_BUDGET values of the budget leg, as fractions of the default index's footprint
+BUDGET_FRACS = (0.3, 0.6)
 ALL_LEGS = LEGS_MAIN + LEGS_WM + LEGS_WALK + LEGS_RDNA + LEGS_FOOT
 
 # footprint ladder rungs: (name, what the rung adds, build switches)
 _OFF = {"CS_FM_PREFIX_K": "0", "CS_FM_LCTX": "0", "CS_FM_CTX_RECORDS": "0", "CS_FM_FULL_SA": "0",
         "CS_FM_DEVICE_TEXT": "0", "CS_FM_WALK": "0"}
 FOOT_RUNGS = [
-    ("minimal", "occurrence lines, row-sampled SSA, position samples: the reference's members "
-     "(bwt_ as lines, ssa_)", dict(_OFF)),
+    ("minimal", "occurrence lines, row-sampled SSA and inverse-SA samples at the SSA stride: "
+     "the reference's members (bwt_ as lines, ssa_)", dict(_OFF, CS_FM_PSTRIDE="32")),
     ("walk_lines", "+ walk lines (locate: LF + mark + sample index in one line)",
      dict(_OFF, CS_FM_WALK="1")),
     ("prefix_table", "+ k-mer prefix table (count: the first k steps in one read)",
@@ -380,6 +382,8 @@ def main():
                     help="N > 1: keep each rank's counts (no gather to rank 0)")
     ap.add_argument("--prefix-k", type=int, default=None,
                     help="prefix-table depth override (0 = off; default automatic)")
+    ap.add_argument("--hbm-budget", default=None,
+                    help="HBM budget of the headline index (CS_FM_HBM_BUDGET: bytes, K/M/G/T suffix)")
     ap.add_argument("--legs", default="all",
                     help="comma-separated legs of a full N=1 run (%s), 'all' or 'none'"
                          % ",".join(ALL_LEGS))
@@ -389,6 +393,8 @@ def main():
     args = ap.parse_args()
     if args.prefix_k is not None:
         os.environ["CS_FM_PREFIX_K"] = str(args.prefix_k)
+    if args.hbm_budget is not None:
+        os.environ["CS_FM_HBM_BUDGET"] = args.hbm_budget
     legs = (set(ALL_LEGS) if args.legs == "all" else set() if args.legs == "none"
             else set(x for x in args.legs.split(",") if x))
     if args.only:
@@ -936,6 +942,38 @@ def main():
         lg["footprint"] = {"what": "the same text and batch indexed with the optional structures "
                                    "added one at a time (HBM footprint vs throughput)",
                            "rungs": ladder}
+
+    if "budget" in legs:
+        # the same text under an HBM budget (CS_FM_HBM_BUDGET): the engine adds its optional
+        # structures in build order while the index fits
+        full_b = lg.get("footprint", {}).get("rungs", [{}])[-1].get("index_bytes")
+        if not full_b:
+            fx, _ = build_index(pkg, text, N, args.ssa_stride, local_dev)
+            full_b = int(sum(fx.export_meta()[1]))
+            del fx
+        rows = []
+        for fr in BUDGET_FRACS:
+            budget = int(full_b * fr)
+            fx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev,
+                                 {"CS_FM_HBM_BUDGET": str(budget)})
+            fi = fx.info()
+            nbytes = int(sum(fx.export_meta()[1]))
+            o8 = torch.empty(B, dtype=torch.int64, device=dev)
+            wall, kern_s, _ = time_launches(
+                lambda: fx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(), sh),
+                max(3, args.steps // 8), 1, stream)
+            ok = counts is None or bool(np.array_equal(o8.cpu().numpy(), counts))
+            del o8
+            rows.append({"budget_bytes": budget, "index_bytes": nbytes, "build_s": bs,
+                         "prefix_k": fi.prefix_k, "left_contexts": bool(fi.context_bytes),
+                         "record_bytes": fi.record_bytes, "walk_lines": bool(fi.walk_bytes),
+                         "full_sa": bool(fi.full_sa_bytes), "text_in_hbm": bool(fi.text_in_hbm),
+                         "count_patterns_per_s": B / kern_s, "count_matches_headline": ok})
+            log(rank, "budget %.1f GB: %.1f GB, count %.3g/s" % (budget / 1e9, nbytes / 1e9, B / kern_s))
+            del fx
+            torch.cuda.synchronize()
+        lg["budget"] = {"what": "CS_FM_HBM_BUDGET at fractions of the default footprint (%d B)" % full_b,
+                        "rows": rows}
 
     if legs & set(LEGS_RDNA) and args.kind == "dna":
         # repetitive DNA: copies of a 2^20-base seed with ~0.75 % substitutions, so a

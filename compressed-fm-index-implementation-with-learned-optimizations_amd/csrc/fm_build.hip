@@ -246,7 +246,7 @@ cs_status build_sa_device(const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hip
 }
 
 static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm_index* h,
-                              hipStream_t st, PhaseLog& plog);
+                              hipStream_t st, PhaseLog& plog, DevBuf* sa_pending = nullptr);
 
 // Text-position sample stride (inverse-SA samples for extract; walk-line marks and
 // their position samples for locate): an eighth of the SSA stride, half for wide
@@ -312,6 +312,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   h->pstride = position_stride(stride, h->wide);
   h->nisa = (n + h->pstride - 1) / h->pstride;  // text positions 0, pstride, ... < n
   FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
+  DevBuf sa_pending;  // with an HBM budget: the full SA, kept at the end if it still fits
   bool bucketed = n >= (1ull << 32);
   if (const char* e = std::getenv("CS_FM_SA_BUILDER"))
     if (std::string(e) == "bucketed") bucketed = true;
@@ -341,20 +342,24 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     bool keep = h->lf_exact;
     if (const char* e = std::getenv("CS_FM_FULL_SA")) keep = keep && std::atoi(e) != 0;
     size_t free_b = 0, total_b = 0;
-    if (keep && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > total_b / 8 + n * 8) {
+    if (keep && h->hbm_budget) {
+      // an HBM budget: the full SA ranks after the count structures, so it is decided
+      // last (finish_index), replacing the walk lines when it fits
+      std::swap(sa_pending.p, sa.p);
+    } else if (keep && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > total_b / 8 + n * 8) {
       h->d_sa = sa.p;  // the handle owns it from here
       sa.p = nullptr;
     }
   }
   plog.mark("suffix array + bwt + ssa");
 
-  return finish_index(bwt, hist, h, st, plog);
+  return finish_index(bwt, hist, h, st, plog, &sa_pending);
 }
 
 // Everything after the BWT and the samples: rank structure, C[], node table, prefix
 // table, walk lines.  Shared by the text builder and cs_fm_create.
 static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm_index* h,
-                              hipStream_t st, PhaseLog& plog) {
+                              hipStream_t st, PhaseLog& plog, DevBuf* sa_pending) {
   const uint64_t n = h->n;
   NodeTable& T = h->h_table;
   // --- rank structure: occurrence lines (<= 4 frequent symbols) or the wavelet
@@ -506,6 +511,21 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
     if (cs != CS_OK) return cs;
   }
   plog.mark("context records");
+  if (sa_pending && sa_pending->p) {
+    // budget builds: the full suffix array replaces the walk lines and their position
+    // samples when the index still fits its budget with it
+    const uint64_t walk_b = (h->d_walk ? h->nwalk * 32 : 0) + (h->d_wssa ? h->nisa * h->sample_bytes() : 0);
+    if (index_hbm_bytes(h) + n * 4 <= h->hbm_budget + walk_b) {
+      if (h->d_walk) FMX_HIP(hipFree(h->d_walk));
+      if (h->d_wssa) FMX_HIP(hipFree(h->d_wssa));
+      h->d_walk = h->d_wssa = nullptr;
+      h->nwalk = 0;
+      h->walk_marks = 0;
+      h->d_sa = sa_pending->p;  // the handle owns it from here
+      sa_pending->p = nullptr;
+    }
+    sa_pending->release();
+  }
   FMX_HIP(hipMalloc(&h->d_err, 8));
   FMX_HIP(hipMemsetAsync(h->d_err, 0xFF, 8, st));
   FMX_HIP(hipStreamSynchronize(st));

@@ -756,6 +756,11 @@ cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_i
   bool pos_marks = h->lf_exact && h->d_isa && h->nisa == (n + h->pstride - 1) / h->pstride;
   if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
     if (std::string(e) == "row") pos_marks = false;
+  const uint64_t rows = h->wide ? WalkLineW::kRows : WalkLine::kRows;
+  if (!hbm_room(h, (n / rows + 1) * 32 + (pos_marks ? h->nisa * h->sample_bytes() : 0))) {
+    h->walk_marks = 0;  // locate walks over the rank structure instead
+    return CS_OK;
+  }
   h->walk_marks = pos_marks ? 2u : 1u;
   return h->wide ? build_walk_t<WalkLineW>(bwt, n, map, pos_marks, h, st)
                  : build_walk_t<WalkLine>(bwt, n, map, pos_marks, h, st);

@@ -375,6 +375,7 @@ cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params*
   cs_default_build_params(&dp);
   if (!p) p = &dp;
   return build_handle(device, out, [&](cs_fm_index* h, hipStream_t st) {
+    h->hbm_budget = hbm_budget_env();
     cs_status s = build_index_device(d_text, n, p->ssa_stride, h, st);
     if (s == CS_OK && host_text) h->h_text.assign(host_text, host_text + n);
     if (s == CS_OK) s = keep_device_text(h, d_text, true, st);
@@ -431,6 +432,7 @@ cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint
     return CS_ERR_INVALID;
   }
   return build_handle(device, out, [&](cs_fm_index* h, hipStream_t st) {
+    h->hbm_budget = hbm_budget_env();
     cs_status s = build_index_from_bwt(bwt, n, ssa, nsamples, ssa_stride, h, st);
     if (s == CS_OK && text) h->h_text.assign(text, text + n);
     if (s == CS_OK && text) s = keep_device_text(h, text, false, st);

@@ -13,6 +13,9 @@
 
 struct cs_fm_index {
   int device = 0;
+  // HBM budget of the whole index (CS_FM_HBM_BUDGET at build time; 0 = none): the optional
+  // speed structures are added in build order while they fit (fm_io.hip hbm_room)
+  uint64_t hbm_budget = 0;
   uint64_t n = 0;
   uint32_t stride = 32;
   void* d_lines = nullptr;            // 8 levels x nlines rank lines
@@ -202,6 +205,14 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
 cs_status build_left_contexts(cs_fm_index* h, hipStream_t st);
 cs_status build_context_records(cs_fm_index* h, hipStream_t st);
 cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st);
+// HBM held by the index's device arrays so far (the image parts, fm_io.hip)
+uint64_t index_hbm_bytes(const cs_fm_index* h);
+// Whether an optional structure of `bytes` may be allocated: the device keeps an eighth
+// of its HBM free (query buffers), and with a budget the index stays within it — `freed`
+// bytes of the index are released once the structure is built (a replacement).
+bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed = 0);
+// CS_FM_HBM_BUDGET: bytes, with an optional K / M / G / T suffix (powers of 1000); 0 = none
+uint64_t hbm_budget_env();
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,
                     hipStream_t st);
 

@@ -23,6 +23,7 @@
 // parts table, lines, ssa, isa[, ptab][, walk][, wssa][, lctx] as device buffers.
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <sstream>
@@ -211,6 +212,40 @@ cs_status alloc_parts(cs_fm_index* h, const std::vector<Part>& parts) {
 }
 
 }  // namespace
+
+uint64_t index_hbm_bytes(const cs_fm_index* hc) {
+  cs_fm_index* h = const_cast<cs_fm_index*>(hc);  // sizes only
+  uint64_t b = 0;
+  for (const Part& p : index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr))
+    if (*p.dptr) b += p.bytes;
+  return b;
+}
+
+bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed) {
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
+  if (bytes + total_b / 8 > free_b) return false;
+  if (!h->hbm_budget) return true;
+  const uint64_t have = index_hbm_bytes(h);
+  return have + bytes <= h->hbm_budget + freed;
+}
+
+uint64_t hbm_budget_env() {
+  const char* e = std::getenv("CS_FM_HBM_BUDGET");
+  if (!e || !*e) return 0;
+  char* end = nullptr;
+  const double v = std::strtod(e, &end);
+  double mul = 1;
+  switch (end && *end ? *end : ' ') {
+    case 'K': case 'k': mul = 1e3; break;
+    case 'M': case 'm': mul = 1e6; break;
+    case 'G': case 'g': mul = 1e9; break;
+    case 'T': case 't': mul = 1e12; break;
+    default: break;
+  }
+  return v > 0 ? (uint64_t)(v * mul) : 0;
+}
+
 }  // namespace fmx
 
 using namespace fmx;

@@ -1830,7 +1830,13 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   if (cap > (1ull << 32)) cap = 1ull << 32;
   size_t free_b = 0, total_b = 0;
   FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  const uint64_t budget = free_b > total_b / 8 ? (free_b - total_b / 8) / 8 : 0;
+  uint64_t budget = free_b > total_b / 8 ? (free_b - total_b / 8) / 8 : 0;
+  if (h->hbm_budget) {  // the index's HBM budget: the largest table that still fits it
+    const uint64_t have = index_hbm_bytes(h);
+    const uint64_t left = h->hbm_budget > have ? (h->hbm_budget - have) / h->ptab_entry_bytes() : 0;
+    if (left < budget) budget = left;
+    if (cap > budget) cap = budget;
+  }
   if (cap > budget && budget >= 4096) cap = budget;
   uint32_t k = 0;
   uint64_t entries = 1;
@@ -1881,9 +1887,7 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   const uint32_t sb = occ ? 2 : 2 * h->h_table.qlevels;
   const uint32_t q = occ ? kCtxQ : (32 / sb < 16 ? 32 / sb : 16);
   const uint64_t rows = ((h->n + R - 1) & ~(uint64_t)(R - 1)) + R;
-  size_t free_b = 0, total_b = 0;
-  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (rows * eb + total_b / 8 > free_b) return CS_OK;
+  if (!hbm_room(h, rows * eb)) return CS_OK;
   FMX_HIP(hipMalloc(&h->d_lctx, rows * eb));
   h->nlctx = rows;
   h->lctx_q = q;
@@ -1983,9 +1987,8 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
     if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
       if (std::atoi(e) == 0) return CS_OK;
     if (h->n > kRecQCtx * entries) return CS_OK;
-    size_t free_q = 0, total_q = 0;
-    FMX_HIP(hipMemGetInfo(&free_q, &total_q));
-    if (entries * 16 + total_q / 8 > free_q) return CS_OK;
+    // the records replace the 8-B table
+    if (!hbm_room(h, entries * 16, entries * h->ptab_entry_bytes())) return CS_OK;
     void* rq = nullptr;
     FMX_HIP(hipMalloc(&rq, entries * 16));
     k_fill_records_q<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
@@ -2013,9 +2016,8 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   }
   if (!want) return CS_OK;
   const uint64_t bytes = entries * (fmt == 2 ? 16 : 32);
-  size_t free_b = 0, total_b = 0;
-  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (bytes + total_b / 8 > free_b) return CS_OK;
+  // the records replace the 8-B table
+  if (!hbm_room(h, bytes, entries * h->ptab_entry_bytes())) return CS_OK;
   void* rec = nullptr;
   FMX_HIP(hipMalloc(&rec, bytes));
   if (fmt == 2)
@@ -2045,9 +2047,7 @@ cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_devic
   if (!src || !h->n || h->d_dtext) return CS_OK;
   if (const char* e = std::getenv("CS_FM_DEVICE_TEXT"))
     if (std::atoi(e) == 0) return CS_OK;
-  size_t free_b = 0, total_b = 0;
-  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  if (h->n + total_b / 8 > free_b) return CS_OK;
+  if (!hbm_room(h, h->n)) return CS_OK;
   FMX_HIP(hipMalloc(&h->d_dtext, h->n));
   FMX_HIP(hipMemcpyAsync(h->d_dtext, src, h->n,
                          src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));

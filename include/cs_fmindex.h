@@ -96,7 +96,15 @@ void cs_default_build_params(cs_build_params* p);
  * C[], row-sampled SSA, and the rank structure: occurrence lines when at most four
  * symbols hold all but 128 BWT rows, else a quaternary wavelet matrix of occurrence
  * lines; environment CS_FM_ENGINE=wavelet selects the reference's binary 8-level
- * wavelet matrix instead).  `text` is a host pointer. */
+ * wavelet matrix instead).  `text` is a host pointer.
+ * HBM footprint: besides the base structures (rank lines, SSA, inverse-SA samples) the
+ * build adds optional speed structures while an eighth of the device stays free — walk
+ * lines, the k-mer prefix table, left contexts, context records, the full suffix array,
+ * the text.  Environment CS_FM_HBM_BUDGET=<bytes>[K|M|G|T] (powers of 1000) caps the
+ * whole index instead: the structures are added in that order while the index fits (the
+ * prefix table takes the largest k that fits; the full suffix array, when it fits,
+ * replaces the walk lines).  Results never depend on the budget, only throughput does
+ * (bench.py legs "footprint" and "budget"). */
 cs_status cs_fm_build_from_text(const uint8_t* text, uint64_t n, const cs_build_params* p,
                                 int device, cs_fm_index** out);
 /* Same, with the text already in device memory on `device`. */

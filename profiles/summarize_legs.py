@@ -28,9 +28,13 @@ import sys
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
               "count_m64": "count", "count_fixed": "count", "wm_count": "count",
-              "wm_lf_loop": "count", "locate": "k_locate_sa", "locate_ssa_rows": "k_walk",
-              "wm_locate_ssa": "k_walk", "locate_ssa": "k_walk_fused", "count_rdna": "count",
-              "locate_rdna": "k_locate_sa"}
+              "wm_lf_loop": "count", "locate": ("k_locate_sa", "k_locate_sa_wide"),
+              "locate_ssa_rows": "k_walk", "wm_locate_ssa": "k_walk",
+              "locate_ssa": ("k_walk_fused", "k_walk_fused_wide"), "count_rdna": "count",
+              "locate_rdna": ("k_locate_sa", "k_locate_sa_wide")}
+
+# legs whose phase-2 reads are contiguous runs of the suffix array, not random rows
+LEG_STREAMED = {"locate_rdna"}
 
 
 def rows(pattern):
@@ -103,8 +107,9 @@ def main():
         if want == "count":
             cands = [n for n in res["pmc"] if n.startswith("k_count_ctx_") or n.startswith("k_count_qctx")
                      or n == "k_count"]
-        else:
-            cands = [n for n in res["pmc"] if n == want]
+        else:  # the phase-2 kernel that ran longest (a lane per pattern, or a block per wide range)
+            want = (want,) if isinstance(want, str) else want
+            cands = [n for n in res["pmc"] if n in want]
         kname = max(cands, key=lambda n: res["kernels"].get(n, {}).get("total_ns", 0)) if cands else None
         lo = (b.get("legs") or {}).get(leg) or {}
         if leg == "count":
@@ -117,9 +122,13 @@ def main():
         kc = res["pmc"].get(kname, {}) if kname else {}
         if kname and "FETCH_SIZE" in kc and stream_rd is not None:
             req = kc["FETCH_SIZE"] * 1024 / 64
+            # a leg whose kernel streams (thousands of contiguous SA rows per range): every
+            # request is a 128-B streaming read tallied at 64 B (the guide's x2)
+            hbm = (req * 128 if leg in LEG_STREAMED
+                   else stream_rd + max(req - stream_rd / 128, 0) * 32)
             e = {"leg": leg, "kernel": kname, "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
                  "read_requests_per_launch": req, "stream_read_bytes_per_launch": stream_rd,
-                 "hbm_bytes_per_launch": stream_rd + max(req - stream_rd / 128, 0) * 32,
+                 "hbm_bytes_per_launch": hbm,
                  "l2_hit_rate": kc.get("l2_hit_rate"),
                  "kernel_mean_ns_profiled": res["kernels"].get(kname, {}).get("mean_ns"),
                  "tag": tag}

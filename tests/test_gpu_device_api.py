@@ -265,3 +265,40 @@ def test_concurrent_host_batches_share_pages():
     assert not errs, errs
     assert all(np.array_equal(r, want) for r in res["all"])
     assert all(np.array_equal(r, want[lo:]) for r in res["win"])
+
+
+@pytest.mark.parametrize("kind", ["dna", "bytes"])
+def test_hbm_budget(kind, monkeypatch):
+    """CS_FM_HBM_BUDGET: the optional structures are added in build order while the index
+    fits; every budget answers count / locate / extract exactly as the default build, the
+    footprint never exceeds max(budget, the base structures), and an ample budget builds
+    the default index."""
+    pkg = load_pkg()
+    t = (O.gen_dna(21, 2_000_000) if kind == "dna" else O.gen_bytes(21, 1_000_000)).tobytes()
+    m = 20 if kind == "dna" else 6
+    P = O.gen_patterns_text(np.frombuffer(t, np.uint8), m, 20_000, seed=9)
+    P = np.concatenate([P, O.gen_patterns_uniform(b"ACGT" if kind == "dna" else bytes(range(1, 256)),
+                                                  m, 5_000, seed=10)])
+    buf = P.reshape(-1)
+    offs = np.arange(0, (len(P) + 1) * m, m, dtype=np.uint64)
+    ref = pkg.FMIndex.build_from_text(t)
+    want_c = ref.count_batch(buf=buf, offs=offs)
+    want_l = ref.locate_batch(buf=buf[: 2000 * m], offs=offs[:2001], limit=50)
+    full = int(sum(ref.export_meta()[1]))
+    del ref
+    sizes = []
+    for budget in (1, full // 4, full // 2, (3 * full) // 4, full, 10 * full):
+        monkeypatch.setenv("CS_FM_HBM_BUDGET", str(budget))
+        g = pkg.FMIndex.build_from_text(t)
+        nb = int(sum(g.export_meta()[1]))
+        sizes.append(nb)
+        assert g.count_batch(buf=buf, offs=offs).tolist() == want_c.tolist(), budget
+        lo, lp = g.locate_batch(buf=buf[: 2000 * m], offs=offs[:2001], limit=50)
+        assert np.asarray(lo).tolist() == np.asarray(want_l[0]).tolist(), budget
+        assert np.asarray(lp).tolist() == np.asarray(want_l[1]).tolist(), budget
+        assert g.extract(len(t) // 3, 40) == t[len(t) // 3: len(t) // 3 + 40]
+        del g
+    base = sizes[0]  # budget 1 B: the base structures only
+    for budget, nb in zip((1, full // 4, full // 2, (3 * full) // 4, full, 10 * full), sizes):
+        assert nb <= max(budget, base), (budget, nb, sizes)
+    assert max(sizes) == sizes[-1] == full, sizes  # an ample budget builds the default index
