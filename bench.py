@@ -68,7 +68,8 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
-             "count_m64", "count_fixed", "locate", "locate_ssa_rows", "host_batch", "extract"]
+             "count_m64", "count_fixed", "locate", "locate_one", "locate_ssa_rows", "host_batch",
+             "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
 # repetitive DNA of the same size (cs_synth_text_device kind 2): heavy-tailed ranges
@@ -302,6 +303,57 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
                               "traffic": pmc_traffic(wl_key, name),
                               "dependent_reads_per_s": reads / walk_s,
                               "frac_of_random_access_ceiling": reads / walk_s / RANDOM_CEIL}}
+
+
+def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limit=100000):
+    """locate of the batch in one call (cs_fm_locate_device: one launch over full-SA
+    indexes — search, look-back scan of the counts, positions — the two phases otherwise),
+    wall time per call including the read-back of the total; positions checked to spell
+    their patterns."""
+    B, m = W.B, W.m
+    stream = torch.cuda.current_stream()
+    d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    cap = 2 * B
+    d_pos = torch.empty(cap, dtype=torch.int64, device=dev)
+    walls, evs = [], []
+    tot = 0
+    for it in range(reps):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        tot, ok = idx.locate_device(W.pats.data_ptr(), W.offs.data_ptr(), B, limit, d_oo.data_ptr(),
+                                    d_pos.data_ptr(), cap, sh)
+        e1.record(stream)
+        walls.append(time.perf_counter() - t0)
+        torch.cuda.synchronize()
+        evs.append(e0.elapsed_time(e1) / 1e3)
+        if not ok:  # grow the buffer once and time again
+            cap = tot
+            d_pos = torch.empty(cap, dtype=torch.int64, device=dev)
+    tl = min(walls)
+    pos = d_pos[:tot]
+    oo = d_oo.cpu().numpy()
+    owner = torch.from_numpy(np.repeat(np.arange(B), np.diff(oo).astype(np.int64))).to(dev)
+    okv = True
+    for a in range(0, tot, 1 << 24):
+        p, w = pos[a:a + (1 << 24)], owner[a:a + (1 << 24)]
+        win = text[(p.unsqueeze(1) + torch.arange(m, device=dev)).long()]
+        okv &= bool((win == W.pats.view(B, m)[w]).all().item())
+    del owner, d_pos, d_oo
+    # algorithmic bytes of the one launch: the count's (record + contexts + pattern stream)
+    # + one 4-B SA read per position + the offsets and positions written
+    rnd, acc, _ = W.accounting(idx, info, 0, sh, dev)
+    alg = rnd + B * m + (B + 1) * 8 + tot * 4 + (B + 1) * 8 + tot * 8
+    reads = acc + tot
+    return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
+            "patterns_per_s": B / tl, "positions_per_s": tot / tl, "limit": limit,
+            "event_ms": min(evs) * 1e3, "positions_verified": okv,
+            "roofline": {"bound": "hbm", "achieved": alg / tl / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / tl / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_query": alg / B,
+                         "stream_read_bytes_per_launch": B * m + (B + 1) * 8,
+                         "traffic": pmc_traffic(wl_key, name), "random_accesses_per_s": reads / tl,
+                         "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}
 
 
 def build_index(pkg, text, N, stride, dev_index, env=None):
@@ -677,6 +729,11 @@ def main():
             lg["locate"] = locate_leg("locate", "locate (fm_index.cpp:107-157), limit 100000: positions "
                                       "from the full suffix array" if info.full_sa_bytes else
                                       "locate, limit 100000", idx, info, wl, W, text, 0, dev, sh)
+        if "locate_one" in legs:
+            lg["locate_one"] = locate_one_leg(
+                "locate_one", "locate (fm_index.cpp:107-157), limit 100000, in one call "
+                "(cs_fm_locate_device: one launch — search, look-back scan, positions from the "
+                "full suffix array)", idx, info, wl, W, text, dev, sh)
         if "locate_ssa_rows" in legs:
             lg["locate_ssa_rows"] = locate_leg(
                 "locate_ssa_rows", "locate with the reference's SSA walk (fm_index.cpp:125-153): LF over the occurrence "
@@ -1026,9 +1083,10 @@ def main():
                    **({"count": res.get("roofline")} if args.only == "count" else {}),
                    "legs": lg}
         elif lg:
-            # the locate leg stays at the top level as before
-            if "locate" in lg:
-                res["locate"] = lg["locate"]
+            # locate at the top level: the one-call form (cs_fm_locate_device), else the
+            # two phases
+            if "locate_one" in lg or "locate" in lg:
+                res["locate"] = lg.get("locate_one") or lg["locate"]
             res["legs"] = lg
         print(json.dumps(res), flush=True)
     if world > 1:

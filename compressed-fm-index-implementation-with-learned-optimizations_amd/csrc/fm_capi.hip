@@ -808,6 +808,39 @@ cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_p
                               (hipStream_t)stream, flags);
 }
 
+cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (!total || !d_out_offs || (npat && !d_offs) || (cap && !d_out_pos)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  bool done = false;
+  s = launch_locate_onepass(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, st,
+                            &done);
+  if (s != CS_OK) return s;
+  if (!done) {  // the two phases: ranges, then (when the total fits) the positions
+    StreamBuf sp;
+    FMX_HIP(sp.alloc((npat ? npat : 1) * 8, st));
+    s = launch_locate_ranges(h, d_pats, d_offs, npat, limit, sp.as<uint64_t>(), d_out_offs, total, st);
+    if (s != CS_OK) return s;
+    if (*total > cap) {
+      set_error("locate: capacity too small");
+      return CS_ERR_CAPACITY;
+    }
+    return walk_checked(h, sp.as<uint64_t>(), d_out_offs, npat, *total, d_out_pos, st);
+  }
+  if (*total > cap) {
+    set_error("locate: capacity too small");
+    return CS_ERR_CAPACITY;
+  }
+  return CS_OK;
+}
+
 cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
                                       const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                                       uint64_t* d_out_pos, uint32_t flags, void* stream) {
@@ -873,8 +906,49 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
   s = b.load(h, pats, offs, npat, st);
   if (s != CS_OK) return s;
   StreamBuf d_sp, d_oo;
-  FMX_HIP(d_sp.alloc(npat * 8, st));
   FMX_HIP(d_oo.alloc((npat + 1) * 8, st));
+  {
+    // one call (launch_locate_onepass) on the indexes it serves: positions for up to
+    // two per pattern (or cap) in a first pass, the exact total in a second when more
+    uint64_t dcap = npat * 2 > (1u << 20) ? npat * 2 : (1u << 20);
+    if (dcap > cap) dcap = cap;
+    StreamBuf d_pos;
+    FMX_HIP(d_pos.alloc((dcap ? dcap : 1) * 8, st));
+    bool done = false;
+    s = launch_locate_onepass(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
+                              d_oo.as<uint64_t>(), d_pos.as<uint64_t>(), dcap, total, st, &done);
+    if (s != CS_OK) return s;
+    if (done && *total > dcap && *total <= cap) {
+      dcap = *total;
+      FMX_HIP(d_pos.alloc(dcap * 8, st));
+      s = launch_locate_onepass(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
+                                d_oo.as<uint64_t>(), d_pos.as<uint64_t>(), dcap, total, st, &done);
+      if (s != CS_OK) return s;
+    }
+    if (done) {
+      {
+        HostPin po;
+        po.pin(h, out_offs, (npat + 1) * 8, st);
+        FMX_HIP(po.copy(out_offs, d_oo.p, (npat + 1) * 8, false, st));
+      }
+      FMX_HIP(hipStreamSynchronize(st));
+      if (*total > cap) {
+        set_error("locate output capacity too small");
+        return CS_ERR_CAPACITY;
+      }
+      if (!*total) return CS_OK;
+      if (!out_pos) {
+        set_error("null output buffer");
+        return CS_ERR_INVALID;
+      }
+      HostPin pp;
+      pp.pin(h, out_pos, *total * 8, st);
+      FMX_HIP(pp.copy(out_pos, d_pos.p, *total * 8, false, st));
+      FMX_HIP(hipStreamSynchronize(st));
+      return CS_OK;
+    }
+  }
+  FMX_HIP(d_sp.alloc(npat * 8, st));
   s = launch_locate_ranges(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
                            d_sp.as<uint64_t>(), d_oo.as<uint64_t>(), total, st);
   if (s != CS_OK) return s;

@@ -185,6 +185,10 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                hipStream_t st, uint32_t flags = 0);
 // err: device word receiving the smallest overrunning row index (UINT64_MAX = none);
 // null = the handle's shared flag (the asynchronous API, cs_fm_locate_check)
+cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                                uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                                uint64_t* d_out_pos, uint64_t cap, uint64_t* total, hipStream_t st,
+                                bool* done);
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st,

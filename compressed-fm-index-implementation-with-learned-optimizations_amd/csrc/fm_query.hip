@@ -775,13 +775,15 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
-// the patterns of a k_count_ctx lane that need the general search (st == 3)
-template <class E, int U, bool kLoc, bool kPacked, int W>
+// the patterns of a k_count_ctx lane that need the general search (st == 3); kOne: the
+// locate results stay in the lane's registers (kc, kr)
+template <class E, int U, bool kLoc, bool kPacked, int W, bool kOne = false>
 __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable& T,
                                              const uint8_t* __restrict__ pats, const uint8_t* st,
                                              const uint64_t* o0, const uint32_t* m, uint64_t q0,
                                              const CountOut& co, uint64_t limit,
-                                             uint64_t* __restrict__ rec) {
+                                             uint64_t* __restrict__ rec, uint64_t* kc = nullptr,
+                                             uint64_t* kr = nullptr) {
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -790,8 +792,13 @@ __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable
     if constexpr (kLoc) {
       uint64_t r;
       const uint64_t c = locate_search<E>(ix, T, pats + o0[j], m[j], r);
-      cnt_out[q] = c < limit ? c : limit;
-      rec[q] = r;
+      if constexpr (kOne) {
+        kc[j] = c < limit ? c : limit;
+        kr[j] = r;
+      } else {
+        cnt_out[q] = c < limit ? c : limit;
+        rec[q] = r;
+      }
     } else if constexpr (kPacked) {
       const PackedDna P{o0[j]};
       store_count<W>(co, q, count_pattern<E>(ix, T, P, m[j]));
@@ -802,12 +809,175 @@ __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable
   }
 }
 
-template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false>
+// Batch locate in one call (cs_fm_locate_device) over an index that keeps the full suffix
+// array: three launches and one host synchronisation —
+//   (1) k_count_ctx with kOne: the staged search; per pattern min(count, limit) (u32: the
+//       index is narrow) and its record; per block ("tile") the block's total;
+//   (2) k_scan_tiles: the exclusive scan of the tile totals (one block; C4: 24 k tiles);
+//   (3) k_locate_emit: per tile, the block's scan of its counts plus the tile's prefix
+//       give the output offsets, then the positions straight from the records through SA.
+// Against the two phases this drops the scan of a 100-MB count array, 8 of the 16 B
+// written per pattern and the host round trip between the phases.  A single launch with
+// a decoupled look-back across tiles was measured first: every block then waits for the
+// slowest search among its predecessors (3.2 ms against 1.1 ms for the two phases, C4).
+struct OnePass {
+  uint32_t* cnt = nullptr;               // (1) -> (3): min(count, limit) per pattern
+  uint64_t* rec = nullptr;               // (1) -> (3): the pattern's record
+  uint64_t* tiles = nullptr;             // per tile: its total, then its exclusive prefix
+  const uint32_t* sa = nullptr;          // full suffix array
+  uint64_t* out_offs = nullptr;          // npat + 1 exclusive offsets
+  uint64_t* out_pos = nullptr;           // positions, `cap` of them
+  uint64_t cap = 0;
+  uint64_t* wide = nullptr;              // (q, first row) of ranges over kLocSmall rows
+  unsigned long long* nwide = nullptr;
+  uint64_t wide_cap = 0;
+};
+
+// Exclusive scan over the block's U x kBlk values in pattern order (segment j holds the
+// patterns q0 + j kBlk, j < U): mine[j] = the offset of the lane's j-th value inside the
+// block, agg = the block's total.  Every thread of the block.
+template <int U>
+__device__ __forceinline__ void block_scan(const uint64_t* kc, uint64_t* mine, uint64_t& agg) {
+  constexpr int NW = kBlk / 64;
+  __shared__ uint64_t s_wsum[U][NW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t x[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    x[j] = kc[j];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(x[j], d, 64);
+      if (lane >= d) x[j] += y;
+    }
+    if (lane == 63) s_wsum[j][wv] = x[j];
+  }
+  __syncthreads();
+  agg = 0;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    uint64_t before = agg;
+    for (int w2 = 0; w2 < NW; ++w2) {
+      if (w2 < wv) before += s_wsum[j][w2];
+      agg += s_wsum[j][w2];
+    }
+    mine[j] = before + x[j] - kc[j];
+  }
+}
+
+// (1)'s tail: the lane's results and the tile's total
+template <int U>
+__device__ __forceinline__ void locate_split_store(uint64_t npat, uint64_t tile, uint64_t q0,
+                                                   const uint64_t* kc, const uint64_t* kr,
+                                                   const OnePass& op) {
+  uint64_t mine[U], agg;
+  block_scan<U>(kc, mine, agg);
+  if (threadIdx.x == 0) op.tiles[tile] = agg;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    if (q >= npat) continue;
+    op.cnt[q] = (uint32_t)kc[j];
+    op.rec[q] = kr[j];
+  }
+}
+
+// (2): exclusive scan of the tile totals in place, one block; total -> *total_out
+__global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tiles, uint64_t ntiles,
+                                                     uint64_t* __restrict__ total_out) {
+  __shared__ uint64_t s_w[16];
+  __shared__ uint64_t s_carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (uint64_t b = 0; b < ntiles; b += blockDim.x) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t v = i < ntiles ? tiles[i] : 0;
+    uint64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int w2 = 0; w2 < (int)(blockDim.x / 64); ++w2) {
+      if (w2 < wv) pre += s_w[w2];
+      tot += s_w[w2];
+    }
+    const uint64_t carry = s_carry;
+    if (i < ntiles) tiles[i] = carry + pre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry = carry + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *total_out = s_carry;
+}
+
+// (3): offsets and positions of tile blockIdx.x
+template <int U>
+__global__ __launch_bounds__(kBlk) void k_locate_emit(uint64_t n, uint64_t npat, OnePass op) {
+  const uint64_t tile = blockIdx.x;
+  const uint64_t q0 = tile * (uint64_t)(kBlk * U) + threadIdx.x;
+  uint64_t kc[U], kr[U], mine[U], agg;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    kc[j] = q < npat ? op.cnt[q] : 0;
+    kr[j] = q < npat ? op.rec[q] : 0;
+  }
+  block_scan<U>(kc, mine, agg);
+  const uint64_t base = op.tiles[tile];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    if (q >= npat) continue;
+    const uint64_t a = base + mine[j], c = kc[j];
+    op.out_offs[q] = a;
+    if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
+    const uint64_t s = kr[j];
+    if (s & kLocCtx) {  // a context window k characters before the end (k_locate_sa)
+      const uint64_t r0 = s & kLocRowMask, adj = (s >> 60) & 7u;
+      uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+      for (uint64_t i = 0; i < c; ++i) {
+        const uint32_t f = (uint32_t)__ffs(rel) - 1u;
+        const uint64_t p = op.sa[r0 + f];
+        op.out_pos[a + i] = p >= adj ? p - adj : p + n - adj;
+        rel &= rel - 1u;
+      }
+    } else if (c <= kLocSmall) {
+      for (uint64_t i = 0; i < c; ++i) op.out_pos[a + i] = op.sa[s + i];
+    } else {
+      const unsigned long long e = atomicAdd(op.nwide, 1ull);
+      if (e < op.wide_cap) {
+        op.wide[2 * e] = q;
+        op.wide[2 * e + 1] = s;
+      }
+    }
+  }
+}
+
+// the ranges over kLocSmall rows: a block per range
+__global__ __launch_bounds__(kBlk) void k_locate_emit_wide(const uint32_t* __restrict__ sa,
+                                                           const uint64_t* __restrict__ offs,
+                                                           uint64_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ wide,
+                                                           const unsigned long long* __restrict__ nwide,
+                                                           uint64_t wide_cap) {
+  const uint64_t nw = *nwide < wide_cap ? *nwide : wide_cap;
+  for (uint64_t e = blockIdx.x; e < nw; e += gridDim.x) {
+    const uint64_t q = wide[2 * e], s = wide[2 * e + 1], a = offs[q], c = offs[q + 1] - a;
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) out[a + j] = sa[s + j];
+  }
+}
+
+template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false>
 __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, CountOut co,
                                                     uint64_t limit, uint64_t* __restrict__ rec,
-                                                    uint64_t fixed_m) {
+                                                    uint64_t fixed_m, OnePass op = OnePass{}) {
   // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
   // kNoBar: the general search reads the node table through the caches instead of a
   // block-wide LDS copy, so no wave waits at a block barrier for the block's slowest
@@ -817,16 +987,20 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   __shared__ uint16_t cmap[256];
   __shared__ NodeTable T;
   static_assert(kBlk >= 256, "one map entry per thread");
+  static_assert(!kOne || (kLoc && !kNoBar), "the one-call locate is a locate with barriers");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   __syncthreads();
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
   const uint32_t K = ix.ptab_k;
   const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
+  uint64_t kc[U], kr[U];  // kOne: min(count, limit) and the record of each of the lane's patterns
+#pragma unroll
+  for (int j = 0; j < U; ++j) kc[j] = kr[j] = 0;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U];
   uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search
-  if (kLoc && q0 == 0) cnt_out[npat] = 0;  // scan slot for the total
+  if (kLoc && !kOne && q0 == 0) cnt_out[npat] = 0;  // scan slot for the total
   // (A)
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -979,7 +1153,10 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     }
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (q < npat && st[j] != 3) {
-      if (kLoc) {
+      if constexpr (kOne) {
+        kc[j] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
+        kr[j] = rv[j];
+      } else if (kLoc) {
         cnt_out[q] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
         rec[q] = rv[j];
       } else {
@@ -993,6 +1170,15 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
   for (int j = 0; j < U; ++j) general |= st[j] == 3;
   if constexpr (kNoBar) {
     if (general) general_rest<E, U, kLoc, kPacked, W>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec);
+    return;
+  }
+  if constexpr (kOne) {
+    if (__syncthreads_or(general)) {
+      load_table(T, ix.table);
+      __syncthreads();
+      general_rest<E, U, kLoc, kPacked, W, true>(ix, T, pats, st, o0, m, q0, co, limit, rec, kc, kr);
+    }
+    locate_split_store<U>(npat, blockIdx.x, q0, kc, kr, op);
     return;
   }
   if (!__syncthreads_or(general)) return;
@@ -2200,6 +2386,65 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
   if (!npat) return CS_OK;
   FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), query_dev(h, flags), d_pats,
                d_offs, npat, d_out);
+  return CS_OK;
+}
+
+// Batch locate in one call (OnePass above): occurrence lines with a prefix table, left
+// contexts and the full suffix array (C2, C4).  *done = false when the index has another
+// shape (the caller runs the two phases).  Writes d_out_offs (npat + 1) and, when the
+// total fits `cap`, every position; synchronises `st` for *total.  CS_FM_LOCATE_ONEPASS=0
+// (read per call) turns it off.
+cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                                uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                                uint64_t* d_out_pos, uint64_t cap, uint64_t* total, hipStream_t st,
+                                bool* done) {
+  *done = false;
+  if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
+    if (std::atoi(e) == 0) return CS_OK;
+  const DevIndex ix = h->dev();
+  if (h->line_fmt != kFmtOcc || !ix.ptab_k || !ix.lctx || !h->d_sa || !h->lf_exact || h->wide)
+    return CS_OK;
+  *done = true;
+  if (!npat) {
+    FMX_HIP(hipMemsetAsync(d_out_offs, 0, 8, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    *total = 0;
+    return CS_OK;
+  }
+  constexpr int U = 2;
+  const uint64_t tiles = (npat + kBlk * U - 1) / (kBlk * U);
+  if (tiles > 0xFFFFFFFFull) {
+    set_error("batch too large for one launch");
+    return CS_ERR_INVALID;
+  }
+  // a range wider than kLocSmall rows takes over kLocSmall positions of the capacity
+  const uint64_t wide_cap = cap / (kLocSmall + 1) + 1;
+  StreamBuf ws;
+  FMX_HIP(ws.alloc(npat * 12 + tiles * 8 + 8 + wide_cap * 16, st));
+  OnePass op;
+  op.rec = ws.as<uint64_t>();
+  op.tiles = op.rec + npat;
+  op.nwide = reinterpret_cast<unsigned long long*>(op.tiles + tiles);
+  op.wide = reinterpret_cast<uint64_t*>(op.nwide + 1);
+  op.cnt = reinterpret_cast<uint32_t*>(op.wide + 2 * wide_cap);
+  op.sa = static_cast<const uint32_t*>(h->d_sa);
+  op.out_offs = d_out_offs;
+  op.out_pos = d_out_pos;
+  op.cap = d_out_pos ? cap : 0;
+  op.wide_cap = wide_cap;
+  FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
+  const CountOut co{nullptr, nullptr, nullptr, 0, 8};
+  k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
+      ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  FMX_HIP(hipGetLastError());
+  k_scan_tiles<<<1, 1024, 0, st>>>(op.tiles, tiles, d_out_offs + npat);
+  FMX_HIP(hipGetLastError());
+  k_locate_emit<U><<<(unsigned)tiles, kBlk, 0, st>>>(h->n, npat, op);
+  FMX_HIP(hipGetLastError());
+  k_locate_emit_wide<<<1024, kBlk, 0, st>>>(op.sa, d_out_offs, d_out_pos, op.wide, op.nwide, wide_cap);
+  FMX_HIP(hipGetLastError());
+  FMX_HIP(hipMemcpyAsync(total, d_out_offs + npat, 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
 }
 

@@ -303,6 +303,17 @@ cs_status cs_fm_locate_walk_device_async_ex(const cs_fm_index* h, const uint64_t
                                             const uint64_t* d_out_offs, uint64_t npat,
                                             uint64_t total, uint64_t* d_out_pos, uint32_t flags,
                                             void* stream);
+/* locate of a batch in one call — FMIndex::locate (fm_index.cpp:107-157) for every
+ * pattern: d_out_offs (npat + 1 entries) = the exclusive scan of min(count, limit), and
+ * d_out_pos[d_out_offs[q] ..] pattern q's positions in the reference's row order.  On
+ * indexes that keep the full suffix array (occurrence lines with a prefix table and
+ * left contexts: C2, C4) one launch does the search, the scan (a decoupled look-back
+ * across blocks) and the positions; otherwise the two phases above run back to back.
+ * Returns CS_ERR_CAPACITY with *total set and the offsets written when the positions do
+ * not fit `cap` (positions are then incomplete).  Synchronises `stream`. */
+cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream);
 /* Measurement twin of phase 2 (bench.py's walk roofline): d_steps[j] = the LF steps the
  * walk of reported row j takes before its sample (0 with the full suffix array). */
 cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,

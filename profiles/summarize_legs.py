@@ -31,7 +31,8 @@ LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "wm_lf_loop": "count", "locate": ("k_locate_sa", "k_locate_sa_wide"),
               "locate_ssa_rows": "k_walk", "wm_locate_ssa": "k_walk",
               "locate_ssa": ("k_walk_fused", "k_walk_fused_wide"), "count_rdna": "count",
-              "locate_rdna": ("k_locate_sa", "k_locate_sa_wide")}
+              "locate_rdna": ("k_locate_sa", "k_locate_sa_wide"),
+              "locate_one": ("k_count_ctx_onepass",)}
 
 # legs whose phase-2 reads are contiguous runs of the suffix array, not random rows
 LEG_STREAMED = {"locate_rdna"}
@@ -48,9 +49,12 @@ def rows(pattern):
 def short(name):
     """Readable kernel name: k_count_ctx (count) / k_count_ctx_loc (locate phase 1) with
     the template's U, packed flag and count width; the others by their base name."""
-    m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)(?:, (?:true|false))?>", name)
+    m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)"
+                  r"(?:, (true|false))?(?:, (true|false))?>", name)
     if m:
-        eng, u, loc, packed, w = m.groups()
+        eng, u, loc, packed, w, nobar, one = m.groups()
+        if one == "true":
+            return "k_count_ctx_onepass"
         if loc == "true":
             return "k_count_ctx_loc"
         return "k_count_ctx%s_w%s" % ("_packed" if packed == "true" else "", w)

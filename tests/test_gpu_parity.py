@@ -717,6 +717,47 @@ def test_query_flags_locate(built, pkg, name):
             assert pos[oo[q]:oo[q + 1]].tolist() == o.locate(p, limit=lim), (name, f, p)
 
 
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_locate_one_call(built, pkg, name):
+    """cs_fm_locate_device (one launch over full-SA indexes: search, look-back scan,
+    positions; the two phases otherwise): the oracle's positions in row order for every
+    pattern, at limits that cut context windows and wide ranges; with a capacity one short
+    of the total it reports the total and leaves the offsets right."""
+    g, o = built(name)
+    t = TEXTS[name]
+    pats = _substrings_and_mutants(t, (1, 2, 4, 7, 12, 20), 20, len(t) + 5) + [b""]
+    buf, offs = O.pack_patterns(pats)
+    d_buf = torch.from_numpy(buf.copy()).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    npat = len(pats)
+    for lim in (1, 3, 40, 100000):
+        want = []
+        try:
+            want = [o.locate(p, limit=lim) for p in pats]
+        except RuntimeError:
+            want = None  # the reference's overrun (no unique terminator)
+        d_oo = torch.zeros(npat + 1, dtype=torch.int64, device="cuda")
+        tot_w = sum(len(w) for w in want) if want is not None else npat * min(lim, len(t))
+        d_pos = torch.zeros(max(tot_w, 1), dtype=torch.int64, device="cuda")
+        try:
+            tot, ok = g.locate_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim, d_oo.data_ptr(),
+                                      d_pos.data_ptr(), d_pos.numel())
+        except RuntimeError as e:
+            assert want is None and str(e) == "locate: LF walk exceeded text length", (name, lim, e)
+            continue
+        assert want is not None and ok, (name, lim)
+        oo = d_oo.cpu().numpy()
+        assert tot == oo[-1] == tot_w, (name, lim)
+        pos = d_pos[:tot].cpu().numpy()
+        for q, p in enumerate(pats):
+            assert pos[oo[q]:oo[q + 1]].tolist() == want[q], (name, lim, p)
+        if tot:
+            d_oo2 = torch.zeros(npat + 1, dtype=torch.int64, device="cuda")
+            tot2, ok2 = g.locate_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim,
+                                        d_oo2.data_ptr(), d_pos.data_ptr(), tot - 1)
+            assert tot2 == tot and not ok2 and torch.equal(d_oo2, d_oo), (name, lim)
+
+
 @pytest.mark.parametrize("name", ["dna_5k", "bytes_5k", "all_same", "runs", "rare_N_41", "banana"])
 def test_count_widths(built, pkg, name):
     """uint32 counts equal the uint64 ones; uint8 counts saturate at 255 with every
