@@ -882,18 +882,26 @@ __device__ __forceinline__ void locate_split_store(uint64_t npat, uint64_t tile,
   }
 }
 
-// (2): exclusive scan of the tile totals in place, one block; total -> *total_out
+// (2): exclusive scan of the tile totals in place, one block; total -> *total_out.  Each
+// thread scans a contiguous run of tiles in registers (one round of loads, not one per
+// 1024 tiles: 47 -> ~10 us for C4's 24 k tiles), then the block scans the run totals.
 __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tiles, uint64_t ntiles,
                                                      uint64_t* __restrict__ total_out) {
+  constexpr int kRun = 32;  // tiles per thread per round: 32 k tiles per round
   __shared__ uint64_t s_w[16];
   __shared__ uint64_t s_carry;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_carry = 0;
   __syncthreads();
-  for (uint64_t b = 0; b < ntiles; b += blockDim.x) {
-    const uint64_t i = b + threadIdx.x;
-    const uint64_t v = i < ntiles ? tiles[i] : 0;
-    uint64_t x = v;
+  for (uint64_t b = 0; b < ntiles; b += (uint64_t)blockDim.x * kRun) {
+    const uint64_t i0 = b + (uint64_t)threadIdx.x * kRun;
+    uint64_t v[kRun], run = 0;
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      v[r] = i0 + r < ntiles ? tiles[i0 + r] : 0;
+      run += v[r];
+    }
+    uint64_t x = run;  // inclusive scan of the run totals over the wave
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint64_t y = __shfl_up(x, d, 64);
@@ -906,10 +914,14 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tile
       if (w2 < wv) pre += s_w[w2];
       tot += s_w[w2];
     }
-    const uint64_t carry = s_carry;
-    if (i < ntiles) tiles[i] = carry + pre + x - v;
+    uint64_t acc = s_carry + pre + x - run;
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      if (i0 + r < ntiles) tiles[i0 + r] = acc;
+      acc += v[r];
+    }
     __syncthreads();
-    if (threadIdx.x == 0) s_carry = carry + tot;
+    if (threadIdx.x == 0) s_carry += tot;
     __syncthreads();
   }
   if (threadIdx.x == 0) *total_out = s_carry;

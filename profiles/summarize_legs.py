@@ -28,7 +28,9 @@ import sys
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
               "count_m64": "count", "count_fixed": "count", "wm_count": "count",
-              "wm_lf_loop": "count", "locate": ("k_locate_sa", "k_locate_sa_wide"),
+              "wm_lf_loop": "count",
+              "locate": ("k_locate_sa", "k_locate_sa_wide", "k_walk_fused", "k_walk_fused_wide",
+                         "k_walk_lines", "k_walk_short"),
               "locate_ssa_rows": "k_walk", "wm_locate_ssa": "k_walk",
               "locate_ssa": ("k_walk_fused", "k_walk_fused_wide"), "count_rdna": "count",
               "locate_rdna": ("k_locate_sa", "k_locate_sa_wide"),
@@ -64,6 +66,9 @@ def short(name):
     m = re.search(r"k_count<[^,]*?(\w+)(<\w+>)?, (true|false)>", name)
     if m:
         return "k_count_packed" if m.group(3) == "true" else "k_count"
+    for k in ("k_walk_samples", "k_walk_pack", "k_walk_base"):  # index build
+        if k in name:
+            return k
     for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk_fused_wide",
               "k_walk_fused", "k_walk",
               "k_locate_ranges", "k_locate_sa_wide", "k_locate_sa", "k_expand_rows", "k_pack_wire"):

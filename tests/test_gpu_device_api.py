@@ -302,3 +302,33 @@ def test_hbm_budget(kind, monkeypatch):
     for budget, nb in zip((1, full // 4, full // 2, (3 * full) // 4, full, 10 * full), sizes):
         assert nb <= max(budget, base), (budget, nb, sizes)
     assert max(sizes) == sizes[-1] == full, sizes  # an ample budget builds the default index
+
+
+def test_locate_one_call_many_tiles():
+    """The one-call locate's tile scan over more tiles than one round of k_scan_tiles
+    (> 32 k tiles of 512 patterns: 17 M patterns) equals the two-phase locate."""
+    pkg = load_pkg()
+    st = torch.cuda.current_stream().cuda_stream
+    t = O.gen_dna(33, 200_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    npat, m, lim = 17_000_000, 8, 3
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(5)
+    acgt = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    pats = acgt[torch.randint(0, 4, (npat * m,), device=dev, generator=gen)]
+    offs = torch.arange(0, (npat + 1) * m, m, dtype=torch.int64, device=dev)
+    oo1 = torch.empty(npat + 1, dtype=torch.int64, device=dev)
+    pos1 = torch.empty(npat * lim, dtype=torch.int64, device=dev)
+    tot1, ok = g.locate_device(pats.data_ptr(), offs.data_ptr(), npat, lim, oo1.data_ptr(),
+                               pos1.data_ptr(), pos1.numel(), st)
+    assert ok
+    sp = torch.empty(npat, dtype=torch.int64, device=dev)
+    oo2 = torch.empty(npat + 1, dtype=torch.int64, device=dev)
+    tot2 = g.locate_ranges_device(pats.data_ptr(), offs.data_ptr(), npat, lim, sp.data_ptr(),
+                                  oo2.data_ptr(), st)
+    pos2 = torch.empty(max(tot2, 1), dtype=torch.int64, device=dev)
+    g.locate_walk_device(sp.data_ptr(), oo2.data_ptr(), npat, tot2, pos2.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert tot1 == tot2 and tot1 > 0
+    assert torch.equal(oo1, oo2)
+    assert torch.equal(pos1[:tot1], pos2[:tot2])
