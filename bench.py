@@ -515,14 +515,22 @@ def main():
     if need_main and (not args.only or args.only == "count"):
         # ---- the timed region: K steps of the batch count (+ the gather at N > 1) ----
         coll = world > 1 and not args.no_gather
-        wire_len = shard.wire_bytes(pkg, B) if coll else 0
+        wcap = shard.WIRE_CAP
+        if coll:
+            # the wire form's overflow area holds every count >= 255 of the batch (each step
+            # counts the same batch): sized from the first count, the largest shard's need
+            headline()
+            nover = torch.tensor([int((out >= 255).sum().item())], dtype=torch.int64, device=dev)
+            dist.all_reduce(nover, op=dist.ReduceOp.MAX)
+            wcap = max(shard.WIRE_CAP, int(nover.item()))
+        wire_len = shard.wire_bytes(pkg, B, wcap) if coll else 0
         pg = shard.PipelinedGather(wire_len, world, rank, torch.uint8, dev) if coll else None
 
         def step(k):
             headline()
             if coll:  # exact 1-B wire form, gathered behind the next step's count
                 w = pg.buffer(k)
-                shard.pack_counts(pkg, out, w, stream=sh)
+                shard.pack_counts(pkg, out, w, cap=wcap, stream=sh)
                 pg.submit(k)
 
         for k in range(args.warmup):
@@ -542,7 +550,7 @@ def main():
             evs[k][1].record(stream)
             if coll:
                 w = pg.buffer(k)
-                shard.pack_counts(pkg, out, w, stream=sh)
+                shard.pack_counts(pkg, out, w, cap=wcap, stream=sh)
                 pg.submit(k)
         if coll:
             pg.finish()
@@ -625,15 +633,20 @@ def main():
 
     # ---- N > 1: locate of each rank's shard, positions gathered to rank 0 (gather_v) ----
     if world > 1 and need_main and not args.only:
-        d_sp = torch.empty(B, dtype=torch.int64, device=dev)
         d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
+        cap = 2 * B
+        d_pos = torch.empty(cap, dtype=torch.int64, device=dev)
+        tot, fits = idx.locate_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000, d_oo.data_ptr(),
+                                      d_pos.data_ptr(), cap, sh)  # sizes the position buffer
+        if not fits:
+            d_pos = torch.empty(tot, dtype=torch.int64, device=dev)
+            cap = tot
         torch.cuda.synchronize()
         dist.barrier()
         t1 = time.perf_counter()
-        tot = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000,
-                                       d_sp.data_ptr(), d_oo.data_ptr(), sh)
-        d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
-        idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh)
+        tot, fits = idx.locate_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000, d_oo.data_ptr(),
+                                      d_pos.data_ptr(), cap, sh)
+        assert fits
         parts = shard.gather_v(d_pos[:tot], world, rank)
         torch.cuda.synchronize()
         tl = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
@@ -653,8 +666,9 @@ def main():
                              "positions_per_s": int(tt.item()) / tl.item(), "limit": 100000,
                              "positions_verified": bool(okt.item()),
                              "gathered_positions": int(sum(p.numel() for p in parts)),
+                             "method": "cs_fm_locate_device per rank (one call), then gather_v",
                              "collective": "gather_v of every rank's positions to rank 0"}
-        del d_sp, d_oo, d_pos, owner, win, parts
+        del d_oo, d_pos, owner, win, parts
 
     # ---- N = 1 legs on the headline index ----
     lg = {}
