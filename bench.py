@@ -100,6 +100,29 @@ FOOT_RUNGS = [
 ]
 
 
+class LegGuard:
+    """A failing leg (or the CPU baseline / p50 block) is reported in the JSON line's
+    "leg_errors" instead of losing the whole line."""
+
+    def __init__(self, errs, name):
+        self.errs, self.name = errs, name
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, ev, tb):
+        if et is None or issubclass(et, KeyboardInterrupt):
+            return False
+        import traceback
+        traceback.print_exception(et, ev, tb, file=sys.stderr)
+        self.errs[self.name] = "%s: %s" % (et.__name__, ev)
+        try:
+            torch.cuda.synchronize()
+        except Exception:
+            pass
+        return True
+
+
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
@@ -672,431 +695,442 @@ def main():
 
     # ---- N = 1 legs on the headline index ----
     lg = {}
+    leg_errors = {}
     stream_m = B * m + (B + 1) * 8
-    if need_main and legs & set(LEGS_MAIN):
-        steps, warm = max(3, args.steps // 2), 2
-        if "count_u32" in legs:
-            o4 = torch.empty(B, dtype=torch.int32, device=dev)
-            lg["count_u32"], _ = count_leg(
-                "count_u32", "the headline batch with uint32 counts (exact, n < 2^32)", idx, info, wl,
-                W, lambda: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B, o4.data_ptr(),
-                                               width=4, stream=sh),
-                0, stream_m + 4 * B, steps, warm, stream, sh, dev, counts,
-                lambda: o4.cpu().numpy().astype(np.int64))
-            del o4
-        if "count_packed" in legs and args.kind == "dna" and m <= 32:
-            # 2-bit packed patterns (8 B each, no offsets) and uint32 counts
-            lut = torch.full((256,), 0, dtype=torch.int64, device=dev)
-            lut[torch.tensor(list(b"ACGT"), device=dev)] = torch.arange(4, device=dev)
-            codes = lut[W.pats.view(B, m).long()]
-            packed = (codes << (2 * torch.arange(m, device=dev))).sum(dim=1)
-            del codes
-            o4 = torch.empty(B, dtype=torch.int32, device=dev)
-            lg["count_packed"], _ = count_leg(
-                "count_packed", "the headline batch as 2-bit packed DNA (8 B per pattern), uint32 "
-                "counts", idx, info, wl, W,
-                lambda: idx.count_packed_device(packed.data_ptr(), m, B, o4.data_ptr(), width=4,
-                                                stream=sh),
-                0, 8 * B + 4 * B, steps, warm, stream, sh, dev, counts,
-                lambda: o4.cpu().numpy().astype(np.int64), stream_read=8 * B)
-            del o4, packed
-        for name, fl, what in (("count_table_steps", 2, "prefix table, then the reference's backward-"
-                                "search steps (fm_index.cpp:90-96), one occurrence line per rank pair: "
-                                "no left contexts / context records (CS_Q_NO_CONTEXTS)"),
-                               ("count_lf_loop", 3, "the reference's whole backward-search loop "
-                                "(fm_index.cpp:84-98) from C[], every character one rank step over "
-                                "the occurrence lines (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS)")):
-            if name in legs:
-                o8 = torch.empty(B, dtype=torch.int64, device=dev)
-                lg[name], _ = count_leg(
-                    name, what, idx, info, wl, W,
-                    lambda fl=fl, o8=o8: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
-                                                             o8.data_ptr(), flags=fl, stream=sh),
-                    fl, stream_m + 8 * B, max(3, steps // 4), 1, stream, sh, dev, counts,
-                    lambda o8=o8: o8.cpu().numpy())
-                del o8
-        for name, mm in (("count_m32", 32), ("count_m64", 64)):
-            if name in legs:
-                Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
-                o8 = torch.empty(B, dtype=torch.int64, device=dev)
-                r, got = count_leg(
-                    name, "Q_text %d-mers through the headline index: prefix table, %d rank steps, "
-                    "then the left contexts" % (mm, mm - info.prefix_k - info.context_q),
-                    idx, info, wl, Wm,
-                    lambda Wm=Wm, o8=o8: idx.count_batch_device(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
-                                                                o8.data_ptr(), sh),
-                    0, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
-                    lambda o8=o8: o8.cpu().numpy())
-                r["found_frac"] = float((got >= 1).mean())
-                lg[name] = r
-                del Wm, o8
-        if "count_fixed" in legs:
-            # one-length k-mers back to back (cs_fm_count_fixed_device: no offsets array)
-            fo = torch.empty(B, dtype=torch.int64, device=dev)
-            lg["count_fixed"], _ = count_leg(
-                "count_fixed", "the headline batch as one-length k-mers (no offsets array)", idx, info,
-                wl, W, lambda: idx.count_fixed_device(W.pats.data_ptr(), m, B, fo.data_ptr(), sh),
-                0, B * m + 8 * B, steps, warm, stream, sh, dev, counts, lambda: fo.cpu().numpy(),
-                stream_read=B * m)
-            del fo
-        if "locate" in legs:
-            lg["locate"] = locate_leg("locate", "locate (fm_index.cpp:107-157), limit 100000: positions "
-                                      "from the full suffix array" if info.full_sa_bytes else
-                                      "locate, limit 100000", idx, info, wl, W, text, 0, dev, sh)
-        if "locate_one" in legs:
-            lg["locate_one"] = locate_one_leg(
-                "locate_one", "locate (fm_index.cpp:107-157), limit 100000, in one call "
-                "(cs_fm_locate_device: one launch — search, look-back scan, positions from the "
-                "full suffix array)", idx, info, wl, W, text, dev, sh)
-        if "locate_ssa_rows" in legs:
-            lg["locate_ssa_rows"] = locate_leg(
-                "locate_ssa_rows", "locate with the reference's SSA walk (fm_index.cpp:125-153): LF over the occurrence "
-                "lines to a row with row %% %d == 0, SA sample + steps (CS_Q_NO_FULL_SA | "
-                "CS_Q_NO_WALK_LINES)" % args.ssa_stride, idx, info, wl, W, text, 4 | 8, dev, sh, reps=2)
-        if "host_batch" in legs and counts is not None:
-            # the batch handed over in host memory (PCIe in and out inside the call)
-            hbuf = W.pats.cpu().numpy()
-            hoffs = W.offs.cpu().numpy().astype(np.uint64)
-            ht = []
-            for it in range(3):
-                t1 = time.perf_counter()
-                hc = idx.count_batch(buf=hbuf, offs=hoffs)
-                ht.append(time.perf_counter() - t1)
-            lg["host_batch"] = {"patterns": B, "seconds": min(ht), "patterns_per_s": B / min(ht),
-                                "h2d_bytes": int(hbuf.nbytes + hoffs.nbytes),
-                                "matches_device_batch": bool(np.array_equal(hc, counts.astype(np.uint64)))}
-            del hbuf, hoffs, hc
-        if "extract" in legs and args.extract_batch:
-            K_, XL = args.extract_batch, 20
-            g = torch.Generator(device="cpu").manual_seed(7)
-            xpos = torch.randint(0, N - XL, (K_,), generator=g, dtype=torch.int64).to(dev)
-            xlen = torch.full((K_,), XL, dtype=torch.int64, device=dev)
-            xoff = torch.arange(0, (K_ + 1) * XL, XL, dtype=torch.int64, device=dev)
-            xout = torch.empty(K_ * XL, dtype=torch.uint8, device=dev)
-            xt = []
-            for it in range(3):
-                torch.cuda.synchronize()
-                t1 = time.perf_counter()
-                idx.extract_device(xpos.data_ptr(), xlen.data_ptr(), xoff.data_ptr(), K_,
-                                   xout.data_ptr(), sh)
-                torch.cuda.synchronize()
-                xt.append(time.perf_counter() - t1)
-            want = text[(xpos.unsqueeze(1) + torch.arange(XL, device=dev)).long()].reshape(-1)
-            lg["extract"] = {"queries": K_, "len": XL, "seconds": min(xt),
-                             "queries_per_s": K_ / min(xt), "bytes_per_s": K_ * XL / min(xt),
-                             "verified": bool(torch.equal(want, xout)),
-                             "method": ("copy from the text in HBM (text_.substr)" if info.text_in_hbm
-                                        else "LF inversion from inverse-SA samples")}
-            del xpos, xlen, xoff, xout, want
+    with LegGuard(leg_errors, "main legs"):
+        if need_main and legs & set(LEGS_MAIN):
+            steps, warm = max(3, args.steps // 2), 2
+            if "count_u32" in legs:
+                o4 = torch.empty(B, dtype=torch.int32, device=dev)
+                lg["count_u32"], _ = count_leg(
+                    "count_u32", "the headline batch with uint32 counts (exact, n < 2^32)", idx, info, wl,
+                    W, lambda: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B, o4.data_ptr(),
+                                                   width=4, stream=sh),
+                    0, stream_m + 4 * B, steps, warm, stream, sh, dev, counts,
+                    lambda: o4.cpu().numpy().astype(np.int64))
+                del o4
+            if "count_packed" in legs and args.kind == "dna" and m <= 32:
+                # 2-bit packed patterns (8 B each, no offsets) and uint32 counts
+                lut = torch.full((256,), 0, dtype=torch.int64, device=dev)
+                lut[torch.tensor(list(b"ACGT"), device=dev)] = torch.arange(4, device=dev)
+                codes = lut[W.pats.view(B, m).long()]
+                packed = (codes << (2 * torch.arange(m, device=dev))).sum(dim=1)
+                del codes
+                o4 = torch.empty(B, dtype=torch.int32, device=dev)
+                lg["count_packed"], _ = count_leg(
+                    "count_packed", "the headline batch as 2-bit packed DNA (8 B per pattern), uint32 "
+                    "counts", idx, info, wl, W,
+                    lambda: idx.count_packed_device(packed.data_ptr(), m, B, o4.data_ptr(), width=4,
+                                                    stream=sh),
+                    0, 8 * B + 4 * B, steps, warm, stream, sh, dev, counts,
+                    lambda: o4.cpu().numpy().astype(np.int64), stream_read=8 * B)
+                del o4, packed
+            for name, fl, what in (("count_table_steps", 2, "prefix table, then the reference's backward-"
+                                    "search steps (fm_index.cpp:90-96), one occurrence line per rank pair: "
+                                    "no left contexts / context records (CS_Q_NO_CONTEXTS)"),
+                                   ("count_lf_loop", 3, "the reference's whole backward-search loop "
+                                    "(fm_index.cpp:84-98) from C[], every character one rank step over "
+                                    "the occurrence lines (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS)")):
+                if name in legs:
+                    o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                    lg[name], _ = count_leg(
+                        name, what, idx, info, wl, W,
+                        lambda fl=fl, o8=o8: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
+                                                                 o8.data_ptr(), flags=fl, stream=sh),
+                        fl, stream_m + 8 * B, max(3, steps // 4), 1, stream, sh, dev, counts,
+                        lambda o8=o8: o8.cpu().numpy())
+                    del o8
+            for name, mm in (("count_m32", 32), ("count_m64", 64)):
+                if name in legs:
+                    Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
+                    o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                    r, got = count_leg(
+                        name, "Q_text %d-mers through the headline index: prefix table, %d rank steps, "
+                        "then the left contexts" % (mm, mm - info.prefix_k - info.context_q),
+                        idx, info, wl, Wm,
+                        lambda Wm=Wm, o8=o8: idx.count_batch_device(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
+                                                                    o8.data_ptr(), sh),
+                        0, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
+                        lambda o8=o8: o8.cpu().numpy())
+                    r["found_frac"] = float((got >= 1).mean())
+                    lg[name] = r
+                    del Wm, o8
+            if "count_fixed" in legs:
+                # one-length k-mers back to back (cs_fm_count_fixed_device: no offsets array)
+                fo = torch.empty(B, dtype=torch.int64, device=dev)
+                lg["count_fixed"], _ = count_leg(
+                    "count_fixed", "the headline batch as one-length k-mers (no offsets array)", idx, info,
+                    wl, W, lambda: idx.count_fixed_device(W.pats.data_ptr(), m, B, fo.data_ptr(), sh),
+                    0, B * m + 8 * B, steps, warm, stream, sh, dev, counts, lambda: fo.cpu().numpy(),
+                    stream_read=B * m)
+                del fo
+            if "locate" in legs:
+                lg["locate"] = locate_leg("locate", "locate (fm_index.cpp:107-157), limit 100000: positions "
+                                          "from the full suffix array" if info.full_sa_bytes else
+                                          "locate, limit 100000", idx, info, wl, W, text, 0, dev, sh)
+            if "locate_one" in legs:
+                lg["locate_one"] = locate_one_leg(
+                    "locate_one", "locate (fm_index.cpp:107-157), limit 100000, in one call "
+                    "(cs_fm_locate_device: one launch — search, look-back scan, positions from the "
+                    "full suffix array)", idx, info, wl, W, text, dev, sh)
+            if "locate_ssa_rows" in legs:
+                lg["locate_ssa_rows"] = locate_leg(
+                    "locate_ssa_rows", "locate with the reference's SSA walk (fm_index.cpp:125-153): LF over the occurrence "
+                    "lines to a row with row %% %d == 0, SA sample + steps (CS_Q_NO_FULL_SA | "
+                    "CS_Q_NO_WALK_LINES)" % args.ssa_stride, idx, info, wl, W, text, 4 | 8, dev, sh, reps=2)
+            if "host_batch" in legs and counts is not None:
+                # the batch handed over in host memory (PCIe in and out inside the call)
+                hbuf = W.pats.cpu().numpy()
+                hoffs = W.offs.cpu().numpy().astype(np.uint64)
+                ht = []
+                for it in range(3):
+                    t1 = time.perf_counter()
+                    hc = idx.count_batch(buf=hbuf, offs=hoffs)
+                    ht.append(time.perf_counter() - t1)
+                lg["host_batch"] = {"patterns": B, "seconds": min(ht), "patterns_per_s": B / min(ht),
+                                    "h2d_bytes": int(hbuf.nbytes + hoffs.nbytes),
+                                    "matches_device_batch": bool(np.array_equal(hc, counts.astype(np.uint64)))}
+                del hbuf, hoffs, hc
+            if "extract" in legs and args.extract_batch:
+                K_, XL = args.extract_batch, 20
+                g = torch.Generator(device="cpu").manual_seed(7)
+                xpos = torch.randint(0, N - XL, (K_,), generator=g, dtype=torch.int64).to(dev)
+                xlen = torch.full((K_,), XL, dtype=torch.int64, device=dev)
+                xoff = torch.arange(0, (K_ + 1) * XL, XL, dtype=torch.int64, device=dev)
+                xout = torch.empty(K_ * XL, dtype=torch.uint8, device=dev)
+                xt = []
+                for it in range(3):
+                    torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                    idx.extract_device(xpos.data_ptr(), xlen.data_ptr(), xoff.data_ptr(), K_,
+                                       xout.data_ptr(), sh)
+                    torch.cuda.synchronize()
+                    xt.append(time.perf_counter() - t1)
+                want = text[(xpos.unsqueeze(1) + torch.arange(XL, device=dev)).long()].reshape(-1)
+                lg["extract"] = {"queries": K_, "len": XL, "seconds": min(xt),
+                                 "queries_per_s": K_ / min(xt), "bytes_per_s": K_ * XL / min(xt),
+                                 "verified": bool(torch.equal(want, xout)),
+                                 "method": ("copy from the text in HBM (text_.substr)" if info.text_in_hbm
+                                            else "LF inversion from inverse-SA samples")}
+                del xpos, xlen, xoff, xout, want
 
     # ---- p50 single-pattern latency (>= 1000 single-pattern calls
     #      through the C++ facade, end to end, as tools/benchmark.cpp:154-166) ----
-    if rank == 0 and args.p50_calls and counts is not None:
-        import ctypes as C
-        hp = np.ascontiguousarray(W.pats[: args.p50_calls * m].cpu().numpy())
-        nq = hp.size // m
-        blib = C.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libcs_bench.so"))
-        fn = blib.cs_bench_facade_count_latency
-        fn.restype = C.c_int
-        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
-                       C.c_int]
+    with LegGuard(leg_errors, "p50"):
+        if rank == 0 and args.p50_calls and counts is not None:
+            import ctypes as C
+            hp = np.ascontiguousarray(W.pats[: args.p50_calls * m].cpu().numpy())
+            nq = hp.size // m
+            blib = C.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libcs_bench.so"))
+            fn = blib.cs_bench_facade_count_latency
+            fn.restype = C.c_int
+            fn.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
+                           C.c_int]
 
-        def facade_p50(serve):
-            cnt1 = np.zeros(nq, np.uint64)
-            lat = np.zeros(nq, np.float64)
-            if fn(idx._h, hp.ctypes.data, m, nq, cnt1.ctypes.data, lat.ctypes.data, serve) != 0:
-                raise RuntimeError("p50 facade loop failed: " + pkg.lib().cs_fm_last_error().decode())
-            assert np.array_equal(cnt1, counts[:nq].astype(np.uint64))
-            return lat
+            def facade_p50(serve):
+                cnt1 = np.zeros(nq, np.uint64)
+                lat = np.zeros(nq, np.float64)
+                if fn(idx._h, hp.ctypes.data, m, nq, cnt1.ctypes.data, lat.ctypes.data, serve) != 0:
+                    raise RuntimeError("p50 facade loop failed: " + pkg.lib().cs_fm_last_error().decode())
+                assert np.array_equal(cnt1, counts[:nq].astype(np.uint64))
+                return lat
 
-        # serving mode (FMIndex::serve: a resident wave answers from a pinned mailbox)
-        # is the headline p50; the one-launch-per-call path is reported beside it
-        lat = facade_p50(1)
-        lat_launch = facade_p50(0)
-        res["p50_us"] = float(np.median(lat))
-        res["p95_us"] = float(np.percentile(lat, 95))
-        res["p50_method"] = ("cs::FMIndex::count via the C++ facade in serving mode "
-                             "(FMIndex::serve), %d calls, steady_clock" % nq)
-        res["p50_launch_us"] = float(np.median(lat_launch))
-        res["p95_launch_us"] = float(np.percentile(lat_launch, 95))
-        lat_py = []
-        for q in range(min(nq, 1000)):
-            b = hp[q * m:(q + 1) * m].tobytes()
-            t1 = time.perf_counter()
-            idx.count(b)
-            lat_py.append((time.perf_counter() - t1) * 1e6)
-        res["p50_python_us"] = float(np.median(lat_py))
-        res["in_batch_us_per_query"] = res["ms_per_step"] * 1e3 / B
+            # serving mode (FMIndex::serve: a resident wave answers from a pinned mailbox)
+            # is the headline p50; the one-launch-per-call path is reported beside it
+            lat = facade_p50(1)
+            lat_launch = facade_p50(0)
+            res["p50_us"] = float(np.median(lat))
+            res["p95_us"] = float(np.percentile(lat, 95))
+            res["p50_method"] = ("cs::FMIndex::count via the C++ facade in serving mode "
+                                 "(FMIndex::serve), %d calls, steady_clock" % nq)
+            res["p50_launch_us"] = float(np.median(lat_launch))
+            res["p95_launch_us"] = float(np.percentile(lat_launch, 95))
+            lat_py = []
+            for q in range(min(nq, 1000)):
+                b = hp[q * m:(q + 1) * m].tobytes()
+                t1 = time.perf_counter()
+                idx.count(b)
+                lat_py.append((time.perf_counter() - t1) * 1e6)
+            res["p50_python_us"] = float(np.median(lat_py))
+            res["in_batch_us_per_query"] = res["ms_per_step"] * 1e3 / B
 
     # ---- CPU baseline: the reference's count() and locate() on host cores (rank 0, N=1) ----
-    if rank == 0 and world == 1 and not args.no_cpu and counts is not None:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle as O  # CPU baseline / checker only
-        # the process's CPU share: OMP_NUM_THREADS on the GPU box (16 per GPU there; the
-        # machine's count is many times that), else the affinity set
-        threads = (args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-                   or len(os.sched_getaffinity(0)))
-        Q = args.cpu_queries
-        if Q is None:
-            Q = max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16, 2 * threads)
-        t1 = time.perf_counter()
-        d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
-        idx.bwt_device(d_bwt.data_ptr(), sh)
-        bwt = d_bwt.cpu().numpy()
-        del d_bwt
-        ref = O.Index(bwt=bwt, nthreads=threads)
-        prep_s = time.perf_counter() - t1
-        sample = W.pats[: Q * m].cpu().numpy()
-        soffs = np.arange(0, (Q + 1) * m, m, dtype=np.uint64)
-        nt = min(threads, Q)
-        Qp = min(Q, nt)  # the restatement: one pattern per thread
-        t1 = time.perf_counter()
-        cnt, lat = ref.count_batch(buf=sample[: Qp * m], offs=soffs[: Qp + 1], nthreads=nt,
-                                   faithful=True, latencies=True)
-        cpu_s = time.perf_counter() - t1
-        port = {
-            "value": Qp / cpu_s, "unit": "patterns/s", "cores": nt, "kind": "port",
-            "sample": "first %d patterns of the batch, reference-faithful count() "
-                      "(oracle/fm_oracle.c faithful=1), %d host threads" % (Qp, nt),
-            "p50_us": float(np.median(lat) / 1e3), "seconds": cpu_s, "prep_s": prep_s,
-            "matches_gpu": bool(np.array_equal(cnt, counts[:Qp].astype(np.uint64)))}
-        res["cpu_baseline"] = port
-        if O.ref_lib() is not None:
-            # the genuine reference's FMIndex::count / locate (oracle/_ref/libcs_ref.so,
-            # built from the reference's sources) over its own BitVector tables of the
-            # same BWT, plus its bwt_ and ssa_ members for locate
+    with LegGuard(leg_errors, "cpu baseline"):
+        if rank == 0 and world == 1 and not args.no_cpu and counts is not None:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O  # CPU baseline / checker only
+            # the process's CPU share: OMP_NUM_THREADS on the GPU box (16 per GPU there; the
+            # machine's count is many times that), else the affinity set
+            threads = (args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+                       or len(os.sched_getaffinity(0)))
+            Q = args.cpu_queries
+            if Q is None:
+                Q = max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16, 2 * threads)
             t1 = time.perf_counter()
-            gref = O.RefCountIndex(ref)
-            ssa = idx.ssa().astype(np.uint32)
-            gref.attach_locate(bwt, ssa, args.ssa_stride)
-            rprep = time.perf_counter() - t1
+            d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
+            idx.bwt_device(d_bwt.data_ptr(), sh)
+            bwt = d_bwt.cpu().numpy()
+            del d_bwt
+            ref = O.Index(bwt=bwt, nthreads=threads)
+            prep_s = time.perf_counter() - t1
+            sample = W.pats[: Q * m].cpu().numpy()
+            soffs = np.arange(0, (Q + 1) * m, m, dtype=np.uint64)
+            nt = min(threads, Q)
+            Qp = min(Q, nt)  # the restatement: one pattern per thread
             t1 = time.perf_counter()
-            rcnt, rlat = gref.count_batch(sample, soffs, nthreads=nt, latencies=True)
-            ref_s = time.perf_counter() - t1
-            res["cpu_baseline"] = {
-                "value": Q / ref_s, "unit": "patterns/s", "cores": nt, "kind": "reference",
-                "sample": "first %d patterns of the batch (%d per thread), the reference's own "
-                          "FMIndex::count (src/api/fm_index.cpp:79-101, oracle/_ref/libcs_ref.so) "
-                          "over its BitVector tables of the same BWT, %d host threads"
-                          % (Q, Q // nt, nt),
-                "p50_us": float(np.median(rlat) / 1e3), "seconds": ref_s,
-                "prep_s": prep_s + rprep,
-                "matches_gpu": bool(np.array_equal(rcnt, counts[:Q].astype(np.uint64)))}
-            res["cpu_port"] = port
-            # locate: one pattern per thread (a C4 locate is the count's search plus ~31
-            # LF steps, each a wavelet rank with the O(n) scans)
-            Ql = nt
-            t1 = time.perf_counter()
-            nout, lpos, llat = gref.locate_batch(sample[: Ql * m], soffs[: Ql + 1], limit=100000,
-                                                 nthreads=nt)
-            loc_s = time.perf_counter() - t1
-            # the GPU's positions of the same patterns
-            d_sp = torch.empty(Ql, dtype=torch.int64, device=dev)
-            d_oo = torch.empty(Ql + 1, dtype=torch.int64, device=dev)
-            gt = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), Ql, 100000,
-                                          d_sp.data_ptr(), d_oo.data_ptr(), sh)
-            d_pos = torch.empty(max(gt, 1), dtype=torch.int64, device=dev)
-            idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), Ql, gt, d_pos.data_ptr(), sh)
-            goo, gpos = d_oo.cpu().numpy(), d_pos[:gt].cpu().numpy()
-            lok = all(nout[q] == goo[q + 1] - goo[q] and
-                      lpos[q, :min(nout[q], lpos.shape[1])].tolist() ==
-                      gpos[goo[q]:goo[q] + min(nout[q], lpos.shape[1])].tolist() for q in range(Ql))
-            res["cpu_locate"] = {
-                "value": Ql / loc_s, "unit": "patterns/s", "cores": nt, "kind": "reference",
-                "sample": "first %d patterns of the batch (one per thread), the reference's own "
-                          "FMIndex::locate (src/api/fm_index.cpp:107-157), limit 100000, row-sampled "
-                          "SSA stride %d, %d host threads" % (Ql, args.ssa_stride, nt),
-                "p50_us": float(np.median(llat) / 1e3), "seconds": loc_s,
-                "positions": int(max(nout.sum(), 0)), "matches_gpu": bool(lok)}
-            del gref, d_sp, d_oo, d_pos
-        Qf = min(args.cpu_fast_queries, B)
-        if Qf > 0:
-            fs = W.pats[: Qf * m].cpu().numpy()
-            foffs = np.arange(0, (Qf + 1) * m, m, dtype=np.uint64)
-            t1 = time.perf_counter()
-            fcnt = ref.count_batch(buf=fs, offs=foffs, nthreads=threads, faithful=False)
-            fast_s = time.perf_counter() - t1
-            res["cpu_fast"] = {
-                "value": Qf / fast_s, "unit": "patterns/s", "cores": threads, "kind": "port",
-                "sample": "first %d patterns of the batch, oracle count() with precomputed "
-                          "totals (not the reference's cost model), %d host threads" % (Qf, threads),
-                "seconds": fast_s, "matches_gpu": bool(np.array_equal(fcnt, counts[:Qf].astype(np.uint64)))}
-        del ref, bwt
+            cnt, lat = ref.count_batch(buf=sample[: Qp * m], offs=soffs[: Qp + 1], nthreads=nt,
+                                       faithful=True, latencies=True)
+            cpu_s = time.perf_counter() - t1
+            port = {
+                "value": Qp / cpu_s, "unit": "patterns/s", "cores": nt, "kind": "port",
+                "sample": "first %d patterns of the batch, reference-faithful count() "
+                          "(oracle/fm_oracle.c faithful=1), %d host threads" % (Qp, nt),
+                "p50_us": float(np.median(lat) / 1e3), "seconds": cpu_s, "prep_s": prep_s,
+                "matches_gpu": bool(np.array_equal(cnt, counts[:Qp].astype(np.uint64)))}
+            res["cpu_baseline"] = port
+            if O.ref_lib() is not None:
+                # the genuine reference's FMIndex::count / locate (oracle/_ref/libcs_ref.so,
+                # built from the reference's sources) over its own BitVector tables of the
+                # same BWT, plus its bwt_ and ssa_ members for locate
+                t1 = time.perf_counter()
+                gref = O.RefCountIndex(ref)
+                ssa = idx.ssa().astype(np.uint32)
+                gref.attach_locate(bwt, ssa, args.ssa_stride)
+                rprep = time.perf_counter() - t1
+                t1 = time.perf_counter()
+                rcnt, rlat = gref.count_batch(sample, soffs, nthreads=nt, latencies=True)
+                ref_s = time.perf_counter() - t1
+                res["cpu_baseline"] = {
+                    "value": Q / ref_s, "unit": "patterns/s", "cores": nt, "kind": "reference",
+                    "sample": "first %d patterns of the batch (%d per thread), the reference's own "
+                              "FMIndex::count (src/api/fm_index.cpp:79-101, oracle/_ref/libcs_ref.so) "
+                              "over its BitVector tables of the same BWT, %d host threads"
+                              % (Q, Q // nt, nt),
+                    "p50_us": float(np.median(rlat) / 1e3), "seconds": ref_s,
+                    "prep_s": prep_s + rprep,
+                    "matches_gpu": bool(np.array_equal(rcnt, counts[:Q].astype(np.uint64)))}
+                res["cpu_port"] = port
+                # locate: one pattern per thread (a C4 locate is the count's search plus ~31
+                # LF steps, each a wavelet rank with the O(n) scans)
+                Ql = nt
+                t1 = time.perf_counter()
+                nout, lpos, llat = gref.locate_batch(sample[: Ql * m], soffs[: Ql + 1], limit=100000,
+                                                     nthreads=nt)
+                loc_s = time.perf_counter() - t1
+                # the GPU's positions of the same patterns
+                d_sp = torch.empty(Ql, dtype=torch.int64, device=dev)
+                d_oo = torch.empty(Ql + 1, dtype=torch.int64, device=dev)
+                gt = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), Ql, 100000,
+                                              d_sp.data_ptr(), d_oo.data_ptr(), sh)
+                d_pos = torch.empty(max(gt, 1), dtype=torch.int64, device=dev)
+                idx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), Ql, gt, d_pos.data_ptr(), sh)
+                goo, gpos = d_oo.cpu().numpy(), d_pos[:gt].cpu().numpy()
+                lok = all(nout[q] == goo[q + 1] - goo[q] and
+                          lpos[q, :min(nout[q], lpos.shape[1])].tolist() ==
+                          gpos[goo[q]:goo[q] + min(nout[q], lpos.shape[1])].tolist() for q in range(Ql))
+                res["cpu_locate"] = {
+                    "value": Ql / loc_s, "unit": "patterns/s", "cores": nt, "kind": "reference",
+                    "sample": "first %d patterns of the batch (one per thread), the reference's own "
+                              "FMIndex::locate (src/api/fm_index.cpp:107-157), limit 100000, row-sampled "
+                              "SSA stride %d, %d host threads" % (Ql, args.ssa_stride, nt),
+                    "p50_us": float(np.median(llat) / 1e3), "seconds": loc_s,
+                    "positions": int(max(nout.sum(), 0)), "matches_gpu": bool(lok)}
+                del gref, d_sp, d_oo, d_pos
+            Qf = min(args.cpu_fast_queries, B)
+            if Qf > 0:
+                fs = W.pats[: Qf * m].cpu().numpy()
+                foffs = np.arange(0, (Qf + 1) * m, m, dtype=np.uint64)
+                t1 = time.perf_counter()
+                fcnt = ref.count_batch(buf=fs, offs=foffs, nthreads=threads, faithful=False)
+                fast_s = time.perf_counter() - t1
+                res["cpu_fast"] = {
+                    "value": Qf / fast_s, "unit": "patterns/s", "cores": threads, "kind": "port",
+                    "sample": "first %d patterns of the batch, oracle count() with precomputed "
+                              "totals (not the reference's cost model), %d host threads" % (Qf, threads),
+                    "seconds": fast_s, "matches_gpu": bool(np.array_equal(fcnt, counts[:Qf].astype(np.uint64)))}
+            del ref, bwt
 
     # ---- N = 1 legs on the reference's own structure: the binary wavelet matrix ----
     if idx is not None and (legs & (set(LEGS_WM) | set(LEGS_WALK) | set(LEGS_RDNA) | set(LEGS_FOOT))):
         del idx
         idx = None
         torch.cuda.synchronize()
-    if legs & set(LEGS_WM):
-        wm, bs = build_index(pkg, text, N, args.ssa_stride, local_dev,
-                             {"CS_FM_ENGINE": "wavelet", "CS_FM_FULL_SA": "0"})
-        wi = wm.info()
-        wwl = workload_key(args.kind, N, m, B, wi, args.queries)
-        log(rank, "wavelet index built in %.1f s" % bs)
-        for name, fl, what in (("wm_count", 0, "the reference's 8-level binary wavelet matrix "
-                                "(src/core/wavelet.cpp:59-96 over BitVector::rank1, bitvector.cpp:"
-                                "165-230) in 32-B rank lines: prefix table, then one rank-line pair "
-                                "per non-pure level per step"),
-                               ("wm_lf_loop", 1, "the reference's structure and its whole backward-"
-                                "search loop from C[] (fm_index.cpp:84-98): every character an "
-                                "8-level wavelet rank pair (CS_Q_NO_PREFIX)")):
-            if name in legs:
+    with LegGuard(leg_errors, "wavelet legs"):
+        if legs & set(LEGS_WM):
+            wm, bs = build_index(pkg, text, N, args.ssa_stride, local_dev,
+                                 {"CS_FM_ENGINE": "wavelet", "CS_FM_FULL_SA": "0"})
+            wi = wm.info()
+            wwl = workload_key(args.kind, N, m, B, wi, args.queries)
+            log(rank, "wavelet index built in %.1f s" % bs)
+            for name, fl, what in (("wm_count", 0, "the reference's 8-level binary wavelet matrix "
+                                    "(src/core/wavelet.cpp:59-96 over BitVector::rank1, bitvector.cpp:"
+                                    "165-230) in 32-B rank lines: prefix table, then one rank-line pair "
+                                    "per non-pure level per step"),
+                                   ("wm_lf_loop", 1, "the reference's structure and its whole backward-"
+                                    "search loop from C[] (fm_index.cpp:84-98): every character an "
+                                    "8-level wavelet rank pair (CS_Q_NO_PREFIX)")):
+                if name in legs:
+                    o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                    lg[name], _ = count_leg(
+                        name, what, wm, wi, wwl, W,
+                        lambda fl=fl, o8=o8: wm.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
+                                                                o8.data_ptr(), flags=fl, stream=sh),
+                        fl, stream_m + 8 * B, max(3, args.steps // 8), 1, stream, sh, dev, counts,
+                        lambda o8=o8: o8.cpu().numpy())
+                    lg[name]["build_s"] = bs
+                    del o8
+            if "wm_locate_ssa" in legs:
+                lg["wm_locate_ssa"] = locate_leg(
+                    "wm_locate_ssa", "the reference's locate on its own structure: backward search, then the SSA walk "
+                    "(fm_index.cpp:125-153) by LF over the 8-level wavelet matrix to a row with row %% "
+                    "%d == 0" % args.ssa_stride, wm, wi, wwl, W, text, 0, dev, sh, reps=2)
+            del wm
+            torch.cuda.synchronize()
+    with LegGuard(leg_errors, "walk legs"):
+        if legs & set(LEGS_WALK):
+            wk, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, {"CS_FM_FULL_SA": "0"})
+            ki = wk.info()
+            log(rank, "walk-line index built in %.1f s" % bs)
+            kwl = workload_key(args.kind, N, m, B, ki, args.queries) + ":walk"
+            lg["locate_ssa"] = locate_leg(
+                "locate_ssa", "locate without the full suffix array (the C5 layout at C4): SSA stride %d, LF walk over "
+                "walk lines (symbol, occ and sample mark in one 32-B line) to the first row the "
+                "reference samples or a text position marked every %d" % (args.ssa_stride, ki.position_stride),
+                wk, ki, kwl, W, text, 0, dev, sh)
+            lg["locate_ssa"]["build_s"] = bs
+            del wk
+            torch.cuda.synchronize()
+
+    with LegGuard(leg_errors, "footprint"):
+        if "footprint" in legs:
+            # the throughput each rung of HBM buys: count of the headline batch (kernel time,
+            # HIP events) and locate (both phases, wall) on the same text, one rung at a time
+            ladder = []
+            for rung, what, env in FOOT_RUNGS:
+                fx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, env)
+                fi = fx.info()
+                nbytes = int(sum(fx.export_meta()[1]))
                 o8 = torch.empty(B, dtype=torch.int64, device=dev)
-                lg[name], _ = count_leg(
-                    name, what, wm, wi, wwl, W,
-                    lambda fl=fl, o8=o8: wm.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
-                                                            o8.data_ptr(), flags=fl, stream=sh),
-                    fl, stream_m + 8 * B, max(3, args.steps // 8), 1, stream, sh, dev, counts,
-                    lambda o8=o8: o8.cpu().numpy())
-                lg[name]["build_s"] = bs
+                wall, kern_s, _ = time_launches(
+                    lambda: fx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(), sh),
+                    max(3, args.steps // 8), 1, stream)
+                ok = counts is None or bool(np.array_equal(o8.cpu().numpy(), counts))
                 del o8
-        if "wm_locate_ssa" in legs:
-            lg["wm_locate_ssa"] = locate_leg(
-                "wm_locate_ssa", "the reference's locate on its own structure: backward search, then the SSA walk "
-                "(fm_index.cpp:125-153) by LF over the 8-level wavelet matrix to a row with row %% "
-                "%d == 0" % args.ssa_stride, wm, wi, wwl, W, text, 0, dev, sh, reps=2)
-        del wm
-        torch.cuda.synchronize()
-    if legs & set(LEGS_WALK):
-        wk, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, {"CS_FM_FULL_SA": "0"})
-        ki = wk.info()
-        log(rank, "walk-line index built in %.1f s" % bs)
-        kwl = workload_key(args.kind, N, m, B, ki, args.queries) + ":walk"
-        lg["locate_ssa"] = locate_leg(
-            "locate_ssa", "locate without the full suffix array (the C5 layout at C4): SSA stride %d, LF walk over "
-            "walk lines (symbol, occ and sample mark in one 32-B line) to the first row the "
-            "reference samples or a text position marked every %d" % (args.ssa_stride, ki.position_stride),
-            wk, ki, kwl, W, text, 0, dev, sh)
-        lg["locate_ssa"]["build_s"] = bs
-        del wk
-        torch.cuda.synchronize()
-
-    if "footprint" in legs:
-        # the throughput each rung of HBM buys: count of the headline batch (kernel time,
-        # HIP events) and locate (both phases, wall) on the same text, one rung at a time
-        ladder = []
-        for rung, what, env in FOOT_RUNGS:
-            fx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, env)
-            fi = fx.info()
-            nbytes = int(sum(fx.export_meta()[1]))
-            o8 = torch.empty(B, dtype=torch.int64, device=dev)
-            wall, kern_s, _ = time_launches(
-                lambda: fx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(), sh),
-                max(3, args.steps // 8), 1, stream)
-            ok = counts is None or bool(np.array_equal(o8.cpu().numpy(), counts))
-            del o8
-            d_sp = torch.empty(B, dtype=torch.int64, device=dev)
-            d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
-            lt = []
-            for it in range(2):
+                d_sp = torch.empty(B, dtype=torch.int64, device=dev)
+                d_oo = torch.empty(B + 1, dtype=torch.int64, device=dev)
+                lt = []
+                for it in range(2):
+                    torch.cuda.synchronize()
+                    t1 = time.perf_counter()
+                    tot = fx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000,
+                                                  d_sp.data_ptr(), d_oo.data_ptr(), sh)
+                    d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
+                    fx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh)
+                    torch.cuda.synchronize()
+                    lt.append(time.perf_counter() - t1)
+                    del d_pos
+                del d_sp, d_oo
+                ladder.append({"rung": rung, "adds": what, "index_bytes": nbytes,
+                               "bytes_per_text_byte": nbytes / N, "build_s": bs,
+                               "engine": engine_name(fi), "prefix_k": fi.prefix_k,
+                               "count_patterns_per_s": B / kern_s, "count_kernel_ms": kern_s * 1e3,
+                               "count_matches_headline": ok,
+                               "locate_patterns_per_s": B / min(lt), "locate_ms": min(lt) * 1e3})
+                log(rank, "footprint %s: %.1f GB, count %.3g/s, locate %.3g/s" % (
+                    rung, nbytes / 1e9, B / kern_s, B / min(lt)))
+                del fx
                 torch.cuda.synchronize()
-                t1 = time.perf_counter()
-                tot = fx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000,
-                                              d_sp.data_ptr(), d_oo.data_ptr(), sh)
-                d_pos = torch.empty(max(tot, 1), dtype=torch.int64, device=dev)
-                fx.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), B, tot, d_pos.data_ptr(), sh)
+            lg["footprint"] = {"what": "the same text and batch indexed with the optional structures "
+                                       "added one at a time (HBM footprint vs throughput)",
+                               "rungs": ladder}
+
+    with LegGuard(leg_errors, "budget"):
+        if "budget" in legs:
+            # the same text under an HBM budget (CS_FM_HBM_BUDGET): the engine adds its optional
+            # structures in build order while the index fits
+            full_b = lg.get("footprint", {}).get("rungs", [{}])[-1].get("index_bytes")
+            if not full_b:
+                fx, _ = build_index(pkg, text, N, args.ssa_stride, local_dev)
+                full_b = int(sum(fx.export_meta()[1]))
+                del fx
+            rows = []
+            for fr in BUDGET_FRACS:
+                budget = int(full_b * fr)
+                fx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev,
+                                     {"CS_FM_HBM_BUDGET": str(budget)})
+                fi = fx.info()
+                nbytes = int(sum(fx.export_meta()[1]))
+                o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                wall, kern_s, _ = time_launches(
+                    lambda: fx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(), sh),
+                    max(3, args.steps // 8), 1, stream)
+                ok = counts is None or bool(np.array_equal(o8.cpu().numpy(), counts))
+                del o8
+                rows.append({"budget_bytes": budget, "index_bytes": nbytes, "build_s": bs,
+                             "prefix_k": fi.prefix_k, "left_contexts": bool(fi.context_bytes),
+                             "record_bytes": fi.record_bytes, "walk_lines": bool(fi.walk_bytes),
+                             "full_sa": bool(fi.full_sa_bytes), "text_in_hbm": bool(fi.text_in_hbm),
+                             "count_patterns_per_s": B / kern_s, "count_matches_headline": ok})
+                log(rank, "budget %.1f GB: %.1f GB, count %.3g/s" % (budget / 1e9, nbytes / 1e9, B / kern_s))
+                del fx
                 torch.cuda.synchronize()
-                lt.append(time.perf_counter() - t1)
-                del d_pos
-            del d_sp, d_oo
-            ladder.append({"rung": rung, "adds": what, "index_bytes": nbytes,
-                           "bytes_per_text_byte": nbytes / N, "build_s": bs,
-                           "engine": engine_name(fi), "prefix_k": fi.prefix_k,
-                           "count_patterns_per_s": B / kern_s, "count_kernel_ms": kern_s * 1e3,
-                           "count_matches_headline": ok,
-                           "locate_patterns_per_s": B / min(lt), "locate_ms": min(lt) * 1e3})
-            log(rank, "footprint %s: %.1f GB, count %.3g/s, locate %.3g/s" % (
-                rung, nbytes / 1e9, B / kern_s, B / min(lt)))
-            del fx
-            torch.cuda.synchronize()
-        lg["footprint"] = {"what": "the same text and batch indexed with the optional structures "
-                                   "added one at a time (HBM footprint vs throughput)",
-                           "rungs": ladder}
+            lg["budget"] = {"what": "CS_FM_HBM_BUDGET at fractions of the default footprint (%d B)" % full_b,
+                            "rows": rows}
 
-    if "budget" in legs:
-        # the same text under an HBM budget (CS_FM_HBM_BUDGET): the engine adds its optional
-        # structures in build order while the index fits
-        full_b = lg.get("footprint", {}).get("rungs", [{}])[-1].get("index_bytes")
-        if not full_b:
-            fx, _ = build_index(pkg, text, N, args.ssa_stride, local_dev)
-            full_b = int(sum(fx.export_meta()[1]))
-            del fx
-        rows = []
-        for fr in BUDGET_FRACS:
-            budget = int(full_b * fr)
-            fx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev,
-                                 {"CS_FM_HBM_BUDGET": str(budget)})
-            fi = fx.info()
-            nbytes = int(sum(fx.export_meta()[1]))
+    with LegGuard(leg_errors, "repetitive-DNA legs"):
+        if legs & set(LEGS_RDNA) and args.kind == "dna":
+            # repetitive DNA: copies of a 2^20-base seed with ~0.75 % substitutions, so a
+            # text 20-mer occurs in most of the ~3800 copies: ranges thousands of rows wide
+            # step through the rank structure instead of ending in a context record
+            rtext = torch.empty(N + 16, dtype=torch.uint8, device=dev)
+            pkg.synth_text_device("rdna", 42, L, rtext.data_ptr(), sh)
+            torch.cuda.synchronize()
+            rx, bs = build_index(pkg, rtext, N, args.ssa_stride, local_dev)
+            ri = rx.info()
+            rwl = workload_key("rdna", N, m, B, ri, args.queries)
+            log(rank, "repetitive-DNA index built in %.1f s" % bs)
+            RW = Workload(pkg, rtext, N, m, lo, B, args.kind, args.queries, dev, sh)
             o8 = torch.empty(B, dtype=torch.int64, device=dev)
-            wall, kern_s, _ = time_launches(
-                lambda: fx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(), sh),
-                max(3, args.steps // 8), 1, stream)
-            ok = counts is None or bool(np.array_equal(o8.cpu().numpy(), counts))
-            del o8
-            rows.append({"budget_bytes": budget, "index_bytes": nbytes, "build_s": bs,
-                         "prefix_k": fi.prefix_k, "left_contexts": bool(fi.context_bytes),
-                         "record_bytes": fi.record_bytes, "walk_lines": bool(fi.walk_bytes),
-                         "full_sa": bool(fi.full_sa_bytes), "text_in_hbm": bool(fi.text_in_hbm),
-                         "count_patterns_per_s": B / kern_s, "count_matches_headline": ok})
-            log(rank, "budget %.1f GB: %.1f GB, count %.3g/s" % (budget / 1e9, nbytes / 1e9, B / kern_s))
-            del fx
+            if "count_rdna" in legs:
+                r, got = count_leg(
+                    "count_rdna", "Q_text 20-mers of a repetitive DNA text of the same size (copies of a "
+                    "2^20-base seed, ~0.75 %% substitutions; cs_synth_text_device kind 2) through the "
+                    "headline engine", rx, ri, rwl, RW,
+                    lambda: rx.count_batch_device(RW.pats.data_ptr(), RW.offs.data_ptr(), B, o8.data_ptr(), sh),
+                    0, stream_m + 8 * B, max(3, args.steps // 4), 1, stream, sh, dev, None,
+                    lambda: o8.cpu().numpy())
+                # the search paths taken, from the per-query bytes of the measurement twin:
+                # one 16-B context record alone, or more reads (context sectors, rank steps)
+                qb = torch.empty(B, dtype=torch.int64, device=dev)
+                rx.count_bytes_device(RW.pats.data_ptr(), RW.offs.data_ptr(), B, qb.data_ptr(), sh)
+                eb = ri.prefix_bytes // (ri.prefix_sigma ** ri.prefix_k) if ri.prefix_k else 0
+                r.update({"build_s": bs, "found_frac": float((got >= 1).mean()),
+                          "count_mean": float(got.mean()), "count_p50": float(np.median(got)),
+                          "count_p99": float(np.percentile(got, 99)), "count_max": int(got.max()),
+                          "record_only_frac": float((qb == eb).float().mean().item()),
+                          "fallback_frac": float((qb > eb).float().mean().item())})
+                del qb
+                lg["count_rdna"] = r
+            if "locate_rdna" in legs:
+                # 1/125 of the batch: ~3,300 positions per pattern at limit 100000
+                LB = max(1, B // 125)
+                LW = Workload.__new__(Workload)
+                LW.m, LW.B, LW.pats, LW.offs = m, LB, RW.pats[: LB * m], RW.offs[: LB + 1]
+                lg["locate_rdna"] = locate_leg(
+                    "locate_rdna", "locate (limit 100000) of %d repetitive-DNA 20-mers: thousands of "
+                    "positions per pattern from the full suffix array" % LB, rx, ri, rwl, LW, rtext, 0,
+                    dev, sh, reps=2)
+            del rx, RW, o8, rtext
             torch.cuda.synchronize()
-        lg["budget"] = {"what": "CS_FM_HBM_BUDGET at fractions of the default footprint (%d B)" % full_b,
-                        "rows": rows}
-
-    if legs & set(LEGS_RDNA) and args.kind == "dna":
-        # repetitive DNA: copies of a 2^20-base seed with ~0.75 % substitutions, so a
-        # text 20-mer occurs in most of the ~3800 copies: ranges thousands of rows wide
-        # step through the rank structure instead of ending in a context record
-        rtext = torch.empty(N + 16, dtype=torch.uint8, device=dev)
-        pkg.synth_text_device("rdna", 42, L, rtext.data_ptr(), sh)
-        torch.cuda.synchronize()
-        rx, bs = build_index(pkg, rtext, N, args.ssa_stride, local_dev)
-        ri = rx.info()
-        rwl = workload_key("rdna", N, m, B, ri, args.queries)
-        log(rank, "repetitive-DNA index built in %.1f s" % bs)
-        RW = Workload(pkg, rtext, N, m, lo, B, args.kind, args.queries, dev, sh)
-        o8 = torch.empty(B, dtype=torch.int64, device=dev)
-        if "count_rdna" in legs:
-            r, got = count_leg(
-                "count_rdna", "Q_text 20-mers of a repetitive DNA text of the same size (copies of a "
-                "2^20-base seed, ~0.75 %% substitutions; cs_synth_text_device kind 2) through the "
-                "headline engine", rx, ri, rwl, RW,
-                lambda: rx.count_batch_device(RW.pats.data_ptr(), RW.offs.data_ptr(), B, o8.data_ptr(), sh),
-                0, stream_m + 8 * B, max(3, args.steps // 4), 1, stream, sh, dev, None,
-                lambda: o8.cpu().numpy())
-            # the search paths taken, from the per-query bytes of the measurement twin:
-            # one 16-B context record alone, or more reads (context sectors, rank steps)
-            qb = torch.empty(B, dtype=torch.int64, device=dev)
-            rx.count_bytes_device(RW.pats.data_ptr(), RW.offs.data_ptr(), B, qb.data_ptr(), sh)
-            eb = ri.prefix_bytes // (ri.prefix_sigma ** ri.prefix_k) if ri.prefix_k else 0
-            r.update({"build_s": bs, "found_frac": float((got >= 1).mean()),
-                      "count_mean": float(got.mean()), "count_p50": float(np.median(got)),
-                      "count_p99": float(np.percentile(got, 99)), "count_max": int(got.max()),
-                      "record_only_frac": float((qb == eb).float().mean().item()),
-                      "fallback_frac": float((qb > eb).float().mean().item())})
-            del qb
-            lg["count_rdna"] = r
-        if "locate_rdna" in legs:
-            # 1/125 of the batch: ~3,300 positions per pattern at limit 100000
-            LB = max(1, B // 125)
-            LW = Workload.__new__(Workload)
-            LW.m, LW.B, LW.pats, LW.offs = m, LB, RW.pats[: LB * m], RW.offs[: LB + 1]
-            lg["locate_rdna"] = locate_leg(
-                "locate_rdna", "locate (limit 100000) of %d repetitive-DNA 20-mers: thousands of "
-                "positions per pattern from the full suffix array" % LB, rx, ri, rwl, LW, rtext, 0,
-                dev, sh, reps=2)
-        del rx, RW, o8, rtext
-        torch.cuda.synchronize()
 
     if rank == 0:
         if args.only:
             res = {"only": args.only, "workload_key": wl if need_main else None,
                    **({"count": res.get("roofline")} if args.only == "count" else {}),
                    "legs": lg}
-        elif lg:
+        if leg_errors:
+            res["leg_errors"] = leg_errors
+        if lg and not args.only:
             # locate at the top level: the one-call form (cs_fm_locate_device), else the
             # two phases
             if "locate_one" in lg or "locate" in lg:
