@@ -68,8 +68,8 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
-             "count_m64", "count_fixed", "locate", "locate_one", "locate_ssa_rows", "host_batch",
-             "extract"]
+             "count_m64", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
+             "host_batch", "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
 # repetitive DNA of the same size (cs_synth_text_device kind 2): heavy-tailed ranges
@@ -755,6 +755,20 @@ def main():
                     r["found_frac"] = float((got >= 1).mean())
                     lg[name] = r
                     del Wm, o8
+            if "count_unif" in legs and args.queries == "text":
+                # SURVEY §8(d)'s secondary batch Q_unif: uniform random patterns of the text's
+                # alphabet (most 20-mers absent from a 4 GB text)
+                Wu = Workload(pkg, text, N, m, lo, B, args.kind, "unif", dev, sh)
+                o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                r, got = count_leg(
+                    "count_unif", "Q_unif: uniform random %d-mers (SURVEY §8(d) secondary batch)" % m,
+                    idx, info, wl + ":unif", Wu,
+                    lambda Wu=Wu, o8=o8: idx.count_batch_device(Wu.pats.data_ptr(), Wu.offs.data_ptr(), B,
+                                                                o8.data_ptr(), sh),
+                    0, stream_m + 8 * B, steps, warm, stream, sh, dev, None, lambda o8=o8: o8.cpu().numpy())
+                r["found_frac"] = float((got >= 1).mean())
+                lg["count_unif"] = r
+                del Wu, o8
             if "count_fixed" in legs:
                 # one-length k-mers back to back (cs_fm_count_fixed_device: no offsets array)
                 fo = torch.empty(B, dtype=torch.int64, device=dev)

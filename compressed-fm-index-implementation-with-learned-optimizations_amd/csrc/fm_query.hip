@@ -866,19 +866,34 @@ __device__ __forceinline__ void block_scan(const uint64_t* kc, uint64_t* mine, u
 }
 
 // (1)'s tail: the lane's results and the tile's total
+// A pattern reporting exactly one position gets it here, from the record already in the
+// lane (its first row: SA[row] - k for a context window), so its SA read overlaps the
+// other blocks' record reads instead of waiting for k_locate_emit; the record then holds
+// kLocStash | position.  (C4 Q_text: 99.6 % of the patterns.)
+constexpr uint64_t kLocStash = 1ull << 62;  // with bit 63 clear: not a window, not a row
 template <int U>
-__device__ __forceinline__ void locate_split_store(uint64_t npat, uint64_t tile, uint64_t q0,
-                                                   const uint64_t* kc, const uint64_t* kr,
-                                                   const OnePass& op) {
-  uint64_t mine[U], agg;
+__device__ __forceinline__ void locate_split_store(uint64_t n, uint64_t npat, uint64_t tile,
+                                                   uint64_t q0, const uint64_t* kc,
+                                                   const uint64_t* kr, const OnePass& op) {
+  uint64_t mine[U], agg, rs[U];
   block_scan<U>(kc, mine, agg);
   if (threadIdx.x == 0) op.tiles[tile] = agg;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk, s = kr[j];
+    rs[j] = s;
+    if (q >= npat || kc[j] != 1) continue;
+    const uint64_t row = (s & kLocCtx) ? (s & kLocRowMask) : s;
+    const uint64_t adj = (s & kLocCtx) ? (s >> 60) & 7u : 0;
+    const uint64_t p = op.sa[row];
+    rs[j] = kLocStash | (p >= adj ? p - adj : p + n - adj);
+  }
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (q >= npat) continue;
     op.cnt[q] = (uint32_t)kc[j];
-    op.rec[q] = kr[j];
+    op.rec[q] = rs[j];
   }
 }
 
@@ -949,7 +964,9 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(uint64_t n, uint64_t npat,
     op.out_offs[q] = a;
     if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
     const uint64_t s = kr[j];
-    if (s & kLocCtx) {  // a context window k characters before the end (k_locate_sa)
+    if ((s >> 62) == 1) {  // kLocStash: the one position, read by the search kernel
+      op.out_pos[a] = s & 0xFFFFFFFFull;
+    } else if (s & kLocCtx) {  // a context window k characters before the end (k_locate_sa)
       const uint64_t r0 = s & kLocRowMask, adj = (s >> 60) & 7u;
       uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
       for (uint64_t i = 0; i < c; ++i) {
@@ -1190,7 +1207,7 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
       __syncthreads();
       general_rest<E, U, kLoc, kPacked, W, true>(ix, T, pats, st, o0, m, q0, co, limit, rec, kc, kr);
     }
-    locate_split_store<U>(npat, blockIdx.x, q0, kc, kr, op);
+    locate_split_store<U>(ix.n, npat, blockIdx.x, q0, kc, kr, op);
     return;
   }
   if (!__syncthreads_or(general)) return;
