@@ -211,6 +211,30 @@ constexpr uint32_t kRecCtx = 12;
 constexpr uint32_t kRec16Ctx = 9;
 constexpr uint32_t kRec16Q = 5;
 constexpr uint32_t kRec16Wide = 15;
+// Compact records of a wide index (n >= 2^32; C5, k = 16: 7.5 rows per k-mer): 4-character
+// contexts (8 bits, the low bits of the rows' lctx entries) of rows 0-9 — dword 1 bits 4-27
+// rows 0-2, dword 2 rows 3-6, dword 3 bits 0-23 rows 7-9 — and bits 32-37 of sp in dword 3
+// bits 24-29.  Enough for a 20-mer at k = 16.  A k-mer whose range the 8-B wide table
+// escaped (wider than kPtabEsc) has width kRec16Wide and dword 2 = ~0: its search starts
+// from C[].
+constexpr uint32_t kRec16CtxW = 10;
+constexpr uint32_t kRec16QW = 4;
+constexpr uint32_t kRec16NoRange = 0xFFFFFFFFu;
+__device__ __forceinline__ uint64_t rec16_sp(uint32_t x, uint32_t w, uint32_t wide) {
+  return (uint64_t)x | (wide ? (uint64_t)((w >> 24) & 0x3Fu) << 32 : 0ull);
+}
+// the rows' contexts of a wide compact record, as u16 entries in dw[0..4]
+__device__ __forceinline__ void rec16w_contexts(uint32_t y, uint32_t z, uint32_t w, uint32_t dw[5]) {
+  uint32_t e[10];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) e[i] = (y >> (4 + 8 * i)) & 0xFFu;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[3 + i] = (z >> (8 * i)) & 0xFFu;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) e[7 + i] = (w >> (8 * i)) & 0xFFu;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dw[i] = e[2 * i] | (e[2 * i + 1] << 16);
+}
 // the rows' contexts of a compact record, as u16 entries in dw[0..4] (dw[4] bits 0-15)
 __device__ __forceinline__ void rec16_contexts(uint32_t y, uint32_t z, uint32_t w, uint32_t dw[5]) {
   const uint64_t lo = (uint64_t)y | ((uint64_t)z << 32);
@@ -239,9 +263,9 @@ __device__ __forceinline__ bool ptab_at(const DevIndex& ix, uint64_t t, uint64_t
   if (ix.ptab_rec == 2) {
     const uint4 r = static_cast<const uint4*>(ix.ptab)[t];
     const uint32_t wc = r.y & 15u;
-    sp = r.x;
-    ep = (uint64_t)r.x + (wc == kRec16Wide ? r.z : wc);
-    return true;
+    sp = rec16_sp(r.x, r.w, ix.wide);
+    ep = sp + (wc == kRec16Wide ? r.z : wc);
+    return !(wc == kRec16Wide && r.z == kRec16NoRange);
   }
   if (ix.wide) {
     const uint64_t e = static_cast<const uint64_t*>(ix.ptab)[t];

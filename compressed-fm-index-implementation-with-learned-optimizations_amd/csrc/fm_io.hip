@@ -224,7 +224,10 @@ uint64_t index_hbm_bytes(const cs_fm_index* hc) {
 bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
-  if (bytes + total_b / 8 > free_b) return false;
+  // the built index leaves an eighth free; a replacement (freed > 0) needs both copies
+  // for a moment, within 2 GB of the device's free memory
+  const uint64_t net = bytes > freed ? bytes - freed : 0;
+  if (net + total_b / 8 > free_b || bytes + (2ull << 30) > free_b) return false;
   if (!h->hbm_budget) return true;
   const uint64_t have = index_hbm_bytes(h);
   return have + bytes <= h->hbm_budget + freed;

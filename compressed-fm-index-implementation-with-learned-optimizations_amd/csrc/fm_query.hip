@@ -481,7 +481,8 @@ __device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTa
 enum : uint32_t { kCtxNone = 0, kCtxAbsent = 1, kCtxOk = 2 };
 // whether a record's inline contexts answer k characters over a w-row range
 __device__ __forceinline__ bool rec_inline(const DevIndex& ix, uint64_t k, uint64_t w) {
-  return ix.ptab_rec == 2 ? k <= kRec16Q : ix.ptab_rec == 3 ? w <= kRecQCtx : w <= kRecCtx;
+  return ix.ptab_rec == 2 ? k <= (ix.wide ? kRec16QW : kRec16Q)
+                          : ix.ptab_rec == 3 ? w <= kRecQCtx : w <= kRecCtx;
 }
 // inl: the contexts of a context record whose range [sp, ep) is at most kRecCtx rows
 // (already read with the record: no further access), else null.
@@ -520,7 +521,10 @@ __device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTabl
     hi = (uint32_t)(ep - sp);
     if (ix.ptab_rec == 2) {
       uint32_t d[5];
-      rec16_contexts(inl[1], inl[2], inl[3], d);
+      if (ix.wide)
+        rec16w_contexts(inl[1], inl[2], inl[3], d);
+      else
+        rec16_contexts(inl[1], inl[2], inl[3], d);
       w[0] = make_uint4(d[0], d[1], d[2], d[3]);
       w[1] = make_uint4(d[4], 0, 0, 0);
     } else {
@@ -1103,11 +1107,15 @@ __global__ __launch_bounds__(kBlk) void k_count_ctx(DevIndex ix, const uint8_t* 
     } else if (ix.ptab_rec == 2) {
       const uint4 a = static_cast<const uint4*>(ix.ptab)[t[j]];
       const uint32_t wc = a.y & 15u;
-      sp[j] = a.x;
-      inl[j] = wc != kRec16Wide && k[j] <= kRec16Q;
-      ep[j] = (uint64_t)a.x + (wc == kRec16Wide ? a.z : wc);
+      sp[j] = rec16_sp(a.x, a.w, ix.wide);
+      inl[j] = wc != kRec16Wide && k[j] <= (ix.wide ? kRec16QW : kRec16Q);
+      ep[j] = sp[j] + (wc == kRec16Wide ? a.z : wc);
+      if (wc == kRec16Wide && a.z == kRec16NoRange) st[j] = 3;  // escaped: from C[]
       uint32_t d[5];
-      rec16_contexts(a.y, a.z, a.w, d);
+      if (ix.wide)
+        rec16w_contexts(a.y, a.z, a.w, d);
+      else
+        rec16_contexts(a.y, a.z, a.w, d);
       w[j][0] = make_uint4(d[0], d[1], d[2], d[3]);
       w[j][1] = make_uint4(d[4], 0u, 0u, 0u);
     } else if (!ptab_at(ix, t[j], sp[j], ep[j])) {
@@ -2170,6 +2178,40 @@ __global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict
   }
 }
 
+// Compact records of a wide index from its packed 8-B table (fm_device.hpp kRec16CtxW):
+// 4-character contexts of rows 0-9, bits 32-37 of sp in dword 3.
+__global__ __launch_bounds__(kBlk) void k_fill_records16_wide(const uint64_t* __restrict__ tab,
+                                                              uint64_t entries,
+                                                              const uint16_t* __restrict__ lctx,
+                                                              uint4* __restrict__ rec) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
+    const uint64_t e = tab[t], w = e >> 38, sp = e & ((1ull << 38) - 1);
+    const uint32_t sph = (uint32_t)(sp >> 32) << 24;
+    if (w == kPtabEsc) {  // the 8-B table escaped this range: the search starts from C[]
+      rec[t] = make_uint4(0u, kRec16Wide, kRec16NoRange, 0u);
+      continue;
+    }
+    bool esc = false;
+    uint32_t y = 0, z = 0, x3 = 0;
+    for (uint32_t i = 0; i < kRec16CtxW && i < w; ++i) {
+      const uint32_t c = lctx[sp + i];
+      esc |= (c & kCtxEsc) != 0;
+      const uint32_t b = c & 0xFFu;
+      if (i < 3)
+        y |= b << (4 + 8 * i);
+      else if (i < 7)
+        z |= b << (8 * (i - 3));
+      else
+        x3 |= b << (8 * (i - 7));
+    }
+    if (w > kRec16CtxW || esc)
+      rec[t] = make_uint4((uint32_t)sp, kRec16Wide, (uint32_t)w, sph);
+    else
+      rec[t] = make_uint4((uint32_t)sp, y | (uint32_t)w, z, x3 | sph);
+  }
+}
+
 // Quaternary-matrix records (fm_device.hpp kRecQCtx): sp, width, contexts of rows 0-1.
 __global__ __launch_bounds__(kBlk) void k_fill_records_q(const uint2* __restrict__ tab,
                                                          uint64_t entries,
@@ -2196,7 +2238,8 @@ __global__ __launch_bounds__(kBlk) void k_fill_records_q(const uint2* __restrict
 // left after the table then reads its context sector).
 cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   h->ptab_rec = 0;
-  if (!h->d_ptab || !h->ptab_k || !h->d_lctx || h->wide) return CS_OK;
+  if (!h->d_ptab || !h->ptab_k || !h->d_lctx) return CS_OK;
+  if (h->wide && h->lctx_eb != 2) return CS_OK;  // wide records: occurrence lines only
   const uint64_t entries = h->ptab_entries();
   if (h->lctx_eb == 4) {  // quaternary matrix: 16-B records when ranges average <= 2 rows
     if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
@@ -2225,9 +2268,13 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   // the 20-mers of the DNA workloads; the compact q = 5 still does from k = 15
   bool want = h->ptab_k >= 13;
   uint32_t fmt = h->ptab_k >= 15 && h->n <= 4 * entries ? 2 : 1;
+  if (h->wide) {  // compact only (sp needs more than 32 bits); ranges averaging <= 8 rows
+    want = h->ptab_k >= 15 && h->n <= 8 * entries;
+    fmt = 2;
+  }
   if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) {
     want = std::atoi(e) != 0;
-    fmt = std::atoi(e) == 16 ? 2 : 1;
+    fmt = h->wide || std::atoi(e) == 16 ? 2 : 1;
   }
   if (!want) return CS_OK;
   const uint64_t bytes = entries * (fmt == 2 ? 16 : 32);
@@ -2235,7 +2282,11 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   if (!hbm_room(h, bytes, entries * h->ptab_entry_bytes())) return CS_OK;
   void* rec = nullptr;
   FMX_HIP(hipMalloc(&rec, bytes));
-  if (fmt == 2)
+  if (h->wide)
+    k_fill_records16_wide<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
+        static_cast<const uint64_t*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
+        static_cast<uint4*>(rec));
+  else if (fmt == 2)
     k_fill_records16<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
         static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
         static_cast<uint4*>(rec));
