@@ -647,6 +647,11 @@ def main():
                            "engine": engine_name(info)},
                 "roofline": rf,
                 "build_s": build_s,
+                "index_hbm_bytes": int(sum(idx.export_meta()[1])),
+                "index_parts": {"prefix_table_or_records": info.prefix_bytes,
+                                "left_contexts": info.context_bytes, "rank_lines": info.rank_bytes,
+                                "walk_lines": info.walk_bytes, "full_sa": info.full_sa_bytes,
+                                "ssa": info.ssa_bytes, "text_in_hbm": bool(info.text_in_hbm)},
                 "replicate": args.replicate if world > 1 else "single",
                 "replicate_s": replicate_s,
                 "found_frac": found / B,
