@@ -72,6 +72,9 @@ LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", 
              "host_batch", "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
+# the learned occurrence lines (the reference's learned occ, as int16
+# residuals against a per-superblock linear model): the headline and the whole LF loop
+LEGS_LEARNED = ["learned_count", "learned_lf_loop"]
 # repetitive DNA of the same size (cs_synth_text_device kind 2): heavy-tailed ranges
 LEGS_RDNA = ["count_rdna", "locate_rdna"]
 # the HBM footprint / throughput trade-off: the same text indexed with the optional
@@ -79,7 +82,7 @@ LEGS_RDNA = ["count_rdna", "locate_rdna"]
 LEGS_FOOT = ["footprint", "budget"]
 # CS_FM_HBM_BUDGET values of the budget leg, as fractions of the default index's footprint
 BUDGET_FRACS = (0.3, 0.6)
-ALL_LEGS = LEGS_MAIN + LEGS_WM + LEGS_WALK + LEGS_RDNA + LEGS_FOOT
+ALL_LEGS = LEGS_MAIN + LEGS_WM + LEGS_WALK + LEGS_LEARNED + LEGS_RDNA + LEGS_FOOT
 
 # footprint ladder rungs: (name, what the rung adds, build switches)
 _OFF = {"CS_FM_PREFIX_K": "0", "CS_FM_LCTX": "0", "CS_FM_CTX_RECORDS": "0", "CS_FM_FULL_SA": "0",
@@ -504,7 +507,8 @@ def main():
     torch.cuda.synchronize()
     replicate_s = None
     need_main = not (args.only and (args.only in LEGS_WM or args.only in LEGS_WALK
-                                    or args.only in LEGS_RDNA or args.only in LEGS_FOOT))
+                                    or args.only in LEGS_LEARNED or args.only in LEGS_RDNA
+                                    or args.only in LEGS_FOOT))
     idx = None
     if need_main:
         if args.replicate == "broadcast" and world > 1:
@@ -970,7 +974,8 @@ def main():
             del ref, bwt
 
     # ---- N = 1 legs on the reference's own structure: the binary wavelet matrix ----
-    if idx is not None and (legs & (set(LEGS_WM) | set(LEGS_WALK) | set(LEGS_RDNA) | set(LEGS_FOOT))):
+    if idx is not None and (legs & (set(LEGS_WM) | set(LEGS_WALK) | set(LEGS_LEARNED) | set(LEGS_RDNA)
+                                    | set(LEGS_FOOT))):
         del idx
         idx = None
         torch.cuda.synchronize()
@@ -1018,6 +1023,31 @@ def main():
                 wk, ki, kwl, W, text, 0, dev, sh)
             lg["locate_ssa"]["build_s"] = bs
             del wk
+            torch.cuda.synchronize()
+
+    with LegGuard(leg_errors, "learned legs"):
+        if legs & set(LEGS_LEARNED) and args.kind == "dna":
+            lx, bs = build_index(pkg, text, N, args.ssa_stride, local_dev, {"CS_FM_ENGINE": "learned"})
+            li = lx.info()
+            lwl = workload_key(args.kind, N, m, B, li, args.queries)
+            log(rank, "learned-lines index built in %.1f s" % bs)
+            for name, fl, what in (("learned_count", 0, "the headline on learned occurrence lines (%d rows "
+                                    "per 32-B line: int16 residuals against a linear model per superblock, "
+                                    "src/core/bitvector_learned.cpp:114-203)" % li.line_bits),
+                                   ("learned_lf_loop", 3, "the reference's whole backward-search loop over the "
+                                    "learned occurrence lines (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS)")):
+                if name in legs:
+                    o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                    lg[name], _ = count_leg(
+                        name, what, lx, li, lwl, W,
+                        lambda fl=fl, o8=o8: lx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B,
+                                                                o8.data_ptr(), flags=fl, stream=sh),
+                        fl, stream_m + 8 * B, max(3, args.steps // 8), 1, stream, sh, dev, counts,
+                        lambda o8=o8: o8.cpu().numpy())
+                    lg[name].update({"build_s": bs, "rank_line_bytes": li.rank_bytes,
+                                     "index_hbm_bytes": int(sum(lx.export_meta()[1]))})
+                    del o8
+            del lx
             torch.cuda.synchronize()
 
     with LegGuard(leg_errors, "footprint"):
