@@ -63,6 +63,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # measured random-read ceiling of MI355X: profiles/microbench/gather_bench.hip, 8..32-B
 # random reads over a 4 GB table at 49-52 G accesses/s (profiles/r01/gather_bench*.txt)
 RANDOM_CEIL = 5.0e10
+# the count kernel's access mix without its logic — per access one random 16-B read from a
+# 17-GB table + 32 B streamed in + 8 B streamed out (gather_bench k_mixed,
+# profiles/r02/gather_bench_mixed_17g.txt): 33.4-33.6 G accesses/s
+MIXED_CEIL = 3.35e10
 PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
@@ -216,7 +220,9 @@ def roofline(alg_random, alg_stream, accesses, kern_s, B, traffic, stream_read=N
             "random_accesses_per_query": accesses / B,
             "random_accesses_per_s": accesses / kern_s,
             "random_access_ceiling_per_s": RANDOM_CEIL,
-            "frac_of_random_access_ceiling": accesses / kern_s / RANDOM_CEIL}
+            "frac_of_random_access_ceiling": accesses / kern_s / RANDOM_CEIL,
+            "access_mix_ceiling_per_s": MIXED_CEIL,
+            "frac_of_access_mix_ceiling": accesses / kern_s / MIXED_CEIL}
 
 
 def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, steps, warmup,
