@@ -72,7 +72,7 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
-             "count_m64", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
+             "count_m64", "count_m64_steps", "count_m150", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
              "host_batch", "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
@@ -755,17 +755,22 @@ def main():
                         fl, stream_m + 8 * B, max(3, steps // 4), 1, stream, sh, dev, counts,
                         lambda o8=o8: o8.cpu().numpy())
                     del o8
-            for name, mm in (("count_m32", 32), ("count_m64", 64)):
+            ver = "rank steps until the range is at most 8 rows, then the rows' suffix-array entries " \
+                  "and the text before them (verification)" if info.full_sa_bytes and info.text_in_hbm else None
+            for name, mm, fl in (("count_m32", 32, 0), ("count_m64", 64, 0), ("count_m64_steps", 64, 16),
+                                 ("count_m150", 150, 0)):
                 if name in legs:
                     Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
                     o8 = torch.empty(B, dtype=torch.int64, device=dev)
+                    steps_what = "%d rank steps, then the left contexts" % (mm - info.prefix_k - info.context_q)
                     r, got = count_leg(
-                        name, "Q_text %d-mers through the headline index: prefix table, %d rank steps, "
-                        "then the left contexts" % (mm, mm - info.prefix_k - info.context_q),
+                        name, "Q_text %d-mers through the headline index: prefix table, %s%s" % (
+                            mm, ver if ver and not fl else steps_what,
+                            " (CS_Q_NO_VERIFY)" if fl else ""),
                         idx, info, wl, Wm,
-                        lambda Wm=Wm, o8=o8: idx.count_batch_device(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
-                                                                    o8.data_ptr(), sh),
-                        0, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
+                        lambda Wm=Wm, o8=o8, fl=fl: idx.count_device_ex(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
+                                                                        o8.data_ptr(), flags=fl, stream=sh),
+                        fl, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
                         lambda o8=o8: o8.cpu().numpy())
                     r["found_frac"] = float((got >= 1).mean())
                     lg[name] = r

@@ -119,6 +119,11 @@ struct DevIndex {
   // 2^lmodel_shift lines.
   const void* lmodel;
   uint32_t lmodel_shift;
+  // Full suffix array (u32) and text (n bytes) of an lf_exact index that keeps both in
+  // HBM, for verifying narrow ranges against the text (fm_query.hip verify_count); null
+  // otherwise or under CS_Q_NO_CONTEXTS / CS_Q_NO_VERIFY.
+  const uint32_t* vsa;
+  const uint8_t* vtext;
 };
 
 // Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q

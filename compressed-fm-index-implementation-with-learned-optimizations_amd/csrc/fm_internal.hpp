@@ -121,6 +121,9 @@ struct cs_fm_index {
     d.lctx_sb = lctx_sb;
     d.lmodel = d_lmodel;
     d.lmodel_shift = lmodel_shift;
+    const bool ver = d_sa && d_dtext && lf_exact && !wide;
+    d.vsa = ver ? static_cast<const uint32_t*>(d_sa) : nullptr;
+    d.vtext = ver ? static_cast<const uint8_t*>(d_dtext) : nullptr;
     return d;
   }
 };

@@ -594,6 +594,131 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
   return count_rest<E>(ix, T, P, k, sp, ep, bytes, inl);
 }
 
+// Verification against the text (lf_exact indexes that keep the full suffix array and the
+// text in HBM: DevIndex::vsa / vtext).  Row r of [sp, ep) survives the k remaining steps
+// iff its chain spells P[k-1], ..., P[0]; LF^t(r) is the row of the rotation SA[r] - t, so
+// that chain is text[SA[r] - k .. SA[r]) (cyclically, as the rotations).  A narrow range
+// with many characters left is therefore finished by reading its rows' SA entries (one
+// sector: the rows are consecutive) and comparing k text bytes before each — two
+// dependent rounds of reads instead of k rank steps (a 64-mer: 49 steps).  The result is
+// the count the steps would give, exactly.
+constexpr uint32_t kVerifyRows = 8;
+constexpr uint32_t kVerifyWords = 4;  // text words compared per round (32 characters)
+
+// bytes P[j, j + 8) as a little-endian uint64, from realigned dword loads that touch only
+// dwords holding bytes of P[0, k) (bytes at or past k: unspecified)
+__device__ __forceinline__ uint64_t pat8(const uint8_t* P, uint64_t j, uint64_t k) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(P) + j;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint32_t off = (uint32_t)(a & 3);
+  const uint64_t left = k - j;
+  const uint32_t nb = off + (uint32_t)(left < 8 ? left : 8);  // bytes spanned from w
+  const uint32_t w0 = w[0];
+  const uint32_t w1 = nb > 4 ? w[1] : 0u;
+  const uint32_t w2 = nb > 8 ? w[2] : 0u;
+  const uint64_t lo = ((uint64_t)w1 << 32) | w0;
+  return off ? (lo >> (8 * off)) | ((uint64_t)w2 << (64 - 8 * off)) : lo;
+}
+__device__ __forceinline__ uint64_t pat8(PackedDna P, uint64_t j, uint64_t) {
+  uint64_t x = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) x |= (uint64_t)P[j + i] << (8 * i);
+  return x;
+}
+// A pattern read byte by byte: copies in kernel arguments or LDS (k_count_one, the
+// resident server), where realigned word loads would force the copy to scratch.
+struct BytePat {
+  const uint8_t* b;
+  __device__ __forceinline__ uint32_t operator[](uint64_t i) const { return b[i]; }
+};
+__device__ __forceinline__ uint64_t pat8(BytePat P, uint64_t j, uint64_t k) {
+  uint64_t x = 0;
+  for (uint32_t i = 0; i < 8 && j + i < k; ++i) x |= (uint64_t)P[j + i] << (8 * i);
+  return x;
+}
+// the mask of the bytes of a chunk at j that lie inside P[0, k)
+__device__ __forceinline__ uint64_t chunk_mask(uint64_t j, uint64_t k) {
+  return k - j >= 8 ? ~0ull : (1ull << (8 * (k - j))) - 1;
+}
+// text[t, t + 8) from the aligned words w0 (holding t) and w1 (the next one)
+__device__ __forceinline__ uint64_t text8(uint64_t w0, uint64_t w1, uint64_t t) {
+  const uint32_t sh = (uint32_t)(t & 7) * 8;
+  return sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+}
+
+// text[q, q + k) == P[0, k), cyclically (positions mod n).  Windows inside [0, n) compare
+// 8 kVerifyWords bytes per round of aligned 8-B loads; a window through the end of the text (a row
+// whose suffix starts fewer than k positions into the text) byte by byte.
+template <class PT>
+__device__ __forceinline__ bool window_eq(const DevIndex& ix, PT P, uint64_t q, uint64_t k,
+                                          uint64_t* bytes) {
+  const uint64_t n = ix.n;
+  if (q + k > n) {
+    for (uint64_t j = 0; j < k; ++j) {
+      uint64_t t = q + j;
+      if (t >= n) t -= n;
+      if (ix.vtext[t] != (uint8_t)P[j]) return false;
+    }
+    if (bytes) *bytes += 64;
+    return true;
+  }
+  const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
+  const uint64_t last = (q + k - 1) >> 3;  // the last word holding a byte of the window
+  for (uint64_t j0 = 0; j0 < k; j0 += 8 * kVerifyWords) {
+    const uint64_t a = (q + j0) >> 3;
+    uint64_t w[kVerifyWords + 1];
+#pragma unroll
+    for (uint32_t i = 0; i <= kVerifyWords; ++i) w[i] = a + i <= last ? tw[a + i] : 0ull;
+    if (bytes) *bytes += 8 * kVerifyWords;
+    uint64_t diff = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kVerifyWords; ++i) {
+      const uint64_t j = j0 + 8 * i;
+      if (j < k) diff |= (text8(w[i], w[i + 1], q + j) ^ pat8(P, j, k)) & chunk_mask(j, k);
+    }
+    if (diff) return false;
+  }
+  return true;
+}
+
+// The rows' SA entries (consecutive rows: one sector) in one round, then — for two rows or
+// more — one aligned 8-B word at the start of every row's window in one round (1-8 of its
+// first characters against the same pattern chunk), then the full window of the few rows
+// that pass.
+template <class PT>
+__device__ __forceinline__ uint64_t verify_count(const DevIndex& ix, PT P, uint64_t k,
+                                                 uint64_t sp, uint64_t ep, uint64_t* bytes) {
+  const uint32_t w = (uint32_t)(ep - sp);
+  const uint64_t n = ix.n;
+  const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
+  uint32_t pos[kVerifyRows];
+#pragma unroll
+  for (uint32_t i = 0; i < kVerifyRows; ++i) pos[i] = i < w ? ix.vsa[sp + i] : 0u;
+  if (bytes) *bytes += 32 + (w > 1 ? 32ull * w : 0ull);
+  const uint64_t p0 = pat8(P, 0, k) & chunk_mask(0, k);
+  uint32_t pass = w == 1 ? 1u : 0u;  // one row: straight to its full window
+#pragma unroll
+  for (uint32_t i = 0; i < kVerifyRows; ++i) {
+    if (i >= w || w == 1) break;
+    const uint64_t p = pos[i];
+    const uint64_t q = p >= k ? p - k : p + n - k;  // P[0] sits at text[q]
+    const uint32_t sh = (uint32_t)(q & 7) * 8;
+    const uint64_t x = tw[q >> 3] >> sh;  // text[q, q + 8 - (q & 7)): inside the word
+    const uint64_t msk = chunk_mask(0, k) & (~0ull >> sh) & (q + 8 <= n ? ~0ull : (1ull << (8 * (n - q))) - 1);
+    if (((x ^ p0) & msk) == 0) pass |= 1u << i;
+  }
+  uint64_t cnt = 0;
+  while (pass) {
+    const uint32_t i = (uint32_t)__ffs(pass) - 1u;
+    pass &= pass - 1;
+    uint64_t p = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < kVerifyRows; ++t) p = t == i ? pos[t] : p;  // no dynamic register index
+    cnt += window_eq(ix, P, p >= k ? p - k : p + n - k, k, bytes) ? 1u : 0u;
+  }
+  return cnt;
+}
+
 // The rest of a count() from the range [sp, ep) (non-empty) with P[0..k) still to
 // process (fm_index.cpp:90-98); inl as search_start's.
 template <class E, class PT>
@@ -603,6 +728,9 @@ __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTab
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
   bool ctx = E::kCtx && ix.lctx != nullptr;
   while (k > 0) {
+    // verification pays once it saves more than the one step + context read it replaces
+    if (ix.vsa && ep - sp <= kVerifyRows && k > (ctx ? ix.lctx_q + 1u : 2u) && k < ix.n)
+      return verify_count(ix, P, k, sp, ep, bytes);
     if (inl && !rec_inline(ix, k, ep - sp)) inl = nullptr;
     if (ctx && k <= ix.lctx_q && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
       uint64_t cnt;
@@ -1244,7 +1372,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
 // P[k-1], ..., P[0] are exactly the rows that survive the reference's remaining k steps
 // (fm_index.cpp:90-96).
 template <int U, int W>
-__global__ __launch_bounds__(kBlk) void k_count_qctx(DevIndex ix, const uint8_t* __restrict__ pats,
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void k_count_qctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs,
                                                      uint64_t npat, CountOut co, uint64_t fixed_m) {
   // bits 0-7 table digit (kNoCode: outside the table alphabet), 8-15 dense code, bit 16 the
@@ -1394,13 +1522,19 @@ __global__ __launch_bounds__(kBlk) void k_count_qctx(DevIndex ix, const uint8_t*
 // through the cache hierarchy instead of being staged into LDS.
 template <class E>
 __global__ void k_count_one(DevIndex ix, OnePattern p, uint64_t* __restrict__ out) {
+  // the pattern to LDS first, one dword per lane: searching straight from the kernel
+  // argument miscompiled (the first bytes of a chunk of verify_count's came out wrong)
+  __shared__ uint32_t pb[OnePattern::kMax / 4];
+  if (threadIdx.x < OnePattern::kMax / 4)
+    pb[threadIdx.x] = reinterpret_cast<const uint32_t*>(p.b)[threadIdx.x];
+  __syncthreads();
   if (threadIdx.x != 0) return;
   const NodeTable& T = *ix.table;
   uint64_t res;
   if (p.m == 0) res = ix.n;       // fm_index.cpp:80
   else if (ix.n == 0) res = 0;    // :81
   else {
-    res = count_pattern<E>(ix, T, p.b, p.m);
+    res = count_pattern<E>(ix, T, BytePat{reinterpret_cast<const uint8_t*>(pb)}, p.m);
   }
   // system-scope store: the host polls this word instead of waiting for the stream
   __hip_atomic_store(out, res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1447,7 +1581,7 @@ __global__ __launch_bounds__(64) void k_count_server(DevIndex ix, const uint64_t
           if (m == 0) res = ix.n;        // fm_index.cpp:80
           else if (ix.n == 0) res = 0;   // :81
           else {
-            res = count_pattern<E>(ix, T, pat, m);
+            res = count_pattern<E>(ix, T, BytePat{pat}, m);
           }
           __hip_atomic_store(resp, res, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           __hip_atomic_store(resp + 1, (uint64_t)want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2356,6 +2490,7 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
     d.lctx = nullptr;
     d.lctx_q = 0;
   }
+  if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY)) d.vsa = nullptr, d.vtext = nullptr;
   if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
   return d;
 }

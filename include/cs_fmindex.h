@@ -222,7 +222,12 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
  * be run and timed on any index:
  *   CS_Q_NO_PREFIX     start every search from C[] (fm_index.cpp:84-89): no prefix table
  *   CS_Q_NO_CONTEXTS   step every remaining character through the rank structure
- *                      (fm_index.cpp:90-96): no left contexts, no context records
+ *                      (fm_index.cpp:90-96): no left contexts, no context records, no
+ *                      verification against the text
+ *   CS_Q_NO_VERIFY     no verification of narrow ranges against the text (an index
+ *                      keeping the full suffix array and the text finishes a search
+ *                      whose range is at most 8 rows by comparing the characters left
+ *                      with the text before each row's suffix)
  *   CS_Q_NO_FULL_SA    locate phase 2: walk LF to the sampled rows (fm_index.cpp:125-153)
  *                      even when the full suffix array is kept
  *   CS_Q_NO_WALK_LINES locate phase 2: walk the rank structure to the reference's row
@@ -231,6 +236,7 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
 #define CS_Q_NO_CONTEXTS 2u
 #define CS_Q_NO_FULL_SA 4u
 #define CS_Q_NO_WALK_LINES 8u
+#define CS_Q_NO_VERIFY 16u
 
 /* Where a batch count writes.  width 8: uint64 counts (the reference's return type,
  * fm_index.hpp:26).  width 4: uint32, exact while n < 2^32 (CS_ERR_INVALID otherwise).

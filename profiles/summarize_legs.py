@@ -27,7 +27,8 @@ import sys
 # the kernel that carries each leg's work
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
-              "count_m64": "count", "count_fixed": "count", "wm_count": "count",
+              "count_m64": "count", "count_m64_steps": "count", "count_m150": "count",
+              "count_fixed": "count", "wm_count": "count",
               "wm_lf_loop": "count", "learned_count": "count", "learned_lf_loop": "count",
               "count_unif": "count",
               "locate": ("k_locate_sa", "k_locate_sa_wide", "k_walk_fused", "k_walk_fused_wide",

@@ -628,7 +628,7 @@ def test_create_from_arrays(pkg, name):
 
 # ---- query forms: flags (CS_Q_*), count widths, packed DNA ----------------------
 
-FLAG_SETS = {"none": 0, "no_prefix": 1, "no_contexts": 2, "loop": 3}
+FLAG_SETS = {"none": 0, "no_prefix": 1, "no_contexts": 2, "loop": 3, "no_verify": 16}
 
 
 def _substrings_and_mutants(t, lengths, per, seed):
@@ -688,8 +688,38 @@ def test_query_flags_count(built, pkg, name):
     # than a 16-B record (skewed texts with compact records)
     eb = max(g.info().record_bytes, 8)
     assert nb["loop"] + eb * len(pats) >= nb["no_contexts"] or g.info().prefix_k == 0, nb
-    if g.info().context_q == 0:
-        assert nb["no_contexts"] == nb["none"], nb
+    if g.info().context_q == 0:  # no contexts: CS_Q_NO_CONTEXTS leaves out only the verification
+        assert nb["no_contexts"] == nb["no_verify"], nb
+
+
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_count_verify_long(built, pkg, name):
+    """Long patterns, with and without the verification of narrow ranges against the
+    text (CS_Q_NO_VERIFY; fm_query.hip verify_count): substrings and mutants up to 500
+    characters, cyclic substrings across the end of the text (through the terminator) and
+    periodic patterns longer than the text — the oracle's counts (fm_index.cpp:84-100)."""
+    g, o = built(name)
+    t = TEXTS[name]
+    n = len(t)
+    rng = np.random.default_rng(n + 17)
+    pats = _substrings_and_mutants(t, (12, 18, 24, 40, 64, 130, 500), 6, n + 11)
+    tt = t * 3
+    for _ in range(12):  # rotations' prefixes that wrap: the tail, then the head
+        a = int(rng.integers(1, min(n, 40) + 1))
+        b = int(rng.integers(0, min(n, 40) + 1))
+        pats.append(t[n - a:] + t[:b])
+    for m in (n - 1, n, n + 1, 2 * n + 3):
+        if m > 0:
+            i = int(rng.integers(0, n))
+            pats.append(tt[i:i + m])
+    pats = [p for p in pats if p]
+    want = [o.count(p) for p in pats]
+    for f in (0, 16):
+        got, _, _ = _count_ex(g, pats, flags=f)
+        assert got.tolist() == want, (name, f)
+    # single patterns (k_count_one: the pattern in the kernel arguments, up to 128 bytes)
+    one = [i for i, p in enumerate(pats) if len(p) <= 128][::3]
+    assert [g.count(pats[i]) for i in one] == [want[i] for i in one], name
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))
