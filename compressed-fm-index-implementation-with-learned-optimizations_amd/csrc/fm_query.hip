@@ -681,25 +681,26 @@ __device__ __forceinline__ bool window_eq(const DevIndex& ix, PT P, uint64_t q, 
   return true;
 }
 
-// The rows' SA entries (consecutive rows: one sector) in one round, then — for two rows or
-// more — one aligned 8-B word at the start of every row's window in one round (1-8 of its
-// first characters against the same pattern chunk), then the full window of the few rows
-// that pass.
+// The rows of [sp, ep) (at most kVerifyRows) worth a full comparison: for two rows or more,
+// their SA entries (consecutive rows: one sector) in one round, then one aligned 8-B word
+// at the start of every row's window in one round (1-8 of its first characters against
+// the same pattern chunk).  Bit i: row sp + i.
 template <class PT>
-__device__ __forceinline__ uint64_t verify_count(const DevIndex& ix, PT P, uint64_t k,
-                                                 uint64_t sp, uint64_t ep, uint64_t* bytes) {
+__device__ __forceinline__ uint32_t verify_filter(const DevIndex& ix, PT P, uint64_t k,
+                                                  uint64_t sp, uint64_t ep, uint64_t* bytes) {
   const uint32_t w = (uint32_t)(ep - sp);
+  if (w == 1) return 1u;
   const uint64_t n = ix.n;
   const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
   uint32_t pos[kVerifyRows];
 #pragma unroll
   for (uint32_t i = 0; i < kVerifyRows; ++i) pos[i] = i < w ? ix.vsa[sp + i] : 0u;
-  if (bytes) *bytes += 32 + (w > 1 ? 32ull * w : 0ull);
+  if (bytes) *bytes += 32 + 32ull * w;
   const uint64_t p0 = pat8(P, 0, k) & chunk_mask(0, k);
-  uint32_t pass = w == 1 ? 1u : 0u;  // one row: straight to its full window
+  uint32_t pass = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kVerifyRows; ++i) {
-    if (i >= w || w == 1) break;
+    if (i >= w) break;
     const uint64_t p = pos[i];
     const uint64_t q = p >= k ? p - k : p + n - k;  // P[0] sits at text[q]
     const uint32_t sh = (uint32_t)(q & 7) * 8;
@@ -707,14 +708,30 @@ __device__ __forceinline__ uint64_t verify_count(const DevIndex& ix, PT P, uint6
     const uint64_t msk = chunk_mask(0, k) & (~0ull >> sh) & (q + 8 <= n ? ~0ull : (1ull << (8 * (n - q))) - 1);
     if (((x ^ p0) & msk) == 0) pass |= 1u << i;
   }
+  return pass;
+}
+
+// P[s, ...) as a pattern of its own
+__device__ __forceinline__ const uint8_t* pat_shift(const uint8_t* P, uint64_t s) { return P + s; }
+__device__ __forceinline__ BytePat pat_shift(BytePat P, uint64_t s) { return BytePat{P.b + s}; }
+__device__ __forceinline__ PackedDna pat_shift(PackedDna P, uint64_t s) {
+  return PackedDna{s < 32 ? P.x >> (2 * s) : 0ull};
+}
+
+// The candidate rows base + i (bit i of mm) — their contexts matched P[k - qf, k), or they
+// passed verify_filter (qf = 0): each one's SA entry, then P[0, k - qf) against the text
+// before its suffix's last qf characters.
+template <class PT>
+__device__ __forceinline__ uint64_t verify_rows(const DevIndex& ix, PT P, uint64_t k, uint32_t qf,
+                                                uint64_t base, uint32_t mm, uint64_t* bytes) {
+  const uint64_t n = ix.n;
   uint64_t cnt = 0;
-  while (pass) {
-    const uint32_t i = (uint32_t)__ffs(pass) - 1u;
-    pass &= pass - 1;
-    uint64_t p = 0;
-#pragma unroll
-    for (uint32_t t = 0; t < kVerifyRows; ++t) p = t == i ? pos[t] : p;  // no dynamic register index
-    cnt += window_eq(ix, P, p >= k ? p - k : p + n - k, k, bytes) ? 1u : 0u;
+  while (mm) {
+    const uint32_t i = (uint32_t)__ffs(mm) - 1u;
+    mm &= mm - 1;
+    const uint64_t p = ix.vsa[base + i];
+    if (bytes) *bytes += 32;
+    cnt += window_eq(ix, P, p >= k ? p - k : p + n - k, k - qf, bytes) ? 1u : 0u;
   }
   return cnt;
 }
@@ -727,16 +744,38 @@ __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTab
                                                uint64_t* bytes, const uint32_t* inl) {
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
   bool ctx = E::kCtx && ix.lctx != nullptr;
+  // context characters a record holds inline
+  const uint32_t qi = ix.ptab_rec == 2 ? (ix.wide ? kRec16QW : kRec16Q) : ix.lctx_q;
   while (k > 0) {
-    // verification pays once it saves more than the one step + context read it replaces
-    if (ix.vsa && ep - sp <= kVerifyRows && k > (ctx ? ix.lctx_q + 1u : 2u) && k < ix.n)
-      return verify_count(ix, P, k, sp, ep, bytes);
-    if (inl && !rec_inline(ix, k, ep - sp)) inl = nullptr;
-    if (ctx && k <= ix.lctx_q && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
-      uint64_t cnt;
-      if (ctx_count<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, cnt, bytes, inl)) return cnt;
-      ctx = false;
+    // verification against the text pays once it saves more than the one step + context
+    // read it replaces; the contexts (of the record: no read, or of a sector) filter the
+    // rows first, on P's last qf characters
+    const bool ver = ix.vsa && k > (ctx ? ix.lctx_q + 1u : 2u) && k < ix.n;
+    uint32_t qf = 0;
+    if (ctx && k <= ix.lctx_q) qf = (uint32_t)k;
+    else if (ctx && ver) qf = inl && rec_inline(ix, qi, ep - sp) ? qi : ix.lctx_q;
+    if (inl && !(qf && rec_inline(ix, qf, ep - sp))) inl = nullptr;
+    uint32_t mm = 0;
+    uint64_t base = sp;
+    bool cand = false;
+    if (qf && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
+      const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, pat_shift(P, k - qf), qf, sp, ep, mm,
+                                                       base, bytes, inl);
+      if (r == kCtxAbsent) return 0;
+      if (r == kCtxOk) {
+        if (qf == k) return (uint64_t)__popc(mm);
+        cand = true;
+      } else {
+        ctx = false;  // an escaped context or a rare symbol
+      }
     }
+    if (!cand && ver && ep - sp <= kVerifyRows) {
+      mm = verify_filter(ix, P, k, sp, ep, bytes);
+      base = sp;
+      qf = 0;
+      cand = true;
+    }
+    if (cand) return verify_rows(ix, P, k, qf, base, mm, bytes);
     inl = nullptr;
     --k;
     if (!E::step(ix, T, P[k], sp, ep, bytes)) return 0;
