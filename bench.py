@@ -73,7 +73,7 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
              "count_m64", "count_m64_steps", "count_m150", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
-             "host_batch", "extract"]
+             "locate_m64", "locate_m64_steps", "host_batch", "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
 # the learned occurrence lines (the reference's learned occ, as int16
@@ -812,6 +812,21 @@ def main():
                     "locate_ssa_rows", "locate with the reference's SSA walk (fm_index.cpp:125-153): LF over the occurrence "
                     "lines to a row with row %% %d == 0, SA sample + steps (CS_Q_NO_FULL_SA | "
                     "CS_Q_NO_WALK_LINES)" % args.ssa_stride, idx, info, wl, W, text, 4 | 8, dev, sh, reps=2)
+            for name, mm, one in (("locate_m64", 64, True), ("locate_m64_steps", 64, False)):
+                # long patterns: a narrow range finishes by verification against the text
+                # (positions SA[r] - k of the verified rows), or steps to the end (CS_Q_NO_VERIFY)
+                if name in legs and (one or info.full_sa_bytes):
+                    Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
+                    if one:
+                        lg[name] = locate_one_leg(
+                            name, "locate of Q_text %d-mers in one call: record, contexts, then %s" % (
+                                mm, ver or "rank steps"), idx, info, wl, Wm, text, dev, sh)
+                    else:
+                        lg[name] = locate_leg(
+                            name, "locate of Q_text %d-mers, rank steps to the end (CS_Q_NO_VERIFY), "
+                            "positions from the full suffix array" % mm, idx, info, wl, Wm, text, 16,
+                            dev, sh, reps=2)
+                    del Wm
             if "host_batch" in legs and counts is not None:
                 # the batch handed over in host memory (PCIe in and out inside the call)
                 hbuf = W.pats.cpu().numpy()

@@ -800,6 +800,46 @@ constexpr uint64_t kLocSmall = 32;
 constexpr int kWalkAdjShift = 56;
 constexpr uint64_t kWalkRowMask = (1ull << kWalkAdjShift) - 1;
 
+// A window of rows verified against the text (locate_search, indexes with DevIndex::vsa):
+// bits 60-62 zero (a context window has k >= 1 there), bits 38-49 the matches relative to
+// the first one, bits 50-59 k.  Its positions are SA[row] - k as for a context window.
+constexpr uint32_t kLocVerRelBits = 12;
+constexpr uint64_t kLocVerMaxK = (1u << 10) - 1;
+
+// rows, adjustment and match bits of a window record (s & kLocCtx)
+__device__ __forceinline__ void loc_window(uint64_t s, uint64_t& r0, uint64_t& adj, uint32_t& rel) {
+  r0 = s & kLocRowMask;
+  adj = (s >> 60) & 7u;
+  if (adj) {
+    rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+  } else {
+    rel = (uint32_t)(s >> 38) & ((1u << kLocVerRelBits) - 1u);
+    adj = (s >> 50) & kLocVerMaxK;
+  }
+}
+
+// The rows base + i (bit i of mm) whose window text[SA - k, SA - qf) spells P[0, k - qf)
+// (verify_rows' test, as a mask).
+template <class PT>
+__device__ __forceinline__ uint32_t verify_mask(const DevIndex& ix, PT P, uint64_t k, uint32_t qf,
+                                                uint64_t base, uint32_t mm) {
+  const uint64_t n = ix.n;
+  uint32_t out = 0;
+  while (mm) {
+    const uint32_t i = (uint32_t)__ffs(mm) - 1u;
+    mm &= mm - 1;
+    const uint64_t p = ix.vsa[base + i];
+    if (window_eq(ix, P, p >= k ? p - k : p + n - k, k - qf, nullptr)) out |= 1u << i;
+  }
+  return out;
+}
+
+// locate()'s search (fm_index.cpp:107-124): the count and the pattern's record — its
+// range's first row, a context window (the last <= 7 characters over the left contexts),
+// or a verified window (long patterns over lf_exact indexes with the full suffix array and
+// the text: the rows of a narrow range whose text before their suffix spells the rest of
+// the pattern, count_rest's verification; SA[r] - k is then the position, so phase 2 reads
+// the same SA entries the verification read).
 template <class E, class PT>
 __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const NodeTable& T,
                                                   PT P, uint64_t m,
@@ -811,23 +851,62 @@ __device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const Node
   if (sp >= ep) return 0;
   constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);
   bool ctx = E::kCtx && ix.lctx != nullptr && ix.lf_exact;
+  bool ver = ix.vsa != nullptr;  // implies lf_exact
+  const uint32_t qi = ix.ptab_rec == 2 ? kRec16Q : ix.lctx_q;  // vsa: narrow indexes only
   while (k > 0) {
-    if (inl && !rec_inline(ix, k, ep - sp)) inl = nullptr;
-    if (ctx && k <= ix.lctx_q && k <= 7 && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
-      uint32_t mm = 0;
-      uint64_t base;
-      const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, mm, base,
-                                                       nullptr, inl);
-      if (r == kCtxAbsent || (r == kCtxOk && mm == 0)) return 0;
-      if (r == kCtxOk) {
-        const uint32_t f = (uint32_t)__ffs(mm) - 1u;
-        const uint32_t rel = mm >> f;
-        if ((rel >> kLocSpanBits) == 0) {
-          rec = kLocCtx | (k << 60) | ((uint64_t)rel << 38) | (base + f);
-          return (uint64_t)__popc(mm);
+    const uint64_t w = ep - sp;
+    const bool fits = ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R;
+    if (ctx && k <= ix.lctx_q && k <= 7) {
+      const uint32_t* in = inl && rec_inline(ix, k, w) ? inl : nullptr;
+      if (in || fits) {
+        uint32_t mm = 0;
+        uint64_t base;
+        const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, mm, base,
+                                                         nullptr, in);
+        if (r == kCtxAbsent || (r == kCtxOk && mm == 0)) return 0;
+        if (r == kCtxOk) {
+          const uint32_t f = (uint32_t)__ffs(mm) - 1u;
+          const uint32_t rel = mm >> f;
+          if ((rel >> kLocSpanBits) == 0) {
+            rec = kLocCtx | (k << 60) | ((uint64_t)rel << 38) | (base + f);
+            return (uint64_t)__popc(mm);
+          }
+        }
+        ctx = false;
+      }
+    }
+    if (ver && k > (ctx ? ix.lctx_q + 1u : 2u) && k < ix.n && k <= kLocVerMaxK) {
+      uint32_t qf = 0, mm = 0;
+      uint64_t base = sp;
+      bool cand = false;
+      if (ctx) {  // filter on P's last qf characters first (count_rest)
+        qf = inl && rec_inline(ix, qi, w) ? qi : ix.lctx_q;
+        const uint32_t* in = inl && rec_inline(ix, qf, w) ? inl : nullptr;
+        if (in || fits) {
+          const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, pat_shift(P, k - qf), qf, sp, ep,
+                                                           mm, base, nullptr, in);
+          if (r == kCtxAbsent) return 0;
+          if (r == kCtxOk) cand = true;
+          else ctx = false;
         }
       }
-      ctx = false;
+      if (!cand && w <= kVerifyRows) {
+        mm = verify_filter(ix, P, k, sp, ep, nullptr);
+        base = sp;
+        qf = 0;
+        cand = true;
+      }
+      if (cand) {
+        mm = verify_mask(ix, P, k, qf, base, mm);
+        if (!mm) return 0;
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u;
+        const uint32_t rel = mm >> f;
+        if ((rel >> kLocVerRelBits) == 0) {
+          rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
+          return (uint64_t)__popc(mm);
+        }
+        ver = false;  // matches too far apart for the record: step on
+      }
     }
     inl = nullptr;
     --k;
@@ -1054,9 +1133,10 @@ __device__ __forceinline__ void locate_split_store(uint64_t n, uint64_t npat, ui
     const uint64_t q = q0 + (uint64_t)j * kBlk, s = kr[j];
     rs[j] = s;
     if (q >= npat || kc[j] != 1) continue;
-    const uint64_t row = (s & kLocCtx) ? (s & kLocRowMask) : s;
-    const uint64_t adj = (s & kLocCtx) ? (s >> 60) & 7u : 0;
-    const uint64_t p = op.sa[row];
+    uint64_t row = s, adj = 0;
+    uint32_t rel;
+    if (s & kLocCtx) loc_window(s, row, adj, rel);
+    const uint64_t p = op.sa[row];  // a window's only match is its first row
     rs[j] = kLocStash | (p >= adj ? p - adj : p + n - adj);
   }
 #pragma unroll
@@ -1137,9 +1217,10 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(uint64_t n, uint64_t npat,
     const uint64_t s = kr[j];
     if ((s >> 62) == 1) {  // kLocStash: the one position, read by the search kernel
       op.out_pos[a] = s & 0xFFFFFFFFull;
-    } else if (s & kLocCtx) {  // a context window k characters before the end (k_locate_sa)
-      const uint64_t r0 = s & kLocRowMask, adj = (s >> 60) & 7u;
-      uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+    } else if (s & kLocCtx) {  // a window k characters before the end (k_locate_sa)
+      uint64_t r0, adj;
+      uint32_t rel;
+      loc_window(s, r0, adj, rel);
       for (uint64_t i = 0; i < c; ++i) {
         const uint32_t f = (uint32_t)__ffs(rel) - 1u;
         const uint64_t p = op.sa[r0 + f];
@@ -2529,7 +2610,8 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
     d.lctx = nullptr;
     d.lctx_q = 0;
   }
-  if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY)) d.vsa = nullptr, d.vtext = nullptr;
+  // CS_Q_NO_FULL_SA: locate's phase 2 walks, and a walk takes no verified windows
+  if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA)) d.vsa = nullptr, d.vtext = nullptr;
   if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
   return d;
 }
@@ -2765,8 +2847,9 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa(const uint32_t* __restrict__
     const uint64_t a = offs[q], c = offs[q + 1] - a, s = sp[q];
     if (!c) continue;
     if (s & kLocCtx) {
-      const uint64_t r0 = s & kLocRowMask, adj = (s >> 60) & 7u;
-      uint32_t rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
+      uint64_t r0, adj;
+      uint32_t rel;
+      loc_window(s, r0, adj, rel);
       for (uint64_t j = 0; j < c; ++j) {
         const uint32_t f = (uint32_t)__ffs(rel) - 1u;
         const uint64_t p = sa[r0 + f];

@@ -722,6 +722,65 @@ def test_count_verify_long(built, pkg, name):
     assert [g.count(pats[i]) for i in one] == [want[i] for i in one], name
 
 
+def _locate_two_phase(g, pats, lim, flags):
+    buf, offs = O.pack_patterns(pats)
+    d_buf = torch.from_numpy(buf.copy()).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    npat = len(pats)
+    d_sp = torch.zeros(npat, dtype=torch.int64, device="cuda")
+    d_oo = torch.zeros(npat + 1, dtype=torch.int64, device="cuda")
+    tot = g.locate_ranges_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim, d_sp.data_ptr(),
+                                 d_oo.data_ptr(), flags=flags)
+    d_pos = torch.zeros(max(tot, 1), dtype=torch.int64, device="cuda")
+    g.locate_walk_device(d_sp.data_ptr(), d_oo.data_ptr(), npat, tot, d_pos.data_ptr(), flags=flags)
+    oo = d_oo.cpu().numpy()
+    pos = d_pos[:tot].cpu().numpy()
+    return [pos[oo[q]:oo[q + 1]].tolist() for q in range(npat)]
+
+
+@pytest.mark.parametrize("name", sorted(TEXTS))
+def test_locate_verify_long(built, pkg, name):
+    """locate of long patterns: with the full suffix array and the text in HBM a narrow
+    range finishes by verification (fm_query.hip locate_search: a verified-window record,
+    positions SA[r] - k), without it (CS_Q_NO_VERIFY, CS_Q_NO_FULL_SA) by rank steps — in
+    one call and in two phases, at limits that cut the windows: the oracle's positions in
+    row order (fm_index.cpp:107-157), or its overrun error."""
+    g, o = built(name)
+    t = TEXTS[name]
+    n = len(t)
+    rng = np.random.default_rng(n + 29)
+    pats = _substrings_and_mutants(t, (10, 16, 24, 40, 64, 130, 300), 5, n + 13)
+    tt = t * 3
+    for _ in range(8):  # windows through the end of the text
+        a = int(rng.integers(1, min(n, 40) + 1))
+        b = int(rng.integers(0, min(n, 40) + 1))
+        pats.append(t[n - a:] + t[:b])
+    for m in (n - 1, n + 1):
+        if m > 0:
+            i = int(rng.integers(0, n))
+            pats.append(tt[i:i + m])
+    pats = [p for p in pats if p]
+    for lim in (1, 2, 100000):
+        try:
+            want = [o.locate(p, limit=lim) for p in pats]
+        except RuntimeError:
+            want = None  # the reference's overrun (no unique terminator)
+        for f in (0, 16, 4):
+            try:
+                got = _locate_two_phase(g, pats, lim, f)
+            except RuntimeError as e:
+                assert want is None and str(e) == "locate: LF walk exceeded text length", (name, lim, f)
+                continue
+            assert want is not None, (name, lim, f)
+            for q, p in enumerate(pats):
+                assert got[q] == want[q], (name, lim, f, p)
+        if want is None:
+            continue
+        offs, pos = g.locate_batch(pats, limit=lim)
+        for q, p in enumerate(pats):
+            assert pos[offs[q]:offs[q + 1]].tolist() == want[q], (name, lim, p)
+
+
 @pytest.mark.parametrize("name", sorted(TEXTS))
 def test_query_flags_locate(built, pkg, name):
     """locate with phase 2 forced onto the LF walk (CS_Q_NO_FULL_SA) and onto the
