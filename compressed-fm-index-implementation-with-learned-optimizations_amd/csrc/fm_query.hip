@@ -603,7 +603,7 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
 // dependent rounds of reads instead of k rank steps (a 64-mer: 49 steps).  The result is
 // the count the steps would give, exactly.
 constexpr uint32_t kVerifyRows = 8;
-constexpr uint32_t kVerifyWords = 4;  // text words compared per round (32 characters)
+constexpr uint32_t kVerifyWords = 8;  // text words compared per round (64 characters)
 
 // bytes P[j, j + 8) as a little-endian uint64, from realigned dword loads that touch only
 // dwords holding bytes of P[0, k) (bytes at or past k: unspecified)
