@@ -249,18 +249,48 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
                               hipStream_t st, PhaseLog& plog, DevBuf* sa_pending = nullptr);
 
 // Text-position sample stride (inverse-SA samples for extract; walk-line marks and
-// their position samples for locate): an eighth of the SSA stride, half for wide
-// indexes (n >= 2^32, u64 samples: their HBM goes to the left contexts first), at
-// least 1.  A locate walk then averages about pstride / 2 steps instead of
+// their position samples for locate): an eighth of the SSA stride, a quarter for wide
+// indexes (n >= 2^32, u64 samples: their HBM goes to the left contexts and context
+// records first; their inverse-SA samples are thinned to every second one after the
+// walk lines are built, thin_isa), at least 1.  A locate walk then averages about pstride / 2 steps instead of
 // stride / 2, an extract (stride - pstride) / 2 fewer; the reference's row-sampled
 // SSA (fm_index.cpp:57-66) is kept as is.  The samples cost 2 x sample bytes x
 // n / pstride (C4: 4 GB, C5: 32 GB).  C4 walk of 12.5 M positions: 1.8 ms at
 // pstride 8, 1.3 ms at 4 (profiles/r01/locate_phases_c4_p*.json).  CS_FM_PSTRIDE
 // overrides.
 static uint32_t position_stride(uint32_t stride, bool wide) {
-  uint32_t p = stride / (wide ? 2u : 8u);
+  uint32_t p = stride / (wide ? 4u : 8u);
   if (const char* e = std::getenv("CS_FM_PSTRIDE")) p = (uint32_t)std::atoi(e);
   return p ? p : 1u;
+}
+
+template <class S>
+__global__ void k_thin(const S* __restrict__ in, uint64_t nout, uint32_t f, S* __restrict__ out) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nout; k += gs) out[k] = in[k * f];
+}
+
+// Keep every f-th inverse-SA sample (stride xstride = f pstride): extract then starts
+// at most f pstride positions past its end instead of pstride; the walk marks and their
+// position samples (built from the full set) stay at pstride.
+static cs_status thin_isa(cs_fm_index* h, uint32_t f, hipStream_t st) {
+  const uint64_t xs = (uint64_t)h->pstride * f;
+  const uint64_t nout = (h->n + xs - 1) / xs;
+  void* out = nullptr;
+  FMX_HIP(hipMalloc(&out, (nout ? nout : 1) * h->sample_bytes()));
+  if (h->wide)
+    k_thin<uint64_t><<<grid_for(nout, kBlk, 16384), kBlk, 0, st>>>(
+        static_cast<const uint64_t*>(h->d_isa), nout, f, static_cast<uint64_t*>(out));
+  else
+    k_thin<uint32_t><<<grid_for(nout, kBlk, 16384), kBlk, 0, st>>>(
+        static_cast<const uint32_t*>(h->d_isa), nout, f, static_cast<uint32_t*>(out));
+  FMX_HIP(hipGetLastError());
+  FMX_HIP(hipStreamSynchronize(st));
+  FMX_HIP(hipFree(h->d_isa));
+  h->d_isa = out;
+  h->nisa = nout;
+  h->xstride = (uint32_t)xs;
+  return CS_OK;
 }
 
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
@@ -311,6 +341,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   FMX_HIP(hipMalloc(&h->d_ssa, (h->nsamples ? h->nsamples : 1) * h->sample_bytes()));
   h->pstride = position_stride(stride, h->wide);
   h->nisa = (n + h->pstride - 1) / h->pstride;  // text positions 0, pstride, ... < n
+  h->xstride = h->pstride;
   FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
   DevBuf sa_pending;  // with an HBM budget: the full SA, kept at the end if it still fits
   bool bucketed = n >= (1ull << 32);
@@ -431,6 +462,10 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   }
   FMX_HIP(hipStreamSynchronize(st));
   bwt.release();
+  if (h->wide && h->nisa) {  // the walk marks are built: extract keeps every second sample
+    cs_status ts = thin_isa(h, 2, st);
+    if (ts != CS_OK) return ts;
+  }
   plog.mark("wavelet levels");
 
   // --- node table from the histogram ---
@@ -514,7 +549,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   if (sa_pending && sa_pending->p) {
     // budget builds: the full suffix array replaces the walk lines and their position
     // samples when the index still fits its budget with it
-    const uint64_t walk_b = (h->d_walk ? h->nwalk * 32 : 0) + (h->d_wssa ? h->nisa * h->sample_bytes() : 0);
+    const uint64_t walk_b = (h->d_walk ? h->nwalk * 32 : 0) + (h->d_wssa ? h->nwssa * h->sample_bytes() : 0);
     if (index_hbm_bytes(h) + n * 4 <= h->hbm_budget + walk_b) {
       if (h->d_walk) FMX_HIP(hipFree(h->d_walk));
       if (h->d_wssa) FMX_HIP(hipFree(h->d_wssa));
@@ -553,7 +588,7 @@ cs_status build_index_from_bwt(const uint8_t* bwt_host, uint64_t n, const uint32
   }
   h->n = n;
   h->stride = stride;
-  h->pstride = stride;
+  h->pstride = h->xstride = stride;
   h->wide = false;
   h->nsamples = nsamples;
   h->nisa = 0;

@@ -726,6 +726,7 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
     FMX_HIP(hipGetLastError());
   }
   if (pos_marks) {
+    h->nwssa = h->nisa;
     FMX_HIP(hipMalloc(&h->d_wssa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
     if (h->wide)
       k_walk_samples<W, uint64_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(

@@ -105,7 +105,7 @@ struct DevIndex {
   // smallest last symbol: lf_exact).
   const void* isa;
   uint64_t nisa;
-  uint32_t pstride;      // their text-position stride (finer than the SSA's; extract, walk marks)
+  uint32_t pstride;      // their text-position stride (finer than the SSA's; cs_fm_index::xstride)
   uint32_t lf_exact;
   // Walk lines and the samples they index (WalkLine above); null when absent.
   const void* walk;

@@ -34,7 +34,9 @@ struct cs_fm_index {
   void* d_sa = nullptr;               // full suffix array, u32 (lf_exact prefix-doubling builds)
   void* d_isa = nullptr;              // inverse-SA samples (extract, walk-line marks)
   uint64_t nisa = 0;
-  uint32_t pstride = 32;              // their text-position stride (position_stride())
+  uint32_t pstride = 32;              // walk-mark text-position stride (position_stride())
+  uint32_t xstride = 32;              // the inverse-SA samples' stride (pstride; 2 pstride wide)
+  uint64_t nwssa = 0;                 // walk position samples (n / pstride with position marks)
   bool lf_exact = false;              // unique smallest last symbol: LF inverts SA
   void* d_walk = nullptr;             // walk lines (occurrence engine; WalkLine / WalkLineW)
   uint64_t nwalk = 0;
@@ -112,7 +114,7 @@ struct cs_fm_index {
     d.ptab_rec = ptab_rec;
     d.isa = d_isa;
     d.nisa = nisa;
-    d.pstride = pstride;
+    d.pstride = xstride;  // device code reads it only with the inverse-SA samples (extract)
     d.lf_exact = lf_exact ? 1u : 0u;
     d.walk = d_walk;
     d.wssa = d_wssa ? d_wssa : d_ssa;
