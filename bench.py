@@ -73,7 +73,8 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
              "count_m64", "count_m64_steps", "count_m150", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
-             "locate_m64", "locate_m64_steps", "host_batch", "extract"]
+             "locate_m64", "locate_m64_steps", "count_stream", "count_stream_packed", "host_batch",
+             "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
 # the learned occurrence lines (the reference's learned occ, as int16
@@ -388,6 +389,89 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
                          "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}
 
 
+def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False):
+    """count of patterns streamed from host memory (BASELINE C5: "1 B streamed 20-mer
+    count()", 125 M per GPU): `chunks` batches of W.B patterns from page-locked host
+    buffers — the caller's, reused for every chunk — through two device slots: the H2D
+    copy of chunk i+1 on a copy stream overlaps the count of chunk i on the launch stream
+    and the D2H copy of chunk i-1's counts on a third stream (events order the slots).
+    PCIe-bound: reported against a plain H2D copy of the same bytes, timed alone."""
+    B, m = W.B, W.m
+    comp = torch.cuda.current_stream()
+    cin, cout = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    if packed:  # 2-bit DNA, 8 B per pattern, u32 counts
+        lut = torch.zeros(256, dtype=torch.int64, device=dev)
+        lut[torch.tensor(list(b"ACGT"), device=dev)] = torch.arange(4, device=dev)
+        codes = lut[W.pats.view(B, m).long()]
+        hin = [((codes << (2 * torch.arange(m, device=dev))).sum(dim=1)).cpu().pin_memory()]
+        del codes
+        cdt, cw = torch.int32, 4
+    else:  # the reference's byte strings with u64 offsets, u64 counts
+        hin = [W.pats.cpu().pin_memory(), W.offs.cpu().pin_memory()]
+        cdt, cw = torch.int64, 8
+    dslot = [[torch.empty_like(x, device=dev) for x in hin] for _ in range(2)]
+    dout = [torch.empty(B, dtype=cdt, device=dev) for _ in range(2)]
+    hout = [torch.empty(B, dtype=cdt).pin_memory() for _ in range(2)]
+    in_bytes = sum(x.numel() * x.element_size() for x in hin)
+
+    def launch(s, st):
+        if packed:
+            idx.count_packed_device(dslot[s][0].data_ptr(), m, B, dout[s].data_ptr(), width=4, stream=st)
+        else:
+            idx.count_batch_device(dslot[s][0].data_ptr(), dslot[s][1].data_ptr(), B, dout[s].data_ptr(), st)
+
+    def run(nchunks):
+        loaded = [torch.cuda.Event() for _ in range(2)]
+        counted = [torch.cuda.Event() for _ in range(2)]
+        drained = [None, None]
+        for i in range(nchunks):
+            s = i % 2
+            with torch.cuda.stream(cin):
+                if i >= 2:
+                    cin.wait_event(counted[s])  # the slot's previous count has read its input
+                for d, h in zip(dslot[s], hin):
+                    d.copy_(h, non_blocking=True)
+                loaded[s].record(cin)
+            comp.wait_event(loaded[s])
+            if drained[s] is not None:
+                comp.wait_event(drained[s])  # the slot's previous counts are back on the host
+            launch(s, comp.cuda_stream)
+            counted[s].record(comp)
+            with torch.cuda.stream(cout):
+                cout.wait_event(counted[s])
+                hout[s].copy_(dout[s], non_blocking=True)
+                drained[s] = torch.cuda.Event()
+                drained[s].record(cout)
+        torch.cuda.synchronize()
+
+    run(2)  # warm-up
+    walls = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(chunks)
+        walls.append(time.perf_counter() - t0)
+    tl = min(walls)
+    # the PCIe ceiling: the same H2D bytes alone, one chunk's buffers per copy
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(chunks):
+        for d, h in zip(dslot[i % 2], hin):
+            d.copy_(h, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d_s = time.perf_counter() - t0
+    got = hout[(chunks - 1) % 2].numpy().astype(np.int64)
+    out = {"what": what, "patterns": B * chunks, "chunks": chunks, "chunk_patterns": B, "m": m,
+           "seconds": tl, "patterns_per_s": B * chunks / tl,
+           "h2d_bytes_per_pattern": in_bytes / B, "d2h_bytes_per_pattern": cw,
+           "h2d_GBs": in_bytes * chunks / tl / 1e9,
+           "pcie_h2d_alone_GBs": in_bytes * chunks / h2d_s / 1e9,
+           "frac_of_h2d_alone": h2d_s / tl,
+           "matches_headline": None if ref_counts is None else bool(np.array_equal(got, ref_counts))}
+    del dslot, dout, hout, hin
+    return out
+
+
 def build_index(pkg, text, N, stride, dev_index, env=None):
     """Build with the engine's environment switches `env` set for the build ("" = unset)."""
     saved = {}
@@ -459,6 +543,9 @@ def main():
                     help="patterns timed through the oracle's fast (precomputed) count, all threads")
     ap.add_argument("--extract-batch", type=int, default=1_000_000,
                     help="random 20-byte extracts timed on the device (N=1 only; 0 = skip)")
+    ap.add_argument("--stream-chunks", type=int, default=10,
+                    help="count_stream legs: chunks of --batch patterns streamed from host memory "
+                         "(10 x 12.5 M = C5's 1 B patterns over 8 GPUs, per GPU)")
     ap.add_argument("--replicate", default="build", choices=["build", "broadcast"],
                     help="N > 1: every rank builds its replica, or rank 0 builds and broadcasts "
                          "the device image (RCCL)")
@@ -827,6 +914,15 @@ def main():
                             "positions from the full suffix array" % mm, idx, info, wl, Wm, text, 16,
                             dev, sh, reps=2)
                     del Wm
+            for name, pk in (("count_stream", False), ("count_stream_packed", True)):
+                if name in legs and (not pk or (args.kind == "dna" and m <= 32)):
+                    lg[name] = stream_leg(
+                        name, "count of %d x %d M patterns streamed from page-locked host memory "
+                        "(%s), H2D of the next chunk overlapped with the count and the D2H of the "
+                        "previous counts" % (args.stream_chunks, B // 1000000,
+                                             "2-bit packed DNA, u32 counts" if pk else
+                                             "byte strings + u64 offsets, u64 counts"),
+                        idx, W, dev, sh, counts, chunks=args.stream_chunks, packed=pk)
             if "host_batch" in legs and counts is not None:
                 # the batch handed over in host memory (PCIe in and out inside the call)
                 hbuf = W.pats.cpu().numpy()
