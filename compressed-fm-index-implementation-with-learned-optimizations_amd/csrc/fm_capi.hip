@@ -5,6 +5,8 @@
 #include <cstdlib>
 #include <map>
 #include <cstring>
+#include <memory>
+#include <vector>
 #include <mutex>
 #include <new>
 #include <string>
@@ -210,6 +212,87 @@ struct HostPin {
     pin_registry().release(a);
   }
 };
+
+// A large caller buffer page-locked piece by piece as a chunked call reaches it: the
+// buffer's inner pages are cut into page-aligned pieces, each registered (PinRegistry) just
+// before its first copy is queued — while the stream still runs the earlier chunks — so
+// spans inside held pieces are asynchronous DMA copies; the rest (the partial first and
+// last pages, pieces the registry cannot hold) are HostPin's plain or bounced copies.
+struct PiecewisePin {
+  static constexpr uint64_t kPiece = 32ull << 20;
+  HostPin any;  // plain / bounce copies
+  uintptr_t A = 0, E = 0;  // inner pages [A, E)
+  std::vector<int8_t> held;  // per piece: 0 not yet, 1 held, -1 not held
+  hipStream_t st = nullptr;
+  PiecewisePin(const PiecewisePin&) = delete;
+  PiecewisePin& operator=(const PiecewisePin&) = delete;
+  PiecewisePin(const cs_fm_index* h, const void* p, uint64_t bytes, hipStream_t s) : st(s) {
+    any.h = h;
+    if (bytes < HostPin::kMinBytes) return;
+    A = (reinterpret_cast<uintptr_t>(p) + 4095) & ~uintptr_t(4095);
+    E = (reinterpret_cast<uintptr_t>(p) + bytes) & ~uintptr_t(4095);
+    if (E <= A) A = E = 0;
+    else held.assign((E - A + kPiece - 1) / kPiece, 0);
+  }
+  // whether the host span [x, y) (inside one piece) may be DMA'd asynchronously
+  bool pinned(uintptr_t x) {
+    const uint64_t k = (x - A) / kPiece;
+    if (!held[k]) {
+      const uintptr_t pa = A + k * kPiece, pe = pa + kPiece < E ? pa + kPiece : E;
+      held[k] = pin_registry().acquire(pa, pe) ? 1 : -1;
+    }
+    return held[k] == 1;
+  }
+  // host <-> device copy whose host side is [host, host + n) of this buffer; spans that
+  // are not DMA-able go to `later` (D2H, run after the stream has drained) or are copied
+  // now (H2D)
+  hipError_t copy(void* dst, const void* src, uint64_t n, bool h2d,
+                  std::vector<std::pair<std::pair<void*, const void*>, uint64_t>>* later = nullptr) {
+    const uintptr_t h0 = reinterpret_cast<uintptr_t>(h2d ? src : dst);
+    for (uintptr_t x = h0; x < h0 + n;) {
+      uintptr_t y = h0 + n;
+      bool dma = false;
+      if (x < A) {
+        y = y < A ? y : A;
+      } else if (x < E) {
+        const uintptr_t pe = A + ((x - A) / kPiece + 1) * kPiece;
+        y = y < pe ? y : pe;
+        y = y < E ? y : E;
+        dma = pinned(x);
+      }
+      void* d = static_cast<uint8_t*>(dst) + (x - h0);
+      const void* q = static_cast<const uint8_t*>(src) + (x - h0);
+      hipError_t r = hipSuccess;
+      if (dma)
+        r = hipMemcpyAsync(d, q, y - x, h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost, st);
+      else if (!h2d && later)
+        later->push_back({{d, q}, y - x});
+      else
+        r = any.plain(d, q, y - x, h2d, st);
+      if (r != hipSuccess) return r;
+      x = y;
+    }
+    return hipSuccess;
+  }
+  ~PiecewisePin() {
+    bool any_held = false;
+    for (int8_t v : held) any_held |= v == 1;
+    if (!any_held) return;
+    (void)hipStreamSynchronize(st);  // no copy may still read the pages
+    for (size_t k = 0; k < held.size(); ++k)
+      if (held[k] == 1) pin_registry().release(A + k * kPiece);
+  }
+};
+
+// chunk of a large host batch (cs_fm_count_batch); tuning hook CS_FM_HOST_CHUNK (patterns,
+// read per call)
+uint64_t host_chunk_patterns() {
+  if (const char* e = std::getenv("CS_FM_HOST_CHUNK")) {
+    const long long v = std::atoll(e);
+    if (v > 0) return (uint64_t)v;
+  }
+  return 2ull << 20;
+}
 
 // Stage a host pattern batch into HBM.
 struct StagedBatch {
@@ -608,7 +691,10 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
-  if ((s = check_offsets(offs, npat)) != CS_OK) return s;
+  const uint64_t chunk = host_chunk_patterns();
+  // a chunked batch checks each chunk's offsets just before queuing it (below), while
+  // the stream runs the chunks before it
+  if (npat <= chunk && (s = check_offsets(offs, npat)) != CS_OK) return s;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t bytes = offs[npat] - offs[0];
   const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
@@ -667,16 +753,80 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     std::memcpy(out_counts, hp + o_out, npat * 8);
     return CS_OK;
   }
-  HostPin pin_out;
-  StagedBatch b;
-  s = b.load(h, pats, offs, npat, st);
-  if (s != CS_OK) return s;
-  StreamBuf d_out;
+  if (npat <= chunk) {
+    HostPin pin_out;
+    StagedBatch b;
+    s = b.load(h, pats, offs, npat, st);
+    if (s != CS_OK) return s;
+    StreamBuf d_out;
+    FMX_HIP(d_out.alloc(npat * 8, st));
+    pin_out.pin(h, out_counts, npat * 8, st);
+    s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
+    if (s != CS_OK) return s;
+    FMX_HIP(pin_out.copy(out_counts, d_out.p, npat * 8, false, st));
+    FMX_HIP(hipStreamSynchronize(st));
+    return CS_OK;
+  }
+  // A large batch in chunks of `chunk` patterns, all queued on the stream: the caller's
+  // pages of chunk i + 1 (patterns, offsets, counts) are page-locked on the host while
+  // chunk i's copies and count run (PiecewisePin), instead of the whole batch's before
+  // the first copy (C4, 12.5 M 20-mers: registration was about half of the call).  A
+  // chunk's offsets are copied as they are; its count reads the patterns through a
+  // pointer shifted back by the chunk's first offset (rounded down to a dword).  Counts stay in HBM until their chunk's
+  // D2H copy (the partial pages of the caller's array after the stream has drained).
+  uint64_t maxb = 0;
+  for (uint64_t q0 = 0; q0 < npat; q0 += chunk) {
+    const uint64_t q1 = q0 + chunk < npat ? q0 + chunk : npat;
+    if (offs[q1] < offs[q0]) {
+      set_error("pattern offsets must be non-decreasing");
+      return CS_ERR_INVALID;
+    }
+    if (offs[q1] - offs[q0] > maxb) maxb = offs[q1] - offs[q0];
+  }
+  StreamBuf d_pats, d_offs, d_out;
+  FMX_HIP(d_pats.alloc(maxb + 20, st));
+  FMX_HIP(d_offs.alloc((chunk + 1) * 8, st));
   FMX_HIP(d_out.alloc(npat * 8, st));
-  pin_out.pin(h, out_counts, npat * 8, st);
-  s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
-  if (s != CS_OK) return s;
-  FMX_HIP(pin_out.copy(out_counts, d_out.p, npat * 8, false, st));
+  std::vector<std::pair<std::pair<void*, const void*>, uint64_t>> later;
+  // the counts go back on a stream of their own, so chunk i's D2H overlaps chunk i + 1's
+  // H2D (one event orders each chunk's D2H after its count)
+  struct Side {
+    hipStream_t s = nullptr;
+    hipEvent_t e = nullptr;
+    ~Side() {
+      if (e) (void)hipEventDestroy(e);
+      if (s) (void)hipStreamDestroy(s);
+    }
+  } side;
+  FMX_HIP(hipStreamCreateWithFlags(&side.s, hipStreamNonBlocking));
+  FMX_HIP(hipEventCreateWithFlags(&side.e, hipEventDisableTiming));
+  {
+    PiecewisePin pp(h, pats + offs[0], bytes, st), po(h, offs, (npat + 1) * 8, st),
+        pc(h, out_counts, npat * 8, side.s);
+    for (uint64_t q0 = 0; q0 < npat; q0 += chunk) {
+      const uint64_t q1 = q0 + chunk < npat ? q0 + chunk : npat, nq = q1 - q0;
+      const uint64_t nb = offs[q1] - offs[q0];
+      if ((s = check_offsets(offs + q0, nq)) != CS_OK) return s;  // earlier chunks: drained below
+      // the kernels read patterns as aligned dwords of a 4-aligned base: the chunk's bytes
+      // land at d_pats + (offs[q0] & 3), read through d_pats - (offs[q0] & ~3)
+      const uint64_t sft = offs[q0] & ~3ull;
+      if (nb) FMX_HIP(pp.copy(d_pats.as<uint8_t>() + (offs[q0] - sft), pats + offs[q0], nb, true));
+      FMX_HIP(po.copy(d_offs.p, offs + q0, (nq + 1) * 8, true));
+      s = launch_count(h, d_pats.as<uint8_t>() - sft, d_offs.as<uint64_t>(), nq,
+                       d_out.as<uint64_t>() + q0, st);
+      if (s != CS_OK) return s;
+      FMX_HIP(hipEventRecord(side.e, st));
+      FMX_HIP(hipStreamWaitEvent(side.s, side.e, 0));
+      FMX_HIP(pc.copy(out_counts + q0, d_out.as<uint64_t>() + q0, nq * 8, false, &later));
+    }
+    FMX_HIP(hipStreamSynchronize(side.s));
+    FMX_HIP(hipStreamSynchronize(st));
+  }  // pages released
+  for (auto& c : later) {
+    HostPin any;
+    any.h = h;
+    FMX_HIP(any.plain(c.first.first, c.first.second, c.second, false, st));
+  }
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
 }

@@ -161,6 +161,39 @@ def test_host_batch_buffers_sharing_pages():
     assert (out >= 1).all()
 
 
+@pytest.mark.parametrize("chunk", [333_333, 1 << 20, 0])
+def test_host_batch_chunked(chunk, monkeypatch):
+    """cs_fm_count_batch over a large ragged host batch in chunks (CS_FM_HOST_CHUNK; 0 = the
+    default 2 M patterns): the caller's pages page-locked piece by piece while earlier chunks
+    run; offsets starting inside the caller's buffer (offs[0] > 0), empty patterns, the
+    counts in the same arena right after the patterns — equal to one unchunked call."""
+    pkg = load_pkg()
+    t = O.gen_dna(6, 300_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    rng = np.random.default_rng(3)
+    npat = 2_500_000
+    lens = rng.integers(0, 33, npat)
+    starts = rng.integers(0, len(t) - 40, npat)
+    cols = np.arange(32)
+    sel = (starts[:, None] + cols[None, :])[cols[None, :] < lens[:, None]]
+    body = np.frombuffer(t, np.uint8)[sel].copy()
+    body[rng.random(body.size) < 0.01] = ord("A")  # mutants: some absent
+    lead = 4099
+    start = (lead + body.size + 7) // 8 * 8
+    arena = np.zeros(start + 8 * npat, np.uint8)
+    arena[lead:lead + body.size] = body
+    out = arena[start:].view(np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + lead
+    if chunk:
+        monkeypatch.setenv("CS_FM_HOST_CHUNK", str(chunk))
+    st = pkg.lib().cs_fm_count_batch(g._h, pkg._u8(arena), pkg._u64(offs), npat, pkg._u64(out), None)
+    assert st == 0, pkg.lib().cs_fm_last_error()
+    monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
+    want = g.count_batch(buf=arena[:lead + body.size].copy(), offs=offs)
+    assert np.array_equal(out, want)
+    assert (out[lens == 0] == len(t)).all() and (out >= 1).mean() > 0.5
+
+
 @pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "records16"])
 def test_import_alloc_commit(engine, monkeypatch):
     """Replication without staging copies: the index's own part addresses
@@ -232,12 +265,16 @@ def test_counts_wire(npat, cap):
             shard.unpack_counts(wire, npat)
 
 
-def test_concurrent_host_batches_share_pages():
+@pytest.mark.parametrize("chunk", [0, 300_000])
+def test_concurrent_host_batches_share_pages(chunk, monkeypatch):
     """Two host threads count batches over the same large buffer at once — one the whole
     buffer, one a window starting inside it (overlapping registrations) — on distinct
-    streams: the pin registry shares or bounces the pages, and both get the
+    streams, in one piece or in chunks whose pages are registered piece by piece
+    (CS_FM_HOST_CHUNK): the pin registry shares or bounces the pages, and both get the
     single-thread answer, repeatedly."""
     import threading
+    if chunk:
+        monkeypatch.setenv("CS_FM_HOST_CHUNK", str(chunk))
     pkg = load_pkg()
     t = O.gen_dna(23, 200_000).tobytes()
     g = pkg.FMIndex.build_from_text(t)
