@@ -73,7 +73,8 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
              "count_m64", "count_m64_steps", "count_m150", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
-             "locate_m64", "locate_m64_steps", "count_stream", "count_stream_packed", "host_batch",
+             "locate_m64", "locate_m64_steps", "count_stream", "count_stream_packed",
+             "count_stream_packed_u8", "host_batch",
              "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
 LEGS_WALK = ["locate_ssa"]
@@ -389,13 +390,15 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
                          "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}
 
 
-def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False):
+def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False, u8=False):
     """count of patterns streamed from host memory (BASELINE C5: "1 B streamed 20-mer
     count()", 125 M per GPU): `chunks` batches of W.B patterns from page-locked host
     buffers — the caller's, reused for every chunk — through two device slots: the H2D
     copy of chunk i+1 on a copy stream overlaps the count of chunk i on the launch stream
     and the D2H copy of chunk i-1's counts on a third stream (events order the slots).
-    PCIe-bound: reported against a plain H2D copy of the same bytes, timed alone."""
+    PCIe-bound: reported against a plain H2D copy of the same bytes, timed alone.  u8
+    (packed only): counts as the exact uint8 form, counts >= 255 as (pattern, count) pairs
+    (a quarter of the u32 D2H bytes)."""
     B, m = W.B, W.m
     comp = torch.cuda.current_stream()
     cin, cout = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
@@ -405,17 +408,25 @@ def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False)
         codes = lut[W.pats.view(B, m).long()]
         hin = [((codes << (2 * torch.arange(m, device=dev))).sum(dim=1)).cpu().pin_memory()]
         del codes
-        cdt, cw = torch.int32, 4
+        cdt, cw = (torch.uint8, 1) if u8 else (torch.int32, 4)
     else:  # the reference's byte strings with u64 offsets, u64 counts
         hin = [W.pats.cpu().pin_memory(), W.offs.cpu().pin_memory()]
         cdt, cw = torch.int64, 8
     dslot = [[torch.empty_like(x, device=dev) for x in hin] for _ in range(2)]
     dout = [torch.empty(B, dtype=cdt, device=dev) for _ in range(2)]
     hout = [torch.empty(B, dtype=cdt).pin_memory() for _ in range(2)]
+    XC = 1 << 16  # pair capacity per chunk (u8 form)
+    dexc = [torch.empty(2 * XC + 1, dtype=torch.int64, device=dev) for _ in range(2)] if u8 else None
+    hexc = [torch.empty(2 * XC + 1, dtype=torch.int64).pin_memory() for _ in range(2)] if u8 else None
     in_bytes = sum(x.numel() * x.element_size() for x in hin)
 
     def launch(s, st):
-        if packed:
+        if u8:  # the pair counter sits after the pairs; zeroed on the launch stream
+            dexc[s][2 * XC:].zero_()
+            idx.count_packed_device(dslot[s][0].data_ptr(), m, B, dout[s].data_ptr(), width=1,
+                                    d_exc=dexc[s].data_ptr(), exc_cap=XC,
+                                    d_exc_n=dexc[s].data_ptr() + 16 * XC, stream=st)
+        elif packed:
             idx.count_packed_device(dslot[s][0].data_ptr(), m, B, dout[s].data_ptr(), width=4, stream=st)
         else:
             idx.count_batch_device(dslot[s][0].data_ptr(), dslot[s][1].data_ptr(), B, dout[s].data_ptr(), st)
@@ -440,6 +451,8 @@ def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False)
             with torch.cuda.stream(cout):
                 cout.wait_event(counted[s])
                 hout[s].copy_(dout[s], non_blocking=True)
+                if u8:
+                    hexc[s].copy_(dexc[s], non_blocking=True)
                 drained[s] = torch.cuda.Event()
                 drained[s].record(cout)
         torch.cuda.synchronize()
@@ -461,14 +474,20 @@ def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False)
     torch.cuda.synchronize()
     h2d_s = time.perf_counter() - t0
     got = hout[(chunks - 1) % 2].numpy().astype(np.int64)
+    if u8:  # exact counts from the uint8 form and its pairs
+        e = hexc[(chunks - 1) % 2].numpy()
+        ne = int(e[2 * XC])
+        assert ne <= XC, "pair area too small"
+        pr = e[:2 * ne].reshape(-1, 2)
+        got[pr[:, 0]] = pr[:, 1]
     out = {"what": what, "patterns": B * chunks, "chunks": chunks, "chunk_patterns": B, "m": m,
            "seconds": tl, "patterns_per_s": B * chunks / tl,
-           "h2d_bytes_per_pattern": in_bytes / B, "d2h_bytes_per_pattern": cw,
+           "h2d_bytes_per_pattern": in_bytes / B, "d2h_bytes_per_pattern": cw + (16 * XC + 8) / B * u8,
            "h2d_GBs": in_bytes * chunks / tl / 1e9,
            "pcie_h2d_alone_GBs": in_bytes * chunks / h2d_s / 1e9,
            "frac_of_h2d_alone": h2d_s / tl,
            "matches_headline": None if ref_counts is None else bool(np.array_equal(got, ref_counts))}
-    del dslot, dout, hout, hin
+    del dslot, dout, hout, hin, dexc, hexc
     return out
 
 
@@ -914,15 +933,17 @@ def main():
                             "positions from the full suffix array" % mm, idx, info, wl, Wm, text, 16,
                             dev, sh, reps=2)
                     del Wm
-            for name, pk in (("count_stream", False), ("count_stream_packed", True)):
+            for name, pk, u8 in (("count_stream", False, False), ("count_stream_packed", True, False),
+                                 ("count_stream_packed_u8", True, True)):
                 if name in legs and (not pk or (args.kind == "dna" and m <= 32)):
                     lg[name] = stream_leg(
                         name, "count of %d x %d M patterns streamed from page-locked host memory "
                         "(%s), H2D of the next chunk overlapped with the count and the D2H of the "
                         "previous counts" % (args.stream_chunks, B // 1000000,
-                                             "2-bit packed DNA, u32 counts" if pk else
+                                             ("2-bit packed DNA, exact uint8 counts + pairs" if u8 else
+                                              "2-bit packed DNA, u32 counts") if pk else
                                              "byte strings + u64 offsets, u64 counts"),
-                        idx, W, dev, sh, counts, chunks=args.stream_chunks, packed=pk)
+                        idx, W, dev, sh, counts, chunks=args.stream_chunks, packed=pk, u8=u8)
             if "host_batch" in legs and counts is not None:
                 # the batch handed over in host memory (PCIe in and out inside the call)
                 hbuf = W.pats.cpu().numpy()
