@@ -72,7 +72,7 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
-             "count_m64", "count_m64_steps", "count_m150", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
+             "count_m64", "count_m64_steps", "count_m150", "count_m64_long", "count_m150_long", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
              "locate_m64", "locate_m64_steps", "count_stream", "count_stream_packed",
              "count_stream_packed_u8", "host_batch",
              "extract"]
@@ -864,15 +864,18 @@ def main():
             ver = "rank steps until the range is at most 8 rows, then the rows' suffix-array entries " \
                   "and the text before them (verification)" if info.full_sa_bytes and info.text_in_hbm else None
             for name, mm, fl in (("count_m32", 32, 0), ("count_m64", 64, 0), ("count_m64_steps", 64, 16),
-                                 ("count_m150", 150, 0)):
+                                 ("count_m150", 150, 0), ("count_m64_long", 64, 32),
+                                 ("count_m150_long", 150, 32)):
                 if name in legs:
                     Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
                     o8 = torch.empty(B, dtype=torch.int64, device=dev)
                     steps_what = "%d rank steps, then the left contexts" % (mm - info.prefix_k - info.context_q)
                     r, got = count_leg(
                         name, "Q_text %d-mers through the headline index: prefix table, %s%s" % (
-                            mm, ver if ver and not fl else steps_what,
-                            " (CS_Q_NO_VERIFY)" if fl else ""),
+                            mm, ver if ver and not fl & 16 else steps_what,
+                            " (CS_Q_NO_VERIFY)" if fl & 16 else
+                            " (CS_Q_LONG: one pattern per lane, the text compared with look-ahead)"
+                            if fl & 32 else ""),
                         idx, info, wl, Wm,
                         lambda Wm=Wm, o8=o8, fl=fl: idx.count_device_ex(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
                                                                         o8.data_ptr(), flags=fl, stream=sh),

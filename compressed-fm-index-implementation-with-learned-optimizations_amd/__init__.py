@@ -27,7 +27,7 @@ CS_OK, CS_ERR_INVALID, CS_ERR_OOM, CS_ERR_HIP = 0, 1, 2, 3
 CS_ERR_LF_OVERRUN, CS_ERR_SSA_RANGE, CS_ERR_CAPACITY, CS_ERR_UNSUPPORTED, CS_ERR_NO_DEVICE = 4, 5, 6, 7, 8
 
 # query flags (include/cs_fmindex.h CS_Q_*): results unchanged, structures left out
-Q_NO_PREFIX, Q_NO_CONTEXTS, Q_NO_FULL_SA, Q_NO_WALK_LINES, Q_NO_VERIFY = 1, 2, 4, 8, 16
+Q_NO_PREFIX, Q_NO_CONTEXTS, Q_NO_FULL_SA, Q_NO_WALK_LINES, Q_NO_VERIFY, Q_LONG = 1, 2, 4, 8, 16, 32
 
 _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)

@@ -575,7 +575,7 @@ __device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T
   return true;
 }
 
-template <class E, class PT>
+template <class E, class PT, bool kLA = false>
 __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTable& T, PT P,
                                                uint64_t k, uint64_t sp, uint64_t ep,
                                                uint64_t* bytes, const uint32_t* inl);
@@ -583,7 +583,7 @@ __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTab
 // count() of one pattern (fm_index.cpp:84-100), m >= 1, n >= 1: the backward
 // search, finished over the left contexts once at most kCtxQ characters remain and
 // the range is narrow (engines with contexts, when built).
-template <class E, class PT>
+template <class E, class PT, bool kLA = false>
 __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const NodeTable& T,
                                                   PT P, uint64_t m,
                                                   uint64_t* bytes = nullptr) {
@@ -591,7 +591,7 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
   const uint32_t* inl;
   search_start(ix, T, P, m, sp, ep, k, bytes, &inl);
   if (sp >= ep) return 0;
-  return count_rest<E>(ix, T, P, k, sp, ep, bytes, inl);
+  return count_rest<E, PT, kLA>(ix, T, P, k, sp, ep, bytes, inl);
 }
 
 // Verification against the text (lf_exact indexes that keep the full suffix array and the
@@ -649,7 +649,11 @@ __device__ __forceinline__ uint64_t text8(uint64_t w0, uint64_t w1, uint64_t t) 
 // text[q, q + k) == P[0, k), cyclically (positions mod n).  Windows inside [0, n) compare
 // 8 kVerifyWords bytes per round of aligned 8-B loads; a window through the end of the text (a row
 // whose suffix starts fewer than k positions into the text) byte by byte.
-template <class PT>
+// kLA (long patterns, CS_Q_LONG): rounds of kVerifyWordsLA words, the next round's words loaded before
+// this round compares, so a window of R rounds waits for one HBM round trip plus R - 1
+// overlapped ones instead of R.  The extra registers are why it is a separate kernel.
+constexpr uint32_t kVerifyWordsLA = 16;  // 8 and 12 measured: 150-mers 2.47 / 2.56 vs 2.56·10⁹/s
+template <class PT, bool kLA = false>
 __device__ __forceinline__ bool window_eq(const DevIndex& ix, PT P, uint64_t q, uint64_t k,
                                           uint64_t* bytes) {
   const uint64_t n = ix.n;
@@ -664,6 +668,35 @@ __device__ __forceinline__ bool window_eq(const DevIndex& ix, PT P, uint64_t q, 
   }
   const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
   const uint64_t last = (q + k - 1) >> 3;  // the last word holding a byte of the window
+  if constexpr (kLA) {
+    constexpr uint32_t V = kVerifyWordsLA;
+    uint64_t w[V + 1];
+    uint64_t a = q >> 3;
+#pragma unroll
+    for (uint32_t i = 0; i <= V; ++i) w[i] = a + i <= last ? tw[a + i] : 0ull;
+    for (uint64_t j0 = 0; j0 < k; j0 += 8 * V) {
+      const bool more = j0 + 8 * V < k;
+      uint64_t x[V];  // the next round's words past w[V] (which it starts with)
+#pragma unroll
+      for (uint32_t i = 0; i < V; ++i) {
+        const uint64_t b = a + V + 1 + i;
+        x[i] = more && b <= last ? tw[b] : 0ull;
+      }
+      if (bytes) *bytes += 8 * V;
+      uint64_t diff = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < V; ++i) {
+        const uint64_t j = j0 + 8 * i;
+        if (j < k) diff |= (text8(w[i], w[i + 1], q + j) ^ pat8(P, j, k)) & chunk_mask(j, k);
+      }
+      if (diff) return false;
+      w[0] = w[V];
+#pragma unroll
+      for (uint32_t i = 0; i < V; ++i) w[i + 1] = x[i];
+      a += V;
+    }
+    return true;
+  }
   for (uint64_t j0 = 0; j0 < k; j0 += 8 * kVerifyWords) {
     const uint64_t a = (q + j0) >> 3;
     uint64_t w[kVerifyWords + 1];
@@ -721,7 +754,7 @@ __device__ __forceinline__ PackedDna pat_shift(PackedDna P, uint64_t s) {
 // The candidate rows base + i (bit i of mm) — their contexts matched P[k - qf, k), or they
 // passed verify_filter (qf = 0): each one's SA entry, then P[0, k - qf) against the text
 // before its suffix's last qf characters.
-template <class PT>
+template <class PT, bool kLA = false>
 __device__ __forceinline__ uint64_t verify_rows(const DevIndex& ix, PT P, uint64_t k, uint32_t qf,
                                                 uint64_t base, uint32_t mm, uint64_t* bytes) {
   const uint64_t n = ix.n;
@@ -731,14 +764,14 @@ __device__ __forceinline__ uint64_t verify_rows(const DevIndex& ix, PT P, uint64
     mm &= mm - 1;
     const uint64_t p = ix.vsa[base + i];
     if (bytes) *bytes += 32;
-    cnt += window_eq(ix, P, p >= k ? p - k : p + n - k, k - qf, bytes) ? 1u : 0u;
+    cnt += window_eq<PT, kLA>(ix, P, p >= k ? p - k : p + n - k, k - qf, bytes) ? 1u : 0u;
   }
   return cnt;
 }
 
 // The rest of a count() from the range [sp, ep) (non-empty) with P[0..k) still to
 // process (fm_index.cpp:90-98); inl as search_start's.
-template <class E, class PT>
+template <class E, class PT, bool kLA>
 __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTable& T, PT P,
                                                uint64_t k, uint64_t sp, uint64_t ep,
                                                uint64_t* bytes, const uint32_t* inl) {
@@ -775,7 +808,7 @@ __device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTab
       qf = 0;
       cand = true;
     }
-    if (cand) return verify_rows(ix, P, k, qf, base, mm, bytes);
+    if (cand) return verify_rows<PT, kLA>(ix, P, k, qf, base, mm, bytes);
     inl = nullptr;
     --k;
     if (!E::step(ix, T, P[k], sp, ep, bytes)) return 0;
@@ -969,8 +1002,9 @@ __global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix,
 }
 
 // offs == nullptr: patterns of one length fixed_m at stride fixed_m (cs_fm_count_fixed_device);
-// kPacked: pats holds one uint64 per pattern, fixed_m <= 32 2-bit DNA characters (PackedDna)
-template <class E, bool kPacked>
+// kPacked: pats holds one uint64 per pattern, fixed_m <= 32 2-bit DNA characters (PackedDna);
+// kLA: long patterns (launch_count_ex, CS_Q_LONG), the text comparison with look-ahead
+template <class E, bool kPacked, bool kLA = false>
 __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t npat,
                                                 CountOut co, uint64_t fixed_m) {
@@ -989,7 +1023,7 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
     const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
     if (m == 0) res = ix.n;       // fm_index.cpp:80
     else if (ix.n == 0) res = 0;  // :81
-    else res = count_pattern<E>(ix, T, pats + o0, m);
+    else res = count_pattern<E, const uint8_t*, kLA>(ix, T, pats + o0, m);
   }
   store_count<0>(co, q, res);
 }
@@ -1010,6 +1044,8 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
 // only when LF is one n-cycle (lf_exact).
 // kPacked: one uint64 of 2-bit DNA per pattern (PackedDna), fixed_m characters.
 constexpr uint32_t kFastM = 32;
+// fixed-length batches longer than this take the long-pattern kernel (launch_count_ex)
+constexpr uint64_t kLongM = 96;
 
 // bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
 // (u[i >> 2] >> 8 (i & 3)) & 0xFF.  Reads only the dwords holding pattern bytes.
@@ -2690,6 +2726,17 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
       k_count_qctx<2, 4><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
     else
       k_count_qctx<2, 1><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
+    FMX_HIP(hipGetLastError());
+    return CS_OK;
+  }
+  if (h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa && !packed &&
+      ((flags & CS_Q_LONG) || (!d_offs && fixed_m > kLongM))) {
+    // long patterns: one per lane, the whole search in count_pattern, the
+    // text comparison with look-ahead — kept out of the staged kernel, whose registers
+    // the look-ahead would spill on the 20-mer path (C4: 150-mers 2.19 -> 2.56·10⁹/s;
+    // 64-mers 6.52 -> 6.01·10⁹/s, so only fixed lengths over kLongM take it unasked)
+    k_count<OccE, false, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, fixed_m);
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }

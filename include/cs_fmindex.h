@@ -234,12 +234,18 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
  *   CS_Q_NO_FULL_SA    locate phase 2: walk LF to the sampled rows (fm_index.cpp:125-153)
  *                      even when the full suffix array is kept
  *   CS_Q_NO_WALK_LINES locate phase 2: walk the rank structure to the reference's row
- *                      samples (row % ssa_stride == 0) even when walk lines exist */
+ *                      samples (row % ssa_stride == 0) even when walk lines exist
+ *   CS_Q_LONG          count: a hint that the batch holds long patterns (~100
+ *                      characters and more) — one pattern per lane and the text
+ *                      comparison with look-ahead, outside the 20-mer kernel
+ *                      (occurrence-line indexes that verify; implied by a fixed-length
+ *                      batch with m > 96).  C4: 150-mers +17 %, 64-mers -8 %. */
 #define CS_Q_NO_PREFIX 1u
 #define CS_Q_NO_CONTEXTS 2u
 #define CS_Q_NO_FULL_SA 4u
 #define CS_Q_NO_WALK_LINES 8u
 #define CS_Q_NO_VERIFY 16u
+#define CS_Q_LONG 32u
 
 /* Where a batch count writes.  width 8: uint64 counts (the reference's return type,
  * fm_index.hpp:26).  width 4: uint32, exact while n < 2^32 (CS_ERR_INVALID otherwise).

@@ -714,9 +714,28 @@ def test_count_verify_long(built, pkg, name):
             pats.append(tt[i:i + m])
     pats = [p for p in pats if p]
     want = [o.count(p) for p in pats]
-    for f in (0, 16):
+    for f in (0, 16, 32, 48):  # 32: CS_Q_LONG (one pattern per lane, text look-ahead)
         got, _, _ = _count_ex(g, pats, flags=f)
         assert got.tolist() == want, (name, f)
+    # CS_Q_LONG at the narrow widths: uint32, and uint8 with the exception pairs
+    got4, _, _ = _count_ex(g, pats, width=4, flags=32)
+    assert got4.tolist() == want, name
+    got1, pairs, ne = _count_ex(g, pats, width=1, flags=32)
+    assert ne == sum(1 for c in want if c >= 255), name
+    got1[pairs[:, 0].astype(np.int64)] = pairs[:, 1].astype(np.uint64)
+    assert got1.tolist() == want, name
+    # fixed-length batches (cs_fm_count_fixed_device, no offsets array): 33 and 64 through
+    # the staged kernel's general search, 130 through the long-pattern kernel (m > 96)
+    for m in (33, 64, 130):
+        if n < m:
+            continue
+        fx = _substrings_and_mutants(t, (m,), 20, n + m)
+        fx = [p for p in fx if len(p) == m]
+        d = torch.from_numpy(np.frombuffer(b"".join(fx), np.uint8).copy()).cuda()
+        out = torch.zeros(len(fx), dtype=torch.int64, device="cuda")
+        g.count_fixed_device(d.data_ptr(), m, len(fx), out.data_ptr())
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().astype(np.uint64).tolist() == [o.count(p) for p in fx], (name, m)
     # single patterns (k_count_one: the pattern in the kernel arguments, up to 128 bytes)
     one = [i for i, p in enumerate(pats) if len(p) <= 128][::3]
     assert [g.count(pats[i]) for i in one] == [want[i] for i in one], name
