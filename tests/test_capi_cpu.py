@@ -92,3 +92,13 @@ def test_build_params_defaults_match_reference():
     c = pkg.cs_build_params()
     pkg.lib().cs_default_build_params(c)
     assert (c.S, c.s, c.ssa_stride, c.eps) == (512, 64, 32, 1.0)
+
+
+def test_query_flags_mirror_header():
+    """The Python mirror's Q_* constants equal the header's CS_Q_* query flags."""
+    pkg = load_pkg()
+    src = open(os.path.join(ROOT, "include", "cs_fmindex.h")).read()
+    flags = {k: int(v) for k, v in re.findall(r"#define CS_(Q_[A-Z_]+) (\d+)u", src)}
+    assert "Q_LONG" in flags and len(flags) >= 6
+    for k, v in flags.items():
+        assert getattr(pkg, k) == v, k
