@@ -52,13 +52,19 @@ cs_status check_handle(const cs_fm_index* h, DeviceScope& ds) {
 }
 
 // Host batches: offsets must be non-decreasing (pattern q = [offs[q], offs[q+1])),
-// else a kernel would read past the staged bytes.
-cs_status check_offsets(const uint64_t* offs, uint64_t npat) {
-  for (uint64_t q = 0; q < npat; ++q)
+// else a kernel would read past the staged bytes.  *long_flag (when asked): CS_Q_LONG
+// if every pattern is longer than kLongPatternM (the long-pattern count kernel), else 0.
+cs_status check_offsets(const uint64_t* offs, uint64_t npat, uint32_t* long_flag = nullptr) {
+  uint64_t mn = ~0ull;
+  for (uint64_t q = 0; q < npat; ++q) {
     if (offs[q + 1] < offs[q]) {
       set_error("pattern offsets must be non-decreasing");
       return CS_ERR_INVALID;
     }
+    const uint64_t m = offs[q + 1] - offs[q];
+    mn = m < mn ? m : mn;
+  }
+  if (long_flag) *long_flag = npat && mn > kLongPatternM ? CS_Q_LONG : 0u;
   return CS_OK;
 }
 
@@ -694,7 +700,8 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
   const uint64_t chunk = host_chunk_patterns();
   // a chunked batch checks each chunk's offsets just before queuing it (below), while
   // the stream runs the chunks before it
-  if (npat <= chunk && (s = check_offsets(offs, npat)) != CS_OK) return s;
+  uint32_t lf = 0;  // CS_Q_LONG for a batch of long patterns only
+  if (npat <= chunk && (s = check_offsets(offs, npat, &lf)) != CS_OK) return s;
   hipStream_t st = (hipStream_t)stream;
   const uint64_t bytes = offs[npat] - offs[0];
   const uint64_t o_out = (npat + 1) * 8, o_pats = o_out + npat * 8;
@@ -746,7 +753,7 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     FMX_HIP(hipMemcpyAsync(dp, hp, o_out, hipMemcpyHostToDevice, st));
     if (bytes) FMX_HIP(hipMemcpyAsync(dp + o_pats, hp + o_pats, bytes, hipMemcpyHostToDevice, st));
     s = launch_count(h, dp + o_pats, reinterpret_cast<const uint64_t*>(dp), npat,
-                     reinterpret_cast<uint64_t*>(dp + o_out), st);
+                     reinterpret_cast<uint64_t*>(dp + o_out), st, 0, lf);
     if (s != CS_OK) return s;
     FMX_HIP(hipMemcpyAsync(hp + o_out, dp + o_out, npat * 8, hipMemcpyDeviceToHost, st));
     FMX_HIP(hipStreamSynchronize(st));
@@ -761,7 +768,8 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     StreamBuf d_out;
     FMX_HIP(d_out.alloc(npat * 8, st));
     pin_out.pin(h, out_counts, npat * 8, st);
-    s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st);
+    s = launch_count(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, d_out.as<uint64_t>(), st,
+                     0, lf);
     if (s != CS_OK) return s;
     FMX_HIP(pin_out.copy(out_counts, d_out.p, npat * 8, false, st));
     FMX_HIP(hipStreamSynchronize(st));
@@ -806,14 +814,15 @@ cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uin
     for (uint64_t q0 = 0; q0 < npat; q0 += chunk) {
       const uint64_t q1 = q0 + chunk < npat ? q0 + chunk : npat, nq = q1 - q0;
       const uint64_t nb = offs[q1] - offs[q0];
-      if ((s = check_offsets(offs + q0, nq)) != CS_OK) return s;  // earlier chunks: drained below
+      uint32_t clf = 0;  // per chunk: CS_Q_LONG when all its patterns are long
+      if ((s = check_offsets(offs + q0, nq, &clf)) != CS_OK) return s;  // earlier chunks: drained below
       // the kernels read patterns as aligned dwords of a 4-aligned base: the chunk's bytes
       // land at d_pats + (offs[q0] & 3), read through d_pats - (offs[q0] & ~3)
       const uint64_t sft = offs[q0] & ~3ull;
       if (nb) FMX_HIP(pp.copy(d_pats.as<uint8_t>() + (offs[q0] - sft), pats + offs[q0], nb, true));
       FMX_HIP(po.copy(d_offs.p, offs + q0, (nq + 1) * 8, true));
       s = launch_count(h, d_pats.as<uint8_t>() - sft, d_offs.as<uint64_t>(), nq,
-                       d_out.as<uint64_t>() + q0, st);
+                       d_out.as<uint64_t>() + q0, st, 0, clf);
       if (s != CS_OK) return s;
       FMX_HIP(hipEventRecord(side.e, st));
       FMX_HIP(hipStreamWaitEvent(side.s, side.e, 0));

@@ -169,9 +169,14 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
                              hipStream_t st);
 
 // Query launches (fm_query.hip).
-// d_offs == nullptr: npat patterns of length fixed_m at stride fixed_m
+// d_offs == nullptr: npat patterns of length fixed_m at stride fixed_m; flags CS_Q_*
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                       uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m = 0);
+                       uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m = 0,
+                       uint32_t flags = 0);
+// A batch whose patterns are all longer than this takes the long-pattern count kernel
+// (CS_Q_LONG): fixed-length device batches and host batches, whose lengths are known
+// before the launch.
+constexpr uint64_t kLongPatternM = 96;
 // the general form: output width (fmx::CountOut), query flags (CS_Q_*), packed DNA input
 // (d_pats = one uint64 per pattern of fixed_m 2-bit characters)
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,

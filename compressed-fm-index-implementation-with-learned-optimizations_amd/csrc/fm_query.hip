@@ -1044,8 +1044,6 @@ __global__ __launch_bounds__(kBlk) void k_count(DevIndex ix, const uint8_t* __re
 // only when LF is one n-cycle (lf_exact).
 // kPacked: one uint64 of 2-bit DNA per pattern (PackedDna), fixed_m characters.
 constexpr uint32_t kFastM = 32;
-// fixed-length batches longer than this take the long-pattern kernel (launch_count_ex)
-constexpr uint64_t kLongM = 96;
 
 // bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
 // (u[i >> 2] >> 8 (i & 3)) & 0xFF.  Reads only the dwords holding pattern bytes.
@@ -2653,9 +2651,10 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
 }
 
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                       uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m) {
+                       uint64_t npat, uint64_t* d_out, hipStream_t st, uint64_t fixed_m,
+                       uint32_t flags) {
   CountOut co{d_out, nullptr, nullptr, 0, 8};
-  return launch_count_ex(h, d_pats, d_offs, npat, co, 0, st, fixed_m, false);
+  return launch_count_ex(h, d_pats, d_offs, npat, co, flags, st, fixed_m, false);
 }
 
 // tuning hook CS_FM_COUNT_NOBAR (read per call): 1 = the staged kernel's general search
@@ -2730,11 +2729,12 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
     return CS_OK;
   }
   if (h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa && !packed &&
-      ((flags & CS_Q_LONG) || (!d_offs && fixed_m > kLongM))) {
+      ((flags & CS_Q_LONG) || (!d_offs && fixed_m > kLongPatternM))) {
     // long patterns: one per lane, the whole search in count_pattern, the
     // text comparison with look-ahead — kept out of the staged kernel, whose registers
     // the look-ahead would spill on the 20-mer path (C4: 150-mers 2.19 -> 2.56·10⁹/s;
-    // 64-mers 6.52 -> 6.01·10⁹/s, so only fixed lengths over kLongM take it unasked)
+    // 64-mers 6.52 -> 6.01·10⁹/s, so only batches known to be longer than kLongPatternM
+    // take it unasked)
     k_count<OccE, false, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, fixed_m);
     FMX_HIP(hipGetLastError());

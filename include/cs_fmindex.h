@@ -239,7 +239,9 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
  *                      characters and more) — one pattern per lane and the text
  *                      comparison with look-ahead, outside the 20-mer kernel
  *                      (occurrence-line indexes that verify; implied by a fixed-length
- *                      batch with m > 96).  C4: 150-mers +17 %, 64-mers -8 %. */
+ *                      batch with m > 96 and by a host batch, cs_fm_count_batch, whose
+ *                      patterns are all longer than 96).  C4: 150-mers +17 %, 64-mers
+ *                      -8 %. */
 #define CS_Q_NO_PREFIX 1u
 #define CS_Q_NO_CONTEXTS 2u
 #define CS_Q_NO_FULL_SA 4u

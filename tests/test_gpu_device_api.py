@@ -194,6 +194,32 @@ def test_host_batch_chunked(chunk, monkeypatch):
     assert (out[lens == 0] == len(t)).all() and (out >= 1).mean() > 0.5
 
 
+def test_host_batch_long_chunks(monkeypatch):
+    """Host batches of long patterns take the long-pattern count kernel (CS_Q_LONG) chunk
+    by chunk when every pattern of the chunk is longer than 96 characters; the chunk that
+    holds a short pattern stays on the staged kernel — the oracle's counts either way."""
+    pkg = load_pkg()
+    t = O.gen_dna(8, 200_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    ref = O.Index(t, ssa_stride=32)
+    rng = np.random.default_rng(5)
+    pats = []
+    for i in range(3000):
+        m = int(rng.integers(97, 200))
+        s = int(rng.integers(0, len(t) - m - 1))
+        p = bytearray(t[s:s + m])
+        if i % 3 == 0:  # mutants: mostly absent
+            p[int(rng.integers(0, m))] = ord("A")
+        pats.append(bytes(p))
+    pats[2500] = pats[2500][:20]
+    want = [ref.count(p) for p in pats]
+    monkeypatch.setenv("CS_FM_HOST_CHUNK", "1000")
+    assert g.count_batch(pats).tolist() == want
+    monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
+    assert g.count_batch(pats[:2000]).tolist() == want[:2000]
+    assert g.count_batch(pats).tolist() == want
+
+
 @pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "records16"])
 def test_import_alloc_commit(engine, monkeypatch):
     """Replication without staging copies: the index's own part addresses

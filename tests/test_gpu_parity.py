@@ -724,6 +724,12 @@ def test_count_verify_long(built, pkg, name):
     assert ne == sum(1 for c in want if c >= 255), name
     got1[pairs[:, 0].astype(np.int64)] = pairs[:, 1].astype(np.uint64)
     assert got1.tolist() == want, name
+    # host batches (cs_fm_count_batch): all longer than 96 characters -> the long-pattern
+    # kernel unasked; with one short pattern among them -> the staged kernel
+    lp = [i for i, p in enumerate(pats) if len(p) > 96]
+    if lp:
+        assert g.count_batch([pats[i] for i in lp]).tolist() == [want[i] for i in lp], name
+        assert g.count_batch([pats[i] for i in lp] + [b"A"]).tolist()[:-1] == [want[i] for i in lp], name
     # fixed-length batches (cs_fm_count_fixed_device, no offsets array): 33 and 64 through
     # the staged kernel's general search, 130 through the long-pattern kernel (m > 96)
     for m in (33, 64, 130):
