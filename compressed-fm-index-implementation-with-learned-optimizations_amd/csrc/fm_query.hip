@@ -2694,6 +2694,9 @@ void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t
   else if (packed)
     k_count_ctx<OccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                nullptr, fixed_m);
+  else if (lo && count_nobar())
+    k_count_ctx<LOccE, 2, false, false, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
+                                                                       nullptr, fixed_m);
   else if (lo)
     k_count_ctx<LOccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                  nullptr, fixed_m);
