@@ -45,8 +45,6 @@ ENGINE_VARIANTS = {
     "qwm_unstaged": {"CS_FM_ENGINE": "qwm", "CS_FM_QCTX_STAGED": "0"},  # its count one pattern per lane
     "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
     "learned_sb4": {"CS_FM_ENGINE": "learned", "CS_FM_LEARNED_SHIFT": "2"},  # 4-line superblocks
-    # the staged count's general search without the block barrier, on learned lines
-    "learned_nobar": {"CS_FM_ENGINE": "learned", "CS_FM_COUNT_NOBAR": "1"},
     "wavelet": {"CS_FM_ENGINE": "wavelet"},         # binary wavelet matrix for every text
     "wavelet_line64": {"CS_FM_ENGINE": "wavelet", "CS_FM_LINE_BYTES": "64",  # 64-B rank lines,
                        "CS_FM_DEVICE_TEXT": "0"},                             # LF-inversion extract
