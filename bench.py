@@ -137,19 +137,22 @@ def log(rank, *a):
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(wl, leg):
-    """HBM bytes per launch of `leg` on workload `wl` from the committed PMC summaries."""
-    if os.path.exists(PMC_LEGS):
-        e = json.load(open(PMC_LEGS)).get("%s|%s" % (wl, leg))
-        if e:
-            return e.get("hbm_bytes_per_launch")
-    if leg == "count":  # round-1 summary of the headline kernel
-        prof = os.path.join(ROOT, "profiles", "pmc_count.json")
-        if os.path.exists(prof):
-            pj = json.load(open(prof))
-            if pj.get("workload") == wl:
-                return pj.get("hbm_bytes_per_launch")
-    return None
+def pmc_traffic(wl, leg, kern_s):
+    """HBM bytes per launch of `leg` on workload `wl` from the committed PMC summaries
+    (profiles/pmc_legs.json), -> {"traffic", "traffic_stale", "traffic_profile"}.  A profile
+    describes the code that ran only if its kernel took the time this run's kernel takes:
+    the traffic is attached when the profiled mean kernel time is within +-15 % of
+    `kern_s` (the leg's measured kernel time), else traffic is null and traffic_stale true
+    (the profile belongs to an older kernel)."""
+    e = json.load(open(PMC_LEGS)).get("%s|%s" % (wl, leg)) if os.path.exists(PMC_LEGS) else None
+    if not e:
+        return {"traffic": None, "traffic_stale": None, "traffic_profile": None}
+    prof_s = e.get("kernel_mean_ns_profiled", 0) / 1e9
+    fresh = bool(prof_s and kern_s and abs(prof_s / kern_s - 1) <= 0.15)
+    return {"traffic": e.get("hbm_bytes_per_launch") if fresh else None, "traffic_stale": not fresh,
+            "traffic_profile": {"tag": e.get("tag"), "kernel": e.get("kernel"),
+                                "kernel_ms_profiled": prof_s * 1e3,
+                                "l2_hit_rate": e.get("l2_hit_rate")}}
 
 
 def time_launches(launch, steps, warmup, stream):
@@ -210,11 +213,12 @@ class Workload:
         return rnd, acc, frac
 
 
-def roofline(alg_random, alg_stream, accesses, kern_s, B, traffic, stream_read=None):
+def roofline(alg_random, alg_stream, accesses, kern_s, B, pmc, stream_read=None):
+    """pmc: pmc_traffic()'s dict (traffic + whether its profile matches this kernel)."""
     alg = alg_random + alg_stream
     achieved = alg / kern_s / 1e9
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "frac": achieved / HBM_PEAK_GBS, **pmc,
             "alg_bytes_per_launch": alg, "alg_random_bytes_per_launch": alg_random,
             "alg_stream_bytes_per_launch": alg_stream, "alg_bytes_per_query": alg / B,
             "stream_read_bytes_per_launch": stream_read,
@@ -241,7 +245,7 @@ def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, ste
            "ms_per_launch": wall * 1e3, "kernel_ms_mean": kern_s * 1e3, "kernel_ms_min": kmin,
            "patterns_per_s": W.B / kern_s, "prefix_table_hit_frac": frac,
            "matches_headline": None if ref_counts is None else bool(np.array_equal(got, ref_counts)),
-           "roofline": roofline(rnd, stream_bytes, acc, kern_s, W.B, pmc_traffic(wl_key, name),
+           "roofline": roofline(rnd, stream_bytes, acc, kern_s, W.B, pmc_traffic(wl_key, name, kern_s),
                                 stream_read)}
     return out, got
 
@@ -334,7 +338,7 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
             "walk_roofline": {"bound": "hbm", "achieved": alg / walk_s / 1e9, "peak": HBM_PEAK_GBS,
                               "unit": "GB/s", "frac": alg / walk_s / 1e9 / HBM_PEAK_GBS,
                               "alg_bytes_per_position": alg / max(tot, 1),
-                              "traffic": pmc_traffic(wl_key, name),
+                              **pmc_traffic(wl_key, name, walk_s),
                               "dependent_reads_per_s": reads / walk_s,
                               "frac_of_random_access_ceiling": reads / walk_s / RANDOM_CEIL}}
 
@@ -386,7 +390,7 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
             "roofline": {"bound": "hbm", "achieved": alg / tl / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / tl / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_query": alg / B,
                          "stream_read_bytes_per_launch": B * m + (B + 1) * 8,
-                         "traffic": pmc_traffic(wl_key, name), "random_accesses_per_s": reads / tl,
+                         **pmc_traffic(wl_key, name, min(evs)), "random_accesses_per_s": reads / tl,
                          "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}
 
 
@@ -536,6 +540,76 @@ def engine_name(info):
     return "binary wavelet matrix, 8 levels (%d-B rank lines)" % info.line_bytes
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, child_argv, script=None, env=None):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this script (one
+    per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT set, as
+    torch.distributed.run would) and wait for them.  Called before anything touches the
+    GPU — the parent never initialises HIP and never exec()s; the ranks are children.
+    Rank 0's JSON line is the only stdout line: its other stdout lines (e.g. gloo's
+    connection notices) and the other ranks' stdout go to stderr.  When one rank fails, the others are terminated (by PID) and its exit
+    status is returned; 0 when every rank succeeded."""
+    import signal
+    import subprocess
+    script = script or os.path.abspath(__file__)
+    base = dict(os.environ if env is None else env)
+    base.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(free_port()), "GROUP_RANK": "0", "CS_BENCH_SPAWNED": "1"})
+    import threading
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(child_argv), env=e,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr))
+
+    def relay(pipe):
+        # rank 0's JSON line to stdout; anything else a library prints there to stderr
+        for raw in iter(pipe.readline, b""):
+            line = raw.decode(errors="replace")
+            dst = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            dst.write(line)
+            dst.flush()
+
+    relay_t = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    relay_t.start()
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 10
+        for p in procs:
+            try:
+                p.wait(max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    old = signal.signal(signal.SIGTERM, lambda *_: (stop(), sys.exit(143)))
+    try:
+        rc = 0
+        while [p.poll() for p in procs].count(None):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                print("[bench] a rank exited with status %d; stopping the others" % rc,
+                      file=sys.stderr, flush=True)
+                stop()
+                break
+            time.sleep(0.2)
+        relay_t.join(10)
+        bad = [p.returncode for p in procs if p.returncode != 0]
+        return rc or (bad[0] if bad else 0)
+    finally:
+        signal.signal(signal.SIGTERM, old)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -591,18 +665,40 @@ def main():
         legs = {args.only} - {"count"}
         args.no_cpu, args.p50_calls = True, 0
 
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process starts the N ranks itself (before any GPU call)
+        if args.dist_backend == "nccl" and ndev < args.gpus:
+            sys.exit("bench.py: --gpus %d over RCCL needs %d GPUs, %d visible (rehearse with "
+                     "--dist-backend gloo)" % (args.gpus, args.gpus, ndev))
+        rc = spawn_ranks(args.gpus, sys.argv[1:])
+        sys.exit(rc if rc >= 0 else 128 - rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d: the line would not describe the run"
+                 % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and ndev < int(os.environ.get("LOCAL_WORLD_SIZE", world)):
+        sys.exit("bench.py: RCCL needs one GPU per rank (%d visible)" % ndev)
     local_dev = local % max(ndev, 1)  # identity on an N-GPU node; lets a 1-GPU box rehearse N ranks
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
+    rank_devices = None
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        assert dist.get_rank() == rank
+        # which GPU every rank runs on (PCI bus of its device), gathered to the line
+        pr = torch.cuda.get_device_properties(dev)
+        me = "%d:%s:%s" % (rank, local_dev, getattr(pr, "pci_bus_id", "?"))
+        rank_devices = [None] * world
+        dist.all_gather_object(rank_devices, me)
         legs = set()  # the N=1 legs; N > 1 runs the headline and the sharded locate
     pkg = _load_pkg()
     import importlib
@@ -725,7 +821,7 @@ def main():
         rnd, acc, frac = W.accounting(idx, info, 0, sh, dev)
         stream_b = B * m + (B + 1) * 8 + B * 8  # patterns, offsets, uint64 counts
         if rank == 0:
-            rf = roofline(rnd, stream_b, acc, kern_avg_s, B, pmc_traffic(wl, "count"),
+            rf = roofline(rnd, stream_b, acc, kern_avg_s, B, pmc_traffic(wl, "count", kern_avg_s),
                           B * m + (B + 1) * 8)
             rf.update({"line_bytes": info.line_bytes, "prefix_k": info.prefix_k,
                        "prefix_table_hit_frac": frac, "context_q": info.context_q,
@@ -740,6 +836,10 @@ def main():
                 "value": B * world * args.steps / elapsed,
                 "unit": "patterns/s",
                 "n_gpus": world,
+                "ranks_seen": dist.get_world_size() if world > 1 else 1,
+                "rank_devices": rank_devices,
+                "launcher": ("bench.py --gpus (ranks spawned by bench.py)" if os.environ.get("CS_BENCH_SPAWNED")
+                             else "external (torch.distributed.run)" if world > 1 else "single process"),
                 "steps": args.steps,
                 "warmup": args.warmup,
                 "ms_per_step": elapsed / args.steps * 1e3,

@@ -90,8 +90,15 @@ cs_status scratch_ready(const cs_fm_index* h) {
 struct PinRegistry {
   std::mutex mu;
   std::map<uintptr_t, std::pair<uintptr_t, int>> m;  // start -> (end, references)
+  std::multimap<uintptr_t, uintptr_t> busy;           // plain copies in flight: start -> end
+  static bool overlaps(const std::multimap<uintptr_t, uintptr_t>& b, uintptr_t lo, uintptr_t hi) {
+    for (auto it = b.begin(); it != b.end() && it->first < hi; ++it)
+      if (it->second > lo) return true;
+    return false;
+  }
   // [lo, hi) usable for DMA: inside a registered range (one more reference) or newly
-  // registered; false when it overlaps a registration without lying inside it
+  // registered; false when it overlaps a registration without lying inside it, or a
+  // plain copy in flight (its caller then copies through the bounce arena)
   bool acquire(uintptr_t lo, uintptr_t hi) {
     std::lock_guard<std::mutex> lk(mu);
     auto it = m.upper_bound(lo);
@@ -106,6 +113,7 @@ struct PinRegistry {
       }
     }
     if (it != m.end() && it->first < hi) return false;
+    if (overlaps(busy, lo, hi)) return false;
     if (hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault) != hipSuccess) {
       (void)hipGetLastError();
       return false;
@@ -115,14 +123,23 @@ struct PinRegistry {
   }
   // runs f() (a plain copy of pageable caller memory [lo, hi)) only while no registration
   // overlaps those bytes — else the runtime would take the range for pinned memory that
-  // does not cover it (hipErrorInvalidValue) — holding the lock so none starts meanwhile
+  // does not cover it (hipErrorInvalidValue).  The span is marked busy under the lock, so
+  // no registration over it starts while f() runs, and f() runs without the lock: a large
+  // pageable copy (synchronous through the runtime's staging buffer) does not hold up
+  // other threads' pins, copies and releases.
   template <class F>
   bool unregistered(uintptr_t lo, uintptr_t hi, F&& f) {
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = m.upper_bound(lo);
-    if (it != m.begin() && std::prev(it)->second.first > lo) return false;
-    if (it != m.end() && it->first < hi) return false;
+    std::multimap<uintptr_t, uintptr_t>::iterator mine;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      auto it = m.upper_bound(lo);
+      if (it != m.begin() && std::prev(it)->second.first > lo) return false;
+      if (it != m.end() && it->first < hi) return false;
+      mine = busy.emplace(lo, hi);
+    }
     f();
+    std::lock_guard<std::mutex> lk(mu);
+    busy.erase(mine);
     return true;
   }
   void release(uintptr_t lo) {
@@ -659,7 +676,7 @@ cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pat
   if (s != CS_OK) return s;
   CountOut co;
   if ((s = count_out(h, out, npat, co)) != CS_OK) return s;
-  if (npat && !d_offs && fixed_m && !d_pats) {
+  if (npat && !d_pats && (d_offs || fixed_m)) {  // the same rule as cs_fm_count_fixed_device
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }

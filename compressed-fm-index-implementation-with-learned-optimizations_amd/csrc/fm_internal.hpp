@@ -177,6 +177,10 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
 // (CS_Q_LONG): fixed-length device batches and host batches, whose lengths are known
 // before the launch.
 constexpr uint64_t kLongPatternM = 96;
+// Slack after every index part in HBM (zeroed): the text verification and extract read
+// whole aligned 8-B words, up to 7 bytes past the text's last byte (fm_query.hip
+// window_eq / verify_filter / k_extract_text), so the allocation covers them.
+constexpr uint64_t kPartPad = 64;
 // the general form: output width (fmx::CountOut), query flags (CS_Q_*), packed DNA input
 // (d_pats = one uint64 per pattern of fixed_m 2-bit characters)
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,

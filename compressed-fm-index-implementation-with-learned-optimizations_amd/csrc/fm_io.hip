@@ -207,8 +207,9 @@ cs_status need_device() {
 
 // allocate every part (and the overrun flag) of a handle whose geometry is set
 cs_status alloc_parts(cs_fm_index* h, const std::vector<Part>& parts) {
-  for (const Part& p : parts)
-    if (hipMalloc(p.dptr, p.bytes ? p.bytes : 16) != hipSuccess)
+  for (const Part& p : parts)  // + kPartPad zeroed bytes: word reads past a part's end
+    if (hipMalloc(p.dptr, p.bytes + kPartPad) != hipSuccess ||
+        hipMemset(static_cast<uint8_t*>(*p.dptr) + p.bytes, 0, kPartPad) != hipSuccess)
       return hip_fail(hipGetLastError(), "hipMalloc (index image)");
   if (hipMalloc(&h->d_err, 8) != hipSuccess || hipMemset(h->d_err, 0xFF, 8) != hipSuccess)
     return hip_fail(hipGetLastError(), "hipMalloc (index image)");

@@ -2607,7 +2607,8 @@ cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_devic
   if (const char* e = std::getenv("CS_FM_DEVICE_TEXT"))
     if (std::atoi(e) == 0) return CS_OK;
   if (!hbm_room(h, h->n)) return CS_OK;
-  FMX_HIP(hipMalloc(&h->d_dtext, h->n));
+  FMX_HIP(hipMalloc(&h->d_dtext, h->n + kPartPad));
+  FMX_HIP(hipMemsetAsync(static_cast<uint8_t*>(h->d_dtext) + h->n, 0, kPartPad, st));
   FMX_HIP(hipMemcpyAsync(h->d_dtext, src, h->n,
                          src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
   FMX_HIP(hipStreamSynchronize(st));
@@ -2808,8 +2809,9 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
     set_error("batch too large for one launch");
     return CS_ERR_INVALID;
   }
-  // a range wider than kLocSmall rows takes over kLocSmall positions of the capacity
-  const uint64_t wide_cap = cap / (kLocSmall + 1) + 1;
+  // a range wider than kLocSmall rows takes over kLocSmall positions of the capacity, and
+  // a pattern has at most one
+  const uint64_t wide_cap = std::min<uint64_t>(cap / (kLocSmall + 1) + 1, npat);
   StreamBuf ws;
   FMX_HIP(ws.alloc(npat * 12 + tiles * 8 + 8 + wide_cap * 16, st));
   OnePass op;

@@ -200,7 +200,8 @@ cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, cons
  * layout in device memory, unchecked.  A batch of more than CS_FM_HOST_CHUNK patterns
  * (environment, default 2^21) runs in chunks: each chunk's caller pages are page-locked
  * while the earlier chunks' copies and counts run, and its offsets are checked just before
- * it is queued — on CS_ERR_INVALID the counts of earlier chunks may have been written. */
+ * it is queued — so on CS_ERR_INVALID the contents of out_counts are unspecified (the
+ * counts of earlier chunks may have been written). */
 cs_status cs_fm_count_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,
                             uint64_t npat, uint64_t* out_counts, void* stream);
 /* Batched locate, host buffers.  out_offs has npat+1 entries (CSR into out_pos).

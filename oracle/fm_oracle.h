@@ -65,6 +65,11 @@ void orc_bwt_from_sa(const uint8_t* text, uint64_t n, const uint64_t* sa, uint8_
 /* --- FM index (src/api/fm_index.{hpp,cpp}) --- */
 /* sa_algo: 0 auto (naive for n <= 4096, doubling above), 1 naive, 2 doubling. */
 orc_index* orc_build(const uint8_t* text, uint64_t n, uint32_t ssa_stride, int sa_algo);
+/* 1 iff sa is text's suffix array (a permutation, consecutive suffixes increasing) */
+int orc_check_sa(const uint8_t* text, uint64_t n, const uint64_t* sa, int nthreads);
+/* the same from a caller-checked suffix array (no sort): full-size parity tests */
+orc_index* orc_build_from_sa(const uint8_t* text, uint64_t n, const uint64_t* sa,
+                             uint32_t ssa_stride, int nthreads);
 /* count-only index from a BWT (no text, no SA): used by the CPU baseline */
 orc_index* orc_build_from_bwt(const uint8_t* bwt, uint64_t n);
 orc_index* orc_build_from_bwt_mt(const uint8_t* bwt, uint64_t n, int nthreads);

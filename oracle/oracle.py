@@ -60,6 +60,8 @@ def lib():
         "orc_build": (_vp, [_u8p, C.c_uint64, C.c_uint32, C.c_int]),
         "orc_build_from_bwt": (_vp, [_u8p, C.c_uint64]),
         "orc_build_from_bwt_mt": (_vp, [_u8p, C.c_uint64, C.c_int]),
+        "orc_build_from_sa": (_vp, [_u8p, C.c_uint64, _u64p, C.c_uint32, C.c_int]),
+        "orc_check_sa": (C.c_int, [_u8p, C.c_uint64, _u64p, C.c_int]),
         "orc_free": (None, [_vp]),
         "orc_n": (C.c_uint64, [_vp]),
         "orc_ssa_stride": (C.c_uint32, [_vp]),
@@ -191,9 +193,16 @@ class LevelView:
 class Index:
     """cs::FMIndex restated (src/api/fm_index.{hpp,cpp})."""
 
-    def __init__(self, text=None, ssa_stride=32, sa_algo=0, bwt=None, nthreads=1):
+    def __init__(self, text=None, ssa_stride=32, sa_algo=0, bwt=None, nthreads=1, sa=None):
+        """From the text (suffix sort here), from a BWT (count only), or from the text and
+        a suffix array the caller has checked (check_suffix_array): no sort."""
         L = lib()
-        if bwt is not None:
+        if sa is not None:
+            t = as_u8(text)
+            sa64 = np.ascontiguousarray(sa, np.uint64)
+            assert len(sa64) == len(t) and len(t) > 0
+            self._h = L.orc_build_from_sa(_u8(t), len(t), _u64(sa64), ssa_stride, nthreads)
+        elif bwt is not None:
             b = as_u8(bwt)
             self._h = L.orc_build_from_bwt_mt(_u8(b) if len(b) else _u8(np.zeros(1, np.uint8)),
                                              len(b), nthreads)
@@ -316,6 +325,19 @@ class Index:
 
 
 # ---------------------------------------------------------------------------
+def check_suffix_array(text, sa, nthreads=8):
+    """True iff `sa` is the suffix array of `text` in the reference's order (plain
+    suffix order, a proper prefix first: src/core/sais.hpp:8-16): a permutation of
+    0..n-1 whose consecutive suffixes strictly increase (orc_check_sa)."""
+    t = as_u8(text)
+    sa64 = np.ascontiguousarray(sa, np.uint64)
+    if len(sa64) != len(t):
+        return False
+    if not len(t):
+        return True
+    return bool(lib().orc_check_sa(_u8(t), len(t), _u64(sa64), nthreads))
+
+
 def sa_naive(text) -> np.ndarray:
     t = as_u8(text)
     out = np.zeros(max(len(t), 1), np.uint64)

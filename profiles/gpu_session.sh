@@ -53,7 +53,7 @@ for STEP in "$@"; do
     tests)
       K=()
       [ ${#ARGS[@]} -gt 0 ] && K=(-k "${ARGS[*]}")
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread --durations=80 \
         "${K[@]}" > $OUT/$NAME.log 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/$NAME.log 2>&1 ;;

@@ -8,9 +8,15 @@ properties — no CPU index is built at these sizes:
   * checksum of checksums: sum of count() over ALL k-mers of the alphabet equals
     the number of k-windows of the text that avoid the terminator, and the sum of
     count() over all 256 single bytes equals n.
-The oracle comparison at these sizes is on the sample in bench.py's cpu_baseline
-(matches_gpu); bit-exact oracle parity at sizes the oracle builds in seconds is in
-test_gpu_parity.py.
+and, exactly, against the oracle (oracle/fm_oracle.c):
+
+  * C2 (100 MB): the oracle is built from the text and the device builder's suffix
+    array, after orc_check_sa has proven that array to be the text's suffix array (a
+    permutation with increasing consecutive suffixes) — so no O(n log n) CPU sort —
+    and 200 k Q_text counts and 100 k locates (limit 100) equal its answers;
+  * C4 (4 GB): 1 M Q_text counts equal the oracle's count over the GPU's BWT (the
+    same check as bench.py's cpu_fast), for every C4 index variant.
+Bit-exact parity at sizes the oracle sorts in seconds is in test_gpu_parity.py.
 """
 import itertools
 import os
@@ -19,9 +25,15 @@ import numpy as np
 import pytest
 import torch
 
+import oracle as O  # the checker
 from conftest import load_pkg
 
 pytestmark = pytest.mark.gpu
+
+# host threads of the checker: the process's CPU share (16 per GPU on the box)
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+# C4's oracle counts, shared by the C4 variants (same text, same batch)
+_C4_ORACLE = {}
 
 
 def _build(pkg, kind, L):
@@ -101,8 +113,21 @@ def test_c4_dna_4gb(variant, monkeypatch):
     # C4: n / 4^15 = 3.7 rows per k-mer -> compact 16-B records
     assert info.record_bytes == (0 if variant == "plain_walk" else 16)
     assert info.prefix_bytes == max(info.record_bytes, 8) * info.prefix_sigma ** info.prefix_k
-    P = _qtext(pkg, text, N, 20, 200_000)
-    _check_qtext(idx, host, N, P, nloc=20_000)
+    P = _qtext(pkg, text, N, 20, 1_000_000)
+    cnt = _check_qtext(idx, host, N, P, nloc=20_000)
+    # exact: 1 M counts against the oracle's count over the GPU's BWT (computed once for
+    # the three variants; the BWT is the text's, whatever the index keeps)
+    if "counts" not in _C4_ORACLE:
+        d_bwt = torch.empty(N, dtype=torch.uint8, device=text.device)
+        idx.bwt_device(d_bwt.data_ptr())
+        torch.cuda.synchronize()
+        ref = O.Index(bwt=d_bwt.cpu().numpy(), nthreads=THREADS)
+        del d_bwt
+        buf = np.ascontiguousarray(P).reshape(-1)
+        _C4_ORACLE["counts"] = ref.count_batch(buf=buf, offs=np.arange(0, (len(P) + 1) * 20, 20, dtype=np.uint64),
+                                               nthreads=THREADS)
+        del ref
+    assert np.array_equal(cnt, _C4_ORACLE["counts"]), variant
     ones = idx.count_batch([bytes([c]) for c in range(256)])
     assert int(ones.sum()) == N and ones[ord("$")] == 1
     _kmer_checksum(idx, b"ACGT", 9, N)
@@ -144,9 +169,22 @@ def test_c3_bytes_1gb():
 
 
 def test_c2_dna_100mb_locate_everything():
-    """100 MB: locate every Q_text hit of 200k 20-mers and 12-mers (limit 100)."""
+    """100 MB: locate every Q_text hit of 200k 20-mers and 12-mers (limit 100), and
+    the same counts and (for the first 100 k) positions exactly as the oracle's."""
     pkg = load_pkg()
     idx, text, host, N = _build(pkg, "dna", 99_999_999)
+    sa = pkg.sa_build(host.tobytes())  # the device builder, checked on the host
+    assert O.check_suffix_array(host, sa, nthreads=THREADS)
+    ref = O.Index(host, sa=sa, nthreads=THREADS)
+    assert ref.ssa().tolist() == idx.ssa().tolist()
+    del sa
     for m in (20, 12):
         P = _qtext(pkg, text, N, m, 200_000)
-        _check_qtext(idx, host, N, P, nloc=200_000, limit=100)
+        cnt = _check_qtext(idx, host, N, P, nloc=200_000, limit=100)
+        buf = np.ascontiguousarray(P).reshape(-1)
+        offs = np.arange(0, (len(P) + 1) * m, m, dtype=np.uint64)
+        assert np.array_equal(cnt, ref.count_batch(buf=buf, offs=offs, nthreads=THREADS)), m
+        nl = 100_000
+        woffs, wpos = ref.locate_batch(buf=buf[: nl * m], offs=offs[: nl + 1], limit=100, nthreads=THREADS)
+        goffs, gpos = idx.locate_batch(buf=buf[: nl * m], offs=offs[: nl + 1], limit=100)
+        assert np.array_equal(goffs, woffs) and np.array_equal(gpos, wpos), m

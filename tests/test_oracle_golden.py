@@ -131,3 +131,40 @@ def test_reference_count_only_index(case):
     pats = [bytes.fromhex(h) for h in case["patterns_hex"]]
     buf, offs = O.pack_patterns(pats)
     assert ref.count_batch(buf, offs, nthreads=4).tolist() == case["count"]
+
+
+@pytest.mark.parametrize("case", fm_golden_cases("fm_kat.json", "fm_100k.json"))
+def test_build_from_checked_sa(case):
+    """orc_build_from_sa (the full-size tests' oracle: suffix array supplied, checked by
+    orc_check_sa) answers every golden case exactly as the reference did."""
+    text = golden_text(case["text"])
+    if not text:
+        pytest.skip("empty text: no suffix array to supply")
+    sa = O.sa_doubling(text)
+    assert O.check_suffix_array(text, sa)
+    idx = O.Index(text, ssa_stride=case["ssa_stride"], sa=sa, nthreads=3)
+    pats = [bytes.fromhex(h) for h in case["patterns_hex"]]
+    assert [idx.count(p) for p in pats] == case["count"]
+    for p, loc in zip(pats, case["locate"]):
+        if "pos" in loc:
+            assert idx.locate(p, limit=case["limit"]) == loc["pos"]
+
+
+def test_check_suffix_array_rejects():
+    rng = np.random.default_rng(3)
+    for t in (b"banana$", b"aaaa", b"abab", b"x", O.gen_dna(9, 3000).tobytes(),
+              bytes(rng.integers(0, 256, 2000).astype(np.uint8))):
+        sa = O.sa_naive(t)
+        assert O.check_suffix_array(t, sa)
+        if len(t) > 1:
+            sw = sa.copy()
+            i = int(rng.integers(0, len(t) - 1))
+            sw[[i, i + 1]] = sw[[i + 1, i]]
+            assert not O.check_suffix_array(t, sw)
+            dup = sa.copy()
+            dup[0] = dup[-1]
+            assert not O.check_suffix_array(t, dup)
+        assert not O.check_suffix_array(t, sa[:-1])
+        big = sa.copy()
+        big[0] = len(t)
+        assert not O.check_suffix_array(t, big)
