@@ -435,6 +435,8 @@ void free_index(cs_fm_index* h) {
   if (h->d_isa) (void)hipFree(h->d_isa);
   if (h->d_sa) (void)hipFree(h->d_sa);
   if (h->d_dtext) (void)hipFree(h->d_dtext);
+  if (h->d_ptext) (void)hipFree(h->d_ptext);
+  if (h->d_prare) (void)hipFree(h->d_prare);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
   if (h->d_lctx) (void)hipFree(h->d_lctx);
@@ -590,6 +592,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->full_sa_bytes = h->d_sa ? h->n * 4 : 0u;
   out->record_bytes = h->ptab_rec ? h->ptab_entry_bytes() : 0u;
   out->text_in_hbm = h->d_dtext ? 1u : 0u;
+  out->packed_text_bytes = h->d_ptext ? h->ptext_bytes() : 0;
   return CS_OK;
 }
 

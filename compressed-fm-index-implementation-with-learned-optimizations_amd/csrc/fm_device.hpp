@@ -124,6 +124,13 @@ struct DevIndex {
   // otherwise or under CS_Q_NO_CONTEXTS / CS_Q_NO_VERIFY.
   const uint32_t* vsa;
   const uint8_t* vtext;
+  // The same text 2-bit packed (occurrence codes, character i at bits 2 (i % 32) of word
+  // i / 32, rare symbols as code 0) and the sorted positions of the rare symbols: long
+  // patterns are verified against 32 characters per 8-B word (k_count_long).  Null
+  // unless vtext is set and the index has occurrence lines.
+  const uint64_t* ptext;
+  const uint32_t* prare;
+  uint32_t nrare;
 };
 
 // Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q

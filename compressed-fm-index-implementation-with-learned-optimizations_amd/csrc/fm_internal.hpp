@@ -52,6 +52,13 @@ struct cs_fm_index {
   uint32_t lmodel_shift = 0;
   std::vector<uint8_t> h_text;        // fm_index.hpp:41 text_ (extract only)
   void* d_dtext = nullptr;            // the same text in HBM: extract as a copy (fm_index.cpp:163-167)
+  // 2-bit copy of d_dtext (occurrence codes, 32 characters per u64, rare symbols as code 0)
+  // and the sorted text positions of the rare symbols (<= kMaxExc): long-pattern
+  // verification (fm_query.hip k_count_long); derived on build / open / import, not saved
+  void* d_ptext = nullptr;
+  void* d_prare = nullptr;
+  uint32_t nrare = 0;
+  uint64_t ptext_bytes() const { return ((n + 31) / 32) * 8; }
   uint32_t active_levels[256] = {};
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
@@ -126,6 +133,9 @@ struct cs_fm_index {
     const bool ver = d_sa && d_dtext && lf_exact && !wide;
     d.vsa = ver ? static_cast<const uint32_t*>(d_sa) : nullptr;
     d.vtext = ver ? static_cast<const uint8_t*>(d_dtext) : nullptr;
+    d.ptext = ver && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
+    d.prare = static_cast<const uint32_t*>(d_prare);
+    d.nrare = nrare;
     return d;
   }
 };
@@ -223,6 +233,8 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st);
 cs_status build_left_contexts(cs_fm_index* h, hipStream_t st);
 cs_status build_context_records(cs_fm_index* h, hipStream_t st);
 cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st);
+// the 2-bit text of d_dtext (cs_fm_index::d_ptext), when the index can use it (fm_query.hip)
+cs_status derive_packed_text(cs_fm_index* h, hipStream_t st);
 // HBM held by the index's device arrays so far (the image parts, fm_io.hip)
 uint64_t index_hbm_bytes(const cs_fm_index* h);
 // Whether an optional structure of `bytes` may be allocated: the device keeps an eighth

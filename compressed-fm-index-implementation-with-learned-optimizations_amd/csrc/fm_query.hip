@@ -26,7 +26,9 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
+#include <algorithm>
 #include <cstdlib>
+#include <vector>
 #include <cstring>
 #include <mutex>
 
@@ -1511,6 +1513,289 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   general_rest<E, U, kLoc, kPacked, W>(ix, T, pats, st, o0, m, q0, co, limit, rec);
 }
 
+// Long patterns (round 3; CS_Q_LONG, fixed-length batches over kLongPatternM, host chunks
+// of long patterns) over an lf_exact occurrence-line index that keeps the full suffix array
+// and the text (DevIndex::vsa / vtext) — C2 and C4 by default.  The reference steps m
+// times (fm_index.cpp:88-98); count_rest already finishes a narrow range by verification
+// against the text (rows whose left contexts match, then text[SA - k, SA) against P[0, k)),
+// and this kernel runs that search as a pipeline of independent reads, one pattern per
+// lane, with nothing else live:
+//   (A) the pattern's offsets and its last 32 bytes (realigned dword loads): the
+//       prefix-table index of the last K characters and the context key of the qc = 7
+//       before them, from a 512-B LDS symbol map (no 10.8-KB node table, no barrier);
+//   (B) the table entry — a context record holds the range and its rows' contexts;
+//   (C) the candidate rows: the record's inline contexts, else one or two 32-B context
+//       sectors; a candidate's chain spells the qf characters before the table part;
+//   (D) the SA entry of each candidate (the rows are consecutive: one sector);
+//   (E) the window text[SA - k, SA - qf) against P[0, k - qf): up to kLongWords aligned
+//       8-B words of text AND of the pattern per round, all issued before the compare.
+// A pattern is read once (the general path's count_pattern read its record a second time
+// and held both of a lane's patterns behind a block barrier).  Anything else — a range
+// wider than the record / two sectors, an escaped context, a symbol outside the table's
+// alphabet, a pattern shorter than 32 characters — takes count_pattern with the node table
+// read through the caches.
+template <int V>
+__device__ __forceinline__ bool window_eq_long(const DevIndex& ix, const uint8_t* P, uint64_t q,
+                                               uint64_t L) {
+  const uint64_t n = ix.n;
+  if (q + L > n) {  // a window through the end of the text (cyclic), byte by byte
+    for (uint64_t j = 0; j < L; ++j) {
+      uint64_t t = q + j;
+      if (t >= n) t -= n;
+      if (ix.vtext[t] != P[j]) return false;
+    }
+    return true;
+  }
+  const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
+  const uint64_t* pw = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(P) & ~(uintptr_t)7);
+  const uint64_t ps = reinterpret_cast<uintptr_t>(P) & 7;
+  const uint64_t tlast = (q + L - 1) >> 3, plast = (ps + L - 1) >> 3;  // words holding a byte
+  for (uint64_t j0 = 0; j0 < L; j0 += 8 * V) {
+    const uint64_t ta = (q + j0) >> 3, pa = (ps + j0) >> 3;
+    uint64_t tv[V + 1], pv[V + 1];
+#pragma unroll
+    for (int i = 0; i <= V; ++i) {
+      tv[i] = ta + i <= tlast ? tw[ta + i] : 0ull;
+      pv[i] = pa + i <= plast ? pw[pa + i] : 0ull;
+    }
+    uint64_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+      const uint64_t j = j0 + 8 * (uint64_t)i;
+      if (j < L) diff |= (text8(tv[i], tv[i + 1], q + j) ^ text8(pv[i], pv[i + 1], ps + j)) & chunk_mask(j, L);
+    }
+    if (diff) return false;
+  }
+  return true;
+}
+
+constexpr int kLongWords = 12;  // byte-text words per round (96 characters; no packed text)
+// packed pattern words: the fast path takes P[0, k) of at most 32 kLongPW characters before
+// the table part (a 150-mer at k = 15: 135)
+constexpr uint32_t kLongPW = 5;
+
+// whether a text position of a rare symbol lies in [q, q + L) (sorted list in LDS)
+__device__ __forceinline__ bool rare_in(const uint32_t* r, uint32_t nr, uint64_t q, uint64_t L) {
+  uint32_t lo = 0, hi = nr;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (r[mid] < q) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < nr && r[lo] < q + L;
+}
+
+// text[q, q + L) == P[0, L) against the 2-bit text: the window's kLongPW + 1 words in one
+// round, shifted to the window start and compared with the packed pattern pc (codes of a
+// pattern whose characters are all coded).  A rare symbol in the window is a mismatch (its
+// code 0 in the packed text stands for no pattern character).  Windows through the end of
+// the text: the byte text, cyclically.
+__device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint64_t* pc, const uint8_t* P,
+                                                 uint64_t q, uint64_t L, const uint32_t* rare) {
+  if (q + L > ix.n) return window_eq<const uint8_t*>(ix, P, q, L, nullptr);
+  const uint64_t a = q >> 5, last = (q + L - 1) >> 5;
+  const uint32_t s = (uint32_t)(q & 31) * 2;
+  uint64_t w[kLongPW + 1];
+#pragma unroll
+  for (uint32_t i = 0; i <= kLongPW; ++i) w[i] = a + i <= last ? ix.ptext[a + i] : 0ull;
+  uint64_t diff = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kLongPW; ++i) {
+    const uint64_t j = 32ull * i;
+    if (j < L) {
+      const uint64_t x = s ? (w[i] >> s) | (w[i + 1] << (64 - s)) : w[i];
+      const uint64_t msk = L - j >= 32 ? ~0ull : (1ull << (2 * (L - j))) - 1;
+      diff |= (x ^ pc[i]) & msk;
+    }
+  }
+  return !diff && !rare_in(rare, ix.nrare, q, L);
+}
+
+// kPT: verify against the packed text (DevIndex::ptext), else the byte text in rounds of
+// kLongWords words.  Patterns the pipeline does not answer are appended to `list` (q) for
+// k_count_list, which runs the general search.
+template <int W, bool kPT>
+__global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                     const uint64_t* __restrict__ offs, uint64_t npat,
+                                                     CountOut co, uint64_t fixed_m,
+                                                     uint64_t* __restrict__ list,
+                                                     unsigned long long* __restrict__ nlist) {
+  __shared__ uint16_t cmap[256];
+  __shared__ uint32_t rare[kMaxExc];
+  static_assert(kBlk >= 256, "one map entry per thread");
+  if (threadIdx.x < 256)
+    cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
+  if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+  if (q >= npat) return;
+  // (A)
+  const uint64_t o0 = offs ? offs[q] : q * fixed_m;
+  const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
+  const uint8_t* P = pats + o0;
+  if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
+    store_count<W>(co, q, m == 0 ? ix.n : 0);
+    return;
+  }
+  const uint32_t K = ix.ptab_k;
+  const uint64_t k = m - K;  // characters before the table part (when m >= K)
+  // verification needs the window inside one rotation (k < n, as count_rest's)
+  bool fast = m >= 32 && m > K + kCtxQ && k < ix.n && (!kPT || k <= 32ull * kLongPW);
+  uint32_t t = 0, want = 0;
+  bool cok = true;
+  uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
+#pragma unroll
+  for (uint32_t i = 0; i < kLongPW; ++i) pc[i] = 0;
+  if (fast) {
+    uint32_t u[8];
+    load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
+    if constexpr (kPT) {
+      // P[0, k) as aligned 8-B words (only words holding a byte of it), coded through the map
+      const uint64_t* pw = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(P) & ~(uintptr_t)7);
+      const uint64_t ps = reinterpret_cast<uintptr_t>(P) & 7, plast = (ps + k - 1) >> 3;
+      uint64_t x[4 * kLongPW + 1];
+#pragma unroll
+      for (uint32_t i = 0; i <= 4 * kLongPW; ++i) x[i] = i <= plast ? pw[i] : 0ull;
+#pragma unroll
+      for (uint32_t c = 0; c < 4 * kLongPW; ++c) {
+        const uint64_t y = text8(x[c], x[c + 1], ps);  // P[8c, 8c + 8)
+#pragma unroll
+        for (uint32_t b = 0; b < 8; ++b) {
+          if (8 * c + b < k) {
+            const uint32_t d = cmap[(uint32_t)(y >> (8 * b)) & 0xFFu] >> 8;
+            fast &= d != kNoCode;
+            pc[c >> 2] |= (uint64_t)(d & 3u) << (2 * (8 * (c & 3) + b));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 32; ++i) {
+      const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i >= 32 - K) {  // table part, most significant first
+        const uint32_t d = cmap[b] & 0xFFu;
+        fast &= d != kNoCode;
+        t = t * ix.ptab_sigma + d;
+      } else if (i + K + kCtxQ >= 32) {  // chain symbol 31 - K - i of the context part
+        const uint32_t d = cmap[b] >> 8;
+        cok &= d != kNoCode;
+        want |= (d & 3u) << (2 * (31 - K - i));
+      }
+    }
+  }
+  uint64_t res = 0;
+  bool general = !fast;
+  if (fast) {
+    // (B)
+    uint64_t sp, ep;
+    uint32_t d[6] = {0, 0, 0, 0, 0, 0};  // inline contexts as u16 entries, row i in entry i
+    uint32_t qf = 0;                     // characters they answer (0: none inline)
+    if (ix.ptab_rec == 2) {
+      const uint4 a = static_cast<const uint4*>(ix.ptab)[t];
+      const uint32_t wc = a.y & 15u;
+      sp = a.x;
+      ep = sp + (wc == kRec16Wide ? a.z : wc);
+      if (wc != kRec16Wide) {
+        qf = kRec16Q;
+        rec16_contexts(a.y, a.z, a.w, d);
+      }
+    } else if (ix.ptab_rec == 1) {
+      const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t * 2;
+      const uint4 a = r[0], b = r[1];
+      sp = a.x;
+      ep = (uint64_t)a.x + a.y;
+      if (ep - sp <= kRecCtx) {
+        qf = kCtxQ;
+        d[0] = a.z, d[1] = a.w, d[2] = b.x, d[3] = b.y, d[4] = b.z, d[5] = b.w;
+      }
+    } else {
+      (void)ptab_at(ix, t, sp, ep);  // a narrow plain table escapes nothing
+    }
+    // (C) the candidate rows base + i (bit i of cand)
+    uint64_t base = sp;
+    uint32_t cand = 0;
+    if (sp >= ep) {
+      // the table part does not occur: count 0
+    } else if (!cok) {
+      general = true;  // a rare symbol among the context characters
+    } else if (qf) {
+      const uint32_t msk = qf == kCtxQ ? ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc : (1u << (2 * qf)) - 1u;
+      const uint32_t wq = want & ((1u << (2 * qf)) - 1u);
+      uint32_t esc = 0;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        const uint32_t e = (d[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        cand |= (uint32_t)((e & msk) == wq) << i;
+        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+      }
+      const uint32_t in = (1u << (uint32_t)(ep - sp)) - 1u;
+      general = (esc & in) != 0;  // 32-B records keep the escape bit; compact ones escape whole
+      cand &= in;
+    } else if (ix.lctx && ep - (sp & ~15ull) <= 32) {
+      qf = kCtxQ;
+      base = sp & ~15ull;
+      const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);
+      const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) + base);
+      const uint4 x0 = p[0], x1 = p[1];
+      const uint4 x2 = hi > 16 ? p[2] : make_uint4(0, 0, 0, 0), x3 = hi > 16 ? p[3] : make_uint4(0, 0, 0, 0);
+      const uint32_t dw[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                               x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+      const uint32_t msk = ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc;
+      uint32_t esc = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        cand |= (uint32_t)((e & msk) == want) << i;
+        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+      }
+      const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      general = (esc & in) != 0;
+      cand &= in;
+    } else {
+      general = true;  // wider than the record and two sectors: steps first
+    }
+    if (!general) {
+      // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
+      const uint64_t L = k - qf, n = ix.n;
+      while (cand) {
+        const uint32_t i = (uint32_t)__ffs(cand) - 1u;
+        cand &= cand - 1;
+        const uint64_t p = ix.vsa[base + i];
+        const uint64_t wq = p >= k ? p - k : p + n - k;
+        bool eq;
+        if constexpr (kPT) eq = window_eq_packed(ix, pc, P, wq, L, rare);
+        else eq = window_eq_long<kLongWords>(ix, P, wq, L);
+        res += eq ? 1u : 0u;
+      }
+    }
+  }
+  if (general) {
+    list[atomicAdd(nlist, 1ull)] = q;  // the general search, k_count_list
+    return;
+  }
+  store_count<W>(co, q, res);
+}
+
+// The patterns k_count_long listed: the general search (count_pattern), the node table
+// staged in LDS by the blocks that have work; a fixed grid striding over the list, whose
+// length is read on the device.
+template <int W>
+__global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                     const uint64_t* __restrict__ offs, CountOut co,
+                                                     uint64_t fixed_m, const uint64_t* __restrict__ list,
+                                                     const unsigned long long* __restrict__ nlist) {
+  __shared__ NodeTable T;
+  const uint64_t nl = *nlist;
+  if ((uint64_t)blockIdx.x * kBlk >= nl) return;  // uniform over the block
+  load_table(T, ix.table);
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlk + threadIdx.x; i < nl; i += (uint64_t)gridDim.x * kBlk) {
+    const uint64_t q = list[i];
+    const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
+    store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
+  }
+}
+
 // The batch count over the quaternary wavelet matrix with left contexts (C3: sigma = 256,
 // k = 4 prefix table of 16-B context records, u32 contexts of lctx_q = 4 dense codes):
 // the shape of k_count_ctx for u32 contexts.  (A) the pattern as realigned dword loads,
@@ -2612,6 +2897,93 @@ cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_devic
   FMX_HIP(hipMemcpyAsync(h->d_dtext, src, h->n,
                          src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
   FMX_HIP(hipStreamSynchronize(st));
+  return derive_packed_text(h, st);
+}
+
+// The 2-bit text (cs_fm_index::d_ptext): word w holds the occurrence codes of text[32 w,
+// 32 w + 32), rare symbols as code 0, their positions appended to `rare` (at most cap, the
+// counter counts them all).  A thread per word.
+__global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ text, uint64_t n,
+                                                    const NodeTable* __restrict__ table,
+                                                    uint64_t* __restrict__ out, uint64_t nw,
+                                                    uint32_t* __restrict__ rare, uint32_t cap,
+                                                    unsigned int* __restrict__ nrare) {
+  __shared__ uint8_t code[256];
+  if (threadIdx.x < 256) code[threadIdx.x] = table->occ_code[threadIdx.x];
+  __syncthreads();
+  const uint64_t w = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+  if (w >= nw) return;
+  const uint64_t* tw = reinterpret_cast<const uint64_t*>(text) + 4 * w;  // the text has kPartPad slack
+  uint64_t acc = 0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint64_t x = tw[c];
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t i = 32 * w + 8 * c + b;
+      if (i >= n) break;
+      const uint32_t d = code[(uint32_t)(x >> (8 * b)) & 0xFFu];
+      if (d == kNoCode) {
+        const unsigned int e = atomicAdd(nrare, 1u);
+        if (e < cap) rare[e] = (uint32_t)i;
+      } else {
+        acc |= (uint64_t)d << (2 * (8 * c + b));
+      }
+    }
+  }
+  out[w] = acc;
+}
+
+// Long patterns are verified against 32 text characters per 8-B word instead of 8
+// (k_count_long): n / 4 bytes (C4: 1 GB), for narrow lf_exact occurrence-line indexes that
+// keep the full suffix array and the text in HBM (the verification's preconditions), HBM
+// allowing.  Derived from the text, so it is rebuilt on open / import rather than saved.
+// CS_FM_PACKED_TEXT=0 (read at build / open) leaves it out.
+cs_status derive_packed_text(cs_fm_index* h, hipStream_t st) {
+  if (h->d_ptext || !h->d_dtext || !h->d_sa || !h->lf_exact || h->wide || h->line_fmt != kFmtOcc ||
+      h->n >= (1ull << 32))
+    return CS_OK;
+  if (const char* e = std::getenv("CS_FM_PACKED_TEXT"))
+    if (std::atoi(e) == 0) return CS_OK;
+  const uint64_t nw = (h->n + 31) / 32;
+  if (!hbm_room(h, nw * 8)) return CS_OK;
+  void* pt = nullptr;
+  FMX_HIP(hipMalloc(&pt, nw * 8 + kPartPad));
+  DevBuf rb;
+  if (rb.alloc(kMaxExc * 4 + 8) != hipSuccess) {
+    (void)hipFree(pt);
+    return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
+  }
+  unsigned int* d_n = reinterpret_cast<unsigned int*>(rb.as<uint8_t>() + kMaxExc * 4);
+  hipError_t e = hipMemsetAsync(d_n, 0, 4, st);
+  if (e == hipSuccess) {
+    k_pack_text<<<grid_for(nw, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+        static_cast<const uint8_t*>(h->d_dtext), h->n, h->d_table, static_cast<uint64_t*>(pt), nw,
+        rb.as<uint32_t>(), kMaxExc, d_n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(pt) + nw * 8, 0, kPartPad, st);
+  unsigned int nr = 0;
+  std::vector<uint32_t> pos(kMaxExc);
+  if (e == hipSuccess) e = hipMemcpyAsync(&nr, d_n, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(pos.data(), rb.p, kMaxExc * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess || nr > (unsigned)kMaxExc) {  // more rare positions than the list holds
+    (void)hipFree(pt);
+    return e == hipSuccess ? CS_OK : hip_fail(e, "packed text");
+  }
+  pos.resize(nr);
+  std::sort(pos.begin(), pos.end());
+  void* pr = nullptr;
+  if (hipMalloc(&pr, kMaxExc * 4) != hipSuccess ||
+      (nr && hipMemcpy(pr, pos.data(), nr * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+    (void)hipFree(pt);
+    if (pr) (void)hipFree(pr);
+    return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
+  }
+  h->d_ptext = pt;
+  h->d_prare = pr;
+  h->nrare = nr;
   return CS_OK;
 }
 
@@ -2734,13 +3106,29 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
   }
   if (h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa && !packed &&
       ((flags & CS_Q_LONG) || (!d_offs && fixed_m > kLongPatternM))) {
-    // long patterns: one per lane, the whole search in count_pattern, the
-    // text comparison with look-ahead — kept out of the staged kernel, whose registers
-    // the look-ahead would spill on the 20-mer path (C4: 150-mers 2.19 -> 2.56·10⁹/s;
-    // 64-mers 6.52 -> 6.01·10⁹/s, so only batches known to be longer than kLongPatternM
-    // take it unasked)
-    k_count<OccE, false, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, fixed_m);
+    // long patterns: one per lane in k_count_long (record, candidates, SA, text window as
+    // independent rounds; against the 2-bit text when the index has it), the patterns it
+    // does not answer listed for k_count_list; kept out of the staged kernel, whose
+    // registers the pattern and text words would take from the 20-mer path.  Tuning hook
+    // (read per call): CS_FM_LONG_KERNEL=0 = round 2's kernel (the general search with
+    // look-ahead rounds, k_count<OccE, false, true>), 2 = the byte text even when the
+    // packed text is there.
+    const char* ek = std::getenv("CS_FM_LONG_KERNEL");
+    const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
+    if (ek && std::atoi(ek) == 0) {
+      k_count<OccE, false, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
+    } else {
+      StreamBuf lb;
+      FMX_HIP(lb.alloc(npat * 8 + 8, st));
+      unsigned long long* nl = reinterpret_cast<unsigned long long*>(lb.as<uint64_t>() + npat);
+      FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
+      if (ix.ptext && !(ek && std::atoi(ek) == 2))
+        k_count_long<0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl);
+      else
+        k_count_long<0, false><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl);
+      FMX_HIP(hipGetLastError());
+      k_count_list<0><<<std::min(g, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, co, fixed_m, lb.as<uint64_t>(), nl);
+    }
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }

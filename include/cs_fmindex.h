@@ -87,6 +87,9 @@ typedef struct cs_fm_info {
   uint64_t full_sa_bytes;  /* full suffix array kept for locate (lf_exact builds), 0 = none */
   uint32_t record_bytes;   /* prefix-table entries are context records of 32 or 16 B; 0 = plain table */
   uint32_t text_in_hbm;    /* 1: the text is kept in HBM and extract copies it (as text_.substr) */
+  uint64_t packed_text_bytes; /* 2-bit copy of the text (occurrence lines, lf_exact, full SA and
+                              text in HBM) that long patterns are verified against; 0 = none.
+                              Derived from the text on build / open / import, not saved. */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -98,6 +98,24 @@ class _nobar:
             os.environ["CS_FM_COUNT_NOBAR"] = self.saved
 
 
+class _env:
+    """Per-call engine hooks (read by the library on each call) for the calls inside."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+
+    def __enter__(self):
+        self.saved = {k: os.environ.get(k) for k in self.kw}
+        os.environ.update(self.kw)
+
+    def __exit__(self, *a):
+        for k, v in self.saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 def _learned():
     return os.environ.get("CS_FM_ENGINE") == "learned"
 
@@ -259,6 +277,10 @@ def test_engine_choice(built):
             rec = 16
         assert info.record_bytes == rec, name
         assert info.text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0"), name
+        # the 2-bit text of long-pattern verification: occurrence lines (not learned), narrow,
+        # LF one n-cycle, with the full suffix array and the text in HBM
+        ptext = engine == 1 and full_sa and info.text_in_hbm and not wide
+        assert info.packed_text_bytes == ((info.n + 31) // 32 * 8 if ptext else 0), name
         assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
 
 
@@ -451,6 +473,35 @@ def test_random_large_vs_oracle(pkg, gen, m):
     goffs, gpos = g.locate_batch(buf=buf, offs=offs, limit=lim)
     assert np.array_equal(goffs, woffs)
     assert np.array_equal(gpos, wpos)
+
+
+def test_count_long_kernel_large(pkg):
+    """The long-pattern kernel (k_count_long, CS_Q_LONG) at scale: a 2 M DNA text with rare
+    symbols (N runs, so windows and contexts meet rare rows), 12 k Q_text patterns of 33-200
+    characters plus one-symbol mutants and patterns holding an N — counts equal the
+    oracle's through the packed text (default), the byte text (CS_FM_LONG_KERNEL=2) and
+    round 2's kernel (0), and every pattern of a random length batch agrees."""
+    rng = np.random.default_rng(21)
+    t = O.gen_dna(7, 2_000_000)
+    for at in rng.integers(0, len(t) - 40, 30):  # 30 runs of 1-3 N (<= 128 rare rows)
+        t[at:at + int(rng.integers(1, 4))] = ord("N")
+    t = t.tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    o = O.Index(t)
+    pats = []
+    for m in rng.integers(33, 201, 6000):
+        i = int(rng.integers(0, len(t) - m))
+        p = bytearray(t[i:i + m])
+        pats.append(bytes(p))
+        p[int(rng.integers(0, m))] = b"ACGTN"[int(rng.integers(0, 5))]
+        pats.append(bytes(p))
+    buf, offs = O.pack_patterns(pats)
+    want = o.count_batch(buf=buf, offs=offs, nthreads=8)
+    assert (want[::2] >= 1).all()
+    for lk in ("1", "2", "0"):
+        with _env(CS_FM_LONG_KERNEL=lk):
+            got, _, _ = _count_ex(g, pats, flags=32)
+        assert np.array_equal(got, want), lk
 
 
 @pytest.mark.parametrize("stride", [1, 3, 8, 33, 64])
@@ -742,9 +793,13 @@ def test_count_verify_long(built, pkg, name):
             pats.append(tt[i:i + m])
     pats = [p for p in pats if p]
     want = [o.count(p) for p in pats]
-    for f in (0, 16, 32, 48):  # 32: CS_Q_LONG (one pattern per lane, text look-ahead)
+    for f in (0, 16, 32, 48):  # 32: CS_Q_LONG (k_count_long: one pattern per lane)
         got, _, _ = _count_ex(g, pats, flags=f)
         assert got.tolist() == want, (name, f)
+    for lk in ("0", "2"):  # CS_Q_LONG through round 2's kernel, and on the byte text
+        with _env(CS_FM_LONG_KERNEL=lk):
+            got, _, _ = _count_ex(g, pats, flags=32)
+        assert got.tolist() == want, (name, lk)
     # CS_Q_LONG at the narrow widths: uint32, and uint8 with the exception pairs
     got4, _, _ = _count_ex(g, pats, width=4, flags=32)
     assert got4.tolist() == want, name
