@@ -436,6 +436,8 @@ void free_index(cs_fm_index* h) {
   if (h->d_sa) (void)hipFree(h->d_sa);
   if (h->d_dtext) (void)hipFree(h->d_dtext);
   if (h->d_ptext) (void)hipFree(h->d_ptext);
+  if (h->route_h) (void)hipHostFree(h->route_h);
+  if (h->route_d) (void)hipFree(h->route_d);
   if (h->d_prare) (void)hipFree(h->d_prare);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);

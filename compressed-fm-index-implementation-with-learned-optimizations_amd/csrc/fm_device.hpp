@@ -177,6 +177,19 @@ __device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint6
   }
 }
 
+// Long-pattern routing (fm_query.hip launch_count_staged): seen_h is a word of pinned host
+// memory the host reads before a launch — set (system scope) by the staged count kernel
+// when its batch held a pattern longer than its one-read path takes (kFastM), once per
+// episode thanks to seen_d; while it is set, the staged kernel skips those patterns and
+// k_count_long takes them, setting used_d when there were any, and k_count_list clears
+// seen_h after a batch without them.  Routing changes which kernel counts a pattern,
+// never the count.  All null: no routing.
+struct LongRoute {
+  uint32_t* seen_h = nullptr;
+  uint32_t* seen_d = nullptr;
+  uint32_t* used_d = nullptr;
+};
+
 // A single pattern passed by value in kernel arguments (k_count_one).
 struct OnePattern {
   static constexpr uint32_t kMax = 128;

@@ -59,6 +59,13 @@ struct cs_fm_index {
   void* d_prare = nullptr;
   uint32_t nrare = 0;
   uint64_t ptext_bytes() const { return ((n + 31) / 32) * 8; }
+  // Long-pattern routing of device batches (fm_query.hip launch_count_staged): a pinned,
+  // device-mapped word the count kernels set when a batch held patterns over 32 characters
+  // (then the next batches send those to k_count_long), and two HBM words of bookkeeping.
+  // Allocated on first use.
+  mutable std::mutex route_mu;
+  mutable uint32_t* route_h = nullptr;
+  mutable uint32_t* route_d = nullptr;
   uint32_t active_levels[256] = {};
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
@@ -185,8 +192,8 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
                        uint32_t flags = 0);
 // A batch whose patterns are all longer than this takes the long-pattern count kernel
 // (CS_Q_LONG): fixed-length device batches and host batches, whose lengths are known
-// before the launch.
-constexpr uint64_t kLongPatternM = 96;
+// before the launch.  (The staged kernel's one-read path ends at 32 characters, kFastM.)
+constexpr uint64_t kLongPatternM = 32;
 // Slack after every index part in HBM (zeroed): the text verification and extract read
 // whole aligned 8-B words, up to 7 bytes past the text's last byte (fm_query.hip
 // window_eq / verify_filter / k_extract_text), so the allocation covers them.

@@ -1292,14 +1292,18 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(const uint32_t* __res
 // The count forms (two patterns per lane) are held to 6 waves per SIMD (<= 80 VGPRs, no
 // spills): left alone the compiler gives the packed and uint8 forms 95-104 VGPRs (4-5
 // waves), and the packed count took 0.392 ms per 12.5 M instead of 0.361.
-template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false>
+// kSkipLong: patterns over kFastM characters are left to k_count_long (long-pattern
+// routing, LongRoute); otherwise, with lr set, such a pattern marks lr.seen_h.
+template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false,
+          bool kSkipLong = false>
 __global__ __launch_bounds__(kBlk)
 __attribute__((amdgpu_waves_per_eu(!kLoc && U == 2 ? 6 : 1)))
 void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs,
                                                     uint64_t npat, CountOut co,
                                                     uint64_t limit, uint64_t* __restrict__ rec,
-                                                    uint64_t fixed_m, OnePass op = OnePass{}) {
+                                                    uint64_t fixed_m, OnePass op = OnePass{},
+                                                    LongRoute lr = LongRoute{}) {
   // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
   // kNoBar: the general search reads the node table through the caches instead of a
   // block-wide LDS copy, so no wave waits at a block barrier for the block's slowest
@@ -1321,7 +1325,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   for (int j = 0; j < U; ++j) kc[j] = kr[j] = 0;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U];
-  uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search
+  uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search, 4 left to k_count_long
   if (kLoc && !kOne && q0 == 0) cnt_out[npat] = 0;  // scan slot for the total
   // (A)
 #pragma unroll
@@ -1349,6 +1353,10 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     }
     if (ix.n == 0) continue;  // :81
     st[j] = 3;
+    if (kSkipLong && mm > kFastM) {
+      st[j] = 4;
+      continue;
+    }
     if (mm < K || K == 0 || mm > kFastM) continue;
     const uint32_t wl = (uint32_t)mm;
     uint32_t u[8];
@@ -1376,6 +1384,19 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     t[j] = tt;
     want[j] = ww;
     k[j] = kk;
+  }
+  if constexpr (!kLoc && !kSkipLong) {
+    // long-pattern routing: the first wave to meet a long pattern raises the host's flag
+    if (lr.seen_d) {
+      bool lg = false;
+#pragma unroll
+      for (int j = 0; j < U; ++j) lg |= m[j] > kFastM;
+      if (__any(lg) && (threadIdx.x & 63) == 0 &&
+          !__hip_atomic_load(lr.seen_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        __hip_atomic_store(lr.seen_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lr.seen_h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
   }
   // (B) the table entries (whole context records: their contexts come with them)
   uint4 w[U][4];
@@ -1478,7 +1499,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       }
     }
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if (q < npat && st[j] != 3) {
+    if (q < npat && st[j] < 3) {
       if constexpr (kOne) {
         kc[j] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
         kr[j] = rv[j];
@@ -1585,15 +1606,41 @@ __device__ __forceinline__ bool rare_in(const uint32_t* r, uint32_t nr, uint64_t
   return lo < nr && r[lo] < q + L;
 }
 
-// text[q, q + L) == P[0, L) against the 2-bit text: the window's kLongPW + 1 words in one
-// round, shifted to the window start and compared with the packed pattern pc (codes of a
-// pattern whose characters are all coded).  A rare symbol in the window is a mismatch (its
-// code 0 in the packed text stands for no pattern character).  Windows through the end of
-// the text: the byte text, cyclically.
-__device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint64_t* pc, const uint8_t* P,
-                                                 uint64_t q, uint64_t L, const uint32_t* rare) {
-  if (q + L > ix.n) return window_eq<const uint8_t*>(ix, P, q, L, nullptr);
-  const uint64_t a = q >> 5, last = (q + L - 1) >> 5;
+// The occurrence codes of P[c0, c0 + min(len, 32 kLongPW)) into pc (character i of the
+// chunk at bits 2 (i % 32) of pc[i / 32]), from aligned 8-B words of P (only words holding
+// a byte of the chunk) through the LDS map; false when a character has no code.
+__device__ __forceinline__ bool pack_pattern(const uint8_t* P, uint64_t c0, uint64_t len,
+                                             const uint16_t* cmap, uint64_t pc[kLongPW]) {
+  const uint64_t kk = len < 32ull * kLongPW ? len : 32ull * kLongPW;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(P) + c0;
+  const uint64_t* pw = reinterpret_cast<const uint64_t*>(a & ~(uintptr_t)7);
+  const uint64_t ps = a & 7, plast = (ps + kk - 1) >> 3;
+  uint64_t x[4 * kLongPW + 1];
+#pragma unroll
+  for (uint32_t i = 0; i <= 4 * kLongPW; ++i) x[i] = i <= plast ? pw[i] : 0ull;
+  bool ok = true;
+#pragma unroll
+  for (uint32_t i = 0; i < kLongPW; ++i) pc[i] = 0;
+#pragma unroll
+  for (uint32_t c = 0; c < 4 * kLongPW; ++c) {
+    const uint64_t y = text8(x[c], x[c + 1], ps);  // P[c0 + 8c, c0 + 8c + 8)
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+      if (8 * c + b < kk) {
+        const uint32_t d = cmap[(uint32_t)(y >> (8 * b)) & 0xFFu] >> 8;
+        ok &= d != kNoCode;
+        pc[c >> 2] |= (uint64_t)(d & 3u) << (2 * (8 * (c & 3) + b));
+      }
+    }
+  }
+  return ok;
+}
+
+// text[q, q + len) (len <= 32 kLongPW) against the packed codes pc: the window's words in
+// one round, shifted to its start; true when every code agrees
+__device__ __forceinline__ bool packed_chunk_eq(const DevIndex& ix, const uint64_t* pc, uint64_t q,
+                                                uint64_t len) {
+  const uint64_t a = q >> 5, last = (q + len - 1) >> 5;
   const uint32_t s = (uint32_t)(q & 31) * 2;
   uint64_t w[kLongPW + 1];
 #pragma unroll
@@ -1602,24 +1649,42 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 #pragma unroll
   for (uint32_t i = 0; i < kLongPW; ++i) {
     const uint64_t j = 32ull * i;
-    if (j < L) {
+    if (j < len) {
       const uint64_t x = s ? (w[i] >> s) | (w[i + 1] << (64 - s)) : w[i];
-      const uint64_t msk = L - j >= 32 ? ~0ull : (1ull << (2 * (L - j))) - 1;
+      const uint64_t msk = len - j >= 32 ? ~0ull : (1ull << (2 * (len - j))) - 1;
       diff |= (x ^ pc[i]) & msk;
     }
   }
-  return !diff && !rare_in(rare, ix.nrare, q, L);
+  return !diff;
+}
+
+// text[q, q + L) == P[0, L) against the 2-bit text, pc = the codes of P's first 32 kLongPW
+// characters (pack_pattern at 0, every one coded); the characters after them (patterns over
+// 175 characters at k = 15) against the byte text.  A rare symbol in the packed part of the
+// window is a mismatch (its code 0 in the packed text stands for no pattern character).
+// Windows through the end of the text: the byte text, cyclically.
+__device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint64_t* pc, const uint8_t* P,
+                                                 uint64_t q, uint64_t L, const uint32_t* rare) {
+  if (q + L > ix.n) return window_eq<const uint8_t*>(ix, P, q, L, nullptr);
+  constexpr uint64_t C = 32ull * kLongPW;
+  const uint64_t L0 = L < C ? L : C;
+  if (!packed_chunk_eq(ix, pc, q, L0) || rare_in(rare, ix.nrare, q, L0)) return false;
+  return L == L0 || window_eq<const uint8_t*>(ix, P + C, q + C, L - C, nullptr);
 }
 
 // kPT: verify against the packed text (DevIndex::ptext), else the byte text in rounds of
 // kLongWords words.  Patterns the pipeline does not answer are appended to `list` (q) for
 // k_count_list, which runs the general search.
+// skip_short: the staged kernel has counted the patterns of at most kFastM characters
+// (long-pattern routing); lr.used_d is then raised when the batch held long patterns
+// (sampled: the first wave of every 16th block).
 template <int W, bool kPT>
 __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m,
                                                      uint64_t* __restrict__ list,
-                                                     unsigned long long* __restrict__ nlist) {
+                                                     unsigned long long* __restrict__ nlist,
+                                                     bool skip_short, LongRoute lr) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   static_assert(kBlk >= 256, "one map entry per thread");
@@ -1633,6 +1698,11 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
   const uint64_t o0 = offs ? offs[q] : q * fixed_m;
   const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
   const uint8_t* P = pats + o0;
+  if (skip_short) {
+    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(m > kFastM) && threadIdx.x == 0)
+      __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (m <= kFastM) return;
+  }
   if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
     store_count<W>(co, q, m == 0 ? ix.n : 0);
     return;
@@ -1640,7 +1710,7 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
   const uint32_t K = ix.ptab_k;
   const uint64_t k = m - K;  // characters before the table part (when m >= K)
   // verification needs the window inside one rotation (k < n, as count_rest's)
-  bool fast = m >= 32 && m > K + kCtxQ && k < ix.n && (!kPT || k <= 32ull * kLongPW);
+  bool fast = m >= 32 && m > K + kCtxQ && k < ix.n;
   uint32_t t = 0, want = 0;
   bool cok = true;
   uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
@@ -1649,26 +1719,7 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
   if (fast) {
     uint32_t u[8];
     load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
-    if constexpr (kPT) {
-      // P[0, k) as aligned 8-B words (only words holding a byte of it), coded through the map
-      const uint64_t* pw = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(P) & ~(uintptr_t)7);
-      const uint64_t ps = reinterpret_cast<uintptr_t>(P) & 7, plast = (ps + k - 1) >> 3;
-      uint64_t x[4 * kLongPW + 1];
-#pragma unroll
-      for (uint32_t i = 0; i <= 4 * kLongPW; ++i) x[i] = i <= plast ? pw[i] : 0ull;
-#pragma unroll
-      for (uint32_t c = 0; c < 4 * kLongPW; ++c) {
-        const uint64_t y = text8(x[c], x[c + 1], ps);  // P[8c, 8c + 8)
-#pragma unroll
-        for (uint32_t b = 0; b < 8; ++b) {
-          if (8 * c + b < k) {
-            const uint32_t d = cmap[(uint32_t)(y >> (8 * b)) & 0xFFu] >> 8;
-            fast &= d != kNoCode;
-            pc[c >> 2] |= (uint64_t)(d & 3u) << (2 * (8 * (c & 3) + b));
-          }
-        }
-      }
-    }
+    if constexpr (kPT) fast &= pack_pattern(P, 0, k, cmap, pc);  // P[0, min(k, 160)) coded
 #pragma unroll
     for (uint32_t i = 0; i < 32; ++i) {
       const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
@@ -1769,22 +1820,38 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
       }
     }
   }
-  if (general) {
-    list[atomicAdd(nlist, 1ull)] = q;  // the general search, k_count_list
-    return;
+  // the general search for the rest (k_count_list): one append per wave
+  const uint64_t gm = __ballot(general);
+  if (gm) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t at = 0;
+    if (lane == (uint32_t)__ffsll((unsigned long long)gm) - 1u) at = atomicAdd(nlist, (unsigned long long)__popcll(gm));
+    at = __shfl(at, __ffsll((unsigned long long)gm) - 1, 64);
+    if (general) list[at + __popcll(gm & ((1ull << lane) - 1))] = q;
   }
-  store_count<W>(co, q, res);
+  if (!general) store_count<W>(co, q, res);
 }
 
 // The patterns k_count_long listed: the general search (count_pattern), the node table
 // staged in LDS by the blocks that have work; a fixed grid striding over the list, whose
 // length is read on the device.
+// With routing (lr set, long-pattern mode): block 0 also ends the mode after a batch
+// without long patterns (lr.used_d clear) and re-arms used_d otherwise.
 template <int W>
 __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, CountOut co,
                                                      uint64_t fixed_m, const uint64_t* __restrict__ list,
-                                                     const unsigned long long* __restrict__ nlist) {
+                                                     const unsigned long long* __restrict__ nlist,
+                                                     LongRoute lr) {
   __shared__ NodeTable T;
+  if (lr.used_d && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (__hip_atomic_load(lr.used_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_store(lr.used_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(lr.seen_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(lr.seen_h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
   const uint64_t nl = *nlist;
   if ((uint64_t)blockIdx.x * kBlk >= nl) return;  // uniform over the block
   load_table(T, ix.table);
@@ -3048,10 +3115,66 @@ bool qctx_staged() {
   return !(e && std::atoi(e) == 0);
 }
 
+// k_count_long over the batch (skip_short: only its patterns over kFastM characters),
+// then k_count_list over the patterns it listed; byte_text: the byte text even when the
+// index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
+cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
+                            uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
+                            bool skip_short, const LongRoute& lr, bool byte_text = false) {
+  const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
+  StreamBuf lb;
+  FMX_HIP(lb.alloc(npat * 8 + 8, st));
+  unsigned long long* nl = reinterpret_cast<unsigned long long*>(lb.as<uint64_t>() + npat);
+  FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
+  if (ix.ptext && !byte_text)
+    k_count_long<0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl,
+                                              skip_short, lr);
+  else
+    k_count_long<0, false><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl,
+                                               skip_short, lr);
+  FMX_HIP(hipGetLastError());
+  k_count_list<0><<<std::min(g, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, co, fixed_m, lb.as<uint64_t>(),
+                                                       nl, lr);
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
+}
+
+// The handle's routing words (LongRoute), allocated on first use; all null when the index
+// cannot route (k_count_long needs occurrence lines, the full SA and the text) or the
+// tuning hook CS_FM_LONG_ROUTE=0 (read per call) turns routing off.
+LongRoute long_route(const cs_fm_index* h, const DevIndex& ix) {
+  if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return LongRoute{};
+  if (const char* e = std::getenv("CS_FM_LONG_ROUTE"))
+    if (std::atoi(e) == 0) return LongRoute{};
+  std::lock_guard<std::mutex> lk(h->route_mu);
+  if (!h->route_h) {
+    void *hp = nullptr, *dp = nullptr;
+    if (hipHostMalloc(&hp, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      return LongRoute{};
+    }
+    if (hipMalloc(&dp, 64) != hipSuccess || hipMemset(dp, 0, 64) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipHostFree(hp);
+      if (dp) (void)hipFree(dp);
+      return LongRoute{};
+    }
+    std::memset(hp, 0, 64);
+    h->route_h = static_cast<uint32_t*>(hp);
+    h->route_d = static_cast<uint32_t*>(dp);
+  }
+  void* dev_h = nullptr;
+  if (hipHostGetDevicePointer(&dev_h, h->route_h, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return LongRoute{};
+  }
+  return LongRoute{static_cast<uint32_t*>(dev_h), h->route_d, h->route_d + 1};
+}
+
 // the staged kernel at count width W: table entries (context records) of U patterns per
 // lane in flight together, then their context sectors or rank steps
 template <int W>
-void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t* d_pats,
+cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t* d_pats,
                          const uint64_t* d_offs, uint64_t npat, const CountOut& co,
                          hipStream_t st, uint64_t fixed_m, bool packed) {
   const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U, read per call)
@@ -3061,6 +3184,7 @@ void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t
   }();
   const bool lo = h->line_fmt == kFmtLOcc;
   const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
+  const LongRoute route = packed || lo ? LongRoute{} : long_route(h, ix);
   if (packed && lo)
     k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                 nullptr, fixed_m);
@@ -3082,9 +3206,19 @@ void launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t
   else if (W == 8 && count_nobar())
     k_count_ctx<OccE, 2, false, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                       nullptr, fixed_m);
-  else
+  else if (d_offs && route.seen_h && *reinterpret_cast<volatile uint32_t*>(h->route_h)) {
+    // long-pattern mode (a recent batch held patterns over kFastM characters): the staged
+    // kernel counts the short ones, k_count_long the long ones
+    k_count_ctx<OccE, 2, false, false, W, false, false, true><<<g2, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+    FMX_HIP(hipGetLastError());
+    return launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, true, route);
+  } else
     k_count_ctx<OccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                nullptr, fixed_m);
+                                                                nullptr, fixed_m, OnePass{},
+                                                                d_offs ? route : LongRoute{});
+  FMX_HIP(hipGetLastError());
+  return CS_OK;
 }
 
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
@@ -3114,30 +3248,21 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
     // look-ahead rounds, k_count<OccE, false, true>), 2 = the byte text even when the
     // packed text is there.
     const char* ek = std::getenv("CS_FM_LONG_KERNEL");
-    const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
     if (ek && std::atoi(ek) == 0) {
-      k_count<OccE, false, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m);
+      k_count<OccE, false, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs,
+                                                                                    npat, co, fixed_m);
     } else {
-      StreamBuf lb;
-      FMX_HIP(lb.alloc(npat * 8 + 8, st));
-      unsigned long long* nl = reinterpret_cast<unsigned long long*>(lb.as<uint64_t>() + npat);
-      FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
-      if (ix.ptext && !(ek && std::atoi(ek) == 2))
-        k_count_long<0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl);
-      else
-        k_count_long<0, false><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl);
-      FMX_HIP(hipGetLastError());
-      k_count_list<0><<<std::min(g, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, co, fixed_m, lb.as<uint64_t>(), nl);
+      cs_status r = launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, false, LongRoute{},
+                                      ek && std::atoi(ek) == 2);
+      if (r != CS_OK) return r;
     }
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.ptab_k) {
-    if (co.width == 8) launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
-    else if (co.width == 4) launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
-    else launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
-    FMX_HIP(hipGetLastError());
-    return CS_OK;
+    if (co.width == 8) return launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
+    if (co.width == 4) return launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
+    return launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
   }
   const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
   if (packed)

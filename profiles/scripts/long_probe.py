@@ -3,8 +3,9 @@
 count forms on one index, one process (round 3).
 
 Builds the C4 index once (default 4e9 DNA), then for each pattern length m times the count of
-a Q_text batch through: the staged default path (flags 0: k_count_ctx -> general search,
-the reference for the equality check) and CS_Q_LONG with each CS_FM_LONG_KERNEL value.  Kernel time from HIP events on the launch stream (mean of --reps after a
+a Q_text batch through: the staged kernel alone (flags 0, CS_FM_LONG_ROUTE=0: k_count_ctx ->
+general search; the reference for the equality check), the default path (flags 0: routed to
+k_count_long after the first call) and CS_Q_LONG with each CS_FM_LONG_KERNEL value.  Kernel time from HIP events on the launch stream (mean of --reps after a
 warm-up); every variant's counts must equal the default path's.  Prints one JSON line.
 """
 import argparse
@@ -67,10 +68,20 @@ def main():
         ref = torch.empty(B, dtype=torch.int64, device=dev)
         o8 = torch.empty(B, dtype=torch.int64, device=dev)
         row = {}
+        os.environ["CS_FM_LONG_ROUTE"] = "0"
         mean, mn = timed(lambda: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B, ref.data_ptr(),
                                                      flags=0, stream=sh), args.reps, stream)
-        row["staged_default"] = {"ms": mean, "ms_min": mn, "patterns_per_s": B / mean * 1e3}
+        os.environ.pop("CS_FM_LONG_ROUTE")
+        row["staged_only"] = {"ms": mean, "ms_min": mn, "patterns_per_s": B / mean * 1e3}
         want = ref.clone()
+        # the default path: the warm-up call raises the routing flag, the timed calls route
+        o8.fill_(-1)
+        mean, mn = timed(lambda: idx.count_device_ex(W.pats.data_ptr(), W.offs.data_ptr(), B, o8.data_ptr(),
+                                                     flags=0, stream=sh), args.reps, stream)
+        row["default_routed"] = {"ms": mean, "ms_min": mn, "patterns_per_s": B / mean * 1e3,
+                                 "matches": bool(torch.equal(o8, want))}
+        print("[long_probe] m=%d staged %.3f routed %.3f ms" % (m, row["staged_only"]["ms"], mean),
+              file=sys.stderr, flush=True)
         for v in args.variants.split(","):
             env = {"CS_FM_LONG_KERNEL": v}
             saved = {k: os.environ.get(k) for k in ("CS_FM_LONG_KERNEL",)}

@@ -502,6 +502,9 @@ def test_count_long_kernel_large(pkg):
         with _env(CS_FM_LONG_KERNEL=lk):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert np.array_equal(got, want), lk
+    for _ in range(2):  # the default path: detection, then long-pattern routing
+        got, _, _ = _count_ex(g, pats)
+        assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("stride", [1, 3, 8, 33, 64])
@@ -800,6 +803,18 @@ def test_count_verify_long(built, pkg, name):
         with _env(CS_FM_LONG_KERNEL=lk):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert got.tolist() == want, (name, lk)
+    # long-pattern routing of the default path: the batches above raised the handle's flag,
+    # so these run the staged kernel for the short patterns and k_count_long for the rest;
+    # a batch of short patterns only ends the mode, the next mixed batch raises it again
+    short = [p for p in pats if len(p) <= 32]
+    for _ in range(2):
+        got, _, _ = _count_ex(g, pats)
+        assert got.tolist() == want, name
+        got, _, _ = _count_ex(g, short)
+        assert got.tolist() == [w for p, w in zip(pats, want) if len(p) <= 32], name
+    with _env(CS_FM_LONG_ROUTE="0"):
+        got, _, _ = _count_ex(g, pats)
+    assert got.tolist() == want, name
     # CS_Q_LONG at the narrow widths: uint32, and uint8 with the exception pairs
     got4, _, _ = _count_ex(g, pats, width=4, flags=32)
     assert got4.tolist() == want, name
