@@ -72,7 +72,8 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
-             "count_m64", "count_m64_steps", "count_m150", "count_m64_long", "count_m150_long", "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
+             "count_m64", "count_m64_steps", "count_m150", "count_m150_staged", "count_m64_long", "count_m150_long",
+             "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
              "locate_m64", "locate_m64_steps", "count_stream", "count_stream_packed",
              "count_stream_packed_u8", "host_batch",
              "extract"]
@@ -916,6 +917,7 @@ def main():
 
     # ---- N = 1 legs on the headline index ----
     lg = {}
+    m_counts = {}  # the default path's counts of the m-legs, for the other forms' equality check
     leg_errors = {}
     stream_m = B * m + (B + 1) * 8
     with LegGuard(leg_errors, "main legs"):
@@ -963,25 +965,50 @@ def main():
                     del o8
             ver = "rank steps until the range is at most 8 rows, then the rows' suffix-array entries " \
                   "and the text before them (verification)" if info.full_sa_bytes and info.text_in_hbm else None
-            for name, mm, fl in (("count_m32", 32, 0), ("count_m64", 64, 0), ("count_m64_steps", 64, 16),
-                                 ("count_m150", 150, 0), ("count_m64_long", 64, 32),
-                                 ("count_m150_long", 150, 32)):
+            longk = ("k_count_long: the last 32 characters give the context record and the candidate rows "
+                     "(inline contexts), then each candidate's suffix-array entry and its window against the "
+                     "%s text" % ("2-bit" if info.packed_text_bytes else "byte")) if ver else None
+            for name, mm, fl, env in (("count_m32", 32, 0, None), ("count_m64", 64, 0, None),
+                                      ("count_m64_steps", 64, 16, None), ("count_m150", 150, 0, None),
+                                      ("count_m150_staged", 150, 0, {"CS_FM_LONG_ROUTE": "0"}),
+                                      ("count_m64_long", 64, 32, None), ("count_m150_long", 150, 32, None)):
                 if name in legs:
                     Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
                     o8 = torch.empty(B, dtype=torch.int64, device=dev)
                     steps_what = "%d rank steps, then the left contexts" % (mm - info.prefix_k - info.context_q)
-                    r, got = count_leg(
-                        name, "Q_text %d-mers through the headline index: prefix table, %s%s" % (
-                            mm, ver if ver and not fl & 16 else steps_what,
-                            " (CS_Q_NO_VERIFY)" if fl & 16 else
-                            " (CS_Q_LONG: one pattern per lane, the text compared with look-ahead)"
-                            if fl & 32 else ""),
-                        idx, info, wl, Wm,
-                        lambda Wm=Wm, o8=o8, fl=fl: idx.count_device_ex(Wm.pats.data_ptr(), Wm.offs.data_ptr(), B,
-                                                                        o8.data_ptr(), flags=fl, stream=sh),
-                        fl, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
-                        lambda o8=o8: o8.cpu().numpy())
+                    if fl & 16:
+                        what = "prefix table, %s (CS_Q_NO_VERIFY)" % steps_what
+                    elif fl & 32:
+                        what = "%s (CS_Q_LONG: asked for directly)" % (longk or steps_what)
+                    elif env:
+                        what = ("the staged kernel alone (CS_FM_LONG_ROUTE=0, round 2's default path): prefix "
+                                "table, %s" % (ver or steps_what))
+                    elif mm > 32 and longk:
+                        what = ("the default path: after the first batch with patterns over 32 characters the "
+                                "staged kernel leaves them to %s" % longk)
+                    else:
+                        what = "prefix table, %s" % (ver or steps_what)
+                    saved = {k: os.environ.get(k) for k in (env or {})}
+                    os.environ.update(env or {})
+                    try:
+                        r, got = count_leg(
+                            name, "Q_text %d-mers through the headline index: %s" % (mm, what),
+                            idx, info, wl, Wm,
+                            lambda Wm=Wm, o8=o8, fl=fl: idx.count_device_ex(Wm.pats.data_ptr(), Wm.offs.data_ptr(),
+                                                                            B, o8.data_ptr(), flags=fl, stream=sh),
+                            fl, B * mm + (B + 1) * 8 + 8 * B, max(3, steps // 4), 1, stream, sh, dev, None,
+                            lambda o8=o8: o8.cpu().numpy())
+                    finally:
+                        for k_, v_ in saved.items():
+                            if v_ is None:
+                                os.environ.pop(k_, None)
+                            else:
+                                os.environ[k_] = v_
                     r["found_frac"] = float((got >= 1).mean())
+                    if name == "count_m%d" % mm:
+                        m_counts[mm] = got
+                    else:
+                        r["matches_default"] = bool(np.array_equal(got, m_counts[mm])) if mm in m_counts else None
                     lg[name] = r
                     del Wm, o8
             if "count_unif" in legs and args.queries == "text":
@@ -1128,10 +1155,17 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu and counts is not None:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle as O  # CPU baseline / checker only
-            # the process's CPU share: OMP_NUM_THREADS on the GPU box (16 per GPU there; the
-            # machine's count is many times that), else the affinity set
-            threads = (args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-                       or len(os.sched_getaffinity(0)))
+            # the process's CPU share: the affinity set, capped by OMP_NUM_THREADS where the pool
+            # sets it (the GPU box: 16 per GPU; the host's core count is many times that and is
+            # not ours to use) — reported with the host's count beside it
+            affinity = len(os.sched_getaffinity(0))
+            omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+            threads = args.cpu_threads or (min(affinity, omp) if omp else affinity)
+            cpu_share = {"cores_used": threads, "host_cores": os.cpu_count(), "affinity_cores": affinity,
+                         "omp_num_threads": omp or None,
+                         "share": ("--cpu-threads" if args.cpu_threads else
+                                   "OMP_NUM_THREADS (the pool's CPU share per GPU) within the affinity set"
+                                   if omp and omp < affinity else "the whole affinity set")}
             Q = args.cpu_queries
             if Q is None:
                 Q = max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16, 2 * threads)
@@ -1156,6 +1190,7 @@ def main():
                           "(oracle/fm_oracle.c faithful=1), %d host threads" % (Qp, nt),
                 "p50_us": float(np.median(lat) / 1e3), "seconds": cpu_s, "prep_s": prep_s,
                 "matches_gpu": bool(np.array_equal(cnt, counts[:Qp].astype(np.uint64)))}
+            port.update(cpu_share)
             res["cpu_baseline"] = port
             if O.ref_lib() is not None:
                 # the genuine reference's FMIndex::count / locate (oracle/_ref/libcs_ref.so,
@@ -1177,7 +1212,7 @@ def main():
                               % (Q, Q // nt, nt),
                     "p50_us": float(np.median(rlat) / 1e3), "seconds": ref_s,
                     "prep_s": prep_s + rprep,
-                    "matches_gpu": bool(np.array_equal(rcnt, counts[:Q].astype(np.uint64)))}
+                    "matches_gpu": bool(np.array_equal(rcnt, counts[:Q].astype(np.uint64))), **cpu_share}
                 res["cpu_port"] = port
                 # locate: one pattern per thread (a C4 locate is the count's search plus ~31
                 # LF steps, each a wavelet rank with the O(n) scans)

@@ -192,8 +192,8 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
                        uint32_t flags = 0);
 // A batch whose patterns are all longer than this takes the long-pattern count kernel
 // (CS_Q_LONG): fixed-length device batches and host batches, whose lengths are known
-// before the launch.  (The staged kernel's one-read path ends at 32 characters, kFastM.)
-constexpr uint64_t kLongPatternM = 32;
+// before the launch: 32 characters and more (k_count_long reads a pattern's last 32).
+constexpr uint64_t kLongPatternM = 31;
 // Slack after every index part in HBM (zeroed): the text verification and extract read
 // whole aligned 8-B words, up to 7 bytes past the text's last byte (fm_query.hip
 // window_eq / verify_filter / k_extract_text), so the allocation covers them.

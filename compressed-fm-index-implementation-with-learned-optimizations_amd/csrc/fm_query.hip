@@ -1292,8 +1292,9 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(const uint32_t* __res
 // The count forms (two patterns per lane) are held to 6 waves per SIMD (<= 80 VGPRs, no
 // spills): left alone the compiler gives the packed and uint8 forms 95-104 VGPRs (4-5
 // waves), and the packed count took 0.392 ms per 12.5 M instead of 0.361.
-// kSkipLong: patterns over kFastM characters are left to k_count_long (long-pattern
-// routing, LongRoute); otherwise, with lr set, such a pattern marks lr.seen_h.
+// kSkipLong: patterns of kFastM characters or more whose search the one read cannot finish
+// (m > k + kCtxQ) are left to k_count_long (long-pattern routing, LongRoute); otherwise,
+// with lr set, such a pattern marks lr.seen_h.
 template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false,
           bool kSkipLong = false>
 __global__ __launch_bounds__(kBlk)
@@ -1353,7 +1354,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     }
     if (ix.n == 0) continue;  // :81
     st[j] = 3;
-    if (kSkipLong && mm > kFastM) {
+    if (kSkipLong && mm >= kFastM && mm > K + kCtxQ) {  // k_count_long's (one read cannot answer it)
       st[j] = 4;
       continue;
     }
@@ -1390,7 +1391,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     if (lr.seen_d) {
       bool lg = false;
 #pragma unroll
-      for (int j = 0; j < U; ++j) lg |= m[j] > kFastM;
+      for (int j = 0; j < U; ++j) lg |= m[j] >= kFastM && m[j] > K + kCtxQ;
       if (__any(lg) && (threadIdx.x & 63) == 0 &&
           !__hip_atomic_load(lr.seen_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         __hip_atomic_store(lr.seen_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1675,10 +1676,15 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 // kPT: verify against the packed text (DevIndex::ptext), else the byte text in rounds of
 // kLongWords words.  Patterns the pipeline does not answer are appended to `list` (q) for
 // k_count_list, which runs the general search.
-// skip_short: the staged kernel has counted the patterns of at most kFastM characters
+// skip_short: the staged kernel has counted all but the long patterns (m >= kFastM, m > k + kCtxQ)
 // (long-pattern routing); lr.used_d is then raised when the batch held long patterns
 // (sampled: the first wave of every 16th block).
-template <int W, bool kPT>
+// kBytes: measurement twin (bench.py's roofline) — co.out receives each pattern's random
+// algorithmic bytes instead of its count: the table entry, the context sector(s), per
+// candidate its SA sector (32 B) and the text words of its window.
+// (90 VGPRs, 5 waves per SIMD: held to 80 with waves_per_eu(6) it spills and runs 12-15 %
+// slower, profiles/r03/long_probe_w6_m300.json)
+template <int W, bool kPT, bool kBytes = false>
 __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m,
@@ -1699,14 +1705,17 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
   const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
   const uint8_t* P = pats + o0;
   if (skip_short) {
-    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(m > kFastM) && threadIdx.x == 0)
+    const bool mine = m >= kFastM && m > ix.ptab_k + kCtxQ;  // the staged kernel skipped it
+    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(mine) && threadIdx.x == 0)
       __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (m <= kFastM) return;
+    if (!mine) return;
   }
   if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
-    store_count<W>(co, q, m == 0 ? ix.n : 0);
+    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
+    else store_count<W>(co, q, m == 0 ? ix.n : 0);
     return;
   }
+  uint64_t by = 0;  // kBytes
   const uint32_t K = ix.ptab_k;
   const uint64_t k = m - K;  // characters before the table part (when m >= K)
   // verification needs the window inside one rotation (k < n, as count_rest's)
@@ -1741,6 +1750,7 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
     uint64_t sp, ep;
     uint32_t d[6] = {0, 0, 0, 0, 0, 0};  // inline contexts as u16 entries, row i in entry i
     uint32_t qf = 0;                     // characters they answer (0: none inline)
+    by += ix.ptab_rec == 1 ? 32u : ix.ptab_rec == 2 ? 16u : 8u;
     if (ix.ptab_rec == 2) {
       const uint4 a = static_cast<const uint4*>(ix.ptab)[t];
       const uint32_t wc = a.y & 15u;
@@ -1789,6 +1799,7 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) + base);
       const uint4 x0 = p[0], x1 = p[1];
       const uint4 x2 = hi > 16 ? p[2] : make_uint4(0, 0, 0, 0), x3 = hi > 16 ? p[3] : make_uint4(0, 0, 0, 0);
+      by += hi > 16 ? 64u : 32u;
       const uint32_t dw[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
                                x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
       const uint32_t msk = ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc;
@@ -1813,6 +1824,15 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
         cand &= cand - 1;
         const uint64_t p = ix.vsa[base + i];
         const uint64_t wq = p >= k ? p - k : p + n - k;
+        if constexpr (kBytes) {  // the SA sector, then the window's words
+          constexpr uint64_t C = 32ull * kLongPW;
+          by += 32;
+          if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
+          else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
+          else by += 8 * (((wq + (L < C ? L : C) - 1) >> 5) - (wq >> 5) + 1) +
+                     (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
+          continue;
+        }
         bool eq;
         if constexpr (kPT) eq = window_eq_packed(ix, pc, P, wq, L, rare);
         else eq = window_eq_long<kLongWords>(ix, P, wq, L);
@@ -1829,7 +1849,9 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
     at = __shfl(at, __ffsll((unsigned long long)gm) - 1, 64);
     if (general) list[at + __popcll(gm & ((1ull << lane) - 1))] = q;
   }
-  if (!general) store_count<W>(co, q, res);
+  if (general) return;
+  if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
+  else store_count<W>(co, q, res);
 }
 
 // The patterns k_count_long listed: the general search (count_pattern), the node table
@@ -1837,7 +1859,8 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
 // length is read on the device.
 // With routing (lr set, long-pattern mode): block 0 also ends the mode after a batch
 // without long patterns (lr.used_d clear) and re-arms used_d otherwise.
-template <int W>
+// kBytes: k_count_long's measurement twin (the general search's bytes into co.out).
+template <int W, bool kBytes = false>
 __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, CountOut co,
                                                      uint64_t fixed_m, const uint64_t* __restrict__ list,
@@ -1859,7 +1882,13 @@ __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t*
   for (uint64_t i = blockIdx.x * (uint64_t)kBlk + threadIdx.x; i < nl; i += (uint64_t)gridDim.x * kBlk) {
     const uint64_t q = list[i];
     const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
-    store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
+    if constexpr (kBytes) {
+      uint64_t by = 0;
+      (void)count_pattern<OccE>(ix, T, pats + o0, m, &by);
+      static_cast<uint64_t*>(co.out)[q] = by;
+    } else {
+      store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
+    }
   }
 }
 
@@ -3115,28 +3144,34 @@ bool qctx_staged() {
   return !(e && std::atoi(e) == 0);
 }
 
-// k_count_long over the batch (skip_short: only its patterns over kFastM characters),
+// k_count_long over the batch (skip_short: only its long patterns, as k_count_ctx's kSkipLong),
 // then k_count_list over the patterns it listed; byte_text: the byte text even when the
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
-cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
-                            uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
-                            bool skip_short, const LongRoute& lr, bool byte_text = false) {
+template <bool kBytes>
+cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
+                              uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
+                              bool skip_short, const LongRoute& lr, bool byte_text) {
   const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
   StreamBuf lb;
   FMX_HIP(lb.alloc(npat * 8 + 8, st));
   unsigned long long* nl = reinterpret_cast<unsigned long long*>(lb.as<uint64_t>() + npat);
   FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
   if (ix.ptext && !byte_text)
-    k_count_long<0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl,
-                                              skip_short, lr);
+    k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(),
+                                                      nl, skip_short, lr);
   else
-    k_count_long<0, false><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(), nl,
-                                               skip_short, lr);
+    k_count_long<0, false, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(),
+                                                       nl, skip_short, lr);
   FMX_HIP(hipGetLastError());
-  k_count_list<0><<<std::min(g, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, co, fixed_m, lb.as<uint64_t>(),
-                                                       nl, lr);
+  k_count_list<0, kBytes><<<std::min(g, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, co, fixed_m,
+                                                               lb.as<uint64_t>(), nl, lr);
   FMX_HIP(hipGetLastError());
   return CS_OK;
+}
+cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
+                            uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
+                            bool skip_short, const LongRoute& lr, bool byte_text = false) {
+  return launch_count_long_t<false>(ix, d_pats, d_offs, npat, co, st, fixed_m, skip_short, lr, byte_text);
 }
 
 // The handle's routing words (LongRoute), allocated on first use; all null when the index
@@ -3207,7 +3242,7 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
     k_count_ctx<OccE, 2, false, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                       nullptr, fixed_m);
   else if (d_offs && route.seen_h && *reinterpret_cast<volatile uint32_t*>(h->route_h)) {
-    // long-pattern mode (a recent batch held patterns over kFastM characters): the staged
+    // long-pattern mode (a recent batch held patterns of kFastM characters or more): the staged
     // kernel counts the short ones, k_count_long the long ones
     k_count_ctx<OccE, 2, false, false, W, false, false, true><<<g2, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
@@ -3289,8 +3324,19 @@ cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t 
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                              uint64_t npat, uint64_t* d_out, hipStream_t st, uint32_t flags) {
   if (!npat) return CS_OK;
-  FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), query_dev(h, flags), d_pats,
-               d_offs, npat, d_out);
+  const DevIndex ix = query_dev(h, flags);
+  // the patterns k_count_long counts (CS_Q_LONG: all of them; routed device batches: those
+  // of kFastM characters or more) take its twin, the rest the general search's
+  const bool lk = h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa;
+  const char* ek = std::getenv("CS_FM_LONG_KERNEL");
+  const bool old = ek && std::atoi(ek) == 0;
+  if (!(lk && (flags & CS_Q_LONG) && !old))
+    FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), ix, d_pats, d_offs, npat, d_out);
+  if (lk && !old && ((flags & CS_Q_LONG) || long_route(h, ix).seen_h)) {
+    const CountOut co{d_out, nullptr, nullptr, 0, 8};
+    return launch_count_long_t<true>(ix, d_pats, d_offs, npat, co, st, 0, !(flags & CS_Q_LONG), LongRoute{},
+                                     ek && std::atoi(ek) == 2);
+  }
   return CS_OK;
 }
 

@@ -84,7 +84,7 @@ def main():
               file=sys.stderr, flush=True)
         for v in args.variants.split(","):
             env = {"CS_FM_LONG_KERNEL": v}
-            saved = {k: os.environ.get(k) for k in ("CS_FM_LONG_KERNEL",)}
+            saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             try:
                 o8.fill_(-1)
