@@ -28,7 +28,8 @@ import sys
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
               "count_m64": "count", "count_m64_steps": "count", "count_m150": "count",
-              "count_fixed": "count", "wm_count": "count",
+              "count_fixed": "count", "wm_count": "count", "count_m150_staged": "count",
+              "count_m64_long": "count", "count_m150_long": "count",
               "wm_lf_loop": "count", "learned_count": "count", "learned_lf_loop": "count",
               "count_unif": "count",
               "locate": ("k_locate_sa", "k_locate_sa_wide", "k_walk_fused", "k_walk_fused_wide",
@@ -54,14 +55,22 @@ def short(name):
     """Readable kernel name: k_count_ctx (count) / k_count_ctx_loc (locate phase 1) with
     the template's U, packed flag and count width; the others by their base name."""
     m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)"
-                  r"(?:, (true|false))?(?:, (true|false))?>", name)
+                  r"(?:, (true|false))?(?:, (true|false))?(?:, (true|false))?>", name)
     if m:
-        eng, u, loc, packed, w, nobar, one = m.groups()
+        eng, u, loc, packed, w, nobar, one, skip = m.groups()
         if one == "true":
             return "k_count_ctx_onepass"
         if loc == "true":
             return "k_count_ctx_loc"
-        return "k_count_ctx%s_w%s" % ("_packed" if packed == "true" else "", w)
+        return "k_count_ctx%s%s_w%s" % ("_packed" if packed == "true" else "",
+                                         "_skiplong" if skip == "true" else "", w)
+    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?>", name)
+    if m:  # the third argument: the measurement twin (kBytes)
+        return "k_count_long%s%s" % ("_ptext" if m.group(2) == "true" else "_btext",
+                                     "_bytes" if m.group(3) == "true" else "")
+    m = re.search(r"k_count_list<(\d)(?:, (true|false))?>", name)
+    if m:
+        return "k_count_list_bytes" if m.group(2) == "true" else "k_count_list"
     m = re.search(r"k_count_qctx<(\d), (\d)>", name)
     if m:
         return "k_count_qctx_w%s" % m.group(2)
@@ -117,11 +126,21 @@ def main():
         want = LEG_KERNEL.get(leg, "count")
         if want == "count":
             cands = [n for n in res["pmc"] if n.startswith("k_count_ctx_") or n.startswith("k_count_qctx")
-                     or n == "k_count"]
+                     or n == "k_count" or (n.startswith("k_count_long") and not n.endswith("_bytes"))]
         else:  # the phase-2 kernel that ran longest (a lane per pattern, or a block per wide range)
             want = (want,) if isinstance(want, str) else want
             cands = [n for n in res["pmc"] if n in want]
-        kname = max(cands, key=lambda n: res["kernels"].get(n, {}).get("total_ns", 0)) if cands else None
+        # the timed launches: the candidate dispatched most often (a routed leg's first, warm-up
+        # launch runs the staged kernel once), then the longest in total
+        kname = max(cands, key=lambda n: (res["kernels"].get(n, {}).get("dispatches", 0),
+                                          res["kernels"].get(n, {}).get("total_ns", 0))) if cands else None
+        # a routed long-pattern count runs as k_count_ctx (skipping the long patterns),
+        # k_count_long and k_count_list: the leg's launch is their sum
+        group = [kname]
+        if kname and kname.startswith("k_count_long"):
+            group += [n for n in res["pmc"] if n == "k_count_list" or n.endswith("_skiplong_w8")
+                      or (n.startswith("k_count_ctx_") and "skiplong" in n)]
+            group = sorted(set(group))
         lo = (b.get("legs") or {}).get(leg) or {}
         if leg == "count":
             stream_rd = (b.get("count") or {}).get("stream_read_bytes_per_launch")
@@ -131,17 +150,21 @@ def main():
             stream_rd = lo.get("phase2_stream_read_bytes")
         wl = lo.get("workload_key") or b.get("workload_key")  # the leg's own index
         kc = res["pmc"].get(kname, {}) if kname else {}
+        if len(group) > 1:  # sums over the group (per launch of each)
+            kc = {"FETCH_SIZE": sum(res["pmc"].get(n, {}).get("FETCH_SIZE", 0) for n in group),
+                  "l2_hit_rate": kc.get("l2_hit_rate")}
         if kname and "FETCH_SIZE" in kc and stream_rd is not None:
             req = kc["FETCH_SIZE"] * 1024 / 64
             # a leg whose kernel streams (thousands of contiguous SA rows per range): every
             # request is a 128-B streaming read tallied at 64 B (the guide's x2)
             hbm = (req * 128 if leg in LEG_STREAMED
                    else stream_rd + max(req - stream_rd / 128, 0) * 32)
-            e = {"leg": leg, "kernel": kname, "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
+            e = {"leg": leg, "kernel": "+".join(group) if len(group) > 1 else kname,
+                 "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
                  "read_requests_per_launch": req, "stream_read_bytes_per_launch": stream_rd,
                  "hbm_bytes_per_launch": hbm,
                  "l2_hit_rate": kc.get("l2_hit_rate"),
-                 "kernel_mean_ns_profiled": res["kernels"].get(kname, {}).get("mean_ns"),
+                 "kernel_mean_ns_profiled": sum(res["kernels"].get(n, {}).get("mean_ns", 0) for n in group),
                  "tag": tag}
             e["workload"] = wl
             pmc_legs["%s|%s" % (wl, leg)] = e
