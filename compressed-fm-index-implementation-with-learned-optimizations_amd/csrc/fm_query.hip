@@ -1684,6 +1684,10 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 // candidate its SA sector (32 B) and the text words of its window.
 // (90 VGPRs, 5 waves per SIMD: held to 80 with waves_per_eu(6) it spills and runs 12-15 %
 // slower, profiles/r03/long_probe_w6_m300.json)
+// (Staging the block's patterns in LDS with coalesced 16-B loads, instead of each lane's
+// 8-B loads at a stride of m bytes, was measured: 150-mers 1.91 -> 1.75 ms, but 32- to
+// 100-mers 5-18 % slower — the 38-KB stage leaves 4 waves per SIMD —
+// profiles/r03/long_probe_lds_stage.json; not kept.)
 template <int W, bool kPT, bool kBytes = false>
 __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
@@ -1829,8 +1833,9 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
           by += 32;
           if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
           else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
-          else by += 8 * (((wq + (L < C ? L : C) - 1) >> 5) - (wq >> 5) + 1) +
-                     (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
+          else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
+            by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
+                  (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
           continue;
         }
         bool eq;

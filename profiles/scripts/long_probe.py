@@ -83,7 +83,8 @@ def main():
         print("[long_probe] m=%d staged %.3f routed %.3f ms" % (m, row["staged_only"]["ms"], mean),
               file=sys.stderr, flush=True)
         for v in args.variants.split(","):
-            env = {"CS_FM_LONG_KERNEL": v}
+            # a CS_FM_LONG_KERNEL value, or KEY=VAL[+KEY=VAL] engine hooks
+            env = dict(x.split("=", 1) for x in v.split("+")) if "=" in v else {"CS_FM_LONG_KERNEL": v}
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             try:
