@@ -1063,16 +1063,30 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
 
 // the patterns of a k_count_ctx lane that need the general search (st == 3); kOne: the
 // locate results stay in the lane's registers (kc, kr)
+// rng: k_count_ctx's s_rng ([U][kBlk][2]): the range after the table of a pattern with st 5
 template <class E, int U, bool kLoc, bool kPacked, int W, bool kOne = false>
 __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable& T,
                                              const uint8_t* __restrict__ pats, const uint8_t* st,
                                              const uint64_t* o0, const uint32_t* m, uint64_t q0,
                                              const CountOut& co, uint64_t limit,
                                              uint64_t* __restrict__ rec, uint64_t* kc = nullptr,
-                                             uint64_t* kr = nullptr) {
+                                             uint64_t* kr = nullptr, const uint64_t* rng = nullptr) {
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
 #pragma unroll
   for (int j = 0; j < U; ++j) {
+    if constexpr (!kLoc) {
+      if (st[j] == 5) {  // from the range the table entry gave, m - ptab_k characters left
+        const uint64_t q = q0 + (uint64_t)j * kBlk;
+        const uint64_t* r = rng + 2 * ((uint64_t)j * kBlk + threadIdx.x);
+        const uint64_t k = m[j] - ix.ptab_k;
+        if constexpr (kPacked) {
+          store_count<W>(co, q, count_rest<E>(ix, T, PackedDna{o0[j]}, k, r[0], r[1], nullptr, nullptr));
+        } else {
+          store_count<W>(co, q, count_rest<E>(ix, T, pats + o0[j], k, r[0], r[1], nullptr, nullptr));
+        }
+        continue;
+      }
+    }
     if (st[j] != 3) continue;
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if constexpr (kLoc) {
@@ -1296,7 +1310,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(const uint32_t* __res
 // (m > k + kCtxQ) are left to k_count_long (long-pattern routing, LongRoute); otherwise,
 // with lr set, such a pattern marks lr.seen_h.
 template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false,
-          bool kSkipLong = false>
+          bool kSkipLong = false, bool kRng = true>
 __global__ __launch_bounds__(kBlk)
 __attribute__((amdgpu_waves_per_eu(!kLoc && U == 2 ? 6 : 1)))
 void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
@@ -1313,6 +1327,11 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // node table only when one of its patterns needs the general search
   __shared__ uint16_t cmap[256];
   __shared__ NodeTable T;
+  // count forms: the range [sp, ep) of a pattern the general search finishes (st 5), kept
+  // here across the barrier instead of in registers or read again from its table entry
+  // (kRng; A/B in one process, profiles/r03/ab_range_across_barrier*.json: headline 0.389
+  // vs 0.388 ms, 24-mers 1.32 vs 1.40 ms, repetitive DNA 2.56 vs 2.71 ms)
+  __shared__ uint64_t s_rng[kLoc ? 1 : U][kLoc ? 1 : kBlk][2];
   static_assert(kBlk >= 256, "one map entry per thread");
   static_assert(!kOne || (kLoc && !kNoBar), "the one-call locate is a locate with barriers");
   if (threadIdx.x < 256)
@@ -1326,7 +1345,9 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   for (int j = 0; j < U; ++j) kc[j] = kr[j] = 0;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U];
-  uint8_t st[U];  // 0 done, 1 table, 2 context, 3 general search, 4 left to k_count_long
+  // 0 done, 1 table, 2 context, 3 general search, 4 left to k_count_long, 5 general search
+  // from the range after the table (s_rng)
+  uint8_t st[U];
   if (kLoc && !kOne && q0 == 0) cnt_out[npat] = 0;  // scan slot for the total
   // (A)
 #pragma unroll
@@ -1461,6 +1482,10 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       } else {
         w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
       }
+    } else if constexpr (!kLoc && kRng) {
+      st[j] = 5;  // too wide for the contexts, or no context key: the general search
+      s_rng[j][threadIdx.x][0] = sp[j];
+      s_rng[j][threadIdx.x][1] = ep[j];
     } else {
       st[j] = 3;
     }
@@ -1482,8 +1507,13 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       }
       const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
       const uint32_t mm = match & in;
-      if (esc & in) {
+      if (esc & in) {  // a rare symbol in a row's chain
         st[j] = 3;
+        if constexpr (!kLoc && kRng) {
+          st[j] = 5;
+          s_rng[j][threadIdx.x][0] = sp[j];
+          s_rng[j][threadIdx.x][1] = ep[j];
+        }
       } else if (!kLoc || mm == 0) {
         res[j] = (uint64_t)__popc(mm);
         st[j] = 0;
@@ -1515,9 +1545,11 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // the general search for the rest, with only (o0, m) of each pattern still live
   bool general = false;
 #pragma unroll
-  for (int j = 0; j < U; ++j) general |= st[j] == 3;
+  for (int j = 0; j < U; ++j) general |= st[j] == 3 || st[j] == 5;
   if constexpr (kNoBar) {
-    if (general) general_rest<E, U, kLoc, kPacked, W>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec);
+    if (general)
+      general_rest<E, U, kLoc, kPacked, W>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec, nullptr, nullptr,
+                                           &s_rng[0][0][0]);
     return;
   }
   if constexpr (kOne) {
@@ -1532,7 +1564,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   if (!__syncthreads_or(general)) return;
   load_table(T, ix.table);
   __syncthreads();
-  general_rest<E, U, kLoc, kPacked, W>(ix, T, pats, st, o0, m, q0, co, limit, rec);
+  general_rest<E, U, kLoc, kPacked, W>(ix, T, pats, st, o0, m, q0, co, limit, rec, nullptr, nullptr,
+                                       &s_rng[0][0][0]);
 }
 
 // Long patterns (round 3; CS_Q_LONG, fixed-length batches over kLongPatternM, host chunks
