@@ -249,17 +249,19 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
                               hipStream_t st, PhaseLog& plog, DevBuf* sa_pending = nullptr);
 
 // Text-position sample stride (inverse-SA samples for extract; walk-line marks and
-// their position samples for locate): an eighth of the SSA stride, a quarter for wide
-// indexes (n >= 2^32, u64 samples: their HBM goes to the left contexts and context
-// records first; their inverse-SA samples are thinned to every second one after the
-// walk lines are built, thin_isa), at least 1.  A locate walk then averages about pstride / 2 steps instead of
-// stride / 2, an extract (stride - pstride) / 2 fewer; the reference's row-sampled
-// SSA (fm_index.cpp:57-66) is kept as is.  The samples cost 2 x sample bytes x
-// n / pstride (C4: 4 GB, C5: 32 GB).  C4 walk of 12.5 M positions: 1.8 ms at
-// pstride 8, 1.3 ms at 4 (profiles/r01/locate_phases_c4_p*.json).  CS_FM_PSTRIDE
+// their position samples for locate): an eighth of the SSA stride, at least 1.  A locate
+// walk then averages about pstride / 2 steps instead of stride / 2, an extract
+// (stride - pstride) / 2 fewer; the reference's row-sampled SSA (fm_index.cpp:57-66) is
+// kept as is.  The walk's position samples cost 4 B (narrow) or 5 B (wide: 40-bit
+// entries) x n / pstride (C4: 4 GB, C5: 40 GB); a wide index's inverse-SA samples (u64) are
+// thinned to every eighth once the walk lines are built (thin_isa: C5 8 GB), so its HBM
+// still goes to the left contexts and context records first (round 2 kept C5 at pstride
+// 8 with u64 samples, 3.2 walk steps per position).  C4 walk of 12.5 M positions: 1.8 ms
+// at pstride 8, 1.3 ms at 4 (profiles/r01/locate_phases_c4_p*.json).  CS_FM_PSTRIDE
 // overrides.
 static uint32_t position_stride(uint32_t stride, bool wide) {
-  uint32_t p = stride / (wide ? 4u : 8u);
+  (void)wide;
+  uint32_t p = stride / 8u;
   if (const char* e = std::getenv("CS_FM_PSTRIDE")) p = (uint32_t)std::atoi(e);
   return p ? p : 1u;
 }
@@ -462,8 +464,8 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   }
   FMX_HIP(hipStreamSynchronize(st));
   bwt.release();
-  if (h->wide && h->nisa) {  // the walk marks are built: extract keeps every second sample
-    cs_status ts = thin_isa(h, 2, st);
+  if (h->wide && h->nisa) {  // the walk marks are built: extract keeps every eighth sample
+    cs_status ts = thin_isa(h, 8, st);
     if (ts != CS_OK) return ts;
   }
   plog.mark("wavelet levels");
@@ -549,7 +551,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   if (sa_pending && sa_pending->p) {
     // budget builds: the full suffix array replaces the walk lines and their position
     // samples when the index still fits its budget with it
-    const uint64_t walk_b = (h->d_walk ? h->nwalk * 32 : 0) + (h->d_wssa ? h->nwssa * h->sample_bytes() : 0);
+    const uint64_t walk_b = (h->d_walk ? h->nwalk * 32 : 0) + (h->d_wssa ? h->nwssa * h->wssa_bytes() : 0);
     if (index_hbm_bytes(h) + n * 4 <= h->hbm_budget + walk_b) {
       if (h->d_walk) FMX_HIP(hipFree(h->d_walk));
       if (h->d_wssa) FMX_HIP(hipFree(h->d_wssa));

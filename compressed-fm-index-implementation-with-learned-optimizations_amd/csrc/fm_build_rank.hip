@@ -675,10 +675,11 @@ __global__ void k_walk_base(uint32_t* __restrict__ lines, const uint64_t* __rest
   }
 }
 
-// position samples in mark order: wssa[mark_rank(isa[k])] = k * pstride
-template <class W, class SampleT>
+// position samples in mark order: wssa[mark_rank(isa[k])] = k * pstride; EB = bytes per
+// entry (4, or 5: 40-bit little-endian entries, written byte by byte — entries are disjoint)
+template <class W, class SampleT, int EB>
 __global__ void k_walk_samples(const SampleT* __restrict__ isa, uint64_t nisa, uint32_t pstride,
-                               const void* __restrict__ lines, SampleT* __restrict__ wssa) {
+                               const void* __restrict__ lines, void* __restrict__ wssa) {
   const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nisa; k += gs) {
     uint64_t q;
@@ -686,7 +687,14 @@ __global__ void k_walk_samples(const SampleT* __restrict__ isa, uint64_t nisa, u
     W::locate((uint64_t)isa[k], q, o);
     typename W::Raw v;
     W::load(lines, q, v);
-    wssa[W::mark_rank(v, o)] = (SampleT)(k * pstride);
+    const uint64_t i = W::mark_rank(v, o), val = k * pstride;
+    if constexpr (EB == 5) {
+      uint8_t* b = static_cast<uint8_t*>(wssa) + 5 * i;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) b[j] = (uint8_t)(val >> (8 * j));
+    } else {
+      static_cast<uint32_t*>(wssa)[i] = (uint32_t)val;
+    }
   }
 }
 
@@ -727,15 +735,14 @@ cs_status build_walk_t(const uint8_t* bwt, uint64_t n, const CodeMap& map, bool 
   }
   if (pos_marks) {
     h->nwssa = h->nisa;
-    FMX_HIP(hipMalloc(&h->d_wssa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
+    h->wssa_eb = h->wide ? 5u : 4u;  // positions < 2^40 (n < 2^38)
+    FMX_HIP(hipMalloc(&h->d_wssa, h->nisa * h->wssa_eb + kPartPad));  // + the dword past the last entry
     if (h->wide)
-      k_walk_samples<W, uint64_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
-          static_cast<const uint64_t*>(h->d_isa), h->nisa, h->pstride, h->d_walk,
-          static_cast<uint64_t*>(h->d_wssa));
+      k_walk_samples<W, uint64_t, 5><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
+          static_cast<const uint64_t*>(h->d_isa), h->nisa, h->pstride, h->d_walk, h->d_wssa);
     else
-      k_walk_samples<W, uint32_t><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
-          static_cast<const uint32_t*>(h->d_isa), h->nisa, h->pstride, h->d_walk,
-          static_cast<uint32_t*>(h->d_wssa));
+      k_walk_samples<W, uint32_t, 4><<<grid_for(h->nisa, kBlk, 16384), kBlk, 0, st>>>(
+          static_cast<const uint32_t*>(h->d_isa), h->nisa, h->pstride, h->d_walk, h->d_wssa);
     FMX_HIP(hipGetLastError());
   }
   FMX_HIP(hipStreamSynchronize(st));
@@ -758,7 +765,7 @@ cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_i
   if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
     if (std::string(e) == "row") pos_marks = false;
   const uint64_t rows = h->wide ? WalkLineW::kRows : WalkLine::kRows;
-  if (!hbm_room(h, (n / rows + 1) * 32 + (pos_marks ? h->nisa * h->sample_bytes() : 0))) {
+  if (!hbm_room(h, (n / rows + 1) * 32 + (pos_marks ? h->nisa * (h->wide ? 5u : 4u) : 0))) {
     h->walk_marks = 0;  // locate walks over the rank structure instead
     return CS_OK;
   }

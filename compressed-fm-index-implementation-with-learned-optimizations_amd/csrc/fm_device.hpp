@@ -109,7 +109,8 @@ struct DevIndex {
   uint32_t lf_exact;
   // Walk lines and the samples they index (WalkLine above); null when absent.
   const void* walk;
-  const void* wssa;      // sample of each mark, in row order (u32, u64 wide)
+  const void* wssa;      // sample of each mark, in row order (u32; wide: 40-bit entries)
+  uint32_t wssa_eb;      // bytes per wssa entry: 4, 5 (40 bits, little-endian) or 8
   // Left contexts (null when absent): per BWT row the codes of the lctx_q symbols
   // its LF chain meets, lctx_sb bits each (see kCtxQ below).
   const void* lctx;

@@ -37,6 +37,7 @@ struct cs_fm_index {
   uint32_t pstride = 32;              // walk-mark text-position stride (position_stride())
   uint32_t xstride = 32;              // the inverse-SA samples' stride (pstride; 2 pstride wide)
   uint64_t nwssa = 0;                 // walk position samples (n / pstride with position marks)
+  uint32_t wssa_eb = 0;               // their bytes per entry: 4 narrow, 5 wide (40 bits); 0 = sample_bytes()
   bool lf_exact = false;              // unique smallest last symbol: LF inverts SA
   void* d_walk = nullptr;             // walk lines (occurrence engine; WalkLine / WalkLineW)
   uint64_t nwalk = 0;
@@ -97,6 +98,7 @@ struct cs_fm_index {
   mutable Server server;
 
   uint32_t sample_bytes() const { return wide ? 8 : 4; }
+  uint32_t wssa_bytes() const { return wssa_eb ? wssa_eb : sample_bytes(); }
   uint32_t ptab_rec = 0;             // prefix-table entries: 0 plain, 1 32-B / 2 16-B context records
   uint32_t ptab_entry_bytes() const { return ptab_rec == 1 ? 32 : ptab_rec >= 2 ? 16 : 8; }  // plain: 2 x u32 / packed wide
   uint64_t ptab_entries() const {
@@ -132,6 +134,7 @@ struct cs_fm_index {
     d.lf_exact = lf_exact ? 1u : 0u;
     d.walk = d_walk;
     d.wssa = d_wssa ? d_wssa : d_ssa;
+    d.wssa_eb = d_wssa ? wssa_bytes() : sample_bytes();
     d.lctx = d_lctx;
     d.lctx_q = d_lctx ? lctx_q : 0u;
     d.lctx_sb = lctx_sb;

@@ -12,6 +12,7 @@
 //                    nlines, nsamples, nisa, ptab_k, ptab_sigma, lf_exact, has_text,
 //                    wide, line_fmt, levels, nwalk, walk_marks, has_wssa, nlctx, lctx_q/sb/eb, pstride, nlmodel, lmodel_shift, ptab_rec, has_sa, has_dtext,
 //                    xstride (inverse-SA sample stride), nwssa (walk position samples),
+//                    wssa_eb (their bytes per entry: 4, 5 = 40-bit, 8 = older wide images),
 //                    active <symbol> <mask>
 //   table.bin        NodeTable (fm_device.hpp)
 //   lines.bin        the rank lines (8 wavelet levels, or one occurrence-line array)
@@ -110,7 +111,7 @@ std::vector<Part> index_parts(cs_fm_index* h, bool with_table, bool has_wssa, bo
   v.push_back({"isa.bin", &h->d_isa, h->nisa * sb});
   if (h->ptab_k) v.push_back({"ptab.bin", &h->d_ptab, h->ptab_entries() * h->ptab_entry_bytes()});
   if (h->nwalk) v.push_back({"walk.bin", &h->d_walk, h->nwalk * 32});
-  if (has_wssa) v.push_back({"wssa.bin", &h->d_wssa, h->nwssa * sb});
+  if (has_wssa) v.push_back({"wssa.bin", &h->d_wssa, h->nwssa * h->wssa_bytes()});
   if (h->nlctx) v.push_back({"lctx.bin", &h->d_lctx, h->nlctx * h->lctx_eb});
   if (h->nlmodel) v.push_back({"lmodel.bin", &h->d_lmodel, h->nlmodel * sizeof(LOccModel)});
   if (has_sa) v.push_back({"sa.bin", &h->d_sa, h->n * 4});
@@ -125,7 +126,8 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 "nsamples %llu\nnisa %llu\nptab_k %u\nptab_sigma %u\nlf_exact %d\nhas_text %d\n"
                 "wide %d\nline_fmt %u\nlevels %u\nnwalk %llu\nwalk_marks %u\nhas_wssa %d\n"
                 "nlctx %llu\nlctx_q %u\nlctx_sb %u\nlctx_eb %u\npstride %u\nnlmodel %llu\n"
-                "lmodel_shift %u\nptab_rec %d\nhas_sa %d\nhas_dtext %d\nxstride %u\nnwssa %llu\n",
+                "lmodel_shift %u\nptab_rec %d\nhas_sa %d\nhas_dtext %d\nxstride %u\nnwssa %llu\n"
+                "wssa_eb %u\n",
                 kFormat, (unsigned long long)h->n, h->stride, h->line_bytes, h->line_bits,
                 (unsigned long long)h->nlines, (unsigned long long)h->nsamples,
                 (unsigned long long)h->nisa, h->ptab_k, h->ptab_sigma, h->lf_exact ? 1 : 0,
@@ -134,7 +136,7 @@ std::string meta_text(const cs_fm_index* h, bool has_text) {
                 (unsigned long long)(h->d_lctx ? h->nlctx : 0), h->lctx_q, h->lctx_sb, h->lctx_eb,
                 h->pstride, (unsigned long long)h->nlmodel, h->lmodel_shift, (int)h->ptab_rec,
                 h->d_sa ? 1 : 0, h->d_dtext ? 1 : 0, h->xstride,
-                (unsigned long long)(h->d_wssa ? h->nwssa : 0));
+                (unsigned long long)(h->d_wssa ? h->nwssa : 0), h->wssa_bytes());
   std::string m(buf);
   for (int c = 0; c < 256; ++c) {
     std::snprintf(buf, sizeof buf, "active %d %u\n", c, h->active_levels[c]);
@@ -185,6 +187,11 @@ cs_status meta_parse(const std::string& text, cs_fm_index* h,
   h->pstride = kv["pstride"] ? (uint32_t)kv["pstride"] : h->stride;  // older images: the SSA's
   h->xstride = kv["xstride"] ? (uint32_t)kv["xstride"] : h->pstride;  // older images: one stride
   h->nwssa = kv.count("nwssa") ? kv["nwssa"] : (kv["has_wssa"] ? h->nisa : 0);
+  h->wssa_eb = (uint32_t)kv["wssa_eb"];  // absent in older images: sample_bytes()
+  if (h->wssa_eb != 0 && h->wssa_eb != 4 && h->wssa_eb != 5 && h->wssa_eb != 8) {
+    set_error("bad wssa_eb in " + what);
+    return CS_ERR_INVALID;
+  }
   h->nlmodel = kv["nlmodel"];
   h->lmodel_shift = (uint32_t)kv["lmodel_shift"];
   h->ptab_rec = (uint32_t)kv["ptab_rec"];

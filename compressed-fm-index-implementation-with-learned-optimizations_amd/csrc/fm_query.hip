@@ -2308,7 +2308,13 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
 // The same walk over walk lines (occurrence engine, fm_device.hpp WalkLine): one
 // line per step gives the mark, the sample index and LF.
 __device__ __forceinline__ uint64_t wssa_at(const DevIndex& ix, uint64_t k) {
-  return ix.wide ? static_cast<const uint64_t*>(ix.wssa)[k] : static_cast<const uint32_t*>(ix.wssa)[k];
+  if (ix.wssa_eb == 5) {  // 40-bit entries (wide position samples): the two dwords holding them
+    const uint64_t b = 5 * k;
+    const uint32_t* d = static_cast<const uint32_t*>(ix.wssa) + (b >> 2);
+    const uint64_t x = ((uint64_t)d[1] << 32) | d[0];
+    return (x >> (8 * (b & 3))) & ((1ull << 40) - 1);
+  }
+  return ix.wssa_eb == 8 ? static_cast<const uint64_t*>(ix.wssa)[k] : static_cast<const uint32_t*>(ix.wssa)[k];
 }
 
 // LF(pos) from pos's walk line v (line q, offset o): C[c] + occ(c, pos) from the same

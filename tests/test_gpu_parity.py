@@ -260,8 +260,7 @@ def test_engine_choice(built):
         assert info.context_q == ctx, name
         wide = os.environ.get("CS_FM_WIDE") == "1"
         assert info.full_sa_bytes == (4 * info.n if full_sa else 0), name
-        assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or
-                                        (8 if wide else 4)), name
+        assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or 4), name
         assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
         # context records: narrow occurrence-line indexes with contexts and a table of
         # 14+ characters (none of these texts) or forced; 16 B when forced compact
