@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 #include <cstring>
 #include <mutex>
@@ -1120,8 +1121,15 @@ __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable
 // written per pattern and the host round trip between the phases.  A single launch with
 // a decoupled look-back across tiles was measured first: every block then waits for the
 // slowest search among its predecessors (3.2 ms against 1.1 ms for the two phases, C4).
+// Indexes without the full suffix array but with walk lines and text-position marks (C5;
+// C4 under CS_FM_FULL_SA=0) take the same three launches (round 3): a position is the
+// short walk from its row (walk_position: at most pstride - 1 LF steps, one 32-B walk line
+// each, then the mark's sample) instead of SA[row], in (1) for a pattern's only position
+// and in (3) / k_locate_emit_wide for the rest (kPos: 0 the full SA, 1 WalkLine, 2
+// WalkLineW).  Counts are u64 (cnt64) when the index is wide.
 struct OnePass {
-  uint32_t* cnt = nullptr;               // (1) -> (3): min(count, limit) per pattern
+  uint32_t* cnt = nullptr;               // (1) -> (3): min(count, limit) per pattern (narrow)
+  uint64_t* cnt64 = nullptr;             // the same, wide indexes
   uint64_t* rec = nullptr;               // (1) -> (3): the pattern's record
   uint64_t* tiles = nullptr;             // per tile: its total, then its exclusive prefix
   const uint32_t* sa = nullptr;          // full suffix array
@@ -1132,6 +1140,23 @@ struct OnePass {
   unsigned long long* nwide = nullptr;
   uint64_t wide_cap = 0;
 };
+
+// the text position of BWT row `row` by the short walk, and the same for U rows walked in
+// lockstep (their line reads in flight together) — defined with the walks below
+template <class W>
+__device__ __forceinline__ uint64_t walk_position(const DevIndex& ix, const NodeTable& T, uint64_t row);
+template <class W, int U>
+__device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTable& T, uint64_t* pos,
+                                               bool* act);
+
+// position of BWT row `row` for the one-call locate: SA[row] (kPos 0) or the short walk
+template <int kPos>
+__device__ __forceinline__ uint64_t onepass_pos(const DevIndex& ix, const NodeTable& T, const OnePass& op,
+                                                uint64_t row) {
+  if constexpr (kPos == 0) return op.sa[row];
+  else if constexpr (kPos == 1) return walk_position<WalkLine>(ix, T, row);
+  else return walk_position<WalkLineW>(ix, T, row);
+}
 
 // Exclusive scan over the block's U x kBlk values in pattern order (segment j holds the
 // patterns q0 + j kBlk, j < U): mine[j] = the offset of the lane's j-th value inside the
@@ -1171,29 +1196,45 @@ __device__ __forceinline__ void block_scan(const uint64_t* kc, uint64_t* mine, u
 // other blocks' record reads instead of waiting for k_locate_emit; the record then holds
 // kLocStash | position.  (C4 Q_text: 99.6 % of the patterns.)
 constexpr uint64_t kLocStash = 1ull << 62;  // with bit 63 clear: not a window, not a row
-template <int U>
-__device__ __forceinline__ void locate_split_store(uint64_t n, uint64_t npat, uint64_t tile,
-                                                   uint64_t q0, const uint64_t* kc,
+template <int U, int kPos = 0>
+__device__ __forceinline__ void locate_split_store(const DevIndex& ix, const NodeTable& T, uint64_t npat,
+                                                   uint64_t tile, uint64_t q0, const uint64_t* kc,
                                                    const uint64_t* kr, const OnePass& op) {
+  const uint64_t n = ix.n;
   uint64_t mine[U], agg, rs[U];
   block_scan<U>(kc, mine, agg);
   if (threadIdx.x == 0) op.tiles[tile] = agg;
+  uint64_t row[U], adj[U];
+  bool one[U];
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk, s = kr[j];
     rs[j] = s;
-    if (q >= npat || kc[j] != 1) continue;
-    uint64_t row = s, adj = 0;
+    row[j] = s;
+    adj[j] = 0;
+    one[j] = q < npat && kc[j] == 1;
     uint32_t rel;
-    if (s & kLocCtx) loc_window(s, row, adj, rel);
-    const uint64_t p = op.sa[row];  // a window's only match is its first row
-    rs[j] = kLocStash | (p >= adj ? p - adj : p + n - adj);
+    if (one[j] && (s & kLocCtx)) loc_window(s, row[j], adj[j], rel);  // a window's only match: its first row
   }
+  if constexpr (kPos == 0) {
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (one[j]) row[j] = op.sa[row[j]];
+  } else {  // the lane's walks in lockstep: row[j] becomes the position
+    bool act[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) act[j] = one[j];
+    walk_positions<std::conditional_t<kPos == 1, WalkLine, WalkLineW>, U>(ix, T, row, act);
+  }
+#pragma unroll
+  for (int j = 0; j < U; ++j)
+    if (one[j]) rs[j] = kLocStash | (row[j] >= adj[j] ? row[j] - adj[j] : row[j] + n - adj[j]);
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (q >= npat) continue;
-    op.cnt[q] = (uint32_t)kc[j];
+    if (op.cnt64) op.cnt64[q] = kc[j];
+    else op.cnt[q] = (uint32_t)kc[j];
     op.rec[q] = rs[j];
   }
 }
@@ -1244,16 +1285,26 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tile
 }
 
 // (3): offsets and positions of tile blockIdx.x
-template <int U>
-__global__ __launch_bounds__(kBlk) void k_locate_emit(uint64_t n, uint64_t npat, OnePass op) {
+template <int U, int kPos = 0>
+__global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat, OnePass op) {
+  __shared__ NodeTable T;  // kPos: the walks' C[] and codes
+  const uint64_t n = ix.n;
   const uint64_t tile = blockIdx.x;
   const uint64_t q0 = tile * (uint64_t)(kBlk * U) + threadIdx.x;
   uint64_t kc[U], kr[U], mine[U], agg;
+  bool walk = false;  // a position to walk here (not stashed by (1))
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    kc[j] = q < npat ? op.cnt[q] : 0;
+    kc[j] = q < npat ? (op.cnt64 ? op.cnt64[q] : op.cnt[q]) : 0;
     kr[j] = q < npat ? op.rec[q] : 0;
+    walk |= kc[j] && (kr[j] >> 62) != 1;
+  }
+  if constexpr (kPos != 0) {
+    if (__syncthreads_or(walk)) {
+      load_table(T, ix.table);
+      __syncthreads();
+    }
   }
   block_scan<U>(kc, mine, agg);
   const uint64_t base = op.tiles[tile];
@@ -1266,19 +1317,19 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(uint64_t n, uint64_t npat,
     if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
     const uint64_t s = kr[j];
     if ((s >> 62) == 1) {  // kLocStash: the one position, read by the search kernel
-      op.out_pos[a] = s & 0xFFFFFFFFull;
+      op.out_pos[a] = s & (kLocStash - 1);
     } else if (s & kLocCtx) {  // a window k characters before the end (k_locate_sa)
       uint64_t r0, adj;
       uint32_t rel;
       loc_window(s, r0, adj, rel);
       for (uint64_t i = 0; i < c; ++i) {
         const uint32_t f = (uint32_t)__ffs(rel) - 1u;
-        const uint64_t p = op.sa[r0 + f];
+        const uint64_t p = onepass_pos<kPos>(ix, T, op, r0 + f);
         op.out_pos[a + i] = p >= adj ? p - adj : p + n - adj;
         rel &= rel - 1u;
       }
     } else if (c <= kLocSmall) {
-      for (uint64_t i = 0; i < c; ++i) op.out_pos[a + i] = op.sa[s + i];
+      for (uint64_t i = 0; i < c; ++i) op.out_pos[a + i] = onepass_pos<kPos>(ix, T, op, s + i);
     } else {
       const unsigned long long e = atomicAdd(op.nwide, 1ull);
       if (e < op.wide_cap) {
@@ -1290,16 +1341,19 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(uint64_t n, uint64_t npat,
 }
 
 // the ranges over kLocSmall rows: a block per range
-__global__ __launch_bounds__(kBlk) void k_locate_emit_wide(const uint32_t* __restrict__ sa,
-                                                           const uint64_t* __restrict__ offs,
-                                                           uint64_t* __restrict__ out,
-                                                           const uint64_t* __restrict__ wide,
-                                                           const unsigned long long* __restrict__ nwide,
-                                                           uint64_t wide_cap) {
-  const uint64_t nw = *nwide < wide_cap ? *nwide : wide_cap;
+template <int kPos = 0>
+__global__ __launch_bounds__(kBlk) void k_locate_emit_wide(DevIndex ix, OnePass op, const uint64_t* __restrict__ offs,
+                                                           uint64_t* __restrict__ out) {
+  __shared__ NodeTable T;
+  const uint64_t nw = *op.nwide < op.wide_cap ? *op.nwide : op.wide_cap;
+  if (blockIdx.x >= nw) return;  // uniform over the block
+  if constexpr (kPos != 0) {
+    load_table(T, ix.table);
+    __syncthreads();
+  }
   for (uint64_t e = blockIdx.x; e < nw; e += gridDim.x) {
-    const uint64_t q = wide[2 * e], s = wide[2 * e + 1], a = offs[q], c = offs[q + 1] - a;
-    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) out[a + j] = sa[s + j];
+    const uint64_t q = op.wide[2 * e], s = op.wide[2 * e + 1], a = offs[q], c = offs[q + 1] - a;
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) out[a + j] = onepass_pos<kPos>(ix, T, op, s + j);
   }
 }
 
@@ -1310,7 +1364,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(const uint32_t* __res
 // (m > k + kCtxQ) are left to k_count_long (long-pattern routing, LongRoute); otherwise,
 // with lr set, such a pattern marks lr.seen_h.
 template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false,
-          bool kSkipLong = false, bool kRng = true>
+          bool kSkipLong = false, bool kRng = true, int kPos = 0>
 __global__ __launch_bounds__(kBlk)
 __attribute__((amdgpu_waves_per_eu(!kLoc && U == 2 ? 6 : 1)))
 void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
@@ -1553,12 +1607,19 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     return;
   }
   if constexpr (kOne) {
-    if (__syncthreads_or(general)) {
+    // the walk (kPos) needs the node table for every block with a position to find
+    bool need = general;
+    if constexpr (kPos != 0) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) need |= kc[j] == 1;
+    }
+    if (__syncthreads_or(need)) {
       load_table(T, ix.table);
       __syncthreads();
-      general_rest<E, U, kLoc, kPacked, W, true>(ix, T, pats, st, o0, m, q0, co, limit, rec, kc, kr);
+      if (general)
+        general_rest<E, U, kLoc, kPacked, W, true>(ix, T, pats, st, o0, m, q0, co, limit, rec, kc, kr);
     }
-    locate_split_store<U>(ix.n, npat, blockIdx.x, q0, kc, kr, op);
+    locate_split_store<U, kPos>(ix, T, npat, blockIdx.x, q0, kc, kr, op);
     return;
   }
   if (!__syncthreads_or(general)) return;
@@ -2398,6 +2459,73 @@ __device__ __forceinline__ void walk_short_one(const DevIndex& ix, const NodeTab
     }
     pos = walk_lf<W, kQ>(ix, T, v, q, o, pos);
     ++steps;
+  }
+}
+
+template <class W>
+__device__ __forceinline__ uint64_t walk_position(const DevIndex& ix, const NodeTable& T, uint64_t pos) {
+  // as walk_short_one; an lf_exact index with text-position marks ends every walk within
+  // pstride - 1 steps (the bound below is never reached)
+  const uint64_t n = ix.n;
+  const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
+  for (uint64_t steps = 0; steps < n; ++steps) {
+    uint64_t q;
+    uint32_t o;
+    typename W::Raw v;
+    W::locate(pos, q, o);
+    W::load(ix.walk, q, v);
+    const bool mk = W::mark(v, o);
+    const bool rs = row_mask ? (pos & row_mask) == 0 : pos % ix.stride == 0;
+    if (mk || rs) {  // fm_index.cpp:147-153
+      const uint64_t sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
+      const uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps;
+      return s >= n ? s - n : s;
+    }
+    pos = walk_lf<W, false>(ix, T, v, q, o, pos);
+  }
+  return 0;
+}
+
+template <class W, int U>
+__device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTable& T, uint64_t* pos,
+                                               bool* act) {
+  const uint64_t n = ix.n;
+  const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
+  uint64_t steps[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) steps[j] = 0;
+  for (uint64_t it = 0; it < n; ++it) {
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) any |= act[j];
+    if (!any) return;
+    uint64_t q[U];
+    uint32_t o[U];
+    typename W::Raw v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {  // the lines of every active walk first
+      q[j] = 0, o[j] = 0;
+      if (act[j]) {
+        W::locate(pos[j], q[j], o[j]);
+        W::load(ix.walk, q[j], v[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (!act[j]) continue;
+      const bool mk = W::mark(v[j], o[j]);
+      const bool rs = row_mask ? (pos[j] & row_mask) == 0 : pos[j] % ix.stride == 0;
+      if (mk || rs) {  // fm_index.cpp:147-153
+        const uint64_t sidx = mk ? W::mark_rank(v[j], o[j])
+                                 : (row_mask ? pos[j] >> ix.stride_shift : pos[j] / ix.stride);
+        const uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps[j];
+        pos[j] = s >= n ? s - n : s;
+        act[j] = false;
+      } else {
+        pos[j] = walk_lf<W, false>(ix, T, v[j], q[j], o[j], pos[j]);
+        ++steps[j];
+      }
+    }
   }
 }
 
@@ -3397,8 +3525,16 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
     if (std::atoi(e) == 0) return CS_OK;
   const DevIndex ix = h->dev();
-  if (h->line_fmt != kFmtOcc || !ix.ptab_k || !ix.lctx || !h->d_sa || !h->lf_exact || h->wide)
+  // positions from the full SA (narrow), or by the short walk over walk lines with
+  // text-position marks (OnePass above); CS_FM_LOCATE_ONEPASS=1 keeps the walk indexes on
+  // the two phases (test hook: CS_FM_LOCATE_ONEPASS=2 = the full SA only)
+  const bool by_sa = h->d_sa && !h->wide;
+  bool by_walk = !h->d_sa && h->d_walk && h->d_wssa && h->walk_marks == 2;
+  if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
+    if (std::atoi(e) == 2) by_walk = false;
+  if (h->line_fmt != kFmtOcc || !ix.ptab_k || !ix.lctx || !h->lf_exact || !(by_sa || by_walk))
     return CS_OK;
+  const int kpos = by_sa ? 0 : h->wide ? 2 : 1;
   *done = true;
   if (!npat) {
     FMX_HIP(hipMemsetAsync(d_out_offs, 0, 8, st));
@@ -3416,13 +3552,15 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // a pattern has at most one
   const uint64_t wide_cap = std::min<uint64_t>(cap / (kLocSmall + 1) + 1, npat);
   StreamBuf ws;
-  FMX_HIP(ws.alloc(npat * 12 + tiles * 8 + 8 + wide_cap * 16, st));
+  const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
+  FMX_HIP(ws.alloc(npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16, st));
   OnePass op;
   op.rec = ws.as<uint64_t>();
   op.tiles = op.rec + npat;
   op.nwide = reinterpret_cast<unsigned long long*>(op.tiles + tiles);
   op.wide = reinterpret_cast<uint64_t*>(op.nwide + 1);
-  op.cnt = reinterpret_cast<uint32_t*>(op.wide + 2 * wide_cap);
+  if (h->wide) op.cnt64 = op.wide + 2 * wide_cap;
+  else op.cnt = reinterpret_cast<uint32_t*>(op.wide + 2 * wide_cap);
   op.sa = static_cast<const uint32_t*>(h->d_sa);
   op.out_offs = d_out_offs;
   op.out_pos = d_out_pos;
@@ -3430,14 +3568,28 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide_cap = wide_cap;
   FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
-  k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
-      ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  if (kpos == 0)
+    k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else if (kpos == 1)
+    k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else
+    k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   FMX_HIP(hipGetLastError());
   k_scan_tiles<<<1, 1024, 0, st>>>(op.tiles, tiles, d_out_offs + npat);
   FMX_HIP(hipGetLastError());
-  k_locate_emit<U><<<(unsigned)tiles, kBlk, 0, st>>>(h->n, npat, op);
-  FMX_HIP(hipGetLastError());
-  k_locate_emit_wide<<<1024, kBlk, 0, st>>>(op.sa, d_out_offs, d_out_pos, op.wide, op.nwide, wide_cap);
+  if (kpos == 0) {
+    k_locate_emit<U, 0><<<(unsigned)tiles, kBlk, 0, st>>>(ix, npat, op);
+    k_locate_emit_wide<0><<<1024, kBlk, 0, st>>>(ix, op, d_out_offs, d_out_pos);
+  } else if (kpos == 1) {
+    k_locate_emit<U, 1><<<(unsigned)tiles, kBlk, 0, st>>>(ix, npat, op);
+    k_locate_emit_wide<1><<<1024, kBlk, 0, st>>>(ix, op, d_out_offs, d_out_pos);
+  } else {
+    k_locate_emit<U, 2><<<(unsigned)tiles, kBlk, 0, st>>>(ix, npat, op);
+    k_locate_emit_wide<2><<<1024, kBlk, 0, st>>>(ix, op, d_out_offs, d_out_pos);
+  }
   FMX_HIP(hipGetLastError());
   FMX_HIP(hipMemcpyAsync(total, d_out_offs + npat, 8, hipMemcpyDeviceToHost, st));
   FMX_HIP(hipStreamSynchronize(st));
