@@ -67,6 +67,9 @@ SIGNATURES = {
     "cs_fm_open_directory": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "cs_fm_open_directory_on": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "cs_fm_save_directory": (C.c_int, [_vp, C.c_char_p]),
+    "cs_fm_open_csidx": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
+    "cs_fm_save_csidx": (C.c_int, [_vp, C.c_char_p]),
+    "cs_csidx_check": (C.c_int, [C.c_char_p, _u64p, _u32p, C.POINTER(C.c_int)]),
     "cs_fm_destroy": (None, [_vp]),
     "cs_fm_get_info": (C.c_int, [_vp, C.POINTER(cs_fm_info)]),
     "cs_fm_last_error": (C.c_char_p, []),
@@ -319,6 +322,23 @@ class FMIndex:
 
     def save_directory(self, path: str):
         _check(lib().cs_fm_save_directory(self._h, path.encode()))
+
+    @staticmethod
+    def open_csidx(path: str, device: int | None = None):
+        """Open a single-file index in the reference's CSIDX layout
+        (src/serialization/serialization.hpp:1-83; BWT, SSA, C and text sections)."""
+        if device is None:
+            device = int(os.environ.get("CS_FM_DEVICE", "0"))
+        h = _vp()
+        _check(lib().cs_fm_open_csidx(path.encode(), device, C.byref(h)))
+        idx = FMIndex(h, 0)
+        idx.n = idx.info().n
+        return idx
+
+    def save_csidx(self, path: str):
+        """Write the index as one CSIDX file (serialization.cpp:26-147's layout)."""
+        _check(lib().cs_fm_save_csidx(self._h, path.encode()))
+
 
     # -- queries (fm_index.hpp:26-37) -------------------------------------
     def count(self, pattern) -> int:
@@ -580,3 +600,13 @@ def sa_build(text, device: int = 0) -> np.ndarray:
     out = np.zeros(max(n, 1), np.uint32)
     _check(lib().cs_sa_build(_u8(t), n, out.ctypes.data_as(_u32p), device))
     return out[:n]
+
+
+def csidx_check(path: str) -> dict:
+    """Validate a CSIDX file on the CPU (no device): {"n", "ssa_stride", "has_text"};
+    raises FMIndexError with the reason otherwise."""
+    n = C.c_uint64()
+    st = C.c_uint32()
+    ht = C.c_int()
+    _check(lib().cs_csidx_check(path.encode(), C.byref(n), C.byref(st), C.byref(ht)))
+    return {"n": n.value, "ssa_stride": st.value, "has_text": bool(ht.value)}

@@ -319,6 +319,10 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     return CS_ERR_INVALID;
   }
   *out = nullptr;
+  {  // a single file: the reference's CSIDX format (fm_csidx.cpp)
+    struct stat sb;
+    if (stat(dir, &sb) == 0 && S_ISREG(sb.st_mode)) return cs_fm_open_csidx(dir, device, out);
+  }
   const std::string d(dir);
   errno = 0;
   std::string meta;

@@ -131,6 +131,21 @@ cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint
  * directory fails with CS_ERR_INVALID ("cannot open: <path>"). */
 cs_status cs_fm_open_directory(const char* dir, cs_fm_index** out);
 cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out);
+/* The reference's designed single-file format, CSIDX (src/serialization/serialization.hpp:
+ * 1-83: 88-B header "CSIDX", version 1, text_len, eight 8-B-aligned section offsets; the
+ * mmap reader serialization.cpp:153-335).  The reference never wired it to FMIndex and its
+ * writer does not terminate (serialization.cpp:44-54), so these follow the documented
+ * layout: text [u64 len][bytes], bwt [u64 n][bytes], C [u64 257][u32], ssa [u32 stride][pad]
+ * [u64 count][u32], footer "CSEND"; the wavelet and vEB sections are neither written nor
+ * read (the engine builds its own rank structures from the BWT).
+ * cs_fm_open_csidx: the BWT and the SSA as cs_fm_create takes them (no suffix sorting; the
+ * C array, when present, must match the BWT), the text when present for extract;
+ * cs_fm_open_directory(_on) given a path to such a file opens it the same way.
+ * cs_fm_save_csidx: writes one (n < 2^32).  cs_csidx_check: validates a file on the CPU
+ * (no device): CS_OK with its n, stride and whether it holds the text. */
+cs_status cs_fm_open_csidx(const char* path, int device, cs_fm_index** out);
+cs_status cs_fm_save_csidx(const cs_fm_index* h, const char* path);
+cs_status cs_csidx_check(const char* path, uint64_t* n, uint32_t* ssa_stride, int* has_text);
 /* Writes the index (HBM images of every structure, plus the text when kept) to dir. */
 cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir);
 /* The index as a device image, for replication across GPUs (e.g. a broadcast over
