@@ -1062,6 +1062,31 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
+// load_pattern32 from at most three 16-B aligned vectors (the word selects are arithmetic:
+// a select between array elements becomes a dynamically indexed array, which the compiler
+// moves to LDS).  A vector holding a byte of the batch lies inside its allocation.
+__device__ __forceinline__ void load_pattern32_v16(const uint8_t* __restrict__ pats, uint64_t o0,
+                                                   uint32_t m, uint32_t u[8]) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(pats + o0);
+  const uint4* pv = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+  const uint32_t ps = (uint32_t)(a & 15), end = ps + m;  // bytes [ps, end) of the vectors
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  const uint4 v0 = pv[0], v1 = end > 16 ? pv[1] : z, v2 = end > 32 ? pv[2] : z;
+  const uint64_t e0 = ((uint64_t)v0.y << 32) | v0.x, e1 = ((uint64_t)v0.w << 32) | v0.z;
+  const uint64_t e2 = ((uint64_t)v1.y << 32) | v1.x, e3 = ((uint64_t)v1.w << 32) | v1.z;
+  const uint64_t e4 = ((uint64_t)v2.y << 32) | v2.x, e5 = ((uint64_t)v2.w << 32) | v2.z;
+  const uint64_t sel = ps >= 8 ? ~0ull : 0ull, sh = ps & 7;
+  const uint64_t a0 = text8(e0, e1, sh), a1 = text8(e1, e2, sh), a2 = text8(e2, e3, sh);
+  const uint64_t a3 = text8(e3, e4, sh), a4 = text8(e4, e5, sh);
+  const uint64_t o[4] = {a0 ^ ((a0 ^ a1) & sel), a1 ^ ((a1 ^ a2) & sel), a2 ^ ((a2 ^ a3) & sel),
+                         a3 ^ ((a3 ^ a4) & sel)};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    u[2 * j] = (uint32_t)o[j];
+    u[2 * j + 1] = (uint32_t)(o[j] >> 32);
+  }
+}
+
 // the patterns of a k_count_ctx lane that need the general search (st == 3); kOne: the
 // locate results stay in the lane's registers (kc, kr)
 // rng: k_count_ctx's s_rng ([U][kBlk][2]): the range after the table of a pattern with st 5
@@ -1436,6 +1461,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     if (mm < K || K == 0 || mm > kFastM) continue;
     const uint32_t wl = (uint32_t)mm;
     uint32_t u[8];
+    // (16-B vector loads here, load_pattern32_v16, were measured: 0.3857 against 0.3864 ms,
+    // profiles/r03/ab_pattern_v16.json — the headline is not bound by its load instructions)
     if constexpr (!kPacked) load_pattern32(pats, o0[j], wl, u);
     const uint32_t kk = m[j] - K;
     bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
@@ -1731,15 +1758,74 @@ __device__ __forceinline__ bool pack_pattern(const uint8_t* P, uint64_t c0, uint
   return ok;
 }
 
+// pack_pattern from 16-B aligned vectors (11 loads for a 160-character chunk instead of 21
+// 8-B ones: a lane's pattern lies at a stride of m bytes from its neighbours', so every load
+// instruction touches 64 cache lines and the count of instructions is what the TA/TCP pay).
+// A vector holding a byte of the batch lies inside its allocation (16-B granular).
+__device__ __forceinline__ bool pack_pattern16(const uint8_t* P, uint64_t len, const uint16_t* cmap,
+                                               uint64_t pc[kLongPW]) {
+  const uint64_t kk = len < 32ull * kLongPW ? len : 32ull * kLongPW;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(P);
+  const uint4* pv = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+  const uint32_t ps = (uint32_t)(a & 15), vlast = (uint32_t)((ps + kk - 1) >> 4);
+  constexpr uint32_t NV = (15 + 32 * kLongPW + 15) / 16;  // 11 for kLongPW = 5
+  uint64_t x[2 * NV];
+#pragma unroll
+  for (uint32_t i = 0; i < NV; ++i) {
+    const uint4 v = i <= vlast ? pv[i] : make_uint4(0, 0, 0, 0);
+    x[2 * i] = ((uint64_t)v.y << 32) | v.x;
+    x[2 * i + 1] = ((uint64_t)v.w << 32) | v.z;
+  }
+  static_assert(4 * kLongPW + 1 < 2 * NV, "word c + 2 of the last chunk is loaded");
+  const uint64_t sel = ps >= 8 ? ~0ull : 0ull, sh = ps & 7;
+  bool ok = true;
+#pragma unroll
+  for (uint32_t i = 0; i < kLongPW; ++i) pc[i] = 0;
+#pragma unroll
+  for (uint32_t c = 0; c < 4 * kLongPW; ++c) {
+    const uint64_t y0 = text8(x[c], x[c + 1], sh), y1 = text8(x[c + 1], x[c + 2], sh);
+    const uint64_t y = y0 ^ ((y0 ^ y1) & sel);  // P[8c, 8c + 8)
+#pragma unroll
+    for (uint32_t b = 0; b < 8; ++b) {
+      if (8 * c + b < kk) {
+        const uint32_t d = cmap[(uint32_t)(y >> (8 * b)) & 0xFFu] >> 8;
+        ok &= d != kNoCode;
+        pc[c >> 2] |= (uint64_t)(d & 3u) << (2 * (8 * (c & 3) + b));
+      }
+    }
+  }
+  return ok;
+}
+
 // text[q, q + len) (len <= 32 kLongPW) against the packed codes pc: the window's words in
 // one round, shifted to its start; true when every code agrees
+// kV: the words through 16-B aligned vector loads (3 instead of up to 6 8-B loads)
+template <bool kV = false>
 __device__ __forceinline__ bool packed_chunk_eq(const DevIndex& ix, const uint64_t* pc, uint64_t q,
                                                 uint64_t len) {
   const uint64_t a = q >> 5, last = (q + len - 1) >> 5;
   const uint32_t s = (uint32_t)(q & 31) * 2;
   uint64_t w[kLongPW + 1];
+  if constexpr (kV) {
+    const uint64_t a2 = a & ~1ull, sel = (a & 1) ? ~0ull : 0ull;
+    const ulonglong2* pv = reinterpret_cast<const ulonglong2*>(ix.ptext + a2);
+    constexpr uint32_t NV = (kLongPW + 3) / 2;  // words a2 .. a2 + 2 NV - 1 cover a .. a + kLongPW
+    uint64_t x[2 * NV];
 #pragma unroll
-  for (uint32_t i = 0; i <= kLongPW; ++i) w[i] = a + i <= last ? ix.ptext[a + i] : 0ull;
+    for (uint32_t i = 0; i < NV; ++i) {
+      const ulonglong2 v = a2 + 2 * i <= last ? pv[i] : make_ulonglong2(0, 0);
+      x[2 * i] = v.x;
+      x[2 * i + 1] = v.y;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i <= kLongPW; ++i) {
+      const uint64_t y1 = i + 1 < 2 * NV ? x[i + 1] : 0ull;
+      w[i] = a + i <= last ? x[i] ^ ((x[i] ^ y1) & sel) : 0ull;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t i = 0; i <= kLongPW; ++i) w[i] = a + i <= last ? ix.ptext[a + i] : 0ull;
+  }
   uint64_t diff = 0;
 #pragma unroll
   for (uint32_t i = 0; i < kLongPW; ++i) {
@@ -1758,12 +1844,13 @@ __device__ __forceinline__ bool packed_chunk_eq(const DevIndex& ix, const uint64
 // 175 characters at k = 15) against the byte text.  A rare symbol in the packed part of the
 // window is a mismatch (its code 0 in the packed text stands for no pattern character).
 // Windows through the end of the text: the byte text, cyclically.
+template <bool kV = false>
 __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint64_t* pc, const uint8_t* P,
                                                  uint64_t q, uint64_t L, const uint32_t* rare) {
   if (q + L > ix.n) return window_eq<const uint8_t*>(ix, P, q, L, nullptr);
   constexpr uint64_t C = 32ull * kLongPW;
   const uint64_t L0 = L < C ? L : C;
-  if (!packed_chunk_eq(ix, pc, q, L0) || rare_in(rare, ix.nrare, q, L0)) return false;
+  if (!packed_chunk_eq<kV>(ix, pc, q, L0) || rare_in(rare, ix.nrare, q, L0)) return false;
   return L == L0 || window_eq<const uint8_t*>(ix, P + C, q + C, L - C, nullptr);
 }
 
@@ -1782,7 +1869,9 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 // 8-B loads at a stride of m bytes, was measured: 150-mers 1.91 -> 1.75 ms, but 32- to
 // 100-mers 5-18 % slower — the 38-KB stage leaves 4 waves per SIMD —
 // profiles/r03/long_probe_lds_stage.json; not kept.)
-template <int W, bool kPT, bool kBytes = false>
+// kV16: the pattern's bytes through 16-B aligned vector loads (1: pack_pattern16 and
+// load_tail32_v16, 2: pack_pattern16 only, 3: 2 and the packed window as 16-B vectors)
+template <int W, bool kPT, bool kBytes = false, int kV16 = 0>
 __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m,
@@ -1825,8 +1914,12 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
   for (uint32_t i = 0; i < kLongPW; ++i) pc[i] = 0;
   if (fast) {
     uint32_t u[8];
-    load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
-    if constexpr (kPT) fast &= pack_pattern(P, 0, k, cmap, pc);  // P[0, min(k, 160)) coded
+    if constexpr (kV16 == 1) load_pattern32_v16(pats, o0 + m - 32, 32, u);
+    else load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
+    if constexpr (kPT) {  // P[0, min(k, 160)) coded
+      if constexpr (kV16 >= 2) fast &= pack_pattern16(P, k, cmap, pc);
+      else fast &= pack_pattern(P, 0, k, cmap, pc);
+    }
 #pragma unroll
     for (uint32_t i = 0; i < 32; ++i) {
       const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
@@ -1933,7 +2026,7 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
           continue;
         }
         bool eq;
-        if constexpr (kPT) eq = window_eq_packed(ix, pc, P, wq, L, rare);
+        if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, P, wq, L, rare);
         else eq = window_eq_long<kLongWords>(ix, P, wq, L);
         res += eq ? 1u : 0u;
       }
@@ -3328,7 +3421,21 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
   FMX_HIP(lb.alloc(npat * 8 + 8, st));
   unsigned long long* nl = reinterpret_cast<unsigned long long*>(lb.as<uint64_t>() + npat);
   FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
-  if (ix.ptext && !byte_text)
+  // tuning hook CS_FM_LONG_V16 (read per call): 0 = 8-B pattern / window loads, 3 = 16-B
+  // vectors for the pattern's packed part and the window (the default: C4 150-mers 1.87 ->
+  // 1.55 ms, 64-mers 1.25 -> 1.16-1.21, profiles/r03/long_probe_v16.json), 1 / 2 = partial forms
+  const char* ev = std::getenv("CS_FM_LONG_V16");
+  const int v16 = ev ? std::atoi(ev) : 3;
+  if (ix.ptext && !byte_text && v16 == 1)
+    k_count_long<0, true, kBytes, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
+                                                         lb.as<uint64_t>(), nl, skip_short, lr);
+  else if (ix.ptext && !byte_text && v16 == 2)
+    k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
+                                                         lb.as<uint64_t>(), nl, skip_short, lr);
+  else if (ix.ptext && !byte_text && v16 == 3)
+    k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
+                                                         lb.as<uint64_t>(), nl, skip_short, lr);
+  else if (ix.ptext && !byte_text)
     k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(),
                                                       nl, skip_short, lr);
   else

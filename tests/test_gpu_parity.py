@@ -501,6 +501,10 @@ def test_count_long_kernel_large(pkg):
         with _env(CS_FM_LONG_KERNEL=lk):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert np.array_equal(got, want), lk
+    for v in ("0", "1", "2"):  # the pattern / window load forms (default 3: 16-B vectors)
+        with _env(CS_FM_LONG_V16=v):
+            got, _, _ = _count_ex(g, pats, flags=32)
+        assert np.array_equal(got, want), v
     for _ in range(2):  # the default path: detection, then long-pattern routing
         got, _, _ = _count_ex(g, pats)
         assert np.array_equal(got, want)
@@ -802,6 +806,9 @@ def test_count_verify_long(built, pkg, name):
         with _env(CS_FM_LONG_KERNEL=lk):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert got.tolist() == want, (name, lk)
+    with _env(CS_FM_LONG_V16="0"):  # 8-B pattern and window loads
+        got, _, _ = _count_ex(g, pats, flags=32)
+    assert got.tolist() == want, (name, "v16=0")
     # long-pattern routing of the default path: the batches above raised the handle's flag,
     # so these run the staged kernel for the short patterns and k_count_long for the rest;
     # a batch of short patterns only ends the mode, the next mixed batch raises it again
