@@ -74,7 +74,7 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 LEGS_MAIN = ["count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
              "count_m64", "count_m64_steps", "count_m150", "count_m150_staged", "count_m64_long", "count_m150_long",
              "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
-             "locate_m64", "locate_m64_steps", "count_stream", "count_stream_packed",
+             "locate_m64", "locate_m150", "locate_m64_steps", "count_stream", "count_stream_packed",
              "count_stream_packed_u8", "host_batch",
              "extract"]
 LEGS_WM = ["wm_count", "wm_lf_loop", "wm_locate_ssa"]
@@ -375,8 +375,9 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
     oo = d_oo.cpu().numpy()
     owner = torch.from_numpy(np.repeat(np.arange(B), np.diff(oo).astype(np.int64))).to(dev)
     okv = True
-    for a in range(0, tot, 1 << 24):
-        p, w = pos[a:a + (1 << 24)], owner[a:a + (1 << 24)]
+    ch = max(1, (1 << 28) // m)  # positions per check: a (ch, m) int64 window index of 2 GB
+    for a in range(0, tot, ch):
+        p, w = pos[a:a + ch], owner[a:a + ch]
         win = text[(p.unsqueeze(1) + torch.arange(m, device=dev)).long()]
         okv &= bool((win == W.pats.view(B, m)[w]).all().item())
     del owner, d_pos, d_oo
@@ -1048,15 +1049,21 @@ def main():
                     "locate_ssa_rows", "locate with the reference's SSA walk (fm_index.cpp:125-153): LF over the occurrence "
                     "lines to a row with row %% %d == 0, SA sample + steps (CS_Q_NO_FULL_SA | "
                     "CS_Q_NO_WALK_LINES)" % args.ssa_stride, idx, info, wl, W, text, 4 | 8, dev, sh, reps=2)
-            for name, mm, one in (("locate_m64", 64, True), ("locate_m64_steps", 64, False)):
+            for name, mm, one in (("locate_m64", 64, True), ("locate_m150", 150, True),
+                                  ("locate_m64_steps", 64, False)):
                 # long patterns: a narrow range finishes by verification against the text
                 # (positions SA[r] - k of the verified rows), or steps to the end (CS_Q_NO_VERIFY)
                 if name in legs and (one or info.full_sa_bytes):
                     Wm = Workload(pkg, text, N, mm, lo, B, args.kind, args.queries, dev, sh)
                     if one:
                         lg[name] = locate_one_leg(
-                            name, "locate of Q_text %d-mers in one call: record, contexts, then %s" % (
-                                mm, ver or "rank steps"), idx, info, wl, Wm, text, dev, sh)
+                            name, "locate of Q_text %d-mers in one call: %s" % (
+                                mm, ("after the first batch with patterns over 32 characters the staged "
+                                     "search leaves them to k_locate_long (%s; a pattern's only position "
+                                     "is the verified row's SA entry minus k), then the tile scan and "
+                                     "the positions" % longk) if longk else
+                                ("record, contexts, then %s" % (ver or "rank steps"))),
+                            idx, info, wl, Wm, text, dev, sh)
                     else:
                         lg[name] = locate_leg(
                             name, "locate of Q_text %d-mers, rank steps to the end (CS_Q_NO_VERIFY), "

@@ -54,7 +54,7 @@ class cs_fm_info(C.Structure):
                 ("walk_bytes", C.c_uint64), ("context_q", C.c_uint32), ("position_stride", C.c_uint32),
                 ("context_bytes", C.c_uint64), ("full_sa_bytes", C.c_uint64),
                 ("record_bytes", C.c_uint32), ("text_in_hbm", C.c_uint32),
-                ("packed_text_bytes", C.c_uint64)]
+                ("packed_text_bytes", C.c_uint64), ("window_context_bytes", C.c_uint64)]
 
 
 # Every entry point of include/cs_fmindex.h with its ctypes signature.
@@ -117,6 +117,8 @@ SIGNATURES = {
     "cs_fm_locate_check": (C.c_int, [_vp, _vp]),
     "cs_fm_locate_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
                                       C.POINTER(C.c_uint64), _vp]),
+    "cs_fm_locate_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
+                                         C.POINTER(C.c_uint64), C.c_uint32, _vp]),
     "cs_fm_level_rank1": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint64, _u64p]),
     "cs_fm_wt_rank": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p]),
     "cs_fm_wt_access": (C.c_int, [_vp, _u64p, C.c_uint64, _u8p]),
@@ -474,12 +476,13 @@ class FMIndex:
         f = lib().cs_fm_locate_walk_device if sync else lib().cs_fm_locate_walk_device_async
         _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, stream or None))
 
-    def locate_device(self, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, stream=0):
-        """locate of a batch in one call (cs_fm_locate_device): offsets and, when they fit
-        `cap`, positions -> (total, positions_written)."""
+    def locate_device(self, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, stream=0, flags=0):
+        """locate of a batch in one call (cs_fm_locate_device[_ex]): offsets and, when they fit
+        `cap`, positions -> (total, positions_written).  flags: Q_LONG sends every pattern
+        to the long-pattern search."""
         total = C.c_uint64()
-        st = lib().cs_fm_locate_device(self._h, d_pats, d_offs, npat, limit, d_out_offs,
-                                       d_out_pos or None, cap, C.byref(total), stream or None)
+        st = lib().cs_fm_locate_device_ex(self._h, d_pats, d_offs, npat, limit, d_out_offs,
+                                          d_out_pos or None, cap, C.byref(total), flags, stream or None)
         if st == CS_ERR_CAPACITY:
             return total.value, False
         _check(st)

@@ -436,6 +436,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_sa) (void)hipFree(h->d_sa);
   if (h->d_dtext) (void)hipFree(h->d_dtext);
   if (h->d_ptext) (void)hipFree(h->d_ptext);
+  if (h->d_wctx) (void)hipFree(h->d_wctx);
   if (h->route_h) (void)hipHostFree(h->route_h);
   if (h->route_d) (void)hipFree(h->route_d);
   if (h->d_prare) (void)hipFree(h->d_prare);
@@ -595,6 +596,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->record_bytes = h->ptab_rec ? h->ptab_entry_bytes() : 0u;
   out->text_in_hbm = h->d_dtext ? 1u : 0u;
   out->packed_text_bytes = h->d_ptext ? h->ptext_bytes() : 0;
+  out->window_context_bytes = h->d_wctx ? h->wctx_bytes() : 0;
   return CS_OK;
 }
 
@@ -989,9 +991,10 @@ cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_p
                               (hipStream_t)stream, flags);
 }
 
-cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream) {
+cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
+                                 void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
@@ -1002,12 +1005,13 @@ cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const
   hipStream_t st = (hipStream_t)stream;
   bool done = false;
   s = launch_locate_onepass(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, st,
-                            &done);
+                            &done, flags & CS_Q_LONG);
   if (s != CS_OK) return s;
   if (!done) {  // the two phases: ranges, then (when the total fits) the positions
     StreamBuf sp;
     FMX_HIP(sp.alloc((npat ? npat : 1) * 8, st));
-    s = launch_locate_ranges(h, d_pats, d_offs, npat, limit, sp.as<uint64_t>(), d_out_offs, total, st);
+    s = launch_locate_ranges(h, d_pats, d_offs, npat, limit, sp.as<uint64_t>(), d_out_offs, total, st,
+                             flags & ~CS_Q_LONG);
     if (s != CS_OK) return s;
     if (*total > cap) {
       set_error("locate: capacity too small");
@@ -1020,6 +1024,12 @@ cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const
     return CS_ERR_CAPACITY;
   }
   return CS_OK;
+}
+
+cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream) {
+  return cs_fm_locate_device_ex(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, 0, stream);
 }
 
 cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
@@ -1081,7 +1091,8 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
-  if ((s = check_offsets(offs, npat)) != CS_OK) return s;
+  uint32_t lf = 0;  // CS_Q_LONG for a batch of long patterns only (k_locate_long)
+  if ((s = check_offsets(offs, npat, &lf)) != CS_OK) return s;
   hipStream_t st = (hipStream_t)stream;
   StagedBatch b;
   s = b.load(h, pats, offs, npat, st);
@@ -1097,13 +1108,13 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
     FMX_HIP(d_pos.alloc((dcap ? dcap : 1) * 8, st));
     bool done = false;
     s = launch_locate_onepass(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
-                              d_oo.as<uint64_t>(), d_pos.as<uint64_t>(), dcap, total, st, &done);
+                              d_oo.as<uint64_t>(), d_pos.as<uint64_t>(), dcap, total, st, &done, lf);
     if (s != CS_OK) return s;
     if (done && *total > dcap && *total <= cap) {
       dcap = *total;
       FMX_HIP(d_pos.alloc(dcap * 8, st));
       s = launch_locate_onepass(h, b.pats.as<uint8_t>(), b.offs.as<uint64_t>(), npat, limit,
-                                d_oo.as<uint64_t>(), d_pos.as<uint64_t>(), dcap, total, st, &done);
+                                d_oo.as<uint64_t>(), d_pos.as<uint64_t>(), dcap, total, st, &done, lf);
       if (s != CS_OK) return s;
     }
     if (done) {

@@ -1488,7 +1488,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     want[j] = ww;
     k[j] = kk;
   }
-  if constexpr (!kLoc && !kSkipLong) {
+  if constexpr ((!kLoc || kOne) && !kSkipLong) {
     // long-pattern routing: the first wave to meet a long pattern raises the host's flag
     if (lr.seen_d) {
       bool lg = false;
@@ -1871,48 +1871,52 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 // profiles/r03/long_probe_lds_stage.json; not kept.)
 // kV16: the pattern's bytes through 16-B aligned vector loads (1: pack_pattern16 and
 // load_tail32_v16, 2: pack_pattern16 only, 3: 2 and the packed window as 16-B vectors)
-template <int W, bool kPT, bool kBytes = false, int kV16 = 0>
-__global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
-                                                     const uint64_t* __restrict__ offs, uint64_t npat,
-                                                     CountOut co, uint64_t fixed_m,
-                                                     uint64_t* __restrict__ list,
-                                                     unsigned long long* __restrict__ nlist,
-                                                     bool skip_short, LongRoute lr) {
-  __shared__ uint16_t cmap[256];
-  __shared__ uint32_t rare[kMaxExc];
-  static_assert(kBlk >= 256, "one map entry per thread");
-  if (threadIdx.x < 256)
-    cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
-  if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
-  __syncthreads();
-  const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-  if (q >= npat) return;
-  // (A)
-  const uint64_t o0 = offs ? offs[q] : q * fixed_m;
-  const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
+// P[0, L) (pc: packed, pack_pattern's order) against the window text[SA[r] - k, SA[r] - k + L)
+// held in row r's window context e (k <= kWctxQ; its characters [kWctxQ - k, kWctxQ - k + L))
+__device__ __forceinline__ bool wctx_eq(ulonglong2 e, const uint64_t* pc, uint64_t k, uint64_t L) {
+  const uint32_t sh = 2 * (uint32_t)(kWctxQ - k);
+  uint64_t x0, x1;
+  if (sh == 0) {
+    x0 = e.x;
+    x1 = e.y;
+  } else if (sh < 64) {
+    x0 = (e.x >> sh) | (e.y << (64 - sh));
+    x1 = e.y >> sh;
+  } else {
+    x0 = e.y >> (sh - 64);
+    x1 = 0;
+  }
+  const uint32_t b = 2 * (uint32_t)L;  // bits compared (<= 2 kWctxQ)
+  const uint64_t m0 = b >= 64 ? ~0ull : (1ull << b) - 1;
+  const uint64_t m1 = b > 64 ? (1ull << (b - 64)) - 1 : 0ull;
+  return !(((x0 ^ pc[0]) & m0) | ((x1 ^ pc[1]) & m1));
+}
+
+// (A)-(C) of the long-pattern search of one pattern (m > 0 characters at pats + o0, n > 0):
+// the candidate rows base + i (bit i of cand) whose chains spell the qf characters before the
+// table part — what is left is the window text[SA - k, SA - qf) against P[0, k - qf),
+// k = m - ptab_k.  true: cand holds the candidates (none: the table part does not occur);
+// false: the pipeline cannot answer the pattern (the general search).  pc (kPT): the codes
+// of P[0, min(k, 32 kLongPW)).  by (kBytes): the random bytes read.
+template <bool kPT, bool kBytes, int kV16>
+__device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __restrict__ pats, uint64_t o0,
+                                           uint64_t m, const uint16_t* cmap, uint64_t pc[kLongPW],
+                                           uint64_t& base, uint32_t& cand, uint32_t& qf, uint64_t& by) {
   const uint8_t* P = pats + o0;
-  if (skip_short) {
-    const bool mine = m >= kFastM && m > ix.ptab_k + kCtxQ;  // the staged kernel skipped it
-    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(mine) && threadIdx.x == 0)
-      __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!mine) return;
-  }
-  if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
-    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
-    else store_count<W>(co, q, m == 0 ? ix.n : 0);
-    return;
-  }
-  uint64_t by = 0;  // kBytes
   const uint32_t K = ix.ptab_k;
   const uint64_t k = m - K;  // characters before the table part (when m >= K)
   // verification needs the window inside one rotation (k < n, as count_rest's)
   bool fast = m >= 32 && m > K + kCtxQ && k < ix.n;
   uint32_t t = 0, want = 0;
   bool cok = true;
-  uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
 #pragma unroll
   for (uint32_t i = 0; i < kLongPW; ++i) pc[i] = 0;
-  if (fast) {
+  base = 0;
+  cand = 0;
+  qf = 0;
+  if (!fast) return false;
+  // (A)
+  {
     uint32_t u[8];
     if constexpr (kV16 == 1) load_pattern32_v16(pats, o0 + m - 32, 32, u);
     else load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
@@ -1934,116 +1938,250 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
       }
     }
   }
-  uint64_t res = 0;
-  bool general = !fast;
-  if (fast) {
-    // (B)
-    uint64_t sp, ep;
-    uint32_t d[6] = {0, 0, 0, 0, 0, 0};  // inline contexts as u16 entries, row i in entry i
-    uint32_t qf = 0;                     // characters they answer (0: none inline)
-    by += ix.ptab_rec == 1 ? 32u : ix.ptab_rec == 2 ? 16u : 8u;
-    if (ix.ptab_rec == 2) {
-      const uint4 a = static_cast<const uint4*>(ix.ptab)[t];
-      const uint32_t wc = a.y & 15u;
-      sp = a.x;
-      ep = sp + (wc == kRec16Wide ? a.z : wc);
-      if (wc != kRec16Wide) {
-        qf = kRec16Q;
-        rec16_contexts(a.y, a.z, a.w, d);
-      }
-    } else if (ix.ptab_rec == 1) {
-      const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t * 2;
-      const uint4 a = r[0], b = r[1];
-      sp = a.x;
-      ep = (uint64_t)a.x + a.y;
-      if (ep - sp <= kRecCtx) {
-        qf = kCtxQ;
-        d[0] = a.z, d[1] = a.w, d[2] = b.x, d[3] = b.y, d[4] = b.z, d[5] = b.w;
-      }
-    } else {
-      (void)ptab_at(ix, t, sp, ep);  // a narrow plain table escapes nothing
+  if (!fast) return false;
+  // (B)
+  uint64_t sp, ep;
+  uint32_t d[6] = {0, 0, 0, 0, 0, 0};  // inline contexts as u16 entries, row i in entry i
+  if constexpr (kBytes) by += ix.ptab_rec == 1 ? 32u : ix.ptab_rec == 2 ? 16u : 8u;
+  if (ix.ptab_rec == 2) {
+    const uint4 a = static_cast<const uint4*>(ix.ptab)[t];
+    const uint32_t wc = a.y & 15u;
+    sp = a.x;
+    ep = sp + (wc == kRec16Wide ? a.z : wc);
+    if (wc != kRec16Wide) {
+      qf = kRec16Q;
+      rec16_contexts(a.y, a.z, a.w, d);
     }
-    // (C) the candidate rows base + i (bit i of cand)
-    uint64_t base = sp;
-    uint32_t cand = 0;
-    if (sp >= ep) {
-      // the table part does not occur: count 0
-    } else if (!cok) {
-      general = true;  // a rare symbol among the context characters
-    } else if (qf) {
-      const uint32_t msk = qf == kCtxQ ? ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc : (1u << (2 * qf)) - 1u;
-      const uint32_t wq = want & ((1u << (2 * qf)) - 1u);
-      uint32_t esc = 0;
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const uint32_t e = (d[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        cand |= (uint32_t)((e & msk) == wq) << i;
-        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
-      }
-      const uint32_t in = (1u << (uint32_t)(ep - sp)) - 1u;
-      general = (esc & in) != 0;  // 32-B records keep the escape bit; compact ones escape whole
-      cand &= in;
-    } else if (ix.lctx && ep - (sp & ~15ull) <= 32) {
+  } else if (ix.ptab_rec == 1) {
+    const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t * 2;
+    const uint4 a = r[0], b = r[1];
+    sp = a.x;
+    ep = (uint64_t)a.x + a.y;
+    if (ep - sp <= kRecCtx) {
       qf = kCtxQ;
-      base = sp & ~15ull;
-      const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);
-      const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) + base);
-      const uint4 x0 = p[0], x1 = p[1];
-      const uint4 x2 = hi > 16 ? p[2] : make_uint4(0, 0, 0, 0), x3 = hi > 16 ? p[3] : make_uint4(0, 0, 0, 0);
-      by += hi > 16 ? 64u : 32u;
-      const uint32_t dw[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
-                               x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
-      const uint32_t msk = ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc;
-      uint32_t esc = 0;
+      d[0] = a.z, d[1] = a.w, d[2] = b.x, d[3] = b.y, d[4] = b.z, d[5] = b.w;
+    }
+  } else {
+    (void)ptab_at(ix, t, sp, ep);  // a narrow plain table escapes nothing
+  }
+  // (C) the candidate rows base + i (bit i of cand)
+  base = sp;
+  if (sp >= ep) return true;  // the table part does not occur: count 0
+  if (!cok) return false;     // a rare symbol among the context characters
+  if (qf) {
+    const uint32_t msk = qf == kCtxQ ? ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc : (1u << (2 * qf)) - 1u;
+    const uint32_t wq = want & ((1u << (2 * qf)) - 1u);
+    uint32_t esc = 0;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        cand |= (uint32_t)((e & msk) == want) << i;
-        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
-      }
-      const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-      general = (esc & in) != 0;
-      cand &= in;
-    } else {
-      general = true;  // wider than the record and two sectors: steps first
+    for (int i = 0; i < 12; ++i) {
+      const uint32_t e = (d[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+      cand |= (uint32_t)((e & msk) == wq) << i;
+      esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
     }
-    if (!general) {
-      // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
-      const uint64_t L = k - qf, n = ix.n;
-      while (cand) {
-        const uint32_t i = (uint32_t)__ffs(cand) - 1u;
-        cand &= cand - 1;
-        const uint64_t p = ix.vsa[base + i];
-        const uint64_t wq = p >= k ? p - k : p + n - k;
-        if constexpr (kBytes) {  // the SA sector, then the window's words
-          constexpr uint64_t C = 32ull * kLongPW;
-          by += 32;
-          if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
-          else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
-          else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
-            by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
-                  (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
-          continue;
-        }
-        bool eq;
-        if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, P, wq, L, rare);
-        else eq = window_eq_long<kLongWords>(ix, P, wq, L);
-        res += eq ? 1u : 0u;
-      }
-    }
+    const uint32_t in = (1u << (uint32_t)(ep - sp)) - 1u;
+    cand &= in;
+    return (esc & in) == 0;  // 32-B records keep the escape bit; compact ones escape whole
   }
-  // the general search for the rest (k_count_list): one append per wave
+  if (ix.lctx && ep - (sp & ~15ull) <= 32) {
+    qf = kCtxQ;
+    base = sp & ~15ull;
+    const uint32_t lo = (uint32_t)(sp - base), hi = (uint32_t)(ep - base);
+    const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) + base);
+    const uint4 x0 = p[0], x1 = p[1];
+    const uint4 x2 = hi > 16 ? p[2] : make_uint4(0, 0, 0, 0), x3 = hi > 16 ? p[3] : make_uint4(0, 0, 0, 0);
+    if constexpr (kBytes) by += hi > 16 ? 64u : 32u;
+    const uint32_t dw[16] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w,
+                             x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+    const uint32_t msk = ((1u << (2 * kCtxQ)) - 1u) | kCtxEsc;
+    uint32_t esc = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+      cand |= (uint32_t)((e & msk) == want) << i;
+      esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+    }
+    const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    cand &= in;
+    return (esc & in) == 0;
+  }
+  return false;  // wider than the record and two sectors: steps first
+}
+
+// the general search for the patterns a long-pattern kernel does not answer: appended to
+// `list` (q), one atomic per wave
+__device__ __forceinline__ void long_list_append(bool general, uint64_t q, uint64_t* __restrict__ list,
+                                                 unsigned long long* __restrict__ nlist) {
   const uint64_t gm = __ballot(general);
-  if (gm) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint64_t at = 0;
-    if (lane == (uint32_t)__ffsll((unsigned long long)gm) - 1u) at = atomicAdd(nlist, (unsigned long long)__popcll(gm));
-    at = __shfl(at, __ffsll((unsigned long long)gm) - 1, 64);
-    if (general) list[at + __popcll(gm & ((1ull << lane) - 1))] = q;
+  if (!gm) return;
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t at = 0;
+  if (lane == (uint32_t)__ffsll((unsigned long long)gm) - 1u) at = atomicAdd(nlist, (unsigned long long)__popcll(gm));
+  at = __shfl(at, __ffsll((unsigned long long)gm) - 1, 64);
+  if (general) list[at + __popcll(gm & ((1ull << lane) - 1))] = q;
+}
+
+// kWv: waves per SIMD the registers are held to (0: the compiler's choice; tuning hook
+// CS_FM_LONG_WAVES, read per call)
+template <int W, bool kPT, bool kBytes = false, int kV16 = 0, int kWv = 0>
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kWv ? kWv : 1))) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                     const uint64_t* __restrict__ offs, uint64_t npat,
+                                                     CountOut co, uint64_t fixed_m,
+                                                     uint64_t* __restrict__ list,
+                                                     unsigned long long* __restrict__ nlist,
+                                                     bool skip_short, LongRoute lr) {
+  __shared__ uint16_t cmap[256];
+  __shared__ uint32_t rare[kMaxExc];
+  static_assert(kBlk >= 256, "one map entry per thread");
+  if (threadIdx.x < 256)
+    cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
+  if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+  if (q >= npat) return;
+  const uint64_t o0 = offs ? offs[q] : q * fixed_m;
+  const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
+  if (skip_short) {
+    const bool mine = m >= kFastM && m > ix.ptab_k + kCtxQ;  // the staged kernel skipped it
+    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(mine) && threadIdx.x == 0)
+      __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!mine) return;
   }
+  if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
+    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
+    else store_count<W>(co, q, m == 0 ? ix.n : 0);
+    return;
+  }
+  uint64_t by = 0;  // kBytes
+  uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
+  uint64_t base;
+  uint32_t cand, qf;
+  const bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+  uint64_t res = 0;
+  if (!general) {
+    // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
+    const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
+    while (cand) {
+      const uint32_t i = (uint32_t)__ffs(cand) - 1u;
+      cand &= cand - 1;
+      if constexpr (kPT) {
+        if (ix.wctx && k <= kWctxQ) {  // the window inside the row's window context: one read
+          const ulonglong2 e = ix.wctx[base + i];
+          if (!((e.y >> (kWctxEsc - 64)) & 1u)) {
+            if constexpr (kBytes) by += 32;  // its DRAM sector
+            else res += wctx_eq(e, pc, k, L) ? 1u : 0u;
+            continue;
+          }
+        }
+      }
+      const uint64_t p = ix.vsa[base + i];
+      const uint64_t wq = p >= k ? p - k : p + n - k;
+      if constexpr (kBytes) {  // the SA sector, then the window's words
+        constexpr uint64_t C = 32ull * kLongPW;
+        by += 32;
+        if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
+        else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
+        else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
+          by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
+                (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
+        continue;
+      }
+      bool eq;
+      if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
+      else eq = window_eq_long<kLongWords>(ix, pats + o0, wq, L);
+      res += eq ? 1u : 0u;
+    }
+  }
+  long_list_append(general, q, list, nlist);
   if (general) return;
   if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
   else store_count<W>(co, q, res);
+}
+
+// Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
+constexpr uint64_t kLocTile = 2 * kBlk;
+
+// The long-pattern search for the one-call locate (launch_locate_onepass over full-SA
+// indexes: CS_Q_LONG, host batches of long patterns, long-pattern routing): k_count_long's
+// stages, then per pattern min(count, limit) and its record for k_locate_emit — the only
+// position itself (kLocStash: the SA entry the verification read, minus k) or a verified
+// window (first row, match bits, k), whose positions the emit kernel reads through SA — and
+// each wave adds its patterns' counts to their tile's total (zeroed before, or holding the
+// staged kernel's totals of the short patterns under routing).  The patterns it cannot
+// finish (as k_count_long's, and windows whose matches lie too far apart for the record)
+// go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search), :125 (limit).
+template <int kV16>
+__global__ __launch_bounds__(kBlk) void k_locate_long(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                      const uint64_t* __restrict__ offs, uint64_t npat,
+                                                      uint64_t limit, OnePass op, uint64_t* __restrict__ list,
+                                                      unsigned long long* __restrict__ nlist, bool skip_short,
+                                                      LongRoute lr) {
+  __shared__ uint16_t cmap[256];
+  __shared__ uint32_t rare[kMaxExc];
+  if (threadIdx.x < 256)
+    cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
+  if (threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
+  __syncthreads();
+  // no lane returns early: the wave sums its counts at the end
+  const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+  bool mine = q < npat, general = false;
+  const uint64_t o0 = mine ? offs[q] : 0, m = mine ? offs[q + 1] - o0 : 0;
+  if (skip_short) {
+    const bool lg = mine && m >= kFastM && m > ix.ptab_k + kCtxQ;  // the staged kernel skipped it
+    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(lg) && threadIdx.x == 0)
+      __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    mine = lg;
+  }
+  uint64_t kc = 0, rec = 0;
+  if (mine && m != 0 && ix.n != 0) {  // fm_index.cpp:109: locate("") = {}
+    uint64_t by = 0, pc[kLongPW], base;
+    uint32_t cand, qf;
+    general = !long_stage<true, false, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+    if (!general && cand) {
+      const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
+      uint32_t mm = 0;
+      uint64_t p0 = 0;  // the first matching row's position
+      for (uint32_t c = cand; c; c &= c - 1) {
+        const uint32_t i = (uint32_t)__ffs(c) - 1u;
+        const uint64_t p = ix.vsa[base + i];
+        const uint64_t wq = p >= k ? p - k : p + n - k;
+        if (window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare)) {
+          if (!mm) p0 = wq;
+          mm |= 1u << i;
+        }
+      }
+      if (mm) {
+        const uint64_t c = (uint64_t)__popc(mm);
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u, rel = mm >> f;
+        kc = c < limit ? c : limit;  // fm_index.cpp:125
+        if (kc == 1) rec = kLocStash | p0;
+        else if (kc > 1 && ((rel >> kLocVerRelBits) || k > kLocVerMaxK)) general = true;
+        else rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
+      }
+    }
+  }
+  if (general) kc = 0;  // k_locate_list adds it
+  long_list_append(general, q, list, nlist);
+  if (mine && !general) {
+    op.cnt[q] = (uint32_t)kc;
+    op.rec[q] = rec;
+  }
+  uint64_t s = kc;  // the wave's 64 patterns lie in one tile
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
+}
+
+// Long-pattern routing, once per routed batch (block 0 of the list kernel): end the mode
+// after a batch without long patterns (lr.used_d clear), else re-arm used_d
+__device__ __forceinline__ void long_route_end(const LongRoute& lr) {
+  if (lr.used_d && blockIdx.x == 0 && threadIdx.x == 0) {
+    if (__hip_atomic_load(lr.used_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_store(lr.used_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(lr.seen_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(lr.seen_h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // The patterns k_count_long listed: the general search (count_pattern), the node table
@@ -2059,14 +2197,7 @@ __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t*
                                                      const unsigned long long* __restrict__ nlist,
                                                      LongRoute lr) {
   __shared__ NodeTable T;
-  if (lr.used_d && blockIdx.x == 0 && threadIdx.x == 0) {
-    if (__hip_atomic_load(lr.used_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      __hip_atomic_store(lr.used_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(lr.seen_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(lr.seen_h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  long_route_end(lr);
   const uint64_t nl = *nlist;
   if ((uint64_t)blockIdx.x * kBlk >= nl) return;  // uniform over the block
   load_table(T, ix.table);
@@ -2081,6 +2212,32 @@ __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t*
     } else {
       store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
     }
+  }
+}
+
+// The patterns k_locate_long listed: locate's general search (locate_search), its count
+// and record for k_locate_emit, the count added to the pattern's tile; a fixed grid
+// striding over the list, as k_count_list (which also ends the routing mode here).
+__global__ __launch_bounds__(kBlk) void k_locate_list(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                      const uint64_t* __restrict__ offs, uint64_t limit,
+                                                      OnePass op, const uint64_t* __restrict__ list,
+                                                      const unsigned long long* __restrict__ nlist,
+                                                      LongRoute lr) {
+  __shared__ NodeTable T;
+  long_route_end(lr);
+  const uint64_t nl = *nlist;
+  if ((uint64_t)blockIdx.x * kBlk >= nl) return;  // uniform over the block
+  load_table(T, ix.table);
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * (uint64_t)kBlk + threadIdx.x; i < nl; i += (uint64_t)gridDim.x * kBlk) {
+    const uint64_t q = list[i];
+    const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+    uint64_t r = 0;
+    const uint64_t c = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, r) : 0;
+    const uint64_t kc = c < limit ? c : limit;  // fm_index.cpp:125
+    op.cnt[q] = (uint32_t)kc;
+    op.rec[q] = r;
+    if (kc) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), kc);
   }
 }
 
@@ -3295,6 +3452,68 @@ __global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ 
   out[w] = acc;
 }
 
+// Window contexts (DevIndex::wctx): entry r = the codes of text[SA[r] - kWctxQ, SA[r])
+// (cyclic, as row r's LF chain reads them) from the 2-bit text, character i at bits 2i;
+// bit kWctxEsc when one of those positions holds a rare symbol (the sorted list `rare`).
+// A thread per row: its SA entry (coalesced) and two or three 2-bit words.
+__global__ __launch_bounds__(kBlk) void k_build_wctx(const uint32_t* __restrict__ sa, uint64_t n,
+                                                     const uint64_t* __restrict__ ptext,
+                                                     const uint32_t* __restrict__ rare, uint32_t nr,
+                                                     ulonglong2* __restrict__ out) {
+  __shared__ uint32_t srare[kMaxExc];
+  if (threadIdx.x < nr) srare[threadIdx.x] = rare[threadIdx.x];
+  __syncthreads();
+  const uint64_t r = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t p = sa[r];
+  uint64_t lo = 0, hi = 0;
+  bool esc = false;
+  if (p >= kWctxQ) {
+    const uint64_t q = p - kWctxQ;  // characters [q, p): inside the 2-bit text and its slack
+    const uint64_t a = q >> 5;
+    const uint32_t s = (uint32_t)(q & 31) * 2;
+    const uint64_t w0 = ptext[a], w1 = ptext[a + 1], w2 = ptext[a + 2];
+    lo = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
+    hi = (s ? (w1 >> s) | (w2 << (64 - s)) : w1) & ((1ull << (2 * kWctxQ - 64)) - 1);
+    esc = rare_in(srare, nr, q, kWctxQ);
+  } else {  // through the start of the text: the rotation's characters one by one
+    for (uint32_t i = 0; i < kWctxQ; ++i) {
+      const uint64_t t = (p + 64 * n - kWctxQ + i) % n;
+      const uint64_t c = (ptext[t >> 5] >> (2 * (t & 31))) & 3u;
+      if (i < 32) lo |= c << (2 * i);
+      else hi |= c << (2 * (i - 32));
+      esc |= rare_in(srare, nr, t, 1);
+    }
+  }
+  if (esc) hi |= 1ull << (kWctxEsc - 64);
+  out[r] = make_ulonglong2(lo, hi);
+}
+
+// Window contexts for k_count_long: 16 B per row (C4: 64 GB), built from the full suffix
+// array and the 2-bit text, lowest in the HBM order (after every saved part and the 2-bit
+// text).  A Q_text 33- to 77-mer at k = 15 then costs its record and one window-context
+// read per candidate instead of the record, the SA entry and the 2-bit window after it.
+// CS_FM_WCTX=0 (read at build / open, and by every long-pattern count) leaves them out.
+cs_status derive_window_contexts(cs_fm_index* h, hipStream_t st) {
+  if (h->d_wctx || !h->d_ptext || !h->d_sa || h->n < 1) return CS_OK;
+  if (const char* e = std::getenv("CS_FM_WCTX"))
+    if (std::atoi(e) == 0) return CS_OK;
+  if (!hbm_room(h, h->wctx_bytes())) return CS_OK;
+  void* w = nullptr;
+  FMX_HIP(hipMalloc(&w, h->wctx_bytes() + kPartPad));
+  k_build_wctx<<<grid_for(h->n, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
+      static_cast<const uint32_t*>(h->d_sa), h->n, static_cast<const uint64_t*>(h->d_ptext),
+      static_cast<const uint32_t*>(h->d_prare), h->nrare, static_cast<ulonglong2*>(w));
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    (void)hipFree(w);
+    return hip_fail(e, "window contexts");
+  }
+  h->d_wctx = w;
+  return CS_OK;
+}
+
 // Long patterns are verified against 32 text characters per 8-B word instead of 8
 // (k_count_long): n / 4 bytes (C4: 1 GB), for narrow lf_exact occurrence-line indexes that
 // keep the full suffix array and the text in HBM (the verification's preconditions), HBM
@@ -3345,7 +3564,7 @@ cs_status derive_packed_text(cs_fm_index* h, hipStream_t st) {
   h->d_ptext = pt;
   h->d_prare = pr;
   h->nrare = nr;
-  return CS_OK;
+  return derive_window_contexts(h, st);
 }
 
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
@@ -3379,7 +3598,8 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
     d.lctx_q = 0;
   }
   // CS_Q_NO_FULL_SA: locate's phase 2 walks, and a walk takes no verified windows
-  if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA)) d.vsa = nullptr, d.vtext = nullptr;
+  if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA))
+    d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr, d.wctx = nullptr;
   if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
   return d;
 }
@@ -3409,13 +3629,21 @@ bool qctx_staged() {
   return !(e && std::atoi(e) == 0);
 }
 
+int long_waves() {
+  const char* e = std::getenv("CS_FM_LONG_WAVES");
+  return e ? std::atoi(e) : 0;
+}
+
 // k_count_long over the batch (skip_short: only its long patterns, as k_count_ctx's kSkipLong),
 // then k_count_list over the patterns it listed; byte_text: the byte text even when the
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
 template <bool kBytes>
-cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
+cs_status launch_count_long_t(const DevIndex& ix0, const uint8_t* d_pats, const uint64_t* d_offs,
                               uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
                               bool skip_short, const LongRoute& lr, bool byte_text) {
+  DevIndex ix = ix0;
+  if (const char* e = std::getenv("CS_FM_WCTX"))  // test hook, also read per call: 0 = no window contexts
+    if (std::atoi(e) == 0) ix.wctx = nullptr;
   const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
   StreamBuf lb;
   FMX_HIP(lb.alloc(npat * 8 + 8, st));
@@ -3432,6 +3660,9 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
   else if (ix.ptext && !byte_text && v16 == 2)
     k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
                                                          lb.as<uint64_t>(), nl, skip_short, lr);
+  else if (ix.ptext && !byte_text && v16 == 3 && long_waves() == 5)
+    k_count_long<0, true, kBytes, 3, 5><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
+                                                            lb.as<uint64_t>(), nl, skip_short, lr);
   else if (ix.ptext && !byte_text && v16 == 3)
     k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
                                                          lb.as<uint64_t>(), nl, skip_short, lr);
@@ -3627,7 +3858,7 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
 cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, hipStream_t st,
-                                bool* done) {
+                                bool* done, uint32_t flags) {
   *done = false;
   if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
     if (std::atoi(e) == 0) return CS_OK;
@@ -3658,9 +3889,20 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // a range wider than kLocSmall rows takes over kLocSmall positions of the capacity, and
   // a pattern has at most one
   const uint64_t wide_cap = std::min<uint64_t>(cap / (kLocSmall + 1) + 1, npat);
+  // long patterns (full-SA indexes with the 2-bit text): k_locate_long takes every pattern
+  // of a CS_Q_LONG batch (host batches of long patterns pass it), and under long-pattern
+  // routing (the handle's flag, raised by a staged kernel that met long patterns — count's
+  // or this one's) the staged kernel leaves the long ones to it
+  const bool lk = kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
+  const LongRoute route = lk ? long_route(h, ix) : LongRoute{};
+  const bool long_only = lk && (flags & CS_Q_LONG);
+  const bool routed = lk && !long_only && route.seen_h && *reinterpret_cast<volatile uint32_t*>(h->route_h);
+  static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
   StreamBuf ws;
   const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
-  FMX_HIP(ws.alloc(npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16, st));
+  const uint64_t lo = (npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull;
+  const uint64_t lb = long_only || routed ? npat * 8 + 8 : 0;  // k_locate_long's list
+  FMX_HIP(ws.alloc(lo + lb, st));
   OnePass op;
   op.rec = ws.as<uint64_t>();
   op.tiles = op.rec + npat;
@@ -3675,9 +3917,29 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide_cap = wide_cap;
   FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
-  if (kpos == 0)
+  if (long_only || routed) {
+    uint64_t* list = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(ws.p) + lo);
+    unsigned long long* nl = reinterpret_cast<unsigned long long*>(list + npat);
+    FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
+    if (long_only)
+      FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8, st));
+    else
+      k_count_ctx<OccE, U, true, false, 8, false, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+    FMX_HIP(hipGetLastError());
+    const unsigned g1 = grid_for(npat, kBlk, 0xFFFFFFFFu);
+    const LongRoute lr = routed ? route : LongRoute{};
+    // tuning hook CS_FM_LONG_V16 (k_count_long's): 0 = 8-B pattern / window loads
+    const char* ev = std::getenv("CS_FM_LONG_V16");
+    if (ev && std::atoi(ev) == 0)
+      k_locate_long<0><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, list, nl, routed, lr);
+    else
+      k_locate_long<3><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, list, nl, routed, lr);
+    FMX_HIP(hipGetLastError());
+    k_locate_list<<<std::min(g1, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, limit, op, list, nl, lr);
+  } else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, route);
   else if (kpos == 1)
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);

@@ -90,6 +90,10 @@ typedef struct cs_fm_info {
   uint64_t packed_text_bytes; /* 2-bit copy of the text (occurrence lines, lf_exact, full SA and
                               text in HBM) that long patterns are verified against; 0 = none.
                               Derived from the text on build / open / import, not saved. */
+  uint64_t window_context_bytes; /* per BWT row the 62 characters before its rotation (16 B,
+                              with the 2-bit text, HBM allowing): long-pattern counts compare
+                              a window of up to 62 characters in one read; 0 = none.  Derived,
+                              not saved. */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);
@@ -254,13 +258,16 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
  *                      even when the full suffix array is kept
  *   CS_Q_NO_WALK_LINES locate phase 2: walk the rank structure to the reference's row
  *                      samples (row % ssa_stride == 0) even when walk lines exist
- *   CS_Q_LONG          count: a hint that the batch holds long patterns (~100
- *                      characters and more) — one pattern per lane and the text
- *                      comparison with look-ahead, outside the 20-mer kernel
- *                      (occurrence-line indexes that verify; implied by a fixed-length
- *                      batch with m > 96 and by a host batch, cs_fm_count_batch, whose
- *                      patterns are all longer than 96).  C4: 150-mers +17 %, 64-mers
- *                      -8 %. */
+ *   CS_Q_LONG          count and the one-call locate: a hint that the batch holds long
+ *                      patterns (32 characters and more) — one pattern per lane in the
+ *                      long-pattern kernels (record, candidates, SA entry, 2-bit text
+ *                      window), outside the 20-mer kernel (occurrence-line indexes that
+ *                      keep the full suffix array and the text; implied by a fixed-length
+ *                      batch with m > 31 and by a host batch, cs_fm_count_batch /
+ *                      cs_fm_locate_batch, whose patterns are all longer than 31).  Without
+ *                      it, device batches holding long patterns are routed to the same
+ *                      kernels from the next batch on (the handle's routing flag).
+ *                      Results never change. */
 #define CS_Q_NO_PREFIX 1u
 #define CS_Q_NO_CONTEXTS 2u
 #define CS_Q_NO_FULL_SA 4u
@@ -342,14 +349,21 @@ cs_status cs_fm_locate_walk_device_async_ex(const cs_fm_index* h, const uint64_t
 /* locate of a batch in one call — FMIndex::locate (fm_index.cpp:107-157) for every
  * pattern: d_out_offs (npat + 1 entries) = the exclusive scan of min(count, limit), and
  * d_out_pos[d_out_offs[q] ..] pattern q's positions in the reference's row order.  On
- * indexes that keep the full suffix array (occurrence lines with a prefix table and
- * left contexts: C2, C4) one launch does the search, the scan (a decoupled look-back
- * across blocks) and the positions; otherwise the two phases above run back to back.
- * Returns CS_ERR_CAPACITY with *total set and the offsets written when the positions do
- * not fit `cap` (positions are then incomplete).  Synchronises `stream`. */
+ * occurrence-line indexes with a prefix table and left contexts that keep the full suffix
+ * array (C2, C4) or walk lines with text-position marks (C5) three launches — search,
+ * scan of the per-block totals, positions — and one host synchronisation; otherwise the
+ * two phases above run back to back.  Returns CS_ERR_CAPACITY with *total set and the
+ * offsets written when the positions do not fit `cap` (positions are then incomplete).
+ * Synchronises `stream`. */
 cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                               uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                               uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream);
+/* The same under query flags (CS_Q_*): CS_Q_LONG sends every pattern to the long-pattern
+ * search (k_locate_long); the other flags apply when the two phases run. */
+cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
+                                 void* stream);
 /* Measurement twin of phase 2 (bench.py's walk roofline): d_steps[j] = the LF steps the
  * walk of reported row j takes before its sample (0 with the full suffix array). */
 cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,

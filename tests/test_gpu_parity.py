@@ -280,6 +280,9 @@ def test_engine_choice(built):
         # LF one n-cycle, with the full suffix array and the text in HBM
         ptext = engine == 1 and full_sa and info.text_in_hbm and not wide
         assert info.packed_text_bytes == ((info.n + 31) // 32 * 8 if ptext else 0), name
+        # window contexts (16 B per row) come with the 2-bit text
+        wctx = ptext and os.environ.get("CS_FM_WCTX") != "0"
+        assert info.window_context_bytes == (info.n * 16 if wctx else 0), name
         assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
 
 
@@ -505,9 +508,17 @@ def test_count_long_kernel_large(pkg):
         with _env(CS_FM_LONG_V16=v):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert np.array_equal(got, want), v
+    with _env(CS_FM_WCTX="0"):  # SA entry + 2-bit window instead of the window contexts
+        got, _, _ = _count_ex(g, pats, flags=32)
+    assert np.array_equal(got, want), "wctx=0"
     for _ in range(2):  # the default path: detection, then long-pattern routing
         got, _, _ = _count_ex(g, pats)
         assert np.array_equal(got, want)
+    # locate in one call: k_locate_long (CS_Q_LONG), then detection and routing
+    woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=100, nthreads=8)
+    want_l = [wpos[woffs[q]:woffs[q + 1]].tolist() for q in range(len(pats))]
+    for f in (32, 0, 0):
+        assert _locate_one(g, pats, 100, f) == want_l, f
 
 
 @pytest.mark.parametrize("stride", [1, 3, 8, 33, 64])
@@ -809,6 +820,9 @@ def test_count_verify_long(built, pkg, name):
     with _env(CS_FM_LONG_V16="0"):  # 8-B pattern and window loads
         got, _, _ = _count_ex(g, pats, flags=32)
     assert got.tolist() == want, (name, "v16=0")
+    with _env(CS_FM_WCTX="0"):  # no window contexts: the SA entry and the 2-bit window
+        got, _, _ = _count_ex(g, pats, flags=32)
+    assert got.tolist() == want, (name, "wctx=0")
     # long-pattern routing of the default path: the batches above raised the handle's flag,
     # so these run the staged kernel for the short patterns and k_count_long for the rest;
     # a batch of short patterns only ends the mode, the next mixed batch raises it again
@@ -867,6 +881,26 @@ def _locate_two_phase(g, pats, lim, flags):
     return [pos[oo[q]:oo[q + 1]].tolist() for q in range(npat)]
 
 
+def _locate_one(g, pats, lim, flags=0):
+    """cs_fm_locate_device_ex: per pattern its positions (a first call for the total)."""
+    buf, offs = O.pack_patterns(pats)
+    d_buf = torch.from_numpy(buf.copy()).cuda()
+    d_offs = torch.from_numpy(offs.astype(np.int64)).cuda()
+    npat = len(pats)
+    d_oo = torch.zeros(npat + 1, dtype=torch.int64, device="cuda")
+    tot, ok = g.locate_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim, d_oo.data_ptr(), 0, 0,
+                              flags=flags)
+    d_pos = torch.zeros(max(tot, 1), dtype=torch.int64, device="cuda")
+    if tot:
+        tot2, ok = g.locate_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim, d_oo.data_ptr(),
+                                   d_pos.data_ptr(), tot, flags=flags)
+        assert ok and tot2 == tot
+    oo = d_oo.cpu().numpy()
+    assert oo[-1] == tot
+    pos = d_pos[:tot].cpu().numpy()
+    return [pos[oo[q]:oo[q + 1]].tolist() for q in range(npat)]
+
+
 @pytest.mark.parametrize("name", sorted(TEXTS))
 def test_locate_verify_long(built, pkg, name):
     """locate of long patterns: with the full suffix array and the text in HBM a narrow
@@ -908,6 +942,20 @@ def test_locate_verify_long(built, pkg, name):
         offs, pos = g.locate_batch(pats, limit=lim)
         for q, p in enumerate(pats):
             assert pos[offs[q]:offs[q + 1]].tolist() == want[q], (name, lim, p)
+        # the one call: CS_Q_LONG (k_locate_long for every pattern, then k_locate_list), the
+        # default path twice (the first raises the routing flag on indexes that route, the
+        # second leaves the long patterns to k_locate_long), 8-B loads (CS_FM_LONG_V16=0)
+        for f in (32, 0, 0):
+            assert _locate_one(g, pats, lim, f) == want, (name, lim, f)
+        with _env(CS_FM_LONG_V16="0"):
+            assert _locate_one(g, pats, lim, 32) == want, (name, lim, "v16=0")
+        short = [i for i, p in enumerate(pats) if len(p) < 32]  # ends the routing mode
+        assert _locate_one(g, [pats[i] for i in short], lim) == [want[i] for i in short], (name, lim)
+        lp = [i for i, p in enumerate(pats) if len(p) > 31]  # host batch: CS_Q_LONG unasked
+        if lp:
+            offs, pos = g.locate_batch([pats[i] for i in lp], limit=lim)
+            for j, i in enumerate(lp):
+                assert pos[offs[j]:offs[j + 1]].tolist() == want[i], (name, lim, pats[i])
 
 
 @pytest.mark.parametrize("name", sorted(TEXTS))
