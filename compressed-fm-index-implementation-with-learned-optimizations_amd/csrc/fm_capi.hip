@@ -436,7 +436,6 @@ void free_index(cs_fm_index* h) {
   if (h->d_sa) (void)hipFree(h->d_sa);
   if (h->d_dtext) (void)hipFree(h->d_dtext);
   if (h->d_ptext) (void)hipFree(h->d_ptext);
-  if (h->d_wctx) (void)hipFree(h->d_wctx);
   if (h->route_h) (void)hipHostFree(h->route_h);
   if (h->route_d) (void)hipFree(h->route_d);
   if (h->d_prare) (void)hipFree(h->d_prare);
@@ -596,7 +595,6 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->record_bytes = h->ptab_rec ? h->ptab_entry_bytes() : 0u;
   out->text_in_hbm = h->d_dtext ? 1u : 0u;
   out->packed_text_bytes = h->d_ptext ? h->ptext_bytes() : 0;
-  out->window_context_bytes = h->d_wctx ? h->wctx_bytes() : 0;
   return CS_OK;
 }
 

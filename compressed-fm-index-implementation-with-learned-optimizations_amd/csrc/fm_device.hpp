@@ -132,15 +132,7 @@ struct DevIndex {
   const uint64_t* ptext;
   const uint32_t* prare;
   uint32_t nrare;
-  // Window contexts (null when absent; set only with ptext): per BWT row r the codes of
-  // the kWctxQ characters before its rotation, text[SA[r] - kWctxQ, SA[r]) (cyclic),
-  // character i at bits 2i of the 16-B entry, bit kWctxEsc set when one of them is a rare
-  // symbol — k_count_long compares a window of up to kWctxQ characters with one read
-  // instead of the SA entry and the 2-bit text after it (fm_query.hip derive_window_contexts).
-  const ulonglong2* wctx;
 };
-constexpr uint32_t kWctxQ = 62;
-constexpr uint32_t kWctxEsc = 124;
 
 // Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q
 // characters preceding the row's rotation — symbol t in bits [sb t, sb (t+1)).

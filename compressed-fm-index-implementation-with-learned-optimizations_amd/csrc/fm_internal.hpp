@@ -60,9 +60,6 @@ struct cs_fm_index {
   void* d_prare = nullptr;
   uint32_t nrare = 0;
   uint64_t ptext_bytes() const { return ((n + 31) / 32) * 8; }
-  // window contexts (DevIndex::wctx): 16 B per BWT row, derived with the 2-bit text
-  void* d_wctx = nullptr;
-  uint64_t wctx_bytes() const { return n * 16; }
   // Long-pattern routing of device batches (fm_query.hip launch_count_staged): a pinned,
   // device-mapped word the count kernels set when a batch held patterns over 32 characters
   // (then the next batches send those to k_count_long), and two HBM words of bookkeeping.
@@ -149,7 +146,6 @@ struct cs_fm_index {
     d.ptext = ver && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
     d.prare = static_cast<const uint32_t*>(d_prare);
     d.nrare = nrare;
-    d.wctx = d.ptext && d_wctx ? static_cast<const ulonglong2*>(d_wctx) : nullptr;
     return d;
   }
 };
@@ -249,8 +245,6 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st);
 cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st);
 // the 2-bit text of d_dtext (cs_fm_index::d_ptext), when the index can use it (fm_query.hip)
 cs_status derive_packed_text(cs_fm_index* h, hipStream_t st);
-// the window contexts (cs_fm_index::d_wctx), with the 2-bit text (fm_query.hip)
-cs_status derive_window_contexts(cs_fm_index* h, hipStream_t st);
 // HBM held by the index's device arrays so far (the image parts, fm_io.hip)
 uint64_t index_hbm_bytes(const cs_fm_index* h);
 // Whether an optional structure of `bytes` may be allocated: the device keeps an eighth

@@ -231,7 +231,6 @@ uint64_t index_hbm_bytes(const cs_fm_index* hc) {
   for (const Part& p : index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr))
     if (*p.dptr) b += p.bytes;
   if (h->d_ptext) b += h->ptext_bytes();  // derived, not an image part
-  if (h->d_wctx) b += h->wctx_bytes();
   return b;
 }
 

@@ -1871,27 +1871,6 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 // profiles/r03/long_probe_lds_stage.json; not kept.)
 // kV16: the pattern's bytes through 16-B aligned vector loads (1: pack_pattern16 and
 // load_tail32_v16, 2: pack_pattern16 only, 3: 2 and the packed window as 16-B vectors)
-// P[0, L) (pc: packed, pack_pattern's order) against the window text[SA[r] - k, SA[r] - k + L)
-// held in row r's window context e (k <= kWctxQ; its characters [kWctxQ - k, kWctxQ - k + L))
-__device__ __forceinline__ bool wctx_eq(ulonglong2 e, const uint64_t* pc, uint64_t k, uint64_t L) {
-  const uint32_t sh = 2 * (uint32_t)(kWctxQ - k);
-  uint64_t x0, x1;
-  if (sh == 0) {
-    x0 = e.x;
-    x1 = e.y;
-  } else if (sh < 64) {
-    x0 = (e.x >> sh) | (e.y << (64 - sh));
-    x1 = e.y >> sh;
-  } else {
-    x0 = e.y >> (sh - 64);
-    x1 = 0;
-  }
-  const uint32_t b = 2 * (uint32_t)L;  // bits compared (<= 2 kWctxQ)
-  const uint64_t m0 = b >= 64 ? ~0ull : (1ull << b) - 1;
-  const uint64_t m1 = b > 64 ? (1ull << (b - 64)) - 1 : 0ull;
-  return !(((x0 ^ pc[0]) & m0) | ((x1 ^ pc[1]) & m1));
-}
-
 // (A)-(C) of the long-pattern search of one pattern (m > 0 characters at pats + o0, n > 0):
 // the candidate rows base + i (bit i of cand) whose chains spell the qf characters before the
 // table part — what is left is the window text[SA - k, SA - qf) against P[0, k - qf),
@@ -2020,10 +1999,8 @@ __device__ __forceinline__ void long_list_append(bool general, uint64_t q, uint6
   if (general) list[at + __popcll(gm & ((1ull << lane) - 1))] = q;
 }
 
-// kWv: waves per SIMD the registers are held to (0: the compiler's choice; tuning hook
-// CS_FM_LONG_WAVES, read per call)
-template <int W, bool kPT, bool kBytes = false, int kV16 = 0, int kWv = 0>
-__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kWv ? kWv : 1))) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
+template <int W, bool kPT, bool kBytes = false, int kV16 = 0>
+__global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m,
                                                      uint64_t* __restrict__ list,
@@ -2063,16 +2040,6 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kWv ? kWv 
     while (cand) {
       const uint32_t i = (uint32_t)__ffs(cand) - 1u;
       cand &= cand - 1;
-      if constexpr (kPT) {
-        if (ix.wctx && k <= kWctxQ) {  // the window inside the row's window context: one read
-          const ulonglong2 e = ix.wctx[base + i];
-          if (!((e.y >> (kWctxEsc - 64)) & 1u)) {
-            if constexpr (kBytes) by += 32;  // its DRAM sector
-            else res += wctx_eq(e, pc, k, L) ? 1u : 0u;
-            continue;
-          }
-        }
-      }
       const uint64_t p = ix.vsa[base + i];
       const uint64_t wq = p >= k ? p - k : p + n - k;
       if constexpr (kBytes) {  // the SA sector, then the window's words
@@ -3452,68 +3419,6 @@ __global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ 
   out[w] = acc;
 }
 
-// Window contexts (DevIndex::wctx): entry r = the codes of text[SA[r] - kWctxQ, SA[r])
-// (cyclic, as row r's LF chain reads them) from the 2-bit text, character i at bits 2i;
-// bit kWctxEsc when one of those positions holds a rare symbol (the sorted list `rare`).
-// A thread per row: its SA entry (coalesced) and two or three 2-bit words.
-__global__ __launch_bounds__(kBlk) void k_build_wctx(const uint32_t* __restrict__ sa, uint64_t n,
-                                                     const uint64_t* __restrict__ ptext,
-                                                     const uint32_t* __restrict__ rare, uint32_t nr,
-                                                     ulonglong2* __restrict__ out) {
-  __shared__ uint32_t srare[kMaxExc];
-  if (threadIdx.x < nr) srare[threadIdx.x] = rare[threadIdx.x];
-  __syncthreads();
-  const uint64_t r = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-  if (r >= n) return;
-  const uint64_t p = sa[r];
-  uint64_t lo = 0, hi = 0;
-  bool esc = false;
-  if (p >= kWctxQ) {
-    const uint64_t q = p - kWctxQ;  // characters [q, p): inside the 2-bit text and its slack
-    const uint64_t a = q >> 5;
-    const uint32_t s = (uint32_t)(q & 31) * 2;
-    const uint64_t w0 = ptext[a], w1 = ptext[a + 1], w2 = ptext[a + 2];
-    lo = s ? (w0 >> s) | (w1 << (64 - s)) : w0;
-    hi = (s ? (w1 >> s) | (w2 << (64 - s)) : w1) & ((1ull << (2 * kWctxQ - 64)) - 1);
-    esc = rare_in(srare, nr, q, kWctxQ);
-  } else {  // through the start of the text: the rotation's characters one by one
-    for (uint32_t i = 0; i < kWctxQ; ++i) {
-      const uint64_t t = (p + 64 * n - kWctxQ + i) % n;
-      const uint64_t c = (ptext[t >> 5] >> (2 * (t & 31))) & 3u;
-      if (i < 32) lo |= c << (2 * i);
-      else hi |= c << (2 * (i - 32));
-      esc |= rare_in(srare, nr, t, 1);
-    }
-  }
-  if (esc) hi |= 1ull << (kWctxEsc - 64);
-  out[r] = make_ulonglong2(lo, hi);
-}
-
-// Window contexts for k_count_long: 16 B per row (C4: 64 GB), built from the full suffix
-// array and the 2-bit text, lowest in the HBM order (after every saved part and the 2-bit
-// text).  A Q_text 33- to 77-mer at k = 15 then costs its record and one window-context
-// read per candidate instead of the record, the SA entry and the 2-bit window after it.
-// CS_FM_WCTX=0 (read at build / open, and by every long-pattern count) leaves them out.
-cs_status derive_window_contexts(cs_fm_index* h, hipStream_t st) {
-  if (h->d_wctx || !h->d_ptext || !h->d_sa || h->n < 1) return CS_OK;
-  if (const char* e = std::getenv("CS_FM_WCTX"))
-    if (std::atoi(e) == 0) return CS_OK;
-  if (!hbm_room(h, h->wctx_bytes())) return CS_OK;
-  void* w = nullptr;
-  FMX_HIP(hipMalloc(&w, h->wctx_bytes() + kPartPad));
-  k_build_wctx<<<grid_for(h->n, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-      static_cast<const uint32_t*>(h->d_sa), h->n, static_cast<const uint64_t*>(h->d_ptext),
-      static_cast<const uint32_t*>(h->d_prare), h->nrare, static_cast<ulonglong2*>(w));
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) {
-    (void)hipFree(w);
-    return hip_fail(e, "window contexts");
-  }
-  h->d_wctx = w;
-  return CS_OK;
-}
-
 // Long patterns are verified against 32 text characters per 8-B word instead of 8
 // (k_count_long): n / 4 bytes (C4: 1 GB), for narrow lf_exact occurrence-line indexes that
 // keep the full suffix array and the text in HBM (the verification's preconditions), HBM
@@ -3564,7 +3469,7 @@ cs_status derive_packed_text(cs_fm_index* h, hipStream_t st) {
   h->d_ptext = pt;
   h->d_prare = pr;
   h->nrare = nr;
-  return derive_window_contexts(h, st);
+  return CS_OK;
 }
 
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
@@ -3599,7 +3504,7 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
   }
   // CS_Q_NO_FULL_SA: locate's phase 2 walks, and a walk takes no verified windows
   if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA))
-    d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr, d.wctx = nullptr;
+    d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr;
   if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
   return d;
 }
@@ -3629,21 +3534,13 @@ bool qctx_staged() {
   return !(e && std::atoi(e) == 0);
 }
 
-int long_waves() {
-  const char* e = std::getenv("CS_FM_LONG_WAVES");
-  return e ? std::atoi(e) : 0;
-}
-
 // k_count_long over the batch (skip_short: only its long patterns, as k_count_ctx's kSkipLong),
 // then k_count_list over the patterns it listed; byte_text: the byte text even when the
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
 template <bool kBytes>
-cs_status launch_count_long_t(const DevIndex& ix0, const uint8_t* d_pats, const uint64_t* d_offs,
+cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
                               uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
                               bool skip_short, const LongRoute& lr, bool byte_text) {
-  DevIndex ix = ix0;
-  if (const char* e = std::getenv("CS_FM_WCTX"))  // test hook, also read per call: 0 = no window contexts
-    if (std::atoi(e) == 0) ix.wctx = nullptr;
   const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
   StreamBuf lb;
   FMX_HIP(lb.alloc(npat * 8 + 8, st));
@@ -3660,9 +3557,6 @@ cs_status launch_count_long_t(const DevIndex& ix0, const uint8_t* d_pats, const 
   else if (ix.ptext && !byte_text && v16 == 2)
     k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
                                                          lb.as<uint64_t>(), nl, skip_short, lr);
-  else if (ix.ptext && !byte_text && v16 == 3 && long_waves() == 5)
-    k_count_long<0, true, kBytes, 3, 5><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
-                                                            lb.as<uint64_t>(), nl, skip_short, lr);
   else if (ix.ptext && !byte_text && v16 == 3)
     k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
                                                          lb.as<uint64_t>(), nl, skip_short, lr);

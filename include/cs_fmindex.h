@@ -90,10 +90,6 @@ typedef struct cs_fm_info {
   uint64_t packed_text_bytes; /* 2-bit copy of the text (occurrence lines, lf_exact, full SA and
                               text in HBM) that long patterns are verified against; 0 = none.
                               Derived from the text on build / open / import, not saved. */
-  uint64_t window_context_bytes; /* per BWT row the 62 characters before its rotation (16 B,
-                              with the 2-bit text, HBM allowing): long-pattern counts compare
-                              a window of up to 62 characters in one read; 0 = none.  Derived,
-                              not saved. */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -280,9 +280,6 @@ def test_engine_choice(built):
         # LF one n-cycle, with the full suffix array and the text in HBM
         ptext = engine == 1 and full_sa and info.text_in_hbm and not wide
         assert info.packed_text_bytes == ((info.n + 31) // 32 * 8 if ptext else 0), name
-        # window contexts (16 B per row) come with the 2-bit text
-        wctx = ptext and os.environ.get("CS_FM_WCTX") != "0"
-        assert info.window_context_bytes == (info.n * 16 if wctx else 0), name
         assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
 
 
@@ -508,9 +505,6 @@ def test_count_long_kernel_large(pkg):
         with _env(CS_FM_LONG_V16=v):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert np.array_equal(got, want), v
-    with _env(CS_FM_WCTX="0"):  # SA entry + 2-bit window instead of the window contexts
-        got, _, _ = _count_ex(g, pats, flags=32)
-    assert np.array_equal(got, want), "wctx=0"
     for _ in range(2):  # the default path: detection, then long-pattern routing
         got, _, _ = _count_ex(g, pats)
         assert np.array_equal(got, want)
@@ -820,9 +814,6 @@ def test_count_verify_long(built, pkg, name):
     with _env(CS_FM_LONG_V16="0"):  # 8-B pattern and window loads
         got, _, _ = _count_ex(g, pats, flags=32)
     assert got.tolist() == want, (name, "v16=0")
-    with _env(CS_FM_WCTX="0"):  # no window contexts: the SA entry and the 2-bit window
-        got, _, _ = _count_ex(g, pats, flags=32)
-    assert got.tolist() == want, (name, "wctx=0")
     # long-pattern routing of the default path: the batches above raised the handle's flag,
     # so these run the staged kernel for the short patterns and k_count_long for the rest;
     # a batch of short patterns only ends the mode, the next mixed batch raises it again
