@@ -24,6 +24,8 @@ import re
 import statistics
 import sys
 
+ONE_CALL = ("k_count_ctx_onepass", "k_count_ctx_onepass_skiplong", "k_locate_long", "k_locate_list",
+            "k_locate_emit", "k_locate_emit_wide")
 # the kernel that carries each leg's work
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
@@ -37,7 +39,9 @@ LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "locate_ssa_rows": "k_walk", "wm_locate_ssa": "k_walk",
               "locate_ssa": ("k_walk_fused", "k_walk_fused_wide"), "count_rdna": "count",
               "locate_rdna": ("k_locate_sa", "k_locate_sa_wide"),
-              "locate_one": ("k_count_ctx_onepass",)}
+              # the one-call locate: every kernel of the call (search, long-pattern search and
+              # its list, positions), summed per launch
+              "locate_one": ONE_CALL, "locate_m64": ONE_CALL, "locate_m150": ONE_CALL}
 
 # legs whose phase-2 reads are contiguous runs of the suffix array, not random rows
 LEG_STREAMED = {"locate_rdna"}
@@ -55,16 +59,16 @@ def short(name):
     """Readable kernel name: k_count_ctx (count) / k_count_ctx_loc (locate phase 1) with
     the template's U, packed flag and count width; the others by their base name."""
     m = re.search(r"k_count_ctx<[^,]*?(\w+E?), (\d), (true|false), (true|false), (\d)"
-                  r"(?:, (true|false))?(?:, (true|false))?(?:, (true|false))?>", name)
+                  r"(?:, (true|false))?(?:, (true|false))?(?:, (true|false))?(?:, (true|false))?(?:, (\d))?>", name)
     if m:
-        eng, u, loc, packed, w, nobar, one, skip = m.groups()
-        if one == "true":
-            return "k_count_ctx_onepass"
+        eng, u, loc, packed, w, nobar, one, skip, rng, pos = m.groups()
+        if one == "true":  # the one-call locate's search (skiplong: under long-pattern routing)
+            return "k_count_ctx_onepass%s" % ("_skiplong" if skip == "true" else "")
         if loc == "true":
             return "k_count_ctx_loc"
         return "k_count_ctx%s%s_w%s" % ("_packed" if packed == "true" else "",
                                          "_skiplong" if skip == "true" else "", w)
-    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?>", name)
+    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?(?:, \d+)?>", name)
     if m:  # the third argument: the measurement twin (kBytes)
         return "k_count_long%s%s" % ("_ptext" if m.group(2) == "true" else "_btext",
                                      "_bytes" if m.group(3) == "true" else "")
@@ -81,7 +85,7 @@ def short(name):
         if k in name:
             return k
     for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk_fused_wide",
-              "k_walk_fused", "k_walk",
+              "k_walk_fused", "k_walk", "k_locate_long", "k_locate_list", "k_locate_emit_wide", "k_locate_emit",
               "k_locate_ranges", "k_locate_sa_wide", "k_locate_sa", "k_expand_rows", "k_pack_wire"):
         if k in name:
             return k
@@ -137,7 +141,11 @@ def main():
         # a routed long-pattern count runs as k_count_ctx (skipping the long patterns),
         # k_count_long and k_count_list: the leg's launch is their sum
         group = [kname]
-        if kname and kname.startswith("k_count_long"):
+        if want is ONE_CALL:  # routed (the long-pattern search ran): its kernels, else the plain call's
+            routed = "k_locate_long" in res["kernels"]
+            group = sorted(n for n in cands if n in res["kernels"] and
+                           (n != "k_count_ctx_onepass" if routed else n != "k_count_ctx_onepass_skiplong"))
+        elif kname and kname.startswith("k_count_long"):
             group += [n for n in res["pmc"] if n == "k_count_list" or n.endswith("_skiplong_w8")
                       or (n.startswith("k_count_ctx_") and "skiplong" in n)]
             group = sorted(set(group))
@@ -148,6 +156,8 @@ def main():
             stream_rd = lo["roofline"].get("stream_read_bytes_per_launch")
         else:
             stream_rd = lo.get("phase2_stream_read_bytes")
+        if want is ONE_CALL and stream_rd is not None and lo.get("patterns"):
+            stream_rd += 12 * lo["patterns"]  # the emit kernel's read of the counts and records
         wl = lo.get("workload_key") or b.get("workload_key")  # the leg's own index
         kc = res["pmc"].get(kname, {}) if kname else {}
         if len(group) > 1:  # sums over the group (per launch of each)
