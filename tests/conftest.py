@@ -14,7 +14,9 @@ sys.path.insert(0, ROOT)
 
 
 # Time budget of the GPU suite (`pytest -m gpu`, one MI355X): at most ~550 s of the driver's
-# 900-s step.  Round 3: 8,686 tests in 506 s (profiles/r03/pytest_gpu_all_r03i.log) — 20
+# 900-s step.  Round 3: 8,686 tests in 506 s (profiles/r03/pytest_gpu_all_r03i.log), 570 s with
+# the one-call long-pattern locate checked on every variant, trimmed back to the variants
+# that run it (profiles/r03/pytest_gpu_all_r03n.log) — 20
 # engine variants x ~30 texts in test_gpu_parity.py (~23 s per variant) and the full-size
 # configs in test_gpu_scale.py (C5 2 x 36 s, C4 3 x 6-20 s).  A new engine variant costs
 # ~23 s; a new per-text test ~1 s per variant: trim elsewhere before adding either.

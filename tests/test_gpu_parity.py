@@ -508,11 +508,13 @@ def test_count_long_kernel_large(pkg):
     for _ in range(2):  # the default path: detection, then long-pattern routing
         got, _, _ = _count_ex(g, pats)
         assert np.array_equal(got, want)
-    # locate in one call: k_locate_long (CS_Q_LONG), then detection and routing
-    woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=100, nthreads=8)
-    want_l = [wpos[woffs[q]:woffs[q + 1]].tolist() for q in range(len(pats))]
-    for f in (32, 0, 0):
-        assert _locate_one(g, pats, 100, f) == want_l, f
+    # locate in one call: k_locate_long (CS_Q_LONG), then detection and routing (indexes with
+    # the 2-bit text)
+    if g.info().packed_text_bytes:
+        woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=100, nthreads=8)
+        want_l = [wpos[woffs[q]:woffs[q + 1]].tolist() for q in range(len(pats))]
+        for f in (32, 0, 0):
+            assert _locate_one(g, pats, 100, f) == want_l, f
 
 
 @pytest.mark.parametrize("stride", [1, 3, 8, 33, 64])
@@ -934,8 +936,11 @@ def test_locate_verify_long(built, pkg, name):
         for q, p in enumerate(pats):
             assert pos[offs[q]:offs[q + 1]].tolist() == want[q], (name, lim, p)
         # the one call: CS_Q_LONG (k_locate_long for every pattern, then k_locate_list), the
-        # default path twice (the first raises the routing flag on indexes that route, the
-        # second leaves the long patterns to k_locate_long), 8-B loads (CS_FM_LONG_V16=0)
+        # default path twice (the first raises the routing flag, the second leaves the long
+        # patterns to k_locate_long), 8-B loads (CS_FM_LONG_V16=0) — on the indexes that take
+        # the long-pattern kernels (the 2-bit text; the others' one call is checked above)
+        if not g.info().packed_text_bytes:
+            continue
         for f in (32, 0, 0):
             assert _locate_one(g, pats, lim, f) == want, (name, lim, f)
         with _env(CS_FM_LONG_V16="0"):
