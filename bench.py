@@ -924,7 +924,7 @@ def main():
     with LegGuard(leg_errors, "main legs"):
         if need_main and legs & set(LEGS_MAIN):
             steps, warm = max(3, args.steps // 2), 2
-            if "count_u32" in legs:
+            if "count_u32" in legs and N < 2 ** 32:  # uint32 counts need n < 2^32
                 o4 = torch.empty(B, dtype=torch.int32, device=dev)
                 lg["count_u32"], _ = count_leg(
                     "count_u32", "the headline batch with uint32 counts (exact, n < 2^32)", idx, info, wl,
@@ -933,7 +933,7 @@ def main():
                     0, stream_m + 4 * B, steps, warm, stream, sh, dev, counts,
                     lambda: o4.cpu().numpy().astype(np.int64))
                 del o4
-            if "count_packed" in legs and args.kind == "dna" and m <= 32:
+            if "count_packed" in legs and args.kind == "dna" and m <= 32 and N < 2 ** 32:
                 # 2-bit packed patterns (8 B each, no offsets) and uint32 counts
                 lut = torch.full((256,), 0, dtype=torch.int64, device=dev)
                 lut[torch.tensor(list(b"ACGT"), device=dev)] = torch.arange(4, device=dev)
@@ -1072,7 +1072,8 @@ def main():
                     del Wm
             for name, pk, u8 in (("count_stream", False, False), ("count_stream_packed", True, False),
                                  ("count_stream_packed_u8", True, True)):
-                if name in legs and (not pk or (args.kind == "dna" and m <= 32)):
+                # (u32 counts: n < 2^32; the uint8 form holds any count)
+                if name in legs and (not pk or (args.kind == "dna" and m <= 32 and (u8 or N < 2 ** 32))):
                     lg[name] = stream_leg(
                         name, "count of %d x %d M patterns streamed from page-locked host memory "
                         "(%s), H2D of the next chunk overlapped with the count and the D2H of the "
@@ -1415,7 +1416,9 @@ def main():
                             "rows": rows}
 
     with LegGuard(leg_errors, "repetitive-DNA legs"):
-        if legs & set(LEGS_RDNA) and args.kind == "dna":
+        # (a second text and index of the headline's size: C4-sized configs only — at C5 the
+        # two 32-GB texts and the index do not fit beside each other)
+        if legs & set(LEGS_RDNA) and args.kind == "dna" and N < 2 ** 32:
             # repetitive DNA: copies of a 2^20-base seed with ~0.75 % substitutions, so a
             # text 20-mer occurs in most of the ~3800 copies: ranges thousands of rows wide
             # step through the rank structure instead of ending in a context record

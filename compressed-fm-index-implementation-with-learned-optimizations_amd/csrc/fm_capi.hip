@@ -1002,9 +1002,12 @@ cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, co
   }
   hipStream_t st = (hipStream_t)stream;
   bool done = false;
-  s = launch_locate_onepass(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, st,
-                            &done, flags & CS_Q_LONG);
-  if (s != CS_OK) return s;
+  // any flag but CS_Q_LONG leaves structures out: the two phases honour it
+  if (!(flags & ~CS_Q_LONG)) {
+    s = launch_locate_onepass(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, st,
+                              &done, flags & CS_Q_LONG);
+    if (s != CS_OK) return s;
+  }
   if (!done) {  // the two phases: ranges, then (when the total fits) the positions
     StreamBuf sp;
     FMX_HIP(sp.alloc((npat ? npat : 1) * 8, st));

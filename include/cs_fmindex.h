@@ -355,7 +355,7 @@ cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const
                               uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                               uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream);
 /* The same under query flags (CS_Q_*): CS_Q_LONG sends every pattern to the long-pattern
- * search (k_locate_long); the other flags apply when the two phases run. */
+ * search (k_locate_long); any other flag runs the two phases under the flags. */
 cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                                  uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                                  uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,

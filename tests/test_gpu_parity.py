@@ -1023,6 +1023,8 @@ def test_locate_one_call(built, pkg, name):
         pos = d_pos[:tot].cpu().numpy()
         for q, p in enumerate(pats):
             assert pos[oo[q]:oo[q + 1]].tolist() == want[q], (name, lim, p)
+        if lim == 40:  # cs_fm_locate_device_ex under CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS: the two phases
+            assert _locate_one(g, pats, lim, 3) == want, (name, lim)
         if tot:
             d_oo2 = torch.zeros(npat + 1, dtype=torch.int64, device="cuda")
             tot2, ok2 = g.locate_device(d_buf.data_ptr(), d_offs.data_ptr(), npat, lim,
