@@ -940,6 +940,8 @@ def test_locate_verify_long(built, pkg, name):
         # patterns to k_locate_long), 8-B loads (CS_FM_LONG_V16=0) — on the indexes that take
         # the long-pattern kernels (the 2-bit text; the others' one call is checked above)
         if not g.info().packed_text_bytes:
+            if lim == 100000:  # CS_Q_LONG where the long-pattern kernels do not apply: the usual call
+                assert _locate_one(g, pats, lim, 32) == want, (name, lim, "Q_LONG")
             continue
         for f in (32, 0, 0):
             assert _locate_one(g, pats, lim, f) == want, (name, lim, f)
