@@ -163,7 +163,10 @@ template <int W>
 __device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint64_t v) {
   const uint32_t w = W ? (uint32_t)W : o.width;
   if (w == 8) {
-    static_cast<uint64_t*>(o.out)[q] = v;
+    // non-temporal: the counts stream out past the caches that the random record reads
+    // use (C4 headline 0.396 -> 0.388 ms in one box session; non-temporal pattern loads
+    // were measured too, 0.408 ms: profiles/r03/ab_nt_store.jsonl)
+    __builtin_nontemporal_store(v, static_cast<uint64_t*>(o.out) + q);
   } else if (w == 4) {
     static_cast<uint32_t*>(o.out)[q] = (uint32_t)v;
   } else {
