@@ -1152,6 +1152,15 @@ __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable
 // each, then the mark's sample) instead of SA[row], in (1) for a pattern's only position
 // and in (3) / k_locate_emit_wide for the rest (kPos: 0 the full SA, 1 WalkLine, 2
 // WalkLineW).  Counts are u64 (cnt64) when the index is wide.
+// The one-call locate's outputs (offsets and positions) leave through non-temporal stores:
+// nothing on the device reads them again (C4 one call 0.853 -> 0.818 ms in an A/B on one
+// box; the search kernel's records and counts, which the emit kernel reads back, measured
+// the same either way: profiles/r03/ab_nt_locate.jsonl)
+template <class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+  __builtin_nontemporal_store(v, p);
+}
+
 struct OnePass {
   uint32_t* cnt = nullptr;               // (1) -> (3): min(count, limit) per pattern (narrow)
   uint64_t* cnt64 = nullptr;             // the same, wide indexes
@@ -1338,11 +1347,11 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (q >= npat) continue;
     const uint64_t a = base + mine[j], c = kc[j];
-    op.out_offs[q] = a;
+    st_out(op.out_offs + q, a);
     if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
     const uint64_t s = kr[j];
     if ((s >> 62) == 1) {  // kLocStash: the one position, read by the search kernel
-      op.out_pos[a] = s & (kLocStash - 1);
+      st_out(op.out_pos + a, s & (kLocStash - 1));
     } else if (s & kLocCtx) {  // a window k characters before the end (k_locate_sa)
       uint64_t r0, adj;
       uint32_t rel;
@@ -1350,11 +1359,11 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
       for (uint64_t i = 0; i < c; ++i) {
         const uint32_t f = (uint32_t)__ffs(rel) - 1u;
         const uint64_t p = onepass_pos<kPos>(ix, T, op, r0 + f);
-        op.out_pos[a + i] = p >= adj ? p - adj : p + n - adj;
+        st_out(op.out_pos + a + i, p >= adj ? p - adj : p + n - adj);
         rel &= rel - 1u;
       }
     } else if (c <= kLocSmall) {
-      for (uint64_t i = 0; i < c; ++i) op.out_pos[a + i] = onepass_pos<kPos>(ix, T, op, s + i);
+      for (uint64_t i = 0; i < c; ++i) st_out(op.out_pos + a + i, onepass_pos<kPos>(ix, T, op, s + i));
     } else {
       const unsigned long long e = atomicAdd(op.nwide, 1ull);
       if (e < op.wide_cap) {
