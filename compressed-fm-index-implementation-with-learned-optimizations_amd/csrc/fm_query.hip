@@ -1387,7 +1387,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(DevIndex ix, OnePass 
   }
   for (uint64_t e = blockIdx.x; e < nw; e += gridDim.x) {
     const uint64_t q = op.wide[2 * e], s = op.wide[2 * e + 1], a = offs[q], c = offs[q + 1] - a;
-    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) out[a + j] = onepass_pos<kPos>(ix, T, op, s + j);
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) st_out(out + a + j, onepass_pos<kPos>(ix, T, op, s + j));
   }
 }
 
@@ -2573,7 +2573,7 @@ __global__ __launch_bounds__(kBlk) void k_walk(DevIndex ix, const uint64_t* __re
     } else if (phase == kSample) {
       uint64_t s = smp + steps;  // :147-153
       s = s >= n ? s - n : s;
-      out[j] = steps_only ? steps : s >= adj ? s - adj : s + n - adj;
+      st_out(out + j, steps_only ? steps : s >= adj ? s - adj : s + n - adj);
       phase = kFetch;
     } else if (phase == kWalk) {
       // loop condition of fm_index.cpp:130: stop at a sampled row or after n steps
@@ -2680,7 +2680,7 @@ __device__ __forceinline__ void walk_short_one(const DevIndex& ix, const NodeTab
       const uint64_t sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
       uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps;  // :147-153
       s = s >= n ? s - n : s;
-      out[j] = steps_only ? steps : s >= adj ? s - adj : s + n - adj;
+      st_out(out + j, steps_only ? steps : s >= adj ? s - adj : s + n - adj);
       return;
     }
     pos = walk_lf<W, kQ>(ix, T, v, q, o, pos);
@@ -2899,7 +2899,7 @@ __global__ __launch_bounds__(kBlk) void k_walk_lines(DevIndex ix, const uint64_t
     } else if (phase == kSample) {
       uint64_t s = smp + steps;  // :147-153
       s = s >= n ? s - n : s;
-      out[j] = steps_only ? steps : s >= adj ? s - adj : s + n - adj;
+      st_out(out + j, steps_only ? steps : s >= adj ? s - adj : s + n - adj);
       if (jn < end) {
         j = jn;
         pos = row & kWalkRowMask;
@@ -3932,11 +3932,11 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa(const uint32_t* __restrict__
       for (uint64_t j = 0; j < c; ++j) {
         const uint32_t f = (uint32_t)__ffs(rel) - 1u;
         const uint64_t p = sa[r0 + f];
-        out[a + j] = p >= adj ? p - adj : p + n - adj;
+        st_out(out + a + j, p >= adj ? p - adj : p + n - adj);
         rel &= rel - 1u;
       }
     } else if (c <= kLocSmall) {
-      for (uint64_t j = 0; j < c; ++j) out[a + j] = sa[s + j];
+      for (uint64_t j = 0; j < c; ++j) st_out(out + a + j, (uint64_t)sa[s + j]);
     } else {
       wide[atomicAdd(nwide, 1ull)] = q;
     }
@@ -3952,7 +3952,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa_wide(const uint32_t* __restr
   const uint64_t nw = *nwide;
   for (uint64_t e = blockIdx.x; e < nw; e += gridDim.x) {
     const uint64_t q = wide[e], a = offs[q], c = offs[q + 1] - a, s = sp[q];
-    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) out[a + j] = sa[s + j];
+    for (uint64_t j = threadIdx.x; j < c; j += blockDim.x) st_out(out + a + j, (uint64_t)sa[s + j]);
   }
 }
 
