@@ -1231,9 +1231,11 @@ __device__ __forceinline__ void block_scan(const uint64_t* kc, uint64_t* mine, u
 // kLocStash | position.  (C4 Q_text: 99.6 % of the patterns.)
 constexpr uint64_t kLocStash = 1ull << 62;  // with bit 63 clear: not a window, not a row
 template <int U, int kPos = 0>
+// skip: bit j set = the lane's j-th pattern is k_locate_long's (routing): its count and record
+// are left for that kernel to write (it adds its count to the tile)
 __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const NodeTable& T, uint64_t npat,
                                                    uint64_t tile, uint64_t q0, const uint64_t* kc,
-                                                   const uint64_t* kr, const OnePass& op) {
+                                                   const uint64_t* kr, const OnePass& op, uint32_t skip = 0) {
   const uint64_t n = ix.n;
   uint64_t mine[U], agg, rs[U];
   block_scan<U>(kc, mine, agg);
@@ -1266,7 +1268,7 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if (q >= npat) continue;
+    if (q >= npat || ((skip >> j) & 1u)) continue;
     if (op.cnt64) op.cnt64[q] = kc[j];
     else op.cnt[q] = (uint32_t)kc[j];
     op.rec[q] = rs[j];
@@ -1655,7 +1657,12 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       if (general)
         general_rest<E, U, kLoc, kPacked, W, true>(ix, T, pats, st, o0, m, q0, co, limit, rec, kc, kr);
     }
-    locate_split_store<U, kPos>(ix, T, npat, blockIdx.x, q0, kc, kr, op);
+    uint32_t skip = 0;  // kSkipLong: the patterns left to k_locate_long
+    if constexpr (kSkipLong) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) skip |= (uint32_t)(st[j] == 4) << j;
+    }
+    locate_split_store<U, kPos>(ix, T, npat, blockIdx.x, q0, kc, kr, op, skip);
     return;
   }
   if (!__syncthreads_or(general)) return;
