@@ -45,7 +45,7 @@ for STEP in "$@"; do
   ENVS=()
   ARGS=()
   for x in "${W[@]:1}"; do
-    if [[ $x =~ ^[A-Z_]+=.* ]]; then ENVS+=("$x"); else ARGS+=("$x"); fi
+    if [[ $x =~ ^[A-Z_][A-Z0-9_]*=.* ]]; then ENVS+=("$x"); else ARGS+=("$x"); fi
   done
   NAME="${TAG}_${n}_${KIND}"
   echo "[gpu_session] step $n: $STEP" >&2
