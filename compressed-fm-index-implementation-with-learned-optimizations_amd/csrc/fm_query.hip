@@ -1393,6 +1393,15 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(DevIndex ix, OnePass 
   }
 }
 
+// A 16-B context record: a random read nothing re-reads, through a non-temporal load so it
+// does not displace the pattern stream's lines in the caches (C4 headline 0.394 -> 0.382 ms,
+// four rounds of an A/B in fresh processes on one box: profiles/r03/ab_nt_record_load.jsonl)
+__device__ __forceinline__ uint4 load_record16(const void* tab, uint64_t t) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 r = __builtin_nontemporal_load(static_cast<const u32x4*>(tab) + t);
+  return make_uint4(r.x, r.y, r.z, r.w);
+}
+
 // The count forms (two patterns per lane) are held to 6 waves per SIMD (<= 80 VGPRs, no
 // spills): left alone the compiler gives the packed and uint8 forms 95-104 VGPRs (4-5
 // waves), and the packed count took 0.392 ms per 12.5 M instead of 0.361.
@@ -1529,7 +1538,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       w[j][1] = make_uint4(b.z, b.w, 0u, 0u);
       inl[j] = ep[j] - sp[j] <= kRecCtx;
     } else if (ix.ptab_rec == 2) {
-      const uint4 a = static_cast<const uint4*>(ix.ptab)[t[j]];
+      const uint4 a = load_record16(ix.ptab, t[j]);
       const uint32_t wc = a.y & 15u;
       sp[j] = rec16_sp(a.x, a.w, ix.wide);
       inl[j] = wc != kRec16Wide && k[j] <= (ix.wide ? kRec16QW : kRec16Q);
@@ -1939,7 +1948,7 @@ __device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __
   uint32_t d[6] = {0, 0, 0, 0, 0, 0};  // inline contexts as u16 entries, row i in entry i
   if constexpr (kBytes) by += ix.ptab_rec == 1 ? 32u : ix.ptab_rec == 2 ? 16u : 8u;
   if (ix.ptab_rec == 2) {
-    const uint4 a = static_cast<const uint4*>(ix.ptab)[t];
+    const uint4 a = load_record16(ix.ptab, t);
     const uint32_t wc = a.y & 15u;
     sp = a.x;
     ep = sp + (wc == kRec16Wide ? a.z : wc);
@@ -2309,7 +2318,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void 
     c0[j] = c1[j] = 0;
     if (st[j] != 1 && st[j] != 2) continue;
     if (ix.ptab_rec == 3) {
-      const uint4 a = static_cast<const uint4*>(ix.ptab)[t[j]];
+      const uint4 a = load_record16(ix.ptab, t[j]);
       sp[j] = a.x;
       ep[j] = (uint64_t)a.x + a.y;
       c0[j] = a.z;

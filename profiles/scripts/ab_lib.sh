@@ -11,7 +11,7 @@ TAG=$1
 shift
 OUT=$ROOT/gpurun_out/ab_lib_$TAG.jsonl
 : > "$OUT"
-for round in 1 2; do
+for round in $(seq 1 ${AB_ROUNDS:-2}); do
   for V in "$@"; do
     cp "$PKG/libcs_fmindex_$V.so" "$PKG/libcs_fmindex.so"
     echo "[ab_lib] round $round $V" >&2
