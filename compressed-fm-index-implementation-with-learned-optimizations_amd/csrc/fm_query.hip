@@ -597,6 +597,13 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
   return count_rest<E, PT, kLA>(ix, T, P, k, sp, ep, bytes, inl);
 }
 
+// One suffix-array entry: a random read nothing re-reads, non-temporal as the records are
+// (C4 one-call locate 0.835 -> 0.815 ms, 64-mer count 1.268 -> 1.256 ms, three A/B rounds:
+// profiles/r03/ab_nt_sa_load.jsonl)
+__device__ __forceinline__ uint32_t load_sa(const uint32_t* sa, uint64_t r) {
+  return __builtin_nontemporal_load(sa + r);
+}
+
 // Verification against the text (lf_exact indexes that keep the full suffix array and the
 // text in HBM: DevIndex::vsa / vtext).  Row r of [sp, ep) survives the k remaining steps
 // iff its chain spells P[k-1], ..., P[0]; LF^t(r) is the row of the rotation SA[r] - t, so
@@ -765,7 +772,7 @@ __device__ __forceinline__ uint64_t verify_rows(const DevIndex& ix, PT P, uint64
   while (mm) {
     const uint32_t i = (uint32_t)__ffs(mm) - 1u;
     mm &= mm - 1;
-    const uint64_t p = ix.vsa[base + i];
+    const uint64_t p = load_sa(ix.vsa, base + i);
     if (bytes) *bytes += 32;
     cnt += window_eq<PT, kLA>(ix, P, p >= k ? p - k : p + n - k, k - qf, bytes) ? 1u : 0u;
   }
@@ -864,7 +871,7 @@ __device__ __forceinline__ uint32_t verify_mask(const DevIndex& ix, PT P, uint64
   while (mm) {
     const uint32_t i = (uint32_t)__ffs(mm) - 1u;
     mm &= mm - 1;
-    const uint64_t p = ix.vsa[base + i];
+    const uint64_t p = load_sa(ix.vsa, base + i);
     if (window_eq(ix, P, p >= k ? p - k : p + n - k, k - qf, nullptr)) out |= 1u << i;
   }
   return out;
@@ -1187,7 +1194,7 @@ __device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTab
 template <int kPos>
 __device__ __forceinline__ uint64_t onepass_pos(const DevIndex& ix, const NodeTable& T, const OnePass& op,
                                                 uint64_t row) {
-  if constexpr (kPos == 0) return op.sa[row];
+  if constexpr (kPos == 0) return load_sa(op.sa, row);
   else if constexpr (kPos == 1) return walk_position<WalkLine>(ix, T, row);
   else return walk_position<WalkLineW>(ix, T, row);
 }
@@ -1255,7 +1262,7 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
   if constexpr (kPos == 0) {
 #pragma unroll
     for (int j = 0; j < U; ++j)
-      if (one[j]) row[j] = op.sa[row[j]];
+      if (one[j]) row[j] = load_sa(op.sa, row[j]);
   } else {  // the lane's walks in lockstep: row[j] becomes the position
     bool act[U];
 #pragma unroll
@@ -2065,7 +2072,7 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
     while (cand) {
       const uint32_t i = (uint32_t)__ffs(cand) - 1u;
       cand &= cand - 1;
-      const uint64_t p = ix.vsa[base + i];
+      const uint64_t p = load_sa(ix.vsa, base + i);
       const uint64_t wq = p >= k ? p - k : p + n - k;
       if constexpr (kBytes) {  // the SA sector, then the window's words
         constexpr uint64_t C = 32ull * kLongPW;
@@ -2134,7 +2141,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_long(DevIndex ix, const uint8_t
       uint64_t p0 = 0;  // the first matching row's position
       for (uint32_t c = cand; c; c &= c - 1) {
         const uint32_t i = (uint32_t)__ffs(c) - 1u;
-        const uint64_t p = ix.vsa[base + i];
+        const uint64_t p = load_sa(ix.vsa, base + i);
         const uint64_t wq = p >= k ? p - k : p + n - k;
         if (window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare)) {
           if (!mm) p0 = wq;
@@ -3947,7 +3954,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa(const uint32_t* __restrict__
       loc_window(s, r0, adj, rel);
       for (uint64_t j = 0; j < c; ++j) {
         const uint32_t f = (uint32_t)__ffs(rel) - 1u;
-        const uint64_t p = sa[r0 + f];
+        const uint64_t p = load_sa(sa, r0 + f);
         st_out(out + a + j, p >= adj ? p - adj : p + n - adj);
         rel &= rel - 1u;
       }
