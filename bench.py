@@ -13,7 +13,12 @@ scaling: --batch per GPU); every step's counts are gathered to rank 0 over RCCL
 step k overlapped with the count of step k+1; the timed region closes after the
 last gather.
 
-Extra fields on the JSON line:
+Output: ONE compact JSON line on stdout (<= 4 KB, compact_line(): the contract's fields, the
+count kernel's roofline, cpu_baseline, p50 and a locate summary), and the full result below
+— every leg — in the --legs-out file (default gpurun_out/bench_full_n<N>_<time>.json) and on
+stderr.
+
+Fields of the full result:
   roofline     the count kernel against HBM: achieved = algorithmic bytes per
                launch / mean kernel time (HIP events on the launch stream).
                Algorithmic bytes = the random reads the search needs (prefix-table
@@ -136,6 +141,85 @@ class LegGuard:
 def log(rank, *a):
     if rank == 0:
         print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+# the stdout line must survive a reader that keeps only the last few KB of the run's output
+# (round 3's 46-KB line with every leg inside was cut to its tail): the headline fields below,
+# the full result (every leg) in the --legs-out file and on stderr
+LINE_MAX = 4096
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "alg_bytes_per_launch",
+              "kernel_ms_mean", "frac_of_random_access_ceiling")
+_CPU_KEYS = ("value", "unit", "cores", "kind", "cores_used", "host_cores", "matches_gpu", "p50_us")
+_CFG_KEYS = ("workload", "batch_per_gpu", "global_batch", "m", "ssa_stride", "parallelism", "index")
+
+
+def _sig(x, d=4):
+    """Round floats to d significant digits (the line's numbers, not its precision claims)."""
+    if isinstance(x, float):
+        return float("%.*g" % (d, x))
+    if isinstance(x, dict):
+        return {k: _sig(v, d) for k, v in x.items()}
+    if isinstance(x, list):
+        return [_sig(v, d) for v in x]
+    return x
+
+
+def compact_line(res, legs_file=None):
+    """The one stdout JSON line: the headline of `res` (bench.py's full result) in at most
+    LINE_MAX bytes.  Kept: the contract's fields, the count kernel's roofline, the CPU
+    baseline, p50 and a two-number locate summary; the legs stay in the full result.  Fields
+    are dropped from the end of an optional list until the line fits."""
+    if "only" in res:  # profiling passes (--only): the leg object is the whole point
+        return json.dumps(res)
+    out = {k: res[k] for k in ("metric", "value", "unit", "n_gpus", "ranks_seen", "steps", "warmup",
+                               "ms_per_step", "higher_is_better", "scaling", "vs_baseline", "dtype",
+                               "data") if k in res}
+    if "value" in out:
+        out["value"] = float("%.6g" % out["value"])
+    if "config" in res:
+        out["config"] = {k: res["config"][k] for k in _CFG_KEYS if k in res["config"]}
+    rf = res.get("roofline")
+    if rf:
+        out["roofline"] = _sig({k: rf.get(k) for k in _ROOF_KEYS})
+    cb = res.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = _sig({k: cb.get(k) for k in _CPU_KEYS if k in cb})
+        out["cpu_baseline"]["sample"] = str(cb.get("sample", ""))[:160]
+    for k in ("p50_us", "p50_launch_us"):
+        if k in res:
+            out[k] = _sig(res[k])
+    loc = res.get("locate")
+    if loc:
+        rl = loc.get("roofline") or loc.get("walk_roofline") or {}
+        out["locate"] = _sig({"patterns_per_s": loc.get("patterns_per_s"), "frac": rl.get("frac")})
+    opt = []  # optional, dropped last-first while the line is too long
+    if "gather_verified" in res:
+        out["gather_verified"] = res["gather_verified"]
+    if res.get("leg_errors"):
+        out["leg_errors"] = sorted(res["leg_errors"])[:8]
+        opt.append("leg_errors")
+    if legs_file:
+        out["legs_file"] = legs_file
+        opt.append("legs_file")
+    if "found_frac" in res:
+        out["found_frac"] = _sig(res["found_frac"])
+        opt.append("found_frac")
+    if res.get("config", {}).get("engine"):
+        out["config"]["engine"] = res["config"]["engine"]
+        opt.append(("config", "engine"))
+    line = json.dumps(out)
+    while len(line.encode()) > LINE_MAX and opt:
+        k = opt.pop()
+        if isinstance(k, tuple):
+            out[k[0]].pop(k[1], None)
+        else:
+            out.pop(k, None)
+        line = json.dumps(out)
+    if len(line.encode()) > LINE_MAX:  # never expected: the kept fields are bounded
+        out.pop("cpu_baseline", None)
+        out["config"] = {"workload": str(out.get("config", {}).get("workload", ""))[:200]}
+        line = json.dumps(out)
+    return line
 
 
 def pmc_traffic(wl, leg, kern_s):
@@ -653,6 +737,10 @@ def main():
     ap.add_argument("--legs", default="all",
                     help="comma-separated legs of a full N=1 run (%s), 'all' or 'none'"
                          % ",".join(ALL_LEGS))
+    ap.add_argument("--legs-out", default=None,
+                    help="file for the full result with every leg (default gpurun_out/"
+                         "bench_full_n<N>_<time>.json; 'none' = stderr only); stdout gets the "
+                         "compact headline line (<= 4 KB)")
     ap.add_argument("--only", default=None,
                     help="run only this leg ('count' = the headline) and print its object "
                          "(profiling passes)")
@@ -1476,7 +1564,22 @@ def main():
             if "locate_one" in lg or "locate" in lg:
                 res["locate"] = lg.get("locate_one") or lg["locate"]
             res["legs"] = lg
-        print(json.dumps(res), flush=True)
+        legs_file = None
+        if args.legs_out != "none" and not args.only:
+            legs_file = args.legs_out or os.path.join(
+                "gpurun_out", "bench_full_n%d_%s.json" % (world, time.strftime("%Y%m%d_%H%M%S")))
+            try:
+                path = legs_file if os.path.isabs(legs_file) else os.path.join(ROOT, legs_file)
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "w") as f:
+                    json.dump(res, f)
+            except OSError as e:
+                log(rank, "could not write %s: %s" % (legs_file, e))
+                legs_file = None
+        if not args.only:
+            # the full result (every leg) on stderr as well, one line
+            print("[bench] full result: " + json.dumps(res), file=sys.stderr, flush=True)
+        print(compact_line(res, legs_file), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -9,7 +9,8 @@
 #   "tests [pytest -k expr]"       the -m gpu suite (or the tests matching expr)
 #   "smoke"                        __graft_entry__.smoke()
 #   "bench <cfg> [VAR=val ...] [bench.py args ...]"
-#                                  one bench.py line; <cfg> picks the BASELINE config:
+#                                  one bench.py line (<name>.json; every leg in <name>.full.json);
+#                                  <cfg> picks the BASELINE config:
 #                                  c2 (100 MB DNA, 1 M 20-mers), c3 (1 GB bytes, 10 M 8-mers),
 #                                  c4 (the default), c5 (32 GB DNA); VAR=val set the engine's
 #                                  environment switches (CS_FM_ENGINE=wavelet, CS_FM_COUNT_U=1, ...)
@@ -60,7 +61,7 @@ for STEP in "$@"; do
     bench)
       C=$(cfg_args "${ARGS[0]}") || exit 1
       NAME="${NAME}_${ARGS[0]}"
-      env "${ENVS[@]}" timeout -k 10 600 python -u bench.py $C "${ARGS[@]:1}" > $OUT/$NAME.json 2> $OUT/$NAME.err ;;
+      env "${ENVS[@]}" timeout -k 10 600 python -u bench.py $C --legs-out $OUT/$NAME.full.json "${ARGS[@]:1}" > $OUT/$NAME.json 2> $OUT/$NAME.err ;;
     prof)
       C=$(cfg_args "${ARGS[0]}") || exit 1
       env "${ENVS[@]}" timeout -k 10 900 bash profiles/profile_legs.sh "${TAG}_${ARGS[0]}" "${ARGS[1]}" $C \
