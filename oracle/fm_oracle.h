@@ -108,6 +108,18 @@ int orc_locate_batch(const orc_index* idx, const uint8_t* pats, const uint64_t* 
                      uint64_t npat, uint64_t limit, uint64_t* out_offs, uint64_t* out_pos,
                      uint64_t cap, int nthreads, int faithful);
 
+/* --- Index-free full-size checks --- */
+/* SSA samples of an index built elsewhere, for locate() over a BWT-only index */
+void orc_attach_ssa(orc_index* idx, const uint64_t* samples, uint64_t nsamples, uint32_t stride);
+/* count() of npat patterns of length m (pats: npat*m bytes) by scanning the text: the
+ * occurrences of each pattern in text[0..n) (= count() with a unique smallest terminator,
+ * SURVEY.md §0.4); for the first nloc patterns also their positions ascending (CSR:
+ * loc_offs[nloc+1] into loc_pos[cap]).  ORC_ERR_CAPACITY when cap is too small (loc_offs
+ * then holds the sizes).  nthreads threads on disjoint ranges of the text. */
+int orc_scan_count(const uint8_t* text, uint64_t n, const uint8_t* pats, uint64_t m,
+                   uint64_t npat, uint64_t* counts, uint64_t nloc, uint64_t* loc_offs,
+                   uint64_t* loc_pos, uint64_t cap, int nthreads);
+
 /* --- Synthetic inputs --- */
 uint64_t orc_splitmix64(uint64_t* state);
 /* DNA: 32 bases per draw, 2 bits each LSB-first -> "ACGT", then '$'.  Writes len+1 bytes. */

@@ -81,6 +81,9 @@ def lib():
         "orc_count_batch": (None, [_vp, _u8p, _u64p, C.c_uint64, _u64p, C.c_int, C.c_int, _u64p]),
         "orc_locate_batch": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, C.c_uint64, _u64p, _u64p,
                                        C.c_uint64, C.c_int, C.c_int]),
+        "orc_attach_ssa": (None, [_vp, _u64p, C.c_uint64, C.c_uint32]),
+        "orc_scan_count": (C.c_int, [_u8p, C.c_uint64, _u8p, C.c_uint64, C.c_uint64, _u64p,
+                                     C.c_uint64, _u64p, _u64p, C.c_uint64, C.c_int]),
         "orc_gen_dna": (None, [C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_bytes": (None, [C.c_uint64, C.c_uint64, _u8p]),
         "orc_gen_rdna": (None, [C.c_uint64, C.c_uint64, _u8p]),
@@ -278,6 +281,13 @@ class Index:
             raise RuntimeError("oracle locate status %d" % st)
         return [int(v) for v in out[: nout.value]]
 
+    def attach_ssa(self, samples, stride):
+        """The row-sampled SSA of an index built elsewhere (for a BWT-only index: locate
+        then walks LF over this BWT, fm_index.cpp:125-153, with these samples)."""
+        s = np.ascontiguousarray(samples, np.uint64)
+        lib().orc_attach_ssa(self._h, _u64(s) if len(s) else _u64(np.zeros(1, np.uint64)), len(s),
+                             stride)
+
     def extract(self, pos, length):
         cap = max(1, min(length, self.n))
         out = np.zeros(cap, np.uint8)
@@ -325,6 +335,35 @@ class Index:
 
 
 # ---------------------------------------------------------------------------
+def scan_count(text, pats, nloc=0, nthreads=8):
+    """count() of every row of `pats` (npat x m bytes, one length) by scanning the text for
+    its occurrences (orc_scan_count) — no index, so a full-size GPU index is checked against
+    the text alone; equal to count() when the text ends in a unique smallest terminator
+    (SURVEY.md §0.4).  nloc > 0: also the positions of the first nloc patterns, ascending
+    (locate()'s positions in text order) -> (counts, offs[nloc+1], pos)."""
+    t = as_u8(text)
+    P = np.ascontiguousarray(pats, np.uint8)
+    npat, m = P.shape
+    counts = np.zeros(max(npat, 1), np.uint64)
+    buf = P.reshape(-1) if P.size else np.zeros(1, np.uint8)
+    tt = t if len(t) else np.zeros(1, np.uint8)
+    if not nloc:
+        st = lib().orc_scan_count(_u8(tt), len(t), _u8(buf), m, npat, _u64(counts), 0, None, None,
+                                  0, nthreads)
+        assert st == ORC_OK, st
+        return counts[:npat]
+    offs = np.zeros(nloc + 1, np.uint64)
+    cap = 4 * nloc + 4096
+    for _ in range(2):
+        pos = np.zeros(cap, np.uint64)
+        st = lib().orc_scan_count(_u8(tt), len(t), _u8(buf), m, npat, _u64(counts), nloc, _u64(offs),
+                                  _u64(pos), cap, nthreads)
+        if st == ORC_OK:
+            return counts[:npat], offs, pos[: int(offs[-1])]
+        cap = int(offs[-1])
+    raise RuntimeError("orc_scan_count status %d" % st)
+
+
 def check_suffix_array(text, sa, nthreads=8):
     """True iff `sa` is the suffix array of `text` in the reference's order (plain
     suffix order, a proper prefix first: src/core/sais.hpp:8-16): a permutation of

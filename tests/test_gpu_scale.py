@@ -1,21 +1,23 @@
-"""Full-size GPU checks (BASELINE.json configs C2-C5) through size-independent
-properties — no CPU index is built at these sizes:
+"""Full-size GPU checks (BASELINE.json configs C2-C5).
 
-  * every Q_text pattern (a substring sampled at a known position) is found;
-  * every located position p satisfies text[p:p+m] == pattern, positions are
-    distinct, the sampled position is among them, and each list has
-    min(count, limit) entries;
-  * checksum of checksums: sum of count() over ALL k-mers of the alphabet equals
-    the number of k-windows of the text that avoid the terminator, and the sum of
-    count() over all 256 single bytes equals n.
-and, exactly, against the oracle (oracle/fm_oracle.c):
-
-  * C2 (100 MB): the oracle is built from the text and the device builder's suffix
-    array, after orc_check_sa has proven that array to be the text's suffix array (a
-    permutation with increasing consecutive suffixes) — so no O(n log n) CPU sort —
-    and 200 k Q_text counts and 100 k locates (limit 100) equal its answers;
-  * C4 (4 GB): 1 M Q_text counts equal the oracle's count over the GPU's BWT (the
-    same check as bench.py's cpu_fast), for every C4 index variant.
+Exact, and independent of anything the GPU built:
+  * C3, C4, C5: count() of 100 k-1 M Q_text and 100 k Q_unif patterns equals the number of
+    occurrences of each pattern in the text, found by scanning the text itself
+    (oracle.scan_count, orc_scan_count: a rolling hash over every window, confirmed by
+    memcmp; valid because every synthetic text ends in a unique smallest terminator,
+    SURVEY.md §0.4, fm_index.cpp:79-101) — no suffix array, BWT or index of ours involved;
+  * the located positions of 20-100 k patterns, sorted, are exactly the scan's positions
+    (all of them when count <= limit, else a subset of limit distinct ones);
+  * C4: 100 k locates in the reference's ROW order (fm_index.cpp:125-153) equal the
+    oracle's locate over the GPU's BWT with the GPU's row-sampled SSA (the LF walk of the
+    reference restated, oracle/fm_oracle.c orc_locate) — the order is the one thing the scan
+    cannot pin; the scan pins the BWT's answers;
+  * C2 (100 MB): the oracle is built from the text and the device builder's suffix array
+    after orc_check_sa has proven it the text's suffix array, and 200 k counts and 100 k
+    locates (limit 100) equal its answers, in row order.
+Properties on top: every Q_text pattern is found and its sampled position located;
+positions are distinct and spell their pattern; the sum of count() over all k-mers equals the
+number of text windows, over all single bytes n.
 Bit-exact parity at sizes the oracle sorts in seconds is in test_gpu_parity.py.
 """
 import itertools
@@ -32,8 +34,8 @@ pytestmark = pytest.mark.gpu
 
 # host threads of the checker: the process's CPU share (16 per GPU on the box)
 THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
-# C4's oracle counts, shared by the C4 variants (same text, same batch)
-_C4_ORACLE = {}
+# C4's scan results, shared by the C4 variants (same text, same batches)
+_C4_SCAN = {}
 
 
 def _build(pkg, kind, L):
@@ -54,6 +56,41 @@ def _qtext(pkg, text, N, m, npat):
                               torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     return pats.cpu().numpy().reshape(npat, m)
+
+
+def _qunif(pkg, kind, m, npat, dev):
+    pats = torch.empty(npat * m, dtype=torch.uint8, device=dev)
+    pkg.synth_random_patterns_device(kind, m, 0, npat, 4242, pats.data_ptr(), None,
+                                     torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return pats.cpu().numpy().reshape(npat, m)
+
+
+def _flat(P):
+    npat, m = P.shape
+    return np.ascontiguousarray(P).reshape(-1), np.arange(0, (npat + 1) * m, m, dtype=np.uint64)
+
+
+def _scan_exact(idx, host, P, nloc, limit=1000, scan=None):
+    """count() of every row of P and the positions of the first nloc against the text scan;
+    -> (counts, scan result) (`scan` reuses a result for the same text and batch)."""
+    buf, offs = _flat(P)
+    cnt = idx.count_batch(buf=buf, offs=offs)
+    if scan is None:
+        scan = O.scan_count(host, P, nloc=nloc, nthreads=THREADS)
+    scnt, soffs, spos = scan
+    bad = np.flatnonzero(cnt != scnt)
+    assert bad.size == 0, ("count != text scan", bad[:5], cnt[bad[:5]], scnt[bad[:5]])
+    goffs, gpos = idx.locate_batch(buf=buf[: nloc * P.shape[1]], offs=offs[: nloc + 1], limit=limit)
+    assert np.array_equal(np.diff(goffs), np.minimum(scnt[:nloc], limit))
+    for q in range(nloc):
+        g = np.sort(gpos[goffs[q]:goffs[q + 1]])
+        w = spos[soffs[q]:soffs[q + 1]]
+        if scnt[q] <= limit:
+            assert np.array_equal(g, w), q
+        else:
+            assert len(np.unique(g)) == len(g) and np.isin(g, w).all(), q
+    return cnt, scan
 
 
 def _sampled_positions(N, m, npat, seed=4242):
@@ -114,20 +151,24 @@ def test_c4_dna_4gb(variant, monkeypatch):
     assert info.record_bytes == (0 if variant == "plain_walk" else 16)
     assert info.prefix_bytes == max(info.record_bytes, 8) * info.prefix_sigma ** info.prefix_k
     P = _qtext(pkg, text, N, 20, 1_000_000)
-    cnt = _check_qtext(idx, host, N, P, nloc=20_000)
-    # exact: 1 M counts against the oracle's count over the GPU's BWT (computed once for
-    # the three variants; the BWT is the text's, whatever the index keeps)
-    if "counts" not in _C4_ORACLE:
+    _check_qtext(idx, host, N, P, nloc=20_000)
+    # exact against the text itself: 1 M Q_text counts, 100 k located (sets), 100 k Q_unif
+    _, _C4_SCAN["text"] = _scan_exact(idx, host, P, 100_000, scan=_C4_SCAN.get("text"))
+    U = _qunif(pkg, "dna", 20, 100_000, text.device)
+    _, _C4_SCAN["unif"] = _scan_exact(idx, host, U, 1_000, scan=_C4_SCAN.get("unif"))
+    if variant == "auto":
+        # row order: the reference's LF walk over the GPU's BWT with the GPU's SSA samples
         d_bwt = torch.empty(N, dtype=torch.uint8, device=text.device)
         idx.bwt_device(d_bwt.data_ptr())
         torch.cuda.synchronize()
         ref = O.Index(bwt=d_bwt.cpu().numpy(), nthreads=THREADS)
         del d_bwt
-        buf = np.ascontiguousarray(P).reshape(-1)
-        _C4_ORACLE["counts"] = ref.count_batch(buf=buf, offs=np.arange(0, (len(P) + 1) * 20, 20, dtype=np.uint64),
-                                               nthreads=THREADS)
+        ref.attach_ssa(idx.ssa(), idx.info().ssa_stride)
+        buf, offs = _flat(P[:100_000])
+        woffs, wpos = ref.locate_batch(buf=buf, offs=offs, limit=1000, nthreads=THREADS)
         del ref
-    assert np.array_equal(cnt, _C4_ORACLE["counts"]), variant
+        goffs, gpos = idx.locate_batch(buf=buf, offs=offs, limit=1000)
+        assert np.array_equal(goffs, woffs) and np.array_equal(gpos, wpos)
     ones = idx.count_batch([bytes([c]) for c in range(256)])
     assert int(ones.sum()) == N and ones[ord("$")] == 1
     _kmer_checksum(idx, b"ACGT", 9, N)
@@ -151,6 +192,9 @@ def test_c5_dna_32gb_wide(engine, monkeypatch):
         assert info.engine == 1 and info.rare_rows == 1
     P = _qtext(pkg, text, N, 20, 200_000)
     _check_qtext(idx, host, N, P, nloc=20_000)
+    # exact against the text itself (no reference oracle exists at n >= 2^32)
+    _scan_exact(idx, host, P[:100_000], 20_000)
+    _scan_exact(idx, host, _qunif(pkg, "dna", 20, 100_000, text.device), 1_000)
     ones = idx.count_batch([bytes([c]) for c in range(256)])
     assert int(ones.sum()) == N and ones[ord("$")] == 1
     _kmer_checksum(idx, b"ACGT", 9, N)
@@ -163,6 +207,8 @@ def test_c3_bytes_1gb():
     idx, text, host, N = _build(pkg, "bytes", 999_999_999)
     P = _qtext(pkg, text, N, 8, 100_000)
     _check_qtext(idx, host, N, P, nloc=20_000)
+    _scan_exact(idx, host, P, 20_000)
+    _scan_exact(idx, host, _qunif(pkg, "bytes", 8, 100_000, text.device), 1_000)
     ones = idx.count_batch([bytes([c]) for c in range(256)])
     assert int(ones.sum()) == N and ones[0] == 1
     _kmer_checksum(idx, bytes(range(1, 256)), 2, N)

@@ -168,3 +168,48 @@ def test_check_suffix_array_rejects():
         big = sa.copy()
         big[0] = len(t)
         assert not O.check_suffix_array(t, big)
+
+
+@pytest.mark.parametrize("fname", ["fm_100k.json", "fm_1m.json"])
+def test_scan_count_matches_reference(fname):
+    """The index-free scan (orc_scan_count, the full-size checker of test_gpu_scale.py)
+    against the genuine reference's counts and positions (row order sorted = text order):
+    every fixture case with a unique smallest terminator, grouped by pattern length."""
+    for case in load_golden(fname)["cases"]:
+        text = golden_text(case["text"])
+        t = np.frombuffer(text, np.uint8)
+        if not (t[-1] < t[:-1]).all():
+            continue  # the scan equals count() only with a unique smallest terminator
+        pats = [bytes.fromhex(h) for h in case["patterns_hex"]]
+        for m in sorted(set(len(p) for p in pats)):
+            sel = [q for q, p in enumerate(pats) if len(p) == m and p]
+            P = np.frombuffer(b"".join(pats[q] for q in sel), np.uint8).reshape(len(sel), m)
+            cnt, offs, pos = O.scan_count(t, P, nloc=len(sel), nthreads=4)
+            assert cnt.tolist() == [case["count"][q] for q in sel], (fname, m)
+            for k, q in enumerate(sel):
+                want = sorted(case["locate"][q]["pos"]) if case["count"][q] <= case["limit"] else None
+                if want is not None:
+                    assert pos[offs[k]:offs[k + 1]].tolist() == want, (fname, m, q)
+
+
+def test_scan_count_edge_cases():
+    t = np.frombuffer(b"abababab$", np.uint8)
+    P = np.frombuffer(b"abaab$ba", np.uint8).reshape(4, 2)  # ab, aa, b$, ba
+    cnt, offs, pos = O.scan_count(t, P, nloc=4, nthreads=3)
+    assert cnt.tolist() == [4, 0, 1, 3]
+    assert pos.tolist() == [0, 2, 4, 6, 7, 1, 3, 5] and offs.tolist() == [0, 4, 4, 5, 8]
+    # duplicates share one count; windows at both ends; more threads than windows
+    P = np.frombuffer(b"abb$abb$", np.uint8).reshape(4, 2)
+    assert O.scan_count(t, P, nthreads=16).tolist() == [4, 1, 4, 1]
+    assert O.scan_count(t, np.frombuffer(b"abababab$x", np.uint8).reshape(1, 10)).tolist() == [0]
+    # rdna: heavy repeats, the index and the scan agree on every Q_text 20-mer
+    r = O.gen_rdna(42, 300_000)
+    idx = O.Index(r)
+    Q = O.gen_patterns_text(r, 20, 3000, seed=4242)
+    assert np.array_equal(O.scan_count(r, Q, nthreads=8), idx.count_batch([bytes(p) for p in Q]))
+    # and on a σ = 256 text, 8-mers and 3-mers (many hits)
+    b = O.gen_bytes(7, 200_000)
+    ib = O.Index(b)
+    for m in (8, 3, 1):
+        Q = O.gen_patterns_text(b, m, 2000, seed=11)
+        assert np.array_equal(O.scan_count(b, Q, nthreads=8), ib.count_batch([bytes(p) for p in Q]))
