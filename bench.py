@@ -464,17 +464,35 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
         p, w = pos[a:a + ch], owner[a:a + ch]
         win = text[(p.unsqueeze(1) + torch.arange(m, device=dev)).long()]
         okv &= bool((win == W.pats.view(B, m)[w]).all().item())
+    # algorithmic bytes of the call, per pattern: a pattern the locate records answer
+    # (cs_fm_locate_record_hits_device) reads its 16-B locate record; any other the count's
+    # reads (record + context sectors, cs_fm_count_bytes_device) and one 32-B DRAM sector of
+    # SA per reported position (the DRAM's access granularity, as the count legs charge
+    # their lines) — plus the stream: patterns and offsets in, the search's u32 count and
+    # 8-B record per pattern out and back in, the offsets and positions out
+    cnt = torch.from_numpy(np.diff(oo).astype(np.int64)).to(dev)
     del owner, d_pos, d_oo
-    # algorithmic bytes of the one launch: the count's (record + contexts + pattern stream)
-    # + one 4-B SA read per position + the offsets and positions written
-    rnd, acc, _ = W.accounting(idx, info, 0, sh, dev)
-    alg = rnd + B * m + (B + 1) * 8 + tot * 4 + (B + 1) * 8 + tot * 8
-    reads = acc + tot
+    qb = torch.empty(B, dtype=torch.int64, device=dev)
+    idx.count_bytes_device(W.pats.data_ptr(), W.offs.data_ptr(), B, qb.data_ptr(), sh)
+    hit = torch.zeros(B, dtype=torch.uint8, device=dev)
+    if info.locate_record_bytes:
+        idx.locate_record_hits_device(W.pats.data_ptr(), W.offs.data_ptr(), B, hit.data_ptr(), sh)
+    hb = hit.bool()
+    nhit = int(hb.sum().item())
+    rnd = 16 * nhit + int(torch.where(hb, 0, qb + 32 * cnt).sum().item())
+    # random reads: one per 16-B record, one per 32-B sector or line, one SA sector per position
+    acc = nhit + int(torch.where(hb, 0, (qb + 31) // 32 + cnt).sum().item())
+    del qb, hit, hb, cnt
+    stream_b = B * m + (B + 1) * 8 + B * 12 * 2 + (B + 1) * 8 + tot * 8
+    alg = rnd + stream_b
+    reads = acc
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl, "limit": limit,
             "event_ms": min(evs) * 1e3, "positions_verified": okv,
+            "locate_record_hit_frac": nhit / B,
             "roofline": {"bound": "hbm", "achieved": alg / tl / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": alg / tl / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_query": alg / B,
+                         "alg_random_bytes_per_launch": rnd, "alg_stream_bytes_per_launch": stream_b,
                          "stream_read_bytes_per_launch": B * m + (B + 1) * 8,
                          **pmc_traffic(wl_key, name, min(evs)), "random_accesses_per_s": reads / tl,
                          "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}

@@ -28,6 +28,7 @@ CS_ERR_LF_OVERRUN, CS_ERR_SSA_RANGE, CS_ERR_CAPACITY, CS_ERR_UNSUPPORTED, CS_ERR
 
 # query flags (include/cs_fmindex.h CS_Q_*): results unchanged, structures left out
 Q_NO_PREFIX, Q_NO_CONTEXTS, Q_NO_FULL_SA, Q_NO_WALK_LINES, Q_NO_VERIFY, Q_LONG = 1, 2, 4, 8, 16, 32
+Q_NO_LOC_RECORDS = 64
 
 _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)
@@ -54,7 +55,7 @@ class cs_fm_info(C.Structure):
                 ("walk_bytes", C.c_uint64), ("context_q", C.c_uint32), ("position_stride", C.c_uint32),
                 ("context_bytes", C.c_uint64), ("full_sa_bytes", C.c_uint64),
                 ("record_bytes", C.c_uint32), ("text_in_hbm", C.c_uint32),
-                ("packed_text_bytes", C.c_uint64)]
+                ("packed_text_bytes", C.c_uint64), ("locate_record_bytes", C.c_uint64)]
 
 
 # Every entry point of include/cs_fmindex.h with its ctypes signature.
@@ -70,6 +71,7 @@ SIGNATURES = {
     "cs_fm_open_csidx": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "cs_fm_save_csidx": (C.c_int, [_vp, C.c_char_p]),
     "cs_csidx_check": (C.c_int, [C.c_char_p, _u64p, _u32p, C.POINTER(C.c_int)]),
+    "cs_csidx_write": (C.c_int, [C.c_char_p, _u8p, C.c_uint64, _u32p, C.c_uint64, C.c_uint32, _u8p]),
     "cs_fm_destroy": (None, [_vp]),
     "cs_fm_get_info": (C.c_int, [_vp, C.POINTER(cs_fm_info)]),
     "cs_fm_last_error": (C.c_char_p, []),
@@ -97,6 +99,7 @@ SIGNATURES = {
     "cs_fm_extract_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_bytes_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, C.c_uint32, _vp]),
+    "cs_fm_locate_record_hits_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_batch_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64,
                                               C.POINTER(cs_count_out), C.c_uint32, _vp]),
     "cs_fm_count_packed_device": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64,
@@ -459,6 +462,11 @@ class FMIndex:
         _check(lib().cs_fm_count_bytes_device_ex(self._h, d_pats, d_offs, npat, d_out, flags,
                                                  stream or None))
 
+    def locate_record_hits_device(self, d_pats, d_offs, npat, d_hit, stream=0):
+        """Per pattern 1 when the locate records answer it in one read (roofline accounting)."""
+        _check(lib().cs_fm_locate_record_hits_device(self._h, d_pats, d_offs, npat, d_hit,
+                                                     stream or None))
+
     def locate_ranges_device(self, d_pats, d_offs, npat, limit, d_sp, d_out_offs, stream=0,
                              flags=0) -> int:
         total = C.c_uint64()
@@ -603,6 +611,21 @@ def sa_build(text, device: int = 0) -> np.ndarray:
     out = np.zeros(max(n, 1), np.uint32)
     _check(lib().cs_sa_build(_u8(t), n, out.ctypes.data_as(_u32p), device))
     return out[:n]
+
+
+def csidx_write(path: str, bwt, ssa, ssa_stride: int, text=None):
+    """cs_csidx_write: a CSIDX file from host arrays (the reference's bwt_ / ssa_ / text_
+    members) on the host, no device."""
+    b = np.ascontiguousarray(np.frombuffer(bytes(bwt), np.uint8) if isinstance(bwt, (bytes, bytearray))
+                             else bwt, np.uint8)
+    s_ = np.ascontiguousarray(ssa, np.uint32)
+    t = None
+    if text is not None:
+        t = np.ascontiguousarray(np.frombuffer(bytes(text), np.uint8) if isinstance(text, (bytes, bytearray))
+                                 else text, np.uint8)
+    _check(lib().cs_csidx_write(path.encode(), _u8(b) if len(b) else None, len(b),
+                                s_.ctypes.data_as(_u32p) if len(s_) else None, len(s_), ssa_stride,
+                                _u8(t) if t is not None and len(t) else None))
 
 
 def csidx_check(path: str) -> dict:

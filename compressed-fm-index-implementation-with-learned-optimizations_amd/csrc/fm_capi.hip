@@ -436,8 +436,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_sa) (void)hipFree(h->d_sa);
   if (h->d_dtext) (void)hipFree(h->d_dtext);
   if (h->d_ptext) (void)hipFree(h->d_ptext);
-  if (h->route_h) (void)hipHostFree(h->route_h);
-  if (h->route_d) (void)hipFree(h->route_d);
+  if (h->d_lrec) (void)hipFree(h->d_lrec);
   if (h->d_prare) (void)hipFree(h->d_prare);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
@@ -489,6 +488,7 @@ cs_status build_common(const uint8_t* d_text, uint64_t n, const cs_build_params*
     cs_status s = build_index_device(d_text, n, p->ssa_stride, h, st);
     if (s == CS_OK && host_text) h->h_text.assign(host_text, host_text + n);
     if (s == CS_OK) s = keep_device_text(h, d_text, true, st);
+    if (s == CS_OK) s = derive_locate_records(h, st);
     return s;
   });
 }
@@ -546,6 +546,7 @@ cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint
     cs_status s = build_index_from_bwt(bwt, n, ssa, nsamples, ssa_stride, h, st);
     if (s == CS_OK && text) h->h_text.assign(text, text + n);
     if (s == CS_OK && text) s = keep_device_text(h, text, false, st);
+    if (s == CS_OK) s = derive_locate_records(h, st);
     return s;
   });
 }
@@ -595,6 +596,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->record_bytes = h->ptab_rec ? h->ptab_entry_bytes() : 0u;
   out->text_in_hbm = h->d_dtext ? 1u : 0u;
   out->packed_text_bytes = h->d_ptext ? h->ptext_bytes() : 0;
+  out->locate_record_bytes = h->d_lrec ? h->lrec_bytes() : 0;
   return CS_OK;
 }
 
@@ -647,6 +649,19 @@ cs_status cs_fm_count_bytes_device_ex(const cs_fm_index* h, const uint8_t* d_pat
     return CS_ERR_INVALID;
   }
   return launch_count_bytes(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream, flags);
+}
+
+cs_status cs_fm_locate_record_hits_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                          const uint64_t* d_offs, uint64_t npat, uint8_t* d_hit,
+                                          void* stream) {
+  DeviceScope dscope;
+  cs_status s = check_handle(h, dscope);
+  if (s != CS_OK) return s;
+  if (npat && (!d_offs || !d_pats || !d_hit)) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return launch_locrec_hits(h, d_pats, d_offs, npat, d_hit, (hipStream_t)stream);
 }
 
 // cs_count_out -> the kernels' CountOut, validated
@@ -1002,17 +1017,17 @@ cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, co
   }
   hipStream_t st = (hipStream_t)stream;
   bool done = false;
-  // any flag but CS_Q_LONG leaves structures out: the two phases honour it
-  if (!(flags & ~CS_Q_LONG)) {
+  // any flag but CS_Q_LONG / CS_Q_NO_LOC_RECORDS leaves structures out: the two phases honour it
+  if (!(flags & ~(CS_Q_LONG | CS_Q_NO_LOC_RECORDS))) {
     s = launch_locate_onepass(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, st,
-                              &done, flags & CS_Q_LONG);
+                              &done, flags & (CS_Q_LONG | CS_Q_NO_LOC_RECORDS));
     if (s != CS_OK) return s;
   }
   if (!done) {  // the two phases: ranges, then (when the total fits) the positions
     StreamBuf sp;
     FMX_HIP(sp.alloc((npat ? npat : 1) * 8, st));
     s = launch_locate_ranges(h, d_pats, d_offs, npat, limit, sp.as<uint64_t>(), d_out_offs, total, st,
-                             flags & ~CS_Q_LONG);
+                             flags & ~(CS_Q_LONG | CS_Q_NO_LOC_RECORDS));
     if (s != CS_OK) return s;
     if (*total > cap) {
       set_error("locate: capacity too small");

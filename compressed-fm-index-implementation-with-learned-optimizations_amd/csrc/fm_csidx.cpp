@@ -139,14 +139,71 @@ cs_status csidx_parse(const std::vector<uint8_t>& f, std::vector<uint8_t>& bwt, 
   return CS_OK;
 }
 
+// the whole file, sized by fstat and read in one pass (no growth by repeated
+// insert, read errors reported)
 bool read_file(const char* path, std::vector<uint8_t>& f) {
   std::FILE* fp = std::fopen(path, "rb");
   if (!fp) return false;
-  uint8_t buf[1 << 16];
-  size_t k;
-  while ((k = std::fread(buf, 1, sizeof buf, fp)) > 0) f.insert(f.end(), buf, buf + k);
+  struct stat sb;
+  if (fstat(fileno(fp), &sb) != 0 || sb.st_size < 0) {
+    std::fclose(fp);
+    return false;
+  }
+  f.resize((size_t)sb.st_size);
+  const size_t k = f.empty() ? 0 : std::fread(f.data(), 1, f.size(), fp);
+  const bool ok = k == f.size() && !std::ferror(fp);
   std::fclose(fp);
-  return true;
+  return ok;
+}
+
+// The file IndexWriter would write for these members (serialization.cpp:64-147): header,
+// text (optional), BWT, C_ (the BWT's cumulative histogram, fm_index.cpp:36-47), SSA, footer.
+cs_status csidx_write(const char* path, const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint64_t ns,
+                      uint32_t stride, const uint8_t* text) {
+  if (n >= (1ull << 32)) return report(CS_ERR_UNSUPPORTED, "CSIDX: u32 samples need n < 2^32");
+  if (stride == 0 || ns != (n + stride - 1) / stride)
+    return report(CS_ERR_INVALID, "CSIDX: the SSA must hold ceil(n / stride) samples");
+  uint64_t hist[256] = {0};
+  for (uint64_t i = 0; i < n; ++i) ++hist[bwt[i]];
+  uint32_t c32[257];
+  uint64_t cum = 0;
+  for (int c = 0; c < 257; ++c) {
+    c32[c] = (uint32_t)cum;
+    if (c < 256) cum += hist[c];
+  }
+  Writer w;
+  w.f = std::fopen(path, "wb");
+  if (!w.f) return report(CS_ERR_INVALID, std::string("cannot write: ") + path);
+  Header hd;
+  std::memset(&hd, 0, sizeof hd);
+  std::memcpy(hd.magic, "CSIDX", 5);
+  hd.version = 1;
+  hd.text_len = n;
+  w.raw(&hd, sizeof hd);  // rewritten with the offsets at the end (IndexWriter::finalize)
+  if (text) {
+    w.align8();
+    hd.offsets[kText] = w.at;
+    w.array(text, n);
+  }
+  w.align8();
+  hd.offsets[kBwt] = w.at;
+  w.array(bwt, n);
+  w.align8();
+  hd.offsets[kCArr] = w.at;
+  w.array(c32, 257);
+  w.align8();
+  hd.offsets[kSsa] = w.at;
+  w.raw(&stride, 4);
+  w.align8();
+  w.array(ssa, ns);
+  w.align8();
+  hd.offsets[7] = w.at;
+  w.raw(&kFooter, 8);
+  if (std::fseek(w.f, 0, SEEK_SET) != 0) w.ok = false;
+  else if (std::fwrite(&hd, sizeof hd, 1, w.f) != 1) w.ok = false;
+  if (std::fclose(w.f) != 0) w.ok = false;
+  if (!w.ok) return report(CS_ERR_INVALID, std::string("cannot write: ") + path);
+  return CS_OK;
 }
 
 }  // namespace
@@ -213,47 +270,15 @@ cs_status cs_fm_save_csidx(const cs_fm_index* h, const char* path) {
   if ((s = cs_fm_get_ssa(h, s64.data(), ns, &ns)) != CS_OK) return s;
   std::vector<uint32_t> ssa(ns);
   for (uint64_t k = 0; k < ns; ++k) ssa[k] = (uint32_t)s64[k];
-  uint64_t c64[257];
-  if ((s = cs_fm_get_C(h, c64)) != CS_OK) return s;
-  uint32_t c32[257];
-  for (int c = 0; c < 257; ++c) c32[c] = (uint32_t)c64[c];
   uint64_t nt = 0;
   const bool has_text = !n || cs_fm_extract(h, 0, n, text.data(), &nt) == CS_OK;
+  return csidx_write(path, bwt.data(), n, ssa.data(), ns, info.ssa_stride, has_text ? text.data() : nullptr);
+}
 
-  Writer w;
-  w.f = std::fopen(path, "wb");
-  if (!w.f) return report(CS_ERR_INVALID, std::string("cannot write: ") + path);
-  Header hd;
-  std::memset(&hd, 0, sizeof hd);
-  std::memcpy(hd.magic, "CSIDX", 5);
-  hd.version = 1;
-  hd.text_len = n;
-  w.raw(&hd, sizeof hd);  // rewritten with the offsets at the end (IndexWriter::finalize)
-  if (has_text) {
-    w.align8();
-    hd.offsets[kText] = w.at;
-    w.array(text.data(), n);
-  }
-  w.align8();
-  hd.offsets[kBwt] = w.at;
-  w.array(bwt.data(), n);
-  w.align8();
-  hd.offsets[kCArr] = w.at;
-  w.array(c32, 257);
-  w.align8();
-  hd.offsets[kSsa] = w.at;
-  const uint32_t stride = info.ssa_stride;
-  w.raw(&stride, 4);
-  w.align8();
-  w.array(ssa.data(), ns);
-  w.align8();
-  hd.offsets[7] = w.at;
-  w.raw(&kFooter, 8);
-  if (std::fseek(w.f, 0, SEEK_SET) != 0) w.ok = false;
-  else if (std::fwrite(&hd, sizeof hd, 1, w.f) != 1) w.ok = false;
-  if (std::fclose(w.f) != 0) w.ok = false;
-  if (!w.ok) return report(CS_ERR_INVALID, std::string("cannot write: ") + path);
-  return CS_OK;
+cs_status cs_csidx_write(const char* path, const uint8_t* bwt, uint64_t n, const uint32_t* ssa,
+                         uint64_t nsamples, uint32_t ssa_stride, const uint8_t* text) {
+  if (!path || (n && !bwt) || (nsamples && !ssa)) return report(CS_ERR_INVALID, "null argument");
+  return csidx_write(path, bwt, n, ssa, nsamples, ssa_stride, text);
 }
 
 }  // extern "C"

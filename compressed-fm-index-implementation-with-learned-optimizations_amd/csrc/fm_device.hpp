@@ -132,7 +132,29 @@ struct DevIndex {
   const uint64_t* ptext;
   const uint32_t* prare;
   uint32_t nrare;
+  // Locate records (null when absent; see kLocRec below): one 16-B record per
+  // (ptab_k + 1)-mer, index = the prefix-table index of its last ptab_k characters plus
+  // digit(first character) * 4^ptab_k.
+  const void* lrec;
 };
+
+// Locate records (narrow lf_exact occurrence-line indexes with 16-B context records, the
+// left contexts and the full SA; C4: k + 1 = 16, 69 GB).  A Q_text locate through the
+// context record reads the record, then the matching row's SA entry — two dependent random
+// reads where count needs one.  The locate record of a (k+1)-mer holds the SA values
+// themselves: for a (k+1)-mer with at most kLocRecRows rows, dwords 0-2 = SA[row i] for its
+// rows i < w, dword 3 = the rows' kLocRecQ-character left contexts (8 bits each, the low bits
+// of their lctx entries) at bits 8i, and w at bits 24-26 (kLocRecNone: more rows, or an
+// escaped context — read the context record instead).  A pattern of k+1+j characters, j <=
+// kLocRecQ, matches row i iff the low 2j bits of its context spell the j characters before
+// the (k+1)-mer (the backward-search invariant, fm_device.hpp kCtxQ), and a single matching
+// row's position is SA[row i] - j (SA[LF^j(r)] = SA[r] - j, lf_exact).  C4 (n / 4^16 = 0.93
+// rows per 16-mer): a text 20-mer's 16-mer has at most 3 rows 93 % of the time.  Built from
+// the k-mer's context record and lctx: the rows of c.x are the rows r of x with BWT[r] = c
+// (the first symbol of r's chain), in order, with SA[r] - 1 and r's chain shifted by one.
+constexpr uint32_t kLocRecRows = 3;
+constexpr uint32_t kLocRecQ = 4;
+constexpr uint32_t kLocRecNone = 7;
 
 // Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q
 // characters preceding the row's rotation — symbol t in bits [sb t, sb (t+1)).
@@ -181,17 +203,21 @@ __device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint6
   }
 }
 
-// Long-pattern routing (fm_query.hip launch_count_staged): seen_h is a word of pinned host
-// memory the host reads before a launch — set (system scope) by the staged count kernel
-// when its batch held a pattern longer than its one-read path takes (kFastM), once per
-// episode thanks to seen_d; while it is set, the staged kernel skips those patterns and
-// k_count_long takes them, setting used_d when there were any, and k_count_list clears
-// seen_h after a batch without them.  Routing changes which kernel counts a pattern,
-// never the count.  All null: no routing.
-struct LongRoute {
-  uint32_t* seen_h = nullptr;
-  uint32_t* seen_d = nullptr;
-  uint32_t* used_d = nullptr;
+// Long-pattern routing inside one call (fm_query.hip launch_count_staged / the one-call
+// locate): the staged kernel leaves the patterns its one read cannot answer (m >= kFastM and
+// m > k + kCtxQ) to the long-pattern kernel launched behind it on the same stream.  Block b
+// of the staged kernel (its kLongRegion patterns) lists them in region b of `list` — the
+// pattern's offset inside the region (u16), the number in cnt[b] — and zeroes cnt2[b];
+// the long-pattern kernel walks the regions (lengths read on the device), and what it cannot
+// finish goes to region lists `list2` / `cnt2` for the general-search kernel after it.  No
+// host synchronisation and no state in the handle: every list is the call's own buffer, so
+// concurrent calls on other streams cannot interfere.  All null: no routing.
+constexpr uint32_t kLongRegion = 512;  // = 2 kBlk: the staged kernels' patterns per block (U = 2)
+struct LongList {
+  uint16_t* list = nullptr;
+  uint32_t* cnt = nullptr;
+  uint16_t* list2 = nullptr;
+  uint32_t* cnt2 = nullptr;
 };
 
 // A single pattern passed by value in kernel arguments (k_count_one).
@@ -246,6 +272,36 @@ constexpr uint32_t kRec16Wide = 15;
 // bits 24-29.  Enough for a 20-mer at k = 16.  A k-mer whose range the 8-B wide table
 // escaped (wider than kPtabEsc) has width kRec16Wide and dword 2 = ~0: its search starts
 // from C[].
+// Majority contexts of a wide compact record (narrow indexes, round 4): a range wider than
+// kRec16Ctx rows whose rows' contexts repeat — repetitive text, where a k-mer's rows are
+// copies of one locus — keeps the two most frequent kRec16Q-character contexts with their
+// exact counts: dword 1 bit 4 (kRec16Maj) set, bit 5 (kRec16MajAll) when every row's context
+// is one of the two, bits 6-15 context A, bits 16-25 context B; dword 3 count A (bits 0-15)
+// and count B (bits 16-31, 0 = no B).  A count of a pattern with kRec16Q characters before
+// the table part is then the count of its context (0 when absent from a complete list) — the
+// rows surviving the reference's remaining steps are the rows whose chain spells them
+// (kCtxQ), exactly.  Built only for ranges without escaped contexts, of at most kRec16MajScan
+// rows, whose counts fit 16 bits.
+constexpr uint32_t kRec16Maj = 1u << 4;
+constexpr uint32_t kRec16MajAll = 1u << 5;
+constexpr uint32_t kRec16MajScan = 1u << 20;
+// the count of the kRec16Q-character context want10 from a majority record, when it answers
+__device__ __forceinline__ bool rec16_majority(uint32_t y, uint32_t w3, uint32_t want10, uint64_t& cnt) {
+  if (!(y & kRec16Maj)) return false;
+  if (want10 == ((y >> 6) & 0x3FFu)) {
+    cnt = w3 & 0xFFFFu;
+    return true;
+  }
+  if ((w3 >> 16) && want10 == ((y >> 16) & 0x3FFu)) {
+    cnt = w3 >> 16;
+    return true;
+  }
+  if (y & kRec16MajAll) {
+    cnt = 0;
+    return true;
+  }
+  return false;
+}
 constexpr uint32_t kRec16CtxW = 10;
 constexpr uint32_t kRec16QW = 4;
 constexpr uint32_t kRec16NoRange = 0xFFFFFFFFu;

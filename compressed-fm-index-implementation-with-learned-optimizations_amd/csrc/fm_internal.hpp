@@ -60,13 +60,10 @@ struct cs_fm_index {
   void* d_prare = nullptr;
   uint32_t nrare = 0;
   uint64_t ptext_bytes() const { return ((n + 31) / 32) * 8; }
-  // Long-pattern routing of device batches (fm_query.hip launch_count_staged): a pinned,
-  // device-mapped word the count kernels set when a batch held patterns over 32 characters
-  // (then the next batches send those to k_count_long), and two HBM words of bookkeeping.
-  // Allocated on first use.
-  mutable std::mutex route_mu;
-  mutable uint32_t* route_h = nullptr;
-  mutable uint32_t* route_d = nullptr;
+  // Locate records (fmx::DevIndex::lrec): 16 B per (ptab_k + 1)-mer, derived from the context
+  // records, the left contexts and the full SA on build / open / import, not saved
+  void* d_lrec = nullptr;
+  uint64_t lrec_bytes() const { return d_lrec ? (16ull << (2 * (ptab_k + 1))) : 0; }
   uint32_t active_levels[256] = {};
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
@@ -145,6 +142,7 @@ struct cs_fm_index {
     d.vtext = ver ? static_cast<const uint8_t*>(d_dtext) : nullptr;
     d.ptext = ver && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
     d.prare = static_cast<const uint32_t*>(d_prare);
+    d.lrec = d_sa && lf_exact && !wide ? d_lrec : nullptr;
     d.nrare = nrare;
     return d;
   }
@@ -213,6 +211,9 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
 // the resident server kernel (one wave) on the handle's server stream
 cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t idle_ticks,
                               uint64_t life_ticks);
+// measurement twin of the one-call locate's locate records (cs_fm_locate_record_hits_device)
+cs_status launch_locrec_hits(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                             uint64_t npat, uint8_t* d_hit, hipStream_t st);
 cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
@@ -245,6 +246,13 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st);
 cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st);
 // the 2-bit text of d_dtext (cs_fm_index::d_ptext), when the index can use it (fm_query.hip)
 cs_status derive_packed_text(cs_fm_index* h, hipStream_t st);
+// the locate records (cs_fm_index::d_lrec, fm_device.hpp kLocRec*) when the index can use them
+cs_status derive_locate_records(cs_fm_index* h, hipStream_t st);
+// both derived parts (open / import)
+inline cs_status derive_parts(cs_fm_index* h, hipStream_t st) {
+  cs_status s = derive_packed_text(h, st);
+  return s == CS_OK ? derive_locate_records(h, st) : s;
+}
 // HBM held by the index's device arrays so far (the image parts, fm_io.hip)
 uint64_t index_hbm_bytes(const cs_fm_index* h);
 // Whether an optional structure of `bytes` may be allocated: the device keeps an eighth

@@ -231,6 +231,7 @@ uint64_t index_hbm_bytes(const cs_fm_index* hc) {
   for (const Part& p : index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr))
     if (*p.dptr) b += p.bytes;
   if (h->d_ptext) b += h->ptext_bytes();  // derived, not an image part
+  b += h->lrec_bytes();                    // the same
   return b;
 }
 
@@ -396,7 +397,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     }
     std::fclose(t);
   }
-  if ((s = derive_packed_text(h, nullptr)) != CS_OK) return fail(s);
+  if ((s = derive_parts(h, nullptr)) != CS_OK) return fail(s);
   *out = h;
   return CS_OK;
 }
@@ -471,7 +472,7 @@ cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d
       return fail(hip_fail(hipGetLastError(), "hipMemcpy (import)"));
   if (hipMemcpy(&h->h_table, h->d_table, sizeof(NodeTable), hipMemcpyDeviceToHost) != hipSuccess)
     return fail(hip_fail(hipGetLastError(), "hipMemcpy (import table)"));
-  if ((s = derive_packed_text(h, nullptr)) != CS_OK) return fail(s);
+  if ((s = derive_parts(h, nullptr)) != CS_OK) return fail(s);
   *out = h;
   return CS_OK;
 }
@@ -533,7 +534,7 @@ cs_status cs_fm_import_commit(cs_fm_index* h) {
   FMX_HIP(ds.enter(h->device));
   FMX_HIP(hipDeviceSynchronize());  // the caller's copies into the parts (any stream)
   FMX_HIP(hipMemcpy(&h->h_table, h->d_table, sizeof(NodeTable), hipMemcpyDeviceToHost));
-  return derive_packed_text(h, nullptr);
+  return derive_parts(h, nullptr);
 }
 
 }  // extern "C"

@@ -420,12 +420,15 @@ struct QWM {
 // still to process (P[k-1] .. P[0]).  Requires m >= 1.
 // With context records, *inl receives the entry's contexts (kRecCtx u16 in 6 dwords),
 // or the compact record itself (fm_device.hpp kRec16Ctx) when it holds contexts.
+// maj: a wide compact record's majority contexts (kRec16Maj), when it holds them.
 template <class PT>
 __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable& T,
                                              PT P, uint64_t m,
                                              uint64_t& sp, uint64_t& ep, uint64_t& k,
-                                             uint64_t* bytes, const uint32_t** inl = nullptr) {
+                                             uint64_t* bytes, const uint32_t** inl = nullptr,
+                                             const uint32_t** maj = nullptr) {
   if (inl) *inl = nullptr;
+  if (maj) *maj = nullptr;
   if (ix.ptab_k && m >= ix.ptab_k) {
     uint32_t t = 0;
     bool ok = true;
@@ -439,9 +442,13 @@ __device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable
       if (inl && ix.ptab_rec == 3 && ep - sp <= kRecQCtx)
         *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4 + 2;
       if (inl && ix.ptab_rec == 1) *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 8 + 2;
-      if (inl && ix.ptab_rec == 2) {
+      if ((inl || maj) && ix.ptab_rec == 2) {
         const uint32_t* r = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4;
-        if ((r[1] & 15u) != kRec16Wide) *inl = r;
+        if ((r[1] & 15u) != kRec16Wide) {
+          if (inl) *inl = r;
+        } else if (maj && !ix.wide && (r[1] & kRec16Maj)) {
+          *maj = r;
+        }
       }
       k = m - ix.ptab_k;
       return;
@@ -591,9 +598,20 @@ __device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const Node
                                                   PT P, uint64_t m,
                                                   uint64_t* bytes = nullptr) {
   uint64_t sp, ep, k;
-  const uint32_t* inl;
-  search_start(ix, T, P, m, sp, ep, k, bytes, &inl);
+  const uint32_t *inl, *maj;
+  search_start(ix, T, P, m, sp, ep, k, bytes, &inl, &maj);
   if (sp >= ep) return 0;
+  if (maj && k == kRec16Q) {  // a wide record's majority contexts (kRec16Maj)
+    uint32_t want = 0;
+    bool ok = true;
+    for (uint32_t t = 0; t < kRec16Q; ++t) {  // chain symbol t = P[k-1-t]
+      const uint32_t d = T.occ_code[P[kRec16Q - 1 - t]];
+      ok &= d != kNoCode;
+      want |= (d & 3u) << (2 * t);
+    }
+    uint64_t c;
+    if (ok && rec16_majority(maj[1], maj[3], want, c)) return c;
+  }
   return count_rest<E, PT, kLA>(ix, T, P, k, sp, ep, bytes, inl);
 }
 
@@ -1255,7 +1273,7 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
     rs[j] = s;
     row[j] = s;
     adj[j] = 0;
-    one[j] = q < npat && kc[j] == 1;
+    one[j] = q < npat && kc[j] == 1 && (s >> 62) != 1;  // (not stashed by a locate record)
     uint32_t rel;
     if (one[j] && (s & kLocCtx)) loc_window(s, row[j], adj[j], rel);  // a window's only match: its first row
   }
@@ -1413,8 +1431,8 @@ __device__ __forceinline__ uint4 load_record16(const void* tab, uint64_t t) {
 // spills): left alone the compiler gives the packed and uint8 forms 95-104 VGPRs (4-5
 // waves), and the packed count took 0.392 ms per 12.5 M instead of 0.361.
 // kSkipLong: patterns of kFastM characters or more whose search the one read cannot finish
-// (m > k + kCtxQ) are left to k_count_long (long-pattern routing, LongRoute); otherwise,
-// with lr set, such a pattern marks lr.seen_h.
+// (m > k + kCtxQ) are listed for k_count_long / k_locate_long (long-pattern routing inside the
+// call, LongList: region blockIdx.x of ll.list, its length in ll.cnt).
 template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false,
           bool kSkipLong = false, bool kRng = true, int kPos = 0>
 __global__ __launch_bounds__(kBlk)
@@ -1424,7 +1442,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                     uint64_t npat, CountOut co,
                                                     uint64_t limit, uint64_t* __restrict__ rec,
                                                     uint64_t fixed_m, OnePass op = OnePass{},
-                                                    LongRoute lr = LongRoute{}) {
+                                                    LongList ll = LongList{}) {
   // offs == nullptr: patterns of one length fixed_m at stride fixed_m (count only)
   // kNoBar: the general search reads the node table through the caches instead of a
   // block-wide LDS copy, so no wave waits at a block barrier for the block's slowest
@@ -1433,6 +1451,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // node table only when one of its patterns needs the general search
   __shared__ uint16_t cmap[256];
   __shared__ NodeTable T;
+  __shared__ uint32_t s_nlong;  // kSkipLong: the block's listed patterns
   // count forms: the range [sp, ep) of a pattern the general search finishes (st 5), kept
   // here across the barrier instead of in registers or read again from its table entry
   // (kRng; A/B in one process, profiles/r03/ab_range_across_barrier*.json: headline 0.389
@@ -1440,8 +1459,10 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   __shared__ uint64_t s_rng[kLoc ? 1 : U][kLoc ? 1 : kBlk][2];
   static_assert(kBlk >= 256, "one map entry per thread");
   static_assert(!kOne || (kLoc && !kNoBar), "the one-call locate is a locate with barriers");
+  static_assert(!kSkipLong || (!kNoBar && U * kBlk == kLongRegion), "a block lists one region");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
+  if (kSkipLong && threadIdx.x == 0) s_nlong = 0;
   __syncthreads();
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
   const uint32_t K = ix.ptab_k;
@@ -1451,6 +1472,11 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   for (int j = 0; j < U; ++j) kc[j] = kr[j] = 0;
   uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U];
+  // the one-call locate over the full SA: the locate record (fm_device.hpp kLocRec*) of the
+  // pattern's last k + 1 characters answers it in one read when the pattern has at most
+  // kLocRecQ characters before them (lqm bit j: pattern j takes it, at index lt[j])
+  constexpr bool kLR = kOne && kPos == 0;
+  uint32_t lt[kLR ? U : 1], lqm = 0;
   // 0 done, 1 table, 2 context, 3 general search, 4 left to k_count_long, 5 general search
   // from the range after the table (s_rng)
   uint8_t st[U];
@@ -1493,7 +1519,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     if constexpr (!kPacked) load_pattern32(pats, o0[j], wl, u);
     const uint32_t kk = m[j] - K;
     bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
-    uint32_t tt = 0, ww = 0;
+    uint32_t tt = 0, ww = 0, dl = kNoCode;
 #pragma unroll
     for (uint32_t i = 0; i < kFastM; ++i) {
       uint32_t b;
@@ -1507,6 +1533,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
         const uint32_t d = cmap[b] >> 8;
         cok &= d != kNoCode;
         ww |= (d & 3u) << (2 * (kk - 1 - i));
+        if constexpr (kLR)
+          if (i + 1 == kk) dl = cmap[b] & 0xFFu;  // the (k+1)-mer's first character (its table digit)
       }
     }
     if (!ok) continue;
@@ -1514,17 +1542,45 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     t[j] = tt;
     want[j] = ww;
     k[j] = kk;
+    if constexpr (kLR) {
+      // (ix.lrec implies a 4-symbol table of k <= 15: the index fits 32 bits)
+      if (ix.lrec && cok && kk >= 1 && kk - 1 <= kLocRecQ && dl != kNoCode) {
+        lt[j] = (dl << (2 * K)) + tt;
+        lqm |= 1u << j;
+      }
+    }
   }
-  if constexpr ((!kLoc || kOne) && !kSkipLong) {
-    // long-pattern routing: the first wave to meet a long pattern raises the host's flag
-    if (lr.seen_d) {
-      bool lg = false;
+  if constexpr (kSkipLong) {
+    // the long patterns into the block's region of the call's list (k_count_long /
+    // k_locate_long take them): an LDS counter orders them, the count follows the barrier
 #pragma unroll
-      for (int j = 0; j < U; ++j) lg |= m[j] >= kFastM && m[j] > K + kCtxQ;
-      if (__any(lg) && (threadIdx.x & 63) == 0 &&
-          !__hip_atomic_load(lr.seen_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        __hip_atomic_store(lr.seen_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(lr.seen_h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int j = 0; j < U; ++j)
+      if (st[j] == 4) {
+        const uint32_t at = atomicAdd(&s_nlong, 1u);
+        ll.list[(uint64_t)blockIdx.x * kLongRegion + at] = (uint16_t)(threadIdx.x + j * kBlk);
+      }
+  }
+  if constexpr (kLR) {
+    // (B0) the locate records: no match, or one matching row whose SA value the record holds,
+    // finishes the pattern here (its position stashed as the emit kernel copies it); more
+    // rows or matches read the context record below
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (!((lqm >> j) & 1u)) continue;
+      const uint4 a = load_record16(ix.lrec, lt[j]);
+      const uint32_t c = a.w >> 24;
+      if (c == kLocRecNone) continue;
+      const uint32_t j2 = k[j] - 1, mask = (1u << (2 * j2)) - 1u, want2 = want[j] >> 2;
+      uint32_t mm = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < kLocRecRows; ++i)
+        mm |= (uint32_t)(i < c && ((a.w >> (8 * i)) & mask) == want2) << i;
+      if (mm & (mm - 1u)) continue;  // two or three positions: the context record's window
+      st[j] = 0;
+      res[j] = mm ? 1u : 0u;
+      if (mm) {
+        const uint64_t v = mm == 1u ? a.x : mm == 2u ? a.y : a.z;
+        rv[j] = kLocStash | (v >= j2 ? v - j2 : v + ix.n - j2);
       }
     }
   }
@@ -1557,7 +1613,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       else
         rec16_contexts(a.y, a.z, a.w, d);
       w[j][0] = make_uint4(d[0], d[1], d[2], d[3]);
-      w[j][1] = make_uint4(d[4], 0u, 0u, 0u);
+      // (count forms: the record's dwords 1 and 3 for a wide record's majority contexts)
+      w[j][1] = make_uint4(d[4], kLoc ? 0u : a.y, kLoc ? 0u : a.w, 0u);
     } else if (!ptab_at(ix, t[j], sp[j], ep[j])) {
       st[j] = 3;
     }
@@ -1578,6 +1635,9 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     } else if (st[j] == 2 && inl[j] && ix.lctx) {
       bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record
       w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
+    } else if (!kLoc && st[j] == 2 && ix.ptab_rec == 2 && !ix.wide && k[j] == kRec16Q &&
+               (w[j][1].y & 15u) == kRec16Wide && rec16_majority(w[j][1].y, w[j][1].z, want[j], res[j])) {
+      st[j] = 0;  // a wide record's majority contexts (kRec16Maj): the count in the one read
     } else if (st[j] == 2 && ix.lctx && ep[j] - (sp[j] & ~15ull) <= 32) {
       bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
@@ -1667,7 +1727,12 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
 #pragma unroll
       for (int j = 0; j < U; ++j) need |= kc[j] == 1;
     }
-    if (__syncthreads_or(need)) {
+    const bool any_need = __syncthreads_or(need);
+    if (kSkipLong && threadIdx.x == 0) {  // the block's long patterns are listed (barrier above)
+      ll.cnt[blockIdx.x] = s_nlong;
+      ll.cnt2[blockIdx.x] = 0;
+    }
+    if (any_need) {
       load_table(T, ix.table);
       __syncthreads();
       if (general)
@@ -1681,7 +1746,12 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     locate_split_store<U, kPos>(ix, T, npat, blockIdx.x, q0, kc, kr, op, skip);
     return;
   }
-  if (!__syncthreads_or(general)) return;
+  const bool any_general = __syncthreads_or(general);
+  if (kSkipLong && threadIdx.x == 0) {  // the block's long patterns are listed (barrier above)
+    ll.cnt[blockIdx.x] = s_nlong;
+    ll.cnt2[blockIdx.x] = 0;
+  }
+  if (!any_general) return;
   load_table(T, ix.table);
   __syncthreads();
   general_rest<E, U, kLoc, kPacked, W>(ix, T, pats, st, o0, m, q0, co, limit, rec, nullptr, nullptr,
@@ -1889,9 +1959,9 @@ __device__ __forceinline__ bool window_eq_packed(const DevIndex& ix, const uint6
 // kPT: verify against the packed text (DevIndex::ptext), else the byte text in rounds of
 // kLongWords words.  Patterns the pipeline does not answer are appended to `list` (q) for
 // k_count_list, which runs the general search.
-// skip_short: the staged kernel has counted all but the long patterns (m >= kFastM, m > k + kCtxQ)
-// (long-pattern routing); lr.used_d is then raised when the batch held long patterns
-// (sampled: the first wave of every 16th block).
+// from_list: the patterns the staged kernel listed (LongList regions, long-pattern routing),
+// else every pattern; skip_short (measurement twin only): every pattern is read and only the
+// long ones (m >= kFastM, m > k + kCtxQ: the ones a routed call lists) are searched.
 // kBytes: measurement twin (bench.py's roofline) — co.out receives each pattern's random
 // algorithmic bytes instead of its count: the table entry, the context sector(s), per
 // candidate its SA sector (32 B) and the text words of its window.
@@ -2018,26 +2088,47 @@ __device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __
   return false;  // wider than the record and two sectors: steps first
 }
 
-// the general search for the patterns a long-pattern kernel does not answer: appended to
-// `list` (q), one atomic per wave
-__device__ __forceinline__ void long_list_append(bool general, uint64_t q, uint64_t* __restrict__ list,
-                                                 unsigned long long* __restrict__ nlist) {
-  const uint64_t gm = __ballot(general);
-  if (!gm) return;
-  const uint32_t lane = threadIdx.x & 63;
-  uint64_t at = 0;
-  if (lane == (uint32_t)__ffsll((unsigned long long)gm) - 1u) at = atomicAdd(nlist, (unsigned long long)__popcll(gm));
-  at = __shfl(at, __ffsll((unsigned long long)gm) - 1, 64);
-  if (general) list[at + __popcll(gm & ((1ull << lane) - 1))] = q;
+// the general search for the patterns a long-pattern kernel does not answer: listed in the
+// region of pattern q (LongList list2 / cnt2; the regions are kLongRegion patterns wide)
+__device__ __forceinline__ void long_list_append(bool general, uint64_t q, const LongList& ll) {
+  if (!general) return;
+  const uint64_t r = q / kLongRegion;
+  const uint32_t at = atomicAdd(ll.cnt2 + r, 1u);
+  ll.list2[r * kLongRegion + at] = (uint16_t)(q - r * kLongRegion);
+}
+
+// The patterns of one long-pattern launch: from the staged kernel's region lists (ll.list /
+// ll.cnt: block b of the grid walks regions b, b + grid, ...; the lengths are read on the
+// device, so an empty list costs the launch) or, without a list (CS_Q_LONG, fixed-length
+// batches of long patterns), every pattern q < npat.  f(q, active) runs with the whole block
+// in lockstep (active = q is a pattern to search), so f may use wave collectives; the q of
+// every lane of a wave, active or not, lies in one region (= one tile of the one-call locate).
+template <class F>
+__device__ __forceinline__ void long_patterns(const LongList& ll, bool from_list, uint64_t npat, F&& f) {
+  if (from_list) {
+    const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
+    for (uint64_t r = blockIdx.x; r < regions; r += gridDim.x) {
+      const uint32_t c = ll.cnt[r];  // uniform over the block
+      for (uint32_t i0 = 0; i0 < c; i0 += kBlk) {
+        const uint32_t i = i0 + threadIdx.x;
+        const bool act = i < c;
+        // (an inactive lane gets the region's first pattern: same tile, same region)
+        f(r * kLongRegion + (act ? ll.list[r * kLongRegion + i] : 0u), act);
+      }
+    }
+  } else {
+    for (uint64_t b0 = blockIdx.x * (uint64_t)kBlk; b0 < npat; b0 += (uint64_t)gridDim.x * kBlk) {
+      const uint64_t q = b0 + threadIdx.x;
+      f(q, q < npat);
+    }
+  }
 }
 
 template <int W, bool kPT, bool kBytes = false, int kV16 = 0>
 __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
-                                                     CountOut co, uint64_t fixed_m,
-                                                     uint64_t* __restrict__ list,
-                                                     unsigned long long* __restrict__ nlist,
-                                                     bool skip_short, LongRoute lr) {
+                                                     CountOut co, uint64_t fixed_m, LongList ll,
+                                                     bool from_list, bool skip_short) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   static_assert(kBlk >= 256, "one map entry per thread");
@@ -2045,198 +2136,182 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
-  const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-  if (q >= npat) return;
-  const uint64_t o0 = offs ? offs[q] : q * fixed_m;
-  const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
-  if (skip_short) {
-    const bool mine = m >= kFastM && m > ix.ptab_k + kCtxQ;  // the staged kernel skipped it
-    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(mine) && threadIdx.x == 0)
-      __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!mine) return;
-  }
-  if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
-    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
-    else store_count<W>(co, q, m == 0 ? ix.n : 0);
-    return;
-  }
-  uint64_t by = 0;  // kBytes
-  uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
-  uint64_t base;
-  uint32_t cand, qf;
-  const bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
-  uint64_t res = 0;
-  if (!general) {
-    // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
-    const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
-    while (cand) {
-      const uint32_t i = (uint32_t)__ffs(cand) - 1u;
-      cand &= cand - 1;
-      const uint64_t p = load_sa(ix.vsa, base + i);
-      const uint64_t wq = p >= k ? p - k : p + n - k;
-      if constexpr (kBytes) {  // the SA sector, then the window's words
-        constexpr uint64_t C = 32ull * kLongPW;
-        by += 32;
-        if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
-        else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
-        else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
-          by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
-                (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
-        continue;
-      }
-      bool eq;
-      if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
-      else eq = window_eq_long<kLongWords>(ix, pats + o0, wq, L);
-      res += eq ? 1u : 0u;
+  long_patterns(ll, from_list, npat, [&](uint64_t q, bool act) {
+    if (!act) return;
+    const uint64_t o0 = offs ? offs[q] : q * fixed_m;
+    const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
+    // skip_short (the measurement twin of a routed batch): only the patterns the staged
+    // kernel lists
+    if (skip_short && !(m >= kFastM && m > ix.ptab_k + kCtxQ)) return;
+    if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
+      if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
+      else store_count<W>(co, q, m == 0 ? ix.n : 0);
+      return;
     }
-  }
-  long_list_append(general, q, list, nlist);
-  if (general) return;
-  if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
-  else store_count<W>(co, q, res);
+    uint64_t by = 0;  // kBytes
+    uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
+    uint64_t base;
+    uint32_t cand, qf;
+    const bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+    uint64_t res = 0;
+    if (!general) {
+      // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
+      const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
+      while (cand) {
+        const uint32_t i = (uint32_t)__ffs(cand) - 1u;
+        cand &= cand - 1;
+        const uint64_t p = load_sa(ix.vsa, base + i);
+        const uint64_t wq = p >= k ? p - k : p + n - k;
+        if constexpr (kBytes) {  // the SA sector, then the window's words
+          constexpr uint64_t C = 32ull * kLongPW;
+          by += 32;
+          if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
+          else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
+          else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
+            by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
+                  (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
+          continue;
+        }
+        bool eq;
+        if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
+        else eq = window_eq_long<kLongWords>(ix, pats + o0, wq, L);
+        res += eq ? 1u : 0u;
+      }
+    }
+    long_list_append(general, q, ll);
+    if (general) return;
+    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
+    else store_count<W>(co, q, res);
+  });
 }
 
 // Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
 constexpr uint64_t kLocTile = 2 * kBlk;
+static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns");
 
 // The long-pattern search for the one-call locate (launch_locate_onepass over full-SA
-// indexes: CS_Q_LONG, host batches of long patterns, long-pattern routing): k_count_long's
-// stages, then per pattern min(count, limit) and its record for k_locate_emit — the only
-// position itself (kLocStash: the SA entry the verification read, minus k) or a verified
-// window (first row, match bits, k), whose positions the emit kernel reads through SA — and
-// each wave adds its patterns' counts to their tile's total (zeroed before, or holding the
-// staged kernel's totals of the short patterns under routing).  The patterns it cannot
-// finish (as k_count_long's, and windows whose matches lie too far apart for the record)
-// go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search), :125 (limit).
+// indexes: CS_Q_LONG, host batches of long patterns, and the long patterns the staged kernel
+// lists): k_count_long's stages, then per pattern min(count, limit) and its record for
+// k_locate_emit — the only position itself (kLocStash: the SA entry the verification read,
+// minus k) or a verified window (first row, match bits, k), whose positions the emit kernel
+// reads through SA — and the counts added to their tile's total (zeroed before, or holding the
+// staged kernel's totals of the short patterns): a list region is one tile, so the block adds
+// its sum once per region; without a list a wave's 64 patterns lie in one tile.  The patterns
+// it cannot finish (as k_count_long's, and windows whose matches lie too far apart for the
+// record) go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search), :125 (limit).
 template <int kV16>
 __global__ __launch_bounds__(kBlk) void k_locate_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                       const uint64_t* __restrict__ offs, uint64_t npat,
-                                                      uint64_t limit, OnePass op, uint64_t* __restrict__ list,
-                                                      unsigned long long* __restrict__ nlist, bool skip_short,
-                                                      LongRoute lr) {
+                                                      uint64_t limit, OnePass op, LongList ll, bool from_list) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   if (threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
-  // no lane returns early: the wave sums its counts at the end
-  const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-  bool mine = q < npat, general = false;
-  const uint64_t o0 = mine ? offs[q] : 0, m = mine ? offs[q + 1] - o0 : 0;
-  if (skip_short) {
-    const bool lg = mine && m >= kFastM && m > ix.ptab_k + kCtxQ;  // the staged kernel skipped it
-    if (lr.used_d && (blockIdx.x & 15) == 0 && threadIdx.x < 64 && __any(lg) && threadIdx.x == 0)
-      __hip_atomic_store(lr.used_d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    mine = lg;
-  }
-  uint64_t kc = 0, rec = 0;
-  if (mine && m != 0 && ix.n != 0) {  // fm_index.cpp:109: locate("") = {}
-    uint64_t by = 0, pc[kLongPW], base;
-    uint32_t cand, qf;
-    general = !long_stage<true, false, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
-    if (!general && cand) {
-      const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
-      uint32_t mm = 0;
-      uint64_t p0 = 0;  // the first matching row's position
-      for (uint32_t c = cand; c; c &= c - 1) {
-        const uint32_t i = (uint32_t)__ffs(c) - 1u;
-        const uint64_t p = load_sa(ix.vsa, base + i);
-        const uint64_t wq = p >= k ? p - k : p + n - k;
-        if (window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare)) {
-          if (!mm) p0 = wq;
-          mm |= 1u << i;
+  long_patterns(ll, from_list, npat, [&](uint64_t q, bool mine) {
+    bool general = false;
+    const uint64_t o0 = mine ? offs[q] : 0, m = mine ? offs[q + 1] - o0 : 0;
+    uint64_t kc = 0, rec = 0;
+    if (mine && m != 0 && ix.n != 0) {  // fm_index.cpp:109: locate("") = {}
+      uint64_t by = 0, pc[kLongPW], base;
+      uint32_t cand, qf;
+      general = !long_stage<true, false, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+      if (!general && cand) {
+        const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
+        uint32_t mm = 0;
+        uint64_t p0 = 0;  // the first matching row's position
+        for (uint32_t c = cand; c; c &= c - 1) {
+          const uint32_t i = (uint32_t)__ffs(c) - 1u;
+          const uint64_t p = load_sa(ix.vsa, base + i);
+          const uint64_t wq = p >= k ? p - k : p + n - k;
+          if (window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare)) {
+            if (!mm) p0 = wq;
+            mm |= 1u << i;
+          }
+        }
+        if (mm) {
+          const uint64_t c = (uint64_t)__popc(mm);
+          const uint32_t f = (uint32_t)__ffs(mm) - 1u, rel = mm >> f;
+          kc = c < limit ? c : limit;  // fm_index.cpp:125
+          if (kc == 1) rec = kLocStash | p0;
+          else if (kc > 1 && ((rel >> kLocVerRelBits) || k > kLocVerMaxK)) general = true;
+          else rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
         }
       }
-      if (mm) {
-        const uint64_t c = (uint64_t)__popc(mm);
-        const uint32_t f = (uint32_t)__ffs(mm) - 1u, rel = mm >> f;
-        kc = c < limit ? c : limit;  // fm_index.cpp:125
-        if (kc == 1) rec = kLocStash | p0;
-        else if (kc > 1 && ((rel >> kLocVerRelBits) || k > kLocVerMaxK)) general = true;
-        else rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
-      }
     }
-  }
-  if (general) kc = 0;  // k_locate_list adds it
-  long_list_append(general, q, list, nlist);
-  if (mine && !general) {
-    op.cnt[q] = (uint32_t)kc;
-    op.rec[q] = rec;
-  }
-  uint64_t s = kc;  // the wave's 64 patterns lie in one tile
+    if (general) kc = 0;  // k_locate_list adds it
+    long_list_append(mine && general, q, ll);
+    if (mine && !general) {
+      op.cnt[q] = (uint32_t)kc;
+      op.rec[q] = rec;
+    }
+    uint64_t s = kc;  // the wave's 64 patterns lie in one tile (long_patterns)
 #pragma unroll
-  for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
+    for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
+  });
 }
 
-// Long-pattern routing, once per routed batch (block 0 of the list kernel): end the mode
-// after a batch without long patterns (lr.used_d clear), else re-arm used_d
-__device__ __forceinline__ void long_route_end(const LongRoute& lr) {
-  if (lr.used_d && blockIdx.x == 0 && threadIdx.x == 0) {
-    if (__hip_atomic_load(lr.used_d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-      __hip_atomic_store(lr.used_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(lr.seen_d, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(lr.seen_h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
-// The patterns k_count_long listed: the general search (count_pattern), the node table
-// staged in LDS by the blocks that have work; a fixed grid striding over the list, whose
-// length is read on the device.
-// With routing (lr set, long-pattern mode): block 0 also ends the mode after a batch
-// without long patterns (lr.used_d clear) and re-arms used_d otherwise.
-// kBytes: k_count_long's measurement twin (the general search's bytes into co.out).
+// The patterns k_count_long listed (LongList list2 / cnt2): the general search
+// (count_pattern), the node table staged in LDS by the blocks that have work; block b walks
+// regions b, b + grid, ...  kBytes: k_count_long's measurement twin (the general search's
+// bytes into co.out).
 template <int W, bool kBytes = false>
 __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t* __restrict__ pats,
-                                                     const uint64_t* __restrict__ offs, CountOut co,
-                                                     uint64_t fixed_m, const uint64_t* __restrict__ list,
-                                                     const unsigned long long* __restrict__ nlist,
-                                                     LongRoute lr) {
+                                                     const uint64_t* __restrict__ offs, uint64_t npat,
+                                                     CountOut co, uint64_t fixed_m, LongList ll) {
   __shared__ NodeTable T;
-  long_route_end(lr);
-  const uint64_t nl = *nlist;
-  if ((uint64_t)blockIdx.x * kBlk >= nl) return;  // uniform over the block
-  load_table(T, ix.table);
-  __syncthreads();
-  for (uint64_t i = blockIdx.x * (uint64_t)kBlk + threadIdx.x; i < nl; i += (uint64_t)gridDim.x * kBlk) {
-    const uint64_t q = list[i];
-    const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
-    if constexpr (kBytes) {
-      uint64_t by = 0;
-      (void)count_pattern<OccE>(ix, T, pats + o0, m, &by);
-      static_cast<uint64_t*>(co.out)[q] = by;
-    } else {
-      store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
+  bool staged = false;
+  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
+  for (uint64_t r = blockIdx.x; r < regions; r += gridDim.x) {
+    const uint32_t c = ll.cnt2[r];  // uniform over the block
+    if (!c) continue;
+    if (!staged) {
+      load_table(T, ix.table);
+      __syncthreads();
+      staged = true;
+    }
+    for (uint32_t i = threadIdx.x; i < c; i += kBlk) {
+      const uint64_t q = r * kLongRegion + ll.list2[r * kLongRegion + i];
+      const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
+      if constexpr (kBytes) {
+        uint64_t by = 0;
+        (void)count_pattern<OccE>(ix, T, pats + o0, m, &by);
+        static_cast<uint64_t*>(co.out)[q] = by;
+      } else {
+        store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
+      }
     }
   }
 }
 
 // The patterns k_locate_long listed: locate's general search (locate_search), its count
-// and record for k_locate_emit, the count added to the pattern's tile; a fixed grid
-// striding over the list, as k_count_list (which also ends the routing mode here).
+// and record for k_locate_emit, the count added to the pattern's tile; as k_count_list.
 __global__ __launch_bounds__(kBlk) void k_locate_list(DevIndex ix, const uint8_t* __restrict__ pats,
-                                                      const uint64_t* __restrict__ offs, uint64_t limit,
-                                                      OnePass op, const uint64_t* __restrict__ list,
-                                                      const unsigned long long* __restrict__ nlist,
-                                                      LongRoute lr) {
+                                                      const uint64_t* __restrict__ offs, uint64_t npat,
+                                                      uint64_t limit, OnePass op, LongList ll) {
   __shared__ NodeTable T;
-  long_route_end(lr);
-  const uint64_t nl = *nlist;
-  if ((uint64_t)blockIdx.x * kBlk >= nl) return;  // uniform over the block
-  load_table(T, ix.table);
-  __syncthreads();
-  for (uint64_t i = blockIdx.x * (uint64_t)kBlk + threadIdx.x; i < nl; i += (uint64_t)gridDim.x * kBlk) {
-    const uint64_t q = list[i];
-    const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
-    uint64_t r = 0;
-    const uint64_t c = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, r) : 0;
-    const uint64_t kc = c < limit ? c : limit;  // fm_index.cpp:125
-    op.cnt[q] = (uint32_t)kc;
-    op.rec[q] = r;
-    if (kc) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), kc);
+  bool staged = false;
+  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
+  for (uint64_t r = blockIdx.x; r < regions; r += gridDim.x) {
+    const uint32_t c = ll.cnt2[r];  // uniform over the block
+    if (!c) continue;
+    if (!staged) {
+      load_table(T, ix.table);
+      __syncthreads();
+      staged = true;
+    }
+    for (uint32_t i = threadIdx.x; i < c; i += kBlk) {
+      const uint64_t q = r * kLongRegion + ll.list2[r * kLongRegion + i];
+      const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+      uint64_t rr = 0;
+      const uint64_t cc = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, rr) : 0;
+      const uint64_t kc = cc < limit ? cc : limit;  // fm_index.cpp:125
+      op.cnt[q] = (uint32_t)kc;
+      op.rec[q] = rr;
+      if (kc) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), kc);
+    }
   }
 }
 
@@ -2499,6 +2574,54 @@ __global__ __launch_bounds__(kBlk) void k_count_bytes(DevIndex ix, const uint8_t
   uint64_t bytes = 0;
   if (m && ix.n) (void)count_pattern<E>(ix, T, pats + o0, m, &bytes);
   out[q] = bytes;
+}
+
+// Measurement twin of the one-call locate's locate-record stage (bench.py's locate roofline):
+// hit[q] = 1 when the locate record of pattern q answers it in one read — the (A)/(B0) logic
+// of k_count_ctx<..., kOne> for one pattern: no matching row, or one whose SA value the
+// record holds — else 0 (the context record, its window and SA entries follow).
+__global__ __launch_bounds__(kBlk) void k_locrec_hits(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                      const uint64_t* __restrict__ offs, uint64_t npat,
+                                                      uint8_t* __restrict__ hit) {
+  __shared__ uint16_t cmap[256];
+  if (threadIdx.x < 256)
+    cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
+  __syncthreads();
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q >= npat) return;
+  const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+  const uint32_t K = ix.ptab_k;
+  uint8_t h = 0;
+  if (ix.lrec && ix.lctx && K && m >= K + 1 && m <= K + 1 + kLocRecQ) {
+    const uint32_t kk = (uint32_t)m - K;
+    uint32_t tt = 0, ww = 0, dl = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < (uint32_t)m; ++i) {
+      const uint32_t b = pats[o0 + i];
+      if (i >= kk) {
+        const uint32_t d = cmap[b] & 0xFFu;
+        ok &= d != kNoCode;
+        tt = tt * ix.ptab_sigma + d;
+      } else {
+        const uint32_t d = cmap[b] >> 8;
+        ok &= d != kNoCode;
+        ww |= (d & 3u) << (2 * (kk - 1 - i));
+        if (i + 1 == kk) {
+          dl = cmap[b] & 0xFFu;
+          ok &= dl != kNoCode;
+        }
+      }
+    }
+    if (ok) {
+      const uint4 a = static_cast<const uint4*>(ix.lrec)[(dl << (2 * K)) + tt];
+      const uint32_t c = a.w >> 24, j2 = kk - 1, mask = (1u << (2 * j2)) - 1u;
+      uint32_t mm = 0;
+      for (uint32_t i = 0; i < kLocRecRows; ++i)
+        mm |= (uint32_t)(i < c && ((a.w >> (8 * i)) & mask) == (ww >> 2)) << i;
+      h = c != kLocRecNone && !(mm & (mm - 1u));
+    }
+  }
+  hit[q] = h;
 }
 
 template <class E>
@@ -3266,10 +3389,42 @@ __global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict
       else
         hi |= (c & 0x3FFu) << (10 * (i - 6));
     }
-    if (w > kRec16Ctx || esc)
-      rec[t] = make_uint4(e.x, kRec16Wide, w, 0u);
-    else
+    if (w <= kRec16Ctx && !esc) {
       rec[t] = make_uint4(e.x, (uint32_t)lo | w, (uint32_t)(lo >> 32), hi);
+      continue;
+    }
+    // a wide range: its two most frequent contexts (Misra-Gries with two counters finds every
+    // context above a third of the rows; a second pass counts the candidates exactly)
+    uint32_t y = kRec16Wide, w3 = 0;
+    if (!esc && w > kRec16Ctx && w <= kRec16MajScan) {
+      uint32_t ca = 0, cb = 0, na = 0, nb = 0;
+      for (uint32_t i = 0; i < w && !esc; ++i) {
+        const uint32_t c = lctx[e.x + i];
+        esc |= (c & kCtxEsc) != 0;
+        const uint32_t v = c & 0x3FFu;
+        if (na && v == ca) ++na;
+        else if (nb && v == cb) ++nb;
+        else if (!na) ca = v, na = 1;
+        else if (!nb) cb = v, nb = 1;
+        else --na, --nb;
+      }
+      uint32_t xa = 0, xb = 0;
+      for (uint32_t i = 0; i < w && !esc; ++i) {
+        const uint32_t v = lctx[e.x + i] & 0x3FFu;
+        xa += na && v == ca;
+        xb += nb && v == cb;
+      }
+      if (!esc && na && xb > xa) {  // A the more frequent
+        const uint32_t tc = ca; ca = cb; cb = tc;
+        const uint32_t tx = xa; xa = xb; xb = tx;
+      }
+      if (!esc && xa && xa <= 0xFFFFu && xb <= 0xFFFFu) {
+        y |= kRec16Maj | (ca << 6) | (xb ? cb << 16 : 0u);
+        if (xa + xb == w) y |= kRec16MajAll;
+        w3 = xa | (xb << 16);
+      }
+    }
+    rec[t] = make_uint4(e.x, y, w, w3);
   }
 }
 
@@ -3504,6 +3659,95 @@ cs_status derive_packed_text(cs_fm_index* h, hipStream_t st) {
   return CS_OK;
 }
 
+// Locate records (fm_device.hpp kLocRec*) of the (k+1)-mers c.x, from the k-mer x's context
+// record and left contexts: a lane per k-mer x.  The rows of c.x are the rows r of x whose
+// chain starts with c (BWT[r] = c), in order (LF keeps the order of equal symbols); each
+// gives SA[r] - 1 (mod n) and its chain shifted by one symbol.  o2d: the table digit of
+// occurrence code o in byte o.  A range wider than kLocRecScan rows, or one holding an
+// escaped context, makes all four children kLocRecNone (their locates read the context
+// record instead); a child with more than kLocRecRows rows is kLocRecNone too.
+constexpr uint32_t kLocRecScan = 64;
+__global__ __launch_bounds__(kBlk) void k_fill_locrec(const uint4* __restrict__ rec, uint64_t entries,
+                                                      const uint16_t* __restrict__ lctx,
+                                                      const uint32_t* __restrict__ sa, uint64_t n,
+                                                      uint32_t o2d, uint4* __restrict__ out) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
+    const uint4 a = rec[t];
+    const uint32_t wc = a.y & 15u;
+    const bool wide = wc == kRec16Wide;
+    const uint64_t sp = a.x;
+    const uint32_t w = wide ? a.z : wc;
+    bool none = wide && (a.z == kRec16NoRange || a.z > kLocRecScan);
+    uint32_t ctx10[kRec16Ctx];  // inline record: the rows' 5-symbol chains
+    if (!wide) {
+      uint32_t dw[5];
+      rec16_contexts(a.y, a.z, a.w, dw);
+#pragma unroll
+      for (uint32_t i = 0; i < kRec16Ctx; ++i) ctx10[i] = (dw[i >> 1] >> (16 * (i & 1))) & 0x3FFu;
+    }
+    if (wide && !none)
+      for (uint32_t i = 0; i < w; ++i) none |= (lctx[sp + i] & kCtxEsc) != 0;
+#pragma unroll
+    for (uint32_t d = 0; d < 4; ++d) {
+      uint32_t c = 0, cx = 0, sv[kLocRecRows] = {0u, 0u, 0u};
+      for (uint32_t i = 0; i < w && !none; ++i) {
+        const uint32_t e = wide ? lctx[sp + i] : ctx10[i < kRec16Ctx ? i : 0];
+        if (((o2d >> (8 * (e & 3u))) & 0xFFu) != d) continue;
+        if (c < kLocRecRows) {
+          const uint32_t v = sa[sp + i];
+          const uint32_t v1 = v ? v - 1u : (uint32_t)(n - 1);
+#pragma unroll
+          for (uint32_t r = 0; r < kLocRecRows; ++r)
+            if (r == c) sv[r] = v1;
+          cx |= ((e >> 2) & 0xFFu) << (8 * c);
+        }
+        ++c;
+      }
+      out[(uint64_t)d * entries + t] = none || c > kLocRecRows
+                                           ? make_uint4(0u, 0u, 0u, kLocRecNone << 24)
+                                           : make_uint4(sv[0], sv[1], sv[2], cx | (c << 24));
+    }
+  }
+}
+
+// Build the locate records when the index can use them: narrow lf_exact occurrence-line
+// indexes with 16-B context records over a 4-symbol table of k <= 15, the left contexts and
+// the full suffix array (C4: k = 15 -> 4^16 records, 69 GB), HBM allowing (an eighth of the
+// device stays free; within CS_FM_HBM_BUDGET).  CS_FM_LOC_RECORDS=0 (read at build / open /
+// import) leaves them out.  Derived from the other parts, not saved.
+cs_status derive_locate_records(cs_fm_index* h, hipStream_t st) {
+  if (h->d_lrec || h->ptab_rec != 2 || !h->d_ptab || !h->d_sa || !h->lf_exact || h->wide ||
+      !h->d_lctx || h->lctx_eb != 2 || h->line_fmt != kFmtOcc || h->ptab_sigma != 4 ||
+      h->ptab_k < 1 || h->ptab_k + 1 > 16 || h->n >= (1ull << 32))
+    return CS_OK;
+  if (const char* e = std::getenv("CS_FM_LOC_RECORDS"))
+    if (std::atoi(e) == 0) return CS_OK;
+  // the table digit of each occurrence code; every code must have one
+  uint32_t o2d = 0xFFFFFFFFu;
+  for (int c = 0; c < 256; ++c) {
+    const uint32_t oc = h->h_table.occ_code[c], d = h->h_table.code[c];
+    if (oc < 4 && d < 4) o2d = (o2d & ~(0xFFu << (8 * oc))) | (d << (8 * oc));
+  }
+  for (int oc = 0; oc < 4; ++oc)
+    if (((o2d >> (8 * oc)) & 0xFFu) >= 4) return CS_OK;
+  const uint64_t entries = h->ptab_entries(), bytes = entries * 4 * 16;
+  if (!hbm_room(h, bytes)) return CS_OK;
+  void* p = nullptr;
+  FMX_HIP(hipMalloc(&p, bytes));
+  k_fill_locrec<<<grid_for(entries, kBlk, 1u << 20), kBlk, 0, st>>>(
+      static_cast<const uint4*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
+      static_cast<const uint32_t*>(h->d_sa), h->n, o2d, static_cast<uint4*>(p));
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return hip_fail(e, "locate records");
+  }
+  h->d_lrec = p;
+  return CS_OK;
+}
+
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
                          const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st) {
   if (!k) return CS_OK;
@@ -3538,6 +3782,7 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
   if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA))
     d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr;
   if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
+  if (flags & (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS | CS_Q_NO_FULL_SA | CS_Q_NO_LOC_RECORDS)) d.lrec = nullptr;
   return d;
 }
 
@@ -3569,77 +3814,95 @@ bool qctx_staged() {
 // k_count_long over the batch (skip_short: only its long patterns, as k_count_ctx's kSkipLong),
 // then k_count_list over the patterns it listed; byte_text: the byte text even when the
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
+// The call's long-pattern lists (LongList): region lists of the staged kernel (list / cnt,
+// unless `direct`) and of k_count_long / k_locate_long for the general search (list2 / cnt2),
+// u16 offsets inside the regions; in one stream-ordered allocation.  Direct launches (every
+// pattern to the long kernel, no staged kernel before it) zero cnt2 here; otherwise the
+// staged kernel does, block by block.
+struct LongBufs {
+  StreamBuf buf;
+  LongList ll;
+  cs_status alloc(uint64_t npat, bool direct, hipStream_t st) {
+    const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion, slots = regions * kLongRegion;
+    const uint64_t lists = (direct ? 1 : 2) * slots * 2, cnts = (direct ? 1 : 2) * regions * 4;
+    FMX_HIP(buf.alloc(lists + cnts, st));
+    uint8_t* p = buf.as<uint8_t>();
+    ll.list2 = reinterpret_cast<uint16_t*>(p);
+    ll.cnt2 = reinterpret_cast<uint32_t*>(p + lists);
+    if (!direct) {
+      ll.list = ll.list2 + slots;
+      ll.cnt = ll.cnt2 + regions;
+    } else {
+      FMX_HIP(hipMemsetAsync(ll.cnt2, 0, regions * 4, st));
+    }
+    return CS_OK;
+  }
+};
+
+// blocks of the long-pattern kernels walking the lists (long_patterns): two rounds of the
+// blocks resident at 5 waves per SIMD (256 CUs x 5 blocks of 4 waves)
+constexpr unsigned kLongListGrid = 2560;
+
+// k_count_long over the batch (from_list: the staged kernel's lists in ll), then k_count_list
+// over what it could not finish.  skip_short (twin): every pattern read, only the long ones
+// searched.
 template <bool kBytes>
 cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
                               uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
-                              bool skip_short, const LongRoute& lr, bool byte_text) {
-  const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
-  StreamBuf lb;
-  FMX_HIP(lb.alloc(npat * 8 + 8, st));
-  unsigned long long* nl = reinterpret_cast<unsigned long long*>(lb.as<uint64_t>() + npat);
-  FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
+                              const LongList* routed, bool skip_short, bool byte_text) {
+  LongBufs own;
+  LongList ll;
+  if (routed) {
+    ll = *routed;
+  } else {
+    cs_status s = own.alloc(npat, true, st);
+    if (s != CS_OK) return s;
+    ll = own.ll;
+  }
+  const bool from_list = routed != nullptr;
+  const unsigned g = from_list ? std::min(grid_for(npat, kLongRegion, 0xFFFFFFFFu), kLongListGrid)
+                               : grid_for(npat, kBlk, 0xFFFFFFFFu);
   // tuning hook CS_FM_LONG_V16 (read per call): 0 = 8-B pattern / window loads, 3 = 16-B
   // vectors for the pattern's packed part and the window (the default: C4 150-mers 1.87 ->
   // 1.55 ms, 64-mers 1.25 -> 1.16-1.21, profiles/r03/long_probe_v16.json), 1 / 2 = partial forms
   const char* ev = std::getenv("CS_FM_LONG_V16");
   const int v16 = ev ? std::atoi(ev) : 3;
   if (ix.ptext && !byte_text && v16 == 1)
-    k_count_long<0, true, kBytes, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
-                                                         lb.as<uint64_t>(), nl, skip_short, lr);
+    k_count_long<0, true, kBytes, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
+                                                         skip_short);
   else if (ix.ptext && !byte_text && v16 == 2)
-    k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
-                                                         lb.as<uint64_t>(), nl, skip_short, lr);
+    k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
+                                                         skip_short);
   else if (ix.ptext && !byte_text && v16 == 3)
-    k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m,
-                                                         lb.as<uint64_t>(), nl, skip_short, lr);
+    k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
+                                                         skip_short);
   else if (ix.ptext && !byte_text)
-    k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(),
-                                                      nl, skip_short, lr);
+    k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
+                                                      skip_short);
   else
-    k_count_long<0, false, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, lb.as<uint64_t>(),
-                                                       nl, skip_short, lr);
+    k_count_long<0, false, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
+                                                       skip_short);
   FMX_HIP(hipGetLastError());
-  k_count_list<0, kBytes><<<std::min(g, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, co, fixed_m,
-                                                               lb.as<uint64_t>(), nl, lr);
+  k_count_list<0, kBytes><<<std::min(grid_for(npat, kLongRegion, 0xFFFFFFFFu), 1024u), kBlk, 0, st>>>(
+      ix, d_pats, d_offs, npat, co, fixed_m, ll);
   FMX_HIP(hipGetLastError());
   return CS_OK;
 }
 cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
                             uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
-                            bool skip_short, const LongRoute& lr, bool byte_text = false) {
-  return launch_count_long_t<false>(ix, d_pats, d_offs, npat, co, st, fixed_m, skip_short, lr, byte_text);
+                            const LongList* routed, bool byte_text = false) {
+  return launch_count_long_t<false>(ix, d_pats, d_offs, npat, co, st, fixed_m, routed, false, byte_text);
 }
 
-// The handle's routing words (LongRoute), allocated on first use; all null when the index
-// cannot route (k_count_long needs occurrence lines, the full SA and the text) or the
-// tuning hook CS_FM_LONG_ROUTE=0 (read per call) turns routing off.
-LongRoute long_route(const cs_fm_index* h, const DevIndex& ix) {
-  if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return LongRoute{};
+// Whether device batches are routed (the staged kernel lists its long patterns for
+// k_count_long / k_locate_long in the same call): indexes k_count_long serves (occurrence
+// lines, the full SA and the text); the tuning hook CS_FM_LONG_ROUTE=0 (read per call) keeps
+// every pattern in the staged kernel (round 2's path).
+bool can_route(const cs_fm_index* h, const DevIndex& ix) {
+  if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return false;
   if (const char* e = std::getenv("CS_FM_LONG_ROUTE"))
-    if (std::atoi(e) == 0) return LongRoute{};
-  std::lock_guard<std::mutex> lk(h->route_mu);
-  if (!h->route_h) {
-    void *hp = nullptr, *dp = nullptr;
-    if (hipHostMalloc(&hp, 64, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
-      (void)hipGetLastError();
-      return LongRoute{};
-    }
-    if (hipMalloc(&dp, 64) != hipSuccess || hipMemset(dp, 0, 64) != hipSuccess) {
-      (void)hipGetLastError();
-      (void)hipHostFree(hp);
-      if (dp) (void)hipFree(dp);
-      return LongRoute{};
-    }
-    std::memset(hp, 0, 64);
-    h->route_h = static_cast<uint32_t*>(hp);
-    h->route_d = static_cast<uint32_t*>(dp);
-  }
-  void* dev_h = nullptr;
-  if (hipHostGetDevicePointer(&dev_h, h->route_h, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    return LongRoute{};
-  }
-  return LongRoute{static_cast<uint32_t*>(dev_h), h->route_d, h->route_d + 1};
+    if (std::atoi(e) == 0) return false;
+  return true;
 }
 
 // the staged kernel at count width W: table entries (context records) of U patterns per
@@ -3655,7 +3918,6 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   }();
   const bool lo = h->line_fmt == kFmtLOcc;
   const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
-  const LongRoute route = packed || lo ? LongRoute{} : long_route(h, ix);
   if (packed && lo)
     k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                 nullptr, fixed_m);
@@ -3677,17 +3939,19 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   else if (W == 8 && count_nobar())
     k_count_ctx<OccE, 2, false, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                       nullptr, fixed_m);
-  else if (d_offs && route.seen_h && *reinterpret_cast<volatile uint32_t*>(h->route_h)) {
-    // long-pattern mode (a recent batch held patterns of kFastM characters or more): the staged
-    // kernel counts the short ones, k_count_long the long ones
+  else if (d_offs && can_route(h, ix)) {
+    // long-pattern routing inside the call: the staged kernel counts the short patterns and
+    // lists the long ones, k_count_long (and k_count_list) take them from its lists
+    LongBufs lb;
+    cs_status s = lb.alloc(npat, false, st);
+    if (s != CS_OK) return s;
     k_count_ctx<OccE, 2, false, false, W, false, false, true><<<g2, kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
+        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
     FMX_HIP(hipGetLastError());
-    return launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, true, route);
+    return launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, &lb.ll);
   } else
     k_count_ctx<OccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                nullptr, fixed_m, OnePass{},
-                                                                d_offs ? route : LongRoute{});
+                                                                nullptr, fixed_m);
   FMX_HIP(hipGetLastError());
   return CS_OK;
 }
@@ -3723,7 +3987,7 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
       k_count<OccE, false, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs,
                                                                                     npat, co, fixed_m);
     } else {
-      cs_status r = launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, false, LongRoute{},
+      cs_status r = launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, nullptr,
                                       ek && std::atoi(ek) == 2);
       if (r != CS_OK) return r;
     }
@@ -3768,11 +4032,21 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
   const bool old = ek && std::atoi(ek) == 0;
   if (!(lk && (flags & CS_Q_LONG) && !old))
     FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), ix, d_pats, d_offs, npat, d_out);
-  if (lk && !old && ((flags & CS_Q_LONG) || long_route(h, ix).seen_h)) {
+  // (a routed call's long patterns: can_route; ADVICE r03: the twin now follows the call)
+  if (lk && !old && ((flags & CS_Q_LONG) || can_route(h, ix))) {
     const CountOut co{d_out, nullptr, nullptr, 0, 8};
-    return launch_count_long_t<true>(ix, d_pats, d_offs, npat, co, st, 0, !(flags & CS_Q_LONG), LongRoute{},
+    return launch_count_long_t<true>(ix, d_pats, d_offs, npat, co, st, 0, nullptr, !(flags & CS_Q_LONG),
                                      ek && std::atoi(ek) == 2);
   }
+  return CS_OK;
+}
+
+cs_status launch_locrec_hits(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                             uint64_t npat, uint8_t* d_hit, hipStream_t st) {
+  if (!npat) return CS_OK;
+  const DevIndex ix = h->dev();
+  k_locrec_hits<<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, d_hit);
+  FMX_HIP(hipGetLastError());
   return CS_OK;
 }
 
@@ -3788,7 +4062,8 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   *done = false;
   if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
     if (std::atoi(e) == 0) return CS_OK;
-  const DevIndex ix = h->dev();
+  DevIndex ix = h->dev();
+  if (flags & CS_Q_NO_LOC_RECORDS) ix.lrec = nullptr;
   // positions from the full SA (narrow), or by the short walk over walk lines with
   // text-position marks (OnePass above); CS_FM_LOCATE_ONEPASS=1 keeps the walk indexes on
   // the two phases (test hook: CS_FM_LOCATE_ONEPASS=2 = the full SA only)
@@ -3816,19 +4091,16 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // a pattern has at most one
   const uint64_t wide_cap = std::min<uint64_t>(cap / (kLocSmall + 1) + 1, npat);
   // long patterns (full-SA indexes with the 2-bit text): k_locate_long takes every pattern
-  // of a CS_Q_LONG batch (host batches of long patterns pass it), and under long-pattern
-  // routing (the handle's flag, raised by a staged kernel that met long patterns — count's
-  // or this one's) the staged kernel leaves the long ones to it
+  // of a CS_Q_LONG batch (host batches of long patterns pass it) and, routed (can_route),
+  // the long patterns the staged kernel lists in the same call
   const bool lk = kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
-  const LongRoute route = lk ? long_route(h, ix) : LongRoute{};
   const bool long_only = lk && (flags & CS_Q_LONG);
-  const bool routed = lk && !long_only && route.seen_h && *reinterpret_cast<volatile uint32_t*>(h->route_h);
+  const bool routed = lk && !long_only && can_route(h, ix);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
   StreamBuf ws;
   const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
   const uint64_t lo = (npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull;
-  const uint64_t lb = long_only || routed ? npat * 8 + 8 : 0;  // k_locate_long's list
-  FMX_HIP(ws.alloc(lo + lb, st));
+  FMX_HIP(ws.alloc(lo, st));
   OnePass op;
   op.rec = ws.as<uint64_t>();
   op.tiles = op.rec + npat;
@@ -3844,28 +4116,27 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
   if (long_only || routed) {
-    uint64_t* list = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(ws.p) + lo);
-    unsigned long long* nl = reinterpret_cast<unsigned long long*>(list + npat);
-    FMX_HIP(hipMemsetAsync(nl, 0, 8, st));
+    LongBufs lb;
+    cs_status ls = lb.alloc(npat, long_only, st);
+    if (ls != CS_OK) return ls;
     if (long_only)
       FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8, st));
     else
       k_count_ctx<OccE, U, true, false, 8, false, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
-          ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+          ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
     FMX_HIP(hipGetLastError());
-    const unsigned g1 = grid_for(npat, kBlk, 0xFFFFFFFFu);
-    const LongRoute lr = routed ? route : LongRoute{};
+    const unsigned g1 = routed ? std::min((unsigned)tiles, kLongListGrid) : grid_for(npat, kBlk, 0xFFFFFFFFu);
     // tuning hook CS_FM_LONG_V16 (k_count_long's): 0 = 8-B pattern / window loads
     const char* ev = std::getenv("CS_FM_LONG_V16");
     if (ev && std::atoi(ev) == 0)
-      k_locate_long<0><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, list, nl, routed, lr);
+      k_locate_long<0><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll, routed);
     else
-      k_locate_long<3><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, list, nl, routed, lr);
+      k_locate_long<3><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll, routed);
     FMX_HIP(hipGetLastError());
-    k_locate_list<<<std::min(g1, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, limit, op, list, nl, lr);
+    k_locate_list<<<std::min((unsigned)tiles, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
   } else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, route);
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else if (kpos == 1)
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);

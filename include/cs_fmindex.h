@@ -90,6 +90,10 @@ typedef struct cs_fm_info {
   uint64_t packed_text_bytes; /* 2-bit copy of the text (occurrence lines, lf_exact, full SA and
                               text in HBM) that long patterns are verified against; 0 = none.
                               Derived from the text on build / open / import, not saved. */
+  uint64_t locate_record_bytes; /* locate records (one-call locate: the SA values of the
+                              rows of every (k+1)-mer with at most 3 rows, beside their
+                              contexts, so a 20-mer's position is one read); 0 = none.
+                              Derived on build / open / import, not saved. */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);
@@ -146,6 +150,13 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
 cs_status cs_fm_open_csidx(const char* path, int device, cs_fm_index** out);
 cs_status cs_fm_save_csidx(const cs_fm_index* h, const char* path);
 cs_status cs_csidx_check(const char* path, uint64_t* n, uint32_t* ssa_stride, int* has_text);
+/* Write a CSIDX file from host index arrays, on the host (no device): the reference's
+ * members bwt_ (n bytes), ssa_ (ceil(n / ssa_stride) u32 samples) and, optional (NULL),
+ * text_ — the file IndexWriter would write for them (serialization.cpp:64-147: header,
+ * text, BWT, C_ = the BWT's cumulative histogram, SSA, footer; 8-B aligned sections).
+ * cs_fm_save_csidx writes through the same writer. */
+cs_status cs_csidx_write(const char* path, const uint8_t* bwt, uint64_t n, const uint32_t* ssa,
+                         uint64_t nsamples, uint32_t ssa_stride, const uint8_t* text);
 /* Writes the index (HBM images of every structure, plus the text when kept) to dir. */
 cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir);
 /* The index as a device image, for replication across GPUs (e.g. a broadcast over
@@ -261,8 +272,11 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
  *                      keep the full suffix array and the text; implied by a fixed-length
  *                      batch with m > 31 and by a host batch, cs_fm_count_batch /
  *                      cs_fm_locate_batch, whose patterns are all longer than 31).  Without
- *                      it, device batches holding long patterns are routed to the same
- *                      kernels from the next batch on (the handle's routing flag).
+ *                      it, the long patterns of a device batch are routed to the same
+ *                      kernels inside the call (the 20-mer kernel lists them in the call's
+ *                      own buffer; the handle holds no routing state).
+ *   CS_Q_NO_LOC_RECORDS the one-call locate without the locate records (the context
+ *                      record, then the matching row's SA entry: two dependent reads)
  *                      Results never change. */
 #define CS_Q_NO_PREFIX 1u
 #define CS_Q_NO_CONTEXTS 2u
@@ -270,6 +284,7 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
 #define CS_Q_NO_WALK_LINES 8u
 #define CS_Q_NO_VERIFY 16u
 #define CS_Q_LONG 32u
+#define CS_Q_NO_LOC_RECORDS 64u
 
 /* Where a batch count writes.  width 8: uint64 counts (the reference's return type,
  * fm_index.hpp:26).  width 4: uint32, exact while n < 2^32 (CS_ERR_INVALID otherwise).
@@ -308,6 +323,12 @@ cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
 cs_status cs_fm_count_bytes_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
                                       const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                       uint32_t flags, void* stream);
+/* Measurement twin of the one-call locate's locate records (bench.py's locate roofline):
+ * d_hit[q] = 1 when the index's locate records (cs_fm_info.locate_record_bytes) answer
+ * pattern q in one read, else 0. */
+cs_status cs_fm_locate_record_hits_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                          const uint64_t* d_offs, uint64_t npat, uint8_t* d_hit,
+                                          void* stream);
 /* locate phase 1: backward search; d_sp[q] = the pattern's record for phase 2 (the
  * first row of its range, or an encoded window of matching rows when the search
  * finished over the left contexts — treat it as opaque), d_out_offs = exclusive scan

@@ -458,6 +458,15 @@ def ref_lib():
         R.ref_locate_batch.restype = None
         R.ref_locate_batch.argtypes = [C.c_void_p, _u8p, _u64p, C.c_uint64, C.c_uint64, C.c_int,
                                        C.c_uint64, C.POINTER(C.c_int64), _u64p, _u64p]
+        if hasattr(R, "ref_csidx_open"):  # serialization.cpp in the shim (round 4)
+            R.ref_csidx_open.restype = C.c_void_p
+            R.ref_csidx_open.argtypes = [C.c_char_p, C.c_char_p, C.c_uint64]
+            R.ref_csidx_close.restype = None
+            R.ref_csidx_close.argtypes = [C.c_void_p]
+            R.ref_csidx_header.restype = None
+            R.ref_csidx_header.argtypes = [C.c_void_p, _u64p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+            R.ref_csidx_section.restype = C.c_void_p
+            R.ref_csidx_section.argtypes = [C.c_void_p, C.c_int, _u64p, C.POINTER(C.c_uint32)]
         _ref = R
     return _ref
 
@@ -518,3 +527,35 @@ class RefCountIndex:
         if R is not None and getattr(self, "_h", None):
             R.ref_free(self._h)
             self._h = None
+
+
+def ref_read_csidx(path):
+    """A CSIDX file through the reference's own reader (cs::IndexReader, src/serialization/
+    serialization.cpp:153-335, compiled into oracle/_ref/libcs_ref.so): {"text_len", "flags",
+    "version", "text", "bwt", "C", "ssa", "stride"} as its getters return them (None for an
+    absent section), or RuntimeError with the reader's exception text."""
+    R = ref_lib()
+    if R is None or not hasattr(R, "ref_csidx_open"):
+        raise FileNotFoundError(REF_LIB)
+    err = C.create_string_buffer(256)
+    h = R.ref_csidx_open(path.encode(), err, 256)
+    if not h:
+        raise RuntimeError(err.value.decode())
+    try:
+        n, fl, ver = C.c_uint64(), C.c_uint32(), C.c_uint32()
+        R.ref_csidx_header(h, C.byref(n), C.byref(fl), C.byref(ver))
+        out = {"text_len": n.value, "flags": fl.value, "version": ver.value}
+        for which, key, dt in ((0, "text", np.uint8), (1, "bwt", np.uint8), (2, "C", np.uint32),
+                               (3, "ssa", np.uint32)):
+            k, st = C.c_uint64(), C.c_uint32()
+            ptr = R.ref_csidx_section(h, which, C.byref(k), C.byref(st))
+            if not ptr:
+                out[key] = None
+                continue
+            nb = k.value * np.dtype(dt).itemsize
+            out[key] = np.frombuffer(C.string_at(ptr, nb), dt).copy() if nb else np.zeros(0, dt)
+            if which == 3:
+                out["stride"] = st.value
+        return out
+    finally:
+        R.ref_csidx_close(h)

@@ -24,6 +24,7 @@
 #include "api/fm_index.hpp"
 #undef private
 #include "core/bwt.hpp"
+#include "serialization/serialization.hpp"
 
 extern "C" {
 
@@ -171,6 +172,42 @@ uint64_t ref_wt_rank(void* h, uint8_t c, uint64_t i) {
 
 uint64_t ref_level_rank1(void* h, int level, uint64_t i) {
   return static_cast<cs::FMIndex*>(h)->wavelet_.levels_[level].rank1(i);
+}
+
+// CSIDX through the reference's own mmap reader (src/serialization/serialization.cpp:153-335):
+// the file's sections exactly as cs::IndexReader returns them (pointers into its mapping).
+// Returns a handle, or nullptr with the exception's text in err.
+void* ref_csidx_open(const char* path, char* err, uint64_t errcap) {
+  try {
+    return new cs::IndexReader(path);
+  } catch (const std::exception& e) {
+    if (err && errcap) {
+      std::strncpy(err, e.what(), errcap - 1);
+      err[errcap - 1] = 0;
+    }
+    return nullptr;
+  }
+}
+void ref_csidx_close(void* h) { delete static_cast<cs::IndexReader*>(h); }
+// header fields: text_len, flags, version
+void ref_csidx_header(void* h, uint64_t* text_len, uint32_t* flags, uint32_t* version) {
+  const cs::IndexHeader* hd = static_cast<cs::IndexReader*>(h)->header();
+  *text_len = hd->text_len;
+  *flags = hd->flags;
+  *version = hd->version;
+}
+// section `which` (0 text, 1 bwt, 2 C, 3 ssa): its element count and data pointer
+// (null when absent); stride for the SSA
+const void* ref_csidx_section(void* h, int which, uint64_t* count, uint32_t* stride) {
+  auto* r = static_cast<cs::IndexReader*>(h);
+  size_t k = 0;
+  const void* p = nullptr;
+  if (which == 0) p = r->get_text(&k);
+  else if (which == 1) p = r->get_bwt(&k);
+  else if (which == 2) p = r->get_c_array(&k);
+  else p = r->get_ssa(&k, stride);
+  *count = p ? k : 0;
+  return p;
 }
 
 }  // extern "C"

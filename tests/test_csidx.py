@@ -3,12 +3,14 @@ writer serialization.cpp:26-147, reader :153-335), read and written over the C A
 (csrc/fm_csidx.cpp).
 
 The reference's writer never finishes a file (IndexWriter::align_to does not advance,
-serialization.cpp:44-54) and FMIndex never calls it, so no reference-written CSIDX exists:
-the files here are written by `write_csidx` below from the documented layout, holding the
-oracle's BWT / SSA / C (the members build_from_text leaves, fm_index.cpp:36-66).  Parity for
-the format itself is therefore anchored on the header declaration, not on a reference
-file ("parity unpinned" for the byte layout beyond it); the answers of an opened index are
-pinned by the oracle as everywhere else.
+serialization.cpp:44-54) and FMIndex never calls it, so no reference-written CSIDX exists.
+The layout is pinned against the reference's own READER instead (round 4): files written by
+cs_csidx_write (the host writer cs_fm_save_csidx uses too) from the oracle's members (the
+ones build_from_text leaves, fm_index.cpp:36-66) are opened by the genuine cs::IndexReader
+(serialization.cpp:153-335, compiled into oracle/_ref/libcs_ref.so by `make -C oracle ref`),
+whose getters must return exactly those members; the GPU test then checks that a device
+index's save_csidx writes the same bytes.  Files written by `write_csidx` below (the
+documented layout in Python) exercise the reader's validation.
 """
 import os
 import struct
@@ -89,6 +91,61 @@ TEXTS = {
 def _arrays(t, stride=16):
     o = O.Index(t, ssa_stride=stride)
     return o, o.bwt().tobytes(), o.ssa(), np.asarray(o.C(), np.uint64)
+
+
+# ---- CPU: the writer against the reference's own reader ------------------------------
+
+REF_READS = pytest.mark.skipif(not (O.ref_lib() is not None and hasattr(O.ref_lib(), "ref_csidx_open")),
+                               reason="oracle/_ref/libcs_ref.so (make -C oracle ref) not built")
+
+
+@REF_READS
+@pytest.mark.parametrize("name", sorted(TEXTS) + ["dna_100k"])
+@pytest.mark.parametrize("with_text", [False, True])
+@pytest.mark.parametrize("stride", [1, 7, 32])
+def test_writer_vs_reference_reader(tmp_path, name, with_text, stride):
+    """cs_csidx_write's file through cs::IndexReader (the reference's mmap reader): header
+    magic / version accepted (serialization.cpp:171-174), text_len, and every section the
+    getters return — get_text, get_bwt, get_c_array (C_, 257 x u32), get_ssa with its stride
+    — equal to the oracle's members; our own reader agrees (cs_csidx_check)."""
+    pkg = load_pkg()
+    t = TEXTS[name] if name in TEXTS else O.gen_dna(8, 99_999).tobytes()
+    o, bwt, ssa, C = _arrays(t, stride)
+    p = str(tmp_path / "w.csidx")
+    pkg.csidx_write(p, bwt, ssa, stride, t if with_text else None)
+    r = O.ref_read_csidx(p)
+    assert r["version"] == 1 and r["text_len"] == len(t)
+    assert r["bwt"].tobytes() == bwt
+    assert np.array_equal(r["C"], C.astype(np.uint32))
+    assert r["stride"] == stride and np.array_equal(r["ssa"], ssa.astype(np.uint32))
+    assert (r["text"].tobytes() if r["text"] is not None else None) == (t if with_text else None)
+    assert pkg.csidx_check(p) == {"n": len(t), "ssa_stride": stride, "has_text": with_text}
+    # the Python restatement of the layout writes the same bytes
+    q = str(tmp_path / "py.csidx")
+    write_csidx(q, bwt, ssa, stride, t if with_text else None, C=C.astype(np.uint32))
+    assert open(p, "rb").read() == open(q, "rb").read()
+
+
+@REF_READS
+def test_reference_reader_rejects_what_we_reject(tmp_path):
+    """A bad magic is refused by both readers with the reference's message."""
+    pkg = load_pkg()
+    o, bwt, ssa, C = _arrays(TEXTS["banana"], 4)
+    p = str(tmp_path / "bad.csidx")
+    write_csidx(p, bwt, ssa, 4, magic=b"CSIDY\0\0\0")
+    with pytest.raises(RuntimeError, match="Invalid index file: bad magic or version"):
+        O.ref_read_csidx(p)
+    with pytest.raises(RuntimeError, match="bad magic or version"):
+        pkg.csidx_check(p)
+
+
+def test_writer_rejects_bad_arrays(tmp_path):
+    pkg = load_pkg()
+    o, bwt, ssa, C = _arrays(TEXTS["banana"], 4)
+    with pytest.raises(RuntimeError, match="ceil"):
+        pkg.csidx_write(str(tmp_path / "x.csidx"), bwt, ssa[:-1], 4)
+    with pytest.raises(RuntimeError, match="ceil"):
+        pkg.csidx_write(str(tmp_path / "x.csidx"), bwt, ssa, 0)
 
 
 # ---- CPU: the reader's validation (no device) -----------------------------------
@@ -205,6 +262,11 @@ def test_save_csidx_round_trip(tmp_path, name):
     o = O.Index(t, ssa_stride=stride)
     text, bwt, C, st, ssa = read_csidx(p)
     assert text == t and bwt == o.bwt().tobytes() and st == stride
+    # the bytes the host writer (pinned against cs::IndexReader on the CPU) writes for the
+    # oracle's members
+    q = str(tmp_path / "host.csidx")
+    pkg.csidx_write(q, o.bwt().tobytes(), o.ssa(), stride, t)
+    assert open(p, "rb").read() == open(q, "rb").read()
     assert np.array_equal(ssa, o.ssa().astype(np.uint32))
     assert np.array_equal(C, np.asarray(o.C(), np.uint32))
     assert pkg.csidx_check(p) == {"n": len(t), "ssa_stride": stride, "has_text": True}

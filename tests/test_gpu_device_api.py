@@ -103,6 +103,70 @@ def test_concurrent_calls_share_nothing_mutable():
     assert not bad, bad[:5]
 
 
+def test_long_routing_concurrent_streams():
+    """Long-pattern routing inside the call (fm_device.hpp LongList): the
+    staged kernel lists the patterns its one read cannot answer and k_count_long /
+    k_locate_long take them from the call's own lists — no state in the handle.  4 host
+    threads, each on its own stream, alternate short-only, long-only and mixed device batches
+    (counts, and locates in one call) on one handle: every result equals the oracle's."""
+    import threading
+    pkg = load_pkg()
+    t = O.gen_dna(9, 400_000)
+    g = pkg.FMIndex.build_from_text(t.tobytes())
+    if not g.info().packed_text_bytes:
+        pytest.skip("no long-pattern kernels on this index")
+    o = O.Index(t)
+    rng = np.random.default_rng(2)
+    batches = []
+    for kind in ("short", "long", "mixed", "mixed_sparse"):
+        pats = []
+        for _ in range(3000):
+            if kind == "short" or (kind == "mixed_sparse" and rng.random() < 0.97):
+                m = int(rng.integers(1, 32))
+            elif kind == "long":
+                m = int(rng.integers(32, 160))
+            else:
+                m = int(rng.integers(1, 160))
+            i = int(rng.integers(0, len(t) - m))
+            p = bytearray(t[i:i + m].tobytes())
+            if rng.random() < 0.3:
+                p[int(rng.integers(0, m))] = b"ACGT"[int(rng.integers(0, 4))]
+            pats.append(bytes(p))
+        buf, offs = O.pack_patterns(pats)
+        woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=50, nthreads=8)
+        batches.append((buf, offs, o.count_batch(buf=buf, offs=offs, nthreads=8), woffs, wpos))
+    bad = []
+
+    def worker(seed):
+        rng_w = np.random.default_rng(seed)
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            for it in range(24):
+                buf, offs, want, woffs, wpos = batches[int(rng_w.integers(len(batches)))]
+                npat = len(offs) - 1
+                d_p, d_o = _dev(buf, torch.uint8), _dev(offs.astype(np.int64), torch.int64)
+                d_c = torch.empty(npat, dtype=torch.int64, device="cuda")
+                g.count_batch_device(d_p.data_ptr(), d_o.data_ptr(), npat, d_c.data_ptr(), s.cuda_stream)
+                d_oo = torch.empty(npat + 1, dtype=torch.int64, device="cuda")
+                d_pos = torch.empty(max(int(woffs[-1]), 1), dtype=torch.int64, device="cuda")
+                tot, ok = g.locate_device(d_p.data_ptr(), d_o.data_ptr(), npat, 50, d_oo.data_ptr(),
+                                          d_pos.data_ptr(), d_pos.numel(), s.cuda_stream)
+                s.synchronize()
+                if not np.array_equal(d_c.cpu().numpy().astype(np.uint64), want):
+                    bad.append(("count", seed, it))
+                if not (ok and tot == woffs[-1] and
+                        np.array_equal(d_oo.cpu().numpy().astype(np.uint64), woffs) and
+                        np.array_equal(d_pos[:tot].cpu().numpy().astype(np.uint64), wpos)):
+                    bad.append(("locate", seed, it))
+
+    th = [threading.Thread(target=worker, args=(sd,)) for sd in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad, bad[:5]
+
+
 @pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "learned", "records", "records16"])
 def test_export_import_image(engine, monkeypatch):
     """The device image (cs_fm_export_meta/_parts -> cs_fm_import): the copy answers

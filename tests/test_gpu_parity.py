@@ -120,6 +120,10 @@ def _learned():
     return os.environ.get("CS_FM_ENGINE") == "learned"
 
 
+def _wide():
+    return os.environ.get("CS_FM_WIDE") == "1"
+
+
 def _texts():
     rng = np.random.default_rng(11)
     out = {
@@ -505,11 +509,11 @@ def test_count_long_kernel_large(pkg):
         with _env(CS_FM_LONG_V16=v):
             got, _, _ = _count_ex(g, pats, flags=32)
         assert np.array_equal(got, want), v
-    for _ in range(2):  # the default path: detection, then long-pattern routing
+    for _ in range(2):  # the default path: long-pattern routing inside the call
         got, _, _ = _count_ex(g, pats)
         assert np.array_equal(got, want)
-    # locate in one call: k_locate_long (CS_Q_LONG), then detection and routing (indexes with
-    # the 2-bit text)
+    # locate in one call: k_locate_long (CS_Q_LONG), then the default path's routing (indexes
+    # with the 2-bit text)
     if g.info().packed_text_bytes:
         woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=100, nthreads=8)
         want_l = [wpos[woffs[q]:woffs[q + 1]].tolist() for q in range(len(pats))]
@@ -816,9 +820,9 @@ def test_count_verify_long(built, pkg, name):
     with _env(CS_FM_LONG_V16="0"):  # 8-B pattern and window loads
         got, _, _ = _count_ex(g, pats, flags=32)
     assert got.tolist() == want, (name, "v16=0")
-    # long-pattern routing of the default path: the batches above raised the handle's flag,
-    # so these run the staged kernel for the short patterns and k_count_long for the rest;
-    # a batch of short patterns only ends the mode, the next mixed batch raises it again
+    # long-pattern routing of the default path (inside the call since round 4): the staged
+    # kernel counts the short patterns and lists the rest for k_count_long; short-only and
+    # mixed batches alternate
     short = [p for p in pats if len(p) <= 32]
     for _ in range(2):
         got, _, _ = _count_ex(g, pats)
@@ -936,8 +940,8 @@ def test_locate_verify_long(built, pkg, name):
         for q, p in enumerate(pats):
             assert pos[offs[q]:offs[q + 1]].tolist() == want[q], (name, lim, p)
         # the one call: CS_Q_LONG (k_locate_long for every pattern, then k_locate_list), the
-        # default path twice (the first raises the routing flag, the second leaves the long
-        # patterns to k_locate_long), 8-B loads (CS_FM_LONG_V16=0) — on the indexes that take
+        # default path twice (the staged kernel lists the long patterns for k_locate_long in
+        # the same call), 8-B loads (CS_FM_LONG_V16=0) — on the indexes that take
         # the long-pattern kernels (the 2-bit text; the others' one call is checked above)
         if not g.info().packed_text_bytes:
             if lim == 100000:  # CS_Q_LONG where the long-pattern kernels do not apply: the usual call
@@ -947,7 +951,7 @@ def test_locate_verify_long(built, pkg, name):
             assert _locate_one(g, pats, lim, f) == want, (name, lim, f)
         with _env(CS_FM_LONG_V16="0"):
             assert _locate_one(g, pats, lim, 32) == want, (name, lim, "v16=0")
-        short = [i for i, p in enumerate(pats) if len(p) < 32]  # ends the routing mode
+        short = [i for i, p in enumerate(pats) if len(p) < 32]  # nothing to list
         assert _locate_one(g, [pats[i] for i in short], lim) == [want[i] for i in short], (name, lim)
         lp = [i for i, p in enumerate(pats) if len(p) > 31]  # host batch: CS_Q_LONG unasked
         if lp:
@@ -1034,6 +1038,43 @@ def test_locate_one_call(built, pkg, name):
             assert tot2 == tot and not ok2 and torch.equal(d_oo2, d_oo), (name, lim)
 
 
+def test_locate_records(pkg):
+    """The one-call locate through the locate records (fm_device.hpp kLocRec*: the SA values
+    of each (k+1)-mer's rows beside their contexts, round 4) against the oracle's positions in
+    row order and against the same call without them (CS_Q_NO_LOC_RECORDS): a DNA text with
+    40-base pieces copied 2-7 times (so (k+1)-mers have 0..7+ rows) and a few N, every pattern
+    length from k-1 to k+7 (text substrings, one-character mutants, uniform), limits 1, 2 and
+    100000.  Built with 16-B context records (CS_FM_CTX_RECORDS=16, their precondition); the
+    variants without the records' other preconditions skip."""
+    rng = np.random.default_rng(5)
+    t = bytearray(O.gen_dna(77, 199_999)[:-1].tobytes())
+    for c in range(400):
+        a = int(rng.integers(0, len(t) - 40))
+        piece = bytes(t[a:a + 40])
+        for _ in range(1 + c % 7):
+            b = int(rng.integers(0, len(t) - 40))
+            t[b:b + 40] = piece
+    for i in rng.integers(0, len(t), 12):
+        t[int(i)] = ord("N")
+    t = bytes(t) + b"$"
+    with _env(CS_FM_CTX_RECORDS="16"):
+        g = pkg.FMIndex.build_from_text(t, pkg.BuildParams())
+    info = g.info()
+    if not info.locate_record_bytes:
+        pytest.skip("this variant builds no locate records")
+    assert info.record_bytes == 16 and info.locate_record_bytes == 16 * 4 ** (info.prefix_k + 1)
+    o = O.Index(t)
+    K = info.prefix_k
+    pats = []
+    for m in range(max(1, K - 1), K + 8):
+        pats += _substrings_and_mutants(t, (m,), 150, m)
+        pats += [bytes(p) for p in O.gen_patterns_uniform(b"ACGT", m, 20, seed=m)]
+    for lim in (1, 2, 100000):
+        want = [o.locate(p, limit=lim) for p in pats]
+        assert _locate_one(g, pats, lim) == want, lim
+        assert _locate_one(g, pats, lim, pkg.Q_NO_LOC_RECORDS) == want, lim
+
+
 @pytest.mark.parametrize("name", ["dna_5k", "bytes_5k", "all_same", "runs", "rare_N_41", "banana"])
 def test_count_widths(built, pkg, name):
     """uint32 counts equal the uint64 ones; uint8 counts saturate at 255 with every
@@ -1114,6 +1155,60 @@ def test_repetitive_text_vs_oracle(pkg):
         woffs, wpos = o.locate_batch(buf=b2, offs=o2, limit=lim, nthreads=8)
         goffs, gpos = g.locate_batch(buf=b2, offs=o2, limit=lim)
         assert np.array_equal(goffs, woffs) and np.array_equal(gpos, wpos), lim
+
+
+def test_majority_records_vs_oracle(pkg):
+    """Wide compact records keep their two most frequent contexts with exact counts
+    (fm_device.hpp kRec16Maj, round 4): on a repetitive text (copies of a seed with ~1 %
+    substitutions) a pattern of k + 5 characters whose k-mer range is hundreds of rows wide
+    is counted from the record alone.  Counts of k+3 .. k+7-mers — text substrings (the
+    dominant context), mutants of their first characters (minority and absent contexts) and
+    uniform patterns — equal the oracle's through the staged device batch, the host batch, the
+    fixed-length form and the reference's plain steps (CS_Q_NO_CONTEXTS); most (k+5)-mer
+    substrings then take one 16-B read (the measurement twin's bytes)."""
+    rng = np.random.default_rng(21)
+    seed = rng.choice(list(b"ACGT"), 5000).astype(np.uint8)
+    t = np.tile(seed, 300)
+    mut = rng.random(len(t)) < 0.01
+    t[mut] = rng.choice(list(b"ACGT"), int(mut.sum())).astype(np.uint8)
+    t = t.tobytes() + b"$"
+    with _env(CS_FM_CTX_RECORDS="16"):
+        g = pkg.FMIndex.build_from_text(t)
+    o = O.Index(t)
+    info = g.info()
+    K = max(info.prefix_k, 1)
+    pats = []
+    for m in range(K + 3, K + 8):
+        P = O.gen_patterns_text(np.frombuffer(t, np.uint8), m, 400, seed=m)
+        for p in P:
+            pats.append(bytes(p))
+            q = bytearray(p)
+            q[int(rng.integers(0, min(5, m)))] = b"ACGT"[int(rng.integers(0, 4))]
+            pats.append(bytes(q))
+        pats += [bytes(p) for p in O.gen_patterns_uniform(b"ACGT", m, 50, seed=m + 100)]
+    buf, offs = O.pack_patterns(pats)
+    want = o.count_batch(buf=buf, offs=offs, nthreads=8)
+    got, _, _ = _count_ex(g, pats)
+    assert np.array_equal(got, want)
+    assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
+    got, _, _ = _count_ex(g, pats, flags=2)  # CS_Q_NO_CONTEXTS: the reference's steps
+    assert np.array_equal(got, want)
+    m5 = [p for p in pats if len(p) == K + 5]
+    d5 = torch.from_numpy(np.frombuffer(b"".join(m5), np.uint8).copy()).cuda()
+    f5 = torch.empty(len(m5), dtype=torch.int64, device="cuda")
+    g.count_fixed_device(d5.data_ptr(), K + 5, len(m5), f5.data_ptr())
+    torch.cuda.synchronize()
+    assert f5.cpu().numpy().astype(np.uint64).tolist() == [int(w) for p, w in zip(pats, want) if len(p) == K + 5]
+    if info.record_bytes == 16 and info.engine in (1, 3) and not _wide():
+        sub = [bytes(p) for p in O.gen_patterns_text(np.frombuffer(t, np.uint8), K + 5, 400, seed=K + 5)]
+        b2, o2 = O.pack_patterns(sub)
+        d_b, d_o = torch.from_numpy(b2.copy()).cuda(), torch.from_numpy(o2.astype(np.int64)).cuda()
+        qb = torch.empty(len(sub), dtype=torch.int64, device="cuda")
+        g.count_bytes_device(d_b.data_ptr(), d_o.data_ptr(), len(sub), qb.data_ptr())
+        cnt = o.count_batch(buf=b2, offs=o2)
+        torch.cuda.synchronize()
+        wide = cnt > 9
+        assert wide.mean() > 0.5 and (qb.cpu().numpy()[wide] == 16).mean() > 0.8
 
 
 def test_open_reference_style_directory(pkg, tmp_path):
