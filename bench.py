@@ -298,22 +298,39 @@ class Workload:
         return rnd, acc, frac
 
 
+def dram_basis(alg, stream_read, accesses, pmc):
+    """What the roofline fractions are taken on: with a fresh PMC
+    profile of the leg, the bytes are min(algorithmic, measured HBM traffic) — cache hits
+    (the first backward-search steps from C[] share lines across patterns) are not HBM
+    reads — and the random accesses are the DRAM's: the calibrated traffic is the stream plus
+    one 32-B DRAM access per random read request (profiles/summarize.py), so requests =
+    (traffic - stream) / 32.  Without a fresh profile, the algorithmic figures.
+    -> (bytes, random accesses, basis)."""
+    tr = pmc.get("traffic")
+    if tr:
+        return min(alg, tr), max(0.0, (tr - (stream_read or 0)) / 32.0), "pmc"
+    return alg, accesses, "algorithmic"
+
+
 def roofline(alg_random, alg_stream, accesses, kern_s, B, pmc, stream_read=None):
     """pmc: pmc_traffic()'s dict (traffic + whether its profile matches this kernel)."""
     alg = alg_random + alg_stream
-    achieved = alg / kern_s / 1e9
+    fb, acc, basis = dram_basis(alg, stream_read, accesses, pmc)
+    achieved = fb / kern_s / 1e9
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, **pmc,
+            "frac": achieved / HBM_PEAK_GBS, **pmc, "basis": basis,
             "alg_bytes_per_launch": alg, "alg_random_bytes_per_launch": alg_random,
             "alg_stream_bytes_per_launch": alg_stream, "alg_bytes_per_query": alg / B,
+            "alg_GBs": alg / kern_s / 1e9,
             "stream_read_bytes_per_launch": stream_read,
-            "random_accesses_per_launch": accesses,
-            "random_accesses_per_query": accesses / B,
-            "random_accesses_per_s": accesses / kern_s,
+            "alg_random_accesses_per_launch": accesses,
+            "random_accesses_per_launch": acc,
+            "random_accesses_per_query": acc / B,
+            "random_accesses_per_s": acc / kern_s,
             "random_access_ceiling_per_s": RANDOM_CEIL,
-            "frac_of_random_access_ceiling": accesses / kern_s / RANDOM_CEIL,
+            "frac_of_random_access_ceiling": acc / kern_s / RANDOM_CEIL,
             "access_mix_ceiling_per_s": MIXED_CEIL,
-            "frac_of_access_mix_ceiling": accesses / kern_s / MIXED_CEIL}
+            "frac_of_access_mix_ceiling": acc / kern_s / MIXED_CEIL}
 
 
 def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, steps, warmup,
@@ -397,35 +414,44 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
     step_bytes = walk_step_bytes(info, idx)
     uses_sa = info.full_sa_bytes and not (flags & 4)
     walk_lines = not uses_sa and info.walk_bytes and not (flags & 8)
-    # phase 2's random reads: the full SA one entry per position; walk lines one 32-B
-    # line per visited row (the start row and every LF step: the line holds the row's
-    # mark, symbol and occ) + one sample; the row-sampled walk one LF step's lines per
-    # step (a sampled row is known from its index) + one sample
+    # phase 2's random reads: the full SA one dependent read per reported range — a range's
+    # rows are consecutive, so its SA entries are one run of ceil(4 c / 32) 32-B sectors,
+    # the first random, the rest streamed (repetitive DNA: thousands per range); walk lines
+    # one 32-B line per visited row (the start row and every LF step: the line holds the
+    # row's mark, symbol and occ) + one sample; the row-sampled walk one LF step's lines
+    # per step (a sampled row is known from its index) + one sample
+    cnts = np.diff(oo).astype(np.int64)
     if uses_sa:
-        lines, reads = 0.0, float(tot)
-    elif walk_lines:
-        lines = float(st + tot)
-        reads = lines + tot
+        nz = int((cnts > 0).sum())
+        sa_sectors = int(((cnts * 4 + 31) // 32).sum())
+        lines, reads = 0.0, float(nz)
+        alg = sa_sectors * 32 + tot * 8 + B * 16
+        stream_rd = 16 * B + (sa_sectors - nz) * 32
     else:
-        lines = st * (step_bytes / 32.0)
+        if walk_lines:
+            lines = float(st + tot)
+        else:
+            lines = st * (step_bytes / 32.0)
         reads = lines + tot
-    # algorithmic bytes: those reads, the record/offsets read and the position written
-    alg = lines * 32 + tot * ((4 if uses_sa else sb) + 8) + B * 16
-    # streamed reads of the phase-2 kernel (PMC correction, profiles/summarize_legs.py): the
-    # records + offsets (full SA, fused walk-line walk) or the expanded rows (k_walk)
-    stream_rd = 16 * B if (uses_sa or walk_lines) else 8 * tot
+        # algorithmic bytes: those reads, the record/offsets read and the position written
+        alg = lines * 32 + tot * (sb + 8) + B * 16
+        # streamed reads of the phase-2 kernel (PMC correction, profiles/summarize_legs.py):
+        # the records + offsets (fused walk-line walk) or the expanded rows (k_walk)
+        stream_rd = 16 * B if walk_lines else 8 * tot
+    wpmc = pmc_traffic(wl_key, name, walk_s)
+    wb, wreads, wbasis = dram_basis(alg, stream_rd, reads, wpmc)
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl,
             "phase1_ms": min(t1s) * 1e3, "phase2_ms": walk_s * 1e3, "limit": limit,
             "flags": flags, "positions_verified": ok,
             "walk_lf_steps_per_position": st / max(tot, 1),
             "phase2_stream_read_bytes": stream_rd, "phase2_alg_bytes": alg,
-            "walk_roofline": {"bound": "hbm", "achieved": alg / walk_s / 1e9, "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": alg / walk_s / 1e9 / HBM_PEAK_GBS,
-                              "alg_bytes_per_position": alg / max(tot, 1),
-                              **pmc_traffic(wl_key, name, walk_s),
-                              "dependent_reads_per_s": reads / walk_s,
-                              "frac_of_random_access_ceiling": reads / walk_s / RANDOM_CEIL}}
+            "walk_roofline": {"bound": "hbm", "achieved": wb / walk_s / 1e9, "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": wb / walk_s / 1e9 / HBM_PEAK_GBS, "basis": wbasis,
+                              "alg_bytes": alg, "alg_bytes_per_position": alg / max(tot, 1),
+                              **wpmc, "alg_dependent_reads": reads,
+                              "dependent_reads_per_s": wreads / walk_s,
+                              "frac_of_random_access_ceiling": wreads / walk_s / RANDOM_CEIL}}
 
 
 def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limit=100000):
@@ -485,16 +511,19 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
     del qb, hit, hb, cnt
     stream_b = B * m + (B + 1) * 8 + B * 12 * 2 + (B + 1) * 8 + tot * 8
     alg = rnd + stream_b
-    reads = acc
+    stream_rd = B * m + (B + 1) * 8 + B * 12  # patterns, offsets, the search's results read back
+    lpmc = pmc_traffic(wl_key, name, min(evs))
+    fb, reads, basis = dram_basis(alg, stream_rd, acc, lpmc)
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl, "limit": limit,
             "event_ms": min(evs) * 1e3, "positions_verified": okv,
             "locate_record_hit_frac": nhit / B,
-            "roofline": {"bound": "hbm", "achieved": alg / tl / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": alg / tl / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_query": alg / B,
+            "roofline": {"bound": "hbm", "achieved": fb / tl / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": fb / tl / 1e9 / HBM_PEAK_GBS, "basis": basis, "alg_bytes_per_launch": alg,
+                         "alg_bytes_per_query": alg / B,
                          "alg_random_bytes_per_launch": rnd, "alg_stream_bytes_per_launch": stream_b,
-                         "stream_read_bytes_per_launch": B * m + (B + 1) * 8,
-                         **pmc_traffic(wl_key, name, min(evs)), "random_accesses_per_s": reads / tl,
+                         "stream_read_bytes_per_launch": stream_rd, "alg_random_accesses_per_launch": acc,
+                         **lpmc, "random_accesses_per_s": reads / tl,
                          "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}
 
 
@@ -1281,8 +1310,12 @@ def main():
                                    "OMP_NUM_THREADS (the pool's CPU share per GPU) within the affinity set"
                                    if omp and omp < affinity else "the whole affinity set")}
             Q = args.cpu_queries
+            wide = N >= 2 ** 32  # C5: the reference's u32 tables cannot hold it
             if Q is None:
-                Q = max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16, 2 * threads)
+                # one pattern per thread at n >= 2^32: a faithful count() there scans 8 x 4 GB
+                # bitvectors per rank (~1 min per 20-mer)
+                Q = threads if wide else max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16,
+                                             2 * threads)
             t1 = time.perf_counter()
             d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
             idx.bwt_device(d_bwt.data_ptr(), sh)
@@ -1306,7 +1339,7 @@ def main():
                 "matches_gpu": bool(np.array_equal(cnt, counts[:Qp].astype(np.uint64)))}
             port.update(cpu_share)
             res["cpu_baseline"] = port
-            if O.ref_lib() is not None:
+            if O.ref_lib() is not None and not wide:
                 # the genuine reference's FMIndex::count / locate (oracle/_ref/libcs_ref.so,
                 # built from the reference's sources) over its own BitVector tables of the
                 # same BWT, plus its bwt_ and ssa_ members for locate

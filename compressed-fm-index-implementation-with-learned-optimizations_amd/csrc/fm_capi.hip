@@ -600,6 +600,23 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   return CS_OK;
 }
 
+// A device batch may pass d_pats = NULL when every pattern is empty (the kernels read no
+// pattern byte then): with a null d_pats the batch's byte span d_offs[npat] - d_offs[0] is
+// read back (one synchronous 16-B copy on `stream`, only on this path) and must be 0
+// (round 3 rejected such a batch outright).
+static cs_status null_pats_ok(const uint8_t* d_pats, const uint64_t* d_offs, uint64_t npat, hipStream_t st) {
+  if (!npat || d_pats || !d_offs) return CS_OK;
+  uint64_t ends[2] = {0, 0};
+  FMX_HIP(hipMemcpyAsync(&ends[0], d_offs, 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipMemcpyAsync(&ends[1], d_offs + npat, 8, hipMemcpyDeviceToHost, st));
+  FMX_HIP(hipStreamSynchronize(st));
+  if (ends[1] != ends[0]) {
+    set_error("null batch pointer");
+    return CS_ERR_INVALID;
+  }
+  return CS_OK;
+}
+
 cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream) {
@@ -610,6 +627,7 @@ cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
+  if ((s = null_pats_ok(d_pats, d_offs, npat, (hipStream_t)stream)) != CS_OK) return s;
   return launch_count(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
 }
 
@@ -696,10 +714,11 @@ cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pat
   if (s != CS_OK) return s;
   CountOut co;
   if ((s = count_out(h, out, npat, co)) != CS_OK) return s;
-  if (npat && !d_pats && (d_offs || fixed_m)) {  // the same rule as cs_fm_count_fixed_device
+  if (npat && !d_pats && !d_offs && fixed_m) {  // the same rule as cs_fm_count_fixed_device
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
+  if ((s = null_pats_ok(d_pats, d_offs, npat, (hipStream_t)stream)) != CS_OK) return s;
   return launch_count_ex(h, d_pats, d_offs, npat, co, flags, (hipStream_t)stream,
                          d_offs ? 0 : fixed_m, false);
 }
@@ -1000,6 +1019,7 @@ cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_p
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
+  if ((s = null_pats_ok(d_pats, d_offs, npat, (hipStream_t)stream)) != CS_OK) return s;
   return launch_locate_ranges(h, d_pats, d_offs, npat, limit, d_sp, d_out_offs, total,
                               (hipStream_t)stream, flags);
 }
@@ -1016,6 +1036,7 @@ cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, co
     return CS_ERR_INVALID;
   }
   hipStream_t st = (hipStream_t)stream;
+  if ((s = null_pats_ok(d_pats, d_offs, npat, st)) != CS_OK) return s;
   bool done = false;
   // any flag but CS_Q_LONG / CS_Q_NO_LOC_RECORDS leaves structures out: the two phases honour it
   if (!(flags & ~(CS_Q_LONG | CS_Q_NO_LOC_RECORDS))) {

@@ -1613,8 +1613,11 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       else
         rec16_contexts(a.y, a.z, a.w, d);
       w[j][0] = make_uint4(d[0], d[1], d[2], d[3]);
-      // (count forms: the record's dwords 1 and 3 for a wide record's majority contexts)
-      w[j][1] = make_uint4(d[4], kLoc ? 0u : a.y, kLoc ? 0u : a.w, 0u);
+      w[j][1] = make_uint4(d[4], 0u, 0u, 0u);
+      // count forms: a wide record's majority contexts (kRec16Maj) may give the count here
+      if (!kLoc && wc == kRec16Wide && st[j] == 2 && k[j] == kRec16Q && !ix.wide &&
+          rec16_majority(a.y, a.w, want[j], res[j]))
+        st[j] = 0;
     } else if (!ptab_at(ix, t[j], sp[j], ep[j])) {
       st[j] = 3;
     }
@@ -1635,9 +1638,6 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     } else if (st[j] == 2 && inl[j] && ix.lctx) {
       bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record
       w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
-    } else if (!kLoc && st[j] == 2 && ix.ptab_rec == 2 && !ix.wide && k[j] == kRec16Q &&
-               (w[j][1].y & 15u) == kRec16Wide && rec16_majority(w[j][1].y, w[j][1].z, want[j], res[j])) {
-      st[j] = 0;  // a wide record's majority contexts (kRec16Maj): the count in the one read
     } else if (st[j] == 2 && ix.lctx && ep[j] - (sp[j] & ~15ull) <= 32) {
       bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
@@ -2097,38 +2097,102 @@ __device__ __forceinline__ void long_list_append(bool general, uint64_t q, const
   ll.list2[r * kLongRegion + at] = (uint16_t)(q - r * kLongRegion);
 }
 
-// The patterns of one long-pattern launch: from the staged kernel's region lists (ll.list /
-// ll.cnt: block b of the grid walks regions b, b + grid, ...; the lengths are read on the
-// device, so an empty list costs the launch) or, without a list (CS_Q_LONG, fixed-length
-// batches of long patterns), every pattern q < npat.  f(q, active) runs with the whole block
-// in lockstep (active = q is a pattern to search), so f may use wave collectives; the q of
-// every lane of a wave, active or not, lies in one region (= one tile of the one-call locate).
+// The patterns of one long-pattern launch (kList): the staged kernel's region lists
+// (ll.list / ll.cnt: block b of the grid walks regions b, b + grid, ...; the lengths are read
+// on the device, so an empty list costs the launch).  f(q, active) runs with the whole
+// block in lockstep (active = q is a pattern to search), so f may use wave collectives; the
+// q of every lane of a wave, active or not, lies in one region (= one tile of the one-call
+// locate).  Without a list (CS_Q_LONG, fixed-length batches of long patterns) the kernels
+// take one pattern per lane over a grid covering the batch, as before round 4 (a loop there
+// costs k_count_long 40 VGPRs).
+// The regions of block b that hold patterns: b + t gridDim.x for t < kBlk (the grid is
+// launched with at least regions / kBlk blocks, long_list_grid), their counts read by one load
+// per thread — an empty list costs two barriers, not a chain of dependent loads — and the
+// nonempty ones listed in LDS (s_t[0 .. *s_n)).
+__device__ __forceinline__ void list_regions(const uint32_t* __restrict__ cnt, uint64_t regions,
+                                             uint32_t* s_t, uint32_t* s_n) {
+  if (threadIdx.x == 0) *s_n = 0;
+  __syncthreads();
+  const uint64_t r = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x;
+  if (r < regions && cnt[r]) s_t[atomicAdd(s_n, 1u)] = threadIdx.x;
+  __syncthreads();
+}
+
 template <class F>
-__device__ __forceinline__ void long_patterns(const LongList& ll, bool from_list, uint64_t npat, F&& f) {
-  if (from_list) {
-    const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-    for (uint64_t r = blockIdx.x; r < regions; r += gridDim.x) {
-      const uint32_t c = ll.cnt[r];  // uniform over the block
-      for (uint32_t i0 = 0; i0 < c; i0 += kBlk) {
-        const uint32_t i = i0 + threadIdx.x;
-        const bool act = i < c;
-        // (an inactive lane gets the region's first pattern: same tile, same region)
-        f(r * kLongRegion + (act ? ll.list[r * kLongRegion + i] : 0u), act);
-      }
-    }
-  } else {
-    for (uint64_t b0 = blockIdx.x * (uint64_t)kBlk; b0 < npat; b0 += (uint64_t)gridDim.x * kBlk) {
-      const uint64_t q = b0 + threadIdx.x;
-      f(q, q < npat);
+__device__ __forceinline__ void long_list_patterns(const LongList& ll, uint64_t npat, F&& f) {
+  __shared__ uint32_t s_t[kBlk], s_n;
+  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
+  list_regions(ll.cnt, regions, s_t, &s_n);
+  const uint32_t nr = s_n;
+  for (uint32_t e = 0; e < nr; ++e) {
+    const uint64_t r = blockIdx.x + (uint64_t)s_t[e] * gridDim.x;
+    const uint32_t c = ll.cnt[r];  // uniform over the block
+    for (uint32_t i0 = 0; i0 < c; i0 += kBlk) {
+      const uint32_t i = i0 + threadIdx.x;
+      const bool act = i < c;
+      // (an inactive lane gets the region's first pattern: same tile, same region)
+      f(r * kLongRegion + (act ? ll.list[r * kLongRegion + i] : 0u), act);
     }
   }
 }
 
-template <int W, bool kPT, bool kBytes = false, int kV16 = 0>
+// k_count_long's search of one pattern q (< npat, the batch's offsets or fixed_m)
+template <int W, bool kPT, bool kBytes, int kV16>
+__device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t* __restrict__ pats,
+                                               const uint64_t* __restrict__ offs, const CountOut& co,
+                                               uint64_t fixed_m, const LongList& ll, bool skip_short,
+                                               const uint16_t* cmap, const uint32_t* rare, uint64_t q) {
+  const uint64_t o0 = offs ? offs[q] : q * fixed_m;
+  const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
+  // skip_short (the measurement twin of a routed batch): only the patterns the staged
+  // kernel lists
+  if (skip_short && !(m >= kFastM && m > ix.ptab_k + kCtxQ)) return;
+  if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
+    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
+    else store_count<W>(co, q, m == 0 ? ix.n : 0);
+    return;
+  }
+  uint64_t by = 0;  // kBytes
+  uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
+  uint64_t base;
+  uint32_t cand, qf;
+  const bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+  uint64_t res = 0;
+  if (!general) {
+    // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
+    const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
+    while (cand) {
+      const uint32_t i = (uint32_t)__ffs(cand) - 1u;
+      cand &= cand - 1;
+      const uint64_t p = load_sa(ix.vsa, base + i);
+      const uint64_t wq = p >= k ? p - k : p + n - k;
+      if constexpr (kBytes) {  // the SA sector, then the window's words
+        constexpr uint64_t C = 32ull * kLongPW;
+        by += 32;
+        if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
+        else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
+        else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
+          by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
+                (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
+        continue;
+      }
+      bool eq;
+      if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
+      else eq = window_eq_long<kLongWords>(ix, pats + o0, wq, L);
+      res += eq ? 1u : 0u;
+    }
+  }
+  long_list_append(general, q, ll);
+  if (general) return;
+  if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
+  else store_count<W>(co, q, res);
+}
+
+template <int W, bool kPT, bool kBytes = false, int kV16 = 0, bool kList = false>
 __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m, LongList ll,
-                                                     bool from_list, bool skip_short) {
+                                                     bool skip_short) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   static_assert(kBlk >= 256, "one map entry per thread");
@@ -2136,53 +2200,14 @@ __global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t*
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
-  long_patterns(ll, from_list, npat, [&](uint64_t q, bool act) {
-    if (!act) return;
-    const uint64_t o0 = offs ? offs[q] : q * fixed_m;
-    const uint64_t m = offs ? offs[q + 1] - o0 : fixed_m;
-    // skip_short (the measurement twin of a routed batch): only the patterns the staged
-    // kernel lists
-    if (skip_short && !(m >= kFastM && m > ix.ptab_k + kCtxQ)) return;
-    if (m == 0 || ix.n == 0) {  // fm_index.cpp:80-81
-      if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = 0;
-      else store_count<W>(co, q, m == 0 ? ix.n : 0);
-      return;
-    }
-    uint64_t by = 0;  // kBytes
-    uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
-    uint64_t base;
-    uint32_t cand, qf;
-    const bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
-    uint64_t res = 0;
-    if (!general) {
-      // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
-      const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
-      while (cand) {
-        const uint32_t i = (uint32_t)__ffs(cand) - 1u;
-        cand &= cand - 1;
-        const uint64_t p = load_sa(ix.vsa, base + i);
-        const uint64_t wq = p >= k ? p - k : p + n - k;
-        if constexpr (kBytes) {  // the SA sector, then the window's words
-          constexpr uint64_t C = 32ull * kLongPW;
-          by += 32;
-          if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
-          else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
-          else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
-            by += 32 * ((((wq + (L < C ? L : C) - 1) >> 2) >> 5) - ((wq >> 2) >> 5) + 1) +
-                  (L > C ? 8ull * kVerifyWords * ((L - C + 8 * kVerifyWords - 1) / (8 * kVerifyWords)) : 0);
-          continue;
-        }
-        bool eq;
-        if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
-        else eq = window_eq_long<kLongWords>(ix, pats + o0, wq, L);
-        res += eq ? 1u : 0u;
-      }
-    }
-    long_list_append(general, q, ll);
-    if (general) return;
-    if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
-    else store_count<W>(co, q, res);
-  });
+  if constexpr (kList) {
+    long_list_patterns(ll, npat, [&](uint64_t q, bool act) {
+      if (act) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, false, cmap, rare, q);
+    });
+  } else {
+    const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+    if (q < npat) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, skip_short, cmap, rare, q);
+  }
 }
 
 // Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
@@ -2199,58 +2224,74 @@ static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns
 // its sum once per region; without a list a wave's 64 patterns lie in one tile.  The patterns
 // it cannot finish (as k_count_long's, and windows whose matches lie too far apart for the
 // record) go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search), :125 (limit).
+// k_locate_long's search of pattern q (mine: q is one to search); every lane of the wave
+// calls it (the wave sums its counts into the tile of its patterns)
 template <int kV16>
+__device__ __forceinline__ void locate_long_one(const DevIndex& ix, const uint8_t* __restrict__ pats,
+                                                const uint64_t* __restrict__ offs, uint64_t limit,
+                                                const OnePass& op, const LongList& ll,
+                                                const uint16_t* cmap, const uint32_t* rare, uint64_t q,
+                                                bool mine) {
+  bool general = false;
+  const uint64_t o0 = mine ? offs[q] : 0, m = mine ? offs[q + 1] - o0 : 0;
+  uint64_t kc = 0, rec = 0;
+  if (mine && m != 0 && ix.n != 0) {  // fm_index.cpp:109: locate("") = {}
+    uint64_t by = 0, pc[kLongPW], base;
+    uint32_t cand, qf;
+    general = !long_stage<true, false, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+    if (!general && cand) {
+      const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
+      uint32_t mm = 0;
+      uint64_t p0 = 0;  // the first matching row's position
+      for (uint32_t c = cand; c; c &= c - 1) {
+        const uint32_t i = (uint32_t)__ffs(c) - 1u;
+        const uint64_t p = load_sa(ix.vsa, base + i);
+        const uint64_t wq = p >= k ? p - k : p + n - k;
+        if (window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare)) {
+          if (!mm) p0 = wq;
+          mm |= 1u << i;
+        }
+      }
+      if (mm) {
+        const uint64_t c = (uint64_t)__popc(mm);
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u, rel = mm >> f;
+        kc = c < limit ? c : limit;  // fm_index.cpp:125
+        if (kc == 1) rec = kLocStash | p0;
+        else if (kc > 1 && ((rel >> kLocVerRelBits) || k > kLocVerMaxK)) general = true;
+        else rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
+      }
+    }
+  }
+  if (general) kc = 0;  // k_locate_list adds it
+  long_list_append(mine && general, q, ll);
+  if (mine && !general) {
+    op.cnt[q] = (uint32_t)kc;
+    op.rec[q] = rec;
+  }
+  uint64_t s = kc;  // the wave's 64 patterns lie in one tile
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
+}
+
+template <int kV16, bool kList>
 __global__ __launch_bounds__(kBlk) void k_locate_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                       const uint64_t* __restrict__ offs, uint64_t npat,
-                                                      uint64_t limit, OnePass op, LongList ll, bool from_list) {
+                                                      uint64_t limit, OnePass op, LongList ll) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   if (threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
-  long_patterns(ll, from_list, npat, [&](uint64_t q, bool mine) {
-    bool general = false;
-    const uint64_t o0 = mine ? offs[q] : 0, m = mine ? offs[q + 1] - o0 : 0;
-    uint64_t kc = 0, rec = 0;
-    if (mine && m != 0 && ix.n != 0) {  // fm_index.cpp:109: locate("") = {}
-      uint64_t by = 0, pc[kLongPW], base;
-      uint32_t cand, qf;
-      general = !long_stage<true, false, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
-      if (!general && cand) {
-        const uint64_t k = m - ix.ptab_k, L = k - qf, n = ix.n;
-        uint32_t mm = 0;
-        uint64_t p0 = 0;  // the first matching row's position
-        for (uint32_t c = cand; c; c &= c - 1) {
-          const uint32_t i = (uint32_t)__ffs(c) - 1u;
-          const uint64_t p = load_sa(ix.vsa, base + i);
-          const uint64_t wq = p >= k ? p - k : p + n - k;
-          if (window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare)) {
-            if (!mm) p0 = wq;
-            mm |= 1u << i;
-          }
-        }
-        if (mm) {
-          const uint64_t c = (uint64_t)__popc(mm);
-          const uint32_t f = (uint32_t)__ffs(mm) - 1u, rel = mm >> f;
-          kc = c < limit ? c : limit;  // fm_index.cpp:125
-          if (kc == 1) rec = kLocStash | p0;
-          else if (kc > 1 && ((rel >> kLocVerRelBits) || k > kLocVerMaxK)) general = true;
-          else rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
-        }
-      }
-    }
-    if (general) kc = 0;  // k_locate_list adds it
-    long_list_append(mine && general, q, ll);
-    if (mine && !general) {
-      op.cnt[q] = (uint32_t)kc;
-      op.rec[q] = rec;
-    }
-    uint64_t s = kc;  // the wave's 64 patterns lie in one tile (long_patterns)
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
-  });
+  if constexpr (kList) {
+    long_list_patterns(ll, npat, [&](uint64_t q, bool act) {
+      locate_long_one<kV16>(ix, pats, offs, limit, op, ll, cmap, rare, q, act);
+    });
+  } else {  // no lane returns early: the wave sums its counts at the end
+    const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
+    locate_long_one<kV16>(ix, pats, offs, limit, op, ll, cmap, rare, q, q < npat);
+  }
 }
 
 // The patterns k_count_long listed (LongList list2 / cnt2): the general search
@@ -2262,16 +2303,16 @@ __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t*
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m, LongList ll) {
   __shared__ NodeTable T;
-  bool staged = false;
+  __shared__ uint32_t s_t[kBlk], s_n;
   const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-  for (uint64_t r = blockIdx.x; r < regions; r += gridDim.x) {
-    const uint32_t c = ll.cnt2[r];  // uniform over the block
-    if (!c) continue;
-    if (!staged) {
-      load_table(T, ix.table);
-      __syncthreads();
-      staged = true;
-    }
+  list_regions(ll.cnt2, regions, s_t, &s_n);
+  const uint32_t nr = s_n;
+  if (!nr) return;  // uniform over the block
+  load_table(T, ix.table);
+  __syncthreads();
+  for (uint32_t e = 0; e < nr; ++e) {
+    const uint64_t r = blockIdx.x + (uint64_t)s_t[e] * gridDim.x;
+    const uint32_t c = ll.cnt2[r];
     for (uint32_t i = threadIdx.x; i < c; i += kBlk) {
       const uint64_t q = r * kLongRegion + ll.list2[r * kLongRegion + i];
       const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
@@ -2292,16 +2333,16 @@ __global__ __launch_bounds__(kBlk) void k_locate_list(DevIndex ix, const uint8_t
                                                       const uint64_t* __restrict__ offs, uint64_t npat,
                                                       uint64_t limit, OnePass op, LongList ll) {
   __shared__ NodeTable T;
-  bool staged = false;
+  __shared__ uint32_t s_t[kBlk], s_n;
   const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-  for (uint64_t r = blockIdx.x; r < regions; r += gridDim.x) {
-    const uint32_t c = ll.cnt2[r];  // uniform over the block
-    if (!c) continue;
-    if (!staged) {
-      load_table(T, ix.table);
-      __syncthreads();
-      staged = true;
-    }
+  list_regions(ll.cnt2, regions, s_t, &s_n);
+  const uint32_t nr = s_n;
+  if (!nr) return;  // uniform over the block
+  load_table(T, ix.table);
+  __syncthreads();
+  for (uint32_t e = 0; e < nr; ++e) {
+    const uint64_t r = blockIdx.x + (uint64_t)s_t[e] * gridDim.x;
+    const uint32_t c = ll.cnt2[r];
     for (uint32_t i = threadIdx.x; i < c; i += kBlk) {
       const uint64_t q = r * kLongRegion + ll.list2[r * kLongRegion + i];
       const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
@@ -3839,9 +3880,15 @@ struct LongBufs {
   }
 };
 
-// blocks of the long-pattern kernels walking the lists (long_patterns): two rounds of the
-// blocks resident at 5 waves per SIMD (256 CUs x 5 blocks of 4 waves)
+// blocks of the kernels walking the region lists (list_regions): two rounds of the blocks
+// resident at 5 waves per SIMD (256 CUs x 5 blocks of 4 waves), and at least regions / kBlk
+// so that a block's regions fit one load per thread
 constexpr unsigned kLongListGrid = 2560;
+unsigned long_list_grid(uint64_t npat) {
+  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
+  const uint64_t g = std::max<uint64_t>(std::min<uint64_t>(regions, kLongListGrid), (regions + kBlk - 1) / kBlk);
+  return (unsigned)std::max<uint64_t>(g, 1);
+}
 
 // k_count_long over the batch (from_list: the staged kernel's lists in ll), then k_count_list
 // over what it could not finish.  skip_short (twin): every pattern read, only the long ones
@@ -3859,31 +3906,30 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
     if (s != CS_OK) return s;
     ll = own.ll;
   }
-  const bool from_list = routed != nullptr;
-  const unsigned g = from_list ? std::min(grid_for(npat, kLongRegion, 0xFFFFFFFFu), kLongListGrid)
-                               : grid_for(npat, kBlk, 0xFFFFFFFFu);
+  const unsigned g = routed ? long_list_grid(npat) : grid_for(npat, kBlk, 0xFFFFFFFFu);
   // tuning hook CS_FM_LONG_V16 (read per call): 0 = 8-B pattern / window loads, 3 = 16-B
   // vectors for the pattern's packed part and the window (the default: C4 150-mers 1.87 ->
   // 1.55 ms, 64-mers 1.25 -> 1.16-1.21, profiles/r03/long_probe_v16.json), 1 / 2 = partial forms
   const char* ev = std::getenv("CS_FM_LONG_V16");
   const int v16 = ev ? std::atoi(ev) : 3;
-  if (ix.ptext && !byte_text && v16 == 1)
-    k_count_long<0, true, kBytes, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
-                                                         skip_short);
+  if (routed && ix.ptext && !byte_text && v16 == 3)  // the routed default
+    k_count_long<0, true, kBytes, 3, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+  else if (routed && ix.ptext && !byte_text)
+    k_count_long<0, true, kBytes, 0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+  else if (routed)
+    k_count_long<0, false, kBytes, 0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+  else if (ix.ptext && !byte_text && v16 == 1)
+    k_count_long<0, true, kBytes, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   else if (ix.ptext && !byte_text && v16 == 2)
-    k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
-                                                         skip_short);
+    k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   else if (ix.ptext && !byte_text && v16 == 3)
-    k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
-                                                         skip_short);
+    k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   else if (ix.ptext && !byte_text)
-    k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
-                                                      skip_short);
+    k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   else
-    k_count_long<0, false, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, from_list,
-                                                       skip_short);
+    k_count_long<0, false, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   FMX_HIP(hipGetLastError());
-  k_count_list<0, kBytes><<<std::min(grid_for(npat, kLongRegion, 0xFFFFFFFFu), 1024u), kBlk, 0, st>>>(
+  k_count_list<0, kBytes><<<long_list_grid(npat), kBlk, 0, st>>>(
       ix, d_pats, d_offs, npat, co, fixed_m, ll);
   FMX_HIP(hipGetLastError());
   return CS_OK;
@@ -4125,15 +4171,20 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
       k_count_ctx<OccE, U, true, false, 8, false, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
     FMX_HIP(hipGetLastError());
-    const unsigned g1 = routed ? std::min((unsigned)tiles, kLongListGrid) : grid_for(npat, kBlk, 0xFFFFFFFFu);
+    const unsigned g1 = routed ? long_list_grid(npat) : grid_for(npat, kBlk, 0xFFFFFFFFu);
     // tuning hook CS_FM_LONG_V16 (k_count_long's): 0 = 8-B pattern / window loads
     const char* ev = std::getenv("CS_FM_LONG_V16");
-    if (ev && std::atoi(ev) == 0)
-      k_locate_long<0><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll, routed);
+    const bool v0 = ev && std::atoi(ev) == 0;
+    if (routed && v0)
+      k_locate_long<0, true><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
+    else if (routed)
+      k_locate_long<3, true><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
+    else if (v0)
+      k_locate_long<0, false><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
     else
-      k_locate_long<3><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll, routed);
+      k_locate_long<3, false><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
     FMX_HIP(hipGetLastError());
-    k_locate_list<<<std::min((unsigned)tiles, 1024u), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
+    k_locate_list<<<long_list_grid(npat), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
   } else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);

@@ -241,7 +241,9 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
                              uint64_t cap, uint64_t* total, void* stream);
 
 /* Device-resident batch entry points (no host staging, asynchronous on `stream`
- * unless stated). */
+ * unless stated).  d_pats may be NULL when every pattern of the batch is empty (the
+ * count / locate forms then read d_offs[0] and d_offs[npat] back, synchronising `stream`,
+ * and return CS_ERR_INVALID unless they are equal). */
 cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
                                    void* stream);

@@ -33,7 +33,7 @@ cfg_args() {
     c2) echo "--text-bytes 99999999 --batch 1000000" ;;
     c3) echo "--kind bytes --text-bytes 999999999 --m 8 --batch 10000000" ;;
     c4) echo "" ;;
-    c5) echo "--text-bytes 31999999999 --no-cpu" ;;
+    c5) echo "--text-bytes 31999999999" ;;
     *) echo "unknown config $1" >&2; return 1 ;;
   esac
 }

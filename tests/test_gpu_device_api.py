@@ -103,6 +103,32 @@ def test_concurrent_calls_share_nothing_mutable():
     assert not bad, bad[:5]
 
 
+def test_null_pattern_pointer():
+    """A device batch of empty patterns may pass d_pats = NULL (count("") = n, locate("") =
+    {}, fm_index.cpp:80, :109); with a non-empty pattern a NULL d_pats is CS_ERR_INVALID
+    (ADVICE r03)."""
+    pkg = load_pkg()
+    t = O.gen_dna(4, 5000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    st = torch.cuda.current_stream().cuda_stream
+    for offs, ok in (([7, 7, 7, 7], True), ([0, 0, 3, 3], False)):
+        d_o = _dev(np.array(offs, np.int64), torch.int64)
+        d_c = torch.full((3,), -1, dtype=torch.int64, device="cuda")
+        if ok:
+            g.count_batch_device(0, d_o.data_ptr(), 3, d_c.data_ptr(), st)
+            torch.cuda.synchronize()
+            assert d_c.cpu().tolist() == [len(t)] * 3
+            d_oo = torch.full((4,), -1, dtype=torch.int64, device="cuda")
+            tot, done = g.locate_device(0, d_o.data_ptr(), 3, 10, d_oo.data_ptr(), 0, 0, st)
+            assert done and tot == 0 and d_oo.cpu().tolist() == [0, 0, 0, 0]
+        else:
+            with pytest.raises(RuntimeError, match="null batch pointer"):
+                g.count_batch_device(0, d_o.data_ptr(), 3, d_c.data_ptr(), st)
+            d_oo = torch.zeros(4, dtype=torch.int64, device="cuda")
+            with pytest.raises(RuntimeError, match="null batch pointer"):
+                g.locate_device(0, d_o.data_ptr(), 3, 10, d_oo.data_ptr(), 0, 0, st)
+
+
 def test_long_routing_concurrent_streams():
     """Long-pattern routing inside the call (fm_device.hpp LongList): the
     staged kernel lists the patterns its one read cannot answer and k_count_long /
