@@ -110,8 +110,10 @@ FOOT_RUNGS = [
      dict(_OFF, CS_FM_WALK="1", CS_FM_PREFIX_K="", CS_FM_LCTX="")),
     ("context_records", "+ context records (count: one read)",
      dict(_OFF, CS_FM_WALK="1", CS_FM_PREFIX_K="", CS_FM_LCTX="", CS_FM_CTX_RECORDS="")),
-    ("full", "+ full suffix array and the text (the default build: locate one SA read, "
-     "extract a copy)", {}),
+    ("full_sa_text", "+ full suffix array and the text (locate one SA read after the record, "
+     "extract a copy)", {"CS_FM_LOC_RECORDS": "0"}),
+    ("full", "+ locate records (the default build, round 4: a Q_text 20-mer's position in one "
+     "16-B read)", {}),
 ]
 
 

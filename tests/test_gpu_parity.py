@@ -1044,8 +1044,8 @@ def test_locate_records(pkg):
     row order and against the same call without them (CS_Q_NO_LOC_RECORDS): a DNA text with
     40-base pieces copied 2-7 times (so (k+1)-mers have 0..7+ rows) and a few N, every pattern
     length from k-1 to k+7 (text substrings, one-character mutants, uniform), limits 1, 2 and
-    100000.  Built with 16-B context records (CS_FM_CTX_RECORDS=16, their precondition); the
-    variants without the records' other preconditions skip."""
+    100000.  Built with 16-B and with 32-B context records (CS_FM_CTX_RECORDS=16 / 1, their
+    precondition); the variants without the records' other preconditions skip."""
     rng = np.random.default_rng(5)
     t = bytearray(O.gen_dna(77, 199_999)[:-1].tobytes())
     for c in range(400):
@@ -1057,22 +1057,29 @@ def test_locate_records(pkg):
     for i in rng.integers(0, len(t), 12):
         t[int(i)] = ord("N")
     t = bytes(t) + b"$"
-    with _env(CS_FM_CTX_RECORDS="16"):
-        g = pkg.FMIndex.build_from_text(t, pkg.BuildParams())
-    info = g.info()
-    if not info.locate_record_bytes:
-        pytest.skip("this variant builds no locate records")
-    assert info.record_bytes == 16 and info.locate_record_bytes == 16 * 4 ** (info.prefix_k + 1)
     o = O.Index(t)
-    K = info.prefix_k
-    pats = []
-    for m in range(max(1, K - 1), K + 8):
-        pats += _substrings_and_mutants(t, (m,), 150, m)
-        pats += [bytes(p) for p in O.gen_patterns_uniform(b"ACGT", m, 20, seed=m)]
-    for lim in (1, 2, 100000):
-        want = [o.locate(p, limit=lim) for p in pats]
-        assert _locate_one(g, pats, lim) == want, lim
-        assert _locate_one(g, pats, lim, pkg.Q_NO_LOC_RECORDS) == want, lim
+    built_any = False
+    for rec in ("16", "1"):  # compact 16-B context records (C4), 32-B ones (C2)
+        with _env(CS_FM_CTX_RECORDS=rec):
+            g = pkg.FMIndex.build_from_text(t, pkg.BuildParams())
+        info = g.info()
+        if not info.locate_record_bytes:
+            continue
+        built_any = True
+        assert info.record_bytes == (16 if rec == "16" else 32)
+        assert info.locate_record_bytes == 16 * 4 ** (info.prefix_k + 1)
+        K = info.prefix_k
+        pats = []
+        for m in range(max(1, K - 1), K + 8):
+            pats += _substrings_and_mutants(t, (m,), 150, m)
+            pats += [bytes(p) for p in O.gen_patterns_uniform(b"ACGT", m, 20, seed=m)]
+        for lim in (1, 2, 100000):
+            want = [o.locate(p, limit=lim) for p in pats]
+            assert _locate_one(g, pats, lim) == want, (rec, lim)
+            assert _locate_one(g, pats, lim, pkg.Q_NO_LOC_RECORDS) == want, (rec, lim)
+        del g
+    if not built_any:
+        pytest.skip("this variant builds no locate records")
 
 
 @pytest.mark.parametrize("name", ["dna_5k", "bytes_5k", "all_same", "runs", "rare_N_41", "banana"])
