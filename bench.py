@@ -68,6 +68,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # measured random-read ceiling of MI355X: profiles/microbench/gather_bench.hip, 8..32-B
 # random reads over a 4 GB table at 49-52 G accesses/s (profiles/r01/gather_bench*.txt)
 RANDOM_CEIL = 5.0e10
+# the same microbenchmark by table size and read width (profiles/r01, r02, r04 gather_bench_*g
+# .txt, `indep`, grid 8192): random reads are dearer over larger tables (address translation
+# reach), so a leg's accesses are set against the ceiling of the structure they hit — the
+# record table (16 B) for the headline, the 2-GB occurrence lines (32-B lines) for the
+# reference's loop
+RANDOM_CEIL_BY_GB = {16: ((4, 51.9e9), (17, 48.0e9), (32, 47.2e9), (34, 48.6e9), (69, 47.1e9)),
+                     32: ((4, 48.6e9), (17, 39.1e9), (32, 38.5e9), (34, 38.4e9), (69, 38.0e9))}
+
+
+def random_ceiling(table_bytes, width):
+    """The measured random-read rate for `width`-byte reads over a table of `table_bytes`
+    (nearest measured size below, else the smallest); None = RANDOM_CEIL."""
+    pts = RANDOM_CEIL_BY_GB.get(16 if width and width <= 16 else 32)
+    if not table_bytes or not pts:
+        return RANDOM_CEIL
+    gb = table_bytes / 1e9
+    below = [r for g, r in pts if g <= gb * 1.05]
+    return below[-1] if below else pts[0][1]
 # the count kernel's access mix without its logic — per access one random 16-B read from a
 # 17-GB table + 32 B streamed in + 8 B streamed out (gather_bench k_mixed,
 # profiles/r02/gather_bench_mixed_17g.txt): 33.4-33.6 G accesses/s
@@ -314,10 +332,12 @@ def dram_basis(alg, stream_read, accesses, pmc):
     return alg, accesses, "algorithmic"
 
 
-def roofline(alg_random, alg_stream, accesses, kern_s, B, pmc, stream_read=None):
-    """pmc: pmc_traffic()'s dict (traffic + whether its profile matches this kernel)."""
+def roofline(alg_random, alg_stream, accesses, kern_s, B, pmc, stream_read=None, table=None):
+    """pmc: pmc_traffic()'s dict (traffic + whether its profile matches this kernel);
+    table: (bytes, read width) of the structure the random reads hit."""
     alg = alg_random + alg_stream
     fb, acc, basis = dram_basis(alg, stream_read, accesses, pmc)
+    ceil = random_ceiling(*table) if table else RANDOM_CEIL
     achieved = fb / kern_s / 1e9
     return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, **pmc, "basis": basis,
@@ -329,8 +349,9 @@ def roofline(alg_random, alg_stream, accesses, kern_s, B, pmc, stream_read=None)
             "random_accesses_per_launch": acc,
             "random_accesses_per_query": acc / B,
             "random_accesses_per_s": acc / kern_s,
-            "random_access_ceiling_per_s": RANDOM_CEIL,
-            "frac_of_random_access_ceiling": acc / kern_s / RANDOM_CEIL,
+            "random_access_ceiling_per_s": ceil,
+            "random_access_table_bytes": table[0] if table else None,
+            "frac_of_random_access_ceiling": acc / kern_s / ceil,
             "access_mix_ceiling_per_s": MIXED_CEIL,
             "frac_of_access_mix_ceiling": acc / kern_s / MIXED_CEIL}
 
@@ -344,13 +365,18 @@ def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, ste
         stream_read = W.B * W.m + (W.B + 1) * 8
     wall, kern_s, kmin = time_launches(launch, steps, warmup, stream)
     rnd, acc, frac = W.accounting(idx, info, flags, sh, dev)
+    # the structure most random reads hit: the rank lines when the search steps (the whole
+    # loop, no contexts, no verification), else the table of context records / entries
+    steps_mostly = flags & (1 | 2 | 16)
+    table = ((info.rank_bytes, info.line_bytes) if steps_mostly or not info.prefix_bytes
+             else (info.prefix_bytes, info.record_bytes or 8))
     got = read_counts()
     out = {"what": what, "workload_key": wl_key, "patterns": W.B, "m": W.m, "flags": flags,
            "ms_per_launch": wall * 1e3, "kernel_ms_mean": kern_s * 1e3, "kernel_ms_min": kmin,
            "patterns_per_s": W.B / kern_s, "prefix_table_hit_frac": frac,
            "matches_headline": None if ref_counts is None else bool(np.array_equal(got, ref_counts)),
            "roofline": roofline(rnd, stream_bytes, acc, kern_s, W.B, pmc_traffic(wl_key, name, kern_s),
-                                stream_read)}
+                                stream_read, table)}
     return out, got
 
 
@@ -442,6 +468,9 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
         stream_rd = 16 * B if walk_lines else 8 * tot
     wpmc = pmc_traffic(wl_key, name, walk_s)
     wb, wreads, wbasis = dram_basis(alg, stream_rd, reads, wpmc)
+    # the structure the dependent reads hit: the suffix array, the walk lines, or the rank lines
+    wceil = random_ceiling(*((info.full_sa_bytes, 16) if uses_sa else
+                             (info.walk_bytes, 32) if walk_lines else (info.rank_bytes, info.line_bytes)))
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl,
             "phase1_ms": min(t1s) * 1e3, "phase2_ms": walk_s * 1e3, "limit": limit,
@@ -453,7 +482,8 @@ def locate_leg(name, what, idx, info, wl_key, W, text, flags, dev, sh, reps=3, l
                               "alg_bytes": alg, "alg_bytes_per_position": alg / max(tot, 1),
                               **wpmc, "alg_dependent_reads": reads,
                               "dependent_reads_per_s": wreads / walk_s,
-                              "frac_of_random_access_ceiling": wreads / walk_s / RANDOM_CEIL}}
+                              "random_access_ceiling_per_s": wceil,
+                              "frac_of_random_access_ceiling": wreads / walk_s / wceil}}
 
 
 def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limit=100000):
@@ -516,6 +546,7 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
     stream_rd = B * m + (B + 1) * 8 + B * 12  # patterns, offsets, the search's results read back
     lpmc = pmc_traffic(wl_key, name, min(evs))
     fb, reads, basis = dram_basis(alg, stream_rd, acc, lpmc)
+    lceil = random_ceiling(info.locate_record_bytes or info.prefix_bytes, 16)
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl, "limit": limit,
             "event_ms": min(evs) * 1e3, "positions_verified": okv,
@@ -526,7 +557,8 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
                          "alg_random_bytes_per_launch": rnd, "alg_stream_bytes_per_launch": stream_b,
                          "stream_read_bytes_per_launch": stream_rd, "alg_random_accesses_per_launch": acc,
                          **lpmc, "random_accesses_per_s": reads / tl,
-                         "frac_of_random_access_ceiling": reads / tl / RANDOM_CEIL}}
+                         "random_access_ceiling_per_s": lceil,
+                         "frac_of_random_access_ceiling": reads / tl / lceil}}
 
 
 def stream_leg(name, what, idx, W, dev, sh, ref_counts, chunks=10, packed=False, u8=False):
@@ -961,7 +993,9 @@ def main():
         stream_b = B * m + (B + 1) * 8 + B * 8  # patterns, offsets, uint64 counts
         if rank == 0:
             rf = roofline(rnd, stream_b, acc, kern_avg_s, B, pmc_traffic(wl, "count", kern_avg_s),
-                          B * m + (B + 1) * 8)
+                          B * m + (B + 1) * 8,
+                          (info.prefix_bytes, info.record_bytes or 8) if info.prefix_bytes
+                          else (info.rank_bytes, info.line_bytes))
             rf.update({"line_bytes": info.line_bytes, "prefix_k": info.prefix_k,
                        "prefix_table_hit_frac": frac, "context_q": info.context_q,
                        # SURVEY.md §8(d)'s per-query figure for the reference's structure

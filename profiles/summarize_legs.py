@@ -68,7 +68,7 @@ def short(name):
             return "k_count_ctx_loc"
         return "k_count_ctx%s%s_w%s" % ("_packed" if packed == "true" else "",
                                          "_skiplong" if skip == "true" else "", w)
-    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?(?:, \d+)?>", name)
+    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?(?:, \d+)?(?:, (true|false))?>", name)
     if m:  # the third argument: the measurement twin (kBytes)
         return "k_count_long%s%s" % ("_ptext" if m.group(2) == "true" else "_btext",
                                      "_bytes" if m.group(3) == "true" else "")
