@@ -73,8 +73,10 @@ RANDOM_CEIL = 5.0e10
 # reach), so a leg's accesses are set against the ceiling of the structure they hit — the
 # record table (16 B) for the headline, the 2-GB occurrence lines (32-B lines) for the
 # reference's loop
-RANDOM_CEIL_BY_GB = {16: ((4, 51.9e9), (17, 48.0e9), (32, 47.2e9), (34, 48.6e9), (69, 47.1e9)),
-                     32: ((4, 48.6e9), (17, 39.1e9), (32, 38.5e9), (34, 38.4e9), (69, 38.0e9))}
+RANDOM_CEIL_BY_GB = {16: ((1, 54.3e9), (2, 53.2e9), (4, 51.9e9), (17, 48.0e9), (32, 47.2e9), (34, 48.6e9),
+                          (69, 47.1e9)),
+                     32: ((1, 54.0e9), (2, 53.5e9), (4, 48.6e9), (17, 39.1e9), (32, 38.5e9), (34, 38.4e9),
+                          (69, 38.0e9))}
 
 
 def random_ceiling(table_bytes, width):

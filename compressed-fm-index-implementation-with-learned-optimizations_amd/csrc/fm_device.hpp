@@ -205,20 +205,29 @@ __device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint6
 
 // Long-pattern routing inside one call (fm_query.hip launch_count_staged / the one-call
 // locate): the staged kernel leaves the patterns its one read cannot answer (m >= kFastM and
-// m > k + kCtxQ) to the long-pattern kernel launched behind it on the same stream.  Block b
-// of the staged kernel (its kLongRegion patterns) lists them in region b of `list` — the
-// pattern's offset inside the region (u16), the number in cnt[b] — and zeroes cnt2[b];
-// the long-pattern kernel walks the regions (lengths read on the device), and what it cannot
-// finish goes to region lists `list2` / `cnt2` for the general-search kernel after it.  No
-// host synchronisation and no state in the handle: every list is the call's own buffer, so
-// concurrent calls on other streams cannot interfere.  All null: no routing.
+// m > k + kCtxQ) to the long-pattern kernel launched behind it on the same stream.  Lists
+// are per wave of the staged kernel, so no block barrier orders them: wave w of block b
+// (its 128 patterns b kLongRegion + {64 w + l, kBlk + 64 w + l : l < 64}) owns slot
+// 4 b + w and lists its long patterns there — each pattern's offset inside the block's
+// region (u16) at list[slot kLongSlot + i], the number in cnt[slot] (a ballot orders them) —
+// and zeroes cnt2[slot]; the list kernels read every slot's length on the device and take
+// the entries of their slots flattened (all lanes busy), and what they cannot finish goes
+// to the slot lists `list2` / `cnt2` of the pattern for the general-search kernel after
+// them.  No host synchronisation and no state in the handle: every list is the call's own
+// buffer, so concurrent calls on other streams cannot interfere.  All null: no routing.
 constexpr uint32_t kLongRegion = 512;  // = 2 kBlk: the staged kernels' patterns per block (U = 2)
+constexpr uint32_t kLongSlot = 128;    // a wave's patterns (64 lanes x U = 2): one slot
+constexpr uint32_t kSlotsPerRegion = kLongRegion / kLongSlot;
 struct LongList {
   uint16_t* list = nullptr;
   uint32_t* cnt = nullptr;
   uint16_t* list2 = nullptr;
   uint32_t* cnt2 = nullptr;
 };
+// the slot of pattern q: its block's region, the wave of the lane that holds it
+__host__ __device__ inline uint64_t long_slot(uint64_t q) {
+  return (q / kLongRegion) * kSlotsPerRegion + ((q % kLongRegion) % 256) / 64;
+}
 
 // A single pattern passed by value in kernel arguments (k_count_one).
 struct OnePattern {

@@ -1198,6 +1198,7 @@ struct OnePass {
   uint64_t* wide = nullptr;              // (q, first row) of ranges over kLocSmall rows
   unsigned long long* nwide = nullptr;
   uint64_t wide_cap = 0;
+  uint32_t defer = 0;  // locate records: a pattern its record does not answer -> k_locate_list
 };
 
 // the text position of BWT row `row` by the short walk, and the same for U rows walked in
@@ -1418,6 +1419,24 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(DevIndex ix, OnePass 
   }
 }
 
+// The lanes' patterns j with bit j of `m` set into the wave's slot of a LongList list (their
+// offsets inside the block's region, in ballot order) and their number into cnt[slot] (0
+// when none).  Every lane of the wave, in uniform control flow.
+template <int U = 2>
+__device__ __forceinline__ void wave_list(uint16_t* list, uint32_t* cnt, uint64_t slot, uint32_t m) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const bool b = (m >> j) & 1u;
+    const uint64_t bal = __ballot(b);
+    if (b) list[slot * kLongSlot + n + __popcll(bal & below)] = (uint16_t)(threadIdx.x + j * kBlk);
+    n += __popcll(bal);
+  }
+  if (lane == 0) cnt[slot] = n;
+}
+
 // A 16-B context record: a random read nothing re-reads, through a non-temporal load so it
 // does not displace the pattern stream's lines in the caches (C4 headline 0.394 -> 0.382 ms,
 // four rounds of an A/B in fresh processes on one box: profiles/r03/ab_nt_record_load.jsonl)
@@ -1434,7 +1453,7 @@ __device__ __forceinline__ uint4 load_record16(const void* tab, uint64_t t) {
 // r03 weak item 3; held to 6 it spills 80 VGPRs).
 // kSkipLong: patterns of kFastM characters or more whose search the one read cannot finish
 // (m > k + kCtxQ) are listed for k_count_long / k_locate_long (long-pattern routing inside the
-// call, LongList: region blockIdx.x of ll.list, its length in ll.cnt).
+// call, LongList: each wave lists its own in its slot, so the barrier-free form takes it too).
 template <class E, int U, bool kLoc, bool kPacked, int W, bool kNoBar = false, bool kOne = false,
           bool kSkipLong = false, bool kRng = true, int kPos = 0>
 __global__ __launch_bounds__(kBlk)
@@ -1453,8 +1472,6 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // node table only when one of its patterns needs the general search
   __shared__ uint16_t cmap[256];
   __shared__ NodeTable T;
-  __shared__ uint32_t s_nlong;  // kSkipLong: the block's listed patterns
-  __shared__ uint32_t s_ndef;   // kOne over locate records: the block's deferred patterns
   // count forms: the range [sp, ep) of a pattern the general search finishes (st 5), kept
   // here across the barrier instead of in registers or read again from its table entry
   // (kRng; A/B in one process, profiles/r03/ab_range_across_barrier*.json: headline 0.389
@@ -1462,10 +1479,9 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   __shared__ uint64_t s_rng[kLoc ? 1 : U][kLoc ? 1 : kBlk][2];
   static_assert(kBlk >= 256, "one map entry per thread");
   static_assert(!kOne || (kLoc && !kNoBar), "the one-call locate is a locate with barriers");
-  static_assert(!kSkipLong || (!kNoBar && U * kBlk == kLongRegion), "a block lists one region");
+  static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
-  if (threadIdx.x == 0) s_nlong = s_ndef = 0;
   __syncthreads();
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
   const uint32_t K = ix.ptab_k;
@@ -1479,7 +1495,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // pattern's last k + 1 characters answers it in one read when the pattern has at most
   // kLocRecQ characters before them (lqm bit j: pattern j takes it, at index lt[j])
   constexpr bool kLR = kOne && kPos == 0;
-  uint32_t lt[kLR ? U : 1], lqm = 0;
+  uint32_t lt[kLR ? U : 1], lqm = 0, defm = 0;
   // 0 done, 1 table, 2 context, 3 general search, 4 left to k_count_long, 5 general search
   // from the range after the table (s_rng), 7 left to k_locate_list (a locate record that
   // does not answer it)
@@ -1554,15 +1570,16 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       }
     }
   }
+  // the wave's slot of the call's lists (kSkipLong, and kOne's deferred patterns)
+  const uint64_t slot = (uint64_t)blockIdx.x * kSlotsPerRegion + (threadIdx.x >> 6);
   if constexpr (kSkipLong) {
-    // the long patterns into the block's region of the call's list (k_count_long /
-    // k_locate_long take them): an LDS counter orders them, the count follows the barrier
+    // the long patterns into the wave's slot (k_count_long / k_locate_long take them), in
+    // ballot order; the count forms zero the slot of the general-search list too
+    uint32_t lm = 0;
 #pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (st[j] == 4) {
-        const uint32_t at = atomicAdd(&s_nlong, 1u);
-        ll.list[(uint64_t)blockIdx.x * kLongRegion + at] = (uint16_t)(threadIdx.x + j * kBlk);
-      }
+    for (int j = 0; j < U; ++j) lm |= (uint32_t)(st[j] == 4) << j;
+    wave_list<U>(ll.list, ll.cnt, slot, lm);
+    if (!kOne && (threadIdx.x & 63) == 0) ll.cnt2[slot] = 0;
   }
   if constexpr (kLR) {
     // (B0) the locate records: no match, or one matching row whose SA value the record holds,
@@ -1580,12 +1597,11 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
         mm |= (uint32_t)(i < c && ((a.w >> (8 * i)) & mask) == want2) << i;
       if (c == kLocRecNone || (mm & (mm - 1u))) {
         // more rows, or two or three positions: the context record's window — in
-        // k_locate_list when the call has lists (the block then waits for no second read),
-        // else below
-        if (ll.list2) {
+        // k_locate_list when the call defers them (op.defer: the block then waits for no
+        // second read), else below
+        if (op.defer) {
           st[j] = 7;
-          const uint32_t at = atomicAdd(&s_ndef, 1u);
-          ll.list2[(uint64_t)blockIdx.x * kLongRegion + at] = (uint16_t)(threadIdx.x + j * kBlk);
+          defm |= 1u << j;
         }
         continue;
       }
@@ -1596,6 +1612,10 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
         rv[j] = kLocStash | (v >= j2 ? v - j2 : v + ix.n - j2);
       }
     }
+  }
+  if constexpr (kOne) {
+    // the deferred patterns into the wave's slot of the general-search list (zeroed when none)
+    if (ll.cnt2) wave_list<U>(ll.list2, ll.cnt2, slot, defm);
   }
   // (B) the table entries (whole context records: their contexts come with them)
   uint4 w[U][4];
@@ -1741,10 +1761,6 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       for (int j = 0; j < U; ++j) need |= kc[j] == 1;
     }
     const bool any_need = __syncthreads_or(need);
-    if (threadIdx.x == 0) {  // the block's long and deferred patterns are listed (barrier above)
-      if (kSkipLong) ll.cnt[blockIdx.x] = s_nlong;
-      if (ll.cnt2) ll.cnt2[blockIdx.x] = s_ndef;
-    }
     if (any_need) {
       load_table(T, ix.table);
       __syncthreads();
@@ -1758,10 +1774,6 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     return;
   }
   const bool any_general = __syncthreads_or(general);
-  if (kSkipLong && threadIdx.x == 0) {  // the block's long patterns are listed (barrier above)
-    ll.cnt[blockIdx.x] = s_nlong;
-    ll.cnt2[blockIdx.x] = 0;
-  }
   if (!any_general) return;
   load_table(T, ix.table);
   __syncthreads();
@@ -2100,52 +2112,86 @@ __device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __
 }
 
 // the general search for the patterns a long-pattern kernel does not answer: listed in the
-// region of pattern q (LongList list2 / cnt2; the regions are kLongRegion patterns wide)
+// slot of pattern q (LongList list2 / cnt2: a slot holds at most its kLongSlot patterns, and
+// a pattern is listed there once — by the staged kernel's deferral or here)
 __device__ __forceinline__ void long_list_append(bool general, uint64_t q, const LongList& ll) {
   if (!general) return;
-  const uint64_t r = q / kLongRegion;
-  const uint32_t at = atomicAdd(ll.cnt2 + r, 1u);
-  ll.list2[r * kLongRegion + at] = (uint16_t)(q - r * kLongRegion);
+  const uint64_t sl = long_slot(q);
+  const uint32_t at = atomicAdd(ll.cnt2 + sl, 1u);
+  ll.list2[sl * kLongSlot + at] = (uint16_t)(q % kLongRegion);
 }
 
-// The patterns of one long-pattern launch (kList): the staged kernel's region lists
-// (ll.list / ll.cnt: block b of the grid walks regions b, b + grid, ...; the lengths are read
-// on the device, so an empty list costs the launch).  f(q, active) runs with the whole
-// block in lockstep (active = q is a pattern to search), so f may use wave collectives; the
-// q of every lane of a wave, active or not, lies in one region (= one tile of the one-call
-// locate).  Without a list (CS_Q_LONG, fixed-length batches of long patterns) the kernels
-// take one pattern per lane over a grid covering the batch, as before round 4 (a loop there
-// costs k_count_long 40 VGPRs).
-// The regions of block b that hold patterns: b + t gridDim.x for t < kBlk (the grid is
-// launched with at least regions / kBlk blocks, long_list_grid), their counts read by one load
-// per thread — an empty list costs two barriers, not a chain of dependent loads — and the
-// nonempty ones listed in LDS (s_t[0 .. *s_n)).
-__device__ __forceinline__ void list_regions(const uint32_t* __restrict__ cnt, uint64_t regions,
-                                             uint32_t* s_t, uint32_t* s_n) {
-  if (threadIdx.x == 0) *s_n = 0;
-  __syncthreads();
-  const uint64_t r = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x;
-  if (r < regions && cnt[r]) s_t[atomicAdd(s_n, 1u)] = threadIdx.x;
-  __syncthreads();
+// The patterns of one list launch (kList): the entries of the slots of block b — slots b,
+// b + grid, ... (the grid is launched with at least slots / kBlk blocks, long_list_grid) —
+// their lengths read by one load per thread and scanned in LDS, then taken flattened, kBlk
+// at a time, so every lane has a pattern while the block has any (an empty list costs one
+// load and two barriers).  f(q, active) runs with the whole block in lockstep (active = q is
+// a pattern to search; an inactive lane gets the block's first entry), so f may use wave
+// collectives — a wave's patterns may lie in several regions (tiles).  Returns the block's
+// number of entries (uniform).  Without a list (CS_Q_LONG, fixed-length batches of long
+// patterns) the kernels take one pattern per lane over a grid covering the batch, as before
+// round 4 (a loop there costs k_count_long 40 VGPRs).  c: the length of the thread's slot
+// (slot_count), read before so that a block with nothing listed leaves after one load.
+// slot_count's kFresh: the counts were written in this launch (by this block: the slots a
+// block owns are the same for every thread of one grid) — read at the device's coherence
+// point, past the CU cache another block sharing the line may have filled.
+template <bool kFresh = false>
+__device__ __forceinline__ uint32_t slot_count(const uint32_t* cnt, uint64_t npat) {
+  const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
+  const uint64_t sl = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x;
+  if (sl >= slots) return 0u;
+  if constexpr (kFresh) return __hip_atomic_load(cnt + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return cnt[sl];
 }
 
 template <class F>
-__device__ __forceinline__ void long_list_patterns(const LongList& ll, uint64_t npat, F&& f) {
-  __shared__ uint32_t s_t[kBlk], s_n;
-  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-  list_regions(ll.cnt, regions, s_t, &s_n);
-  const uint32_t nr = s_n;
-  for (uint32_t e = 0; e < nr; ++e) {
-    const uint64_t r = blockIdx.x + (uint64_t)s_t[e] * gridDim.x;
-    const uint32_t c = ll.cnt[r];  // uniform over the block
-    for (uint32_t i0 = 0; i0 < c; i0 += kBlk) {
-      const uint32_t i = i0 + threadIdx.x;
-      const bool act = i < c;
-      // (an inactive lane gets the region's first pattern: same tile, same region)
-      f(r * kLongRegion + (act ? ll.list[r * kLongRegion + i] : 0u), act);
-    }
+__device__ __forceinline__ uint32_t list_for_each(const uint16_t* __restrict__ list, uint32_t c, F&& f) {
+  __shared__ uint32_t s_off[kBlk + 1];
+  __shared__ uint32_t s_w[kBlk / 64];
+  // exclusive scan of the counts over the block
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
   }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < (int)(kBlk / 64); ++w2) {
+    if (w2 < (int)wv) pre += s_w[w2];
+    tot += s_w[w2];
+  }
+  s_off[threadIdx.x] = pre + x - c;
+  if (threadIdx.x == 0) s_off[kBlk] = tot;
+  __syncthreads();
+  for (uint32_t e0 = 0; e0 < tot; e0 += kBlk) {
+    const uint32_t e = e0 + threadIdx.x < tot ? e0 + threadIdx.x : 0u;
+    // the slot holding entry e: the last t with s_off[t] <= e (empty slots share offsets)
+    uint32_t lo = 0, hi = kBlk;  // s_off[lo] <= e < s_off[hi]
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_off[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t s2 = blockIdx.x + (uint64_t)lo * gridDim.x;
+    const uint64_t q = s2 / kSlotsPerRegion * kLongRegion + list[s2 * kLongSlot + (e - s_off[lo])];
+    f(q, e0 + threadIdx.x < tot);
+  }
+  return tot;
 }
+
+// the general search of the list2 entries of a block's slots (defined below)
+template <int W, bool kBytes>
+__device__ __forceinline__ void count_list_general(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
+                                                   const uint64_t* __restrict__ offs, const CountOut& co,
+                                                   uint64_t fixed_m, const LongList& ll, uint32_t c);
+__device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
+                                                    const uint64_t* __restrict__ offs, uint64_t limit,
+                                                    const OnePass& op, const LongList& ll, uint32_t c);
 
 // k_count_long's search of one pattern q (< npat, the batch's offsets or fixed_m)
 template <int W, bool kPT, bool kBytes, int kV16>
@@ -2200,21 +2246,34 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
 }
 
 template <int W, bool kPT, bool kBytes = false, int kV16 = 0, bool kList = false>
-__global__ __launch_bounds__(kBlk) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
+// (list mode held to 4 waves per SIMD: left alone it takes 150 VGPRs, 3 waves — hoisted
+// loop invariants and SGPR spills of the list loop — and C4 150-mers routed took 1.93 ms
+// against 1.71, profiles/r04/ab_lib_r04j_count_m150.jsonl)
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 : 1))) void k_count_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m, LongList ll,
                                                      bool skip_short) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   static_assert(kBlk >= 256, "one map entry per thread");
+  uint32_t c1 = 0;
+  if constexpr (kList) {  // a block with nothing listed leaves after one load
+    c1 = slot_count(ll.cnt, npat);
+    if (!__syncthreads_or(c1 != 0)) return;
+  }
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
   if constexpr (kList) {
-    long_list_patterns(ll, npat, [&](uint64_t q, bool act) {
+    list_for_each(ll.list, c1, [&](uint64_t q, bool act) {
       if (act) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, false, cmap, rare, q);
     });
+    // then the general search of what it listed: the same block owns the same slots of list2,
+    // so no second launch (k_count_list) waits for the grid
+    __shared__ NodeTable T;
+    __syncthreads();
+    count_list_general<W, kBytes>(ix, T, pats, offs, co, fixed_m, ll, slot_count<true>(ll.cnt2, npat));
   } else {
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
     if (q < npat) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, skip_short, cmap, rare, q);
@@ -2235,9 +2294,29 @@ static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns
 // its sum once per region; without a list a wave's 64 patterns lie in one tile.  The patterns
 // it cannot finish (as k_count_long's, and windows whose matches lie too far apart for the
 // record) go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search), :125 (limit).
+// Adds each lane's kc (0: nothing) to op.tiles[tile]: one atomic per distinct tile of the
+// wave (a list launch's wave holds one or two slots' patterns, so one or two tiles; a
+// pattern-per-lane atomic puts 512 same-address atomics on every tile: C4 150-mer locate
+// 2.1 -> 3.4 ms).  Every lane of the wave, in uniform control flow.
+__device__ __forceinline__ void wave_tile_add(uint64_t* tiles, uint64_t tile, uint64_t kc) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t pend = __ballot(kc != 0);
+  while (pend) {
+    const uint32_t l = (uint32_t)__ffsll((unsigned long long)pend) - 1u;
+    const uint64_t t = __shfl(tile, (int)l, 64);
+    const bool in = kc != 0 && tile == t;
+    uint64_t s = in ? kc : 0;
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
+    if (lane == l) atomicAdd(reinterpret_cast<unsigned long long*>(tiles + t), s);
+    pend &= ~__ballot(in);
+  }
+}
+
 // k_locate_long's search of pattern q (mine: q is one to search); every lane of the wave
-// calls it (the wave sums its counts into the tile of its patterns)
-template <int kV16>
+// calls it.  kWaveTile: the wave's 64 patterns lie in one tile (one pattern per lane over the
+// batch), so the wave sums its counts into it; else (lists) wave_tile_add.
+template <int kV16, bool kWaveTile>
 __device__ __forceinline__ void locate_long_one(const DevIndex& ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t limit,
                                                 const OnePass& op, const LongList& ll,
@@ -2279,92 +2358,120 @@ __device__ __forceinline__ void locate_long_one(const DevIndex& ix, const uint8_
     op.cnt[q] = (uint32_t)kc;
     op.rec[q] = rec;
   }
-  uint64_t s = kc;  // the wave's 64 patterns lie in one tile
+  if constexpr (kWaveTile) {
+    uint64_t s = kc;
 #pragma unroll
-  for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
+    for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
+  } else {
+    wave_tile_add(op.tiles, q / kLocTile, kc);
+  }
 }
 
 template <int kV16, bool kList>
-__global__ __launch_bounds__(kBlk) void k_locate_long(DevIndex ix, const uint8_t* __restrict__ pats,
+// (list mode held to 4 waves per SIMD as k_count_long's: routed 150-mers 2.13 -> 1.92 ms,
+// profiles/r04/ab_lib_r04j_locate_m150.jsonl)
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 : 1))) void k_locate_long(DevIndex ix, const uint8_t* __restrict__ pats,
                                                       const uint64_t* __restrict__ offs, uint64_t npat,
                                                       uint64_t limit, OnePass op, LongList ll) {
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
+  uint32_t c1 = 0;
+  if constexpr (kList) {  // a block with nothing listed or deferred leaves after one load
+    c1 = slot_count(ll.cnt, npat);
+    if (!__syncthreads_or(c1 != 0 || slot_count(ll.cnt2, npat) != 0)) return;
+  }
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
   if (threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
   if constexpr (kList) {
-    long_list_patterns(ll, npat, [&](uint64_t q, bool act) {
-      locate_long_one<kV16>(ix, pats, offs, limit, op, ll, cmap, rare, q, act);
+    list_for_each(ll.list, c1, [&](uint64_t q, bool act) {
+      locate_long_one<kV16, false>(ix, pats, offs, limit, op, ll, cmap, rare, q, act);
     });
+    // then the general search of what it listed and the staged search deferred (the same
+    // block owns the same slots of list2: no k_locate_list launch)
+    __shared__ NodeTable T;
+    __syncthreads();
+    locate_list_general(ix, T, pats, offs, limit, op, ll, slot_count<true>(ll.cnt2, npat));
   } else {  // no lane returns early: the wave sums its counts at the end
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-    locate_long_one<kV16>(ix, pats, offs, limit, op, ll, cmap, rare, q, q < npat);
+    locate_long_one<kV16, true>(ix, pats, offs, limit, op, ll, cmap, rare, q, q < npat);
   }
 }
 
 // The patterns k_count_long listed (LongList list2 / cnt2): the general search
-// (count_pattern), the node table staged in LDS by the blocks that have work; block b walks
-// regions b, b + grid, ...  kBytes: k_count_long's measurement twin (the general search's
-// bytes into co.out).
+// (count_pattern), the node table staged in LDS by the blocks that have work; block b takes
+// the entries of slots b, b + grid, ... (list_for_each).  kBytes: k_count_long's measurement
+// twin (the general search's bytes into co.out).
+// the general search of the entries of the block's slots of list2 (c: the thread's slot
+// length, slot_count)
+template <int W, bool kBytes>
+__device__ __forceinline__ void count_list_general(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
+                                                   const uint64_t* __restrict__ offs, const CountOut& co,
+                                                   uint64_t fixed_m, const LongList& ll, uint32_t c) {
+  bool staged = false;
+  list_for_each(ll.list2, c, [&](uint64_t q, bool act) {
+    if (!staged) {  // the first round (uniform): the block has entries
+      load_table(T, ix.table);
+      __syncthreads();
+      staged = true;
+    }
+    if (!act) return;
+    const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
+    if constexpr (kBytes) {
+      uint64_t by = 0;
+      (void)count_pattern<OccE>(ix, T, pats + o0, m, &by);
+      static_cast<uint64_t*>(co.out)[q] = by;
+    } else {
+      store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
+    }
+  });
+}
+
 template <int W, bool kBytes = false>
 __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs, uint64_t npat,
                                                      CountOut co, uint64_t fixed_m, LongList ll) {
   __shared__ NodeTable T;
-  __shared__ uint32_t s_t[kBlk], s_n;
-  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-  list_regions(ll.cnt2, regions, s_t, &s_n);
-  const uint32_t nr = s_n;
-  if (!nr) return;  // uniform over the block
-  load_table(T, ix.table);
-  __syncthreads();
-  for (uint32_t e = 0; e < nr; ++e) {
-    const uint64_t r = blockIdx.x + (uint64_t)s_t[e] * gridDim.x;
-    const uint32_t c = ll.cnt2[r];
-    for (uint32_t i = threadIdx.x; i < c; i += kBlk) {
-      const uint64_t q = r * kLongRegion + ll.list2[r * kLongRegion + i];
-      const uint64_t o0 = offs ? offs[q] : q * fixed_m, m = offs ? offs[q + 1] - o0 : fixed_m;
-      if constexpr (kBytes) {
-        uint64_t by = 0;
-        (void)count_pattern<OccE>(ix, T, pats + o0, m, &by);
-        static_cast<uint64_t*>(co.out)[q] = by;
-      } else {
-        store_count<W>(co, q, count_pattern<OccE>(ix, T, pats + o0, m));
-      }
-    }
-  }
+  const uint32_t c = slot_count(ll.cnt2, npat);
+  if (!__syncthreads_or(c != 0)) return;
+  count_list_general<W, kBytes>(ix, T, pats, offs, co, fixed_m, ll, c);
 }
 
-// The patterns k_locate_long listed: locate's general search (locate_search), its count
-// and record for k_locate_emit, the count added to the pattern's tile; as k_count_list.
+// The patterns k_locate_long listed and the staged search deferred: locate's general search
+// (locate_search), its count and record for k_locate_emit, the count added to the pattern's
+// tile; as k_count_list.
+__device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
+                                                    const uint64_t* __restrict__ offs, uint64_t limit,
+                                                    const OnePass& op, const LongList& ll, uint32_t c) {
+  bool staged = false;
+  list_for_each(ll.list2, c, [&](uint64_t q, bool act) {
+    if (!staged) {
+      load_table(T, ix.table);
+      __syncthreads();
+      staged = true;
+    }
+    uint64_t kc = 0;
+    if (act) {
+      const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+      uint64_t rr = 0;
+      const uint64_t cc = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, rr) : 0;
+      kc = cc < limit ? cc : limit;  // fm_index.cpp:125
+      op.cnt[q] = (uint32_t)kc;
+      op.rec[q] = rr;
+    }
+    wave_tile_add(op.tiles, q / kLocTile, kc);
+  });
+}
+
 __global__ __launch_bounds__(kBlk) void k_locate_list(DevIndex ix, const uint8_t* __restrict__ pats,
                                                       const uint64_t* __restrict__ offs, uint64_t npat,
                                                       uint64_t limit, OnePass op, LongList ll) {
   __shared__ NodeTable T;
-  __shared__ uint32_t s_t[kBlk], s_n;
-  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-  list_regions(ll.cnt2, regions, s_t, &s_n);
-  const uint32_t nr = s_n;
-  if (!nr) return;  // uniform over the block
-  load_table(T, ix.table);
-  __syncthreads();
-  for (uint32_t e = 0; e < nr; ++e) {
-    const uint64_t r = blockIdx.x + (uint64_t)s_t[e] * gridDim.x;
-    const uint32_t c = ll.cnt2[r];
-    for (uint32_t i = threadIdx.x; i < c; i += kBlk) {
-      const uint64_t q = r * kLongRegion + ll.list2[r * kLongRegion + i];
-      const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
-      uint64_t rr = 0;
-      const uint64_t cc = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, rr) : 0;
-      const uint64_t kc = cc < limit ? cc : limit;  // fm_index.cpp:125
-      op.cnt[q] = (uint32_t)kc;
-      op.rec[q] = rr;
-      if (kc) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), kc);
-    }
-  }
+  const uint32_t c = slot_count(ll.cnt2, npat);
+  if (!__syncthreads_or(c != 0)) return;
+  locate_list_general(ix, T, pats, offs, limit, op, ll, c);
 }
 
 // The batch count over the quaternary wavelet matrix with left contexts (C3: sigma = 256,
@@ -3849,15 +3956,17 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
   return launch_count_ex(h, d_pats, d_offs, npat, co, flags, st, fixed_m, false);
 }
 
-// tuning hook CS_FM_COUNT_NOBAR (read per call): 1 = the staged kernel's general search
-// reads the node table through the caches (no block barrier), 0 = a block-wide LDS copy
-// behind a barrier.  A template parameter (a runtime flag kept both general searches in
-// one kernel: 100 VGPRs, 4 waves per SIMD instead of 79 / 6), honoured for the
-// headline form (occurrence lines, two patterns per lane, byte-string patterns) and
-// locate's phase 1.
+// tuning hook CS_FM_COUNT_NOBAR (read per call): 1 (the default since round 4) = the staged
+// kernel's general search reads the node table through the caches (no block barrier: a wave
+// whose patterns are done leaves at once instead of waiting at the barrier for the block's
+// slowest record read), 0 = a block-wide LDS copy behind a barrier.  C4 headline A/B in one
+// process (profiles/r04/ab_nobar.json): 0.417 against 0.456 ms per call.  A template
+// parameter (a runtime flag kept both general searches in one kernel: 100 VGPRs, 4 waves per
+// SIMD instead of 79 / 6), honoured for the byte-string forms (occurrence lines, two patterns
+// per lane; routed or not) and locate's phase 1.
 bool count_nobar() {
   const char* e = std::getenv("CS_FM_COUNT_NOBAR");
-  return e && std::atoi(e) == 1;
+  return !(e && std::atoi(e) == 0);
 }
 
 // test / tuning hook CS_FM_QCTX_STAGED (read per call): 0 = the quaternary matrix counts
@@ -3870,38 +3979,40 @@ bool qctx_staged() {
 // k_count_long over the batch (skip_short: only its long patterns, as k_count_ctx's kSkipLong),
 // then k_count_list over the patterns it listed; byte_text: the byte text even when the
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
-// The call's long-pattern lists (LongList): region lists of the staged kernel (list / cnt,
+// The call's long-pattern lists (LongList): slot lists of the staged kernel (list / cnt,
 // unless `direct`) and of k_count_long / k_locate_long for the general search (list2 / cnt2),
-// u16 offsets inside the regions; in one stream-ordered allocation.  Direct launches (every
-// pattern to the long kernel, no staged kernel before it) zero cnt2 here; otherwise the
-// staged kernel does, block by block.
+// u16 offsets inside the slots' regions; in one stream-ordered allocation.  Direct launches
+// (every pattern to the long kernel, no staged kernel before it) zero cnt2 here; otherwise the
+// staged kernel does, wave by wave.
+static_assert(kLongRegion == 2 * kBlk && kLongSlot == 2 * 64, "a slot is one wave's patterns (U = 2)");
 struct LongBufs {
   StreamBuf buf;
   LongList ll;
   cs_status alloc(uint64_t npat, bool direct, hipStream_t st) {
-    const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion, slots = regions * kLongRegion;
-    const uint64_t lists = (direct ? 1 : 2) * slots * 2, cnts = (direct ? 1 : 2) * regions * 4;
+    const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion, slots = regions * kSlotsPerRegion;
+    const uint64_t entries = slots * kLongSlot;
+    const uint64_t lists = (direct ? 1 : 2) * entries * 2, cnts = (direct ? 1 : 2) * slots * 4;
     FMX_HIP(buf.alloc(lists + cnts, st));
     uint8_t* p = buf.as<uint8_t>();
     ll.list2 = reinterpret_cast<uint16_t*>(p);
     ll.cnt2 = reinterpret_cast<uint32_t*>(p + lists);
     if (!direct) {
-      ll.list = ll.list2 + slots;
-      ll.cnt = ll.cnt2 + regions;
+      ll.list = ll.list2 + entries;
+      ll.cnt = ll.cnt2 + slots;
     } else {
-      FMX_HIP(hipMemsetAsync(ll.cnt2, 0, regions * 4, st));
+      FMX_HIP(hipMemsetAsync(ll.cnt2, 0, slots * 4, st));
     }
     return CS_OK;
   }
 };
 
-// blocks of the kernels walking the region lists (list_regions): two rounds of the blocks
-// resident at 5 waves per SIMD (256 CUs x 5 blocks of 4 waves), and at least regions / kBlk
-// so that a block's regions fit one load per thread
+// blocks of the list kernels (list_for_each): two rounds of the blocks resident at 5 waves
+// per SIMD (256 CUs x 5 blocks of 4 waves), and at least slots / kBlk so that a block's
+// slots fit one load per thread
 constexpr unsigned kLongListGrid = 2560;
 unsigned long_list_grid(uint64_t npat) {
-  const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion;
-  const uint64_t g = std::max<uint64_t>(std::min<uint64_t>(regions, kLongListGrid), (regions + kBlk - 1) / kBlk);
+  const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
+  const uint64_t g = std::max<uint64_t>(std::min<uint64_t>(slots, kLongListGrid), (slots + kBlk - 1) / kBlk);
   return (unsigned)std::max<uint64_t>(g, 1);
 }
 
@@ -3944,9 +4055,11 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
   else
     k_count_long<0, false, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   FMX_HIP(hipGetLastError());
-  k_count_list<0, kBytes><<<long_list_grid(npat), kBlk, 0, st>>>(
-      ix, d_pats, d_offs, npat, co, fixed_m, ll);
-  FMX_HIP(hipGetLastError());
+  if (!routed) {  // (a routed k_count_long searches what it listed itself)
+    k_count_list<0, kBytes><<<long_list_grid(npat), kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, fixed_m, ll);
+    FMX_HIP(hipGetLastError());
+  }
   return CS_OK;
 }
 cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
@@ -3997,20 +4110,24 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   else if (W == 8 && U == 4)
     k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
-  else if (W == 8 && count_nobar())
-    k_count_ctx<OccE, 2, false, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
-                                                                      nullptr, fixed_m);
   else if (d_offs && can_route(h, ix)) {
     // long-pattern routing inside the call: the staged kernel counts the short patterns and
     // lists the long ones, k_count_long (and k_count_list) take them from its lists
     LongBufs lb;
     cs_status s = lb.alloc(npat, false, st);
     if (s != CS_OK) return s;
-    k_count_ctx<OccE, 2, false, false, W, false, false, true><<<g2, kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
+    if (count_nobar())
+      k_count_ctx<OccE, 2, false, false, W, true, false, true><<<g2, kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
+    else
+      k_count_ctx<OccE, 2, false, false, W, false, false, true><<<g2, kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
     FMX_HIP(hipGetLastError());
     return launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, &lb.ll);
-  } else
+  } else if (count_nobar())
+    k_count_ctx<OccE, 2, false, false, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
+                                                                      nullptr, fixed_m);
+  else
     k_count_ctx<OccE, 2, false, false, W><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                 nullptr, fixed_m);
   FMX_HIP(hipGetLastError());
@@ -4176,9 +4293,15 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide_cap = wide_cap;
   FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
-  // locate records: a pattern its record does not answer is left to k_locate_list, so the
-  // search kernel's blocks wait for one read (the records answer C4 Q_text 93 %)
-  const bool defer = kpos == 0 && ix.lrec;
+  // locate records: a pattern its record does not answer reads its context record in the
+  // same lane (the default), or is left to k_locate_list (tuning hook CS_FM_LOC_DEFER=1, read
+  // per call: the search kernel's blocks then wait for one read, but k_locate_list searches
+  // the 7 % of C4 Q_text from scratch — 0.786 against 0.631 ms per call in an A/B in one
+  // process, profiles/r04/ab_defer.json)
+  bool defer = false;
+  if (const char* e = std::getenv("CS_FM_LOC_DEFER"))
+    defer = std::atoi(e) == 1 && kpos == 0 && ix.lrec;
+  op.defer = defer ? 1u : 0u;
   if (long_only || routed || defer) {
     LongBufs lb;
     cs_status ls = lb.alloc(npat, long_only, st);
@@ -4207,7 +4330,8 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
         k_locate_long<3, false><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
       FMX_HIP(hipGetLastError());
     }
-    k_locate_list<<<long_list_grid(npat), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
+    if (!routed)  // (a routed k_locate_long searches what it listed and what was deferred)
+      k_locate_list<<<long_list_grid(npat), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
   } else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);

@@ -38,8 +38,9 @@ ENGINE_VARIANTS = {
     "auto_nosa": {"CS_FM_FULL_SA": "0"},            # locate walks (no full suffix array kept)
     # the same short walks from an expanded rows buffer instead of straight from the records
     "auto_nosa_rows": {"CS_FM_FULL_SA": "0", "CS_FM_WALK_ROWS": "1"},
-    # the staged count / locate kernels' general search without the block barrier
-    "auto_nobar": {"CS_FM_COUNT_NOBAR": "1"},
+    # the staged count / locate kernels' general search behind a block barrier (an LDS
+    # copy of the node table; the default reads it through the caches since round 4)
+    "auto_bar": {"CS_FM_COUNT_NOBAR": "0"},
     "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
     "qwm_unstaged": {"CS_FM_ENGINE": "qwm", "CS_FM_QCTX_STAGED": "0"},  # its count one pattern per lane
@@ -81,15 +82,16 @@ def pkg(request):
             os.environ[k] = v
 
 
-class _nobar:
-    """CS_FM_COUNT_NOBAR=1 for the calls inside (read per call): the staged count
-    kernel's general search without the block barrier.  The auto_nobar variant covers it
-    on occurrence lines; the learned variants re-count under it (the learned lines'
+class _bar:
+    """CS_FM_COUNT_NOBAR=0 for the calls inside (read per call): the staged count
+    kernel's general search behind the block barrier (the default reads the node table
+    through the caches, no barrier, since round 4).  The auto_bar variant covers it on
+    occurrence lines; the learned variants re-count under it (the learned lines'
     instantiation of the same hook)."""
 
     def __enter__(self):
         self.saved = os.environ.get("CS_FM_COUNT_NOBAR")
-        os.environ["CS_FM_COUNT_NOBAR"] = "1"
+        os.environ["CS_FM_COUNT_NOBAR"] = "0"
 
     def __exit__(self, *a):
         if self.saved is None:
@@ -325,7 +327,7 @@ def test_count_every_text_vs_oracle(built, name):
     want = [o.count(p) for p in pats]
     assert g.count_batch(pats).tolist() == want, name
     if _learned():
-        with _nobar():
+        with _bar():
             assert g.count_batch(pats).tolist() == want, name
     for p in pats[::37]:  # single-pattern path (kernel arguments)
         assert g.count(p) == o.count(p), (name, p)
@@ -469,7 +471,7 @@ def test_random_large_vs_oracle(pkg, gen, m):
     assert np.array_equal(got, want)
     assert (got[:20000] >= 1).all()
     if _learned():
-        with _nobar():
+        with _bar():
             assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
     lim = 1000
     woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=lim, nthreads=8)
@@ -1044,7 +1046,8 @@ def test_locate_records(pkg):
     row order and against the same call without them (CS_Q_NO_LOC_RECORDS): a DNA text with
     40-base pieces copied 2-7 times (so (k+1)-mers have 0..7+ rows) and a few N, every pattern
     length from k-1 to k+7 (text substrings, one-character mutants, uniform), limits 1, 2 and
-    100000.  Built with 16-B and with 32-B context records (CS_FM_CTX_RECORDS=16 / 1, their
+    100000; also with the records' misses deferred to k_locate_list (CS_FM_LOC_DEFER=1), routed
+    and not.  Built with 16-B and with 32-B context records (CS_FM_CTX_RECORDS=16 / 1, their
     precondition); the variants without the records' other preconditions skip."""
     rng = np.random.default_rng(5)
     t = bytearray(O.gen_dna(77, 199_999)[:-1].tobytes())
@@ -1077,6 +1080,11 @@ def test_locate_records(pkg):
             want = [o.locate(p, limit=lim) for p in pats]
             assert _locate_one(g, pats, lim) == want, (rec, lim)
             assert _locate_one(g, pats, lim, pkg.Q_NO_LOC_RECORDS) == want, (rec, lim)
+            # the misses deferred to k_locate_list (tuning hook), with and without long routing
+            with _env(CS_FM_LOC_DEFER="1"):
+                assert _locate_one(g, pats, lim) == want, (rec, lim, "defer")
+                with _env(CS_FM_LONG_ROUTE="0"):
+                    assert _locate_one(g, pats, lim) == want, (rec, lim, "defer, unrouted")
         del g
     if not built_any:
         pytest.skip("this variant builds no locate records")
@@ -1154,7 +1162,7 @@ def test_repetitive_text_vs_oracle(pkg):
     assert np.median(want[:3000]) > 100
     assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
     if _learned():  # most searches here take the general path the hook changes
-        with _nobar():
+        with _bar():
             assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
     for lim in (50, 5000):
         sub = pats[::7]
