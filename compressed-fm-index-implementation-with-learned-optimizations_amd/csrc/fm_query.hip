@@ -1256,16 +1256,29 @@ __device__ __forceinline__ void block_scan(const uint64_t* kc, uint64_t* mine, u
 // other blocks' record reads instead of waiting for k_locate_emit; the record then holds
 // kLocStash | position.  (C4 Q_text: 99.6 % of the patterns.)
 constexpr uint64_t kLocStash = 1ull << 62;  // with bit 63 clear: not a window, not a row
-template <int U, int kPos = 0>
+// kWaveTile (the barrier-free search, kPos 0): each wave adds its patterns' total to the tile
+// (zeroed before the launch) instead of a block scan storing it, so no wave waits for the
+// block's others
+template <int U, int kPos = 0, bool kWaveTile = false>
 // skip: bit j set = the lane's j-th pattern is k_locate_long's (routing): its count and record
 // are left for that kernel to write (it adds its count to the tile)
 __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const NodeTable& T, uint64_t npat,
                                                    uint64_t tile, uint64_t q0, const uint64_t* kc,
                                                    const uint64_t* kr, const OnePass& op, uint32_t skip = 0) {
   const uint64_t n = ix.n;
-  uint64_t mine[U], agg, rs[U];
-  block_scan<U>(kc, mine, agg);
-  if (threadIdx.x == 0) op.tiles[tile] = agg;
+  uint64_t rs[U];
+  if constexpr (kWaveTile) {
+    uint64_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < U; ++j) sum += kc[j];
+#pragma unroll
+    for (int dd = 32; dd >= 1; dd >>= 1) sum += __shfl_xor(sum, dd, 64);
+    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + tile), sum);
+  } else {
+    uint64_t mine[U], agg;
+    block_scan<U>(kc, mine, agg);
+    if (threadIdx.x == 0) op.tiles[tile] = agg;
+  }
   uint64_t row[U], adj[U];
   bool one[U];
 #pragma unroll
@@ -1301,49 +1314,65 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
   }
 }
 
-// (2): exclusive scan of the tile totals in place, one block; total -> *total_out.  Each
-// thread scans a contiguous run of tiles in registers (one round of loads, not one per
-// 1024 tiles: 47 -> ~10 us for C4's 24 k tiles), then the block scans the run totals.
+// (2): exclusive scan of the tile totals in place, one block; total -> *total_out.  The
+// tiles pass through LDS 16 k at a time (128 KB + padding: a workgroup may hold 160 KB), so
+// the global loads and stores are coalesced — the round-3 form gave each thread 32
+// consecutive tiles straight from memory (strided loads and stores: 28 us for C4's 24 k
+// tiles) — then each thread scans a contiguous run of 16 in registers and the block scans
+// the run totals.
+__device__ __forceinline__ uint32_t scan_pad(uint32_t i) { return i + (i >> 4); }  // LDS bank spread
 __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tiles, uint64_t ntiles,
                                                      uint64_t* __restrict__ total_out) {
-  constexpr int kRun = 32;  // tiles per thread per round: 32 k tiles per round
+  constexpr int kRun = 16;                     // tiles per thread per round
+  constexpr uint32_t kChunk = 1024u * kRun;    // tiles per round
+  __shared__ uint64_t s_v[kChunk + kChunk / kRun];
   __shared__ uint64_t s_w[16];
   __shared__ uint64_t s_carry;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_carry = 0;
-  __syncthreads();
-  for (uint64_t b = 0; b < ntiles; b += (uint64_t)blockDim.x * kRun) {
-    const uint64_t i0 = b + (uint64_t)threadIdx.x * kRun;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) s_carry = 0;
+  for (uint64_t b = 0; b < ntiles; b += kChunk) {
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {  // coalesced: tile b + r 1024 + t
+      const uint64_t i = b + (uint64_t)r * 1024 + t;
+      s_v[scan_pad(r * 1024u + t)] = i < ntiles ? tiles[i] : 0ull;
+    }
+    __syncthreads();
     uint64_t v[kRun], run = 0;
 #pragma unroll
-    for (int r = 0; r < kRun; ++r) {
-      v[r] = i0 + r < ntiles ? tiles[i0 + r] : 0;
+    for (int r = 0; r < kRun; ++r) {  // the thread's run: tiles b + t kRun + r
+      v[r] = s_v[scan_pad(t * kRun + r)];
       run += v[r];
     }
     uint64_t x = run;  // inclusive scan of the run totals over the wave
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint64_t y = __shfl_up(x, d, 64);
-      if (lane >= d) x += y;
+      if (lane >= (uint32_t)d) x += y;
     }
     if (lane == 63) s_w[wv] = x;
     __syncthreads();
     uint64_t pre = 0, tot = 0;
-    for (int w2 = 0; w2 < (int)(blockDim.x / 64); ++w2) {
-      if (w2 < wv) pre += s_w[w2];
+#pragma unroll
+    for (int w2 = 0; w2 < 16; ++w2) {
+      if (w2 < (int)wv) pre += s_w[w2];
       tot += s_w[w2];
     }
     uint64_t acc = s_carry + pre + x - run;
 #pragma unroll
     for (int r = 0; r < kRun; ++r) {
-      if (i0 + r < ntiles) tiles[i0 + r] = acc;
+      s_v[scan_pad(t * kRun + r)] = acc;
       acc += v[r];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) s_carry += tot;
-    __syncthreads();
+    __syncthreads();  // (every thread has read s_carry and s_w of this round)
+    if (t == 0) s_carry += tot;
+#pragma unroll
+    for (int r = 0; r < kRun; ++r) {
+      const uint64_t i = b + (uint64_t)r * 1024 + t;
+      if (i < ntiles) tiles[i] = s_v[scan_pad(r * 1024u + t)];
+    }
+    __syncthreads();  // before the next round's loads overwrite s_v and its scan reads s_carry
   }
-  if (threadIdx.x == 0) *total_out = s_carry;
+  if (t == 0) *total_out = s_carry;
 }
 
 // (3): offsets and positions of tile blockIdx.x
@@ -1478,7 +1507,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // vs 0.388 ms, 24-mers 1.32 vs 1.40 ms, repetitive DNA 2.56 vs 2.71 ms)
   __shared__ uint64_t s_rng[kLoc ? 1 : U][kLoc ? 1 : kBlk][2];
   static_assert(kBlk >= 256, "one map entry per thread");
-  static_assert(!kOne || (kLoc && !kNoBar), "the one-call locate is a locate with barriers");
+  static_assert(!kOne || (kLoc && (!kNoBar || kPos == 0)), "the one-call locate's walks need barriers");
   static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
@@ -1747,7 +1776,17 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   bool general = false;
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3 || st[j] == 5;
-  if constexpr (kNoBar) {
+  if constexpr (kOne && kNoBar) {
+    // the barrier-free one-call search (kPos 0): the general search reads the node table
+    // through the caches, the tile total is added wave by wave (locate_split_store)
+    if (general)
+      general_rest<E, U, kLoc, kPacked, W, true>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec, kc, kr);
+    uint32_t skip = 0;  // the patterns left to k_locate_long (4) and k_locate_list (7)
+#pragma unroll
+    for (int j = 0; j < U; ++j) skip |= (uint32_t)(st[j] == 4 || st[j] == 7) << j;
+    locate_split_store<U, 0, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
+    return;
+  } else if constexpr (kNoBar) {
     if (general)
       general_rest<E, U, kLoc, kPacked, W>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec, nullptr, nullptr,
                                            &s_rng[0][0][0]);
@@ -2442,6 +2481,122 @@ __global__ __launch_bounds__(kBlk) void k_count_list(DevIndex ix, const uint8_t*
 // The patterns k_locate_long listed and the staged search deferred: locate's general search
 // (locate_search), its count and record for k_locate_emit, the count added to the pattern's
 // tile; as k_count_list.
+// The one-call search of a short pattern (K <= m <= kFastM) whose locate record did not
+// answer it (deferred, CS_FM_LOC_DEFER=1), on its own: k_count_ctx kOne's stages for one
+// pattern — the context record, its inline contexts or the context sector(s), the window —
+// and, for a single position, its SA entry (stashed as the search kernel does); anything
+// else (a wide range, an escaped context, a symbol off the table) locate_search with the LDS
+// node table T.  Returns min(count, limit); rec as k_locate_emit reads it.
+__device__ __forceinline__ uint64_t locate_miss_one(const DevIndex& ix, const NodeTable& T,
+                                                    const uint8_t* __restrict__ pats, uint64_t o0, uint32_t m,
+                                                    uint64_t limit, const uint32_t* sa, uint64_t& rec) {
+  const uint32_t K = ix.ptab_k;
+  bool general = m < K || K == 0 || m > kFastM || !ix.lctx || !ix.lf_exact ||
+                 (ix.ptab_rec != 1 && ix.ptab_rec != 2) || ix.wide;
+  uint64_t res = 0, rv = 0;
+  if (!general) {
+    uint32_t u[8];
+    load_pattern32(pats, o0, m, u);
+    const uint32_t kk = m - K;
+    bool ok = kk <= kCtxQ;
+    uint32_t tt = 0, ww = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kFastM; ++i) {
+      const uint32_t b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      if (i >= m - K && i < m) {
+        const uint32_t d = T.code[b];
+        ok &= d != kNoCode;
+        tt = tt * ix.ptab_sigma + d;
+      } else if (i < kk && i < kCtxQ) {
+        const uint32_t d = T.occ_code[b];
+        ok &= d != kNoCode;
+        ww |= (d & 3u) << (2 * (kk - 1 - i));
+      }
+    }
+    general = !ok;
+    uint64_t sp = 0, ep = 0, bs = 0;
+    uint4 w0 = make_uint4(0, 0, 0, 0), w1 = w0, w2 = w0, w3 = w0;
+    bool inl = false;
+    if (!general) {
+      if (ix.ptab_rec == 1) {
+        const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)tt * 2;
+        const uint4 a = r[0], b2 = r[1];
+        sp = a.x;
+        ep = (uint64_t)a.x + a.y;
+        w0 = make_uint4(a.z, a.w, b2.x, b2.y);
+        w1 = make_uint4(b2.z, b2.w, 0u, 0u);
+        inl = ep - sp <= kRecCtx;
+      } else {
+        const uint4 a = load_record16(ix.ptab, tt);
+        const uint32_t wc = a.y & 15u;
+        sp = rec16_sp(a.x, a.w, 0);
+        inl = wc != kRec16Wide && kk <= kRec16Q;
+        ep = sp + (wc == kRec16Wide ? a.z : wc);
+        if (wc == kRec16Wide && a.z == kRec16NoRange) general = true;
+        uint32_t d[5];
+        rec16_contexts(a.y, a.z, a.w, d);
+        w0 = make_uint4(d[0], d[1], d[2], d[3]);
+        w1 = make_uint4(d[4], 0u, 0u, 0u);
+      }
+    }
+    if (!general && sp < ep && kk == 0) {  // the table part is the whole pattern: its range
+      res = ep - sp;
+      rv = sp;
+    } else if (!general && sp < ep) {
+      if (inl) {
+        bs = sp;
+      } else if (ep - (sp & ~15ull) <= 32) {
+        bs = sp & ~15ull;
+        const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) + bs);
+        w0 = p[0];
+        w1 = p[1];
+        if (ep - bs > 16) {
+          w2 = p[2];
+          w3 = p[3];
+        }
+      } else {
+        general = true;
+      }
+    }
+    if (!general && sp < ep && kk != 0) {
+      const uint32_t mask = ((1u << (2 * kk)) - 1u) | kCtxEsc;
+      const uint32_t lo = (uint32_t)(sp - bs), hi = (uint32_t)(ep - bs);
+      const uint32_t dw[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
+                               w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+      uint32_t match = 0, esc = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        match |= (uint32_t)((e & mask) == ww) << i;
+        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+      }
+      const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      const uint32_t mm = match & in;
+      if (esc & in) {
+        general = true;
+      } else if (mm) {
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u, rel = mm >> f;
+        if (rel >> kLocSpanBits) general = true;
+        else {
+          rv = kLocCtx | ((uint64_t)kk << 60) | ((uint64_t)rel << 38) | (bs + f);
+          res = (uint64_t)__popc(mm);
+        }
+      }
+    }
+  }
+  if (general) res = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, rv) : 0;
+  const uint64_t kc = res < limit ? res : limit;  // fm_index.cpp:125
+  if (kc == 1 && sa) {  // the one position now, as locate_split_store does
+    uint64_t row = rv, adj = 0;
+    uint32_t rel;
+    if (rv & kLocCtx) loc_window(rv, row, adj, rel);
+    const uint64_t p = load_sa(sa, row);
+    rv = kLocStash | (p >= adj ? p - adj : p + ix.n - adj);
+  }
+  rec = rv;
+  return kc;
+}
+
 __device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs, uint64_t limit,
                                                     const OnePass& op, const LongList& ll, uint32_t c) {
@@ -2456,8 +2611,12 @@ __device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTabl
     if (act) {
       const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
       uint64_t rr = 0;
-      const uint64_t cc = m && ix.n ? locate_search<OccE>(ix, T, pats + o0, m, rr) : 0;
-      kc = cc < limit ? cc : limit;  // fm_index.cpp:125
+      if (m <= kFastM) {  // a pattern the staged search deferred (its locate record missed)
+        kc = locate_miss_one(ix, T, pats, o0, (uint32_t)m, limit, op.sa, rr);
+      } else {
+        const uint64_t cc = ix.n ? locate_search<OccE>(ix, T, pats + o0, m, rr) : 0;
+        kc = cc < limit ? cc : limit;  // fm_index.cpp:125
+      }
       op.cnt[q] = (uint32_t)kc;
       op.rec[q] = rr;
     }
@@ -3959,11 +4118,12 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
 // tuning hook CS_FM_COUNT_NOBAR (read per call): 1 (the default since round 4) = the staged
 // kernel's general search reads the node table through the caches (no block barrier: a wave
 // whose patterns are done leaves at once instead of waiting at the barrier for the block's
-// slowest record read), 0 = a block-wide LDS copy behind a barrier.  C4 headline A/B in one
-// process (profiles/r04/ab_nobar.json): 0.417 against 0.456 ms per call.  A template
-// parameter (a runtime flag kept both general searches in one kernel: 100 VGPRs, 4 waves per
-// SIMD instead of 79 / 6), honoured for the byte-string forms (occurrence lines, two patterns
-// per lane; routed or not) and locate's phase 1.
+// slowest record read), 0 = a block-wide LDS copy behind a barrier.  C4 headline A/Bs in one
+// process: 0.417 against 0.456 ms per call unrouted (profiles/r04/ab_nobar_unrouted.json),
+// 0.401 against 0.413 back to back routed (ab_nobar_b2b.json).  A template parameter (a
+// runtime flag kept both general searches in one kernel: 100 VGPRs, 4 waves per SIMD instead
+// of 79 / 6), honoured for the two-patterns-per-lane forms over occurrence lines and learned
+// lines (byte strings, routed or not, and 2-bit packed) and locate's phase 1.
 bool count_nobar() {
   const char* e = std::getenv("CS_FM_COUNT_NOBAR");
   return !(e && std::atoi(e) == 0);
@@ -3988,12 +4148,17 @@ static_assert(kLongRegion == 2 * kBlk && kLongSlot == 2 * 64, "a slot is one wav
 struct LongBufs {
   StreamBuf buf;
   LongList ll;
-  cs_status alloc(uint64_t npat, bool direct, hipStream_t st) {
+  static uint64_t bytes(uint64_t npat, bool direct) {
+    const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
+    return (direct ? 1 : 2) * slots * (kLongSlot * 2 + 4);
+  }
+  // into the call's own allocation (`at`, bytes(npat, direct) of it), or one of its own
+  cs_status alloc(uint64_t npat, bool direct, hipStream_t st, void* at = nullptr) {
     const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion, slots = regions * kSlotsPerRegion;
     const uint64_t entries = slots * kLongSlot;
-    const uint64_t lists = (direct ? 1 : 2) * entries * 2, cnts = (direct ? 1 : 2) * slots * 4;
-    FMX_HIP(buf.alloc(lists + cnts, st));
-    uint8_t* p = buf.as<uint8_t>();
+    const uint64_t lists = (direct ? 1 : 2) * entries * 2;
+    if (!at) FMX_HIP(buf.alloc(bytes(npat, direct), st));
+    uint8_t* p = at ? static_cast<uint8_t*>(at) : buf.as<uint8_t>();
     ll.list2 = reinterpret_cast<uint16_t*>(p);
     ll.cnt2 = reinterpret_cast<uint32_t*>(p + lists);
     if (!direct) {
@@ -4092,9 +4257,15 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   }();
   const bool lo = h->line_fmt == kFmtLOcc;
   const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
-  if (packed && lo)
+  if (packed && lo && count_nobar())
+    k_count_ctx<LOccE, 2, false, true, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
+                                                                      nullptr, fixed_m);
+  else if (packed && lo)
     k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                 nullptr, fixed_m);
+  else if (packed && count_nobar())
+    k_count_ctx<OccE, 2, false, true, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
+                                                                     nullptr, fixed_m);
   else if (packed)
     k_count_ctx<OccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                nullptr, fixed_m);
@@ -4275,10 +4446,21 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   const bool long_only = lk && (flags & CS_Q_LONG);
   const bool routed = lk && !long_only && can_route(h, ix);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
+  // locate records: a pattern its record does not answer reads its context record in the
+  // same lane (the default), or is left to k_locate_list (tuning hook CS_FM_LOC_DEFER=1, read
+  // per call: the search kernel's blocks then wait for one read, but k_locate_list searches
+  // the 7 % of C4 Q_text from scratch — 0.786 against 0.631 ms per call in an A/B in one
+  // process, profiles/r04/ab_defer.json)
+  bool defer = false;
+  if (const char* e = std::getenv("CS_FM_LOC_DEFER"))
+    defer = std::atoi(e) == 1 && kpos == 0 && ix.lrec;
   StreamBuf ws;
   const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
   const uint64_t lo = (npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull;
-  FMX_HIP(ws.alloc(lo, st));
+  // (the long-pattern lists, when the call has them, in the same allocation: one
+  // stream-ordered allocation per call, not two)
+  const bool lists = long_only || routed || defer;
+  FMX_HIP(ws.alloc(lo + (lists ? LongBufs::bytes(npat, long_only) : 0), st));
   OnePass op;
   op.rec = ws.as<uint64_t>();
   op.tiles = op.rec + npat;
@@ -4291,25 +4473,28 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.out_pos = d_out_pos;
   op.cap = d_out_pos ? cap : 0;
   op.wide_cap = wide_cap;
-  FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
+  // the barrier-free search (CS_FM_COUNT_NOBAR, kPos 0) adds its tile totals: the tiles are
+  // zeroed with the wide-range counter behind them
+  const bool nobar = kpos == 0 && count_nobar();
+  FMX_HIP(hipMemsetAsync(nobar ? op.tiles : op.tiles + tiles, 0, (nobar ? tiles * 8 : 0) + 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
-  // locate records: a pattern its record does not answer reads its context record in the
-  // same lane (the default), or is left to k_locate_list (tuning hook CS_FM_LOC_DEFER=1, read
-  // per call: the search kernel's blocks then wait for one read, but k_locate_list searches
-  // the 7 % of C4 Q_text from scratch — 0.786 against 0.631 ms per call in an A/B in one
-  // process, profiles/r04/ab_defer.json)
-  bool defer = false;
-  if (const char* e = std::getenv("CS_FM_LOC_DEFER"))
-    defer = std::atoi(e) == 1 && kpos == 0 && ix.lrec;
   op.defer = defer ? 1u : 0u;
   if (long_only || routed || defer) {
     LongBufs lb;
-    cs_status ls = lb.alloc(npat, long_only, st);
+    cs_status ls = lb.alloc(npat, long_only, st, ws.as<uint8_t>() + lo);
     if (ls != CS_OK) return ls;
-    if (long_only)
+    if (long_only && !nobar)
       FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8, st));
+    else if (long_only)
+      ;
+    else if (routed && nobar)
+      k_count_ctx<OccE, U, true, false, 8, true, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
     else if (routed)
       k_count_ctx<OccE, U, true, false, 8, false, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
+          ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
+    else if (nobar)
+      k_count_ctx<OccE, U, true, false, 8, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
     else
       k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
@@ -4332,7 +4517,10 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
     }
     if (!routed)  // (a routed k_locate_long searches what it listed and what was deferred)
       k_locate_list<<<long_list_grid(npat), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
-  } else if (kpos == 0)
+  } else if (kpos == 0 && nobar)
+    k_count_ctx<OccE, U, true, false, 8, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else if (kpos == 1)
