@@ -79,6 +79,9 @@ RANDOM_CEIL_BY_GB = {16: ((1, 54.3e9), (2, 53.2e9), (4, 51.9e9), (17, 48.0e9), (
                           (69, 38.0e9))}
 
 
+HOT_TABLE_BYTES = 1 << 30  # the smallest table measured: the best random-read rate
+
+
 def random_ceiling(table_bytes, width):
     """The measured random-read rate for `width`-byte reads over a table of `table_bytes`
     (nearest measured size below, else the smallest); None = RANDOM_CEIL."""
@@ -329,8 +332,9 @@ def dram_basis(alg, stream_read, accesses, pmc):
     (traffic - stream) / 32.  Without a fresh profile, the algorithmic figures.
     -> (bytes, random accesses, basis)."""
     tr = pmc.get("traffic")
-    if tr:
-        return min(alg, tr), max(0.0, (tr - (stream_read or 0)) / 32.0), "pmc"
+    if tr:  # (accesses: min(algorithmic, DRAM) too — a 32-B line fetched as a 64-B DRAM
+        # request is one access, not two)
+        return min(alg, tr), min(accesses, max(0.0, (tr - (stream_read or 0)) / 32.0)), "pmc"
     return alg, accesses, "algorithmic"
 
 
@@ -369,8 +373,13 @@ def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, ste
     rnd, acc, frac = W.accounting(idx, info, flags, sh, dev)
     # the structure most random reads hit: the rank lines when the search steps (the whole
     # loop, no contexts, no verification), else the table of context records / entries
+    # — except that the rank steps' lines are not spread over the table: every pattern's
+    # first steps from C[] (or from a table range) read the same few lines, which stay in
+    # the L2 / the 256-MB MALL (FETCH_SIZE counts MALL hits as fetches), so those legs are
+    # set against the best measured random rate (a 1-GB table) rather than the table's size
     steps_mostly = flags & (1 | 2 | 16)
-    table = ((info.rank_bytes, info.line_bytes) if steps_mostly or not info.prefix_bytes
+    table = ((HOT_TABLE_BYTES, info.line_bytes) if steps_mostly
+             else (info.rank_bytes, info.line_bytes) if not info.prefix_bytes
              else (info.prefix_bytes, info.record_bytes or 8))
     got = read_counts()
     out = {"what": what, "workload_key": wl_key, "patterns": W.B, "m": W.m, "flags": flags,

@@ -1511,6 +1511,14 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
+  if (kOne && kNoBar && threadIdx.x == 0) {
+    // the block's tile, which its waves add to after the barrier, and the call's wide-range
+    // counter: no memset launch.  The stores are acknowledged by the L2 (where the waves'
+    // atomics land) before this wave reaches the barrier.
+    op.tiles[blockIdx.x] = 0;
+    if (blockIdx.x == 0) *op.nwide = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   __syncthreads();
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
   const uint32_t K = ix.ptab_k;
@@ -4447,10 +4455,12 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   const bool routed = lk && !long_only && can_route(h, ix);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
   // locate records: a pattern its record does not answer reads its context record in the
-  // same lane (the default), or is left to k_locate_list (tuning hook CS_FM_LOC_DEFER=1, read
-  // per call: the search kernel's blocks then wait for one read, but k_locate_list searches
-  // the 7 % of C4 Q_text from scratch — 0.786 against 0.631 ms per call in an A/B in one
-  // process, profiles/r04/ab_defer.json)
+  // same lane (the default), or is listed for the list kernels (tuning hook
+  // CS_FM_LOC_DEFER=1, read per call), which search it with the staged stages
+  // (locate_miss_one).  Deferring shortens the search kernel (C4 Q_text: 468 -> 410 us) but
+  // the 7 % it lists cost the list kernel 130 us of dependent chains: 0.665 against 0.612 ms
+  // per call (profiles/r04/ab_defer_fast_misses.json; 0.786 / 0.631 when the list kernel ran
+  // the general search, ab_defer.json)
   bool defer = false;
   if (const char* e = std::getenv("CS_FM_LOC_DEFER"))
     defer = std::atoi(e) == 1 && kpos == 0 && ix.lrec;
@@ -4473,20 +4483,22 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.out_pos = d_out_pos;
   op.cap = d_out_pos ? cap : 0;
   op.wide_cap = wide_cap;
-  // the barrier-free search (CS_FM_COUNT_NOBAR, kPos 0) adds its tile totals: the tiles are
-  // zeroed with the wide-range counter behind them
+  // the barrier-free search (CS_FM_COUNT_NOBAR, kPos 0) adds its tile totals: each block
+  // zeroes its tile first (and block 0 the wide-range counter); a call without it zeroes the
+  // counter (and, CS_Q_LONG, the tiles) here
   const bool nobar = kpos == 0 && count_nobar();
-  FMX_HIP(hipMemsetAsync(nobar ? op.tiles : op.tiles + tiles, 0, (nobar ? tiles * 8 : 0) + 8, st));
+  if (long_only)
+    FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
+  else if (!nobar)
+    FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
   op.defer = defer ? 1u : 0u;
   if (long_only || routed || defer) {
     LongBufs lb;
     cs_status ls = lb.alloc(npat, long_only, st, ws.as<uint8_t>() + lo);
     if (ls != CS_OK) return ls;
-    if (long_only && !nobar)
-      FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8, st));
-    else if (long_only)
-      ;
+    if (long_only)
+      ;  // (tiles zeroed above)
     else if (routed && nobar)
       k_count_ctx<OccE, U, true, false, 8, true, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
