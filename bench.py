@@ -80,6 +80,7 @@ RANDOM_CEIL_BY_GB = {16: ((1, 54.3e9), (2, 53.2e9), (4, 51.9e9), (17, 48.0e9), (
 
 
 HOT_TABLE_BYTES = 1 << 30  # the smallest table measured: the best random-read rate
+DRAM_ACCESS = 64.0  # HBM bytes per random read request (profiles/summarize_legs.py)
 
 
 def random_ceiling(table_bytes, width):
@@ -327,14 +328,14 @@ def dram_basis(alg, stream_read, accesses, pmc):
     """What the roofline fractions are taken on: with a fresh PMC
     profile of the leg, the bytes are min(algorithmic, measured HBM traffic) — cache hits
     (the first backward-search steps from C[] share lines across patterns) are not HBM
-    reads — and the random accesses are the DRAM's: the calibrated traffic is the stream plus
-    one 32-B DRAM access per random read request (profiles/summarize.py), so requests =
-    (traffic - stream) / 32.  Without a fresh profile, the algorithmic figures.
+    reads — and the random accesses likewise min(algorithmic, the DRAM's): the traffic is
+    the stream plus one 64-B DRAM request per random read (profiles/summarize_legs.py
+    DRAM_ACCESS: the count kernels' requests are all 64 B, TCC_EA0_RDREQ_32B_sum = 0), so
+    requests = (traffic - stream) / 64.  Without a fresh profile, the algorithmic figures.
     -> (bytes, random accesses, basis)."""
     tr = pmc.get("traffic")
-    if tr:  # (accesses: min(algorithmic, DRAM) too — a 32-B line fetched as a 64-B DRAM
-        # request is one access, not two)
-        return min(alg, tr), min(accesses, max(0.0, (tr - (stream_read or 0)) / 32.0)), "pmc"
+    if tr:
+        return min(alg, tr), min(accesses, max(0.0, (tr - (stream_read or 0)) / DRAM_ACCESS)), "pmc"
     return alg, accesses, "algorithmic"
 
 
@@ -534,7 +535,7 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
         win = text[(p.unsqueeze(1) + torch.arange(m, device=dev)).long()]
         okv &= bool((win == W.pats.view(B, m)[w]).all().item())
     # algorithmic bytes of the call, per pattern: a pattern the locate records answer
-    # (cs_fm_locate_record_hits_device) reads its 16-B locate record; any other the count's
+    # (cs_fm_locate_record_hits_device) reads its locate record (64 B, or 16); any other the count's
     # reads (record + context sectors, cs_fm_count_bytes_device) and one 32-B DRAM sector of
     # SA per reported position (the DRAM's access granularity, as the count legs charge
     # their lines) — plus the stream: patterns and offsets in, the search's u32 count and
@@ -548,7 +549,8 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
         idx.locate_record_hits_device(W.pats.data_ptr(), W.offs.data_ptr(), B, hit.data_ptr(), sh)
     hb = hit.bool()
     nhit = int(hb.sum().item())
-    rnd = 16 * nhit + int(torch.where(hb, 0, qb + 32 * cnt).sum().item())
+    rw = getattr(info, "locate_record_width", 0) or 16  # 64-B records: read by four lanes
+    rnd = rw * nhit + int(torch.where(hb, 0, qb + 32 * cnt).sum().item())
     # random reads: one per 16-B record, one per 32-B sector or line, one SA sector per position
     acc = nhit + int(torch.where(hb, 0, (qb + 31) // 32 + cnt).sum().item())
     del qb, hit, hb, cnt

@@ -55,7 +55,8 @@ class cs_fm_info(C.Structure):
                 ("walk_bytes", C.c_uint64), ("context_q", C.c_uint32), ("position_stride", C.c_uint32),
                 ("context_bytes", C.c_uint64), ("full_sa_bytes", C.c_uint64),
                 ("record_bytes", C.c_uint32), ("text_in_hbm", C.c_uint32),
-                ("packed_text_bytes", C.c_uint64), ("locate_record_bytes", C.c_uint64)]
+                ("packed_text_bytes", C.c_uint64), ("locate_record_bytes", C.c_uint64),
+                ("locate_record_width", C.c_uint64)]
 
 
 # Every entry point of include/cs_fmindex.h with its ctypes signature.

@@ -597,6 +597,7 @@ cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out) {
   out->text_in_hbm = h->d_dtext ? 1u : 0u;
   out->packed_text_bytes = h->d_ptext ? h->ptext_bytes() : 0;
   out->locate_record_bytes = h->d_lrec ? h->lrec_bytes() : 0;
+  out->locate_record_width = h->d_lrec ? h->lrec_w : 0;
   return CS_OK;
 }
 

@@ -132,10 +132,12 @@ struct DevIndex {
   const uint64_t* ptext;
   const uint32_t* prare;
   uint32_t nrare;
-  // Locate records (null when absent; see kLocRec below): one 16-B record per
+  // Locate records (null when absent; see kLocRec below): lrec64 = 1: one 64-B record per
+  // ptab_k-mer (kLocRec64*), index = its prefix-table index; else one 16-B record per
   // (ptab_k + 1)-mer, index = the prefix-table index of its last ptab_k characters plus
   // digit(first character) * 4^ptab_k.
   const void* lrec;
+  uint32_t lrec64;
 };
 
 // Locate records (narrow lf_exact occurrence-line indexes with 16-B context records, the
@@ -155,6 +157,21 @@ struct DevIndex {
 constexpr uint32_t kLocRecRows = 3;
 constexpr uint32_t kLocRecQ = 4;
 constexpr uint32_t kLocRecNone = 7;
+
+// 64-B locate records (round 4, the default): a random 64-B block read by four consecutive
+// lanes, 16 B each, costs one DRAM request and runs at the 16-B read rate (49 G/s over 17
+// and 69 GB, profiles/r04/coop_gather_*.txt; one lane reading 64 B: 19 G/s).  So a record
+// per k-mer x (the context record's index) holds up to kLocRec64Rows rows: chunk c (16 B,
+// lane c of the quad) = SA[row 3c + i] in dwords 0-2 and, in dword 3, the rows' 5-character
+// left contexts (10 bits each, the low bits of their lctx entries) at bits 10 i and the
+// number of valid rows in the chunk at bits 30-31.  A pattern of k + j characters, j <=
+// kLocRec64Q, matches row r iff the low 2j bits of r's context spell its first j characters
+// (the backward-search invariant), and a single match's position is SA[r] - j.  More rows
+// than kLocRec64Rows, or an escaped context: every chunk is (~0, 0, 0, 0) — read the
+// context record instead.  C4 (n / 4^15 = 3.7 rows per 15-mer): a text 20-mer's 15-mer has
+// at most 12 rows 99.97 % of the time.
+constexpr uint32_t kLocRec64Rows = 12;
+constexpr uint32_t kLocRec64Q = 5;
 
 // Left context of BWT row r: the codes of BWT[LF^t(r)], t = 0..q-1 — the q
 // characters preceding the row's rotation — symbol t in bits [sb t, sb (t+1)).

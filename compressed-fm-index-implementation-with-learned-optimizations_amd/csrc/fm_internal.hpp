@@ -60,10 +60,14 @@ struct cs_fm_index {
   void* d_prare = nullptr;
   uint32_t nrare = 0;
   uint64_t ptext_bytes() const { return ((n + 31) / 32) * 8; }
-  // Locate records (fmx::DevIndex::lrec): 16 B per (ptab_k + 1)-mer, derived from the context
-  // records, the left contexts and the full SA on build / open / import, not saved
+  // Locate records (fmx::DevIndex::lrec): 64 B per ptab_k-mer (lrec_w 64, the default) or
+  // 16 B per (ptab_k + 1)-mer (lrec_w 16), derived from the context records, the left
+  // contexts and the full SA on build / open / import, not saved
   void* d_lrec = nullptr;
-  uint64_t lrec_bytes() const { return d_lrec ? (16ull << (2 * (ptab_k + 1))) : 0; }
+  uint32_t lrec_w = 0;
+  uint64_t lrec_bytes() const {
+    return !d_lrec ? 0 : lrec_w == 64 ? (64ull << (2 * ptab_k)) : (16ull << (2 * (ptab_k + 1)));
+  }
   uint32_t active_levels[256] = {};
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
@@ -143,6 +147,7 @@ struct cs_fm_index {
     d.ptext = ver && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
     d.prare = static_cast<const uint32_t*>(d_prare);
     d.lrec = d_sa && lf_exact && !wide ? d_lrec : nullptr;
+    d.lrec64 = lrec_w == 64 ? 1u : 0u;
     d.nrare = nrare;
     return d;
   }

@@ -1601,7 +1601,10 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     k[j] = kk;
     if constexpr (kLR) {
       // (ix.lrec implies a 4-symbol table of k <= 15: the index fits 32 bits)
-      if (ix.lrec && cok && kk >= 1 && kk - 1 <= kLocRecQ && dl != kNoCode) {
+      if (ix.lrec && cok && kk >= 1 && ix.lrec64 && kk <= kLocRec64Q) {
+        lt[j] = tt;  // the k-mer's 64-B record
+        lqm |= 1u << j;
+      } else if (ix.lrec && cok && kk >= 1 && !ix.lrec64 && kk - 1 <= kLocRecQ && dl != kNoCode) {
         lt[j] = (dl << (2 * K)) + tt;
         lqm |= 1u << j;
       }
@@ -1619,6 +1622,64 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     if (!kOne && (threadIdx.x & 63) == 0) ll.cnt2[slot] = 0;
   }
   if constexpr (kLR) {
+    if (ix.lrec64) {
+      // (B0') the 64-B locate records (fm_device.hpp kLocRec64*), each read by the four
+      // lanes of a quad together (one DRAM request): lane c of the quad loads chunk c of the
+      // record of each quad-mate's pattern j, matches its rows against that pattern's
+      // context, and the quad sums the matches; no match, or one (its SA value minus the
+      // context length is the position, stashed), finishes the pattern here — more rows or
+      // matches read the context record below.  Uniform control flow (shuffles).
+      const uint32_t ql = threadIdx.x & 3u, qb = (threadIdx.x & 63u) & ~3u;
+      uint4 ch[U][4];
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+#pragma unroll
+        for (uint32_t s2 = 0; s2 < 4; ++s2) {
+          const uint32_t v = __shfl(((lqm >> j) & 1u) ? lt[j] : ~0u, (int)(qb | s2), 64);
+          ch[j][s2] = v != ~0u ? load_record16(ix.lrec, (uint64_t)v * 4 + ql) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        uint32_t mt = 0, mp = 0, mn = 0;  // the lane's own pattern j: matches, position, none
+#pragma unroll
+        for (uint32_t s2 = 0; s2 < 4; ++s2) {
+          const uint32_t wk = __shfl(want[j] | (k[j] << 16), (int)(qb | s2), 64);
+          const uint32_t kq = wk >> 16, ww = wk & 0xFFFFu, mask = (1u << (2 * kq)) - 1u;
+          const uint4 a = ch[j][s2];
+          const uint32_t vc = a.w >> 30;
+          uint32_t n1 = 0, sv = 0;
+#pragma unroll
+          for (uint32_t i = 0; i < 3; ++i)
+            if (i < vc && ((a.w >> (10 * i)) & mask) == ww) {
+              ++n1;
+              sv = i == 0 ? a.x : i == 1 ? a.y : a.z;
+            }
+          uint32_t tot = n1, pos = n1 == 1 ? sv : 0u, none = (vc == 0 && a.x == ~0u) ? 1u : 0u;
+          tot += __shfl_xor(tot, 1, 64);
+          tot += __shfl_xor(tot, 2, 64);
+          pos |= __shfl_xor(pos, 1, 64);
+          pos |= __shfl_xor(pos, 2, 64);
+          none |= __shfl_xor(none, 1, 64);
+          none |= __shfl_xor(none, 2, 64);
+          if (s2 == ql) {
+            mt = tot;
+            mp = pos;
+            mn = none;
+          }
+        }
+        if (!((lqm >> j) & 1u)) continue;
+        if (mn || mt >= 2) {  // the context record's window (below, or k_locate_list)
+          if (op.defer) {
+            st[j] = 7;
+            defm |= 1u << j;
+          }
+          continue;
+        }
+        st[j] = 0;
+        res[j] = mt;
+        if (mt) rv[j] = kLocStash | (mp >= k[j] ? mp - k[j] : mp + ix.n - k[j]);
+      }
+    } else {
     // (B0) the locate records: no match, or one matching row whose SA value the record holds,
     // finishes the pattern here (its position stashed as the emit kernel copies it); more
     // rows or matches read the context record below
@@ -1648,6 +1709,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
         const uint64_t v = mm == 1u ? a.x : mm == 2u ? a.y : a.z;
         rv[j] = kLocStash | (v >= j2 ? v - j2 : v + ix.n - j2);
       }
+    }
     }
   }
   if constexpr (kOne) {
@@ -2918,7 +2980,30 @@ __global__ __launch_bounds__(kBlk) void k_locrec_hits(DevIndex ix, const uint8_t
   const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
   const uint32_t K = ix.ptab_k;
   uint8_t h = 0;
-  if (ix.lrec && ix.lctx && K && m >= K + 1 && m <= K + 1 + kLocRecQ) {
+  if (ix.lrec && ix.lrec64 && ix.lctx && K && m >= K + 1 && m <= K + kLocRec64Q) {
+    const uint32_t kk = (uint32_t)m - K;
+    uint32_t tt = 0, ww = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < (uint32_t)m; ++i) {
+      const uint32_t b = pats[o0 + i];
+      const uint32_t d = i >= kk ? cmap[b] & 0xFFu : cmap[b] >> 8;
+      ok &= d != kNoCode;
+      if (i >= kk) tt = tt * ix.ptab_sigma + d;
+      else ww |= (d & 3u) << (2 * (kk - 1 - i));
+    }
+    if (ok) {
+      const uint32_t mask = (1u << (2 * kk)) - 1u;
+      uint32_t tot = 0;
+      bool none = false;
+      for (uint32_t c = 0; c < 4; ++c) {
+        const uint4 a = static_cast<const uint4*>(ix.lrec)[(uint64_t)tt * 4 + c];
+        const uint32_t vc = a.w >> 30;
+        none |= vc == 0 && a.x == ~0u;
+        for (uint32_t i = 0; i < vc; ++i) tot += ((a.w >> (10 * i)) & mask) == ww;
+      }
+      h = !none && tot <= 1;
+    }
+  } else if (ix.lrec && !ix.lrec64 && ix.lctx && K && m >= K + 1 && m <= K + 1 + kLocRecQ) {
     const uint32_t kk = (uint32_t)m - K;
     uint32_t tt = 0, ww = 0, dl = 0;
     bool ok = true;
@@ -4040,6 +4125,48 @@ __global__ __launch_bounds__(kBlk) void k_fill_locrec(const uint4* __restrict__ 
   }
 }
 
+// 64-B locate records (fm_device.hpp kLocRec64*): the record of k-mer t from its context
+// record (sp, width, inline contexts) or lctx, and the rows' SA entries
+__global__ __launch_bounds__(kBlk) void k_fill_locrec64(const uint4* __restrict__ rec, uint32_t ptab_rec,
+                                                        uint64_t entries,
+                                                        const uint16_t* __restrict__ lctx,
+                                                        const uint32_t* __restrict__ sa,
+                                                        uint4* __restrict__ out) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
+    const uint4 a = ptab_rec == 1 ? make_uint4(rec[2 * t].x, kRec16Wide, rec[2 * t].y, 0u) : rec[t];
+    const uint32_t wc = a.y & 15u;
+    const bool wide = wc == kRec16Wide;
+    const uint64_t sp = a.x;
+    const uint32_t w = wide ? a.z : wc;
+    bool none = w > kLocRec64Rows || (wide && a.z == kRec16NoRange);
+    uint32_t ctx10[kRec16Ctx];  // inline record: the rows' 5-symbol chains
+    if (!wide) {
+      uint32_t dw[5];
+      rec16_contexts(a.y, a.z, a.w, dw);
+#pragma unroll
+      for (uint32_t i = 0; i < kRec16Ctx; ++i) ctx10[i] = (dw[i >> 1] >> (16 * (i & 1))) & 0x3FFu;
+    }
+    if (wide && !none)
+      for (uint32_t i = 0; i < w; ++i) none |= (lctx[sp + i] & kCtxEsc) != 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 4; ++c) {
+      uint4 o = make_uint4(~0u, 0u, 0u, 0u);
+      if (!none) {
+        const uint32_t vc = w > 3 * c ? (w - 3 * c < 3 ? w - 3 * c : 3u) : 0u;
+        uint32_t sv[3] = {0u, 0u, 0u}, cx = vc << 30;
+        for (uint32_t i = 0; i < vc; ++i) {
+          const uint32_t r = 3 * c + i;
+          sv[i] = sa[sp + r];
+          cx |= (wide ? (uint32_t)lctx[sp + r] & 0x3FFu : ctx10[r < kRec16Ctx ? r : 0]) << (10 * i);
+        }
+        o = make_uint4(sv[0], sv[1], sv[2], cx);
+      }
+      out[4 * t + c] = o;
+    }
+  }
+}
+
 // Build the locate records when the index can use them: narrow lf_exact occurrence-line
 // indexes with context records (16 B, or 32 B: C2) over a 4-symbol table of k <= 15, the
 // left contexts and the full suffix array (C4: k = 15 -> 4^16 records, 69 GB; C2: k = 13 ->
@@ -4061,13 +4188,23 @@ cs_status derive_locate_records(cs_fm_index* h, hipStream_t st) {
   }
   for (int oc = 0; oc < 4; ++oc)
     if (((o2d >> (8 * oc)) & 0xFFu) >= 4) return CS_OK;
-  const uint64_t entries = h->ptab_entries(), bytes = entries * 4 * 16;
+  const uint64_t entries = h->ptab_entries(), bytes = entries * 4 * 16;  // either layout
   if (!hbm_room(h, bytes)) return CS_OK;
+  // CS_FM_LOC_REC64=0 (read at build / open / import): the 16-B (k+1)-mer records of early
+  // round 4 instead of the 64-B k-mer ones
+  bool w64 = true;
+  if (const char* e = std::getenv("CS_FM_LOC_REC64"))
+    w64 = std::atoi(e) != 0;
   void* p = nullptr;
   FMX_HIP(hipMalloc(&p, bytes));
-  k_fill_locrec<<<grid_for(entries, kBlk, 1u << 20), kBlk, 0, st>>>(
-      static_cast<const uint4*>(h->d_ptab), h->ptab_rec, entries, static_cast<const uint16_t*>(h->d_lctx),
-      static_cast<const uint32_t*>(h->d_sa), h->n, o2d, static_cast<uint4*>(p));
+  if (w64)
+    k_fill_locrec64<<<grid_for(entries, kBlk, 1u << 20), kBlk, 0, st>>>(
+        static_cast<const uint4*>(h->d_ptab), h->ptab_rec, entries, static_cast<const uint16_t*>(h->d_lctx),
+        static_cast<const uint32_t*>(h->d_sa), static_cast<uint4*>(p));
+  else
+    k_fill_locrec<<<grid_for(entries, kBlk, 1u << 20), kBlk, 0, st>>>(
+        static_cast<const uint4*>(h->d_ptab), h->ptab_rec, entries, static_cast<const uint16_t*>(h->d_lctx),
+        static_cast<const uint32_t*>(h->d_sa), h->n, o2d, static_cast<uint4*>(p));
   hipError_t e = hipGetLastError();
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess) {
@@ -4075,6 +4212,7 @@ cs_status derive_locate_records(cs_fm_index* h, hipStream_t st) {
     return hip_fail(e, "locate records");
   }
   h->d_lrec = p;
+  h->lrec_w = w64 ? 64 : 16;
   return CS_OK;
 }
 

@@ -91,9 +91,11 @@ typedef struct cs_fm_info {
                               text in HBM) that long patterns are verified against; 0 = none.
                               Derived from the text on build / open / import, not saved. */
   uint64_t locate_record_bytes; /* locate records (one-call locate: the SA values of the
-                              rows of every (k+1)-mer with at most 3 rows, beside their
-                              contexts, so a 20-mer's position is one read); 0 = none.
-                              Derived on build / open / import, not saved. */
+                              rows of every k-mer with at most 12 rows (64-B records, read by
+                              four lanes together), or of every (k+1)-mer with at most 3 (16 B),
+                              beside their contexts, so a 20-mer's position is one read);
+                              0 = none.  Derived on build / open / import, not saved. */
+  uint64_t locate_record_width; /* 64 or 16 (bytes per record); 0 = none */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);

@@ -45,6 +45,8 @@ LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
 
 # legs whose phase-2 reads are contiguous runs of the suffix array, not random rows
 LEG_STREAMED = {"locate_rdna"}
+# bytes the HBM moves for one random read request (round 4; rounds 1-3 assumed 32)
+DRAM_ACCESS = 64
 
 
 def rows(pattern):
@@ -167,8 +169,11 @@ def main():
             req = kc["FETCH_SIZE"] * 1024 / 64
             # a leg whose kernel streams (thousands of contiguous SA rows per range): every
             # request is a 128-B streaming read tallied at 64 B (the guide's x2)
+            # the rest one 64-B DRAM request per random read: TCC_EA0_RDREQ_32B_sum is 0
+            # for the count kernels (profiles/r04/pmc_probe_count_packed.json: 13.47 M
+            # requests per 12.5 M packed patterns, all of 64 B; FETCH_SIZE = requests x 64 B)
             hbm = (req * 128 if leg in LEG_STREAMED
-                   else stream_rd + max(req - stream_rd / 128, 0) * 32)
+                   else stream_rd + max(req - stream_rd / 128, 0) * DRAM_ACCESS)
             e = {"leg": leg, "kernel": "+".join(group) if len(group) > 1 else kname,
                  "fetch_size_kb_per_launch": kc["FETCH_SIZE"],
                  "read_requests_per_launch": req, "stream_read_bytes_per_launch": stream_rd,

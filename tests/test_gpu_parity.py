@@ -1042,7 +1042,8 @@ def test_locate_one_call(built, pkg, name):
 
 def test_locate_records(pkg):
     """The one-call locate through the locate records (fm_device.hpp kLocRec*: the SA values
-    of each (k+1)-mer's rows beside their contexts, round 4) against the oracle's positions in
+    of each k-mer's (64 B) or (k+1)-mer's (16 B) rows beside their contexts, round 4) against
+    the oracle's positions in
     row order and against the same call without them (CS_Q_NO_LOC_RECORDS): a DNA text with
     40-base pieces copied 2-7 times (so (k+1)-mers have 0..7+ rows) and a few N, every pattern
     length from k-1 to k+7 (text substrings, one-character mutants, uniform), limits 1, 2 and
@@ -1062,15 +1063,18 @@ def test_locate_records(pkg):
     t = bytes(t) + b"$"
     o = O.Index(t)
     built_any = False
-    for rec in ("16", "1"):  # compact 16-B context records (C4), 32-B ones (C2)
-        with _env(CS_FM_CTX_RECORDS=rec):
+    # compact 16-B context records (C4), 32-B ones (C2); 64-B k-mer locate records read by
+    # four lanes (the default) and the 16-B (k+1)-mer ones (CS_FM_LOC_REC64=0)
+    for rec, w64 in (("16", "1"), ("1", "1"), ("16", "0"), ("1", "0")):
+        with _env(CS_FM_CTX_RECORDS=rec, CS_FM_LOC_REC64=w64):
             g = pkg.FMIndex.build_from_text(t, pkg.BuildParams())
         info = g.info()
         if not info.locate_record_bytes:
             continue
         built_any = True
         assert info.record_bytes == (16 if rec == "16" else 32)
-        assert info.locate_record_bytes == 16 * 4 ** (info.prefix_k + 1)
+        assert info.locate_record_bytes == 16 * 4 ** (info.prefix_k + 1)  # 64 * 4^k as well
+        assert info.locate_record_width == (64 if w64 == "1" else 16)
         K = info.prefix_k
         pats = []
         for m in range(max(1, K - 1), K + 8):
