@@ -4379,15 +4379,20 @@ cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uin
   return launch_count_long_t<false>(ix, d_pats, d_offs, npat, co, st, fixed_m, routed, false, byte_text);
 }
 
-// Whether device batches are routed (the staged kernel lists its long patterns for
+// Whether a device batch is routed (the staged kernel lists its long patterns for
 // k_count_long / k_locate_long in the same call): indexes k_count_long serves (occurrence
-// lines, the full SA and the text); the tuning hook CS_FM_LONG_ROUTE=0 (read per call) keeps
-// every pattern in the staged kernel (round 2's path).
-bool can_route(const cs_fm_index* h, const DevIndex& ix) {
+// lines, the full SA and the text), and batches of kRouteMin patterns or more — the lists
+// cost a call ≈ 8 µs whatever it holds (one stream-ordered allocation and one more launch:
+// C4's 12.5 M 20-mers 0.381 -> 0.397 ms, C2's 1 M 36 -> 47 µs), so a smaller batch keeps
+// every pattern in the staged kernel (round 2's path; its long patterns take the general
+// search: CS_Q_LONG sends a batch of long patterns to k_count_long directly).  Tuning hook
+// CS_FM_LONG_ROUTE (read per call): 0 = never route, 1 = route every batch (the GPU tests
+// set it, so their small batches take the lists), unset = by size.
+constexpr uint64_t kRouteMin = 4u << 20;
+bool can_route(const cs_fm_index* h, const DevIndex& ix, uint64_t npat) {
   if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return false;
-  if (const char* e = std::getenv("CS_FM_LONG_ROUTE"))
-    if (std::atoi(e) == 0) return false;
-  return true;
+  if (const char* e = std::getenv("CS_FM_LONG_ROUTE")) return std::atoi(e) != 0;
+  return npat >= kRouteMin;
 }
 
 // the staged kernel at count width W: table entries (context records) of U patterns per
@@ -4427,7 +4432,7 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   else if (W == 8 && U == 4)
     k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
-  else if (d_offs && can_route(h, ix)) {
+  else if (d_offs && can_route(h, ix, npat)) {
     // long-pattern routing inside the call: the staged kernel counts the short patterns and
     // lists the long ones, k_count_long (and k_count_list) take them from its lists
     LongBufs lb;
@@ -4528,7 +4533,7 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
   if (!(lk && (flags & CS_Q_LONG) && !old))
     FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), ix, d_pats, d_offs, npat, d_out);
   // (a routed call's long patterns: can_route; ADVICE r03: the twin now follows the call)
-  if (lk && !old && ((flags & CS_Q_LONG) || can_route(h, ix))) {
+  if (lk && !old && ((flags & CS_Q_LONG) || can_route(h, ix, npat))) {
     const CountOut co{d_out, nullptr, nullptr, 0, 8};
     return launch_count_long_t<true>(ix, d_pats, d_offs, npat, co, st, 0, nullptr, !(flags & CS_Q_LONG),
                                      ek && std::atoi(ek) == 2);
@@ -4590,7 +4595,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // the long patterns the staged kernel lists in the same call
   const bool lk = kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
   const bool long_only = lk && (flags & CS_Q_LONG);
-  const bool routed = lk && !long_only && can_route(h, ix);
+  const bool routed = lk && !long_only && can_route(h, ix, npat);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
   // locate records: a pattern its record does not answer reads its context record in the
   // same lane (the default), or is listed for the list kernels (tuning hook

@@ -22,6 +22,12 @@ sys.path.insert(0, ROOT)
 # ~23 s; a new per-text test ~1 s per variant: trim elsewhere before adding either.
 GPU_SUITE_BUDGET_S = 550
 
+# Long-pattern routing inside a call (fm_query.hip can_route) is chosen by batch size: only
+# batches of 4 M patterns or more are routed by default.  The tests' batches are small, so
+# they route every batch (CS_FM_LONG_ROUTE=1) to exercise the lists; the tests that need the
+# unrouted path set CS_FM_LONG_ROUTE=0 (or unset it) around their calls.
+os.environ.setdefault("CS_FM_LONG_ROUTE", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box)")

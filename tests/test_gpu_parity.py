@@ -834,6 +834,13 @@ def test_count_verify_long(built, pkg, name):
     with _env(CS_FM_LONG_ROUTE="0"):
         got, _, _ = _count_ex(g, pats)
     assert got.tolist() == want, name
+    saved = os.environ.pop("CS_FM_LONG_ROUTE", None)  # by size: a small batch is not routed
+    try:
+        got, _, _ = _count_ex(g, pats)
+    finally:
+        if saved is not None:
+            os.environ["CS_FM_LONG_ROUTE"] = saved
+    assert got.tolist() == want, (name, "by size")
     # CS_Q_LONG at the narrow widths: uint32, and uint8 with the exception pairs
     got4, _, _ = _count_ex(g, pats, width=4, flags=32)
     assert got4.tolist() == want, name
