@@ -174,7 +174,7 @@ def log(rank, *a):
 # the full result (every leg) in the --legs-out file and on stderr
 LINE_MAX = 4096
 _ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "alg_bytes_per_launch",
-              "kernel_ms_mean", "frac_of_random_access_ceiling")
+              "kernel_ms_mean", "frac_of_random_access_ceiling", "traffic_frac")
 _CPU_KEYS = ("value", "unit", "cores", "kind", "cores_used", "host_cores", "matches_gpu", "p50_us")
 _CFG_KEYS = ("workload", "batch_per_gpu", "global_batch", "m", "ssa_stride", "parallelism", "index")
 
@@ -360,7 +360,10 @@ def roofline(alg_random, alg_stream, accesses, kern_s, B, pmc, stream_read=None,
             "random_access_table_bytes": table[0] if table else None,
             "frac_of_random_access_ceiling": acc / kern_s / ceil,
             "access_mix_ceiling_per_s": MIXED_CEIL,
-            "frac_of_access_mix_ceiling": acc / kern_s / MIXED_CEIL}
+            "frac_of_access_mix_ceiling": acc / kern_s / MIXED_CEIL,
+            # the HBM's own load: the measured traffic (PMC, 64-B requests) per second
+            # against the peak — the random-read regime moves 64 B per 16-B record
+            "traffic_frac": (pmc.get("traffic") or 0) / kern_s / 1e9 / HBM_PEAK_GBS or None}
 
 
 def count_leg(name, what, idx, info, wl_key, W, launch, flags, stream_bytes, steps, warmup,
