@@ -55,7 +55,7 @@ cs_status check_handle(const cs_fm_index* h, DeviceScope& ds) {
 // else a kernel would read past the staged bytes.  *long_flag (when asked): CS_Q_LONG
 // if every pattern is longer than kLongPatternM (the long-pattern count kernel), else 0.
 cs_status check_offsets(const uint64_t* offs, uint64_t npat, uint32_t* long_flag = nullptr) {
-  uint64_t mn = ~0ull;
+  uint64_t mn = ~0ull, mx = 0;
   for (uint64_t q = 0; q < npat; ++q) {
     if (offs[q + 1] < offs[q]) {
       set_error("pattern offsets must be non-decreasing");
@@ -63,8 +63,9 @@ cs_status check_offsets(const uint64_t* offs, uint64_t npat, uint32_t* long_flag
     }
     const uint64_t m = offs[q + 1] - offs[q];
     mn = m < mn ? m : mn;
+    mx = m > mx ? m : mx;
   }
-  if (long_flag) *long_flag = npat && mn > kLongPatternM ? CS_Q_LONG : 0u;
+  if (long_flag) *long_flag = !npat ? 0u : mn > kLongPatternM ? CS_Q_LONG : mx > kLongPatternM ? kQRoute : 0u;
   return CS_OK;
 }
 

@@ -200,6 +200,11 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
 // (CS_Q_LONG): fixed-length device batches and host batches, whose lengths are known
 // before the launch: 32 characters and more (k_count_long reads a pattern's last 32).
 constexpr uint64_t kLongPatternM = 31;
+// Internal query flag (no CS_Q_* bit): the batch holds a pattern of more than kLongPatternM
+// characters — host batches know their lengths, so a mixed host chunk is routed (the staged
+// kernel lists its long patterns for k_count_long in the same call) whatever its size, and
+// a short-only one never pays for the lists (fm_query.hip can_route)
+constexpr uint32_t kQRoute = 1u << 31;
 // Slack after every index part in HBM (zeroed): the text verification and extract read
 // whole aligned 8-B words, up to 7 bytes past the text's last byte (fm_query.hip
 // window_eq / verify_filter / k_extract_text), so the allocation covers them.

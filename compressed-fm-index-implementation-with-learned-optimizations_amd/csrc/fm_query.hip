@@ -4389,10 +4389,10 @@ cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uin
 // CS_FM_LONG_ROUTE (read per call): 0 = never route, 1 = route every batch (the GPU tests
 // set it, so their small batches take the lists), unset = by size.
 constexpr uint64_t kRouteMin = 4u << 20;
-bool can_route(const cs_fm_index* h, const DevIndex& ix, uint64_t npat) {
+bool can_route(const cs_fm_index* h, const DevIndex& ix, uint64_t npat, uint32_t flags) {
   if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return false;
   if (const char* e = std::getenv("CS_FM_LONG_ROUTE")) return std::atoi(e) != 0;
-  return npat >= kRouteMin;
+  return npat >= kRouteMin || (flags & kQRoute);  // (kQRoute: a host batch with long patterns)
 }
 
 // the staged kernel at count width W: table entries (context records) of U patterns per
@@ -4400,7 +4400,8 @@ bool can_route(const cs_fm_index* h, const DevIndex& ix, uint64_t npat) {
 template <int W>
 cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t* d_pats,
                          const uint64_t* d_offs, uint64_t npat, const CountOut& co,
-                         hipStream_t st, uint64_t fixed_m, bool packed) {
+                         hipStream_t st, uint64_t fixed_m, bool packed,
+                         uint32_t flags = 0) {
   const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U, read per call)
     const char* e = std::getenv("CS_FM_COUNT_U");
     const int u = e ? std::atoi(e) : 2;
@@ -4432,7 +4433,7 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   else if (W == 8 && U == 4)
     k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
-  else if (d_offs && can_route(h, ix, npat)) {
+  else if (d_offs && can_route(h, ix, npat, flags)) {
     // long-pattern routing inside the call: the staged kernel counts the short patterns and
     // lists the long ones, k_count_long (and k_count_list) take them from its lists
     LongBufs lb;
@@ -4495,9 +4496,9 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
     return CS_OK;
   }
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.ptab_k) {
-    if (co.width == 8) return launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
-    if (co.width == 4) return launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
-    return launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed);
+    if (co.width == 8) return launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags);
+    if (co.width == 4) return launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags);
+    return launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags);
   }
   const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
   if (packed)
@@ -4533,7 +4534,7 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
   if (!(lk && (flags & CS_Q_LONG) && !old))
     FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), ix, d_pats, d_offs, npat, d_out);
   // (a routed call's long patterns: can_route; ADVICE r03: the twin now follows the call)
-  if (lk && !old && ((flags & CS_Q_LONG) || can_route(h, ix, npat))) {
+  if (lk && !old && ((flags & CS_Q_LONG) || can_route(h, ix, npat, flags))) {
     const CountOut co{d_out, nullptr, nullptr, 0, 8};
     return launch_count_long_t<true>(ix, d_pats, d_offs, npat, co, st, 0, nullptr, !(flags & CS_Q_LONG),
                                      ek && std::atoi(ek) == 2);
@@ -4595,7 +4596,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // the long patterns the staged kernel lists in the same call
   const bool lk = kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
   const bool long_only = lk && (flags & CS_Q_LONG);
-  const bool routed = lk && !long_only && can_route(h, ix, npat);
+  const bool routed = lk && !long_only && can_route(h, ix, npat, flags);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
   // locate records: a pattern its record does not answer reads its context record in the
   // same lane (the default), or is listed for the list kernels (tuning hook

@@ -837,10 +837,13 @@ def test_count_verify_long(built, pkg, name):
     saved = os.environ.pop("CS_FM_LONG_ROUTE", None)  # by size: a small batch is not routed
     try:
         got, _, _ = _count_ex(g, pats)
+        # a host batch knows its lengths: routed when it holds long patterns (kQRoute)
+        got_h = g.count_batch(pats)
     finally:
         if saved is not None:
             os.environ["CS_FM_LONG_ROUTE"] = saved
     assert got.tolist() == want, (name, "by size")
+    assert got_h.tolist() == want, (name, "host batch, by lengths")
     # CS_Q_LONG at the narrow widths: uint32, and uint8 with the exception pairs
     got4, _, _ = _count_ex(g, pats, width=4, flags=32)
     assert got4.tolist() == want, name
