@@ -206,10 +206,11 @@ __device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint6
     // use (C4 headline 0.396 -> 0.388 ms in one box session; non-temporal pattern loads
     // were measured too, 0.408 ms: profiles/r03/ab_nt_store.jsonl)
     __builtin_nontemporal_store(v, static_cast<uint64_t*>(o.out) + q);
-  } else if (w == 4) {
-    static_cast<uint32_t*>(o.out)[q] = (uint32_t)v;
+  } else if (w == 4) {  // (non-temporal as the uint64 counts: packed 0.357 -> 0.350 ms, u32 0.430
+    // -> 0.425, profiles/r04/ab_lib_r04ad_*.jsonl)
+    __builtin_nontemporal_store((uint32_t)v, static_cast<uint32_t*>(o.out) + q);
   } else {
-    static_cast<uint8_t*>(o.out)[q] = (uint8_t)(v < 255 ? v : 255);
+    __builtin_nontemporal_store((uint8_t)(v < 255 ? v : 255), static_cast<uint8_t*>(o.out) + q);
     if (v >= 255) {
       const unsigned long long e = atomicAdd(o.exc_n, 1ull);
       if (e < o.exc_cap) {
