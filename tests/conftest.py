@@ -19,7 +19,9 @@ sys.path.insert(0, ROOT)
 # that run it (profiles/r03/pytest_gpu_all_r03n.log) — 20
 # engine variants x ~30 texts in test_gpu_parity.py (~23 s per variant) and the full-size
 # configs in test_gpu_scale.py (C5 2 x 36 s, C4 3 x 6-20 s).  A new engine variant costs
-# ~23 s; a new per-text test ~1 s per variant: trim elsewhere before adding either.
+# ~23 s; a new per-text test ~1 s per variant: trim elsewhere before adding either.  Round 4:
+# 8,710 tests in 544-557 s (profiles/r04/pytest_gpu_all_r04{w,ae}.log), the scan-oracle checks
+# of test_gpu_scale.py included.
 GPU_SUITE_BUDGET_S = 550
 
 # Long-pattern routing inside a call (fm_query.hip can_route) is chosen by batch size: only
