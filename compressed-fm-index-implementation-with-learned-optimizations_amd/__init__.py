@@ -29,6 +29,12 @@ CS_ERR_LF_OVERRUN, CS_ERR_SSA_RANGE, CS_ERR_CAPACITY, CS_ERR_UNSUPPORTED, CS_ERR
 # query flags (include/cs_fmindex.h CS_Q_*): results unchanged, structures left out
 Q_NO_PREFIX, Q_NO_CONTEXTS, Q_NO_FULL_SA, Q_NO_WALK_LINES, Q_NO_VERIFY, Q_LONG = 1, 2, 4, 8, 16, 32
 Q_NO_LOC_RECORDS = 64
+# tuning selectors (cs_fmindex.h CS_QT_*): equivalent kernels for tests and A/Bs, results
+# unchanged; a handle's defaults come from the CS_FM_* environment when it is created
+QT_BARRIER, QT_NO_ROUTE, QT_COUNT_U1, QT_COUNT_U4 = 1 << 8, 1 << 9, 1 << 10, 1 << 11
+QT_LONG_LOADS8, QT_LONG_ROUND2, QT_LONG_BYTE_TEXT, QT_QCTX_UNSTAGED = 1 << 12, 1 << 13, 1 << 14, 1 << 15
+QT_NO_ONEPASS, QT_ONEPASS_SA, QT_LOC_DEFER, QT_LOCATE_U1 = 1 << 16, 1 << 17, 1 << 18, 1 << 19
+QT_WALK_ROWS, QT_WALK_PERSISTENT, QT_GENERAL_INLANE, QT_GENERAL_LIST_ALL = 1 << 20, 1 << 21, 1 << 22, 1 << 23
 
 _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)
@@ -56,7 +62,7 @@ class cs_fm_info(C.Structure):
                 ("context_bytes", C.c_uint64), ("full_sa_bytes", C.c_uint64),
                 ("record_bytes", C.c_uint32), ("text_in_hbm", C.c_uint32),
                 ("packed_text_bytes", C.c_uint64), ("locate_record_bytes", C.c_uint64),
-                ("locate_record_width", C.c_uint64)]
+                ("locate_record_width", C.c_uint64), ("device_bytes", C.c_uint64)]
 
 
 # Every entry point of include/cs_fmindex.h with its ctypes signature.
@@ -103,6 +109,11 @@ SIGNATURES = {
     "cs_fm_locate_record_hits_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_count_batch_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64,
                                               C.POINTER(cs_count_out), C.c_uint32, _vp]),
+    "cs_fm_workspace_bytes": (C.c_uint64, [_vp, C.c_uint64]),
+    "cs_fm_count_device_ws": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, C.POINTER(cs_count_out),
+                                        C.c_uint32, _vp, C.c_uint64, _vp]),
+    "cs_fm_locate_device_ws": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
+                                         C.POINTER(C.c_uint64), C.c_uint32, _vp, C.c_uint64, _vp]),
     "cs_fm_count_packed_device": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64,
                                             C.POINTER(cs_count_out), C.c_uint32, _vp]),
     "cs_fm_locate_ranges_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
@@ -449,6 +460,31 @@ class FMIndex:
         o = cs_count_out(d_out, width, d_exc, exc_cap, d_exc_n)
         _check(lib().cs_fm_count_batch_device_ex(self._h, d_pats, d_offs, fixed_m, npat,
                                                  C.byref(o), flags, stream or None))
+
+    def workspace_bytes(self, npat: int) -> int:
+        """Device workspace for a count or one-call locate of up to npat patterns
+        (cs_fm_workspace_bytes): zero-filled once by the caller, reused by its calls."""
+        return int(lib().cs_fm_workspace_bytes(self._h, npat))
+
+    def count_device_ws(self, d_pats, d_offs, npat, d_out, d_work, work_bytes, width=8, flags=0,
+                        fixed_m=0, d_exc=None, exc_cap=0, d_exc_n=None, stream=0):
+        """count_device_ex with the caller's workspace (cs_fm_count_device_ws): no allocation
+        inside the call."""
+        o = cs_count_out(d_out, width, d_exc, exc_cap, d_exc_n)
+        _check(lib().cs_fm_count_device_ws(self._h, d_pats, d_offs, fixed_m, npat, C.byref(o), flags,
+                                           d_work or None, work_bytes, stream or None))
+
+    def locate_device_ws(self, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, d_work,
+                         work_bytes, stream=0, flags=0):
+        """locate_device with the caller's workspace (cs_fm_locate_device_ws)."""
+        total = C.c_uint64()
+        st = lib().cs_fm_locate_device_ws(self._h, d_pats, d_offs, npat, limit, d_out_offs,
+                                          d_out_pos or None, cap, C.byref(total), flags,
+                                          d_work or None, work_bytes, stream or None)
+        if st == CS_ERR_CAPACITY:
+            return total.value, False
+        _check(st)
+        return total.value, True
 
     def count_packed_device(self, d_packed, m, npat, d_out, width=8, flags=0, d_exc=None,
                             exc_cap=0, d_exc_n=None, stream=0):

@@ -232,16 +232,55 @@ __device__ __forceinline__ void store_count(const CountOut& o, uint64_t q, uint6
 // the entries of their slots flattened (all lanes busy), and what they cannot finish goes
 // to the slot lists `list2` / `cnt2` of the pattern for the general-search kernel after
 // them.  No host synchronisation and no state in the handle: every list is the call's own
-// buffer, so concurrent calls on other streams cannot interfere.  All null: no routing.
+// buffer (the caller's workspace, or one allocated for the call), so concurrent calls on other
+// streams cannot interfere.  All null: no routing.
+// Round 5: the routed count also lists the patterns its one read cannot finish (the general
+// search: wide ranges, escaped contexts, symbols off the table) in the wave's slot of list2
+// (gen_list), so no lane of the staged kernel runs a dependent chain while 63 others idle,
+// and the waves that list anything add their number to `listed` (kListedLanes counters, one
+// per 256-B line, blockIdx.x % kListedLanes): a list kernel whose counters sum to 0 leaves at
+// its first load — no slot scan.  The counters are zero between calls: the list kernel's last
+// block to retire (the `retire` counter) zeroes them and itself.  A workspace is therefore
+// zero-filled once before its first use (cs_fm_workspace_bytes, cs_fmindex.h).
 constexpr uint32_t kLongRegion = 512;  // = 2 kBlk: the staged kernels' patterns per block (U = 2)
 constexpr uint32_t kLongSlot = 128;    // a wave's patterns (64 lanes x U = 2): one slot
 constexpr uint32_t kSlotsPerRegion = kLongRegion / kLongSlot;
+constexpr uint32_t kListedLanes = 16;
+constexpr uint32_t kListedStride = 64;  // uint32 words between the counters (256 B)
+constexpr uint64_t kListHdrBytes = (uint64_t)(kListedLanes + 1) * kListedStride * 4;  // + retire
 struct LongList {
   uint16_t* list = nullptr;
   uint32_t* cnt = nullptr;
   uint16_t* list2 = nullptr;
   uint32_t* cnt2 = nullptr;
+  uint32_t* hdr = nullptr;  // listed[kListedLanes] (kListedStride apart), then retire
+  uint32_t gen_list = 0;    // the routed count: general-search patterns to list2
 };
+// the staged kernel's wave adds its listed patterns (lane 0; n uniform over the wave)
+__device__ __forceinline__ void list_listed_add(const LongList& ll, uint32_t n) {
+  if (n && (threadIdx.x & 63) == 0)
+    atomicAdd(ll.hdr + (blockIdx.x % kListedLanes) * kListedStride, n);
+}
+// whether any pattern was listed (every thread of a block; uniform)
+__device__ __forceinline__ bool list_any(const LongList& ll) {
+  uint32_t v = 0;
+  if (threadIdx.x < kListedLanes)
+    v = __hip_atomic_load(ll.hdr + threadIdx.x * kListedStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __syncthreads_or(v != 0) != 0;
+}
+// a list kernel's block is done (every thread; after list_any was true): the last block of
+// the grid zeroes the counters for the next call on this workspace
+__device__ __forceinline__ void list_retire(const LongList& ll) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t* retire = ll.hdr + kListedLanes * kListedStride;
+    __threadfence();
+    if (atomicAdd(retire, 1u) == gridDim.x - 1) {
+      for (uint32_t i = 0; i < kListedLanes; ++i) ll.hdr[i * kListedStride] = 0;
+      *retire = 0;
+    }
+  }
+}
 // the slot of pattern q: its block's region, the wave of the lane that holds it
 __host__ __device__ inline uint64_t long_slot(uint64_t q) {
   return (q / kLongRegion) * kSlotsPerRegion + ((q % kLongRegion) % 256) / 64;

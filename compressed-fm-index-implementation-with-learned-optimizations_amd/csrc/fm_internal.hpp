@@ -69,6 +69,14 @@ struct cs_fm_index {
     return !d_lrec ? 0 : lrec_w == 64 ? (64ull << (2 * ptab_k)) : (16ull << (2 * (ptab_k + 1)));
   }
   uint32_t active_levels[256] = {};
+  // Tuning defaults (CS_QT_* bits, cs_fmindex.h) and the host-batch chunk (patterns; 0 = the
+  // default), read from the environment once when the handle is created (read_tuning); every
+  // query ORs its flags over `tune` (fm_query.hip call_flags) and reads no environment
+  uint32_t tune = 0;
+  uint64_t host_chunk = 0;
+  // the routed count: a wave lists its general searches for the list kernel when it holds
+  // at least this many (CS_FM_GENERAL_LIST_MIN; fm_device.hpp LongList::gen_list)
+  uint32_t gen_list_min = 2;
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
   // per-handle pinned + HBM arena instead of per-call hipMalloc/hipFree and
@@ -191,6 +199,19 @@ cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride,
 cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride, cs_fm_index* h,
                              hipStream_t st);
 
+// A caller's device workspace (cs_fm_*_ws entry points, cs_fm_workspace_bytes): null = none
+// (the call allocates what it needs, stream-ordered)
+struct Work {
+  void* p = nullptr;
+  uint64_t bytes = 0;
+};
+// workspace bytes of a routed count / a one-call locate of npat patterns (fm_query.hip)
+uint64_t count_workspace_bytes(const cs_fm_index* h, uint64_t npat);
+uint64_t locate_workspace_bytes(const cs_fm_index* h, uint64_t npat);
+// the tuning defaults of a new handle from the CS_FM_* environment (cs_fm_index::tune,
+// host_chunk; fm_capi.hip): read once when a handle is created, never by a query
+void read_tuning(cs_fm_index* h);
+
 // Query launches (fm_query.hip).
 // d_offs == nullptr: npat patterns of length fixed_m at stride fixed_m; flags CS_Q_*
 cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
@@ -200,11 +221,6 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
 // (CS_Q_LONG): fixed-length device batches and host batches, whose lengths are known
 // before the launch: 32 characters and more (k_count_long reads a pattern's last 32).
 constexpr uint64_t kLongPatternM = 31;
-// Internal query flag (no CS_Q_* bit): the batch holds a pattern of more than kLongPatternM
-// characters — host batches know their lengths, so a mixed host chunk is routed (the staged
-// kernel lists its long patterns for k_count_long in the same call) whatever its size, and
-// a short-only one never pays for the lists (fm_query.hip can_route)
-constexpr uint32_t kQRoute = 1u << 31;
 // Slack after every index part in HBM (zeroed): the text verification and extract read
 // whole aligned 8-B words, up to 7 bytes past the text's last byte (fm_query.hip
 // window_eq / verify_filter / k_extract_text), so the allocation covers them.
@@ -213,7 +229,7 @@ constexpr uint64_t kPartPad = 64;
 // (d_pats = one uint64 per pattern of fixed_m 2-bit characters)
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                           uint64_t npat, const fmx::CountOut& co, uint32_t flags, hipStream_t st,
-                          uint64_t fixed_m, bool packed);
+                          uint64_t fixed_m, bool packed, const Work& work = Work{});
 cs_status launch_count_one(const cs_fm_index* h, const fmx::OnePattern& p, uint64_t* out_host,
                            hipStream_t st);
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
@@ -233,7 +249,7 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
 cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, hipStream_t st,
-                                bool* done, uint32_t flags = 0);
+                                bool* done, uint32_t flags = 0, const Work& work = Work{});
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st,
@@ -265,6 +281,8 @@ inline cs_status derive_parts(cs_fm_index* h, hipStream_t st) {
 }
 // HBM held by the index's device arrays so far (the image parts, fm_io.hip)
 uint64_t index_hbm_bytes(const cs_fm_index* h);
+// every device allocation the handle owns (cs_fm_info.device_bytes, fm_io.hip)
+uint64_t device_bytes(const cs_fm_index* h);
 // Whether an optional structure of `bytes` may be allocated: the device keeps an eighth
 // of its HBM free (query buffers), and with a budget the index stays within it — `freed`
 // bytes of the index are released once the structure is built (a replacement).

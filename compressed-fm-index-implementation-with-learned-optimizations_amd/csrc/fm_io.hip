@@ -235,6 +235,21 @@ uint64_t index_hbm_bytes(const cs_fm_index* hc) {
   return b;
 }
 
+uint64_t device_bytes(const cs_fm_index* hc) {
+  cs_fm_index* h = const_cast<cs_fm_index*>(hc);  // sizes only
+  uint64_t b = 0;
+  // every image part (each allocated with kPartPad zeroed bytes after it), the node table
+  // among them
+  for (const Part& p : index_parts(h, true, h->d_wssa != nullptr, h->d_sa != nullptr, h->d_dtext != nullptr))
+    if (*p.dptr) b += p.bytes + (p.dptr == reinterpret_cast<void**>(&h->d_table) ? 0 : kPartPad);
+  if (h->d_ptext) b += h->ptext_bytes() + kPartPad;  // derived parts
+  b += h->lrec_bytes();
+  if (h->d_prare) b += kMaxExc * 4;
+  if (h->d_err) b += 8;
+  if (h->scratch.d) b += cs_fm_index::kScratchBytes;  // the small-batch arena
+  return b;
+}
+
 bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
@@ -355,6 +370,7 @@ cs_status cs_fm_open_directory_on(const char* dir, int device, cs_fm_index** out
     std::fclose(f);
   }
   auto* h = new cs_fm_index();
+  read_tuning(h);
   std::map<std::string, unsigned long long> kv;
   cs_status s = meta_parse(meta, h, kv, d);
   if (s == CS_OK) s = need_device();
@@ -446,6 +462,7 @@ cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d
   }
   *out = nullptr;
   auto* h = new cs_fm_index();
+  read_tuning(h);
   std::map<std::string, unsigned long long> kv;
   cs_status s = meta_parse(std::string(meta, meta_len), h, kv, "device image");
   if (s == CS_OK) s = need_device();
@@ -500,6 +517,7 @@ cs_status cs_fm_import_alloc(const char* meta, uint64_t meta_len, int device, cs
   }
   *out = nullptr;
   auto* h = new cs_fm_index();
+  read_tuning(h);
   std::map<std::string, unsigned long long> kv;
   cs_status s = meta_parse(std::string(meta, meta_len), h, kv, "device image");
   if (s == CS_OK) s = need_device();

@@ -1452,9 +1452,9 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(DevIndex ix, OnePass 
 
 // The lanes' patterns j with bit j of `m` set into the wave's slot of a LongList list (their
 // offsets inside the block's region, in ballot order) and their number into cnt[slot] (0
-// when none).  Every lane of the wave, in uniform control flow.
+// when none); returns that number (uniform).  Every lane of the wave, in uniform control flow.
 template <int U = 2>
-__device__ __forceinline__ void wave_list(uint16_t* list, uint32_t* cnt, uint64_t slot, uint32_t m) {
+__device__ __forceinline__ uint32_t wave_list(uint16_t* list, uint32_t* cnt, uint64_t slot, uint32_t m) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t n = 0;
@@ -1466,6 +1466,7 @@ __device__ __forceinline__ void wave_list(uint16_t* list, uint32_t* cnt, uint64_
     n += __popcll(bal);
   }
   if (lane == 0) cnt[slot] = n;
+  return n;
 }
 
 // A 16-B context record: a random read nothing re-reads, through a non-temporal load so it
@@ -1614,14 +1615,14 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   }
   // the wave's slot of the call's lists (kSkipLong, and kOne's deferred patterns)
   const uint64_t slot = (uint64_t)blockIdx.x * kSlotsPerRegion + (threadIdx.x >> 6);
+  uint32_t nlisted = 0;  // kSkipLong: the wave's listed patterns (uniform)
   if constexpr (kSkipLong) {
     // the long patterns into the wave's slot (k_count_long / k_locate_long take them), in
-    // ballot order; the count forms zero the slot of the general-search list too
+    // ballot order (the count forms write the general-search slot after (D))
     uint32_t lm = 0;
 #pragma unroll
     for (int j = 0; j < U; ++j) lm |= (uint32_t)(st[j] == 4) << j;
-    wave_list<U>(ll.list, ll.cnt, slot, lm);
-    if (!kOne && (threadIdx.x & 63) == 0) ll.cnt2[slot] = 0;
+    nlisted = wave_list<U>(ll.list, ll.cnt, slot, lm);
   }
   if constexpr (kLR) {
     if (ix.lrec64) {
@@ -1716,7 +1717,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   }
   if constexpr (kOne) {
     // the deferred patterns into the wave's slot of the general-search list (zeroed when none)
-    if (ll.cnt2) wave_list<U>(ll.list2, ll.cnt2, slot, defm);
+    if (ll.cnt2) nlisted += wave_list<U>(ll.list2, ll.cnt2, slot, defm);
+    if (ll.hdr) list_listed_add(ll, nlisted);
   }
   // (B) the table entries (whole context records: their contexts come with them)
   uint4 w[U][4];
@@ -1843,6 +1845,35 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
         store_count<W>(co, q, res[j]);
       }
     }
+  }
+  if constexpr (kSkipLong && !kOne) {
+    // the routed count (round 5): the patterns left to the general search go to the wave's
+    // slot of list2 for k_count_long (whose lanes then all search), unless the call keeps
+    // them in the lane (CS_QT_GENERAL_INLANE); the wave's listed number to the counters
+    // A wave lists them when it holds at least ll.gen_list of them: a wave with one keeps it
+    // (its chain overlaps the other waves' reads, and a batch that lists nothing skips the
+    // list kernel's work; C4 Q_text: the staged kernel 389 us either way, the list kernel 4
+    // against 58 us), a wave with many would idle most of its lanes through their chains
+    // (repetitive DNA: the staged kernel 1060 -> 380 us when listed, profiles/r05/r05b_*).
+    // Threshold A/B (CS_FM_GENERAL_LIST_MIN, C4 call ms, Q_text / repetitive DNA,
+    // profiles/r05/r05c_*): 1: 0.448 / 0.774, 2: 0.395 / 0.758, 4: 0.395 / 0.855, 8: 0.398 /
+    // 1.145 — the default is 2.
+    uint32_t gm = 0, ng = 0;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const bool g = st[j] == 3 || st[j] == 5;
+      gm |= (uint32_t)g << j;
+      ng += (uint32_t)__popcll(__ballot(g));
+    }
+    if (ll.gen_list && ng >= ll.gen_list) {
+      nlisted += wave_list<U>(ll.list2, ll.cnt2, slot, gm);
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if ((gm >> j) & 1u) st[j] = 6;  // listed
+    } else if ((threadIdx.x & 63) == 0) {
+      ll.cnt2[slot] = 0;
+    }
+    list_listed_add(ll, nlisted);
   }
   // the general search for the rest, with only (o0, m) of each pattern still live
   bool general = false;
@@ -2368,9 +2399,15 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
   __shared__ uint32_t rare[kMaxExc];
   static_assert(kBlk >= 256, "one map entry per thread");
   uint32_t c1 = 0;
-  if constexpr (kList) {  // a block with nothing listed leaves after one load
+  if constexpr (kList) {
+    // nothing listed in the whole call (the counters): every block leaves at its first load;
+    // else a block with nothing listed in its slots after one more load (then retired)
+    if (!list_any(ll)) return;
     c1 = slot_count(ll.cnt, npat);
-    if (!__syncthreads_or(c1 != 0)) return;
+    if (!__syncthreads_or(c1 != 0 || slot_count(ll.cnt2, npat) != 0)) {
+      list_retire(ll);
+      return;
+    }
   }
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
@@ -2380,11 +2417,13 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
     list_for_each(ll.list, c1, [&](uint64_t q, bool act) {
       if (act) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, false, cmap, rare, q);
     });
-    // then the general search of what it listed: the same block owns the same slots of list2,
-    // so no second launch (k_count_list) waits for the grid
+    // then the general search of what it listed and what the staged kernel listed there: the
+    // same block owns the same slots of list2, so no second launch (k_count_list) waits for
+    // the grid
     __shared__ NodeTable T;
     __syncthreads();
     count_list_general<W, kBytes>(ix, T, pats, offs, co, fixed_m, ll, slot_count<true>(ll.cnt2, npat));
+    list_retire(ll);
   } else {
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
     if (q < npat) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, skip_short, cmap, rare, q);
@@ -2488,9 +2527,15 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
   __shared__ uint16_t cmap[256];
   __shared__ uint32_t rare[kMaxExc];
   uint32_t c1 = 0;
-  if constexpr (kList) {  // a block with nothing listed or deferred leaves after one load
+  if constexpr (kList) {
+    // nothing listed or deferred in the whole call: every block leaves at its first load;
+    // else a block with nothing in its slots after one more load (then retired)
+    if (!list_any(ll)) return;
     c1 = slot_count(ll.cnt, npat);
-    if (!__syncthreads_or(c1 != 0 || slot_count(ll.cnt2, npat) != 0)) return;
+    if (!__syncthreads_or(c1 != 0 || slot_count(ll.cnt2, npat) != 0)) {
+      list_retire(ll);
+      return;
+    }
   }
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
@@ -2505,6 +2550,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
     __shared__ NodeTable T;
     __syncthreads();
     locate_list_general(ix, T, pats, offs, limit, op, ll, slot_count<true>(ll.cnt2, npat));
+    list_retire(ll);
   } else {  // no lane returns early: the wave sums its counts at the end
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
     locate_long_one<kV16, true>(ix, pats, offs, limit, op, ll, cmap, rare, q, q < npat);
@@ -2700,9 +2746,11 @@ __global__ __launch_bounds__(kBlk) void k_locate_list(DevIndex ix, const uint8_t
                                                       const uint64_t* __restrict__ offs, uint64_t npat,
                                                       uint64_t limit, OnePass op, LongList ll) {
   __shared__ NodeTable T;
+  // (hdr: the staged search listed into the counters, list_any / list_retire)
+  if (ll.hdr && !list_any(ll)) return;
   const uint32_t c = slot_count(ll.cnt2, npat);
-  if (!__syncthreads_or(c != 0)) return;
-  locate_list_general(ix, T, pats, offs, limit, op, ll, c);
+  if (__syncthreads_or(c != 0)) locate_list_general(ix, T, pats, offs, limit, op, ll, c);
+  if (ll.hdr) list_retire(ll);
 }
 
 // The batch count over the quaternary wavelet matrix with left contexts (C3: sigma = 256,
@@ -4263,61 +4311,73 @@ cs_status launch_count(const cs_fm_index* h, const uint8_t* d_pats, const uint64
   return launch_count_ex(h, d_pats, d_offs, npat, co, flags, st, fixed_m, false);
 }
 
-// tuning hook CS_FM_COUNT_NOBAR (read per call): 1 (the default since round 4) = the staged
-// kernel's general search reads the node table through the caches (no block barrier: a wave
-// whose patterns are done leaves at once instead of waiting at the barrier for the block's
-// slowest record read), 0 = a block-wide LDS copy behind a barrier.  C4 headline A/Bs in one
+// Tuning selectors (round 5): the query paths read no environment.
+// A handle takes its defaults from the CS_FM_* variables once, when it is created
+// (read_tuning, fm_capi.hip: cs_fm_index::tune), and a call's flags add CS_QT_* bits over
+// them (cs_fmindex.h), so tests and A/Bs select kernels per call without touching the
+// environment — and a thread that changes the environment cannot race a call.
+//
+// CS_QT_BARRIER (CS_FM_COUNT_NOBAR=0): the staged kernel's general search behind a block-wide
+// LDS copy of the node table; the default (since round 4) reads the node table through the
+// caches with no block barrier, so a wave whose patterns are done leaves at once instead of
+// waiting at the barrier for the block's slowest record read.  C4 headline A/Bs in one
 // process: 0.417 against 0.456 ms per call unrouted (profiles/r04/ab_nobar_unrouted.json),
 // 0.401 against 0.413 back to back routed (ab_nobar_b2b.json).  A template parameter (a
 // runtime flag kept both general searches in one kernel: 100 VGPRs, 4 waves per SIMD instead
 // of 79 / 6), honoured for the two-patterns-per-lane forms over occurrence lines and learned
 // lines (byte strings, routed or not, and 2-bit packed) and locate's phase 1.
-bool count_nobar() {
-  const char* e = std::getenv("CS_FM_COUNT_NOBAR");
-  return !(e && std::atoi(e) == 0);
-}
+inline bool count_nobar(uint32_t flags) { return !(flags & CS_QT_BARRIER); }
 
-// test / tuning hook CS_FM_QCTX_STAGED (read per call): 0 = the quaternary matrix counts
-// through k_count (one pattern per lane) instead of the staged k_count_qctx
-bool qctx_staged() {
-  const char* e = std::getenv("CS_FM_QCTX_STAGED");
-  return !(e && std::atoi(e) == 0);
-}
+// CS_QT_QCTX_UNSTAGED (CS_FM_QCTX_STAGED=0): the quaternary matrix counts through k_count (one
+// pattern per lane) instead of the staged k_count_qctx
+inline bool qctx_staged(uint32_t flags) { return !(flags & CS_QT_QCTX_UNSTAGED); }
+
+// the call's flags with the handle's tuning defaults
+inline uint32_t call_flags(const cs_fm_index* h, uint32_t flags) { return flags | h->tune; }
 
 // k_count_long over the batch (skip_short: only its long patterns, as k_count_ctx's kSkipLong),
 // then k_count_list over the patterns it listed; byte_text: the byte text even when the
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
-// The call's long-pattern lists (LongList): slot lists of the staged kernel (list / cnt,
-// unless `direct`) and of k_count_long / k_locate_long for the general search (list2 / cnt2),
-// u16 offsets inside the slots' regions; in one stream-ordered allocation.  Direct launches
-// (every pattern to the long kernel, no staged kernel before it) zero cnt2 here; otherwise the
-// staged kernel does, wave by wave.
+// The call's long-pattern lists (LongList): the counters' header (kListHdrBytes, zero between
+// calls), slot lists of the staged kernel (list / cnt, unless `direct`) and of k_count_long /
+// k_locate_long for the general search (list2 / cnt2), u16 offsets inside the slots' regions;
+// in the caller's workspace (round 5: cs_fm_workspace_bytes, no allocation in the call) or in
+// one stream-ordered allocation whose header is zeroed here.  Direct launches (every pattern
+// to the long kernel, no staged kernel before it) zero cnt2 here and use no counters;
+// otherwise the staged kernel writes every slot's counts, wave by wave.
 static_assert(kLongRegion == 2 * kBlk && kLongSlot == 2 * 64, "a slot is one wave's patterns (U = 2)");
+static_assert(kListHdrBytes % 256 == 0, "the lists start 256-B aligned");
 struct LongBufs {
   StreamBuf buf;
   LongList ll;
   static uint64_t bytes(uint64_t npat, bool direct) {
     const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
-    return (direct ? 1 : 2) * slots * (kLongSlot * 2 + 4);
+    return kListHdrBytes + (direct ? 1 : 2) * slots * (kLongSlot * 2 + 4);
   }
-  // into the call's own allocation (`at`, bytes(npat, direct) of it), or one of its own
-  cs_status alloc(uint64_t npat, bool direct, hipStream_t st, void* at = nullptr) {
+  // into `at` (bytes(npat, direct) of it: the caller's workspace, whose header the calls keep
+  // zeroed, or the call's own allocation when `fresh`), or an allocation of its own
+  cs_status alloc(uint64_t npat, bool direct, hipStream_t st, void* at = nullptr, bool fresh = true) {
     const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion, slots = regions * kSlotsPerRegion;
     const uint64_t entries = slots * kLongSlot;
     const uint64_t lists = (direct ? 1 : 2) * entries * 2;
     if (!at) FMX_HIP(buf.alloc(bytes(npat, direct), st));
     uint8_t* p = at ? static_cast<uint8_t*>(at) : buf.as<uint8_t>();
+    ll.hdr = reinterpret_cast<uint32_t*>(p);
+    if ((!at || fresh) && !direct) FMX_HIP(hipMemsetAsync(p, 0, kListHdrBytes, st));
+    p += kListHdrBytes;
     ll.list2 = reinterpret_cast<uint16_t*>(p);
     ll.cnt2 = reinterpret_cast<uint32_t*>(p + lists);
     if (!direct) {
       ll.list = ll.list2 + entries;
       ll.cnt = ll.cnt2 + slots;
     } else {
+      ll.hdr = nullptr;
       FMX_HIP(hipMemsetAsync(ll.cnt2, 0, slots * 4, st));
     }
     return CS_OK;
   }
 };
+
 
 // blocks of the list kernels (list_for_each): two rounds of the blocks resident at 5 waves
 // per SIMD (256 CUs x 5 blocks of 4 waves), and at least slots / kBlk so that a block's
@@ -4335,7 +4395,7 @@ unsigned long_list_grid(uint64_t npat) {
 template <bool kBytes>
 cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
                               uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
-                              const LongList* routed, bool skip_short, bool byte_text) {
+                              const LongList* routed, bool skip_short, bool byte_text, bool loads8) {
   LongBufs own;
   LongList ll;
   if (routed) {
@@ -4346,22 +4406,16 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
     ll = own.ll;
   }
   const unsigned g = routed ? long_list_grid(npat) : grid_for(npat, kBlk, 0xFFFFFFFFu);
-  // tuning hook CS_FM_LONG_V16 (read per call): 0 = 8-B pattern / window loads, 3 = 16-B
-  // vectors for the pattern's packed part and the window (the default: C4 150-mers 1.87 ->
-  // 1.55 ms, 64-mers 1.25 -> 1.16-1.21, profiles/r03/long_probe_v16.json), 1 / 2 = partial forms
-  const char* ev = std::getenv("CS_FM_LONG_V16");
-  const int v16 = ev ? std::atoi(ev) : 3;
-  if (routed && ix.ptext && !byte_text && v16 == 3)  // the routed default
+  // CS_QT_LONG_LOADS8 (CS_FM_LONG_V16=0): 8-B pattern / window loads; the default 16-B vectors
+  // for the pattern's packed part and the window (C4 150-mers 1.87 -> 1.55 ms, 64-mers 1.25 ->
+  // 1.16-1.21, profiles/r03/long_probe_v16.json; round 4's partial forms 1 / 2 are gone)
+  if (routed && ix.ptext && !byte_text && !loads8)  // the routed default
     k_count_long<0, true, kBytes, 3, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
   else if (routed && ix.ptext && !byte_text)
     k_count_long<0, true, kBytes, 0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
   else if (routed)
     k_count_long<0, false, kBytes, 0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
-  else if (ix.ptext && !byte_text && v16 == 1)
-    k_count_long<0, true, kBytes, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
-  else if (ix.ptext && !byte_text && v16 == 2)
-    k_count_long<0, true, kBytes, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
-  else if (ix.ptext && !byte_text && v16 == 3)
+  else if (ix.ptext && !byte_text && !loads8)
     k_count_long<0, true, kBytes, 3><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   else if (ix.ptext && !byte_text)
     k_count_long<0, true, kBytes><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
@@ -4377,53 +4431,51 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
 }
 cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
                             uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
-                            const LongList* routed, bool byte_text = false) {
-  return launch_count_long_t<false>(ix, d_pats, d_offs, npat, co, st, fixed_m, routed, false, byte_text);
+                            const LongList* routed, uint32_t flags) {
+  return launch_count_long_t<false>(ix, d_pats, d_offs, npat, co, st, fixed_m, routed, false,
+                                    (flags & CS_QT_LONG_BYTE_TEXT) != 0, (flags & CS_QT_LONG_LOADS8) != 0);
 }
 
-// Whether a device batch is routed (the staged kernel lists its long patterns for
-// k_count_long / k_locate_long in the same call): indexes k_count_long serves (occurrence
-// lines, the full SA and the text), and batches of kRouteMin patterns or more — the lists
-// cost a call ≈ 8 µs whatever it holds (one stream-ordered allocation and one more launch:
-// C4's 12.5 M 20-mers 0.381 -> 0.397 ms, C2's 1 M 36 -> 47 µs), so a smaller batch keeps
-// every pattern in the staged kernel (round 2's path; its long patterns take the general
-// search: CS_Q_LONG sends a batch of long patterns to k_count_long directly).  Tuning hook
-// CS_FM_LONG_ROUTE (read per call): 0 = never route, 1 = route every batch (the GPU tests
-// set it, so their small batches take the lists), unset = by size.
-constexpr uint64_t kRouteMin = 4u << 20;
-bool can_route(const cs_fm_index* h, const DevIndex& ix, uint64_t npat, uint32_t flags) {
+// Whether a device batch is routed (the staged kernel lists its long patterns — and, for
+// counts, the patterns left to the general search — for k_count_long / k_locate_long in the
+// same call): every batch on the indexes k_count_long serves (occurrence lines, the full SA
+// and the text).  Round 4 routed only batches of 4 M patterns or more (kRouteMin): the lists
+// cost a call ≈ 8 µs whatever it held — one stream-ordered allocation and a list kernel that
+// scanned every slot's count (C4's 12.5 M 20-mers 0.381 -> 0.397 ms, C2's 1 M 36 -> 47 µs).
+// Round 5 takes both out: the lists live in the caller's workspace (cs_fm_workspace_bytes)
+// and a list kernel whose counters read 0 leaves at its first load (list_any), so every batch
+// routes and the production path is the one the tests run.
+// CS_QT_NO_ROUTE (CS_FM_LONG_ROUTE=0): never route (the staged kernel alone, round 2's path).
+bool can_route(const cs_fm_index* h, const DevIndex& ix, uint32_t flags) {
   if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return false;
-  if (const char* e = std::getenv("CS_FM_LONG_ROUTE")) return std::atoi(e) != 0;
-  return npat >= kRouteMin || (flags & kQRoute);  // (kQRoute: a host batch with long patterns)
+  return !(flags & CS_QT_NO_ROUTE);
 }
 
 // the staged kernel at count width W: table entries (context records) of U patterns per
 // lane in flight together, then their context sectors or rank steps
 template <int W>
 cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const uint8_t* d_pats,
-                         const uint64_t* d_offs, uint64_t npat, const CountOut& co,
-                         hipStream_t st, uint64_t fixed_m, bool packed,
-                         uint32_t flags = 0) {
-  const int U = [] {  // patterns per lane (test / tuning hook CS_FM_COUNT_U, read per call)
-    const char* e = std::getenv("CS_FM_COUNT_U");
-    const int u = e ? std::atoi(e) : 2;
-    return u == 1 || u == 4 ? u : 2;
-  }();
+                              const uint64_t* d_offs, uint64_t npat, const CountOut& co,
+                              hipStream_t st, uint64_t fixed_m, bool packed, uint32_t flags,
+                              const Work& work) {
+  // patterns per lane: CS_QT_COUNT_U1 / CS_QT_COUNT_U4 (CS_FM_COUNT_U=1 / 4), else 2
+  const int U = (flags & CS_QT_COUNT_U1) ? 1 : (flags & CS_QT_COUNT_U4) ? 4 : 2;
+  const bool nobar = count_nobar(flags);
   const bool lo = h->line_fmt == kFmtLOcc;
   const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
-  if (packed && lo && count_nobar())
+  if (packed && lo && nobar)
     k_count_ctx<LOccE, 2, false, true, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                       nullptr, fixed_m);
   else if (packed && lo)
     k_count_ctx<LOccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                 nullptr, fixed_m);
-  else if (packed && count_nobar())
+  else if (packed && nobar)
     k_count_ctx<OccE, 2, false, true, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                      nullptr, fixed_m);
   else if (packed)
     k_count_ctx<OccE, 2, false, true, W><<<g2, kBlk, 0, st>>>(ix, d_pats, nullptr, npat, co, 0,
                                                                nullptr, fixed_m);
-  else if (lo && count_nobar())
+  else if (lo && nobar)
     k_count_ctx<LOccE, 2, false, false, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                        nullptr, fixed_m);
   else if (lo)
@@ -4435,21 +4487,26 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   else if (W == 8 && U == 4)
     k_count_ctx<OccE, 4, false, false, 8><<<grid_for((npat + 3) / 4, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m);
-  else if (d_offs && can_route(h, ix, npat, flags)) {
-    // long-pattern routing inside the call: the staged kernel counts the short patterns and
-    // lists the long ones, k_count_long (and k_count_list) take them from its lists
+  else if (d_offs && can_route(h, ix, flags)) {
+    // routing inside the call: the staged kernel counts what its one read answers and lists
+    // the long patterns and (unless CS_QT_GENERAL_INLANE) the general-search ones;
+    // k_count_long takes both lists from the workspace (or the call's allocation)
     LongBufs lb;
-    cs_status s = lb.alloc(npat, false, st);
+    const bool ws = work.p && work.bytes >= LongBufs::bytes(npat, false);
+    cs_status s = lb.alloc(npat, false, st, ws ? work.p : nullptr, false);
     if (s != CS_OK) return s;
-    if (count_nobar())
+    // the general searches a wave lists from (LongList::gen_list): CS_QT_GENERAL_INLANE none,
+    // CS_QT_GENERAL_LIST_ALL every one, else the handle's threshold (CS_FM_GENERAL_LIST_MIN)
+    lb.ll.gen_list = (flags & CS_QT_GENERAL_INLANE) ? 0u : (flags & CS_QT_GENERAL_LIST_ALL) ? 1u : h->gen_list_min;
+    if (nobar)
       k_count_ctx<OccE, 2, false, false, W, true, false, true><<<g2, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
     else
       k_count_ctx<OccE, 2, false, false, W, false, false, true><<<g2, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
     FMX_HIP(hipGetLastError());
-    return launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, &lb.ll);
-  } else if (count_nobar())
+    return launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, &lb.ll, flags);
+  } else if (nobar)
     k_count_ctx<OccE, 2, false, false, W, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0,
                                                                       nullptr, fixed_m);
   else
@@ -4459,12 +4516,18 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
   return CS_OK;
 }
 
+uint64_t count_workspace_bytes(const cs_fm_index* h, uint64_t npat) {
+  (void)h;
+  return LongBufs::bytes(npat, false);
+}
+
 cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                           uint64_t npat, const CountOut& co, uint32_t flags, hipStream_t st,
-                          uint64_t fixed_m, bool packed) {
+                          uint64_t fixed_m, bool packed, const Work& work) {
   if (!npat) return CS_OK;
+  flags = call_flags(h, flags);
   const DevIndex ix = query_dev(h, flags);
-  if (h->line_fmt == kFmtQwm && ix.ptab_k && ix.lctx && !ix.wide && !packed && qctx_staged()) {
+  if (h->line_fmt == kFmtQwm && ix.ptab_k && ix.lctx && !ix.wide && !packed && qctx_staged(flags)) {
     // the staged quaternary-matrix kernel (C3)
     const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
     if (co.width == 8)
@@ -4481,26 +4544,24 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
     // long patterns: one per lane in k_count_long (record, candidates, SA, text window as
     // independent rounds; against the 2-bit text when the index has it), the patterns it
     // does not answer listed for k_count_list; kept out of the staged kernel, whose
-    // registers the pattern and text words would take from the 20-mer path.  Tuning hook
-    // (read per call): CS_FM_LONG_KERNEL=0 = round 2's kernel (the general search with
-    // look-ahead rounds, k_count<OccE, false, true>), 2 = the byte text even when the
-    // packed text is there.
-    const char* ek = std::getenv("CS_FM_LONG_KERNEL");
-    if (ek && std::atoi(ek) == 0) {
+    // registers the pattern and text words would take from the 20-mer path.
+    // CS_QT_LONG_ROUND2 (CS_FM_LONG_KERNEL=0): round 2's kernel (the general search with
+    // look-ahead rounds, k_count<OccE, false, true>); CS_QT_LONG_BYTE_TEXT (=2): the byte text
+    // even when the packed text is there.
+    if (flags & CS_QT_LONG_ROUND2) {
       k_count<OccE, false, true><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(ix, d_pats, d_offs,
                                                                                     npat, co, fixed_m);
     } else {
-      cs_status r = launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, nullptr,
-                                      ek && std::atoi(ek) == 2);
+      cs_status r = launch_count_long(ix, d_pats, d_offs, npat, co, st, fixed_m, nullptr, flags);
       if (r != CS_OK) return r;
     }
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.ptab_k) {
-    if (co.width == 8) return launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags);
-    if (co.width == 4) return launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags);
-    return launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags);
+    if (co.width == 8) return launch_count_staged<8>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags, work);
+    if (co.width == 4) return launch_count_staged<4>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags, work);
+    return launch_count_staged<1>(h, ix, d_pats, d_offs, npat, co, st, fixed_m, packed, flags, work);
   }
   const unsigned g = grid_for(npat, kBlk, 0xFFFFFFFFu);
   if (packed)
@@ -4527,19 +4588,19 @@ cs_status launch_count_server(const cs_fm_index* h, uint32_t seq_done, uint64_t 
 cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                              uint64_t npat, uint64_t* d_out, hipStream_t st, uint32_t flags) {
   if (!npat) return CS_OK;
+  flags = call_flags(h, flags);
   const DevIndex ix = query_dev(h, flags);
   // the patterns k_count_long counts (CS_Q_LONG: all of them; routed device batches: those
   // of kFastM characters or more) take its twin, the rest the general search's
   const bool lk = h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa;
-  const char* ek = std::getenv("CS_FM_LONG_KERNEL");
-  const bool old = ek && std::atoi(ek) == 0;
+  const bool old = (flags & CS_QT_LONG_ROUND2) != 0;
   if (!(lk && (flags & CS_Q_LONG) && !old))
     FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), ix, d_pats, d_offs, npat, d_out);
   // (a routed call's long patterns: can_route; ADVICE r03: the twin now follows the call)
-  if (lk && !old && ((flags & CS_Q_LONG) || can_route(h, ix, npat, flags))) {
+  if (lk && !old && ((flags & CS_Q_LONG) || (d_offs && can_route(h, ix, flags)))) {
     const CountOut co{d_out, nullptr, nullptr, 0, 8};
     return launch_count_long_t<true>(ix, d_pats, d_offs, npat, co, st, 0, nullptr, !(flags & CS_Q_LONG),
-                                     ek && std::atoi(ek) == 2);
+                                     (flags & CS_QT_LONG_BYTE_TEXT) != 0, (flags & CS_QT_LONG_LOADS8) != 0);
   }
   return CS_OK;
 }
@@ -4556,24 +4617,33 @@ cs_status launch_locrec_hits(const cs_fm_index* h, const uint8_t* d_pats, const 
 // Batch locate in one call (OnePass above): occurrence lines with a prefix table, left
 // contexts and the full suffix array (C2, C4).  *done = false when the index has another
 // shape (the caller runs the two phases).  Writes d_out_offs (npat + 1) and, when the
-// total fits `cap`, every position; synchronises `st` for *total.  CS_FM_LOCATE_ONEPASS=0
-// (read per call) turns it off.
+// total fits `cap`, every position; synchronises `st` for *total.  CS_QT_NO_ONEPASS
+// (CS_FM_LOCATE_ONEPASS=0) turns it off.
+// The call's buffers (the lists, then per pattern its count and record, the tiles, the wide
+// ranges) in the caller's workspace when it holds locate_workspace_bytes(npat), else in one
+// stream-ordered allocation.
+uint64_t locate_lo_bytes(const cs_fm_index* h, uint64_t npat, uint64_t wide_cap) {
+  const uint64_t tiles = (npat + kLocTile - 1) / kLocTile;
+  const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
+  return (npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull;
+}
+uint64_t locate_workspace_bytes(const cs_fm_index* h, uint64_t npat) {
+  return LongBufs::bytes(npat, false) + locate_lo_bytes(h, npat, npat);
+}
 cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, hipStream_t st,
-                                bool* done, uint32_t flags) {
+                                bool* done, uint32_t flags, const Work& work) {
   *done = false;
-  if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
-    if (std::atoi(e) == 0) return CS_OK;
+  flags = call_flags(h, flags);
+  if (flags & CS_QT_NO_ONEPASS) return CS_OK;
   DevIndex ix = h->dev();
   if (flags & CS_Q_NO_LOC_RECORDS) ix.lrec = nullptr;
   // positions from the full SA (narrow), or by the short walk over walk lines with
-  // text-position marks (OnePass above); CS_FM_LOCATE_ONEPASS=1 keeps the walk indexes on
-  // the two phases (test hook: CS_FM_LOCATE_ONEPASS=2 = the full SA only)
+  // text-position marks (OnePass above); CS_QT_ONEPASS_SA (CS_FM_LOCATE_ONEPASS=2): the full
+  // SA only (a walk index takes the two phases)
   const bool by_sa = h->d_sa && !h->wide;
-  bool by_walk = !h->d_sa && h->d_walk && h->d_wssa && h->walk_marks == 2;
-  if (const char* e = std::getenv("CS_FM_LOCATE_ONEPASS"))
-    if (std::atoi(e) == 2) by_walk = false;
+  const bool by_walk = !h->d_sa && h->d_walk && h->d_wssa && h->walk_marks == 2 && !(flags & CS_QT_ONEPASS_SA);
   if (h->line_fmt != kFmtOcc || !ix.ptab_k || !ix.lctx || !h->lf_exact || !(by_sa || by_walk))
     return CS_OK;
   const int kpos = by_sa ? 0 : h->wide ? 2 : 1;
@@ -4598,27 +4668,34 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // the long patterns the staged kernel lists in the same call
   const bool lk = kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
   const bool long_only = lk && (flags & CS_Q_LONG);
-  const bool routed = lk && !long_only && can_route(h, ix, npat, flags);
+  const bool routed = lk && !long_only && can_route(h, ix, flags);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
   // locate records: a pattern its record does not answer reads its context record in the
-  // same lane (the default), or is listed for the list kernels (tuning hook
-  // CS_FM_LOC_DEFER=1, read per call), which search it with the staged stages
-  // (locate_miss_one).  Deferring shortens the search kernel (C4 Q_text: 468 -> 410 us) but
-  // the 7 % it lists cost the list kernel 130 us of dependent chains: 0.665 against 0.612 ms
+  // same lane (the default), or is listed for the list kernels (CS_QT_LOC_DEFER,
+  // CS_FM_LOC_DEFER=1), which search it with the staged stages (locate_miss_one).  Deferring
+  // shortens the search kernel (C4 Q_text: 468 -> 410 us) but the 7 % it lists cost the list kernel 130 us of dependent chains: 0.665 against 0.612 ms
   // per call (profiles/r04/ab_defer_fast_misses.json; 0.786 / 0.631 when the list kernel ran
   // the general search, ab_defer.json)
-  bool defer = false;
-  if (const char* e = std::getenv("CS_FM_LOC_DEFER"))
-    defer = std::atoi(e) == 1 && kpos == 0 && ix.lrec;
-  StreamBuf ws;
-  const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
-  const uint64_t lo = (npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull;
-  // (the long-pattern lists, when the call has them, in the same allocation: one
-  // stream-ordered allocation per call, not two)
+  const bool defer = (flags & CS_QT_LOC_DEFER) && kpos == 0 && ix.lrec;
+  // (the long-pattern lists, when the call has them, first, in the same buffer: one
+  // stream-ordered allocation per call without a workspace, not two)
   const bool lists = long_only || routed || defer;
-  FMX_HIP(ws.alloc(lo + (lists ? LongBufs::bytes(npat, long_only) : 0), st));
+  const uint64_t lb_bytes = lists ? LongBufs::bytes(npat, long_only) : 0;
+  const uint64_t lo = locate_lo_bytes(h, npat, wide_cap);
+  const bool use_ws = work.p && work.bytes >= LongBufs::bytes(npat, false) + lo;
+  StreamBuf wsb;
+  uint8_t* base;
+  uint64_t lo_at;
+  if (use_ws) {
+    base = static_cast<uint8_t*>(work.p);
+    lo_at = LongBufs::bytes(npat, false);  // (the workspace's lists sit where a count's do)
+  } else {
+    FMX_HIP(wsb.alloc(lb_bytes + lo, st));
+    base = wsb.as<uint8_t>();
+    lo_at = lb_bytes;
+  }
   OnePass op;
-  op.rec = ws.as<uint64_t>();
+  op.rec = reinterpret_cast<uint64_t*>(base + lo_at);
   op.tiles = op.rec + npat;
   op.nwide = reinterpret_cast<unsigned long long*>(op.tiles + tiles);
   op.wide = reinterpret_cast<uint64_t*>(op.nwide + 1);
@@ -4632,7 +4709,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // the barrier-free search (CS_FM_COUNT_NOBAR, kPos 0) adds its tile totals: each block
   // zeroes its tile first (and block 0 the wide-range counter); a call without it zeroes the
   // counter (and, CS_Q_LONG, the tiles) here
-  const bool nobar = kpos == 0 && count_nobar();
+  const bool nobar = kpos == 0 && count_nobar(flags);
   if (long_only)
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
   else if (!nobar)
@@ -4641,7 +4718,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.defer = defer ? 1u : 0u;
   if (long_only || routed || defer) {
     LongBufs lb;
-    cs_status ls = lb.alloc(npat, long_only, st, ws.as<uint8_t>() + lo);
+    cs_status ls = lb.alloc(npat, long_only, st, base, !use_ws);
     if (ls != CS_OK) return ls;
     if (long_only)
       ;  // (tiles zeroed above)
@@ -4660,9 +4737,8 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
     FMX_HIP(hipGetLastError());
     if (long_only || routed) {
       const unsigned g1 = routed ? long_list_grid(npat) : grid_for(npat, kBlk, 0xFFFFFFFFu);
-      // tuning hook CS_FM_LONG_V16 (k_count_long's): 0 = 8-B pattern / window loads
-      const char* ev = std::getenv("CS_FM_LONG_V16");
-      const bool v0 = ev && std::atoi(ev) == 0;
+      // CS_QT_LONG_LOADS8 (k_count_long's): 8-B pattern / window loads
+      const bool v0 = (flags & CS_QT_LONG_LOADS8) != 0;
       if (routed && v0)
         k_locate_long<0, true><<<g1, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
       else if (routed)
@@ -4712,18 +4788,17 @@ cs_status launch_locate_ranges(const cs_fm_index* h, const uint8_t* d_pats,
                                hipStream_t st, uint32_t flags) {
   StreamBuf cnt, tmp;
   FMX_HIP(cnt.alloc((npat + 1) * 8, st));
+  flags = call_flags(h, flags);
   const DevIndex ix = query_dev(h, flags);
   if ((h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc) && ix.lctx && ix.ptab_k) {
-    const int U = [] {  // patterns per lane (tuning hook CS_FM_LOCATE_U: 1 or 2, read per call)
-      const char* e = std::getenv("CS_FM_LOCATE_U");
-      return e && std::atoi(e) == 1 ? 1 : 2;
-    }();
+    // patterns per lane: CS_QT_LOCATE_U1 (CS_FM_LOCATE_U=1) one, else two
+    const int U = (flags & CS_QT_LOCATE_U1) ? 1 : 2;
     const CountOut co{cnt.p, nullptr, nullptr, 0, 8};
     const unsigned g2 = grid_for((npat + 1) / 2, kBlk, 0xFFFFFFFFu);
     if (h->line_fmt == kFmtOcc && U == 1)
       k_count_ctx<OccE, 1, true, false, 8><<<grid_for(npat, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, limit, d_sp, 0);
-    else if (h->line_fmt == kFmtOcc && count_nobar())
+    else if (h->line_fmt == kFmtOcc && count_nobar(flags))
       k_count_ctx<OccE, 2, true, false, 8, true><<<g2, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co,
                                                                       limit, d_sp, 0);
     else if (h->line_fmt == kFmtOcc)  // staged, two patterns per lane
@@ -4794,18 +4869,13 @@ __global__ __launch_bounds__(kBlk) void k_locate_sa_wide(const uint32_t* __restr
   }
 }
 
-// tuning hook CS_FM_WALK_ROWS=1 (read per call): short walks from an expanded rows
-// buffer (k_expand_rows + k_walk_short) instead of straight from the records
-bool walk_rows_hook() {
-  const char* e = std::getenv("CS_FM_WALK_ROWS");
-  return e && std::atoi(e) == 1;
-}
 
 cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
                              const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
                              uint64_t* d_out_pos, hipStream_t st, unsigned long long* err_word,
                              uint32_t flags, uint32_t steps_only) {
   if (!total) return CS_OK;
+  flags = call_flags(h, flags);
   if (h->d_sa && h->lf_exact && !(flags & CS_Q_NO_FULL_SA)) {  // full suffix array: one read per position
     if (steps_only) {  // no LF steps: one SA read per position
       FMX_HIP(hipMemsetAsync(d_out_pos, 0, total * 8, st));
@@ -4835,11 +4905,11 @@ cs_status launch_locate_walk(const cs_fm_index* h, const uint64_t* d_sp,
   unsigned long long* err =
       err_word ? err_word : reinterpret_cast<unsigned long long*>(h->d_err);
   const bool pow2 = ix.stride_shift != 0xFFFFFFFFu;
-  static const bool persistent = [] {  // tuning hook: CS_FM_WALK_PERSISTENT=1
-    const char* e = std::getenv("CS_FM_WALK_PERSISTENT");
-    return e && std::atoi(e) == 1;
-  }();
-  if (ix.walk && h->walk_marks == 2 && !persistent && !walk_rows_hook()) {
+  // CS_QT_WALK_PERSISTENT (CS_FM_WALK_PERSISTENT=1): the persistent walk over a rows buffer;
+  // CS_QT_WALK_ROWS (CS_FM_WALK_ROWS=1): short walks from an expanded rows buffer
+  // (k_expand_rows + k_walk_short) instead of straight from the records
+  const bool persistent = (flags & CS_QT_WALK_PERSISTENT) != 0;
+  if (ix.walk && h->walk_marks == 2 && !persistent && !(flags & CS_QT_WALK_ROWS)) {
     // short walks straight from the records (no rows buffer)
     StreamBuf wide;
     FMX_HIP(wide.alloc((total / (kLocSmall + 1) + 1) * 8 + 8, st));

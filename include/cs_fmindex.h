@@ -96,6 +96,10 @@ typedef struct cs_fm_info {
                               beside their contexts, so a 20-mer's position is one read);
                               0 = none.  Derived on build / open / import, not saved. */
   uint64_t locate_record_width; /* 64 or 16 (bytes per record); 0 = none */
+  uint64_t device_bytes;   /* round 5: every device allocation the handle owns — each image
+                              part with its pad, the derived parts (2-bit text, locate
+                              records, rare-symbol positions), the node table, the overrun
+                              word and the small-batch arena — i.e. the HBM the index holds */
 } cs_fm_info;
 
 void cs_default_build_params(cs_build_params* p);
@@ -229,7 +233,7 @@ cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, cons
 /* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers; offsets must
  * be non-decreasing (checked: CS_ERR_INVALID).  The *_device forms take the same
  * layout in device memory, unchecked.  A batch of more than CS_FM_HOST_CHUNK patterns
- * (environment, default 2^21) runs in chunks: each chunk's caller pages are page-locked
+ * (environment when the handle is created, default 2^21) runs in chunks: each chunk's caller pages are page-locked
  * while the earlier chunks' copies and counts run, and its offsets are checked just before
  * it is queued — so on CS_ERR_INVALID the contents of out_counts are unspecified (the
  * counts of earlier chunks may have been written). */
@@ -289,6 +293,50 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
 #define CS_Q_NO_VERIFY 16u
 #define CS_Q_LONG 32u
 #define CS_Q_NO_LOC_RECORDS 64u
+
+/* Tuning selectors (round 5): flags bits 8-22 choose among equivalent kernels for tests and
+ * A/B measurements — results never change.  A handle takes its defaults from the CS_FM_*
+ * environment once, when it is created (build, create, open, import: the variable named
+ * beside each bit), and a call's flags add these bits over them; no count, locate or extract
+ * call reads the environment.
+ *   CS_QT_BARRIER         staged count / locate phase 1: the general search behind a block-wide
+ *                         LDS copy of the node table (CS_FM_COUNT_NOBAR=0)
+ *   CS_QT_NO_ROUTE        no routing inside the call: the staged kernel searches long
+ *                         patterns itself (CS_FM_LONG_ROUTE=0)
+ *   CS_QT_COUNT_U1 / _U4  staged count: one / four patterns per lane (CS_FM_COUNT_U=1 / 4)
+ *   CS_QT_LONG_LOADS8     long-pattern kernels: 8-B pattern and window loads (CS_FM_LONG_V16=0)
+ *   CS_QT_LONG_ROUND2     CS_Q_LONG counts through round 2's kernel (CS_FM_LONG_KERNEL=0)
+ *   CS_QT_LONG_BYTE_TEXT  long-pattern kernels against the byte text (CS_FM_LONG_KERNEL=2)
+ *   CS_QT_QCTX_UNSTAGED   quaternary matrix: one pattern per lane (CS_FM_QCTX_STAGED=0)
+ *   CS_QT_NO_ONEPASS      cs_fm_locate_device runs the two phases (CS_FM_LOCATE_ONEPASS=0)
+ *   CS_QT_ONEPASS_SA      the one-call locate only over the full SA (CS_FM_LOCATE_ONEPASS=2)
+ *   CS_QT_LOC_DEFER       one-call locate: locate-record misses to the list kernel
+ *                         (CS_FM_LOC_DEFER=1)
+ *   CS_QT_LOCATE_U1       locate phase 1: one pattern per lane (CS_FM_LOCATE_U=1)
+ *   CS_QT_WALK_ROWS       phase 2 walks from an expanded rows buffer (CS_FM_WALK_ROWS=1)
+ *   CS_QT_WALK_PERSISTENT phase 2: the persistent walk kernel (CS_FM_WALK_PERSISTENT=1)
+ *   CS_QT_GENERAL_INLANE  routed count: the staged kernel's lanes run the general searches
+ *                         (patterns the one read cannot finish) themselves; by default a wave
+ *                         holding at least CS_FM_GENERAL_LIST_MIN (2) of them lists them for
+ *                         the list kernel (CS_FM_GENERAL_INLANE=1)
+ *   CS_QT_GENERAL_LIST_ALL routed count: every wave lists its general searches
+ *                         (CS_FM_GENERAL_LIST_ALL=1) */
+#define CS_QT_BARRIER (1u << 8)
+#define CS_QT_NO_ROUTE (1u << 9)
+#define CS_QT_COUNT_U1 (1u << 10)
+#define CS_QT_COUNT_U4 (1u << 11)
+#define CS_QT_LONG_LOADS8 (1u << 12)
+#define CS_QT_LONG_ROUND2 (1u << 13)
+#define CS_QT_LONG_BYTE_TEXT (1u << 14)
+#define CS_QT_QCTX_UNSTAGED (1u << 15)
+#define CS_QT_NO_ONEPASS (1u << 16)
+#define CS_QT_ONEPASS_SA (1u << 17)
+#define CS_QT_LOC_DEFER (1u << 18)
+#define CS_QT_LOCATE_U1 (1u << 19)
+#define CS_QT_WALK_ROWS (1u << 20)
+#define CS_QT_WALK_PERSISTENT (1u << 21)
+#define CS_QT_GENERAL_INLANE (1u << 22)
+#define CS_QT_GENERAL_LIST_ALL (1u << 23)
 
 /* Where a batch count writes.  width 8: uint64 counts (the reference's return type,
  * fm_index.hpp:26).  width 4: uint32, exact while n < 2^32 (CS_ERR_INVALID otherwise).
@@ -385,6 +433,25 @@ cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, co
                                  uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
                                  uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
                                  void* stream);
+/* Device workspace (round 5): a count of a device batch routes its long patterns and the
+ * patterns its one read cannot finish to lists the next kernel takes, and the one-call locate
+ * keeps per-pattern counts, records and tile totals between its kernels.  The plain entry
+ * points allocate that memory per call (stream-ordered); the *_ws forms take it from the
+ * caller — no allocation inside the call.  cs_fm_workspace_bytes(h, npat) bytes serve a
+ * count or a one-call locate of up to npat patterns.  The memory must be zero-filled before
+ * its first use (the calls leave it that way: the list kernel's last block re-zeroes the
+ * counters it used), and one workspace serves one call at a time: calls that share it must
+ * be ordered (one stream, or events).  work_bytes smaller than needed: the call allocates as
+ * the plain form does. */
+uint64_t cs_fm_workspace_bytes(const cs_fm_index* h, uint64_t npat);
+cs_status cs_fm_count_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                                uint64_t fixed_m, uint64_t npat, const cs_count_out* out,
+                                uint32_t flags, void* d_work, uint64_t work_bytes, void* stream);
+cs_status cs_fm_locate_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
+                                 void* d_work, uint64_t work_bytes, void* stream);
+
 /* Measurement twin of phase 2 (bench.py's walk roofline): d_steps[j] = the LF steps the
  * walk of reported row j takes before its sample (0 with the full suffix array). */
 cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,

@@ -28,10 +28,23 @@ def rows(pattern):
     return out
 
 
+def _ctx_is_loc(name):
+    """k_count_ctx<E, U, kLoc, ...>: its third template argument (demangled, or the mangled
+    ...EELi<U>ELb<kLoc>E form)."""
+    import re
+    m = re.search(r"k_count_ctx<[^,]+,\s*\d+,\s*(true|false)", name)
+    if m:
+        return m.group(1) == "true"
+    m = re.search(r"k_count_ctxI.*?EELi\dELb([01])E", name)
+    return bool(m and m.group(1) == "1")
+
+
 def short(name):
-    if "k_count_ctx" in name:  # template <int U, bool kLoc>: count or locate phase 1
-        return "k_count_ctx_loc" if ("Lb1E" in name or ", true>" in name) else "k_count_ctx"
-    for k in ("k_count_bytes", "k_count_one", "k_count_ctx", "k_count", "k_build_lctx", "k_walk_lines", "k_walk_pack",
+    if "k_count_ctx" in name:  # count, or locate (phase 1 / the one-call search)
+        return "k_count_ctx_loc" if _ctx_is_loc(name) else "k_count_ctx"
+    for k in ("k_count_bytes", "k_count_one", "k_count_long", "k_count_list", "k_locate_long",
+              "k_locate_list", "k_locate_emit_wide", "k_locate_emit", "k_scan_tiles", "k_count_qctx",
+              "k_count_ctx", "k_count", "k_build_lctx", "k_walk_lines", "k_walk_pack",
               "k_walk_base", "k_walk_samples", "k_walk", "k_occ_pack", "k_occ_base", "k_locate_ranges", "k_expand_rows", "k_lf", "k_bwt_ssa", "k_bwt",
               "k_build_ptab", "k_locate_sa_wide", "k_locate_sa", "k_extract_text", "k_extract",
               "k_fill_records16", "k_fill_records_q", "k_fill_records",
@@ -52,8 +65,13 @@ def main():
         dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         by.setdefault(n, []).append(dur)
     for n, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
-        res["kernels"][n] = {"dispatches": len(v), "mean_ns": statistics.mean(v), "min_ns": min(v),
-                             "max_ns": max(v), "total_ns": sum(v)}
+        # round 5: the median over the dispatches is the figure to set beside bench.py's
+        # roofline (itself a median over its timed launches) — a slow first dispatch (cold
+        # TLB / caches) moves the mean, not the median
+        res["kernels"][n] = {"dispatches": len(v), "median_ns": statistics.median(v),
+                             "mean_ns": statistics.mean(v), "min_ns": min(v),
+                             "max_ns": max(v), "total_ns": sum(v),
+                             "median_after_first_ns": statistics.median(v[1:]) if len(v) > 1 else None}
     for sub, names in (("pmc_fetch", ["FETCH_SIZE"]), ("pmc_l2", ["TCC_HIT_sum", "TCC_MISS_sum"])):
         for r in rows(os.path.join(d, sub, "**", "*counter_collection.csv")):
             n = short(r.get("Kernel_Name", ""))

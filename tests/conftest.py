@@ -24,11 +24,10 @@ sys.path.insert(0, ROOT)
 # of test_gpu_scale.py included.
 GPU_SUITE_BUDGET_S = 550
 
-# Long-pattern routing inside a call (fm_query.hip can_route) is chosen by batch size: only
-# batches of 4 M patterns or more are routed by default.  The tests' batches are small, so
-# they route every batch (CS_FM_LONG_ROUTE=1) to exercise the lists; the tests that need the
-# unrouted path set CS_FM_LONG_ROUTE=0 (or unset it) around their calls.
-os.environ.setdefault("CS_FM_LONG_ROUTE", "1")
+# Round 5: every device batch routes its long patterns (and the patterns its one read cannot
+# finish) to the list kernel inside the call — no batch-size threshold, no environment read
+# by a query — so the tests' batches run the production path; the
+# unrouted staged kernel is a per-call selector (CS_QT_NO_ROUTE) the long-pattern tests use.
 
 
 def pytest_configure(config):

@@ -253,13 +253,18 @@ def test_host_batch_buffers_sharing_pages():
 
 @pytest.mark.parametrize("chunk", [333_333, 1 << 20, 0])
 def test_host_batch_chunked(chunk, monkeypatch):
-    """cs_fm_count_batch over a large ragged host batch in chunks (CS_FM_HOST_CHUNK; 0 = the
+    """cs_fm_count_batch over a large ragged host batch in chunks (CS_FM_HOST_CHUNK when the
+    handle is created; 0 = the
     default 2 M patterns): the caller's pages page-locked piece by piece while earlier chunks
     run; offsets starting inside the caller's buffer (offs[0] > 0), empty patterns, the
     counts in the same arena right after the patterns — equal to one unchunked call."""
     pkg = load_pkg()
     t = O.gen_dna(6, 300_000).tobytes()
+    if chunk:  # (read when the handle is created)
+        monkeypatch.setenv("CS_FM_HOST_CHUNK", str(chunk))
     g = pkg.FMIndex.build_from_text(t)
+    monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
+    g1 = pkg.FMIndex.build_from_text(t)  # one chunk
     rng = np.random.default_rng(3)
     npat = 2_500_000
     lens = rng.integers(0, 33, npat)
@@ -274,12 +279,9 @@ def test_host_batch_chunked(chunk, monkeypatch):
     arena[lead:lead + body.size] = body
     out = arena[start:].view(np.uint64)
     offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64) + lead
-    if chunk:
-        monkeypatch.setenv("CS_FM_HOST_CHUNK", str(chunk))
     st = pkg.lib().cs_fm_count_batch(g._h, pkg._u8(arena), pkg._u64(offs), npat, pkg._u64(out), None)
     assert st == 0, pkg.lib().cs_fm_last_error()
-    monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
-    want = g.count_batch(buf=arena[:lead + body.size].copy(), offs=offs)
+    want = g1.count_batch(buf=arena[:lead + body.size].copy(), offs=offs)
     assert np.array_equal(out, want)
     assert (out[lens == 0] == len(t)).all() and (out >= 1).mean() > 0.5
 
@@ -303,9 +305,11 @@ def test_host_batch_long_chunks(monkeypatch):
         pats.append(bytes(p))
     pats[2500] = pats[2500][:20]
     want = [ref.count(p) for p in pats]
-    monkeypatch.setenv("CS_FM_HOST_CHUNK", "1000")
+    monkeypatch.setenv("CS_FM_HOST_CHUNK", "1000")  # (read when the handle is created)
+    g = pkg.FMIndex.build_from_text(t)
     assert g.count_batch(pats).tolist() == want
     monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
+    g = pkg.FMIndex.build_from_text(t)
     assert g.count_batch(pats[:2000]).tolist() == want[:2000]
     assert g.count_batch(pats).tolist() == want
 

@@ -82,26 +82,18 @@ def pkg(request):
             os.environ[k] = v
 
 
-class _bar:
-    """CS_FM_COUNT_NOBAR=0 for the calls inside (read per call): the staged count
-    kernel's general search behind the block barrier (the default reads the node table
-    through the caches, no barrier, since round 4).  The auto_bar variant covers it on
-    occurrence lines; the learned variants re-count under it (the learned lines'
-    instantiation of the same hook)."""
-
-    def __enter__(self):
-        self.saved = os.environ.get("CS_FM_COUNT_NOBAR")
-        os.environ["CS_FM_COUNT_NOBAR"] = "0"
-
-    def __exit__(self, *a):
-        if self.saved is None:
-            os.environ.pop("CS_FM_COUNT_NOBAR", None)
-        else:
-            os.environ["CS_FM_COUNT_NOBAR"] = self.saved
+def _bar_count(g, buf, offs):
+    """The staged count kernel's general search behind the block barrier (CS_QT_BARRIER, a
+    per-call tuning selector; the default reads the node table through the caches, no
+    barrier, since round 4).  The auto_bar variant covers it on occurrence lines; the learned
+    variants re-count under it (the learned lines' instantiation)."""
+    return _count_bo(g, buf, offs, flags=load_pkg().QT_BARRIER)
 
 
 class _env:
-    """Per-call engine hooks (read by the library on each call) for the calls inside."""
+    """Build-time engine switches (CS_FM_*, read when a handle is created) for the builds
+    inside.  Since round 5 no query reads the environment: per-call kernel choices are the
+    CS_QT_* flags bits (pkg.QT_*)."""
 
     def __init__(self, **kw):
         self.kw = kw
@@ -326,9 +318,10 @@ def test_count_every_text_vs_oracle(built, name):
                 pats.append(bytes(p))
     want = [o.count(p) for p in pats]
     assert g.count_batch(pats).tolist() == want, name
+    # every general search listed for the list kernel (a wave lists them from 4 by default)
+    assert _count_ex(g, pats, flags=load_pkg().QT_GENERAL_LIST_ALL)[0].tolist() == want, name
     if _learned():
-        with _bar():
-            assert g.count_batch(pats).tolist() == want, name
+        assert _bar_count(g, *O.pack_patterns(pats)).tolist() == want, name
     for p in pats[::37]:  # single-pattern path (kernel arguments)
         assert g.count(p) == o.count(p), (name, p)
     # locate of the same patterns: ranges finished over the contexts hand windows of
@@ -471,8 +464,7 @@ def test_random_large_vs_oracle(pkg, gen, m):
     assert np.array_equal(got, want)
     assert (got[:20000] >= 1).all()
     if _learned():
-        with _bar():
-            assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
+        assert np.array_equal(_bar_count(g, buf, offs), want)
     lim = 1000
     woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=lim, nthreads=8)
     goffs, gpos = g.locate_batch(buf=buf, offs=offs, limit=lim)
@@ -484,7 +476,7 @@ def test_count_long_kernel_large(pkg):
     """The long-pattern kernel (k_count_long, CS_Q_LONG) at scale: a 2 M DNA text with rare
     symbols (N runs, so windows and contexts meet rare rows), 12 k Q_text patterns of 33-200
     characters plus one-symbol mutants and patterns holding an N — counts equal the
-    oracle's through the packed text (default), the byte text (CS_FM_LONG_KERNEL=2) and
+    oracle's through the packed text (default), the byte text (CS_QT_LONG_BYTE_TEXT) and
     round 2's kernel (0), and every pattern of a random length batch agrees."""
     rng = np.random.default_rng(21)
     t = O.gen_dna(7, 2_000_000)
@@ -503,14 +495,11 @@ def test_count_long_kernel_large(pkg):
     buf, offs = O.pack_patterns(pats)
     want = o.count_batch(buf=buf, offs=offs, nthreads=8)
     assert (want[::2] >= 1).all()
-    for lk in ("1", "2", "0"):
-        with _env(CS_FM_LONG_KERNEL=lk):
-            got, _, _ = _count_ex(g, pats, flags=32)
-        assert np.array_equal(got, want), lk
-    for v in ("0", "1", "2"):  # the pattern / window load forms (default 3: 16-B vectors)
-        with _env(CS_FM_LONG_V16=v):
-            got, _, _ = _count_ex(g, pats, flags=32)
-        assert np.array_equal(got, want), v
+    # k_count_long on the packed text (default), the byte text, round 2's kernel; 8-B
+    # pattern / window loads instead of the 16-B vectors
+    for f in (0, pkg.QT_LONG_BYTE_TEXT, pkg.QT_LONG_ROUND2, pkg.QT_LONG_LOADS8):
+        got, _, _ = _count_ex(g, pats, flags=32 | f)
+        assert np.array_equal(got, want), f
     for _ in range(2):  # the default path: long-pattern routing inside the call
         got, _, _ = _count_ex(g, pats)
         assert np.array_equal(got, want)
@@ -743,6 +732,17 @@ def _substrings_and_mutants(t, lengths, per, seed):
     return pats
 
 
+def _count_bo(g, buf, offs, flags=0):
+    """count of a packed batch (buf, offs) through cs_fm_count_batch_device_ex under flags."""
+    d_buf = torch.from_numpy(np.ascontiguousarray(buf).copy()).cuda()
+    d_offs = torch.from_numpy(np.asarray(offs).astype(np.int64)).cuda()
+    npat = len(offs) - 1
+    out = torch.zeros(max(npat, 1), dtype=torch.int64, device="cuda")
+    g.count_device_ex(d_buf.data_ptr(), d_offs.data_ptr(), npat, out.data_ptr(), flags=flags)
+    torch.cuda.synchronize()
+    return out[:npat].cpu().numpy().astype(np.uint64)
+
+
 def _count_ex(g, pats, width=8, flags=0, exc_cap=1 << 16):
     """count through cs_fm_count_batch_device_ex -> (counts as uint64, exception pairs)."""
     buf, offs = O.pack_patterns(pats)
@@ -815,13 +815,10 @@ def test_count_verify_long(built, pkg, name):
     for f in (0, 16, 32, 48):  # 32: CS_Q_LONG (k_count_long: one pattern per lane)
         got, _, _ = _count_ex(g, pats, flags=f)
         assert got.tolist() == want, (name, f)
-    for lk in ("0", "2"):  # CS_Q_LONG through round 2's kernel, and on the byte text
-        with _env(CS_FM_LONG_KERNEL=lk):
-            got, _, _ = _count_ex(g, pats, flags=32)
-        assert got.tolist() == want, (name, lk)
-    with _env(CS_FM_LONG_V16="0"):  # 8-B pattern and window loads
-        got, _, _ = _count_ex(g, pats, flags=32)
-    assert got.tolist() == want, (name, "v16=0")
+    # CS_Q_LONG through round 2's kernel, on the byte text, with 8-B pattern and window loads
+    for f in (pkg.QT_LONG_ROUND2, pkg.QT_LONG_BYTE_TEXT, pkg.QT_LONG_LOADS8):
+        got, _, _ = _count_ex(g, pats, flags=32 | f)
+        assert got.tolist() == want, (name, f)
     # long-pattern routing of the default path (inside the call since round 4): the staged
     # kernel counts the short patterns and lists the rest for k_count_long; short-only and
     # mixed batches alternate
@@ -831,19 +828,13 @@ def test_count_verify_long(built, pkg, name):
         assert got.tolist() == want, name
         got, _, _ = _count_ex(g, short)
         assert got.tolist() == [w for p, w in zip(pats, want) if len(p) <= 32], name
-    with _env(CS_FM_LONG_ROUTE="0"):
-        got, _, _ = _count_ex(g, pats)
-    assert got.tolist() == want, name
-    saved = os.environ.pop("CS_FM_LONG_ROUTE", None)  # by size: a small batch is not routed
-    try:
-        got, _, _ = _count_ex(g, pats)
-        # a host batch knows its lengths: routed when it holds long patterns (kQRoute)
-        got_h = g.count_batch(pats)
-    finally:
-        if saved is not None:
-            os.environ["CS_FM_LONG_ROUTE"] = saved
-    assert got.tolist() == want, (name, "by size")
-    assert got_h.tolist() == want, (name, "host batch, by lengths")
+    # round 5: every batch routes (no size threshold); unrouted (CS_QT_NO_ROUTE: the staged
+    # kernel's general search takes the long patterns), routed with the general searches kept
+    # in the lane (CS_QT_GENERAL_INLANE), and the host batch
+    for f in (pkg.QT_NO_ROUTE, pkg.QT_GENERAL_INLANE, pkg.QT_GENERAL_LIST_ALL):
+        got, _, _ = _count_ex(g, pats, flags=f)
+        assert got.tolist() == want, (name, f)
+    assert g.count_batch(pats).tolist() == want, (name, "host batch")
     # CS_Q_LONG at the narrow widths: uint32, and uint8 with the exception pairs
     got4, _, _ = _count_ex(g, pats, width=4, flags=32)
     assert got4.tolist() == want, name
@@ -953,7 +944,7 @@ def test_locate_verify_long(built, pkg, name):
             assert pos[offs[q]:offs[q + 1]].tolist() == want[q], (name, lim, p)
         # the one call: CS_Q_LONG (k_locate_long for every pattern, then k_locate_list), the
         # default path twice (the staged kernel lists the long patterns for k_locate_long in
-        # the same call), 8-B loads (CS_FM_LONG_V16=0) — on the indexes that take
+        # the same call), 8-B loads (CS_QT_LONG_LOADS8) — on the indexes that take
         # the long-pattern kernels (the 2-bit text; the others' one call is checked above)
         if not g.info().packed_text_bytes:
             if lim == 100000:  # CS_Q_LONG where the long-pattern kernels do not apply: the usual call
@@ -961,8 +952,7 @@ def test_locate_verify_long(built, pkg, name):
             continue
         for f in (32, 0, 0):
             assert _locate_one(g, pats, lim, f) == want, (name, lim, f)
-        with _env(CS_FM_LONG_V16="0"):
-            assert _locate_one(g, pats, lim, 32) == want, (name, lim, "v16=0")
+        assert _locate_one(g, pats, lim, 32 | pkg.QT_LONG_LOADS8) == want, (name, lim, "loads8")
         short = [i for i, p in enumerate(pats) if len(p) < 32]  # nothing to list
         assert _locate_one(g, [pats[i] for i in short], lim) == [want[i] for i in short], (name, lim)
         lp = [i for i, p in enumerate(pats) if len(p) > 31]  # host batch: CS_Q_LONG unasked
@@ -1094,11 +1084,10 @@ def test_locate_records(pkg):
             want = [o.locate(p, limit=lim) for p in pats]
             assert _locate_one(g, pats, lim) == want, (rec, lim)
             assert _locate_one(g, pats, lim, pkg.Q_NO_LOC_RECORDS) == want, (rec, lim)
-            # the misses deferred to k_locate_list (tuning hook), with and without long routing
-            with _env(CS_FM_LOC_DEFER="1"):
-                assert _locate_one(g, pats, lim) == want, (rec, lim, "defer")
-                with _env(CS_FM_LONG_ROUTE="0"):
-                    assert _locate_one(g, pats, lim) == want, (rec, lim, "defer, unrouted")
+            # the misses deferred to the list kernel (CS_QT_LOC_DEFER), with and without routing
+            assert _locate_one(g, pats, lim, pkg.QT_LOC_DEFER) == want, (rec, lim, "defer")
+            assert _locate_one(g, pats, lim, pkg.QT_LOC_DEFER | pkg.QT_NO_ROUTE) == want, \
+                (rec, lim, "defer, unrouted")
         del g
     if not built_any:
         pytest.skip("this variant builds no locate records")
@@ -1176,8 +1165,11 @@ def test_repetitive_text_vs_oracle(pkg):
     assert np.median(want[:3000]) > 100
     assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
     if _learned():  # most searches here take the general path the hook changes
-        with _bar():
-            assert np.array_equal(g.count_batch(buf=buf, offs=offs), want)
+        assert np.array_equal(_bar_count(g, buf, offs), want)
+    # the routed default lists the general searches for the list kernel; in the lane
+    # (CS_QT_GENERAL_INLANE) and unrouted (CS_QT_NO_ROUTE) the same counts
+    for f in (pkg.QT_GENERAL_INLANE, pkg.QT_GENERAL_LIST_ALL, pkg.QT_NO_ROUTE):
+        assert np.array_equal(_count_bo(g, buf, offs, flags=f), want), f
     for lim in (50, 5000):
         sub = pats[::7]
         b2, o2 = O.pack_patterns(sub)

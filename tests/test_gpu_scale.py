@@ -49,6 +49,19 @@ def _build(pkg, kind, L):
     return idx, text, host, N
 
 
+def _trim_pool(dev=0):
+    """Return the device's stream-ordered pool's cached memory (the engine keeps it between
+    calls: keep_pool) and torch's cache, so hipMemGetInfo sees what the handles hold."""
+    import ctypes as C
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    hip = C.CDLL("libamdhip64.so")
+    pool = C.c_void_p()
+    assert hip.hipDeviceGetDefaultMemPool(C.byref(pool), dev) == 0
+    assert hip.hipMemPoolTrimTo(pool, C.c_size_t(0)) == 0
+    torch.cuda.synchronize()
+
+
 def _qtext(pkg, text, N, m, npat):
     dev = text.device
     pats = torch.empty(npat * m, dtype=torch.uint8, device=dev)
@@ -143,9 +156,20 @@ def test_c4_dna_4gb(variant, monkeypatch):
     elif variant == "learned":
         monkeypatch.setenv("CS_FM_ENGINE", "learned")
     pkg = load_pkg()
+    _trim_pool()
+    free0 = torch.cuda.mem_get_info(0)[0]  # (the text is allocated inside _build, 4 GB + 16 B)
     idx, text, host, N = _build(pkg, "dna", 3_999_999_999)
     assert N == 4_000_000_000
     info = idx.info()
+    # the footprint the handle reports is the HBM it holds: every
+    # allocation of the index, the derived locate records and 2-bit text included — device
+    # free memory before the build minus after (pool trimmed, the text's 4 GB taken out)
+    _trim_pool()
+    held = free0 - torch.cuda.mem_get_info(0)[0] - text.numel()
+    assert abs(held - info.device_bytes) <= 0.01 * info.device_bytes, (held, info.device_bytes)
+    if variant == "auto":  # C4's default footprint with the locate records: ~30 B per base
+        assert info.locate_record_bytes == 64 * 4 ** info.prefix_k
+        assert info.device_bytes > 110e9, info.device_bytes
     assert (info.full_sa_bytes > 0) == (variant != "plain_walk")
     # C4: n / 4^15 = 3.7 rows per k-mer -> compact 16-B records
     assert info.record_bytes == (0 if variant == "plain_walk" else 16)
