@@ -342,6 +342,11 @@ void read_tuning(cs_fm_index* h) {
     const long v = std::atol(e);
     if (v >= 1 && v <= 128) h->gen_list_min = (uint32_t)v;
   }
+  h->list_grid = 0;
+  if (const char* e = std::getenv("CS_FM_LIST_GRID")) {
+    const long v = std::atol(e);
+    if (v >= 1 && v <= (1 << 20)) h->list_grid = (uint32_t)v;
+  }
   h->host_chunk = 0;
   if (const char* e = std::getenv("CS_FM_HOST_CHUNK")) {
     const long long v = std::atoll(e);
@@ -712,10 +717,12 @@ cs_status cs_fm_locate_record_hits_device(const cs_fm_index* h, const uint8_t* d
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
-  if (npat && (!d_offs || !d_pats || !d_hit)) {
+  if (npat && (!d_offs || !d_hit)) {
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
+  // (d_pats may be NULL when every pattern is empty, as the other device entry points: ADVICE r04)
+  if ((s = null_pats_ok(d_pats, d_offs, npat, (hipStream_t)stream)) != CS_OK) return s;
   return launch_locrec_hits(h, d_pats, d_offs, npat, d_hit, (hipStream_t)stream);
 }
 

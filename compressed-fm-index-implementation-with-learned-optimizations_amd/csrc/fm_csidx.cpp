@@ -149,9 +149,20 @@ bool read_file(const char* path, std::vector<uint8_t>& f) {
     std::fclose(fp);
     return false;
   }
-  f.resize((size_t)sb.st_size);
-  const size_t k = f.empty() ? 0 : std::fread(f.data(), 1, f.size(), fp);
-  const bool ok = k == f.size() && !std::ferror(fp);
+  // a regular file: its size, then one read; anything else (a FIFO, /dev/stdin, a procfs
+  // file, whose st_size says nothing) in chunks until the end
+  bool ok;
+  if (S_ISREG(sb.st_mode)) {
+    f.resize((size_t)sb.st_size);
+    const size_t k = f.empty() ? 0 : std::fread(f.data(), 1, f.size(), fp);
+    ok = k == f.size() && !std::ferror(fp);
+  } else {
+    f.clear();
+    uint8_t buf[1 << 16];
+    size_t k;
+    while ((k = std::fread(buf, 1, sizeof buf, fp)) > 0) f.insert(f.end(), buf, buf + k);
+    ok = !std::ferror(fp);
+  }
   std::fclose(fp);
   return ok;
 }

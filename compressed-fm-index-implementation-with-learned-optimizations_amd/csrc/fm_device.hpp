@@ -255,7 +255,12 @@ struct LongList {
   uint32_t* cnt2 = nullptr;
   uint32_t* hdr = nullptr;  // listed[kListedLanes] (kListedStride apart), then retire
   uint32_t gen_list = 0;    // the routed count: general-search patterns to list2
+  // the routed count: per list2 entry the range the staged kernel's table read left (sp in
+  // bits 0-31, its width in 32-63; narrow indexes) or kNoRange (the search starts over)
+  uint64_t* rng2 = nullptr;
+  uint32_t grid = 0;  // (host side: the list kernel's grid, cs_fm_index::list_grid; 0 = default)
 };
+constexpr uint64_t kNoRange = ~0ull;
 // the staged kernel's wave adds its listed patterns (lane 0; n uniform over the wave)
 __device__ __forceinline__ void list_listed_add(const LongList& ll, uint32_t n) {
   if (n && (threadIdx.x & 63) == 0)

@@ -77,6 +77,8 @@ struct cs_fm_index {
   // the routed count: a wave lists its general searches for the list kernel when it holds
   // at least this many (CS_FM_GENERAL_LIST_MIN; fm_device.hpp LongList::gen_list)
   uint32_t gen_list_min = 2;
+  // the list kernels' grid (CS_FM_LIST_GRID; 0 = fm_query.hip kLongListGrid)
+  uint32_t list_grid = 0;
 
   // Small host batches (single-pattern queries, p50 latency) stage through a
   // per-handle pinned + HBM arena instead of per-call hipMalloc/hipFree and

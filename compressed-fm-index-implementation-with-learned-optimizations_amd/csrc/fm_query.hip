@@ -1162,17 +1162,19 @@ __device__ __forceinline__ void general_rest(const DevIndex& ix, const NodeTable
 
 // Batch locate in one call (cs_fm_locate_device) over an index that keeps the full suffix
 // array: three launches and one host synchronisation —
-//   (1) k_count_ctx with kOne: the staged search; per pattern min(count, limit) (u32: the
-//       index is narrow) and its record; per block ("tile") the block's total;
+//   (1) k_count_ctx with kOne: the staged search; per pattern its record and, unless the
+//       record is the pattern's only position (kLocStash below: count 1, 99.6 % of C4
+//       Q_text), min(count, limit) — 8 B written per pattern instead of 12;
+//       Per tile (a search block's 2 x 256 patterns) the total, added by each wave.
 //   (2) k_scan_tiles: the exclusive scan of the tile totals (one block; C4: 24 k tiles);
 //   (3) k_locate_emit: per tile, the block's scan of its counts plus the tile's prefix
 //       give the output offsets, then the positions straight from the records through SA.
-// Against the two phases this drops the scan of a 100-MB count array, 8 of the 16 B
-// written per pattern and the host round trip between the phases.  A single launch with
-// a decoupled look-back across tiles was measured first: every block then waits for the
-// slowest search among its predecessors (3.2 ms against 1.1 ms for the two phases, C4).
+// (A look-back inside the search kernel, measured in round 3, made every block wait for the
+// slowest search among its predecessors: 3.2 ms against 1.1 ms; the other forms round 5
+// tried are listed at k_locate_emit.)  Against the two phases this drops the scan of a
+// 100-MB count array and the host round trip between the phases.
 // Indexes without the full suffix array but with walk lines and text-position marks (C5;
-// C4 under CS_FM_FULL_SA=0) take the same three launches (round 3): a position is the
+// C4 under CS_FM_FULL_SA=0) take the same launches (round 3): a position is the
 // short walk from its row (walk_position: at most pstride - 1 LF steps, one 32-B walk line
 // each, then the mark's sample) instead of SA[row], in (1) for a pattern's only position
 // and in (3) / k_locate_emit_wide for the rest (kPos: 0 the full SA, 1 WalkLine, 2
@@ -1187,10 +1189,12 @@ __device__ __forceinline__ void st_out(T* p, T v) {
 }
 
 struct OnePass {
-  uint32_t* cnt = nullptr;               // (1) -> (3): min(count, limit) per pattern (narrow)
+  uint32_t* cnt = nullptr;               // (1) -> (3): min(count, limit) per pattern (narrow),
+                                         // unless its record is a stashed position (count 1)
   uint64_t* cnt64 = nullptr;             // the same, wide indexes
   uint64_t* rec = nullptr;               // (1) -> (3): the pattern's record
-  uint64_t* tiles = nullptr;             // per tile: its total, then its exclusive prefix
+  uint64_t* tiles = nullptr;             // per tile (a search block's patterns): its total, then
+                                         // its exclusive prefix (k_scan_tiles)
   const uint32_t* sa = nullptr;          // full suffix array
   uint64_t* out_offs = nullptr;          // npat + 1 exclusive offsets
   uint64_t* out_pos = nullptr;           // positions, `cap` of them
@@ -1250,18 +1254,24 @@ __device__ __forceinline__ void block_scan(const uint64_t* kc, uint64_t* mine, u
   }
 }
 
-// (1)'s tail: the lane's results and the tile's total
+__device__ __forceinline__ void tile_total_add(const OnePass& op, uint64_t tile, uint64_t v) {
+  atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + tile), v);
+}
+
+// (1)'s tail: the lane's results.
 // A pattern reporting exactly one position gets it here, from the record already in the
 // lane (its first row: SA[row] - k for a context window), so its SA read overlaps the
 // other blocks' record reads instead of waiting for k_locate_emit; the record then holds
-// kLocStash | position.  (C4 Q_text: 99.6 % of the patterns.)
+// kLocStash | position and stands for the count 1 (no count is stored: 8 B per pattern).
+// (C4 Q_text: 99.6 % of the patterns.)
 constexpr uint64_t kLocStash = 1ull << 62;  // with bit 63 clear: not a window, not a row
+__device__ __forceinline__ bool loc_stashed(uint64_t r) { return (r >> 62) == 1; }
+// skip: bit j set = the lane's j-th pattern is k_locate_long's (routing): its count and record
+// are left for that kernel to write
 // kWaveTile (the barrier-free search, kPos 0): each wave adds its patterns' total to the tile
-// (zeroed before the launch) instead of a block scan storing it, so no wave waits for the
+// (zeroed at the block's start) instead of a block scan storing it, so no wave waits for the
 // block's others
 template <int U, int kPos = 0, bool kWaveTile = false>
-// skip: bit j set = the lane's j-th pattern is k_locate_long's (routing): its count and record
-// are left for that kernel to write (it adds its count to the tile)
 __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const NodeTable& T, uint64_t npat,
                                                    uint64_t tile, uint64_t q0, const uint64_t* kc,
                                                    const uint64_t* kr, const OnePass& op, uint32_t skip = 0) {
@@ -1273,7 +1283,7 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
     for (int j = 0; j < U; ++j) sum += kc[j];
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) sum += __shfl_xor(sum, dd, 64);
-    if ((threadIdx.x & 63) == 0 && sum) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + tile), sum);
+    if ((threadIdx.x & 63) == 0 && sum) tile_total_add(op, tile, sum);
   } else {
     uint64_t mine[U], agg;
     block_scan<U>(kc, mine, agg);
@@ -1287,7 +1297,7 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
     rs[j] = s;
     row[j] = s;
     adj[j] = 0;
-    one[j] = q < npat && kc[j] == 1 && (s >> 62) != 1;  // (not stashed by a locate record)
+    one[j] = q < npat && kc[j] == 1 && !loc_stashed(s);  // (not stashed by a locate record)
     uint32_t rel;
     if (one[j] && (s & kLocCtx)) loc_window(s, row[j], adj[j], rel);  // a window's only match: its first row
   }
@@ -1308,8 +1318,11 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     if (q >= npat || ((skip >> j) & 1u)) continue;
-    if (op.cnt64) op.cnt64[q] = kc[j];
-    else op.cnt[q] = (uint32_t)kc[j];
+    if (!(kc[j] == 1 && loc_stashed(rs[j]))) {  // the count, and no stash standing for 1
+      if (op.cnt64) op.cnt64[q] = kc[j];
+      else op.cnt[q] = (uint32_t)kc[j];
+      if (loc_stashed(rs[j])) rs[j] = 0;  // (a limit of 0)
+    }
     op.rec[q] = rs[j];
   }
 }
@@ -1375,7 +1388,13 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tile
   if (t == 0) *total_out = s_carry;
 }
 
-// (3): offsets and positions of tile blockIdx.x
+// (3): offsets and positions of tile blockIdx.x (round 5: a pattern whose record is a stashed
+// position has no count stored: 8 B read per pattern instead of 12.  Tried in round 5 to drop
+// the scan kernel: a decoupled look-back over the tiles — its frontier moves 64 tiles per L2
+// round trip, 0.63 against 0.53 ms per C4 call — 1024 blocks taking a share of the tiles each
+// with a running base — 4 waves per SIMD and a serial tile loop, the emit 125 against 67 us
+// — and share totals added by the search kernel's waves — same-address atomics of
+// neighbouring blocks, the search 426 -> 615 us.)
 template <int U, int kPos = 0>
 __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat, OnePass op) {
   __shared__ NodeTable T;  // kPos: the walks' C[] and codes
@@ -1388,10 +1407,11 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
     // (read once: non-temporal loads, 0.560 -> 0.554 ms per call over three A/B rounds,
-    // profiles/r04/ab_lib_r04af.jsonl)
-    kc[j] = q < npat ? (op.cnt64 ? __builtin_nontemporal_load(op.cnt64 + q) : __builtin_nontemporal_load(op.cnt + q)) : 0;
+    // profiles/r04/ab_lib_r04af.jsonl); the count only where the record is no stash
     kr[j] = q < npat ? __builtin_nontemporal_load(op.rec + q) : 0;
-    walk |= kc[j] && (kr[j] >> 62) != 1;
+    kc[j] = q >= npat ? 0 : loc_stashed(kr[j]) ? 1
+          : (op.cnt64 ? __builtin_nontemporal_load(op.cnt64 + q) : __builtin_nontemporal_load(op.cnt + q));
+    walk |= kc[j] && !loc_stashed(kr[j]);
   }
   if constexpr (kPos != 0) {
     if (__syncthreads_or(walk)) {
@@ -1409,7 +1429,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
     st_out(op.out_offs + q, a);
     if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
     const uint64_t s = kr[j];
-    if ((s >> 62) == 1) {  // kLocStash: the one position, read by the search kernel
+    if (loc_stashed(s)) {  // kLocStash: the one position, read by the search kernel
       st_out(op.out_pos + a, s & (kLocStash - 1));
     } else if (s & kLocCtx) {  // a window k characters before the end (k_locate_sa)
       uint64_t r0, adj;
@@ -1469,6 +1489,28 @@ __device__ __forceinline__ uint32_t wave_list(uint16_t* list, uint32_t* cnt, uin
   return n;
 }
 
+// wave_list, and each listed pattern's payload pay[j] at the same place of `rng`
+template <int U = 2>
+__device__ __forceinline__ uint32_t wave_list_pay(uint16_t* list, uint32_t* cnt, uint64_t* rng, uint64_t slot,
+                                                  uint32_t m, const uint64_t* pay) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t n = 0;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const bool b = (m >> j) & 1u;
+    const uint64_t bal = __ballot(b);
+    if (b) {
+      const uint64_t at = slot * kLongSlot + n + __popcll(bal & below);
+      list[at] = (uint16_t)(threadIdx.x + j * kBlk);
+      rng[at] = pay[j];
+    }
+    n += __popcll(bal);
+  }
+  if (lane == 0) cnt[slot] = n;
+  return n;
+}
+
 // A 16-B context record: a random read nothing re-reads, through a non-temporal load so it
 // does not displace the pattern stream's lines in the caches (C4 headline 0.394 -> 0.382 ms,
 // four rounds of an A/B in fresh processes on one box: profiles/r03/ab_nt_record_load.jsonl)
@@ -1514,7 +1556,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
-  if (kOne && kNoBar && threadIdx.x == 0) {
+  if (kOne && threadIdx.x == 0) {
     // the block's tile, which its waves add to after the barrier, and the call's wide-range
     // counter: no memset launch.  The stores are acknowledged by the L2 (where the waves'
     // atomics land) before this wave reaches the barrier.
@@ -1866,7 +1908,14 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       ng += (uint32_t)__popcll(__ballot(g));
     }
     if (ll.gen_list && ng >= ll.gen_list) {
-      nlisted += wave_list<U>(ll.list2, ll.cnt2, slot, gm);
+      // with the range the table read left (st 5: too wide for the contexts), so the list
+      // kernel steps on from it instead of reading the record again
+      uint64_t pay[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        pay[j] = st[j] == 5 && !ix.wide && ep[j] - sp[j] <= 0xFFFFFFFFull ? (sp[j] | ((ep[j] - sp[j]) << 32))
+                                                                          : kNoRange;
+      nlisted += wave_list_pay<U>(ll.list2, ll.cnt2, ll.rng2, slot, gm, pay);
 #pragma unroll
       for (int j = 0; j < U; ++j)
         if ((gm >> j) & 1u) st[j] = 6;  // listed
@@ -2261,6 +2310,7 @@ __device__ __forceinline__ void long_list_append(bool general, uint64_t q, const
   const uint64_t sl = long_slot(q);
   const uint32_t at = atomicAdd(ll.cnt2 + sl, 1u);
   ll.list2[sl * kLongSlot + at] = (uint16_t)(q % kLongRegion);
+  if (ll.rng2) ll.rng2[sl * kLongSlot + at] = kNoRange;  // (the search starts over)
 }
 
 // The patterns of one list launch (kList): the entries of the slots of block b — slots b,
@@ -2288,6 +2338,7 @@ __device__ __forceinline__ uint32_t slot_count(const uint32_t* cnt, uint64_t npa
 
 template <class F>
 __device__ __forceinline__ uint32_t list_for_each(const uint16_t* __restrict__ list, uint32_t c, F&& f) {
+  static_assert(kBlk == 256, "the slot lookup below searches 256 slots in 8 steps");  // 
   __shared__ uint32_t s_off[kBlk + 1];
   __shared__ uint32_t s_w[kBlk / 64];
   // exclusive scan of the counts over the block
@@ -2324,6 +2375,239 @@ __device__ __forceinline__ uint32_t list_for_each(const uint16_t* __restrict__ l
     f(q, e0 + threadIdx.x < tot);
   }
   return tot;
+}
+
+// list_for_each with two entries per thread and round (e and e + kBlk of 2 kBlk): f(q, act)
+// with q[2], act[2], the whole block in lockstep
+template <class F>
+__device__ __forceinline__ uint32_t list_for_each2(const uint16_t* __restrict__ list, uint32_t c, F&& f) {
+  static_assert(kBlk == 256, "the slot lookup below searches 256 slots in 8 steps");
+  __shared__ uint32_t s_off2[kBlk + 1];
+  __shared__ uint32_t s_w2[kBlk / 64];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_w2[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < (int)(kBlk / 64); ++w2) {
+    if (w2 < (int)wv) pre += s_w2[w2];
+    tot += s_w2[w2];
+  }
+  s_off2[threadIdx.x] = pre + x - c;
+  if (threadIdx.x == 0) s_off2[kBlk] = tot;
+  __syncthreads();
+  for (uint32_t e0 = 0; e0 < tot; e0 += 2 * kBlk) {
+    uint64_t q[2];
+    bool act[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t ee = e0 + threadIdx.x + h * kBlk;
+      act[h] = ee < tot;
+      const uint32_t e = act[h] ? ee : 0u;
+      uint32_t lo = 0, hi = kBlk;  // s_off2[lo] <= e < s_off2[hi]
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off2[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const uint64_t s2 = blockIdx.x + (uint64_t)lo * gridDim.x;
+      // (the entry's index in the list: its slot's base + its place)
+      q[h] = s2 * kLongSlot + (e - s_off2[lo]);
+    }
+    f(q, act);
+  }
+  return tot;
+}
+
+// The rest of up to U listed general searches of the routed count from the ranges the
+// staged kernel's table reads left (LongList::rng2), k[j] <= kCtxQ characters still to
+// step: count_rest's steps without its verification (k <= kCtxQ never verifies), the U
+// patterns in lockstep — every round issues all their line (or context-sector) loads before
+// any is used, so a lane keeps U dependent chains in flight — and the rows' left contexts
+// once the range fits two sectors (ctx_match; an escaped context or a rare symbol steps on).
+// act[j] false on entry: no pattern j.  Reference: fm_index.cpp:90-98.
+template <int U>
+__device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable& T,
+                                            const uint8_t* const* P, uint32_t* k, uint64_t* sp,
+                                            uint64_t* ep, bool* act, uint64_t* res) {
+  bool ctx[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    ctx[j] = ix.lctx != nullptr;
+    res[j] = 0;
+  }
+  // (every round steps a pattern, finishes it, or turns its contexts off once: at most
+  // k + 2 <= kCtxQ + 2 rounds)
+  for (;;) {
+    uint4 b[U][4];  // the two lines of a step, or the two context sectors
+    uint32_t mode[U];  // 0 done, 1 step, 2 contexts
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      mode[j] = 0;
+      if (!act[j]) continue;
+      if (sp[j] >= ep[j] || k[j] == 0) {
+        res[j] = sp[j] < ep[j] ? ep[j] - sp[j] : 0;
+        act[j] = false;
+        continue;
+      }
+      any = true;
+      const uint64_t base = sp[j] & ~15ull;
+      if (ctx[j] && k[j] <= ix.lctx_q && ep[j] - base <= 32) {
+        mode[j] = 2;
+        const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) + base);
+        b[j][0] = p[0];
+        b[j][1] = p[1];
+        if (ep[j] - base > 16) {
+          b[j][2] = p[2];
+          b[j][3] = p[3];
+        } else {
+          b[j][2] = b[j][3] = make_uint4(0, 0, 0, 0);
+        }
+      } else {
+        mode[j] = 1;
+        const uint32_t c = P[j][k[j] - 1];
+        if (T.C[c] == T.C[c + 1]) {  // absent symbol: the range empties
+          res[j] = 0;
+          act[j] = false;
+          mode[j] = 0;
+          continue;
+        }
+        if (T.occ_code[c] != kNoCode) {
+          const uint64_t qa = sp[j] >> 6, qe = ep[j] >> 6;
+          OccLine::Raw va;
+          OccLine::load(ix.lines, qa, va);
+          b[j][0] = va[0];
+          b[j][1] = va[1];
+          if (qe != qa) {
+            OccLine::Raw ve;
+            OccLine::load(ix.lines, qe, ve);
+            b[j][2] = ve[0];
+            b[j][3] = ve[1];
+          } else {
+            b[j][2] = va[0];
+            b[j][3] = va[1];
+          }
+        }
+      }
+    }
+    if (!any) break;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (mode[j] == 2) {
+        uint32_t want = 0;
+        bool ok = true, absent = false;
+        for (uint32_t t = 0; t < k[j]; ++t) {  // chain symbol t = P[k-1-t]
+          const uint32_t c = P[j][k[j] - 1 - t];
+          absent |= T.C[c] == T.C[c + 1];
+          const uint32_t d = T.occ_code[c];
+          ok &= d != kNoCode;
+          want |= (d & 3u) << (2 * t);
+        }
+        if (absent) {
+          res[j] = 0;
+          act[j] = false;
+          continue;
+        }
+        const uint64_t base = sp[j] & ~15ull;
+        const uint32_t lo = (uint32_t)(sp[j] - base), hi = (uint32_t)(ep[j] - base);
+        const uint32_t mask = ((1u << (2 * k[j])) - 1u) | kCtxEsc;
+        const uint32_t* dw = reinterpret_cast<const uint32_t*>(b[j]);
+        uint32_t match = 0, esc = 0;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+          const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+          match |= (uint32_t)((e & mask) == want) << i;
+          esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+        }
+        const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+        if (!ok || (esc & in)) {
+          ctx[j] = false;  // a rare symbol: step on
+        } else {
+          res[j] = (uint64_t)__popc(match & in);
+          act[j] = false;
+        }
+      } else if (mode[j] == 1) {
+        const uint32_t c = P[j][k[j] - 1];
+        const uint32_t code = T.occ_code[c];
+        uint64_t rs, re;
+        if (code == kNoCode) {
+          rs = exc_rank(T, c, sp[j]);
+          re = exc_rank(T, c, ep[j]);
+        } else {
+          const OccLine::Raw va = {b[j][0], b[j][1]}, ve = {b[j][2], b[j][3]};
+          rs = OccE::occ_line(va, code, sp[j]);
+          re = OccE::occ_line(ve, code, ep[j]);
+          if (code == 0 && T.exc_n) {
+            rs -= exc_before(T, sp[j]);
+            re -= exc_before(T, ep[j]);
+          }
+        }
+        sp[j] = T.C[c] + rs;
+        ep[j] = T.C[c] + re;
+        --k[j];
+      }
+    }
+  }
+}
+
+// The routed count's list2 entries (k_count_long kList): two per thread and round; an entry
+// with a range from the staged kernel and at most kCtxQ characters left takes count_steps
+// (the two of a thread in lockstep), any other the general search from the start
+// (count_pattern: no range kept, a wide index, longer rests that verify against the text).
+template <int W>
+__device__ __forceinline__ void count_list_general2(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
+                                                    const uint64_t* __restrict__ offs, const CountOut& co,
+                                                    uint64_t fixed_m, const LongList& ll, uint32_t c) {
+  bool staged = false;
+  list_for_each2(ll.list2, c, [&](const uint64_t* ei, const bool* act) {
+    if (!staged) {  // the first round (uniform): the block has entries
+      load_table(T, ix.table);
+      __syncthreads();
+      staged = true;
+    }
+    uint64_t q[2], sp[2], ep[2], res[2];
+    uint32_t k[2];
+    const uint8_t* P[2];
+    bool lean[2], a2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      lean[h] = false;
+      a2[h] = false;
+      q[h] = 0;
+      k[h] = 0;
+      sp[h] = ep[h] = 0;
+      P[h] = pats;
+      if (!act[h]) continue;
+      const uint64_t e = ei[h];
+      q[h] = e / kLongSlot / kSlotsPerRegion * kLongRegion + ll.list2[e];
+      const uint64_t o0 = offs ? offs[q[h]] : q[h] * fixed_m, m = offs ? offs[q[h] + 1] - o0 : fixed_m;
+      P[h] = pats + o0;
+      const uint64_t r = ll.rng2[e];
+      if (r != kNoRange && m >= ix.ptab_k && m - ix.ptab_k <= kCtxQ) {
+        lean[h] = a2[h] = true;
+        k[h] = (uint32_t)(m - ix.ptab_k);
+        sp[h] = r & 0xFFFFFFFFull;
+        ep[h] = sp[h] + (r >> 32);
+      } else {
+        // (no range: the search from the start, as the staged kernel's general search)
+        store_count<W>(co, q[h], m == 0 ? ix.n : count_pattern<OccE>(ix, T, P[h], m));
+      }
+    }
+    if (lean[0] || lean[1]) {
+      count_steps<2>(ix, T, P, k, sp, ep, a2, res);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (lean[h]) store_count<W>(co, q[h], res[h]);
+    }
+  });
 }
 
 // the general search of the list2 entries of a block's slots (defined below)
@@ -2422,7 +2706,10 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
     // the grid
     __shared__ NodeTable T;
     __syncthreads();
-    count_list_general<W, kBytes>(ix, T, pats, offs, co, fixed_m, ll, slot_count<true>(ll.cnt2, npat));
+    if constexpr (kBytes)
+      count_list_general<W, kBytes>(ix, T, pats, offs, co, fixed_m, ll, slot_count<true>(ll.cnt2, npat));
+    else  // (the staged kernel's general searches with their ranges, two per thread)
+      count_list_general2<W>(ix, T, pats, offs, co, fixed_m, ll, slot_count<true>(ll.cnt2, npat));
     list_retire(ll);
   } else {
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
@@ -2434,21 +2721,11 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
 constexpr uint64_t kLocTile = 2 * kBlk;
 static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns");
 
-// The long-pattern search for the one-call locate (launch_locate_onepass over full-SA
-// indexes: CS_Q_LONG, host batches of long patterns, and the long patterns the staged kernel
-// lists): k_count_long's stages, then per pattern min(count, limit) and its record for
-// k_locate_emit — the only position itself (kLocStash: the SA entry the verification read,
-// minus k) or a verified window (first row, match bits, k), whose positions the emit kernel
-// reads through SA — and the counts added to their tile's total (zeroed before, or holding the
-// staged kernel's totals of the short patterns): a list region is one tile, so the block adds
-// its sum once per region; without a list a wave's 64 patterns lie in one tile.  The patterns
-// it cannot finish (as k_count_long's, and windows whose matches lie too far apart for the
-// record) go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search), :125 (limit).
 // Adds each lane's kc (0: nothing) to op.tiles[tile]: one atomic per distinct tile of the
 // wave (a list launch's wave holds one or two slots' patterns, so one or two tiles; a
 // pattern-per-lane atomic puts 512 same-address atomics on every tile: C4 150-mer locate
 // 2.1 -> 3.4 ms).  Every lane of the wave, in uniform control flow.
-__device__ __forceinline__ void wave_tile_add(uint64_t* tiles, uint64_t tile, uint64_t kc) {
+__device__ __forceinline__ void wave_tile_add(const OnePass& op, uint64_t tile, uint64_t kc) {
   const uint32_t lane = threadIdx.x & 63;
   uint64_t pend = __ballot(kc != 0);
   while (pend) {
@@ -2458,15 +2735,24 @@ __device__ __forceinline__ void wave_tile_add(uint64_t* tiles, uint64_t tile, ui
     uint64_t s = in ? kc : 0;
 #pragma unroll
     for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
-    if (lane == l) atomicAdd(reinterpret_cast<unsigned long long*>(tiles + t), s);
+    if (lane == l) tile_total_add(op, t, s);
     pend &= ~__ballot(in);
   }
 }
 
+// The long-pattern search for the one-call locate (launch_locate_onepass over full-SA
+// indexes: CS_Q_LONG, host batches of long patterns, and the long patterns the staged kernel
+// lists): k_count_long's stages, then per pattern min(count, limit) and its record for
+// k_locate_emit — the only position itself (kLocStash: the SA entry the verification read,
+// minus k) or a verified window (first row, match bits, k), whose positions the emit kernel
+// reads through SA — and the counts added to their tile's total (zeroed before, or holding the
+// staged kernel's totals of the short patterns).
+// The patterns it cannot finish (as k_count_long's, and windows whose matches lie too far
+// apart for the record) go to k_locate_list.  Reference: fm_index.cpp:107-124 (the search),
+// :125 (limit).
 // k_locate_long's search of pattern q (mine: q is one to search); every lane of the wave
-// calls it.  kWaveTile: the wave's 64 patterns lie in one tile (one pattern per lane over the
-// batch), so the wave sums its counts into it; else (lists) wave_tile_add.
-template <int kV16, bool kWaveTile>
+// calls it.
+template <int kV16>
 __device__ __forceinline__ void locate_long_one(const DevIndex& ix, const uint8_t* __restrict__ pats,
                                                 const uint64_t* __restrict__ offs, uint64_t limit,
                                                 const OnePass& op, const LongList& ll,
@@ -2508,14 +2794,7 @@ __device__ __forceinline__ void locate_long_one(const DevIndex& ix, const uint8_
     op.cnt[q] = (uint32_t)kc;
     op.rec[q] = rec;
   }
-  if constexpr (kWaveTile) {
-    uint64_t s = kc;
-#pragma unroll
-    for (int dd = 32; dd >= 1; dd >>= 1) s += __shfl_xor(s, dd, 64);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(reinterpret_cast<unsigned long long*>(op.tiles + q / kLocTile), s);
-  } else {
-    wave_tile_add(op.tiles, q / kLocTile, kc);
-  }
+  wave_tile_add(op, q / kLocTile, kc);
 }
 
 template <int kV16, bool kList>
@@ -2543,7 +2822,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
   __syncthreads();
   if constexpr (kList) {
     list_for_each(ll.list, c1, [&](uint64_t q, bool act) {
-      locate_long_one<kV16, false>(ix, pats, offs, limit, op, ll, cmap, rare, q, act);
+      locate_long_one<kV16>(ix, pats, offs, limit, op, ll, cmap, rare, q, act);
     });
     // then the general search of what it listed and the staged search deferred (the same
     // block owns the same slots of list2: no k_locate_list launch)
@@ -2551,9 +2830,9 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
     __syncthreads();
     locate_list_general(ix, T, pats, offs, limit, op, ll, slot_count<true>(ll.cnt2, npat));
     list_retire(ll);
-  } else {  // no lane returns early: the wave sums its counts at the end
+  } else {
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-    locate_long_one<kV16, true>(ix, pats, offs, limit, op, ll, cmap, rare, q, q < npat);
+    locate_long_one<kV16>(ix, pats, offs, limit, op, ll, cmap, rare, q, q < npat);
   }
 }
 
@@ -2738,7 +3017,7 @@ __device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTabl
       op.cnt[q] = (uint32_t)kc;
       op.rec[q] = rr;
     }
-    wave_tile_add(op.tiles, q / kLocTile, kc);
+    wave_tile_add(op, q / kLocTile, kc);
   });
 }
 
@@ -4352,7 +4631,8 @@ struct LongBufs {
   LongList ll;
   static uint64_t bytes(uint64_t npat, bool direct) {
     const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
-    return kListHdrBytes + (direct ? 1 : 2) * slots * (kLongSlot * 2 + 4);
+    // (+ the ranges of the general-search entries, 8 B each, after the lists and counts)
+    return kListHdrBytes + (direct ? 1 : 2) * slots * (kLongSlot * 2 + 4) + (direct ? 0 : slots * kLongSlot * 8);
   }
   // into `at` (bytes(npat, direct) of it: the caller's workspace, whose header the calls keep
   // zeroed, or the call's own allocation when `fresh`), or an allocation of its own
@@ -4370,6 +4650,7 @@ struct LongBufs {
     if (!direct) {
       ll.list = ll.list2 + entries;
       ll.cnt = ll.cnt2 + slots;
+      ll.rng2 = reinterpret_cast<uint64_t*>(p + lists + 2 * slots * 4);  // (8-B aligned: slots % 4 == 0)
     } else {
       ll.hdr = nullptr;
       FMX_HIP(hipMemsetAsync(ll.cnt2, 0, slots * 4, st));
@@ -4379,13 +4660,33 @@ struct LongBufs {
 };
 
 
-// blocks of the list kernels (list_for_each): two rounds of the blocks resident at 5 waves
-// per SIMD (256 CUs x 5 blocks of 4 waves), and at least slots / kBlk so that a block's
-// slots fit one load per thread
-constexpr unsigned kLongListGrid = 2560;
-unsigned long_list_grid(uint64_t npat) {
+// blocks of the list kernels (list_for_each): one generation of the blocks resident at their
+// 4 waves per SIMD — 4 blocks of 4 waves per CU, 1024 on the MI355X's 256 CUs — and at least
+// slots / kBlk so that a block's slots fit one load per thread.  Round 5 A/B (CS_FM_LIST_GRID,
+// C4 ms per 12.5 M, repetitive DNA / Q_text 64-mers / 150-mers, profiles/r05/r05f, r05g):
+// 512: 0.679 / 1.93 / 2.42; 768: 0.667 / 1.53 / 1.94; 1024: 0.68 / 1.38-1.40 / 1.78-1.79;
+// 1280: 0.744 / 1.72 / 2.12; 2560 (round 4): 0.755 / 1.49 / 1.83 — a second, partial
+// generation of blocks costs a whole chain of dependent reads.
+constexpr unsigned kLongListGrid = 0;  // (0: 4 blocks per CU of the device)
+unsigned list_blocks_per_device() {
+  static std::once_flag once[64];
+  static unsigned g[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+  std::call_once(once[dev], [dev] {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) {
+      (void)hipGetLastError();
+      ncu = 256;
+    }
+    g[dev] = 4u * (unsigned)ncu;
+  });
+  return g[dev];
+}
+unsigned long_list_grid(uint64_t npat, uint32_t want = kLongListGrid) {
   const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
-  const uint64_t g = std::max<uint64_t>(std::min<uint64_t>(slots, kLongListGrid), (slots + kBlk - 1) / kBlk);
+  const uint64_t g = std::max<uint64_t>(std::min<uint64_t>(slots, want ? want : list_blocks_per_device()),
+                                        (slots + kBlk - 1) / kBlk);
   return (unsigned)std::max<uint64_t>(g, 1);
 }
 
@@ -4405,7 +4706,7 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
     if (s != CS_OK) return s;
     ll = own.ll;
   }
-  const unsigned g = routed ? long_list_grid(npat) : grid_for(npat, kBlk, 0xFFFFFFFFu);
+  const unsigned g = routed ? long_list_grid(npat, routed->grid) : grid_for(npat, kBlk, 0xFFFFFFFFu);
   // CS_QT_LONG_LOADS8 (CS_FM_LONG_V16=0): 8-B pattern / window loads; the default 16-B vectors
   // for the pattern's packed part and the window (C4 150-mers 1.87 -> 1.55 ms, 64-mers 1.25 ->
   // 1.16-1.21, profiles/r03/long_probe_v16.json; round 4's partial forms 1 / 2 are gone)
@@ -4498,6 +4799,7 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
     // the general searches a wave lists from (LongList::gen_list): CS_QT_GENERAL_INLANE none,
     // CS_QT_GENERAL_LIST_ALL every one, else the handle's threshold (CS_FM_GENERAL_LIST_MIN)
     lb.ll.gen_list = (flags & CS_QT_GENERAL_INLANE) ? 0u : (flags & CS_QT_GENERAL_LIST_ALL) ? 1u : h->gen_list_min;
+    lb.ll.grid = h->list_grid;
     if (nobar)
       k_count_ctx<OccE, 2, false, false, W, true, false, true><<<g2, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
@@ -4706,14 +5008,11 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.out_pos = d_out_pos;
   op.cap = d_out_pos ? cap : 0;
   op.wide_cap = wide_cap;
-  // the barrier-free search (CS_FM_COUNT_NOBAR, kPos 0) adds its tile totals: each block
-  // zeroes its tile first (and block 0 the wide-range counter); a call without it zeroes the
-  // counter (and, CS_Q_LONG, the tiles) here
+  // the search kernel's blocks zero their tiles (and block 0 the wide-range counter); a
+  // CS_Q_LONG call, which runs no search kernel, zeroes them here
   const bool nobar = kpos == 0 && count_nobar(flags);
   if (long_only)
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
-  else if (!nobar)
-    FMX_HIP(hipMemsetAsync(op.nwide, 0, 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
   op.defer = defer ? 1u : 0u;
   if (long_only || routed || defer) {
@@ -4736,7 +5035,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
           ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op, lb.ll);
     FMX_HIP(hipGetLastError());
     if (long_only || routed) {
-      const unsigned g1 = routed ? long_list_grid(npat) : grid_for(npat, kBlk, 0xFFFFFFFFu);
+      const unsigned g1 = routed ? long_list_grid(npat, h->list_grid) : grid_for(npat, kBlk, 0xFFFFFFFFu);
       // CS_QT_LONG_LOADS8 (k_count_long's): 8-B pattern / window loads
       const bool v0 = (flags & CS_QT_LONG_LOADS8) != 0;
       if (routed && v0)
@@ -4750,7 +5049,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
       FMX_HIP(hipGetLastError());
     }
     if (!routed)  // (a routed k_locate_long searches what it listed and what was deferred)
-      k_locate_list<<<long_list_grid(npat), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
+      k_locate_list<<<long_list_grid(npat, h->list_grid), kBlk, 0, st>>>(ix, d_pats, d_offs, npat, limit, op, lb.ll);
   } else if (kpos == 0 && nobar)
     k_count_ctx<OccE, U, true, false, 8, true, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);

@@ -2,7 +2,7 @@
 # round 5: kernel trace of the routed headline, general searches listed (default) vs in the
 # lane (CS_FM_GENERAL_INLANE=1 at build), and of the repetitive-DNA leg the same two ways
 set -uo pipefail
-O=$PWD/gpurun_out/r05b
+O=$PWD/gpurun_out/${TAG:-r05b}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
