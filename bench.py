@@ -260,7 +260,7 @@ def pmc_traffic(wl, leg, kern_s):
     e = json.load(open(PMC_LEGS)).get("%s|%s" % (wl, leg)) if os.path.exists(PMC_LEGS) else None
     if not e:
         return {"traffic": None, "traffic_stale": None, "traffic_profile": None}
-    prof_s = e.get("kernel_mean_ns_profiled", 0) / 1e9
+    prof_s = (e.get("kernel_median_ns_profiled") or e.get("kernel_mean_ns_profiled", 0)) / 1e9
     fresh = bool(prof_s and kern_s and abs(prof_s / kern_s - 1) <= 0.15)
     return {"traffic": e.get("hbm_bytes_per_launch") if fresh else None, "traffic_stale": not fresh,
             "traffic_profile": {"tag": e.get("tag"), "kernel": e.get("kernel"),
@@ -577,10 +577,13 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
     rnd = rw * nhit + int(torch.where(hb, 0, qb + 32 * cnt).sum().item())
     # random reads: one per 16-B record, one per 32-B sector or line, one SA sector per position
     acc = nhit + int(torch.where(hb, 0, (qb + 31) // 32 + cnt).sum().item())
+    # the search's results, written and read back: an 8-B record per pattern and a 4-B count
+    # unless the record is the pattern's only position (count 1; round 5)
+    mid = 8 * B + 4 * int((cnt != 1).sum().item())
     del qb, hit, hb, cnt
-    stream_b = B * m + (B + 1) * 8 + B * 12 * 2 + (B + 1) * 8 + tot * 8
+    stream_b = B * m + (B + 1) * 8 + mid * 2 + (B + 1) * 8 + tot * 8
     alg = rnd + stream_b
-    stream_rd = B * m + (B + 1) * 8 + B * 12  # patterns, offsets, the search's results read back
+    stream_rd = B * m + (B + 1) * 8 + mid  # patterns, offsets, the search's results read back
     lpmc = pmc_traffic(wl_key, name, min(evs))
     fb, reads, basis = dram_basis(alg, stream_rd, acc, lpmc)
     ltab = info.locate_record_bytes or info.prefix_bytes

@@ -21,7 +21,7 @@ KRE="k_count|k_walk|k_locate|k_expand"
 for LEG in ${LEGS//,/ }; do
   D=$OUT/$LEG
   mkdir -p "$D"
-  BENCH=(python3 "$ROOT/bench.py" --only "$LEG" --steps 6 --warmup 1 "$@")
+  BENCH=(python3 "$ROOT/bench.py" --only "$LEG" --steps ${PROF_STEPS:-6} --warmup ${PROF_WARMUP:-1} "$@")
   echo "[profile_legs] $LEG" >&2
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/trace" -o run -- "${BENCH[@]}" > "$D/bench_trace.json" 2> "$D/trace.err"
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" --output-format csv -d "$D/pmc_fetch" -o run -- "${BENCH[@]}" > "$D/bench_fetch.json" 2> "$D/fetch.err"

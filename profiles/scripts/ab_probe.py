@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""ab_probe.py --hook NAME=VAL [...] — the headline count (C4, Q_text 20-mers, 12.5 M) and
-optional legs with and without engine hooks (read per call), alternated in one process so
-box-to-box spread cancels: rounds x (A, B) kernel times from HIP events.  One JSON line.
---op locate times the one-call locate (cs_fm_locate_device, limit 100000) instead;
---hook-a NAME=VAL sets hooks for variant A (default: none)."""
+"""ab_probe.py --flags-b QT_NAME[,QT_NAME] — the headline count (C4, Q_text 20-mers, 12.5 M) and
+optional pattern lengths with and without tuning selectors (cs_fmindex.h CS_QT_*: per-call
+flags bits, round 5 — no environment is read by a query), alternated in one process so
+box-to-box spread cancels: rounds x (A, B) times from HIP events.  One JSON line.
+--op locate times the one-call locate (limit 100000) instead; --flags-a sets variant A's bits
+(default: none); --b2b times the reps back to back between two events (as bench.py's steps);
+--ws-a / --ws-b give a variant the caller's workspace (cs_fm_*_ws) instead of the per-call
+allocation."""
 import argparse
 import json
 import os
@@ -18,16 +21,25 @@ import bench  # noqa: E402
 from __graft_entry__ import _load_pkg  # noqa: E402
 
 
+def flag_bits(pkg, spec):
+    b = 0
+    for name in filter(None, (spec or "").split(",")):
+        b |= getattr(pkg, name if name.startswith("Q") else "QT_" + name)
+    return b
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--hook", action="append", default=[], help="NAME=VAL for variant B (repeatable)")
-    ap.add_argument("--hook-a", action="append", default=[], help="NAME=VAL for variant A (repeatable)")
+    ap.add_argument("--flags-a", default="", help="tuning bits of variant A (QT_* names, comma-separated)")
+    ap.add_argument("--flags-b", default="", help="tuning bits of variant B")
+    ap.add_argument("--ws-a", action="store_true", help="variant A with a workspace")
+    ap.add_argument("--ws-b", action="store_true", help="variant B with a workspace")
     ap.add_argument("--op", default="count", choices=("count", "locate"))
     ap.add_argument("--rounds", type=int, default=6)
-    ap.add_argument("--b2b", action="store_true",
-                    help="time the reps back to back between two events (as bench.py's steps)")
+    ap.add_argument("--b2b", action="store_true")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--m", default="20")
+    ap.add_argument("--batch", type=int, default=12_500_000)
     ap.add_argument("--text-kind", default="dna", help="dna or rdna")
     ap.add_argument("--text-bytes", type=int, default=3_999_999_999)
     a = ap.parse_args()
@@ -41,59 +53,56 @@ def main():
     pkg.synth_text_device(a.text_kind, 42, a.text_bytes, text.data_ptr(), sh)
     torch.cuda.synchronize()
     idx, _ = bench.build_index(pkg, text, N, 32, 0)
-    B = 12_500_000
-    hooks = {"A": dict(h.split("=", 1) for h in a.hook_a), "B": dict(h.split("=", 1) for h in a.hook)}
-    out = {"op": a.op, "hooks_A": hooks["A"], "hooks_B": hooks["B"], "m": {}}
+    B = a.batch
+    fl = {"A": flag_bits(pkg, a.flags_a), "B": flag_bits(pkg, a.flags_b)}
+    use_ws = {"A": a.ws_a, "B": a.ws_b}
+    wsb = idx.workspace_bytes(B)
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+    out = {"op": a.op, "flags_A": a.flags_a, "flags_B": a.flags_b, "ws_A": a.ws_a, "ws_B": a.ws_b,
+           "batch": B, "text_kind": a.text_kind, "b2b": a.b2b, "m": {}}
     for m in [int(x) for x in a.m.split(",")]:
         W = bench.Workload(pkg, text, N, m, 0, B, "dna", "text", dev, sh)
         o = torch.empty(B + 1, dtype=torch.int64, device=dev)
         cap = 2 * B
         pos = torch.empty(cap if a.op == "locate" else 1, dtype=torch.int64, device=dev)
 
-        def call():
+        def call(var):
+            w, wb = (ws.data_ptr(), wsb) if use_ws[var] else (0, 0)
             if a.op == "count":
-                idx.count_batch_device(W.pats.data_ptr(), W.offs.data_ptr(), B, o.data_ptr(), sh)
+                idx.count_device_ws(W.pats.data_ptr(), W.offs.data_ptr(), B, o.data_ptr(), w, wb,
+                                    flags=fl[var], stream=sh)
             else:
-                _, ok = idx.locate_device(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000, o.data_ptr(),
-                                          pos.data_ptr(), cap, sh)
+                _, ok = idx.locate_device_ws(W.pats.data_ptr(), W.offs.data_ptr(), B, 100000, o.data_ptr(),
+                                             pos.data_ptr(), cap, w, wb, sh, flags=fl[var])
                 if not ok:
                     raise SystemExit("position capacity short")
         res = {"A": [], "B": []}
         ref = None
         for r in range(a.rounds):
             for var in ("A", "B"):
-                saved = {k: os.environ.get(k) for k in list(hooks["A"]) + list(hooks["B"])}
-                os.environ.update(hooks[var])
-                try:
-                    call()
+                call(var)
+                torch.cuda.synchronize()
+                ms = []
+                if a.b2b:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    for _ in range(a.reps):
+                        call(var)
+                    e1.record(st)
                     torch.cuda.synchronize()
-                    ms = []
-                    if a.b2b:
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record(st)
-                        for _ in range(a.reps):
-                            call()
-                        e1.record(st)
-                        torch.cuda.synchronize()
-                        ms.append(e0.elapsed_time(e1) / a.reps)
-                    for _ in range(0 if a.b2b else a.reps):
-                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                        e0.record(st)
-                        call()
-                        e1.record(st)
-                        torch.cuda.synchronize()
-                        ms.append(e0.elapsed_time(e1))
-                    res[var].append(statistics.mean(ms))
-                    if ref is None:
-                        ref = o.clone()
-                    elif not torch.equal(ref, o):
-                        raise SystemExit("counts differ between variants")
-                finally:
-                    for k, v in saved.items():
-                        if v is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = v
+                    ms.append(e0.elapsed_time(e1) / a.reps)
+                for _ in range(0 if a.b2b else a.reps):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(st)
+                    call(var)
+                    e1.record(st)
+                    torch.cuda.synchronize()
+                    ms.append(e0.elapsed_time(e1))
+                res[var].append(statistics.median(ms))
+                if ref is None:
+                    ref = o.clone()
+                elif not torch.equal(ref, o):
+                    raise SystemExit("results differ between variants")
         out["m"][str(m)] = {"A_ms": res["A"], "B_ms": res["B"], "A_median": statistics.median(res["A"]),
                             "B_median": statistics.median(res["B"])}
         print("[ab] m=%d A %.4f B %.4f" % (m, statistics.median(res["A"]), statistics.median(res["B"])),

@@ -111,8 +111,10 @@ def main():
             n = short(r.get("Kernel_Name", ""))
             dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             res["kernels"].setdefault(n, []).append(dur)
-        res["kernels"] = {n: {"dispatches": len(v), "mean_ns": statistics.mean(v), "min_ns": min(v),
-                              "total_ns": sum(v)}
+        # (round 5: the median beside the mean — bench.py's roofline time is a median of its
+        # timed launches, and the first, cold launch moves a mean)
+        res["kernels"] = {n: {"dispatches": len(v), "median_ns": statistics.median(v),
+                              "mean_ns": statistics.mean(v), "min_ns": min(v), "total_ns": sum(v)}
                           for n, v in sorted(res["kernels"].items(), key=lambda kv: -sum(kv[1]))}
         for sub, names in (("pmc_fetch", ["FETCH_SIZE"]), ("pmc_l2", ["TCC_HIT_sum", "TCC_MISS_sum"])):
             for r in rows(os.path.join(ld, sub, "**", "*counter_collection.csv")):
@@ -147,9 +149,12 @@ def main():
             routed = "k_locate_long" in res["kernels"]
             group = sorted(n for n in cands if n in res["kernels"] and
                            (n != "k_count_ctx_onepass" if routed else n != "k_count_ctx_onepass_skiplong"))
-        elif kname and kname.startswith("k_count_long"):
-            group += [n for n in res["pmc"] if n == "k_count_list" or n.endswith("_skiplong_w8")
-                      or (n.startswith("k_count_ctx_") and "skiplong" in n)]
+        elif kname and (kname.startswith("k_count_long") or "skiplong" in kname):
+            # a routed count (round 5: every device batch): the staged kernel, the list kernel
+            # (long patterns and listed general searches) and k_count_list
+            group += [n for n in res["pmc"] if n == "k_count_list" or
+                      (n.startswith("k_count_long") and not n.endswith("_bytes")) or
+                      (n.startswith("k_count_ctx_") and "skiplong" in n)]
             group = sorted(set(group))
         lo = (b.get("legs") or {}).get(leg) or {}
         if leg == "count":
@@ -159,7 +164,8 @@ def main():
         else:
             stream_rd = lo.get("phase2_stream_read_bytes")
         if want is ONE_CALL and stream_rd is not None and lo.get("patterns"):
-            stream_rd += 12 * lo["patterns"]  # the emit kernel's read of the counts and records
+            # the emit kernel's read of the records (round 5: no count beside a stashed position)
+            stream_rd += 8 * lo["patterns"]
         wl = lo.get("workload_key") or b.get("workload_key")  # the leg's own index
         kc = res["pmc"].get(kname, {}) if kname else {}
         if len(group) > 1:  # sums over the group (per launch of each)
@@ -180,6 +186,8 @@ def main():
                  "hbm_bytes_per_launch": hbm,
                  "l2_hit_rate": kc.get("l2_hit_rate"),
                  "kernel_mean_ns_profiled": sum(res["kernels"].get(n, {}).get("mean_ns", 0) for n in group),
+                 "kernel_median_ns_profiled": sum(res["kernels"].get(n, {}).get("median_ns", 0) for n in group),
+                 "dispatches_profiled": res["kernels"].get(kname, {}).get("dispatches"),
                  "tag": tag}
             e["workload"] = wl
             pmc_legs["%s|%s" % (wl, leg)] = e
