@@ -251,16 +251,27 @@ constexpr uint64_t kListHdrBytes = (uint64_t)(kListedLanes + 1) * kListedStride 
 struct LongList {
   uint16_t* list = nullptr;
   uint32_t* cnt = nullptr;
-  uint16_t* list2 = nullptr;
+  uint32_t* list2 = nullptr;  // (u32: the offset in bits 0-8, the routed count's chain above)
   uint32_t* cnt2 = nullptr;
   uint32_t* hdr = nullptr;  // listed[kListedLanes] (kListedStride apart), then retire
   uint32_t gen_list = 0;    // the routed count: general-search patterns to list2
   // the routed count: per list2 entry the range the staged kernel's table read left (sp in
   // bits 0-31, its width in 32-63; narrow indexes) or kNoRange (the search starts over)
+  // (and in the list2 entry's bits 9-26, beside a range, the 2-bit occurrence codes of the
+  // characters still to step — list_chain — or kChainNone: a symbol without a code, the
+  // pattern is read again)
   uint64_t* rng2 = nullptr;
   uint32_t grid = 0;  // (host side: the list kernel's grid, cs_fm_index::list_grid; 0 = default)
 };
 constexpr uint64_t kNoRange = ~0ull;
+// A listed pattern's chain (18 bits, a list2 entry's bits 9-26): its first k <= 7 characters'
+// occurrence codes, character i at bits 2 (k - 1 - i) (the staged kernel's context key: the
+// next character to step at bits 0-1), k at bits 14-16, bit 17 set.
+constexpr uint32_t kChainNone = 0;
+constexpr uint32_t kChainShift = 9;  // log2(kLongRegion): the entry's offset below it
+__host__ __device__ inline uint32_t list_chain(uint32_t codes, uint32_t k) {
+  return codes | (k << 14) | (1u << 17);
+}
 // the staged kernel's wave adds its listed patterns (lane 0; n uniform over the wave)
 __device__ __forceinline__ void list_listed_add(const LongList& ll, uint32_t n) {
   if (n && (threadIdx.x & 63) == 0)

@@ -1388,6 +1388,47 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tile
   if (t == 0) *total_out = s_carry;
 }
 
+// the positions of c <= kLocSmall rows — rows r0 + i, or r0 + the set bits of rel (a context
+// window) — minus adj (mod n), to out: SA reads or walks kEmitRows at a time in lockstep, so
+// a lane's rows are in flight together (round 5: one after the other, C5's emit took 360 us
+// per 12.5 M 20-mers, every wave waiting on a lane's chain of walks)
+constexpr int kEmitRows = 4;
+template <int kPos>
+__device__ __forceinline__ void emit_rows(const DevIndex& ix, const NodeTable& T, const OnePass& op,
+                                          uint64_t* __restrict__ out, uint64_t c, uint64_t r0, uint32_t rel,
+                                          uint64_t adj) {
+  const uint64_t n = ix.n;
+  for (uint64_t i = 0; i < c; i += kEmitRows) {
+    uint64_t row[kEmitRows];
+    bool act[kEmitRows];
+#pragma unroll
+    for (int u = 0; u < kEmitRows; ++u) {
+      act[u] = i + u < c;
+      row[u] = 0;
+      if (!act[u]) continue;
+      if (rel) {
+        row[u] = r0 + (uint32_t)__ffs(rel) - 1u;
+        rel &= rel - 1u;
+      } else {
+        row[u] = r0 + i + u;
+      }
+    }
+    if constexpr (kPos == 0) {
+#pragma unroll
+      for (int u = 0; u < kEmitRows; ++u)
+        if (act[u]) row[u] = load_sa(op.sa, row[u]);
+    } else {
+      bool w[kEmitRows];
+#pragma unroll
+      for (int u = 0; u < kEmitRows; ++u) w[u] = act[u];
+      walk_positions<std::conditional_t<kPos == 1, WalkLine, WalkLineW>, kEmitRows>(ix, T, row, w);
+    }
+#pragma unroll
+    for (int u = 0; u < kEmitRows; ++u)
+      if (act[u]) st_out(out + i + u, row[u] >= adj ? row[u] - adj : row[u] + n - adj);
+  }
+}
+
 // (3): offsets and positions of tile blockIdx.x (round 5: a pattern whose record is a stashed
 // position has no count stored: 8 B read per pattern instead of 12.  Tried in round 5 to drop
 // the scan kernel: a decoupled look-back over the tiles — its frontier moves 64 tiles per L2
@@ -1435,14 +1476,9 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
       uint64_t r0, adj;
       uint32_t rel;
       loc_window(s, r0, adj, rel);
-      for (uint64_t i = 0; i < c; ++i) {
-        const uint32_t f = (uint32_t)__ffs(rel) - 1u;
-        const uint64_t p = onepass_pos<kPos>(ix, T, op, r0 + f);
-        st_out(op.out_pos + a + i, p >= adj ? p - adj : p + n - adj);
-        rel &= rel - 1u;
-      }
+      emit_rows<kPos>(ix, T, op, op.out_pos + a, c, r0, rel, adj);
     } else if (c <= kLocSmall) {
-      for (uint64_t i = 0; i < c; ++i) st_out(op.out_pos + a + i, onepass_pos<kPos>(ix, T, op, s + i));
+      emit_rows<kPos>(ix, T, op, op.out_pos + a, c, s, 0u, 0);
     } else {
       const unsigned long long e = atomicAdd(op.nwide, 1ull);
       if (e < op.wide_cap) {
@@ -1473,8 +1509,8 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit_wide(DevIndex ix, OnePass 
 // The lanes' patterns j with bit j of `m` set into the wave's slot of a LongList list (their
 // offsets inside the block's region, in ballot order) and their number into cnt[slot] (0
 // when none); returns that number (uniform).  Every lane of the wave, in uniform control flow.
-template <int U = 2>
-__device__ __forceinline__ uint32_t wave_list(uint16_t* list, uint32_t* cnt, uint64_t slot, uint32_t m) {
+template <int U = 2, class T>
+__device__ __forceinline__ uint32_t wave_list(T* list, uint32_t* cnt, uint64_t slot, uint32_t m) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t n = 0;
@@ -1482,17 +1518,18 @@ __device__ __forceinline__ uint32_t wave_list(uint16_t* list, uint32_t* cnt, uin
   for (int j = 0; j < U; ++j) {
     const bool b = (m >> j) & 1u;
     const uint64_t bal = __ballot(b);
-    if (b) list[slot * kLongSlot + n + __popcll(bal & below)] = (uint16_t)(threadIdx.x + j * kBlk);
+    if (b) list[slot * kLongSlot + n + __popcll(bal & below)] = (T)(threadIdx.x + j * kBlk);
     n += __popcll(bal);
   }
   if (lane == 0) cnt[slot] = n;
   return n;
 }
 
-// wave_list, and each listed pattern's payload pay[j] at the same place of `rng`
+// wave_list into list2, each listed pattern's chain ch[j] in its entry's upper bits and its
+// payload pay[j] at the same place of `rng`
 template <int U = 2>
-__device__ __forceinline__ uint32_t wave_list_pay(uint16_t* list, uint32_t* cnt, uint64_t* rng, uint64_t slot,
-                                                  uint32_t m, const uint64_t* pay) {
+__device__ __forceinline__ uint32_t wave_list_pay(uint32_t* list, uint32_t* cnt, uint64_t* rng, uint64_t slot,
+                                                  uint32_t m, const uint64_t* pay, const uint32_t* ch) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t n = 0;
@@ -1502,7 +1539,7 @@ __device__ __forceinline__ uint32_t wave_list_pay(uint16_t* list, uint32_t* cnt,
     const uint64_t bal = __ballot(b);
     if (b) {
       const uint64_t at = slot * kLongSlot + n + __popcll(bal & below);
-      list[at] = (uint16_t)(threadIdx.x + j * kBlk);
+      list[at] = (uint32_t)(threadIdx.x + j * kBlk) | (ch[j] << kChainShift);
       rng[at] = pay[j];
     }
     n += __popcll(bal);
@@ -1551,8 +1588,12 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // (kRng; A/B in one process, profiles/r03/ab_range_across_barrier*.json: headline 0.389
   // vs 0.388 ms, 24-mers 1.32 vs 1.40 ms, repetitive DNA 2.56 vs 2.71 ms)
   __shared__ uint64_t s_rng[kLoc ? 1 : U][kLoc ? 1 : kBlk][2];
+  // ... and its chain (list_chain: the codes of the characters before the table's) for the
+  // list kernel, kept here rather than in registers to the listing after (D) (round 5: in
+  // registers the routed kernel spilled 7 VGPRs instead of 3)
+  __shared__ uint32_t s_chn[kLoc ? 1 : U][kLoc ? 1 : kBlk];
   static_assert(kBlk >= 256, "one map entry per thread");
-  static_assert(!kOne || (kLoc && (!kNoBar || kPos == 0)), "the one-call locate's walks need barriers");
+  static_assert(!kOne || kLoc, "the one-call search is a locate form");
   static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
@@ -1829,7 +1870,10 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
         w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
       }
     } else if constexpr (!kLoc && kRng) {
-      st[j] = 5;  // too wide for the contexts, or no context key: the general search
+      // too wide for the contexts, or no context key: the general search (the chain codes
+      // in want[j] stand only when the pattern had its context key, st 2)
+      s_chn[j][threadIdx.x] = st[j] == 2 ? list_chain(want[j], k[j]) : kChainNone;
+      st[j] = 5;
       s_rng[j][threadIdx.x][0] = sp[j];
       s_rng[j][threadIdx.x][1] = ep[j];
     } else {
@@ -1859,6 +1903,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
           st[j] = 5;
           s_rng[j][threadIdx.x][0] = sp[j];
           s_rng[j][threadIdx.x][1] = ep[j];
+          s_chn[j][threadIdx.x] = list_chain(want[j], k[j]);
         }
       } else if (!kLoc || mm == 0) {
         res[j] = (uint64_t)__popc(mm);
@@ -1908,14 +1953,18 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       ng += (uint32_t)__popcll(__ballot(g));
     }
     if (ll.gen_list && ng >= ll.gen_list) {
-      // with the range the table read left (st 5: too wide for the contexts), so the list
-      // kernel steps on from it instead of reading the record again
+      // with the range the table read left (st 5: too wide for the contexts) and the chain
+      // codes of the characters before the table's (list_chain), so the list kernel steps on
+      // from them instead of reading the record, the offsets and the pattern again
       uint64_t pay[U];
+      uint32_t chn[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j)
-        pay[j] = st[j] == 5 && !ix.wide && ep[j] - sp[j] <= 0xFFFFFFFFull ? (sp[j] | ((ep[j] - sp[j]) << 32))
-                                                                          : kNoRange;
-      nlisted += wave_list_pay<U>(ll.list2, ll.cnt2, ll.rng2, slot, gm, pay);
+      for (int j = 0; j < U; ++j) {
+        const bool r = st[j] == 5 && !ix.wide && ep[j] - sp[j] <= 0xFFFFFFFFull;
+        pay[j] = r ? (sp[j] | ((ep[j] - sp[j]) << 32)) : kNoRange;
+        chn[j] = r ? s_chn[j][threadIdx.x] : kChainNone;
+      }
+      nlisted += wave_list_pay<U>(ll.list2, ll.cnt2, ll.rng2, slot, gm, pay, chn);
 #pragma unroll
       for (int j = 0; j < U; ++j)
         if ((gm >> j) & 1u) st[j] = 6;  // listed
@@ -1929,14 +1978,15 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3 || st[j] == 5;
   if constexpr (kOne && kNoBar) {
-    // the barrier-free one-call search (kPos 0): the general search reads the node table
-    // through the caches, the tile total is added wave by wave (locate_split_store)
+    // the barrier-free one-call search: the general search and the walks (kPos 1 / 2) read
+    // the node table through the caches, the tile total is added wave by wave
+    // (locate_split_store)
     if (general)
       general_rest<E, U, kLoc, kPacked, W, true>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec, kc, kr);
     uint32_t skip = 0;  // the patterns left to k_locate_long (4) and k_locate_list (7)
 #pragma unroll
     for (int j = 0; j < U; ++j) skip |= (uint32_t)(st[j] == 4 || st[j] == 7) << j;
-    locate_split_store<U, 0, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
+    locate_split_store<U, kPos, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
     return;
   } else if constexpr (kNoBar) {
     if (general)
@@ -2309,7 +2359,7 @@ __device__ __forceinline__ void long_list_append(bool general, uint64_t q, const
   if (!general) return;
   const uint64_t sl = long_slot(q);
   const uint32_t at = atomicAdd(ll.cnt2 + sl, 1u);
-  ll.list2[sl * kLongSlot + at] = (uint16_t)(q % kLongRegion);
+  ll.list2[sl * kLongSlot + at] = (uint32_t)(q % kLongRegion);
   if (ll.rng2) ll.rng2[sl * kLongSlot + at] = kNoRange;  // (the search starts over)
 }
 
@@ -2336,8 +2386,8 @@ __device__ __forceinline__ uint32_t slot_count(const uint32_t* cnt, uint64_t npa
   else return cnt[sl];
 }
 
-template <class F>
-__device__ __forceinline__ uint32_t list_for_each(const uint16_t* __restrict__ list, uint32_t c, F&& f) {
+template <class T, class F>
+__device__ __forceinline__ uint32_t list_for_each(const T* __restrict__ list, uint32_t c, F&& f) {
   static_assert(kBlk == 256, "the slot lookup below searches 256 slots in 8 steps");  // 
   __shared__ uint32_t s_off[kBlk + 1];
   __shared__ uint32_t s_w[kBlk / 64];
@@ -2371,7 +2421,7 @@ __device__ __forceinline__ uint32_t list_for_each(const uint16_t* __restrict__ l
       else hi = mid;
     }
     const uint64_t s2 = blockIdx.x + (uint64_t)lo * gridDim.x;
-    const uint64_t q = s2 / kSlotsPerRegion * kLongRegion + list[s2 * kLongSlot + (e - s_off[lo])];
+    const uint64_t q = s2 / kSlotsPerRegion * kLongRegion + (list[s2 * kLongSlot + (e - s_off[lo])] & (kLongRegion - 1));
     f(q, e0 + threadIdx.x < tot);
   }
   return tot;
@@ -2380,7 +2430,7 @@ __device__ __forceinline__ uint32_t list_for_each(const uint16_t* __restrict__ l
 // list_for_each with two entries per thread and round (e and e + kBlk of 2 kBlk): f(q, act)
 // with q[2], act[2], the whole block in lockstep
 template <class F>
-__device__ __forceinline__ uint32_t list_for_each2(const uint16_t* __restrict__ list, uint32_t c, F&& f) {
+__device__ __forceinline__ uint32_t list_for_each2(uint32_t c, F&& f) {
   static_assert(kBlk == 256, "the slot lookup below searches 256 slots in 8 steps");
   __shared__ uint32_t s_off2[kBlk + 1];
   __shared__ uint32_t s_w2[kBlk / 64];
@@ -2428,15 +2478,18 @@ __device__ __forceinline__ uint32_t list_for_each2(const uint16_t* __restrict__ 
 
 // The rest of up to U listed general searches of the routed count from the ranges the
 // staged kernel's table reads left (LongList::rng2), k[j] <= kCtxQ characters still to
-// step: count_rest's steps without its verification (k <= kCtxQ never verifies), the U
-// patterns in lockstep — every round issues all their line (or context-sector) loads before
-// any is used, so a lane keeps U dependent chains in flight — and the rows' left contexts
-// once the range fits two sectors (ctx_match; an escaped context or a rare symbol steps on).
-// act[j] false on entry: no pattern j.  Reference: fm_index.cpp:90-98.
+// step, given by their occurrence codes (cw[j]: the list2 entry's chain, the next character at
+// bits 0-1 — no pattern byte is read): count_rest's steps without its verification (k <= kCtxQ
+// never verifies), the U patterns in lockstep — every round issues all their line (or
+// context-sector) loads before any is used, so a lane keeps U dependent chains in flight —
+// and the rows' left contexts once the range fits two sectors (ctx_match; an escaped
+// context steps on).  act[j] false on entry: no pattern j.  Reference: fm_index.cpp:90-98.
+// (Round 5: the list kernel read each pattern's offsets and bytes before its first step and
+// a byte per step — repetitive DNA's list kernel 236 us per 12.5 M 20-mers.)
 template <int U>
-__device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable& T,
-                                            const uint8_t* const* P, uint32_t* k, uint64_t* sp,
-                                            uint64_t* ep, bool* act, uint64_t* res) {
+__device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable& T, uint32_t* cw,
+                                            uint32_t* k, uint64_t* sp, uint64_t* ep, bool* act,
+                                            uint64_t* res) {
   bool ctx[U];
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -2473,28 +2526,19 @@ __device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable&
         }
       } else {
         mode[j] = 1;
-        const uint32_t c = P[j][k[j] - 1];
-        if (T.C[c] == T.C[c + 1]) {  // absent symbol: the range empties
-          res[j] = 0;
-          act[j] = false;
-          mode[j] = 0;
-          continue;
-        }
-        if (T.occ_code[c] != kNoCode) {
-          const uint64_t qa = sp[j] >> 6, qe = ep[j] >> 6;
-          OccLine::Raw va;
-          OccLine::load(ix.lines, qa, va);
-          b[j][0] = va[0];
-          b[j][1] = va[1];
-          if (qe != qa) {
-            OccLine::Raw ve;
-            OccLine::load(ix.lines, qe, ve);
-            b[j][2] = ve[0];
-            b[j][3] = ve[1];
-          } else {
-            b[j][2] = va[0];
-            b[j][3] = va[1];
-          }
+        const uint64_t qa = sp[j] >> 6, qe = ep[j] >> 6;
+        OccLine::Raw va;
+        OccLine::load(ix.lines, qa, va);
+        b[j][0] = va[0];
+        b[j][1] = va[1];
+        if (qe != qa) {
+          OccLine::Raw ve;
+          OccLine::load(ix.lines, qe, ve);
+          b[j][2] = ve[0];
+          b[j][3] = ve[1];
+        } else {
+          b[j][2] = va[0];
+          b[j][3] = va[1];
         }
       }
     }
@@ -2502,23 +2546,9 @@ __device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable&
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       if (mode[j] == 2) {
-        uint32_t want = 0;
-        bool ok = true, absent = false;
-        for (uint32_t t = 0; t < k[j]; ++t) {  // chain symbol t = P[k-1-t]
-          const uint32_t c = P[j][k[j] - 1 - t];
-          absent |= T.C[c] == T.C[c + 1];
-          const uint32_t d = T.occ_code[c];
-          ok &= d != kNoCode;
-          want |= (d & 3u) << (2 * t);
-        }
-        if (absent) {
-          res[j] = 0;
-          act[j] = false;
-          continue;
-        }
         const uint64_t base = sp[j] & ~15ull;
         const uint32_t lo = (uint32_t)(sp[j] - base), hi = (uint32_t)(ep[j] - base);
-        const uint32_t mask = ((1u << (2 * k[j])) - 1u) | kCtxEsc;
+        const uint32_t mask = ((1u << (2 * k[j])) - 1u) | kCtxEsc, want = cw[j] & ((1u << (2 * k[j])) - 1u);
         const uint32_t* dw = reinterpret_cast<const uint32_t*>(b[j]);
         uint32_t match = 0, esc = 0;
 #pragma unroll
@@ -2528,30 +2558,23 @@ __device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable&
           esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
         }
         const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-        if (!ok || (esc & in)) {
-          ctx[j] = false;  // a rare symbol: step on
+        if (esc & in) {
+          ctx[j] = false;  // a rare symbol in a row's chain: step on
         } else {
           res[j] = (uint64_t)__popc(match & in);
           act[j] = false;
         }
       } else if (mode[j] == 1) {
-        const uint32_t c = P[j][k[j] - 1];
-        const uint32_t code = T.occ_code[c];
-        uint64_t rs, re;
-        if (code == kNoCode) {
-          rs = exc_rank(T, c, sp[j]);
-          re = exc_rank(T, c, ep[j]);
-        } else {
-          const OccLine::Raw va = {b[j][0], b[j][1]}, ve = {b[j][2], b[j][3]};
-          rs = OccE::occ_line(va, code, sp[j]);
-          re = OccE::occ_line(ve, code, ep[j]);
-          if (code == 0 && T.exc_n) {
-            rs -= exc_before(T, sp[j]);
-            re -= exc_before(T, ep[j]);
-          }
+        const uint32_t code = cw[j] & 3u, c = T.occ_sym[code];
+        const OccLine::Raw va = {b[j][0], b[j][1]}, ve = {b[j][2], b[j][3]};
+        uint64_t rs = OccE::occ_line(va, code, sp[j]), re = OccE::occ_line(ve, code, ep[j]);
+        if (code == 0 && T.exc_n) {
+          rs -= exc_before(T, sp[j]);
+          re -= exc_before(T, ep[j]);
         }
         sp[j] = T.C[c] + rs;
         ep[j] = T.C[c] + re;
+        cw[j] >>= 2;
         --k[j];
       }
     }
@@ -2559,50 +2582,48 @@ __device__ __forceinline__ void count_steps(const DevIndex& ix, const NodeTable&
 }
 
 // The routed count's list2 entries (k_count_long kList): two per thread and round; an entry
-// with a range from the staged kernel and at most kCtxQ characters left takes count_steps
-// (the two of a thread in lockstep), any other the general search from the start
-// (count_pattern: no range kept, a wide index, longer rests that verify against the text).
+// with a range and a chain from the staged kernel takes count_steps (the two of a thread in
+// lockstep; its list entry, range and chain are its only reads before the first step), any
+// other the general search from the start (count_pattern: no range kept, a wide index, a
+// symbol without an occurrence code, longer rests that verify against the text).
 template <int W>
 __device__ __forceinline__ void count_list_general2(const DevIndex& ix, NodeTable& T, const uint8_t* __restrict__ pats,
                                                     const uint64_t* __restrict__ offs, const CountOut& co,
                                                     uint64_t fixed_m, const LongList& ll, uint32_t c) {
   bool staged = false;
-  list_for_each2(ll.list2, c, [&](const uint64_t* ei, const bool* act) {
+  list_for_each2(c, [&](const uint64_t* ei, const bool* act) {
     if (!staged) {  // the first round (uniform): the block has entries
       load_table(T, ix.table);
       __syncthreads();
       staged = true;
     }
-    uint64_t q[2], sp[2], ep[2], res[2];
-    uint32_t k[2];
-    const uint8_t* P[2];
+    uint64_t q[2], sp[2], ep[2], res[2], r[2];
+    uint32_t k[2], cw[2], ch[2];
     bool lean[2], a2[2];
 #pragma unroll
+    for (int h = 0; h < 2; ++h) {  // (the three loads of both entries first)
+      const uint64_t e = act[h] ? ei[h] : 0;
+      const uint32_t le = ll.list2[e];
+      q[h] = e / kLongSlot / kSlotsPerRegion * kLongRegion + (le & (kLongRegion - 1));
+      r[h] = ll.rng2[e];
+      ch[h] = le >> kChainShift;
+    }
+#pragma unroll
     for (int h = 0; h < 2; ++h) {
-      lean[h] = false;
-      a2[h] = false;
-      q[h] = 0;
-      k[h] = 0;
-      sp[h] = ep[h] = 0;
-      P[h] = pats;
-      if (!act[h]) continue;
-      const uint64_t e = ei[h];
-      q[h] = e / kLongSlot / kSlotsPerRegion * kLongRegion + ll.list2[e];
-      const uint64_t o0 = offs ? offs[q[h]] : q[h] * fixed_m, m = offs ? offs[q[h] + 1] - o0 : fixed_m;
-      P[h] = pats + o0;
-      const uint64_t r = ll.rng2[e];
-      if (r != kNoRange && m >= ix.ptab_k && m - ix.ptab_k <= kCtxQ) {
-        lean[h] = a2[h] = true;
-        k[h] = (uint32_t)(m - ix.ptab_k);
-        sp[h] = r & 0xFFFFFFFFull;
-        ep[h] = sp[h] + (r >> 32);
-      } else {
-        // (no range: the search from the start, as the staged kernel's general search)
-        store_count<W>(co, q[h], m == 0 ? ix.n : count_pattern<OccE>(ix, T, P[h], m));
+      lean[h] = act[h] && r[h] != kNoRange && ((ch[h] >> 17) & 1u);
+      a2[h] = lean[h];
+      k[h] = lean[h] ? (ch[h] >> 14) & 7u : 0u;
+      cw[h] = ch[h] & 0x3FFFu;
+      sp[h] = lean[h] ? r[h] & 0xFFFFFFFFull : 0;
+      ep[h] = lean[h] ? sp[h] + (r[h] >> 32) : 0;
+      if (act[h] && !lean[h]) {
+        // (the search from the start, as the staged kernel's general search)
+        const uint64_t o0 = offs ? offs[q[h]] : q[h] * fixed_m, m = offs ? offs[q[h] + 1] - o0 : fixed_m;
+        store_count<W>(co, q[h], m == 0 ? ix.n : count_pattern<OccE>(ix, T, pats + o0, m));
       }
     }
     if (lean[0] || lean[1]) {
-      count_steps<2>(ix, T, P, k, sp, ep, a2, res);
+      count_steps<2>(ix, T, cw, k, sp, ep, a2, res);
 #pragma unroll
       for (int h = 0; h < 2; ++h)
         if (lean[h]) store_count<W>(co, q[h], res[h]);
@@ -4619,7 +4640,7 @@ inline uint32_t call_flags(const cs_fm_index* h, uint32_t flags) { return flags 
 // index has the packed one (tuning hook CS_FM_LONG_KERNEL=2)
 // The call's long-pattern lists (LongList): the counters' header (kListHdrBytes, zero between
 // calls), slot lists of the staged kernel (list / cnt, unless `direct`) and of k_count_long /
-// k_locate_long for the general search (list2 / cnt2), u16 offsets inside the slots' regions;
+// k_locate_long for the general search (list2 / cnt2), offsets inside the slots' regions (u16; list2 u32 with the chain);
 // in the caller's workspace (round 5: cs_fm_workspace_bytes, no allocation in the call) or in
 // one stream-ordered allocation whose header is zeroed here.  Direct launches (every pattern
 // to the long kernel, no staged kernel before it) zero cnt2 here and use no counters;
@@ -4631,24 +4652,25 @@ struct LongBufs {
   LongList ll;
   static uint64_t bytes(uint64_t npat, bool direct) {
     const uint64_t slots = (npat + kLongRegion - 1) / kLongRegion * kSlotsPerRegion;
-    // (+ the ranges of the general-search entries, 8 B each, after the lists and counts)
-    return kListHdrBytes + (direct ? 1 : 2) * slots * (kLongSlot * 2 + 4) + (direct ? 0 : slots * kLongSlot * 8);
+    // list2 (u32 entries) and cnt2; unless direct, list (u16), cnt and the ranges of the
+    // general-search entries (8 B each)
+    return kListHdrBytes + slots * (kLongSlot * 4 + 4) + (direct ? 0 : slots * (kLongSlot * (2 + 8) + 4));
   }
   // into `at` (bytes(npat, direct) of it: the caller's workspace, whose header the calls keep
   // zeroed, or the call's own allocation when `fresh`), or an allocation of its own
   cs_status alloc(uint64_t npat, bool direct, hipStream_t st, void* at = nullptr, bool fresh = true) {
     const uint64_t regions = (npat + kLongRegion - 1) / kLongRegion, slots = regions * kSlotsPerRegion;
     const uint64_t entries = slots * kLongSlot;
-    const uint64_t lists = (direct ? 1 : 2) * entries * 2;
+    const uint64_t lists = entries * 4 + (direct ? 0 : entries * 2);
     if (!at) FMX_HIP(buf.alloc(bytes(npat, direct), st));
     uint8_t* p = at ? static_cast<uint8_t*>(at) : buf.as<uint8_t>();
     ll.hdr = reinterpret_cast<uint32_t*>(p);
     if ((!at || fresh) && !direct) FMX_HIP(hipMemsetAsync(p, 0, kListHdrBytes, st));
     p += kListHdrBytes;
-    ll.list2 = reinterpret_cast<uint16_t*>(p);
+    ll.list2 = reinterpret_cast<uint32_t*>(p);
     ll.cnt2 = reinterpret_cast<uint32_t*>(p + lists);
     if (!direct) {
-      ll.list = ll.list2 + entries;
+      ll.list = reinterpret_cast<uint16_t*>(p + entries * 4);
       ll.cnt = ll.cnt2 + slots;
       ll.rng2 = reinterpret_cast<uint64_t*>(p + lists + 2 * slots * 4);  // (8-B aligned: slots % 4 == 0)
     } else {
@@ -5010,7 +5032,9 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide_cap = wide_cap;
   // the search kernel's blocks zero their tiles (and block 0 the wide-range counter); a
   // CS_Q_LONG call, which runs no search kernel, zeroes them here
-  const bool nobar = kpos == 0 && count_nobar(flags);
+  // (round 5: the walk forms too — C5's search over walk lines no longer waits at a block
+  // barrier for a 10.8-KB node-table copy before its walks)
+  const bool nobar = count_nobar(flags);
   if (long_only)
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
@@ -5056,8 +5080,14 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else if (kpos == 1 && nobar)
+    k_count_ctx<OccE, U, true, false, 8, true, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else if (kpos == 1)
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else if (nobar)
+    k_count_ctx<OccE, U, true, false, 8, true, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(

@@ -15,7 +15,7 @@ for round in $(seq 1 ${AB_ROUNDS:-2}); do
   for V in "$@"; do
     cp "$PKG/libcs_fmindex_$V.so" "$PKG/libcs_fmindex.so"
     echo "[ab_lib] round $round $V" >&2
-    R=$(timeout -k 10 240 python3 "$ROOT/bench.py" --only "${AB_LEG:-count}" --steps 30 --warmup 5 | tail -1)
+    R=$(timeout -k 10 240 python3 "$ROOT/bench.py" --only "${AB_LEG:-count}" --steps 30 --warmup 5 ${AB_ARGS:-} | tail -1)
     echo "{\"variant\": \"$V\", \"round\": $round, \"result\": $R}" >> "$OUT"
   done
 done

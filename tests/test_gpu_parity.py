@@ -318,7 +318,7 @@ def test_count_every_text_vs_oracle(built, name):
                 pats.append(bytes(p))
     want = [o.count(p) for p in pats]
     assert g.count_batch(pats).tolist() == want, name
-    # every general search listed for the list kernel (a wave lists them from 4 by default)
+    # every general search listed for the list kernel (a wave lists them from 2 by default)
     assert _count_ex(g, pats, flags=load_pkg().QT_GENERAL_LIST_ALL)[0].tolist() == want, name
     if _learned():
         assert _bar_count(g, *O.pack_patterns(pats)).tolist() == want, name

@@ -199,11 +199,13 @@ def test_c4_dna_4gb(variant, monkeypatch):
 
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C5") == "1", reason="C5 disabled")
-@pytest.mark.parametrize("engine", ["auto", "wavelet"])
+@pytest.mark.parametrize("engine", ["auto", pytest.param("wavelet", marks=pytest.mark.skipif(
+    os.environ.get("CS_FM_C5_WAVELET") != "1", reason="opt-in (CS_FM_C5_WAVELET=1): 39 s of the suite's budget"))])
 def test_c5_dna_32gb_wide(engine, monkeypatch):
     """BASELINE configs[4]: 32 GB text (n >= 2^32) — wide index (u64 samples) built by
     the pass-by-pass bucketed suffix sorter, with occurrence lines (default for
-    DNA) or the wavelet matrix in 32-B wide rank lines (Line32W)."""
+    DNA) or the wavelet matrix in 32-B wide rank lines (Line32W; round 5: opt-in — the same
+    wide layout runs at small n in every parity test's wide_wavelet variant)."""
     if engine == "wavelet":
         monkeypatch.setenv("CS_FM_ENGINE", "wavelet")
     pkg = load_pkg()
