@@ -102,7 +102,7 @@ PMC_LEGS = os.path.join(ROOT, "profiles", "pmc_legs.json")
 
 # legs by index: the headline index (occurrence lines + contexts + records + full SA),
 # the reference's binary wavelet matrix, the occurrence engine with walk lines
-LEGS_MAIN = ["count_100m", "count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
+LEGS_MAIN = ["count_100m", "count_streams", "count_u32", "count_packed", "count_table_steps", "count_lf_loop", "count_m32",
              "count_m64", "count_m64_steps", "count_m150", "count_m150_staged", "count_m64_long", "count_m150_long",
              "count_fixed", "count_unif", "locate", "locate_one", "locate_ssa_rows",
              "locate_m64", "locate_m150", "locate_m64_steps", "count_stream", "count_stream_packed",
@@ -220,6 +220,13 @@ def compact_line(res, legs_file=None):
     if loc:
         rl = loc.get("roofline") or loc.get("walk_roofline") or {}
         out["locate"] = _sig({"patterns_per_s": loc.get("patterns_per_s"), "frac": rl.get("frac")})
+    # the index's whole HBM footprint (every allocation of the handle, cs_fm_info.device_bytes)
+    # and the rate at BASELINE configs[3]'s whole 100 M batch in one call
+    if res.get("index_hbm_bytes"):
+        out["index_hbm_bytes"] = res["index_hbm_bytes"]
+    c100 = (res.get("legs") or {}).get("count_100m")
+    if isinstance(c100, dict) and c100.get("patterns_per_s"):
+        out["count_100m_patterns_per_s"] = _sig(c100["patterns_per_s"])
     opt = []  # optional, dropped last-first while the line is too long
     if "gather_verified" in res:
         out["gather_verified"] = res["gather_verified"]
@@ -574,9 +581,26 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
     hb = hit.bool()
     nhit = int(hb.sum().item())
     rw = getattr(info, "locate_record_width", 0) or 16  # 64-B records: read by four lanes
-    rnd = rw * nhit + int(torch.where(hb, 0, qb + 32 * cnt).sum().item())
-    # random reads: one per 16-B record, one per 32-B sector or line, one SA sector per position
-    acc = nhit + int(torch.where(hb, 0, (qb + 31) // 32 + cnt).sum().item())
+    # a position costs one 32-B SA sector (full SA), or over walk lines (no full SA, C5) its
+    # walk: (LF steps + 1) 32-B lines and one sample sector — the steps measured by the walk's
+    # twin (cs_fm_locate_walk_steps_device) over the same rows (round 5: the line charged one
+    # SA sector per position there, 30 M random reads per C5 call instead of 57 M)
+    per_pos = 1.0
+    walk_steps = None
+    if not info.full_sa_bytes and tot:
+        d_sp = torch.empty(B, dtype=torch.int64, device=dev)
+        d_o2 = torch.empty(B + 1, dtype=torch.int64, device=dev)
+        t2 = idx.locate_ranges_device(W.pats.data_ptr(), W.offs.data_ptr(), B, limit, d_sp.data_ptr(),
+                                      d_o2.data_ptr(), sh)
+        stp = torch.empty(max(t2, 1), dtype=torch.int64, device=dev)
+        idx.locate_walk_steps_device(d_sp.data_ptr(), d_o2.data_ptr(), B, t2, stp.data_ptr(), sh)
+        walk_steps = float(stp[:t2].sum().item()) / max(t2, 1)
+        per_pos = walk_steps + 2.0
+        del d_sp, d_o2, stp
+    rnd = rw * nhit + int(torch.where(hb, 0, qb + (32 * per_pos) * cnt).sum().item())
+    # random reads: one per 16-B record, one per 32-B sector or line, per position one SA
+    # sector or the walk's lines and sample
+    acc = nhit + int(torch.where(hb, 0, (qb + 31) // 32 + per_pos * cnt).sum().item())
     # the search's results, written and read back: an 8-B record per pattern and a 4-B count
     # unless the record is the pattern's only position (count 1; round 5)
     mid = 8 * B + 4 * int((cnt != 1).sum().item())
@@ -592,7 +616,7 @@ def locate_one_leg(name, what, idx, info, wl_key, W, text, dev, sh, reps=5, limi
     return {"what": what, "workload_key": wl_key, "patterns": B, "positions": int(tot), "seconds": tl,
             "patterns_per_s": B / tl, "positions_per_s": tot / tl, "limit": limit,
             "event_ms": min(evs) * 1e3, "positions_verified": okv,
-            "locate_record_hit_frac": nhit / B,
+            "locate_record_hit_frac": nhit / B, "walk_lf_steps_per_position": walk_steps,
             "roofline": {"bound": lbound, "achieved": fb / tl / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": fb / tl / 1e9 / HBM_PEAK_GBS, "basis": basis, "alg_bytes_per_launch": alg,
                          "alg_bytes_per_query": alg / B,
@@ -1177,6 +1201,43 @@ def main():
                 r["vs_headline_patterns_per_s"] = r["patterns_per_s"] / (B / kern_avg_s) if kern_avg_s else None
                 lg["count_100m"] = r
                 del WB, ob, wsB, got
+            if "count_streams" in legs:
+                # the headline batch as independent batches issued round-robin over S streams
+                # (a serving loop's pattern), each stream its own workspace and output: K calls
+                # between two synchronisations, wall time per call.  One call's tail (its last
+                # blocks draining, the list kernel) overlaps the next call's head on another
+                # stream (profiles/scripts/stream_probe.py); the headline line itself stays on
+                # one stream, so its per-launch kernel time is the launch's own.
+                ss = [torch.cuda.Stream(device=dev) for _ in range(3)]
+                wss = [torch.zeros(ws_bytes, dtype=torch.uint8, device=dev) for _ in range(3)]
+                oss = [torch.empty(B, dtype=torch.int64, device=dev) for _ in range(3)]
+                K = max(24, args.steps)
+                per = {1: [], 2: [], 3: []}
+
+                def run_s(S):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for i in range(K):
+                        j = i % S
+                        idx.count_device_ws(W.pats.data_ptr(), W.offs.data_ptr(), B, oss[j].data_ptr(),
+                                            wss[j].data_ptr(), ws_bytes, stream=ss[j].cuda_stream)
+                    torch.cuda.synchronize()
+                    return (time.perf_counter() - t0) * 1e3 / K
+
+                for S in per:
+                    run_s(S)
+                for _ in range(3):
+                    for S in per:
+                        per[S].append(run_s(S))
+                same = counts is None or all(np.array_equal(o.cpu().numpy(), counts) for o in oss)
+                lg["count_streams"] = {
+                    "what": "the headline batch as independent batches round-robin over 1 / 2 / 3 streams "
+                            "(own workspace and output each), wall ms per batch, median of 3 rounds",
+                    "patterns": B, "calls": K,
+                    "ms_per_batch": {str(S): statistics.median(v) for S, v in per.items()},
+                    "patterns_per_s": {str(S): B / (statistics.median(v) / 1e3) for S, v in per.items()},
+                    "matches_headline": bool(same)}
+                del ss, wss, oss
             if "count_u32" in legs and N < 2 ** 32:  # uint32 counts need n < 2^32
                 o4 = torch.empty(B, dtype=torch.int32, device=dev)
                 lg["count_u32"], _ = count_leg(

@@ -1203,7 +1203,17 @@ struct OnePass {
   unsigned long long* nwide = nullptr;
   uint64_t wide_cap = 0;
   uint32_t defer = 0;  // locate records: a pattern its record does not answer -> k_locate_list
+  // walk-line indexes (kPos 1 / 2): the positions of patterns with 2..kLocSmall rows, as
+  // (output index, row | adj << 56) pairs for k_locate_walks — one lane per position, so no
+  // emit wave waits on a lane's chain of walks — kLocTile slots per tile (tile t's at
+  // t kLocTile, their number in wcnt[t]: no global counter); past them the emit walks them
+  uint64_t* walks = nullptr;
+  uint32_t* wcnt = nullptr;
 };
+constexpr uint32_t kWalkAdjShift56 = 56;
+// Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
+constexpr uint64_t kLocTile = 2 * kBlk;
+static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns");
 
 // the text position of BWT row `row` by the short walk, and the same for U rows walked in
 // lockstep (their line reads in flight together) — defined with the walks below
@@ -1389,9 +1399,8 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(uint64_t* __restrict__ tile
 }
 
 // the positions of c <= kLocSmall rows — rows r0 + i, or r0 + the set bits of rel (a context
-// window) — minus adj (mod n), to out: SA reads or walks kEmitRows at a time in lockstep, so
-// a lane's rows are in flight together (round 5: one after the other, C5's emit took 360 us
-// per 12.5 M 20-mers, every wave waiting on a lane's chain of walks)
+// window) — minus adj (mod n), to out: SA reads kEmitRows at a time, in flight together
+// (the walk-line forms list their rows instead: emit_walk_lines)
 constexpr int kEmitRows = 4;
 template <int kPos>
 __device__ __forceinline__ void emit_rows(const DevIndex& ix, const NodeTable& T, const OnePass& op,
@@ -1413,19 +1422,156 @@ __device__ __forceinline__ void emit_rows(const DevIndex& ix, const NodeTable& T
         row[u] = r0 + i + u;
       }
     }
-    if constexpr (kPos == 0) {
+    static_assert(kPos == 0, "walk-line indexes list their rows (emit_walk_lines)");
 #pragma unroll
-      for (int u = 0; u < kEmitRows; ++u)
-        if (act[u]) row[u] = load_sa(op.sa, row[u]);
-    } else {
-      bool w[kEmitRows];
-#pragma unroll
-      for (int u = 0; u < kEmitRows; ++u) w[u] = act[u];
-      walk_positions<std::conditional_t<kPos == 1, WalkLine, WalkLineW>, kEmitRows>(ix, T, row, w);
-    }
+    for (int u = 0; u < kEmitRows; ++u)
+      if (act[u]) row[u] = load_sa(op.sa, row[u]);
 #pragma unroll
     for (int u = 0; u < kEmitRows; ++u)
       if (act[u]) st_out(out + i + u, row[u] >= adj ? row[u] - adj : row[u] + n - adj);
+  }
+}
+
+// (3) on walk-line indexes: offsets, the stashed positions, and the rows of every pattern
+// with 2..kLocSmall positions listed for k_locate_walks in the tile's slots (a block scan
+// places them: no atomic) instead of walked here — a lane walking its pattern's positions
+// one after another kept its wave, and the emit, waiting (C5: the emit 360 us per 12.5 M
+// 20-mers; 617 with four walks of a lane in lockstep; 1,156 with one global list counter,
+// 98 k same-address atomics, profiles/r05/r05x, r05y).  A pattern past the tile's kLocTile
+// slots is walked here (its slots below the limit marked void).
+template <int U, int kPos>
+__device__ __forceinline__ void emit_walk_lines(const DevIndex& ix, NodeTable& T, uint64_t npat, uint64_t tile,
+                                                uint64_t q0, const uint64_t* kc, const uint64_t* kr,
+                                                const uint64_t* mine, uint64_t base, const OnePass& op) {
+  using W = std::conditional_t<kPos == 1, WalkLine, WalkLineW>;
+  const uint64_t n = ix.n;
+  uint64_t nl[U], tot = 0;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk, a = base + mine[j], c = kc[j], s = kr[j];
+    nl[j] = 0;
+    if (q >= npat) continue;
+    st_out(op.out_offs + q, a);
+    if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
+    if (loc_stashed(s)) {
+      st_out(op.out_pos + a, s & (kLocStash - 1));
+    } else if ((s & kLocCtx) || c <= kLocSmall) {
+      nl[j] = c;
+    } else {
+      const unsigned long long e = atomicAdd(op.nwide, 1ull);
+      if (e < op.wide_cap) {
+        op.wide[2 * e] = q;
+        op.wide[2 * e + 1] = s;
+      }
+    }
+    tot += nl[j];
+  }
+  // the lane's place among the tile's listed rows
+  uint64_t at, all;
+  block_scan<1>(&tot, &at, all);
+  if (threadIdx.x == 0) op.wcnt[tile] = (uint32_t)(all < kLocTile ? all : kLocTile);
+  uint64_t* const slots = op.walks + 2 * tile * kLocTile;
+  uint32_t fb = 0;  // patterns walked here (past the tile's slots)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (!nl[j]) continue;
+    const uint64_t a = base + mine[j], s = kr[j], c = nl[j];
+    const bool fits = at + c <= kLocTile;
+    fb |= (uint32_t)!fits << j;
+    uint64_t r0 = s, adj = 0;
+    uint32_t rel = 0;
+    if (s & kLocCtx) loc_window(s, r0, adj, rel);
+    for (uint64_t i = 0; i < c; ++i, ++at) {
+      uint64_t row = r0 + i;
+      if (rel) {
+        row = r0 + (uint32_t)__ffs(rel) - 1u;
+        rel &= rel - 1u;
+      }
+      if (at >= kLocTile) continue;
+      slots[2 * at] = fits ? a + i : ~0ull;  // (a void slot: k_locate_walks skips it)
+      slots[2 * at + 1] = row | (adj << kWalkAdjShift56);
+    }
+  }
+  if (__syncthreads_or(fb != 0)) {
+    load_table(T, ix.table);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (!((fb >> j) & 1u)) continue;
+      const uint64_t a = base + mine[j], s = kr[j];
+      uint64_t r0 = s, adj = 0;
+      uint32_t rel = 0;
+      if (s & kLocCtx) loc_window(s, r0, adj, rel);
+      for (uint64_t i = 0; i < nl[j]; ++i) {
+        uint64_t row = r0 + i;
+        if (rel) {
+          row = r0 + (uint32_t)__ffs(rel) - 1u;
+          rel &= rel - 1u;
+        }
+        const uint64_t p = walk_position<W>(ix, T, row);
+        st_out(op.out_pos + a + i, p >= adj ? p - adj : p + n - adj);
+      }
+    }
+  }
+}
+
+// (3') the listed walks (emit_walk_lines): block b takes tiles b, b + grid, ... (one per
+// thread: the grid is at least tiles / kBlk), their slots flattened, two per lane in lockstep
+template <int kPos>
+__global__ __launch_bounds__(kBlk) void k_locate_walks(DevIndex ix, OnePass op, uint64_t ntiles) {
+  using W = std::conditional_t<kPos == 1, WalkLine, WalkLineW>;
+  __shared__ NodeTable T;
+  __shared__ uint32_t s_off[kBlk + 1];
+  __shared__ uint32_t s_w[kBlk / 64];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t mt = blockIdx.x + (uint64_t)threadIdx.x * gridDim.x;
+  const uint32_t c = mt < ntiles ? op.wcnt[mt] : 0u;
+  uint32_t x = c;  // exclusive scan of the tiles' counts over the block
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < (int)(kBlk / 64); ++w2) {
+    if (w2 < (int)wv) pre += s_w[w2];
+    tot += s_w[w2];
+  }
+  s_off[threadIdx.x] = pre + x - c;
+  if (threadIdx.x == 0) s_off[kBlk] = tot;
+  if (tot == 0) return;  // uniform: nothing listed in the block's tiles
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t n = ix.n;
+  for (uint32_t e0 = 0; e0 < tot; e0 += 2 * kBlk) {
+    uint64_t row[2], adj[2], idx[2];
+    bool act[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t ee = e0 + threadIdx.x + h * kBlk;
+      const uint32_t e = ee < tot ? ee : 0u;
+      uint32_t lo = 0, hi = kBlk;  // s_off[lo] <= e < s_off[hi] (empty tiles share offsets)
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (s_off[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const uint64_t* sl = op.walks + 2 * ((blockIdx.x + (uint64_t)lo * gridDim.x) * kLocTile + (e - s_off[lo]));
+      idx[h] = ee < tot ? sl[0] : ~0ull;
+      const uint64_t v = ee < tot ? sl[1] : 0;
+      act[h] = idx[h] != ~0ull;
+      row[h] = v & ((1ull << kWalkAdjShift56) - 1);
+      adj[h] = v >> kWalkAdjShift56;
+    }
+    bool w[2] = {act[0], act[1]};
+    walk_positions<W, 2>(ix, T, row, w);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (act[h]) st_out(op.out_pos + idx[h], row[h] >= adj[h] ? row[h] - adj[h] : row[h] + n - adj[h]);
   }
 }
 
@@ -1438,12 +1584,10 @@ __device__ __forceinline__ void emit_rows(const DevIndex& ix, const NodeTable& T
 // neighbouring blocks, the search 426 -> 615 us.)
 template <int U, int kPos = 0>
 __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat, OnePass op) {
-  __shared__ NodeTable T;  // kPos: the walks' C[] and codes
-  const uint64_t n = ix.n;
+  __shared__ NodeTable T;  // kPos: the walks' C[] and codes (a pattern past walk_cap)
   const uint64_t tile = blockIdx.x;
   const uint64_t q0 = tile * (uint64_t)(kBlk * U) + threadIdx.x;
   uint64_t kc[U], kr[U], mine[U], agg;
-  bool walk = false;  // a position to walk here (not stashed by (1))
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
@@ -1452,38 +1596,36 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
     kr[j] = q < npat ? __builtin_nontemporal_load(op.rec + q) : 0;
     kc[j] = q >= npat ? 0 : loc_stashed(kr[j]) ? 1
           : (op.cnt64 ? __builtin_nontemporal_load(op.cnt64 + q) : __builtin_nontemporal_load(op.cnt + q));
-    walk |= kc[j] && !loc_stashed(kr[j]);
   }
   if constexpr (kPos != 0) {
-    if (__syncthreads_or(walk)) {
-      load_table(T, ix.table);
-      __syncthreads();
-    }
-  }
-  block_scan<U>(kc, mine, agg);
-  const uint64_t base = op.tiles[tile];
+    block_scan<U>(kc, mine, agg);
+    emit_walk_lines<U, kPos>(ix, T, npat, tile, q0, kc, kr, mine, op.tiles[tile], op);
+  } else {
+    block_scan<U>(kc, mine, agg);
+    const uint64_t base = op.tiles[tile];
 #pragma unroll
-  for (int j = 0; j < U; ++j) {
-    const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if (q >= npat) continue;
-    const uint64_t a = base + mine[j], c = kc[j];
-    st_out(op.out_offs + q, a);
-    if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
-    const uint64_t s = kr[j];
-    if (loc_stashed(s)) {  // kLocStash: the one position, read by the search kernel
-      st_out(op.out_pos + a, s & (kLocStash - 1));
-    } else if (s & kLocCtx) {  // a window k characters before the end (k_locate_sa)
-      uint64_t r0, adj;
-      uint32_t rel;
-      loc_window(s, r0, adj, rel);
-      emit_rows<kPos>(ix, T, op, op.out_pos + a, c, r0, rel, adj);
-    } else if (c <= kLocSmall) {
-      emit_rows<kPos>(ix, T, op, op.out_pos + a, c, s, 0u, 0);
-    } else {
-      const unsigned long long e = atomicAdd(op.nwide, 1ull);
-      if (e < op.wide_cap) {
-        op.wide[2 * e] = q;
-        op.wide[2 * e + 1] = s;
+    for (int j = 0; j < U; ++j) {
+      const uint64_t q = q0 + (uint64_t)j * kBlk;
+      if (q >= npat) continue;
+      const uint64_t a = base + mine[j], c = kc[j];
+      st_out(op.out_offs + q, a);
+      if (!c || a + c > op.cap) continue;  // capacity short: the caller sees the total
+      const uint64_t s = kr[j];
+      if (loc_stashed(s)) {  // kLocStash: the one position, read by the search kernel
+        st_out(op.out_pos + a, s & (kLocStash - 1));
+      } else if (s & kLocCtx) {  // a window k characters before the end (k_locate_sa)
+        uint64_t r0, adj;
+        uint32_t rel;
+        loc_window(s, r0, adj, rel);
+        emit_rows<kPos>(ix, T, op, op.out_pos + a, c, r0, rel, adj);
+      } else if (c <= kLocSmall) {
+        emit_rows<kPos>(ix, T, op, op.out_pos + a, c, s, 0u, 0);
+      } else {
+        const unsigned long long e = atomicAdd(op.nwide, 1ull);
+        if (e < op.wide_cap) {
+          op.wide[2 * e] = q;
+          op.wide[2 * e + 1] = s;
+        }
       }
     }
   }
@@ -1593,7 +1735,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // registers the routed kernel spilled 7 VGPRs instead of 3)
   __shared__ uint32_t s_chn[kLoc ? 1 : U][kLoc ? 1 : kBlk];
   static_assert(kBlk >= 256, "one map entry per thread");
-  static_assert(!kOne || kLoc, "the one-call search is a locate form");
+  static_assert(!kOne || (kLoc && (!kNoBar || kPos == 0)), "the one-call walks read the node table from LDS");
   static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
@@ -1978,15 +2120,17 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3 || st[j] == 5;
   if constexpr (kOne && kNoBar) {
-    // the barrier-free one-call search: the general search and the walks (kPos 1 / 2) read
-    // the node table through the caches, the tile total is added wave by wave
-    // (locate_split_store)
+    // the barrier-free one-call search (kPos 0): the general search reads the node table
+    // through the caches, the tile total is added wave by wave (locate_split_store).  (Round 5
+    // measured the walk forms without the barrier too, the walks' C[] and codes read through
+    // the caches: C5's search 1.56 -> 1.70 ms — a walk step then waits on two more dependent
+    // loads — so they keep the LDS table.)
     if (general)
       general_rest<E, U, kLoc, kPacked, W, true>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec, kc, kr);
     uint32_t skip = 0;  // the patterns left to k_locate_long (4) and k_locate_list (7)
 #pragma unroll
     for (int j = 0; j < U; ++j) skip |= (uint32_t)(st[j] == 4 || st[j] == 7) << j;
-    locate_split_store<U, kPos, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
+    locate_split_store<U, 0, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
     return;
   } else if constexpr (kNoBar) {
     if (general)
@@ -2738,9 +2882,6 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
   }
 }
 
-// Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
-constexpr uint64_t kLocTile = 2 * kBlk;
-static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns");
 
 // Adds each lane's kc (0: nothing) to op.tiles[tile]: one atomic per distinct tile of the
 // wave (a list launch's wave holds one or two slots' patterns, so one or two tiles; a
@@ -4946,10 +5087,16 @@ cs_status launch_locrec_hits(const cs_fm_index* h, const uint8_t* d_pats, const 
 // The call's buffers (the lists, then per pattern its count and record, the tiles, the wide
 // ranges) in the caller's workspace when it holds locate_workspace_bytes(npat), else in one
 // stream-ordered allocation.
+// (+ on walk-line indexes the walk list: kLocTile (output index, row) pairs per tile and the
+// tiles' counts)
+uint64_t locate_walk_bytes(const cs_fm_index* h, uint64_t npat) {
+  const uint64_t tiles = (npat + kLocTile - 1) / kLocTile;
+  return h->d_sa ? 0 : ((tiles * 4 + 7) & ~7ull) + tiles * kLocTile * 16;
+}
 uint64_t locate_lo_bytes(const cs_fm_index* h, uint64_t npat, uint64_t wide_cap) {
   const uint64_t tiles = (npat + kLocTile - 1) / kLocTile;
   const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
-  return (npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull;
+  return ((npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull) + locate_walk_bytes(h, npat);
 }
 uint64_t locate_workspace_bytes(const cs_fm_index* h, uint64_t npat) {
   return LongBufs::bytes(npat, false) + locate_lo_bytes(h, npat, npat);
@@ -5025,6 +5172,12 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide = reinterpret_cast<uint64_t*>(op.nwide + 1);
   if (h->wide) op.cnt64 = op.wide + 2 * wide_cap;
   else op.cnt = reinterpret_cast<uint32_t*>(op.wide + 2 * wide_cap);
+  if (kpos != 0) {  // after the counts (8-B aligned), the tiles' walk counts and slots
+    const uint64_t cb = h->wide ? 8 : 4;
+    uint8_t* w = reinterpret_cast<uint8_t*>(op.wide + 2 * wide_cap) + ((npat * cb + 7) & ~7ull);
+    op.wcnt = reinterpret_cast<uint32_t*>(w);
+    op.walks = reinterpret_cast<uint64_t*>(w + ((tiles * 4 + 7) & ~7ull));
+  }
   op.sa = static_cast<const uint32_t*>(h->d_sa);
   op.out_offs = d_out_offs;
   op.out_pos = d_out_pos;
@@ -5032,9 +5185,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide_cap = wide_cap;
   // the search kernel's blocks zero their tiles (and block 0 the wide-range counter); a
   // CS_Q_LONG call, which runs no search kernel, zeroes them here
-  // (round 5: the walk forms too — C5's search over walk lines no longer waits at a block
-  // barrier for a 10.8-KB node-table copy before its walks)
-  const bool nobar = count_nobar(flags);
+  const bool nobar = kpos == 0 && count_nobar(flags);
   if (long_only)
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
@@ -5080,19 +5231,15 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
-  else if (kpos == 1 && nobar)
-    k_count_ctx<OccE, U, true, false, 8, true, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else if (kpos == 1)
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
-        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
-  else if (nobar)
-    k_count_ctx<OccE, U, true, false, 8, true, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   FMX_HIP(hipGetLastError());
+  // (k_locate_walks: 4 blocks per CU, and one tile per thread)
+  const unsigned walk_grid = (unsigned)std::max<uint64_t>(list_blocks_per_device(), (tiles + kBlk - 1) / kBlk);
   k_scan_tiles<<<1, 1024, 0, st>>>(op.tiles, tiles, d_out_offs + npat);
   FMX_HIP(hipGetLastError());
   if (kpos == 0) {
@@ -5100,9 +5247,11 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
     k_locate_emit_wide<0><<<1024, kBlk, 0, st>>>(ix, op, d_out_offs, d_out_pos);
   } else if (kpos == 1) {
     k_locate_emit<U, 1><<<(unsigned)tiles, kBlk, 0, st>>>(ix, npat, op);
+    k_locate_walks<1><<<walk_grid, kBlk, 0, st>>>(ix, op, tiles);
     k_locate_emit_wide<1><<<1024, kBlk, 0, st>>>(ix, op, d_out_offs, d_out_pos);
   } else {
     k_locate_emit<U, 2><<<(unsigned)tiles, kBlk, 0, st>>>(ix, npat, op);
+    k_locate_walks<2><<<walk_grid, kBlk, 0, st>>>(ix, op, tiles);
     k_locate_emit_wide<2><<<1024, kBlk, 0, st>>>(ix, op, d_out_offs, d_out_pos);
   }
   FMX_HIP(hipGetLastError());

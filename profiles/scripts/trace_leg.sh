@@ -10,5 +10,5 @@ cd /tmp && export TMPDIR=/tmp
 env "$@" true
 for kv in "$@"; do export "$kv"; done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$LEG -o run -- \
-  python3 $R/bench.py --only $LEG --steps 20 --warmup 3 > $O/$LEG.json 2> $O/$LEG.err || exit 1
+  python3 $R/bench.py --only $LEG --steps 20 --warmup 3 ${TRACE_ARGS:-} > $O/$LEG.json 2> $O/$LEG.err || exit 1
 python3 $R/profiles/scripts/trace_kernels.py $O/trace_$LEG
