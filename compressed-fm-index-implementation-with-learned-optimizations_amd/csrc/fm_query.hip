@@ -1222,6 +1222,27 @@ __device__ __forceinline__ uint64_t walk_position(const DevIndex& ix, const Node
 template <class W, int U>
 __device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTable& T, uint64_t* pos,
                                                bool* act);
+// the constants an LF step of a walk reads from the node table, held in registers by a
+// barrier-free kernel whose table is the global one (a walk step through the caches waits on
+// two more dependent loads: round 5, C5's one-call search 1.56 -> 1.70 ms that way)
+struct WalkK {
+  uint64_t C[4];     // C[] of each occurrence code's symbol
+  uint32_t nexc;     // rare rows
+  uint64_t exc_row0; // the rare row when there is one (C5's terminator), and C[] of its symbol
+  uint64_t exc_c0;
+};
+__device__ __forceinline__ WalkK walk_consts(const NodeTable& T) {
+  WalkK k;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) k.C[c] = T.C[T.occ_sym[c]];
+  k.nexc = T.exc_n;
+  k.exc_row0 = k.nexc ? T.exc_row[0] : 0;
+  k.exc_c0 = k.nexc ? T.C[T.exc_sym[0]] : 0;
+  return k;
+}
+template <class W, int U>
+__device__ __forceinline__ void walk_positions_k(const DevIndex& ix, const NodeTable& T, const WalkK& K,
+                                                 uint64_t* pos, bool* act);
 
 // position of BWT row `row` for the one-call locate: SA[row] (kPos 0) or the short walk
 template <int kPos>
@@ -1319,7 +1340,10 @@ __device__ __forceinline__ void locate_split_store(const DevIndex& ix, const Nod
     bool act[U];
 #pragma unroll
     for (int j = 0; j < U; ++j) act[j] = one[j];
-    walk_positions<std::conditional_t<kPos == 1, WalkLine, WalkLineW>, U>(ix, T, row, act);
+    if constexpr (kWaveTile)  // (T is the global table: the walks' constants in registers)
+      walk_positions_k<std::conditional_t<kPos == 1, WalkLine, WalkLineW>, U>(ix, T, walk_consts(T), row, act);
+    else
+      walk_positions<std::conditional_t<kPos == 1, WalkLine, WalkLineW>, U>(ix, T, row, act);
   }
 #pragma unroll
   for (int j = 0; j < U; ++j)
@@ -1735,7 +1759,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // registers the routed kernel spilled 7 VGPRs instead of 3)
   __shared__ uint32_t s_chn[kLoc ? 1 : U][kLoc ? 1 : kBlk];
   static_assert(kBlk >= 256, "one map entry per thread");
-  static_assert(!kOne || (kLoc && (!kNoBar || kPos == 0)), "the one-call walks read the node table from LDS");
+  static_assert(!kOne || kLoc, "the one-call search is a locate form");
   static_assert(!kSkipLong || U * kBlk == kLongRegion, "a block's waves list one region's slots");
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
@@ -2120,17 +2144,15 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3 || st[j] == 5;
   if constexpr (kOne && kNoBar) {
-    // the barrier-free one-call search (kPos 0): the general search reads the node table
-    // through the caches, the tile total is added wave by wave (locate_split_store).  (Round 5
-    // measured the walk forms without the barrier too, the walks' C[] and codes read through
-    // the caches: C5's search 1.56 -> 1.70 ms — a walk step then waits on two more dependent
-    // loads — so they keep the LDS table.)
+    // the barrier-free one-call search: the general search reads the node table through the
+    // caches, the walks (kPos 1 / 2) take the few constants a step needs in registers
+    // (WalkK), the tile total is added wave by wave (locate_split_store)
     if (general)
       general_rest<E, U, kLoc, kPacked, W, true>(ix, *ix.table, pats, st, o0, m, q0, co, limit, rec, kc, kr);
     uint32_t skip = 0;  // the patterns left to k_locate_long (4) and k_locate_list (7)
 #pragma unroll
     for (int j = 0; j < U; ++j) skip |= (uint32_t)(st[j] == 4 || st[j] == 7) << j;
-    locate_split_store<U, 0, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
+    locate_split_store<U, kPos, true>(ix, *ix.table, npat, blockIdx.x, q0, kc, kr, op, skip);
     return;
   } else if constexpr (kNoBar) {
     if (general)
@@ -3803,6 +3825,73 @@ __device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTab
   }
 }
 
+// walk_lf over the occurrence-line walk lines with the step's constants in registers (K);
+// more than one rare row takes the table (through the caches) as walk_lf does
+template <class W>
+__device__ __forceinline__ uint64_t walk_lf_k(const NodeTable& T, const WalkK& K, const typename W::Raw& v,
+                                              uint64_t q, uint32_t o, uint64_t pos) {
+  const uint32_t code = W::code(v, o);
+  uint64_t r = W::occ(v, code, q, o);
+  const uint64_t cc = code == 0 ? K.C[0] : code == 1 ? K.C[1] : code == 2 ? K.C[2] : K.C[3];
+  if (code == 0 && K.nexc) {
+    if (K.nexc == 1) {
+      if (pos == K.exc_row0) return K.exc_c0;  // the rare row: no earlier row holds its symbol
+      r -= K.exc_row0 < pos ? 1u : 0u;
+    } else {
+      const uint32_t e = exc_before(T, pos);
+      if (e < T.exc_n && T.exc_row[e] == pos) {
+        const uint32_t c = T.exc_sym[e];
+        return T.C[c] + exc_rank(T, c, pos);
+      }
+      r -= e;
+    }
+  }
+  return cc + r;
+}
+
+template <class W, int U>
+__device__ __forceinline__ void walk_positions_k(const DevIndex& ix, const NodeTable& T, const WalkK& K,
+                                                 uint64_t* pos, bool* act) {
+  const uint64_t n = ix.n;
+  const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
+  uint64_t steps[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) steps[j] = 0;
+  for (uint64_t it = 0; it < n; ++it) {
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) any |= act[j];
+    if (!any) return;
+    uint64_t q[U];
+    uint32_t o[U];
+    typename W::Raw v[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {  // the lines of every active walk first
+      q[j] = 0, o[j] = 0;
+      if (act[j]) {
+        W::locate(pos[j], q[j], o[j]);
+        W::load(ix.walk, q[j], v[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (!act[j]) continue;
+      const bool mk = W::mark(v[j], o[j]);
+      const bool rs = row_mask ? (pos[j] & row_mask) == 0 : pos[j] % ix.stride == 0;
+      if (mk || rs) {  // fm_index.cpp:147-153
+        const uint64_t sidx = mk ? W::mark_rank(v[j], o[j])
+                                 : (row_mask ? pos[j] >> ix.stride_shift : pos[j] / ix.stride);
+        const uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps[j];
+        pos[j] = s >= n ? s - n : s;
+        act[j] = false;
+      } else {
+        pos[j] = walk_lf_k<W>(T, K, v[j], q[j], o[j], pos[j]);
+        ++steps[j];
+      }
+    }
+  }
+}
+
 template <class W, bool kQ>
 __global__ __launch_bounds__(kBlk) void k_walk_short(DevIndex ix, const uint64_t* __restrict__ rows,
                                                      uint64_t total, uint64_t* __restrict__ out,
@@ -5185,7 +5274,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide_cap = wide_cap;
   // the search kernel's blocks zero their tiles (and block 0 the wide-range counter); a
   // CS_Q_LONG call, which runs no search kernel, zeroes them here
-  const bool nobar = kpos == 0 && count_nobar(flags);
+  const bool nobar = count_nobar(flags);
   if (long_only)
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
@@ -5231,8 +5320,14 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   else if (kpos == 0)
     k_count_ctx<OccE, U, true, false, 8, false, true><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else if (kpos == 1 && nobar)
+    k_count_ctx<OccE, U, true, false, 8, true, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else if (kpos == 1)
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 1><<<(unsigned)tiles, kBlk, 0, st>>>(
+        ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
+  else if (nobar)
+    k_count_ctx<OccE, U, true, false, 8, true, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(
         ix, d_pats, d_offs, npat, co, limit, nullptr, 0, op);
   else
     k_count_ctx<OccE, U, true, false, 8, false, true, false, true, 2><<<(unsigned)tiles, kBlk, 0, st>>>(
