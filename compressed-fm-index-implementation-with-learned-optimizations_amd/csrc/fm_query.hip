@@ -1209,7 +1209,12 @@ struct OnePass {
   // t kLocTile, their number in wcnt[t]: no global counter); past them the emit walks them
   uint64_t* walks = nullptr;
   uint32_t* wcnt = nullptr;
+  // k_scan_chained: per scan block its published total (bit 63: ready), zeroed by the search
+  // kernel's block 0 (or a memset where no search kernel runs)
+  unsigned long long* sflags = nullptr;
 };
+constexpr uint32_t kScanBlock = 1024;     // tiles per block of k_scan_chained
+constexpr uint32_t kScanMaxBlocks = 1024; // (its look-back: one predecessor per thread)
 constexpr uint32_t kWalkAdjShift56 = 56;
 // Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
 constexpr uint64_t kLocTile = 2 * kBlk;
@@ -1454,6 +1459,54 @@ __device__ __forceinline__ void emit_rows(const DevIndex& ix, const NodeTable& T
     for (int u = 0; u < kEmitRows; ++u)
       if (act[u]) st_out(out + i + u, row[u] >= adj ? row[u] - adj : row[u] + n - adj);
   }
+}
+
+// (2'): the same scan over ceil(ntiles / 1024) blocks of 1024 tiles (one per thread): each
+// block publishes its total (one flag word), sums its predecessors' — every thread polls one
+// of them — and writes its tiles' exclusive prefixes; the last block writes the total.  The
+// blocks wait only on lower ones, which are dispatched first.  (Round 5: the one-block scan
+// took 18 us of C4's 0.53-ms one-call locate, its 24 k tiles passing through one CU.)
+__global__ __launch_bounds__(kScanBlock) void k_scan_chained(uint64_t* __restrict__ tiles, uint64_t ntiles,
+                                                             uint64_t* __restrict__ total_out,
+                                                             unsigned long long* __restrict__ sflags) {
+  __shared__ uint64_t s_w[kScanBlock / 64];
+  __shared__ uint64_t s_p[kScanBlock / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint64_t i = (uint64_t)blockIdx.x * kScanBlock + t;
+  const uint64_t v = i < ntiles ? tiles[i] : 0ull;
+  uint64_t x = v;  // inclusive scan over the wave, then the block
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  uint64_t pre = 0, agg = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < (int)(kScanBlock / 64); ++w2) {
+    if (w2 < (int)wv) pre += s_w[w2];
+    agg += s_w[w2];
+  }
+  if (t == 0)
+    __hip_atomic_store(sflags + blockIdx.x, (1ull << 63) | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t p = 0;  // predecessor t's total
+  if (t < blockIdx.x) {
+    unsigned long long f;
+    do {
+      f = __hip_atomic_load(sflags + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    } while (!(f >> 63));
+    p = f & ~(1ull << 63);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) p += __shfl_xor(p, d, 64);
+  if (lane == 0) s_p[wv] = p;
+  __syncthreads();
+  uint64_t base = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < (int)(kScanBlock / 64); ++w2) base += s_p[w2];
+  if (i < ntiles) tiles[i] = base + pre + x - v;
+  if (blockIdx.x == gridDim.x - 1 && t == 0) *total_out = base + agg;
 }
 
 // (3) on walk-line indexes: offsets, the stashed positions, and the rows of every pattern
@@ -1769,6 +1822,7 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     // atomics land) before this wave reaches the barrier.
     op.tiles[blockIdx.x] = 0;
     if (blockIdx.x == 0) *op.nwide = 0;
+    if (op.sflags && blockIdx.x < kScanMaxBlocks) op.sflags[blockIdx.x] = 0;
     __builtin_amdgcn_s_waitcnt(0);
   }
   __syncthreads();
@@ -5185,7 +5239,8 @@ uint64_t locate_walk_bytes(const cs_fm_index* h, uint64_t npat) {
 uint64_t locate_lo_bytes(const cs_fm_index* h, uint64_t npat, uint64_t wide_cap) {
   const uint64_t tiles = (npat + kLocTile - 1) / kLocTile;
   const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
-  return ((npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull) + locate_walk_bytes(h, npat);
+  return ((npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull) + locate_walk_bytes(h, npat) +
+         kScanMaxBlocks * 8;
 }
 uint64_t locate_workspace_bytes(const cs_fm_index* h, uint64_t npat) {
   return LongBufs::bytes(npat, false) + locate_lo_bytes(h, npat, npat);
@@ -5261,11 +5316,16 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   op.wide = reinterpret_cast<uint64_t*>(op.nwide + 1);
   if (h->wide) op.cnt64 = op.wide + 2 * wide_cap;
   else op.cnt = reinterpret_cast<uint32_t*>(op.wide + 2 * wide_cap);
-  if (kpos != 0) {  // after the counts (8-B aligned), the tiles' walk counts and slots
+  {
+    // after the counts (8-B aligned): on walk-line indexes the tiles' walk counts and slots,
+    // then the chained scan's flags
     const uint64_t cb = h->wide ? 8 : 4;
     uint8_t* w = reinterpret_cast<uint8_t*>(op.wide + 2 * wide_cap) + ((npat * cb + 7) & ~7ull);
-    op.wcnt = reinterpret_cast<uint32_t*>(w);
-    op.walks = reinterpret_cast<uint64_t*>(w + ((tiles * 4 + 7) & ~7ull));
+    if (kpos != 0) {
+      op.wcnt = reinterpret_cast<uint32_t*>(w);
+      op.walks = reinterpret_cast<uint64_t*>(w + ((tiles * 4 + 7) & ~7ull));
+    }
+    op.sflags = reinterpret_cast<unsigned long long*>(w + locate_walk_bytes(h, npat));
   }
   op.sa = static_cast<const uint32_t*>(h->d_sa);
   op.out_offs = d_out_offs;
@@ -5275,8 +5335,10 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // the search kernel's blocks zero their tiles (and block 0 the wide-range counter); a
   // CS_Q_LONG call, which runs no search kernel, zeroes them here
   const bool nobar = count_nobar(flags);
-  if (long_only)
+  if (long_only) {
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
+    FMX_HIP(hipMemsetAsync(op.sflags, 0, kScanMaxBlocks * 8, st));
+  }
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
   op.defer = defer ? 1u : 0u;
   if (long_only || routed || defer) {
@@ -5335,7 +5397,12 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   FMX_HIP(hipGetLastError());
   // (k_locate_walks: 4 blocks per CU, and one tile per thread)
   const unsigned walk_grid = (unsigned)std::max<uint64_t>(list_blocks_per_device(), (tiles + kBlk - 1) / kBlk);
-  k_scan_tiles<<<1, 1024, 0, st>>>(op.tiles, tiles, d_out_offs + npat);
+  // the chained scan (a block per 1024 tiles) while its look-back fits a block, else one block
+  const uint64_t sblocks = (tiles + kScanBlock - 1) / kScanBlock;
+  if (sblocks <= kScanMaxBlocks)
+    k_scan_chained<<<(unsigned)sblocks, kScanBlock, 0, st>>>(op.tiles, tiles, d_out_offs + npat, op.sflags);
+  else
+    k_scan_tiles<<<1, 1024, 0, st>>>(op.tiles, tiles, d_out_offs + npat);
   FMX_HIP(hipGetLastError());
   if (kpos == 0) {
     k_locate_emit<U, 0><<<(unsigned)tiles, kBlk, 0, st>>>(ix, npat, op);
