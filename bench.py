@@ -323,10 +323,16 @@ class Workload:
         K = 0 if flags & 1 else info.prefix_k
         frac = 0.0
         if K and m >= K:
+            # (in chunks of 4 M patterns: the int64 temporaries of a 100 M batch would take
+            # 28 GB beside C5's 237-GB index)
             code = torch.tensor(list(info.prefix_code), dtype=torch.int64, device=dev)
-            P2 = self.pats.view(B, m).long()
-            frac = float((code[P2[:, m - K:]] != 255).all(dim=1).float().mean().item())
-            del P2
+            P = self.pats.view(B, m)
+            hit = 0
+            for a0 in range(0, B, 1 << 22):
+                P2 = P[a0:a0 + (1 << 22), m - K:].long()
+                hit += int((code[P2] != 255).all(dim=1).sum().item())
+                del P2
+            frac = hit / B
         eb = info.prefix_bytes // (info.prefix_sigma ** K) if K else 0
         hits = int(round(B * frac)) if K else 0
         acc = (rnd - eb * hits) / info.line_bytes + hits
@@ -1490,10 +1496,23 @@ def main():
                 Q = threads if wide else max(256 if N <= 200_000_000 else 32 if N <= 2_000_000_000 else 16,
                                              2 * threads)
             t1 = time.perf_counter()
-            d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
+            host_text = None
+            try:
+                d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
+            except torch.OutOfMemoryError:
+                # (C5: the 237-GB index, the 32-GB text and a 32-GB BWT do not fit together —
+                # the text waits in host memory while the BWT comes out)
+                host_text = text.cpu()
+                del text
+                torch.cuda.empty_cache()
+                d_bwt = torch.empty(N, dtype=torch.uint8, device=dev)
             idx.bwt_device(d_bwt.data_ptr(), sh)
             bwt = d_bwt.cpu().numpy()
             del d_bwt
+            if host_text is not None:
+                torch.cuda.empty_cache()
+                text = host_text.to(dev)
+                del host_text
             ref = O.Index(bwt=bwt, nthreads=threads)
             prep_s = time.perf_counter() - t1
             sample = W.pats[: Q * m].cpu().numpy()

@@ -1087,31 +1087,6 @@ __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats,
   for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
 }
 
-// load_pattern32 from at most three 16-B aligned vectors (the word selects are arithmetic:
-// a select between array elements becomes a dynamically indexed array, which the compiler
-// moves to LDS).  A vector holding a byte of the batch lies inside its allocation.
-__device__ __forceinline__ void load_pattern32_v16(const uint8_t* __restrict__ pats, uint64_t o0,
-                                                   uint32_t m, uint32_t u[8]) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(pats + o0);
-  const uint4* pv = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
-  const uint32_t ps = (uint32_t)(a & 15), end = ps + m;  // bytes [ps, end) of the vectors
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  const uint4 v0 = pv[0], v1 = end > 16 ? pv[1] : z, v2 = end > 32 ? pv[2] : z;
-  const uint64_t e0 = ((uint64_t)v0.y << 32) | v0.x, e1 = ((uint64_t)v0.w << 32) | v0.z;
-  const uint64_t e2 = ((uint64_t)v1.y << 32) | v1.x, e3 = ((uint64_t)v1.w << 32) | v1.z;
-  const uint64_t e4 = ((uint64_t)v2.y << 32) | v2.x, e5 = ((uint64_t)v2.w << 32) | v2.z;
-  const uint64_t sel = ps >= 8 ? ~0ull : 0ull, sh = ps & 7;
-  const uint64_t a0 = text8(e0, e1, sh), a1 = text8(e1, e2, sh), a2 = text8(e2, e3, sh);
-  const uint64_t a3 = text8(e3, e4, sh), a4 = text8(e4, e5, sh);
-  const uint64_t o[4] = {a0 ^ ((a0 ^ a1) & sel), a1 ^ ((a1 ^ a2) & sel), a2 ^ ((a2 ^ a3) & sel),
-                         a3 ^ ((a3 ^ a4) & sel)};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    u[2 * j] = (uint32_t)o[j];
-    u[2 * j + 1] = (uint32_t)(o[j] >> 32);
-  }
-}
-
 // the patterns of a k_count_ctx lane that need the general search (st == 3); kOne: the
 // locate results stay in the lane's registers (kc, kr)
 // rng: k_count_ctx's s_rng ([U][kBlk][2]): the range after the table of a pattern with st 5
@@ -2483,8 +2458,7 @@ __device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __
   // (A)
   {
     uint32_t u[8];
-    if constexpr (kV16 == 1) load_pattern32_v16(pats, o0 + m - 32, 32, u);
-    else load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
+    load_pattern32(pats, o0 + m - 32, 32, u);  // tail byte i = P[m - 32 + i]
     if constexpr (kPT) {  // P[0, min(k, 160)) coded
       if constexpr (kV16 >= 2) fast &= pack_pattern16(P, k, cmap, pc);
       else fast &= pack_pattern(P, 0, k, cmap, pc);

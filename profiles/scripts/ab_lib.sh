@@ -11,6 +11,7 @@ TAG=$1
 shift
 OUT=$ROOT/gpurun_out/ab_lib_$TAG.jsonl
 : > "$OUT"
+cp "$PKG/libcs_fmindex.so" "$PKG/libcs_fmindex_ab_saved.so"  # (restored at the end)
 for round in $(seq 1 ${AB_ROUNDS:-2}); do
   for V in "$@"; do
     cp "$PKG/libcs_fmindex_$V.so" "$PKG/libcs_fmindex.so"
@@ -19,4 +20,4 @@ for round in $(seq 1 ${AB_ROUNDS:-2}); do
     echo "{\"variant\": \"$V\", \"round\": $round, \"result\": $R}" >> "$OUT"
   done
 done
-cp "$PKG/libcs_fmindex_base.so" "$PKG/libcs_fmindex.so"
+cp "$PKG/libcs_fmindex_ab_saved.so" "$PKG/libcs_fmindex.so"
