@@ -17,7 +17,7 @@ shift 2
 OUT=$ROOT/gpurun_out/prof_legs_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-KRE="k_count|k_walk|k_locate|k_expand"
+KRE="k_count|k_walk|k_locate|k_expand|k_scan"
 for LEG in ${LEGS//,/ }; do
   D=$OUT/$LEG
   mkdir -p "$D"

@@ -25,7 +25,7 @@ import statistics
 import sys
 
 ONE_CALL = ("k_count_ctx_onepass", "k_count_ctx_onepass_skiplong", "k_locate_long", "k_locate_list",
-            "k_locate_emit", "k_locate_emit_wide")
+            "k_locate_emit", "k_locate_emit_wide", "k_locate_walks", "k_scan_chained", "k_scan_tiles")
 # the kernel that carries each leg's work
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
               "count_table_steps": "count", "count_lf_loop": "count", "count_m32": "count",
@@ -87,7 +87,8 @@ def short(name):
         if k in name:
             return k
     for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk_fused_wide",
-              "k_walk_fused", "k_walk", "k_locate_long", "k_locate_list", "k_locate_emit_wide", "k_locate_emit",
+              "k_walk_fused", "k_walk", "k_locate_walks", "k_scan_chained", "k_scan_tiles",
+              "k_locate_long", "k_locate_list", "k_locate_emit_wide", "k_locate_emit",
               "k_locate_ranges", "k_locate_sa_wide", "k_locate_sa", "k_expand_rows", "k_pack_wire"):
         if k in name:
             return k
