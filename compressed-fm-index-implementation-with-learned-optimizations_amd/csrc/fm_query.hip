@@ -1640,6 +1640,7 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
   const uint64_t tile = blockIdx.x;
   const uint64_t q0 = tile * (uint64_t)(kBlk * U) + threadIdx.x;
   uint64_t kc[U], kr[U], mine[U], agg;
+  const uint64_t base = op.tiles[tile];  // (issued with the records: its latency overlaps theirs)
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
@@ -1651,10 +1652,9 @@ __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat
   }
   if constexpr (kPos != 0) {
     block_scan<U>(kc, mine, agg);
-    emit_walk_lines<U, kPos>(ix, T, npat, tile, q0, kc, kr, mine, op.tiles[tile], op);
+    emit_walk_lines<U, kPos>(ix, T, npat, tile, q0, kc, kr, mine, base, op);
   } else {
     block_scan<U>(kc, mine, agg);
-    const uint64_t base = op.tiles[tile];
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const uint64_t q = q0 + (uint64_t)j * kBlk;
