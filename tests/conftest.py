@@ -23,7 +23,8 @@ sys.path.insert(0, ROOT)
 # 8,710 tests in 544-557 s (profiles/r04/pytest_gpu_all_r04{w,ae}.log), the scan-oracle checks
 # of test_gpu_scale.py included.
 # Round 5: 8,710 tests in 550.5 s at the round's routing commit (profiles/r05/r05o/pytest_gpu_all.log);
-# 8,709 in 522.6 s after (profiles/r05/r05f1/r05f1_1_tests.log) — the C5
+# 8,709 in 522.6 s after (profiles/r05/r05f1/r05f1_1_tests.log), 517.1 s at the last commit
+# (r05f7_1_tests.log) — the C5
 # wavelet-engine build (39 s) is now opt-in (CS_FM_C5_WAVELET=1; the same wide layout runs at
 # small n in the wide_wavelet variant), for ≈510 s.
 GPU_SUITE_BUDGET_S = 550
