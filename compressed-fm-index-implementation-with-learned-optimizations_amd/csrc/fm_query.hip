@@ -1572,6 +1572,7 @@ __device__ __forceinline__ void emit_walk_lines(const DevIndex& ix, NodeTable& T
 template <int kPos>
 __global__ __launch_bounds__(kBlk) void k_locate_walks(DevIndex ix, OnePass op, uint64_t ntiles) {
   using W = std::conditional_t<kPos == 1, WalkLine, WalkLineW>;
+  static_assert(kBlk == 256, "the tile lookup below searches 256 tiles in 8 steps");
   __shared__ NodeTable T;
   __shared__ uint32_t s_off[kBlk + 1];
   __shared__ uint32_t s_w[kBlk / 64];
