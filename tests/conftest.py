@@ -26,7 +26,10 @@ sys.path.insert(0, ROOT)
 # 8,709 in 522.6 s after (profiles/r05/r05f1/r05f1_1_tests.log), 517.1 s at the last commit
 # (r05f7_1_tests.log) — the C5
 # wavelet-engine build (39 s) is now opt-in (CS_FM_C5_WAVELET=1; the same wide layout runs at
-# small n in the wide_wavelet variant), for ≈510 s.
+# small n in the wide_wavelet variant), for ≈510 s.  The selector check added at the round's
+# end (test_selectors_without_a_variant, 1.2 s per variant) took it to 540.9 s
+# (profiles/r05/r05ah/pytest_gpu_all.log); its texts and batches were then cut: 0.17-0.37 s
+# per variant (profiles/r05/r05ai/sel.log), ≈ 518 s for the suite.
 GPU_SUITE_BUDGET_S = 550
 
 # Round 5: every device batch routes its long patterns (and the patterns its one read cannot

@@ -1185,26 +1185,26 @@ def test_selectors_without_a_variant(pkg):
     with CS_QT_NO_ONEPASS) on an index without the full suffix array, at limits that cut
     ranges and at ones that do not."""
     rng = np.random.default_rng(31)
-    seed = rng.choice(list(b"ACGT"), 3000).astype(np.uint8)
-    rep = np.tile(seed, 200)
+    seed = rng.choice(list(b"ACGT"), 2000).astype(np.uint8)
+    rep = np.tile(seed, 100)
     mut = rng.random(len(rep)) < 0.01
     rep[mut] = rng.choice(list(b"ACGT"), int(mut.sum())).astype(np.uint8)
-    texts = {"dna": O.gen_dna(77, 400_000).tobytes(), "repeats": rep.tobytes() + b"$"}
+    texts = {"dna": O.gen_dna(77, 150_000).tobytes(), "repeats": rep.tobytes() + b"$"}
     for name, t in texts.items():
         with _env(CS_FM_FULL_SA="0"):
             g = pkg.FMIndex.build_from_text(t)
         o = O.Index(t)
         u8 = np.frombuffer(t, np.uint8)
-        pats = [bytes(p) for p in O.gen_patterns_text(u8, 20, 2000, seed=6)]
-        pats += [bytes(p) for p in O.gen_patterns_text(u8, 7, 300, seed=7)]
-        pats += [bytes(rng.choice(list(b"ACGT"), int(m)).astype(np.uint8)) for m in rng.integers(1, 40, 300)]
+        pats = [bytes(p) for p in O.gen_patterns_text(u8, 20, 1000, seed=6)]
+        pats += [bytes(p) for p in O.gen_patterns_text(u8, 7, 200, seed=7)]
+        pats += [bytes(rng.choice(list(b"ACGT"), int(m)).astype(np.uint8)) for m in rng.integers(1, 40, 200)]
         pats += [b"", b"N" * 5, t[:25], t[-26:-1]]
         buf, offs = O.pack_patterns(pats)
         want = o.count_batch(buf=buf, offs=offs, nthreads=8)
         assert np.array_equal(_count_bo(g, buf, offs, flags=pkg.QT_COUNT_U4), want), name
         sub = pats[::5]
         b2, o2 = O.pack_patterns(sub)
-        for lim in (3, 200, 100_000):
+        for lim in (3, 100_000):
             woffs, wpos = o.locate_batch(buf=b2, offs=o2, limit=lim, nthreads=8)
             got = _locate_one(g, sub, lim, flags=pkg.QT_NO_ONEPASS | pkg.QT_WALK_PERSISTENT)
             assert np.array_equal(np.cumsum([0] + [len(q) for q in got]), woffs.astype(np.int64)), (name, lim)
