@@ -1633,8 +1633,10 @@ __global__ __launch_bounds__(kBlk) void k_locate_walks(DevIndex ix, OnePass op, 
 // the scan kernel: a decoupled look-back over the tiles — its frontier moves 64 tiles per L2
 // round trip, 0.63 against 0.53 ms per C4 call — 1024 blocks taking a share of the tiles each
 // with a running base — 4 waves per SIMD and a serial tile loop, the emit 125 against 67 us
-// — and share totals added by the search kernel's waves — same-address atomics of
-// neighbouring blocks, the search 426 -> 615 us.)
+// — share totals added by the search kernel's waves — same-address atomics of
+// neighbouring blocks, the search 426 -> 615 us — and two tiles per block, 4 patterns per
+// lane with both tiles' records in flight before one scan: 0.520 -> 0.536 ms per call,
+// profiles/r05/r05aj.)
 template <int U, int kPos = 0>
 __global__ __launch_bounds__(kBlk) void k_locate_emit(DevIndex ix, uint64_t npat, OnePass op) {
   __shared__ NodeTable T;  // kPos: the walks' C[] and codes (a pattern past walk_cap)
