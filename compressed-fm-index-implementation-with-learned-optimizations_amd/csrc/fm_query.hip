@@ -1075,6 +1075,24 @@ constexpr uint32_t kFastM = 32;
 
 // bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
 // (u[i >> 2] >> 8 (i & 3)) & 0xFF.  Reads only the dwords holding pattern bytes.
+// (the same in two halves, so that several patterns' loads can be in flight before the
+// first is realigned: the dwords, then the realignment)
+// Branch-free: all nine loads are issued, those past the pattern (m = 0: all of them) from
+// `dummy` (any readable 36 B) and zeroed after.
+__device__ __forceinline__ void load_pattern32_raw(const uint8_t* __restrict__ pats, uint64_t o0, uint32_t m,
+                                                   uint32_t w[9], const uint32_t* __restrict__ dummy) {
+  const uint32_t* w0 = reinterpret_cast<const uint32_t*>(pats + (o0 & ~3ull));
+  const uint32_t nw = m ? ((uint32_t)(o0 & 3) + m + 3) >> 2 : 0u;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) w[j] = ((uint32_t)j < nw ? w0 : dummy)[j];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) w[j] = (uint32_t)j < nw ? w[j] : 0u;
+}
+__device__ __forceinline__ void realign_pattern32(uint64_t o0, const uint32_t w[9], uint32_t u[8]) {
+  const uint32_t a = (uint32_t)(o0 & 3) * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) u[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> a);
+}
 __device__ __forceinline__ void load_pattern32(const uint8_t* __restrict__ pats, uint64_t o0,
                                                uint32_t m, uint32_t u[8]) {
   const uint32_t* w0 = reinterpret_cast<const uint32_t*>(pats + (o0 & ~3ull));
@@ -1439,15 +1457,23 @@ __device__ __forceinline__ void emit_rows(const DevIndex& ix, const NodeTable& T
 // (2'): the same scan over ceil(ntiles / 1024) blocks of 1024 tiles (one per thread): each
 // block publishes its total (one flag word), sums its predecessors' — every thread polls one
 // of them — and writes its tiles' exclusive prefixes; the last block writes the total.  The
-// blocks wait only on lower ones, which are dispatched first.  (Round 5: the one-block scan
-// took 18 us of C4's 0.53-ms one-call locate, its 24 k tiles passing through one CU.)
+// blocks wait only on lower ones.  (Round 5: the one-block scan took 18 us of C4's 0.53-ms
+// one-call locate, its 24 k tiles passing through one CU.)  A block's place in the chain is
+// the order in which it STARTS (an atomic ticket, sflags[kScanMaxBlocks], zeroed by the
+// search kernel with the flags), not its blockIdx: a block only ever waits on blocks that
+// are already running, whatever order the dispatcher picks (with other streams'
+// kernels sharing the CUs, blockIdx order is not guaranteed).
 __global__ __launch_bounds__(kScanBlock) void k_scan_chained(uint64_t* __restrict__ tiles, uint64_t ntiles,
                                                              uint64_t* __restrict__ total_out,
                                                              unsigned long long* __restrict__ sflags) {
   __shared__ uint64_t s_w[kScanBlock / 64];
   __shared__ uint64_t s_p[kScanBlock / 64];
+  __shared__ uint32_t s_id;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint64_t i = (uint64_t)blockIdx.x * kScanBlock + t;
+  if (t == 0) s_id = (uint32_t)atomicAdd(sflags + kScanMaxBlocks, 1ull);
+  __syncthreads();
+  const uint32_t bid = s_id;
+  const uint64_t i = (uint64_t)bid * kScanBlock + t;
   const uint64_t v = i < ntiles ? tiles[i] : 0ull;
   uint64_t x = v;  // inclusive scan over the wave, then the block
 #pragma unroll
@@ -1464,9 +1490,9 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_chained(uint64_t* __restric
     agg += s_w[w2];
   }
   if (t == 0)
-    __hip_atomic_store(sflags + blockIdx.x, (1ull << 63) | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sflags + bid, (1ull << 63) | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t p = 0;  // predecessor t's total
-  if (t < blockIdx.x) {
+  if (t < bid) {
     unsigned long long f;
     do {
       f = __hip_atomic_load(sflags + t, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
@@ -1481,7 +1507,7 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_chained(uint64_t* __restric
 #pragma unroll
   for (int w2 = 0; w2 < (int)(kScanBlock / 64); ++w2) base += s_p[w2];
   if (i < ntiles) tiles[i] = base + pre + x - v;
-  if (blockIdx.x == gridDim.x - 1 && t == 0) *total_out = base + agg;
+  if (bid == gridDim.x - 1 && t == 0) *total_out = base + agg;
 }
 
 // (3) on walk-line indexes: offsets, the stashed positions, and the rows of every pattern
@@ -1801,8 +1827,14 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     op.tiles[blockIdx.x] = 0;
     if (blockIdx.x == 0) *op.nwide = 0;
     if (op.sflags && blockIdx.x < kScanMaxBlocks) op.sflags[blockIdx.x] = 0;
+    if (op.sflags && blockIdx.x == 0) op.sflags[kScanMaxBlocks] = 0;  // the chained scan's ticket
     __builtin_amdgcn_s_waitcnt(0);
   }
+  // the list kernels' retire word (list_retire) is this call's from here on, whatever the
+  // caller's memory held: the list kernels run after this kernel in stream order, and no
+  // wave of this kernel touches the word (a workspace that was not zero-filled,
+  // or an aborted call, must not let an early block zero the listed counters)
+  if (ll.hdr && blockIdx.x == 0 && threadIdx.x == 0) ll.hdr[kListedLanes * kListedStride] = 0;
   __syncthreads();
   uint64_t* const cnt_out = static_cast<uint64_t*>(co.out);  // kLoc
   const uint32_t K = ix.ptab_k;
@@ -1822,42 +1854,65 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // does not answer it)
   uint8_t st[U];
   if (kLoc && !kOne && q0 == 0) cnt_out[npat] = 0;  // scan slot for the total
-  // (A)
+  // (A) in three passes, so that the loads of a lane's U patterns are in flight together:
+  // (A1) the offsets, (A2) the pattern bytes, (A3) table index and context key.  Round 6:
+  // written as one pass per pattern, the compiler waited for each pattern's offsets, bytes
+  // and (B) record before issuing the next pattern's loads (an early `continue` and the
+  // decode inside the load's branch kept it from hoisting them) — U = 2 bought no memory
+  // parallelism and the staged kernel took 0.41 ms against 0.34 for the same access mix
+  // (profiles/microbench/mix_bench.hip, profiles/r06/mix_*.txt).
+  // Every load of (A1) and (A2) is issued unconditionally (clamped indices, and a dummy
+  // address for the dwords a pattern does not have): a load inside a divergent branch made
+  // the compiler wait for every load in flight at the branch's end (s_waitcnt vmcnt(0)).
+  uint64_t m1[U];  // (A1) offs[q + 1] (the length once A2 has it)
 #pragma unroll
   for (int j = 0; j < U; ++j) {
-    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    const uint64_t q = q0 + (uint64_t)j * kBlk, qc = q < npat ? q : npat - 1;
     st[j] = 0;
     res[j] = 0;
     rv[j] = 0;
-    o0[j] = 0;
     m[j] = 0;
+    m1[j] = 0;
     t[j] = want[j] = k[j] = 0;
-    if (q >= npat) continue;
-    uint64_t mm;
     if constexpr (kPacked) {
-      o0[j] = reinterpret_cast<const uint64_t*>(pats)[q];  // the pattern itself
-      mm = fixed_m;
+      o0[j] = reinterpret_cast<const uint64_t*>(pats)[qc];  // the pattern itself
+    } else if (offs) {
+      o0[j] = offs[qc];
+      m1[j] = offs[qc + 1];
     } else {
-      o0[j] = offs ? offs[q] : q * fixed_m;
-      mm = offs ? offs[q + 1] - o0[j] : fixed_m;
+      o0[j] = qc * fixed_m;
     }
-    m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
-    if (mm == 0) {
-      res[j] = kLoc ? 0 : ix.n;  // fm_index.cpp:80; locate: :109
-      continue;
-    }
-    if (ix.n == 0) continue;  // :81
-    st[j] = 3;
-    if (kSkipLong && mm >= kFastM && mm > K + kCtxQ) {  // k_count_long's (one read cannot answer it)
-      st[j] = 4;
-      continue;
-    }
-    if (mm < K || K == 0 || mm > kFastM) continue;
-    const uint32_t wl = (uint32_t)mm;
-    uint32_t u[8];
+  }
+  // (A2) lengths, the routing decision, and the raw pattern dwords of the patterns the
+  // fast stages search (fw bit j)
+  uint32_t praw[kPacked ? 1 : U][9];
+  uint32_t fw = 0;
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    const bool live = q < npat;
+    const uint64_t mm = (kPacked || !offs) ? fixed_m : m1[j] - o0[j];
+    m[j] = live ? (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull) : 0u;
+    // 0: empty pattern (count n, fm_index.cpp:80; locate: :109) or none; 3: the general
+    // search; 4: k_count_long's (one read cannot answer it)
+    const bool any = live && mm != 0 && ix.n != 0;  // (:81)
+    const bool lng = kSkipLong && mm >= kFastM && mm > K + kCtxQ;
+    st[j] = !any ? 0 : lng ? 4 : 3;
+    if (live && mm == 0) res[j] = kLoc ? 0 : ix.n;
+    const bool fast = any && !lng && !(mm < K || K == 0 || mm > kFastM);
+    fw |= (uint32_t)fast << j;
     // (16-B vector loads here, load_pattern32_v16, were measured: 0.3857 against 0.3864 ms,
     // profiles/r03/ab_pattern_v16.json — the headline is not bound by its load instructions)
-    if constexpr (!kPacked) load_pattern32(pats, o0[j], wl, u);
+    if constexpr (!kPacked)
+      load_pattern32_raw(pats, o0[j], fast ? m[j] : 0u, praw[j], reinterpret_cast<const uint32_t*>(ix.table));
+  }
+  // (A3)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (!((fw >> j) & 1u)) continue;
+    const uint32_t wl = m[j];
+    uint32_t u[8];
+    if constexpr (!kPacked) realign_pattern32(o0[j], praw[j], u);
     const uint32_t kk = m[j] - K;
     bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
     uint32_t tt = 0, ww = 0, dl = kNoCode;
@@ -2006,19 +2061,23 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   bool inl[U];  // the record's contexts answer the rest
 #pragma unroll
   for (int j = 0; j < U; ++j) inl[j] = false;
+  // the U records first, all in flight together (unconditional loads: the dummy address
+  // for a pattern without one), then their decoding — see (A)
+  const void* const dummy = static_cast<const void*>(ix.table);
+  if (ix.ptab_rec == 2) {
+    uint4 ra[U];
 #pragma unroll
-  for (int j = 0; j < U; ++j) {
-    if (st[j] != 1 && st[j] != 2) continue;
-    if (ix.ptab_rec == 1) {
-      const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t[j] * 2;
-      const uint4 a = r[0], b = r[1];
-      sp[j] = a.x;
-      ep[j] = (uint64_t)a.x + a.y;
-      w[j][0] = make_uint4(a.z, a.w, b.x, b.y);
-      w[j][1] = make_uint4(b.z, b.w, 0u, 0u);
-      inl[j] = ep[j] - sp[j] <= kRecCtx;
-    } else if (ix.ptab_rec == 2) {
-      const uint4 a = load_record16(ix.ptab, t[j]);
+    for (int j = 0; j < U; ++j) {
+      const bool act = st[j] == 1 || st[j] == 2;
+      ra[j] = load_record16(act ? ix.ptab : dummy, act ? (uint64_t)t[j] : 0ull);
+    }
+    // (a compiler barrier: without it the compiler sinks each load into its pattern's decode
+    // branch, and waits for it there before the next pattern's load is issued)
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (st[j] != 1 && st[j] != 2) continue;
+      const uint4 a = ra[j];
       const uint32_t wc = a.y & 15u;
       sp[j] = rec16_sp(a.x, a.w, ix.wide);
       inl[j] = wc != kRec16Wide && k[j] <= (ix.wide ? kRec16QW : kRec16Q);
@@ -2035,8 +2094,33 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       if (!kLoc && wc == kRec16Wide && st[j] == 2 && k[j] == kRec16Q && !ix.wide &&
           rec16_majority(a.y, a.w, want[j], res[j]))
         st[j] = 0;
-    } else if (!ptab_at(ix, t[j], sp[j], ep[j])) {
-      st[j] = 3;
+    }
+  } else if (ix.ptab_rec == 1) {
+    uint4 ra[U], rb[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const bool act = st[j] == 1 || st[j] == 2;
+      const uint4* r = act ? static_cast<const uint4*>(ix.ptab) + (uint64_t)t[j] * 2
+                           : static_cast<const uint4*>(dummy);
+      ra[j] = r[0];
+      rb[j] = r[1];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (st[j] != 1 && st[j] != 2) continue;
+      const uint4 a = ra[j], b = rb[j];
+      sp[j] = a.x;
+      ep[j] = (uint64_t)a.x + a.y;
+      w[j][0] = make_uint4(a.z, a.w, b.x, b.y);
+      w[j][1] = make_uint4(b.z, b.w, 0u, 0u);
+      inl[j] = ep[j] - sp[j] <= kRecCtx;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (st[j] != 1 && st[j] != 2) continue;
+      if (!ptab_at(ix, t[j], sp[j], ep[j])) st[j] = 3;
     }
   }
   // (C) the context sector(s), unless the record holds the range's contexts
@@ -5217,7 +5301,7 @@ uint64_t locate_lo_bytes(const cs_fm_index* h, uint64_t npat, uint64_t wide_cap)
   const uint64_t tiles = (npat + kLocTile - 1) / kLocTile;
   const uint64_t cb = h->wide ? 8 : 4;  // count bytes (a wide index's counts pass 2^32)
   return ((npat * (8 + cb) + tiles * 8 + 8 + wide_cap * 16 + 7) & ~7ull) + locate_walk_bytes(h, npat) +
-         kScanMaxBlocks * 8;
+         (kScanMaxBlocks + 1) * 8;
 }
 uint64_t locate_workspace_bytes(const cs_fm_index* h, uint64_t npat) {
   return LongBufs::bytes(npat, false) + locate_lo_bytes(h, npat, npat);
@@ -5314,7 +5398,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   const bool nobar = count_nobar(flags);
   if (long_only) {
     FMX_HIP(hipMemsetAsync(op.tiles, 0, tiles * 8 + 8, st));
-    FMX_HIP(hipMemsetAsync(op.sflags, 0, kScanMaxBlocks * 8, st));
+    FMX_HIP(hipMemsetAsync(op.sflags, 0, (kScanMaxBlocks + 1) * 8, st));
   }
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
   op.defer = defer ? 1u : 0u;

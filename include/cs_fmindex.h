@@ -294,11 +294,12 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
 #define CS_Q_LONG 32u
 #define CS_Q_NO_LOC_RECORDS 64u
 
-/* Tuning selectors (round 5): flags bits 8-22 choose among equivalent kernels for tests and
+/* Tuning selectors (round 5): flags bits 8-23 choose among equivalent kernels for tests and
  * A/B measurements — results never change.  A handle takes its defaults from the CS_FM_*
  * environment once, when it is created (build, create, open, import: the variable named
- * beside each bit), and a call's flags add these bits over them; no count, locate or extract
- * call reads the environment.
+ * beside each bit), and a call's flags are ORed over them: a call can add a selector but
+ * cannot clear one the handle's environment set (a handle created with CS_FM_LONG_ROUTE=0
+ * never routes).  No count, locate or extract call reads the environment.
  *   CS_QT_BARRIER         staged count / locate phase 1: the general search behind a block-wide
  *                         LDS copy of the node table (CS_FM_COUNT_NOBAR=0)
  *   CS_QT_NO_ROUTE        no routing inside the call: the staged kernel searches long
@@ -438,10 +439,12 @@ cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, co
  * keeps per-pattern counts, records and tile totals between its kernels.  The plain entry
  * points allocate that memory per call (stream-ordered); the *_ws forms take it from the
  * caller — no allocation inside the call.  cs_fm_workspace_bytes(h, npat) bytes serve a
- * count or a one-call locate of up to npat patterns.  The memory must be zero-filled before
- * its first use (the calls leave it that way: the list kernel's last block re-zeroes the
- * counters it used), and one workspace serves one call at a time: calls that share it must
- * be ordered (one stream, or events).  work_bytes smaller than needed: the call allocates as
+ * count or a one-call locate of up to npat patterns.  Zero-fill it once before its first use:
+ * the calls leave it that way (the list kernel's last block re-zeroes the counters it used).
+ * Results do not depend on it — each call's first kernel claims the list kernels' retire word
+ * itself — but a first call on memory that was not zero-filled may scan every list slot.  One
+ * workspace serves one call at a time: calls that share it must be ordered (one stream, or
+ * events).  work_bytes smaller than needed: the call allocates as
  * the plain form does. */
 uint64_t cs_fm_workspace_bytes(const cs_fm_index* h, uint64_t npat);
 cs_status cs_fm_count_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
