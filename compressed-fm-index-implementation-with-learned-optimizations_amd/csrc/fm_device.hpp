@@ -414,6 +414,18 @@ __device__ __forceinline__ void rec16_contexts(uint32_t y, uint32_t z, uint32_t 
 #pragma unroll
   for (int i = 0; i < 5; ++i) dw[i] = e[2 * i] | (e[2 * i + 1] << 16);
 }
+// the rows of a compact record (rec16_contexts' entries) whose context matches the k <= 5
+// chain codes `want` (k = 0: every row): bit i for row i, rows 0..8
+__device__ __forceinline__ uint32_t rec16_match(uint32_t y, uint32_t z, uint32_t w, uint32_t want, uint32_t k) {
+  const uint64_t lo = (uint64_t)y | ((uint64_t)z << 32);
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) m |= (uint32_t)((((uint32_t)(lo >> (4 + 10 * i)) ^ want) & mask) == 0) << i;
+#pragma unroll
+  for (int i = 6; i < 9; ++i) m |= (uint32_t)((((w >> (10 * (i - 6))) ^ want) & mask) == 0) << i;
+  return m;
+}
 __device__ __forceinline__ bool ptab_at(const DevIndex& ix, uint64_t t, uint64_t& sp, uint64_t& ep) {
   if (ix.ptab_rec == 1) {
     const uint2 r = static_cast<const uint2*>(ix.ptab)[t * 4];

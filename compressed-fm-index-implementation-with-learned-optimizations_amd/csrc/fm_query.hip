@@ -1075,6 +1075,12 @@ constexpr uint32_t kFastM = 32;
 
 // bytes [0, m) of a pattern at byte offset o0, m <= 32, realigned: byte i is
 // (u[i >> 2] >> 8 (i & 3)) & 0xFF.  Reads only the dwords holding pattern bytes.
+// 64-bit value lo | hi << 32 of 2-bit digits (digit i at bits 2i, 2i + 1) with the digits'
+// order reversed: digit i at bits 62 - 2i, 63 - 2i (low bit first)
+__device__ __forceinline__ uint64_t rev_pairs64(uint32_t lo, uint32_t hi) {
+  const uint64_t r = ((uint64_t)__builtin_bitreverse32(lo) << 32) | __builtin_bitreverse32(hi);
+  return ((r >> 1) & 0x5555555555555555ull) | ((r & 0x5555555555555555ull) << 1);
+}
 // (the same in two halves, so that several patterns' loads can be in flight before the
 // first is realigned: the dwords, then the realignment)
 // Branch-free: all nine loads are issued, those past the pattern (m = 0: all of them) from
@@ -1906,7 +1912,21 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     if constexpr (!kPacked)
       load_pattern32_raw(pats, o0[j], fast ? m[j] : 0u, praw[j], reinterpret_cast<const uint32_t*>(ix.table));
   }
-  // (A3)
+  // (A3) table index and context key.  A 4-symbol table (every occurrence-line index of DNA)
+  // maps the characters without a branch: each character's map entry (LDS) goes into 2-bit
+  // digit strings and 1-bit invalid masks, and the index and the key are cut from those
+  // strings (reversed in pairs: the table index takes its first character as the most
+  // significant digit).  Round 6: the per-character branches of the general loop below cost
+  // ~750 instructions per pattern, a third of them scalar (exec-mask bookkeeping), and an LDS
+  // round trip per character — the staged kernel issued 4x the vector and 20x the scalar
+  // instructions of the same access mix in mix_bench (profiles/r06/pmc_r06d_*.csv).
+  // The characters a wave's patterns hold, rounded up to a dword (uniform): the loop stops
+  // there (C4 20-mers: 20 of 32).
+  uint32_t lmax = 0;
+#pragma unroll
+  for (int j = 0; j < U; ++j) lmax = ((fw >> j) & 1u) && m[j] > lmax ? m[j] : lmax;
+  const uint32_t nchar = __ballot(lmax > 28) ? 32u : __ballot(lmax > 24) ? 28u : __ballot(lmax > 20) ? 24u
+                         : __ballot(lmax > 16) ? 20u : 16u;
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     if (!((fw >> j) & 1u)) continue;
@@ -1914,23 +1934,55 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     uint32_t u[8];
     if constexpr (!kPacked) realign_pattern32(o0[j], praw[j], u);
     const uint32_t kk = m[j] - K;
-    bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
     uint32_t tt = 0, ww = 0, dl = kNoCode;
+    bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
+    if (ix.ptab_sigma == 4) {
+      uint32_t dlo = 0, dhi = 0, olo = 0, ohi = 0, inv = 0, oinv = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < kFastM; ++i) {
-      uint32_t b;
-      if constexpr (kPacked) b = PackedDna{o0[j]}[i];
-      else b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-      if (i >= wl - K && i < wl) {  // table part, most significant first
-        const uint32_t d = cmap[b] & 0xFFu;
-        ok &= d != kNoCode;
-        tt = tt * ix.ptab_sigma + d;
-      } else if (i < kk && i < kCtxQ) {  // context part: chain symbol kk-1-i
-        const uint32_t d = cmap[b] >> 8;
-        cok &= d != kNoCode;
-        ww |= (d & 3u) << (2 * (kk - 1 - i));
-        if constexpr (kLR)
-          if (i + 1 == kk) dl = cmap[b] & 0xFFu;  // the (k+1)-mer's first character (its table digit)
+      for (uint32_t i = 0; i < kFastM; ++i) {
+        if ((i & 3u) == 0 && i >= nchar) break;
+        uint32_t b;
+        if constexpr (kPacked) b = PackedDna{o0[j]}[i];
+        else b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        const uint32_t e = cmap[b];
+        if (i < 16) {
+          dlo |= (e & 3u) << (2 * i);
+          olo |= ((e >> 8) & 3u) << (2 * i);
+        } else {
+          dhi |= (e & 3u) << (2 * (i - 16));
+          ohi |= ((e >> 8) & 3u) << (2 * (i - 16));
+        }
+        inv |= (uint32_t)((e & 0xFFu) == kNoCode) << i;
+        oinv |= (uint32_t)((e >> 8) == kNoCode) << i;
+      }
+      // character i at bits [62 - 2i, 64 - 2i), low digit bit first
+      const uint64_t rd = rev_pairs64(dlo, dhi), ro = rev_pairs64(olo, ohi);
+      tt = (uint32_t)((rd >> (64 - 2 * wl)) & ((1ull << (2 * K)) - 1ull));
+      ok = (inv & (uint32_t)((((1ull << K) - 1ull) << (wl - K)))) == 0;
+      const uint32_t kq = kk < kCtxQ ? kk : kCtxQ;
+      cok = cok && (oinv & ((1u << kq) - 1u)) == 0;
+      ww = kq ? (uint32_t)((ro >> (64 - 2 * kq)) & ((1ull << (2 * kq)) - 1ull)) : 0u;
+      if constexpr (kLR)
+        if (kk >= 1 && kk <= kCtxQ)  // the (k+1)-mer's first character (its table digit)
+          dl = ((inv >> (kk - 1)) & 1u) ? kNoCode
+                                        : (uint32_t)((((uint64_t)dhi << 32 | dlo) >> (2 * (kk - 1))) & 3u);
+    } else {
+  #pragma unroll
+      for (uint32_t i = 0; i < kFastM; ++i) {
+        uint32_t b;
+        if constexpr (kPacked) b = PackedDna{o0[j]}[i];
+        else b = (u[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+        if (i >= wl - K && i < wl) {  // table part, most significant first
+          const uint32_t d = cmap[b] & 0xFFu;
+          ok &= d != kNoCode;
+          tt = tt * ix.ptab_sigma + d;
+        } else if (i < kk && i < kCtxQ) {  // context part: chain symbol kk-1-i
+          const uint32_t d = cmap[b] >> 8;
+          cok &= d != kNoCode;
+          ww |= (d & 3u) << (2 * (kk - 1 - i));
+          if constexpr (kLR)
+            if (i + 1 == kk) dl = cmap[b] & 0xFFu;  // the (k+1)-mer's first character (its table digit)
+        }
       }
     }
     if (!ok) continue;
@@ -2059,6 +2111,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
   // (B) the table entries (whole context records: their contexts come with them)
   uint4 w[U][4];
   bool inl[U];  // the record's contexts answer the rest
+  // a compact record's inline rows matched in (B) (cm bit j: mrec[j] is (D)'s match mask)
+  uint32_t mrec[U], cm = 0;
 #pragma unroll
   for (int j = 0; j < U; ++j) inl[j] = false;
   // the U records first, all in flight together (unconditional loads: the dummy address
@@ -2083,13 +2137,19 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       inl[j] = wc != kRec16Wide && k[j] <= (ix.wide ? kRec16QW : kRec16Q);
       ep[j] = sp[j] + (wc == kRec16Wide ? a.z : wc);
       if (wc == kRec16Wide && a.z == kRec16NoRange) st[j] = 3;  // escaped: from C[]
-      uint32_t d[5];
-      if (ix.wide)
-        rec16w_contexts(a.y, a.z, a.w, d);
-      else
-        rec16_contexts(a.y, a.z, a.w, d);
-      w[j][0] = make_uint4(d[0], d[1], d[2], d[3]);
-      w[j][1] = make_uint4(d[4], 0u, 0u, 0u);
+      if (!ix.wide && inl[j] && st[j] == 2) {
+        // the record's rows matched against the key in place (no u16 re-layout for (D))
+        mrec[j] = rec16_match(a.y, a.z, a.w, want[j], k[j]);
+        cm |= 1u << j;
+      } else {
+        uint32_t d[5];
+        if (ix.wide)
+          rec16w_contexts(a.y, a.z, a.w, d);
+        else
+          rec16_contexts(a.y, a.z, a.w, d);
+        w[j][0] = make_uint4(d[0], d[1], d[2], d[3]);
+        w[j][1] = make_uint4(d[4], 0u, 0u, 0u);
+      }
       // count forms: a wide record's majority contexts (kRec16Maj) may give the count here
       if (!kLoc && wc == kRec16Wide && st[j] == 2 && k[j] == kRec16Q && !ix.wide &&
           rec16_majority(a.y, a.w, want[j], res[j]))
@@ -2137,8 +2197,8 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       res[j] = ep[j] - sp[j];
       rv[j] = sp[j];
     } else if (st[j] == 2 && inl[j] && ix.lctx) {
-      bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record
-      w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
+      bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record (or mrec[j] matched them)
+      if (!((cm >> j) & 1u)) w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
     } else if (st[j] == 2 && ix.lctx && ep[j] - (sp[j] & ~15ull) <= 32) {
       bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
@@ -2171,11 +2231,26 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
       const uint32_t lo = (uint32_t)(sp[j] - base), hi = (uint32_t)(ep[j] - base);
       const uint32_t* dw = reinterpret_cast<const uint32_t*>(w[j]);
       uint32_t match = 0, esc = 0;
+      if ((cm >> j) & 1u) {
+        match = mrec[j];  // (a compact record's rows hold no escaped context)
+      } else {
+        // two u16 entries per dword; the entries past row 10 only for the lanes whose range
+        // reaches them (context sectors: a divergent branch, not every lane's work)
+        const uint32_t wp = want[j] | (want[j] << 16), mp = mask | (mask << 16);
 #pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        const uint32_t e = (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        match |= (uint32_t)((e & mask) == want[j]) << i;
-        esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
+        for (int d = 0; d < 5; ++d) {
+          const uint32_t x = (dw[d] ^ wp) & mp;
+          match |= ((uint32_t)((x & 0xFFFFu) == 0) | ((uint32_t)((x >> 16) == 0) << 1)) << (2 * d);
+          esc |= (((dw[d] >> 15) & 1u) | ((dw[d] >> 30) & 2u)) << (2 * d);
+        }
+        if (hi > 10) {
+#pragma unroll
+          for (int d = 5; d < 16; ++d) {
+            const uint32_t x = (dw[d] ^ wp) & mp;
+            match |= ((uint32_t)((x & 0xFFFFu) == 0) | ((uint32_t)((x >> 16) == 0) << 1)) << (2 * d);
+            esc |= (((dw[d] >> 15) & 1u) | ((dw[d] >> 30) & 2u)) << (2 * d);
+          }
+        }
       }
       const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
       const uint32_t mm = match & in;
