@@ -125,6 +125,11 @@ struct DevIndex {
   // otherwise or under CS_Q_NO_CONTEXTS / CS_Q_NO_VERIFY.
   const uint32_t* vsa;
   const uint8_t* vtext;
+  // Round 6: the byte text of an lf_exact occurrence-line index WITHOUT the full suffix array
+  // but with walk lines and text-position marks (C5): long patterns' candidate rows are
+  // verified against it at the position their short walk gives (k_count_long kWalk) instead
+  // of stepping every character.  Null otherwise or under CS_Q_NO_CONTEXTS / CS_Q_NO_VERIFY.
+  const uint8_t* wtext;
   // The same text 2-bit packed (occurrence codes, character i at bits 2 (i % 32) of word
   // i / 32, rare symbols as code 0) and the sorted positions of the rare symbols: long
   // patterns are verified against 32 characters per 8-B word (k_count_long).  Null

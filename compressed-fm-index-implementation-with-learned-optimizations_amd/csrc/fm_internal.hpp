@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/cs_fmindex.h"
+#include "../../include/cs_fmindex_tuning.h"
 #include "fm_device.hpp"
 
 struct cs_fm_index {
@@ -154,6 +155,8 @@ struct cs_fm_index {
     const bool ver = d_sa && d_dtext && lf_exact && !wide;
     d.vsa = ver ? static_cast<const uint32_t*>(d_sa) : nullptr;
     d.vtext = ver ? static_cast<const uint8_t*>(d_dtext) : nullptr;
+    d.wtext = !d_sa && d_dtext && d_walk && d_wssa && walk_marks == 2 && lf_exact && line_fmt == fmx::kFmtOcc
+                  ? static_cast<const uint8_t*>(d_dtext) : nullptr;
     d.ptext = ver && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
     d.prare = static_cast<const uint32_t*>(d_prare);
     d.lrec = d_sa && lf_exact && !wide ? d_lrec : nullptr;

@@ -1215,6 +1215,15 @@ struct OnePass {
 constexpr uint32_t kScanBlock = 1024;     // tiles per block of k_scan_chained
 constexpr uint32_t kScanMaxBlocks = 1024; // (its look-back: one predecessor per thread)
 constexpr uint32_t kWalkAdjShift56 = 56;
+__device__ __forceinline__ void onepass_zero(const OnePass& op) {
+  // the call's wide-range counter and the chained scan's flags and ticket (no memset launch;
+  // stream order makes the stores visible to the kernels after this one)
+  if (threadIdx.x == 0) {
+    if (blockIdx.x == 0) *op.nwide = 0;
+    if (op.sflags && blockIdx.x < kScanMaxBlocks) op.sflags[blockIdx.x] = 0;
+    if (op.sflags && blockIdx.x == 0) op.sflags[kScanMaxBlocks] = 0;
+  }
+}
 // Tiles of the one-call locate's scan (k_count_ctx kOne with U = 2 patterns per lane)
 constexpr uint64_t kLocTile = 2 * kBlk;
 static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns");
@@ -2401,18 +2410,18 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
 // alphabet, a pattern shorter than 32 characters — takes count_pattern with the node table
 // read through the caches.
 template <int V>
-__device__ __forceinline__ bool window_eq_long(const DevIndex& ix, const uint8_t* P, uint64_t q,
-                                               uint64_t L) {
+__device__ __forceinline__ bool window_eq_long(const DevIndex& ix, const uint8_t* __restrict__ text,
+                                               const uint8_t* P, uint64_t q, uint64_t L) {
   const uint64_t n = ix.n;
   if (q + L > n) {  // a window through the end of the text (cyclic), byte by byte
     for (uint64_t j = 0; j < L; ++j) {
       uint64_t t = q + j;
       if (t >= n) t -= n;
-      if (ix.vtext[t] != P[j]) return false;
+      if (text[t] != P[j]) return false;
     }
     return true;
   }
-  const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
+  const uint64_t* tw = reinterpret_cast<const uint64_t*>(text);
   const uint64_t* pw = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(P) & ~(uintptr_t)7);
   const uint64_t ps = reinterpret_cast<uintptr_t>(P) & 7;
   const uint64_t tlast = (q + L - 1) >> 3, plast = (ps + L - 1) >> 3;  // words holding a byte
@@ -2647,11 +2656,15 @@ __device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __
   if (ix.ptab_rec == 2) {
     const uint4 a = load_record16(ix.ptab, t);
     const uint32_t wc = a.y & 15u;
-    sp = a.x;
+    sp = rec16_sp(a.x, a.w, ix.wide);  // (wide indexes, round 6: sp's bits 32-37 in the record)
+    if (wc == kRec16Wide && a.z == kRec16NoRange) return false;  // escaped: from C[]
     ep = sp + (wc == kRec16Wide ? a.z : wc);
     if (wc != kRec16Wide) {
-      qf = kRec16Q;
-      rec16_contexts(a.y, a.z, a.w, d);
+      qf = ix.wide ? kRec16QW : kRec16Q;
+      if (ix.wide)
+        rec16w_contexts(a.y, a.z, a.w, d);
+      else
+        rec16_contexts(a.y, a.z, a.w, d);
     }
   } else if (ix.ptab_rec == 1) {
     const uint4* r = static_cast<const uint4*>(ix.ptab) + (uint64_t)t * 2;
@@ -2662,8 +2675,8 @@ __device__ __forceinline__ bool long_stage(const DevIndex& ix, const uint8_t* __
       qf = kCtxQ;
       d[0] = a.z, d[1] = a.w, d[2] = b.x, d[3] = b.y, d[4] = b.z, d[5] = b.w;
     }
-  } else {
-    (void)ptab_at(ix, t, sp, ep);  // a narrow plain table escapes nothing
+  } else if (!ptab_at(ix, t, sp, ep)) {  // (a wide packed entry escaped: from C[])
+    return false;
   }
   // (C) the candidate rows base + i (bit i of cand)
   base = sp;
@@ -2997,7 +3010,13 @@ __device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTabl
                                                     const OnePass& op, const LongList& ll, uint32_t c);
 
 // k_count_long's search of one pattern q (< npat, the batch's offsets or fixed_m)
-template <int W, bool kPT, bool kBytes, int kV16>
+// kWalk (round 6): an index without the full suffix array (DevIndex::wtext:
+// walk lines with text-position marks, the byte text; C5) takes each candidate row's position
+// from its short walk (walk_positions_k: <= pstride - 1 LF steps over walk lines, then the
+// mark's sample) and verifies the window against the byte text — a 64-mer costs the record,
+// the walk (1.4 lines + a sample on C5) and its window, not 48 more backward-search steps.
+// 1: narrow walk lines (WalkLine), 2: wide (WalkLineW).
+template <int W, bool kPT, bool kBytes, int kV16, int kWalk = 0>
 __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t* __restrict__ pats,
                                                const uint64_t* __restrict__ offs, const CountOut& co,
                                                uint64_t fixed_m, const LongList& ll, bool skip_short,
@@ -3024,7 +3043,16 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
     while (cand) {
       const uint32_t i = (uint32_t)__ffs(cand) - 1u;
       cand &= cand - 1;
-      const uint64_t p = load_sa(ix.vsa, base + i);
+      uint64_t p;
+      if constexpr (kWalk != 0) {
+        using WL = std::conditional_t<kWalk == 1, WalkLine, WalkLineW>;
+        uint64_t pos[1] = {base + i};
+        bool act[1] = {true};
+        walk_positions_k<WL, 1>(ix, *ix.table, walk_consts(*ix.table), pos, act);
+        p = pos[0];
+      } else {
+        p = load_sa(ix.vsa, base + i);
+      }
       const uint64_t wq = p >= k ? p - k : p + n - k;
       if constexpr (kBytes) {  // the SA sector, then the window's words
         constexpr uint64_t C = 32ull * kLongPW;
@@ -3038,7 +3066,7 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
       }
       bool eq;
       if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
-      else eq = window_eq_long<kLongWords>(ix, pats + o0, wq, L);
+      else eq = window_eq_long<kLongWords>(ix, kWalk ? ix.wtext : ix.vtext, pats + o0, wq, L);
       res += eq ? 1u : 0u;
     }
   }
@@ -3048,7 +3076,7 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
   else store_count<W>(co, q, res);
 }
 
-template <int W, bool kPT, bool kBytes = false, int kV16 = 0, bool kList = false>
+template <int W, bool kPT, bool kBytes = false, int kV16 = 0, bool kList = false, int kWalk = 0>
 // (list mode held to 4 waves per SIMD: left alone it takes 150 VGPRs, 3 waves — hoisted
 // loop invariants and SGPR spills of the list loop — and C4 150-mers routed took 1.93 ms
 // against 1.71, profiles/r04/ab_lib_r04j_count_m150.jsonl)
@@ -3076,7 +3104,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
   __syncthreads();
   if constexpr (kList) {
     list_for_each(ll.list, c1, [&](uint64_t q, bool act) {
-      if (act) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, false, cmap, rare, q);
+      if (act) count_long_one<W, kPT, kBytes, kV16, kWalk>(ix, pats, offs, co, fixed_m, ll, false, cmap, rare, q);
     });
     // then the general search of what it listed and what the staged kernel listed there: the
     // same block owns the same slots of list2, so no second launch (k_count_list) waits for
@@ -3090,7 +3118,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
     list_retire(ll);
   } else {
     const uint64_t q = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-    if (q < npat) count_long_one<W, kPT, kBytes, kV16>(ix, pats, offs, co, fixed_m, ll, skip_short, cmap, rare, q);
+    if (q < npat) count_long_one<W, kPT, kBytes, kV16, kWalk>(ix, pats, offs, co, fixed_m, ll, skip_short, cmap, rare, q);
   }
 }
 
@@ -3420,15 +3448,23 @@ __global__ __launch_bounds__(kBlk) void k_locate_list(DevIndex ix, const uint8_t
 // (count_rest / ctx_match): after the table, the rows r of [sp, ep) whose chain spells
 // P[k-1], ..., P[0] are exactly the rows that survive the reference's remaining k steps
 // (fm_index.cpp:90-96).
-template <int U, int W>
+// kOne (round 6): the one-call locate's search (OnePass stage (1)) in the
+// same stages — a pattern finished over the contexts stores its window of matching rows at k
+// characters before the end (kLocCtx, lf_exact indexes), the rest its range's first row or
+// the general search's record (locate_search); the block stores counts, records and its tile
+// total as k_count_ctx's kOne form does, so the scan and emit kernels are the occurrence
+// engine's.  The loads of a lane's U patterns are issued together (see k_count_ctx (A)).
+template <int U, int W, bool kOne = false>
 __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void k_count_qctx(DevIndex ix, const uint8_t* __restrict__ pats,
                                                      const uint64_t* __restrict__ offs,
-                                                     uint64_t npat, CountOut co, uint64_t fixed_m) {
+                                                     uint64_t npat, CountOut co, uint64_t fixed_m,
+                                                     uint64_t limit = 0, OnePass op = OnePass{}) {
   // bits 0-7 table digit (kNoCode: outside the table alphabet), 8-15 dense code, bit 16 the
   // symbol occurs (every present symbol has a dense code; with 256 symbols one of them is
   // 0xFF, so kNoCode cannot mark "no code" here)
   __shared__ uint32_t cmap[256];
   __shared__ NodeTable T;
+  if constexpr (kOne) onepass_zero(op);
   if (threadIdx.x < 256) {
     const NodeTable* g = ix.table;
     const uint32_t c = threadIdx.x;
@@ -3437,33 +3473,46 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void 
   __syncthreads();
   const uint32_t K = ix.ptab_k, sb = ix.lctx_sb, Q = ix.lctx_q;
   const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
-  uint64_t o0[U], res[U], sp[U], ep[U];
+  uint64_t o0[U], res[U], sp[U], ep[U], rv[U];
   uint32_t m[U], t[U], want[U], k[U], c0[U], c1[U];
   uint8_t st[U];  // 0 done, 1 table only, 2 table + contexts, 3 general search
-  // (A)
+  // (A1) offsets (clamped: unconditional loads)
+  uint64_t m1[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk, qc = q < npat ? q : npat - 1;
+    st[j] = 0;
+    res[j] = rv[j] = 0;
+    m[j] = 0;
+    t[j] = want[j] = k[j] = 0;
+    o0[j] = offs ? offs[qc] : qc * fixed_m;
+    m1[j] = offs ? offs[qc + 1] : 0;
+  }
+  // (A2) lengths and the pattern dwords of the patterns the stages search
+  uint32_t praw[U][9], fw = 0;
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    st[j] = 0;
-    res[j] = 0;
-    o0[j] = 0;
-    m[j] = 0;
-    t[j] = want[j] = k[j] = 0;
-    if (q >= npat) continue;
-    o0[j] = offs ? offs[q] : q * fixed_m;
-    const uint64_t mm = offs ? offs[q + 1] - o0[j] : fixed_m;
-    m[j] = (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull);
-    if (mm == 0) {
-      res[j] = ix.n;  // fm_index.cpp:80
-      continue;
-    }
-    if (ix.n == 0) continue;  // :81
-    st[j] = 3;
-    if (mm < K || K == 0 || mm > kFastM) continue;
+    const bool live = q < npat;
+    const uint64_t mm = offs ? m1[j] - o0[j] : fixed_m;
+    m[j] = live ? (uint32_t)(mm < 0xFFFFFFFFull ? mm : 0xFFFFFFFFull) : 0u;
+    const bool any = live && mm != 0 && ix.n != 0;  // fm_index.cpp:81
+    if (live && mm == 0) res[j] = kOne ? 0 : ix.n;  // fm_index.cpp:80; locate: :109
+    st[j] = any ? 3 : 0;
+    const bool fast = any && !(mm < K || K == 0 || mm > kFastM);
+    fw |= (uint32_t)fast << j;
+    load_pattern32_raw(pats, o0[j], fast ? m[j] : 0u, praw[j], reinterpret_cast<const uint32_t*>(ix.table));
+  }
+  // (A3)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (!((fw >> j) & 1u)) continue;
     uint32_t u[8];
-    load_pattern32(pats, o0[j], m[j], u);
+    realign_pattern32(o0[j], praw[j], u);
     const uint32_t kk = m[j] - K;
-    const bool cq = kk <= Q && sb * kk <= 32;  // the rest fits one context entry
+    // (kOne: a window of rows gives positions only when LF is one n-cycle, and its record
+    // holds k in 3 bits: k <= 7, as locate_search's windows)
+    const bool cq = kk <= Q && sb * kk <= 32 && (!kOne || (ix.lf_exact && kk <= 7));  // the rest fits one context entry
     bool ok = true, cok = cq;
     uint32_t tt = 0, ww = 0;
 #pragma unroll
@@ -3485,21 +3534,36 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void 
     want[j] = ww;
     k[j] = kk;
   }
-  // (B) the table entries
+  // (B) the table entries, all in flight together (a dummy address for a pattern without one)
+  const void* const dummy = static_cast<const void*>(ix.table);
+  if (ix.ptab_rec == 3) {
+    uint4 ra[U];
 #pragma unroll
-  for (int j = 0; j < U; ++j) {
-    c0[j] = c1[j] = 0;
-    if (st[j] != 1 && st[j] != 2) continue;
-    if (ix.ptab_rec == 3) {
-      const uint4 a = load_record16(ix.ptab, t[j]);
-      sp[j] = a.x;
-      ep[j] = (uint64_t)a.x + a.y;
-      c0[j] = a.z;
-      c1[j] = a.w;
-    } else {
-      const uint2 a = static_cast<const uint2*>(ix.ptab)[t[j]];
-      sp[j] = a.x;
-      ep[j] = a.y;
+    for (int j = 0; j < U; ++j) {
+      const bool act = st[j] == 1 || st[j] == 2;
+      ra[j] = load_record16(act ? ix.ptab : dummy, act ? (uint64_t)t[j] : 0ull);
+    }
+    asm volatile("" ::: "memory");  // (keeps the loads together: see k_count_ctx (B))
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      sp[j] = ra[j].x;
+      ep[j] = (uint64_t)ra[j].x + ra[j].y;
+      c0[j] = ra[j].z;
+      c1[j] = ra[j].w;
+    }
+  } else {
+    uint2 ra[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const bool act = st[j] == 1 || st[j] == 2;
+      ra[j] = (act ? static_cast<const uint2*>(ix.ptab) + t[j] : static_cast<const uint2*>(dummy))[0];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      sp[j] = ra[j].x;
+      ep[j] = ra[j].y;
+      c0[j] = c1[j] = 0;
     }
   }
   // (C) the context sector(s), unless the record holds the range's contexts
@@ -3515,6 +3579,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void 
     } else if (k[j] == 0) {
       st[j] = 0;
       res[j] = ep[j] - sp[j];
+      rv[j] = sp[j];  // kOne: the range's first row
     } else if (st[j] == 2 && ix.ptab_rec == 3 && ep[j] - sp[j] <= kRecQCtx) {
       bs[j] = sp[j];
       w[j][0] = make_uint4(c0[j], c1[j], 0u, 0u);
@@ -3535,6 +3600,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void 
     }
   }
   // (D)
+  uint64_t kc[U], kr[U];
 #pragma unroll
   for (int j = 0; j < U; ++j) {
     if (st[j] == 2) {
@@ -3546,23 +3612,43 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(6))) void 
 #pragma unroll
       for (int i = 0; i < 16; ++i) match |= (uint32_t)((dw[i] & mask) == want[j]) << i;
       const uint32_t in = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-      res[j] = (uint64_t)__popc(match & in);
+      const uint32_t mm = match & in;
+      res[j] = (uint64_t)__popc(mm);
+      if (kOne && mm) {  // the window record (locate_search): rows bs + f + the bits of rel
+        const uint32_t f = (uint32_t)__ffs(mm) - 1u;
+        rv[j] = kLocCtx | ((uint64_t)k[j] << 60) | ((uint64_t)(mm >> f) << 38) | (bs[j] + f);
+      }
       st[j] = 0;
     }
     const uint64_t q = q0 + (uint64_t)j * kBlk;
-    if (q < npat && st[j] != 3) store_count<W>(co, q, res[j]);
+    kc[j] = kr[j] = 0;
+    if (kOne) {
+      if (q < npat && st[j] != 3) {
+        kc[j] = res[j] < limit ? res[j] : limit;  // fm_index.cpp:125
+        kr[j] = rv[j];
+      }
+    } else if (q < npat && st[j] != 3) {
+      store_count<W>(co, q, res[j]);
+    }
   }
   bool general = false;
 #pragma unroll
   for (int j = 0; j < U; ++j) general |= st[j] == 3;
-  if (!__syncthreads_or(general)) return;
-  load_table(T, ix.table);
-  __syncthreads();
+  if (__syncthreads_or(general)) {
+    load_table(T, ix.table);
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < U; ++j) {
-    if (st[j] != 3) continue;
-    store_count<W>(co, q0 + (uint64_t)j * kBlk, count_pattern<QWM>(ix, T, pats + o0[j], m[j]));
+    for (int j = 0; j < U; ++j) {
+      if (st[j] != 3) continue;
+      if constexpr (kOne) {
+        const uint64_t c = locate_search<QWM>(ix, T, pats + o0[j], m[j], kr[j]);
+        kc[j] = c < limit ? c : limit;  // fm_index.cpp:125
+      } else {
+        store_count<W>(co, q0 + (uint64_t)j * kBlk, count_pattern<QWM>(ix, T, pats + o0[j], m[j]));
+      }
+    }
   }
+  if constexpr (kOne) locate_split_store<U, 0>(ix, T, npat, blockIdx.x, q0, kc, kr, op);
 }
 
 // Single-pattern count (FMIndex::count, the p50 path): the pattern travels in the
@@ -3759,6 +3845,39 @@ __global__ __launch_bounds__(kBlk) void k_locate_ranges(DevIndex ix,
   if (m && ix.n) c = locate_search<E>(ix, T, pats + o0, m, rec);  // fm_index.cpp:109: empty -> {}
   sp_out[q] = rec;
   cnt_out[q] = c < limit ? c : limit;  // fm_index.cpp:125 `positions.size() < limit`
+}
+
+// The one-call locate's search (OnePass stage (1)) for any rank engine over an index that
+// keeps the full suffix array (round 6): the binary wavelet matrix (the
+// reference's own structure), learned occurrence lines, and occurrence-line indexes without
+// a prefix table or left contexts — each lane searches its U = 2 patterns with
+// locate_search (phase 1's search, k_locate_ranges) and the block stores counts, records and
+// its tile total as k_count_ctx's kOne form does, so the scan and emit kernels after it are
+// the occurrence engine's.  No host round trip between the phases, no 100-MB count array
+// scanned by rocprim.
+template <class E>
+__global__ __launch_bounds__(kBlk) void k_locate_one_gen(DevIndex ix, const uint8_t* __restrict__ pats,
+                                                         const uint64_t* __restrict__ offs, uint64_t npat,
+                                                         uint64_t limit, OnePass op) {
+  constexpr int U = 2;
+  __shared__ NodeTable T;
+  onepass_zero(op);
+  load_table(T, ix.table);
+  __syncthreads();
+  const uint64_t q0 = blockIdx.x * (uint64_t)(kBlk * U) + threadIdx.x;
+  uint64_t kc[U], kr[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * kBlk;
+    kc[j] = kr[j] = 0;
+    if (q >= npat) continue;
+    const uint64_t o0 = offs[q], m = offs[q + 1] - o0;
+    if (m && ix.n) {  // fm_index.cpp:109: empty -> {}
+      const uint64_t c = locate_search<E>(ix, T, pats + o0, m, kr[j]);
+      kc[j] = c < limit ? c : limit;  // fm_index.cpp:125
+    }
+  }
+  locate_split_store<U, 0>(ix, T, npat, blockIdx.x, q0, kc, kr, op);
 }
 
 // The reported rows of pattern q in row order (fm_index.cpp:125): sp[q] + (j -
@@ -5018,8 +5137,8 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
   }
   // CS_Q_NO_FULL_SA: locate's phase 2 walks, and a walk takes no verified windows
   if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA))
-    d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr;
-  if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr;
+    d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr, d.wtext = nullptr;
+  if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr, d.wtext = nullptr;
   if (flags & (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS | CS_Q_NO_FULL_SA | CS_Q_NO_LOC_RECORDS)) d.lrec = nullptr;
   return d;
 }
@@ -5152,7 +5271,17 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
   // CS_QT_LONG_LOADS8 (CS_FM_LONG_V16=0): 8-B pattern / window loads; the default 16-B vectors
   // for the pattern's packed part and the window (C4 150-mers 1.87 -> 1.55 ms, 64-mers 1.25 ->
   // 1.16-1.21, profiles/r03/long_probe_v16.json; round 4's partial forms 1 / 2 are gone)
-  if (routed && ix.ptext && !byte_text && !loads8)  // the routed default
+  const int walk = ix.vsa ? 0 : ix.wtext ? (ix.wide ? 2 : 1) : 0;
+  if (walk && !kBytes) {  // (round 6) candidates positioned by their short walks (no full SA)
+    if (routed && walk == 2)
+      k_count_long<0, false, false, 0, true, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+    else if (routed)
+      k_count_long<0, false, false, 0, true, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+    else if (walk == 2)
+      k_count_long<0, false, false, 0, false, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+    else
+      k_count_long<0, false, false, 0, false, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+  } else if (routed && ix.ptext && !byte_text && !loads8)  // the routed default
     k_count_long<0, true, kBytes, 3, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
   else if (routed && ix.ptext && !byte_text)
     k_count_long<0, true, kBytes, 0, true><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
@@ -5190,7 +5319,9 @@ cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uin
 // routes and the production path is the one the tests run.
 // CS_QT_NO_ROUTE (CS_FM_LONG_ROUTE=0): never route (the staged kernel alone, round 2's path).
 bool can_route(const cs_fm_index* h, const DevIndex& ix, uint32_t flags) {
-  if (h->line_fmt != kFmtOcc || !ix.vsa || !ix.ptab_k) return false;
+  // (round 6: also indexes without the full SA whose long patterns k_count_long verifies at
+  // their walks' positions, DevIndex::wtext — C5)
+  if (h->line_fmt != kFmtOcc || !(ix.vsa || ix.wtext) || !ix.ptab_k) return false;
   return !(flags & CS_QT_NO_ROUTE);
 }
 
@@ -5240,7 +5371,11 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
     if (s != CS_OK) return s;
     // the general searches a wave lists from (LongList::gen_list): CS_QT_GENERAL_INLANE none,
     // CS_QT_GENERAL_LIST_ALL every one, else the handle's threshold (CS_FM_GENERAL_LIST_MIN)
-    lb.ll.gen_list = (flags & CS_QT_GENERAL_INLANE) ? 0u : (flags & CS_QT_GENERAL_LIST_ALL) ? 1u : h->gen_list_min;
+    // (an index routed for its walk-verified long patterns only, ix.wtext: its general
+    // searches stay in the lane unless the call lists every one — C5's 20-mer count is
+    // unchanged by the routing)
+    lb.ll.gen_list = (flags & CS_QT_GENERAL_INLANE) ? 0u : (flags & CS_QT_GENERAL_LIST_ALL) ? 1u
+                     : ix.vsa ? h->gen_list_min : 0u;
     lb.ll.grid = h->list_grid;
     if (nobar)
       k_count_ctx<OccE, 2, false, false, W, true, false, true><<<g2, kBlk, 0, st>>>(
@@ -5283,7 +5418,7 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
-  if (h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa && !packed &&
+  if (h->line_fmt == kFmtOcc && ix.ptab_k && (ix.vsa || ix.wtext) && !packed &&
       ((flags & CS_Q_LONG) || (!d_offs && fixed_m > kLongPatternM))) {
     // long patterns: one per lane in k_count_long (record, candidates, SA, text window as
     // independent rounds; against the 2-bit text when the index has it), the patterns it
@@ -5395,8 +5530,13 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // SA only (a walk index takes the two phases)
   const bool by_sa = h->d_sa && !h->wide;
   const bool by_walk = !h->d_sa && h->d_walk && h->d_wssa && h->walk_marks == 2 && !(flags & CS_QT_ONEPASS_SA);
-  if (h->line_fmt != kFmtOcc || !ix.ptab_k || !ix.lctx || !h->lf_exact || !(by_sa || by_walk))
-    return CS_OK;
+  // the occurrence engine's staged search (context records, locate records, routing), or —
+  // round 6 — over the full suffix array any other index: the quaternary matrix's staged
+  // search (C3) or the generic one (k_locate_one_gen: the binary wavelet matrix, learned
+  // occurrence lines, indexes without prefix table or contexts)
+  const bool occ_fast = h->line_fmt == kFmtOcc && ix.ptab_k && ix.lctx && h->lf_exact && (by_sa || by_walk);
+  const bool gen = !occ_fast && by_sa;
+  if (!occ_fast && !gen) return CS_OK;
   const int kpos = by_sa ? 0 : h->wide ? 2 : 1;
   *done = true;
   if (!npat) {
@@ -5417,7 +5557,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // long patterns (full-SA indexes with the 2-bit text): k_locate_long takes every pattern
   // of a CS_Q_LONG batch (host batches of long patterns pass it) and, routed (can_route),
   // the long patterns the staged kernel lists in the same call
-  const bool lk = kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
+  const bool lk = occ_fast && kpos == 0 && ix.ptext && ix.vtext && ix.vsa;
   const bool long_only = lk && (flags & CS_Q_LONG);
   const bool routed = lk && !long_only && can_route(h, ix, flags);
   static_assert(kLocTile == (uint64_t)kBlk * U, "k_locate_long's tiles are the staged kernel's");
@@ -5427,7 +5567,7 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   // shortens the search kernel (C4 Q_text: 468 -> 410 us) but the 7 % it lists cost the list kernel 130 us of dependent chains: 0.665 against 0.612 ms
   // per call (profiles/r04/ab_defer_fast_misses.json; 0.786 / 0.631 when the list kernel ran
   // the general search, ab_defer.json)
-  const bool defer = (flags & CS_QT_LOC_DEFER) && kpos == 0 && ix.lrec;
+  const bool defer = occ_fast && (flags & CS_QT_LOC_DEFER) && kpos == 0 && ix.lrec;
   // (the long-pattern lists, when the call has them, first, in the same buffer: one
   // stream-ordered allocation per call without a workspace, not two)
   const bool lists = long_only || routed || defer;
@@ -5477,7 +5617,12 @@ cs_status launch_locate_onepass(const cs_fm_index* h, const uint8_t* d_pats, con
   }
   const CountOut co{nullptr, nullptr, nullptr, 0, 8};
   op.defer = defer ? 1u : 0u;
-  if (long_only || routed || defer) {
+  if (gen) {
+    if (h->line_fmt == kFmtQwm && ix.ptab_k && ix.lctx && !ix.wide && qctx_staged(flags))
+      k_count_qctx<U, 8, true><<<(unsigned)tiles, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, 0, limit, op);
+    else
+      FMX_DISPATCH(h, k_locate_one_gen, (unsigned)tiles, ix, d_pats, d_offs, npat, limit, op);
+  } else if (long_only || routed || defer) {
     LongBufs lb;
     cs_status ls = lb.alloc(npat, long_only, st, base, !use_ws);
     if (ls != CS_OK) return ls;

@@ -294,50 +294,9 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
 #define CS_Q_LONG 32u
 #define CS_Q_NO_LOC_RECORDS 64u
 
-/* Tuning selectors (round 5): flags bits 8-23 choose among equivalent kernels for tests and
- * A/B measurements — results never change.  A handle takes its defaults from the CS_FM_*
- * environment once, when it is created (build, create, open, import: the variable named
- * beside each bit), and a call's flags are ORed over them: a call can add a selector but
- * cannot clear one the handle's environment set (a handle created with CS_FM_LONG_ROUTE=0
- * never routes).  No count, locate or extract call reads the environment.
- *   CS_QT_BARRIER         staged count / locate phase 1: the general search behind a block-wide
- *                         LDS copy of the node table (CS_FM_COUNT_NOBAR=0)
- *   CS_QT_NO_ROUTE        no routing inside the call: the staged kernel searches long
- *                         patterns itself (CS_FM_LONG_ROUTE=0)
- *   CS_QT_COUNT_U1 / _U4  staged count: one / four patterns per lane (CS_FM_COUNT_U=1 / 4)
- *   CS_QT_LONG_LOADS8     long-pattern kernels: 8-B pattern and window loads (CS_FM_LONG_V16=0)
- *   CS_QT_LONG_ROUND2     CS_Q_LONG counts through round 2's kernel (CS_FM_LONG_KERNEL=0)
- *   CS_QT_LONG_BYTE_TEXT  long-pattern kernels against the byte text (CS_FM_LONG_KERNEL=2)
- *   CS_QT_QCTX_UNSTAGED   quaternary matrix: one pattern per lane (CS_FM_QCTX_STAGED=0)
- *   CS_QT_NO_ONEPASS      cs_fm_locate_device runs the two phases (CS_FM_LOCATE_ONEPASS=0)
- *   CS_QT_ONEPASS_SA      the one-call locate only over the full SA (CS_FM_LOCATE_ONEPASS=2)
- *   CS_QT_LOC_DEFER       one-call locate: locate-record misses to the list kernel
- *                         (CS_FM_LOC_DEFER=1)
- *   CS_QT_LOCATE_U1       locate phase 1: one pattern per lane (CS_FM_LOCATE_U=1)
- *   CS_QT_WALK_ROWS       phase 2 walks from an expanded rows buffer (CS_FM_WALK_ROWS=1)
- *   CS_QT_WALK_PERSISTENT phase 2: the persistent walk kernel (CS_FM_WALK_PERSISTENT=1)
- *   CS_QT_GENERAL_INLANE  routed count: the staged kernel's lanes run the general searches
- *                         (patterns the one read cannot finish) themselves; by default a wave
- *                         holding at least CS_FM_GENERAL_LIST_MIN (2) of them lists them for
- *                         the list kernel (CS_FM_GENERAL_INLANE=1)
- *   CS_QT_GENERAL_LIST_ALL routed count: every wave lists its general searches
- *                         (CS_FM_GENERAL_LIST_ALL=1) */
-#define CS_QT_BARRIER (1u << 8)
-#define CS_QT_NO_ROUTE (1u << 9)
-#define CS_QT_COUNT_U1 (1u << 10)
-#define CS_QT_COUNT_U4 (1u << 11)
-#define CS_QT_LONG_LOADS8 (1u << 12)
-#define CS_QT_LONG_ROUND2 (1u << 13)
-#define CS_QT_LONG_BYTE_TEXT (1u << 14)
-#define CS_QT_QCTX_UNSTAGED (1u << 15)
-#define CS_QT_NO_ONEPASS (1u << 16)
-#define CS_QT_ONEPASS_SA (1u << 17)
-#define CS_QT_LOC_DEFER (1u << 18)
-#define CS_QT_LOCATE_U1 (1u << 19)
-#define CS_QT_WALK_ROWS (1u << 20)
-#define CS_QT_WALK_PERSISTENT (1u << 21)
-#define CS_QT_GENERAL_INLANE (1u << 22)
-#define CS_QT_GENERAL_LIST_ALL (1u << 23)
+/* Tuning selectors (flags bits 8-23: equivalent kernels for tests and A/B measurements,
+ * results never change) are declared in cs_fmindex_tuning.h (round 6: kept out of the
+ * drop-in API; a caller of the reference's interface never needs them). */
 
 /* Where a batch count writes.  width 8: uint64 counts (the reference's return type,
  * fm_index.hpp:26).  width 4: uint32, exact while n < 2^32 (CS_ERR_INVALID otherwise).

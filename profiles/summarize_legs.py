@@ -24,6 +24,9 @@ import re
 import statistics
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from srchash import kernel_src_hash  # noqa: E402  (the tree that was profiled)
+
 ONE_CALL = ("k_count_ctx_onepass", "k_count_ctx_onepass_skiplong", "k_locate_long", "k_locate_list",
             "k_locate_emit", "k_locate_emit_wide", "k_locate_walks", "k_scan_chained", "k_scan_tiles")
 # the kernel that carries each leg's work
@@ -189,7 +192,7 @@ def main():
                  "kernel_mean_ns_profiled": sum(res["kernels"].get(n, {}).get("mean_ns", 0) for n in group),
                  "kernel_median_ns_profiled": sum(res["kernels"].get(n, {}).get("median_ns", 0) for n in group),
                  "dispatches_profiled": res["kernels"].get(kname, {}).get("dispatches"),
-                 "tag": tag}
+                 "tag": tag, "src_hash": kernel_src_hash()}
             e["workload"] = wl
             pmc_legs["%s|%s" % (wl, leg)] = e
             res["traffic"] = e

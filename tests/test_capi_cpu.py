@@ -102,3 +102,15 @@ def test_query_flags_mirror_header():
     assert "Q_LONG" in flags and len(flags) >= 6
     for k, v in flags.items():
         assert getattr(pkg, k) == v, k
+
+
+def test_tuning_selectors_mirror_header():
+    """The Python mirror's QT_* selectors equal cs_fmindex_tuning.h's CS_QT_* bits (round 6: the
+    tuning selectors live outside the drop-in header), and the drop-in header declares none."""
+    pkg = load_pkg()
+    src = open(os.path.join(ROOT, "include", "cs_fmindex_tuning.h")).read()
+    bits = {k: 1 << int(v) for k, v in re.findall(r"#define CS_(QT_[A-Z0-9_]+) \(1u << (\d+)\)", src)}
+    assert len(bits) == 16
+    for k, v in bits.items():
+        assert getattr(pkg, k) == v, k
+    assert "#define CS_QT_" not in open(os.path.join(ROOT, "include", "cs_fmindex.h")).read()

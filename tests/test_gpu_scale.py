@@ -145,16 +145,19 @@ def _kmer_checksum(idx, alphabet, k, N):
 
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C4") == "1", reason="C4 disabled")
-@pytest.mark.parametrize("variant", ["auto", "plain_walk", "learned"])
+@pytest.mark.parametrize("variant", ["auto", "plain_walk", "learned", "wavelet"])
 def test_c4_dna_4gb(variant, monkeypatch):
     """BASELINE configs[3] at full size: the default index (context records, left
     contexts, full suffix array), the same without records and full SA (8-B table,
-    context sectors, locate by walk lines), and the learned occurrence lines."""
+    context sectors, locate by walk lines), the learned occurrence lines, and (round 6,
+    VERDICT r05 item 3) the reference's own structure — the 8-level binary wavelet matrix of
+    BitVectors (wavelet.cpp:59-96, bitvector.cpp:165-230) in 32-B rank lines — whose count
+    and one-call locate (k_locate_one_gen) are checked against the same text scan."""
     if variant == "plain_walk":
         monkeypatch.setenv("CS_FM_CTX_RECORDS", "0")
         monkeypatch.setenv("CS_FM_FULL_SA", "0")
-    elif variant == "learned":
-        monkeypatch.setenv("CS_FM_ENGINE", "learned")
+    elif variant in ("learned", "wavelet"):
+        monkeypatch.setenv("CS_FM_ENGINE", variant)
     pkg = load_pkg()
     _trim_pool()
     free0 = torch.cuda.mem_get_info(0)[0]  # (the text is allocated inside _build, 4 GB + 16 B)
@@ -171,8 +174,9 @@ def test_c4_dna_4gb(variant, monkeypatch):
         assert info.locate_record_bytes == 64 * 4 ** info.prefix_k
         assert info.device_bytes > 110e9, info.device_bytes
     assert (info.full_sa_bytes > 0) == (variant != "plain_walk")
-    # C4: n / 4^15 = 3.7 rows per k-mer -> compact 16-B records
-    assert info.record_bytes == (0 if variant == "plain_walk" else 16)
+    # C4: n / 4^15 = 3.7 rows per k-mer -> compact 16-B records (occurrence lines only)
+    assert info.record_bytes == (0 if variant in ("plain_walk", "wavelet") else 16)
+    assert info.engine == {"auto": 1, "plain_walk": 1, "learned": 3, "wavelet": 0}[variant]
     assert info.prefix_bytes == max(info.record_bytes, 8) * info.prefix_sigma ** info.prefix_k
     P = _qtext(pkg, text, N, 20, 1_000_000)
     _check_qtext(idx, host, N, P, nloc=20_000)
@@ -199,13 +203,12 @@ def test_c4_dna_4gb(variant, monkeypatch):
 
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C5") == "1", reason="C5 disabled")
-@pytest.mark.parametrize("engine", ["auto", pytest.param("wavelet", marks=pytest.mark.skipif(
-    os.environ.get("CS_FM_C5_WAVELET") != "1", reason="opt-in (CS_FM_C5_WAVELET=1): 39 s of the suite's budget"))])
+@pytest.mark.parametrize("engine", ["auto", "wavelet"])
 def test_c5_dna_32gb_wide(engine, monkeypatch):
     """BASELINE configs[4]: 32 GB text (n >= 2^32) — wide index (u64 samples) built by
     the pass-by-pass bucketed suffix sorter, with occurrence lines (default for
-    DNA) or the wavelet matrix in 32-B wide rank lines (Line32W; round 5: opt-in — the same
-    wide layout runs at small n in every parity test's wide_wavelet variant)."""
+    DNA) or the wavelet matrix in 32-B wide rank lines (Line32W; opt-in in round 5, back in
+    the default suite in round 6: VERDICT r05 item 3)."""
     if engine == "wavelet":
         monkeypatch.setenv("CS_FM_ENGINE", "wavelet")
     pkg = load_pkg()
