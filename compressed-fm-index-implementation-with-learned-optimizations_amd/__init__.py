@@ -65,7 +65,8 @@ class cs_fm_info(C.Structure):
                 ("locate_record_width", C.c_uint64), ("device_bytes", C.c_uint64)]
 
 
-# Every entry point of include/cs_fmindex.h with its ctypes signature.
+# Every entry point of include/cs_fmindex.h (and cs_fmindex_diag.h, cs_fmindex_replica.h, cs_synth.h)
+# with its ctypes signature.
 SIGNATURES = {
     "cs_default_build_params": (None, [C.POINTER(cs_build_params)]),
     "cs_fm_build_from_text": (C.c_int, [_u8p, C.c_uint64, C.POINTER(cs_build_params), C.c_int,
@@ -102,38 +103,14 @@ SIGNATURES = {
     "cs_fm_import_alloc": (C.c_int, [C.c_char_p, C.c_uint64, C.c_int, C.POINTER(_vp),
                                      C.POINTER(_vp), C.c_uint32]),
     "cs_fm_import_commit": (C.c_int, [_vp]),
-    "cs_fm_count_batch_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
     "cs_fm_extract_device": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint64, _vp, _vp]),
-    "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
-    "cs_fm_count_bytes_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, C.c_uint32, _vp]),
     "cs_fm_locate_record_hits_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, _vp]),
-    "cs_fm_count_batch_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64,
-                                              C.POINTER(cs_count_out), C.c_uint32, _vp]),
     "cs_fm_workspace_bytes": (C.c_uint64, [_vp, C.c_uint64]),
-    "cs_fm_count_device_ws": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, C.POINTER(cs_count_out),
-                                        C.c_uint32, _vp, C.c_uint64, _vp]),
-    "cs_fm_locate_device_ws": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
-                                         C.POINTER(C.c_uint64), C.c_uint32, _vp, C.c_uint64, _vp]),
     "cs_fm_count_packed_device": (C.c_int, [_vp, _vp, C.c_uint32, C.c_uint64,
                                             C.POINTER(cs_count_out), C.c_uint32, _vp]),
-    "cs_fm_locate_ranges_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
-                                                _u64p, C.c_uint32, _vp]),
-    "cs_fm_locate_walk_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp,
-                                              C.c_uint32, _vp]),
     "cs_fm_locate_walk_steps_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp,
                                                  C.c_uint32, _vp]),
-    "cs_fm_count_fixed_device": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
-    "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
-                                             _u64p, _vp]),
-    "cs_fm_locate_walk_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
-    "cs_fm_locate_walk_device_async": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp]),
-    "cs_fm_locate_walk_device_async_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp,
-                                                    C.c_uint32, _vp]),
     "cs_fm_locate_check": (C.c_int, [_vp, _vp]),
-    "cs_fm_locate_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
-                                      C.POINTER(C.c_uint64), _vp]),
-    "cs_fm_locate_device_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
-                                         C.POINTER(C.c_uint64), C.c_uint32, _vp]),
     "cs_fm_level_rank1": (C.c_int, [_vp, C.c_int, _u64p, C.c_uint64, _u64p]),
     "cs_fm_wt_rank": (C.c_int, [_vp, _u8p, _u64p, C.c_uint64, _u64p]),
     "cs_fm_wt_access": (C.c_int, [_vp, _u64p, C.c_uint64, _u8p]),
@@ -150,6 +127,17 @@ SIGNATURES = {
                                            C.c_uint64, _vp, _vp, _vp]),
     "cs_synth_random_patterns_device": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64,
                                                    C.c_uint64, _vp, _vp, _vp]),
+    # round 6: one count and one locate entry (flags + optional workspace), the two locate phases
+    "cs_fm_count_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, C.POINTER(cs_count_out),
+                                     C.c_uint32, _vp, C.c_uint64, _vp]),
+    "cs_fm_locate_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp, C.c_uint64,
+                                      C.POINTER(C.c_uint64), C.c_uint32, _vp, C.c_uint64, _vp]),
+    "cs_fm_locate_ranges_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, _vp,
+                                             _u64p, C.c_uint32, _vp]),
+    "cs_fm_locate_walk_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp, C.c_uint32,
+                                           C.c_int, _vp]),
+    # include/cs_fmindex_diag.h (measurement twins; building blocks below)
+    "cs_fm_count_bytes_device": (C.c_int, [_vp, _vp, _vp, C.c_uint64, _vp, C.c_uint32, _vp]),
 }
 
 _lib = None
@@ -440,11 +428,12 @@ class FMIndex:
 
     # -- device-resident batches (raw device pointers, e.g. torch data_ptr()) --
     def count_batch_device(self, d_pats: int, d_offs: int, npat: int, d_out: int, stream: int = 0):
-        _check(lib().cs_fm_count_batch_device(self._h, d_pats, d_offs, npat, d_out, stream or None))
+        """count() of a device batch into uint64 counts (cs_fm_count_device, no flags)."""
+        self.count_device_ws(d_pats, d_offs, npat, d_out, 0, 0, stream=stream)
 
     def count_fixed_device(self, d_pats: int, m: int, npat: int, d_out: int, stream: int = 0):
         """count of npat patterns of length m laid out back to back (no offsets array)."""
-        _check(lib().cs_fm_count_fixed_device(self._h, d_pats, m, npat, d_out, stream or None))
+        self.count_device_ws(d_pats, None, npat, d_out, 0, 0, fixed_m=m, stream=stream)
 
     def extract_device(self, d_pos, d_len, d_out_offs, k, d_out, stream=0):
         """Batched extract with device buffers (d_out_offs = scan of clamped lengths)."""
@@ -453,13 +442,12 @@ class FMIndex:
 
     def count_device_ex(self, d_pats, d_offs, npat, d_out, width=8, flags=0, fixed_m=0,
                         d_exc=None, exc_cap=0, d_exc_n=None, stream=0):
-        """count() of a device batch, general form (cs_fm_count_batch_device_ex): d_offs
-        or None for npat patterns of length fixed_m back to back; counts as uint64
+        """count() of a device batch, general form (cs_fm_count_device without a workspace):
+        d_offs or None for npat patterns of length fixed_m back to back; counts as uint64
         (width 8), uint32 (4) or uint8 with (index, count) pairs for counts >= 255 (1);
         flags Q_* leave structures out (same results)."""
-        o = cs_count_out(d_out, width, d_exc, exc_cap, d_exc_n)
-        _check(lib().cs_fm_count_batch_device_ex(self._h, d_pats, d_offs, fixed_m, npat,
-                                                 C.byref(o), flags, stream or None))
+        self.count_device_ws(d_pats, d_offs, npat, d_out, 0, 0, width, flags, fixed_m, d_exc, exc_cap,
+                             d_exc_n, stream)
 
     def workspace_bytes(self, npat: int) -> int:
         """Device workspace for a count or one-call locate of up to npat patterns
@@ -468,19 +456,19 @@ class FMIndex:
 
     def count_device_ws(self, d_pats, d_offs, npat, d_out, d_work, work_bytes, width=8, flags=0,
                         fixed_m=0, d_exc=None, exc_cap=0, d_exc_n=None, stream=0):
-        """count_device_ex with the caller's workspace (cs_fm_count_device_ws): no allocation
-        inside the call."""
+        """count() of a device batch (cs_fm_count_device) with the caller's workspace (no
+        allocation inside the call; d_work 0: none)."""
         o = cs_count_out(d_out, width, d_exc, exc_cap, d_exc_n)
-        _check(lib().cs_fm_count_device_ws(self._h, d_pats, d_offs, fixed_m, npat, C.byref(o), flags,
-                                           d_work or None, work_bytes, stream or None))
+        _check(lib().cs_fm_count_device(self._h, d_pats, d_offs or None, fixed_m, npat, C.byref(o), flags,
+                                        d_work or None, work_bytes, stream or None))
 
     def locate_device_ws(self, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, d_work,
                          work_bytes, stream=0, flags=0):
-        """locate_device with the caller's workspace (cs_fm_locate_device_ws)."""
+        """locate_device with the caller's workspace (cs_fm_locate_device; d_work 0: none)."""
         total = C.c_uint64()
-        st = lib().cs_fm_locate_device_ws(self._h, d_pats, d_offs, npat, limit, d_out_offs,
-                                          d_out_pos or None, cap, C.byref(total), flags,
-                                          d_work or None, work_bytes, stream or None)
+        st = lib().cs_fm_locate_device(self._h, d_pats, d_offs, npat, limit, d_out_offs,
+                                       d_out_pos or None, cap, C.byref(total), flags,
+                                       d_work or None, work_bytes, stream or None)
         if st == CS_ERR_CAPACITY:
             return total.value, False
         _check(st)
@@ -496,8 +484,8 @@ class FMIndex:
 
     def count_bytes_device(self, d_pats, d_offs, npat, d_out, stream=0, flags=0):
         """Per-query algorithmic HBM bytes of the search (roofline accounting)."""
-        _check(lib().cs_fm_count_bytes_device_ex(self._h, d_pats, d_offs, npat, d_out, flags,
-                                                 stream or None))
+        _check(lib().cs_fm_count_bytes_device(self._h, d_pats, d_offs, npat, d_out, flags,
+                                              stream or None))
 
     def locate_record_hits_device(self, d_pats, d_offs, npat, d_hit, stream=0):
         """Per pattern 1 when the locate records answer it in one read (roofline accounting)."""
@@ -507,31 +495,24 @@ class FMIndex:
     def locate_ranges_device(self, d_pats, d_offs, npat, limit, d_sp, d_out_offs, stream=0,
                              flags=0) -> int:
         total = C.c_uint64()
-        _check(lib().cs_fm_locate_ranges_device_ex(self._h, d_pats, d_offs, npat, limit, d_sp,
-                                                   d_out_offs, C.byref(total), flags,
-                                                   stream or None))
+        _check(lib().cs_fm_locate_ranges_device(self._h, d_pats, d_offs, npat, limit, d_sp,
+                                                d_out_offs, C.byref(total), flags,
+                                                stream or None))
         return total.value
 
     def locate_walk_device(self, d_sp, d_out_offs, npat, total, d_out_pos, stream=0, sync=True,
                            flags=0):
-        if flags:
-            f = lib().cs_fm_locate_walk_device_ex if sync else lib().cs_fm_locate_walk_device_async_ex
-            _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, flags, stream or None))
-            return
-        f = lib().cs_fm_locate_walk_device if sync else lib().cs_fm_locate_walk_device_async
-        _check(f(self._h, d_sp, d_out_offs, npat, total, d_out_pos, stream or None))
+        """locate phase 2 (cs_fm_locate_walk_device); sync False: the overrun error goes to the
+        next locate_check."""
+        _check(lib().cs_fm_locate_walk_device(self._h, d_sp, d_out_offs, npat, total, d_out_pos, flags,
+                                              1 if sync else 0, stream or None))
 
     def locate_device(self, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, stream=0, flags=0):
-        """locate of a batch in one call (cs_fm_locate_device[_ex]): offsets and, when they fit
-        `cap`, positions -> (total, positions_written).  flags: Q_LONG sends every pattern
-        to the long-pattern search."""
-        total = C.c_uint64()
-        st = lib().cs_fm_locate_device_ex(self._h, d_pats, d_offs, npat, limit, d_out_offs,
-                                          d_out_pos or None, cap, C.byref(total), flags, stream or None)
-        if st == CS_ERR_CAPACITY:
-            return total.value, False
-        _check(st)
-        return total.value, True
+        """locate of a batch in one call (cs_fm_locate_device, no workspace): offsets and, when
+        they fit `cap`, positions -> (total, positions_written).  flags: Q_LONG sends every
+        pattern to the long-pattern search."""
+        return self.locate_device_ws(d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, 0, 0,
+                                     stream, flags)
 
     def locate_walk_steps_device(self, d_sp, d_out_offs, npat, total, d_steps, stream=0, flags=0):
         """LF steps of each reported row's walk (measurement twin of the walk)."""

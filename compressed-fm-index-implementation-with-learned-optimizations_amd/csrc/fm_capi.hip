@@ -477,6 +477,7 @@ void free_index(cs_fm_index* h) {
   if (h->d_ptext) (void)hipFree(h->d_ptext);
   if (h->d_lrec) (void)hipFree(h->d_lrec);
   if (h->d_prare) (void)hipFree(h->d_prare);
+  if (h->d_prare64) (void)hipFree(h->d_prare64);
   if (h->d_walk) (void)hipFree(h->d_walk);
   if (h->d_wssa) (void)hipFree(h->d_wssa);
   if (h->d_lctx) (void)hipFree(h->d_lctx);
@@ -659,48 +660,9 @@ static cs_status null_pats_ok(const uint8_t* d_pats, const uint64_t* d_offs, uin
   return CS_OK;
 }
 
-cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
-                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
-                                   void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (npat && (!d_offs || !d_out)) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  if ((s = null_pats_ok(d_pats, d_offs, npat, (hipStream_t)stream)) != CS_OK) return s;
-  return launch_count(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
-}
-
-cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, uint64_t m,
-                                   uint64_t npat, uint64_t* d_out, void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (npat && (!d_out || (m && !d_pats))) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  return launch_count(h, d_pats, nullptr, npat, d_out, (hipStream_t)stream, m);
-}
-
 cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
                                    const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
-                                   void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (npat && (!d_offs || !d_out)) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  return launch_count_bytes(h, d_pats, d_offs, npat, d_out, (hipStream_t)stream);
-}
-
-cs_status cs_fm_count_bytes_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
-                                      const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
-                                      uint32_t flags, void* stream) {
+                                   uint32_t flags, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
@@ -756,21 +718,15 @@ uint64_t cs_fm_workspace_bytes(const cs_fm_index* h, uint64_t npat) {
   return c > l ? c : l;
 }
 
-cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
-                                      const uint64_t* d_offs, uint64_t fixed_m, uint64_t npat,
-                                      const cs_count_out* out, uint32_t flags, void* stream) {
-  return cs_fm_count_device_ws(h, d_pats, d_offs, fixed_m, npat, out, flags, nullptr, 0, stream);
-}
-
-cs_status cs_fm_count_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                                uint64_t fixed_m, uint64_t npat, const cs_count_out* out,
-                                uint32_t flags, void* d_work, uint64_t work_bytes, void* stream) {
+cs_status cs_fm_count_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                             uint64_t fixed_m, uint64_t npat, const cs_count_out* out,
+                             uint32_t flags, void* d_work, uint64_t work_bytes, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
   CountOut co;
   if ((s = count_out(h, out, npat, co)) != CS_OK) return s;
-  if (npat && !d_pats && !d_offs && fixed_m) {  // the same rule as cs_fm_count_fixed_device
+  if (npat && !d_pats && !d_offs && fixed_m) {  // (a fixed-length batch of non-empty patterns)
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
@@ -998,49 +954,6 @@ cs_status cs_fm_count(const cs_fm_index* h, const uint8_t* pattern, uint64_t m, 
   return cs_fm_count_batch(h, pattern, offs, 1, out, nullptr);
 }
 
-cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
-                                     const uint64_t* d_offs, uint64_t npat, uint64_t limit,
-                                     uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
-                                     void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (!total || !d_out_offs || (npat && (!d_offs || !d_sp))) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  return launch_locate_ranges(h, d_pats, d_offs, npat, limit, d_sp, d_out_offs, total,
-                              (hipStream_t)stream);
-}
-
-cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d_sp,
-                                         const uint64_t* d_out_offs, uint64_t npat,
-                                         uint64_t total, uint64_t* d_out_pos, void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  return launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream);
-}
-
-cs_status cs_fm_locate_walk_device_async_ex(const cs_fm_index* h, const uint64_t* d_sp,
-                                            const uint64_t* d_out_offs, uint64_t npat,
-                                            uint64_t total, uint64_t* d_out_pos, uint32_t flags,
-                                            void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  return launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream,
-                            nullptr, flags);
-}
-
 cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
@@ -1064,10 +977,10 @@ static cs_status walk_checked(const cs_fm_index* h, const uint64_t* d_sp,
   return check_locate_error(h, e, st);
 }
 
-cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
-                                        const uint64_t* d_offs, uint64_t npat, uint64_t limit,
-                                        uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
-                                        uint32_t flags, void* stream) {
+cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
+                                     const uint64_t* d_offs, uint64_t npat, uint64_t limit,
+                                     uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
+                                     uint32_t flags, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
@@ -1080,10 +993,10 @@ cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_p
                               (hipStream_t)stream, flags);
 }
 
-cs_status cs_fm_locate_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
-                                 void* d_work, uint64_t work_bytes, void* stream) {
+cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
+                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
+                              void* d_work, uint64_t work_bytes, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
@@ -1123,23 +1036,9 @@ cs_status cs_fm_locate_device_ws(const cs_fm_index* h, const uint8_t* d_pats, co
   return CS_OK;
 }
 
-cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
-                                 void* stream) {
-  return cs_fm_locate_device_ws(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, flags,
-                                nullptr, 0, stream);
-}
-
-cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream) {
-  return cs_fm_locate_device_ex(h, d_pats, d_offs, npat, limit, d_out_offs, d_out_pos, cap, total, 0, stream);
-}
-
-cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
-                                      const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                                      uint64_t* d_out_pos, uint32_t flags, void* stream) {
+cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,
+                                   const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
+                                   uint64_t* d_out_pos, uint32_t flags, int sync, void* stream) {
   DeviceScope dscope;
   cs_status s = check_handle(h, dscope);
   if (s != CS_OK) return s;
@@ -1147,6 +1046,8 @@ cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp
     set_error("null batch pointer");
     return CS_ERR_INVALID;
   }
+  if (!sync)  // the overrun flag goes to the next cs_fm_locate_check
+    return launch_locate_walk(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream, nullptr, flags);
   return walk_checked(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream, flags);
 }
 
@@ -1162,19 +1063,6 @@ cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d
     return CS_ERR_INVALID;
   }
   return walk_checked(h, d_sp, d_out_offs, npat, total, d_steps, (hipStream_t)stream, flags, 1);
-}
-
-cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,
-                                   const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                                   uint64_t* d_out_pos, void* stream) {
-  DeviceScope dscope;
-  cs_status s = check_handle(h, dscope);
-  if (s != CS_OK) return s;
-  if (total && (!d_sp || !d_out_offs || !d_out_pos)) {
-    set_error("null batch pointer");
-    return CS_ERR_INVALID;
-  }
-  return walk_checked(h, d_sp, d_out_offs, npat, total, d_out_pos, (hipStream_t)stream);
 }
 
 cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const uint64_t* offs,

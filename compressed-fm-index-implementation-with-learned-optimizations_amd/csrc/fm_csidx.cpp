@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/cs_fmindex.h"
+#include "../../include/cs_fmindex_diag.h"
 
 namespace fmx {
 void set_error(const std::string& msg);  // fm_capi.hip: cs_fm_last_error()'s text

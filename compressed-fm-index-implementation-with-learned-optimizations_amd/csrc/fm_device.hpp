@@ -130,6 +130,10 @@ struct DevIndex {
   // verified against it at the position their short walk gives (k_count_long kWalk) instead
   // of stepping every character.  Null otherwise or under CS_Q_NO_CONTEXTS / CS_Q_NO_VERIFY.
   const uint8_t* wtext;
+  // ... and its rare-symbol positions (u64, sorted; the packed text stores them as code 0) when
+  // the walk-verified long patterns compare against the 2-bit text (ptext, no full SA)
+  const uint64_t* wrare;
+  uint32_t nwrare;
   // The same text 2-bit packed (occurrence codes, character i at bits 2 (i % 32) of word
   // i / 32, rare symbols as code 0) and the sorted positions of the rare symbols: long
   // patterns are verified against 32 characters per 8-B word (k_count_long).  Null

@@ -10,6 +10,8 @@
 
 #include "../../include/cs_fmindex.h"
 #include "../../include/cs_fmindex_tuning.h"
+#include "../../include/cs_fmindex_diag.h"
+#include "../../include/cs_fmindex_replica.h"
 #include "fm_device.hpp"
 
 struct cs_fm_index {
@@ -60,6 +62,16 @@ struct cs_fm_index {
   void* d_ptext = nullptr;
   void* d_prare = nullptr;
   uint32_t nrare = 0;
+  // (round 6) the same as u64 positions for an index whose long patterns are verified at
+  // their walks' positions (walk_verify()): n may pass 2^32 there
+  void* d_prare64 = nullptr;
+  uint32_t nrare64 = 0;
+  // lf_exact occurrence lines with walk lines and text-position marks and no full SA (C5):
+  // k_count_long positions a long pattern's candidate rows by their short walks and verifies
+  // them against the text (the 2-bit text d_ptext, else the byte text d_dtext)
+  bool walk_verify() const {
+    return !d_sa && d_walk && d_wssa && walk_marks == 2 && lf_exact && line_fmt == fmx::kFmtOcc;
+  }
   uint64_t ptext_bytes() const { return ((n + 31) / 32) * 8; }
   // Locate records (fmx::DevIndex::lrec): 64 B per ptab_k-mer (lrec_w 64, the default) or
   // 16 B per (ptab_k + 1)-mer (lrec_w 16), derived from the context records, the left
@@ -155,9 +167,10 @@ struct cs_fm_index {
     const bool ver = d_sa && d_dtext && lf_exact && !wide;
     d.vsa = ver ? static_cast<const uint32_t*>(d_sa) : nullptr;
     d.vtext = ver ? static_cast<const uint8_t*>(d_dtext) : nullptr;
-    d.wtext = !d_sa && d_dtext && d_walk && d_wssa && walk_marks == 2 && lf_exact && line_fmt == fmx::kFmtOcc
-                  ? static_cast<const uint8_t*>(d_dtext) : nullptr;
-    d.ptext = ver && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
+    d.wtext = walk_verify() && d_dtext ? static_cast<const uint8_t*>(d_dtext) : nullptr;
+    d.ptext = (ver || walk_verify()) && d_ptext ? static_cast<const uint64_t*>(d_ptext) : nullptr;
+    d.wrare = static_cast<const uint64_t*>(d_prare64);
+    d.nwrare = nrare64;
     d.prare = static_cast<const uint32_t*>(d_prare);
     d.lrec = d_sa && lf_exact && !wide ? d_lrec : nullptr;
     d.lrec64 = lrec_w == 64 ? 1u : 0u;
@@ -276,7 +289,10 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st);
 cs_status build_context_records(cs_fm_index* h, hipStream_t st);
 cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st);
 // the 2-bit text of d_dtext (cs_fm_index::d_ptext), when the index can use it (fm_query.hip)
-cs_status derive_packed_text(cs_fm_index* h, hipStream_t st);
+// (src: the build's device text when the index does not keep one — its 2-bit form is still
+// derived for walk_verify() indexes; the buffer is the caller's input, not counted against the
+// eighth of HBM the built index leaves free)
+cs_status derive_packed_text(cs_fm_index* h, hipStream_t st, const uint8_t* src = nullptr);
 // the locate records (cs_fm_index::d_lrec, fm_device.hpp kLocRec*) when the index can use them
 cs_status derive_locate_records(cs_fm_index* h, hipStream_t st);
 // both derived parts (open / import)
@@ -291,7 +307,9 @@ uint64_t device_bytes(const cs_fm_index* h);
 // Whether an optional structure of `bytes` may be allocated: the device keeps an eighth
 // of its HBM free (query buffers), and with a budget the index stays within it — `freed`
 // bytes of the index are released once the structure is built (a replacement).
-bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed = 0);
+// `transient`: device bytes in use now that are not the index's and go away after the build
+// (the caller's text): counted as free for the eighth, not for the allocation itself.
+bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed = 0, uint64_t transient = 0);
 // CS_FM_HBM_BUDGET: bytes, with an optional K / M / G / T suffix (powers of 1000); 0 = none
 uint64_t hbm_budget_env();
 cs_status launch_lf(const cs_fm_index* h, const uint64_t* d_rows, uint64_t k, uint64_t* d_out,

@@ -245,18 +245,19 @@ uint64_t device_bytes(const cs_fm_index* hc) {
   if (h->d_ptext) b += h->ptext_bytes() + kPartPad;  // derived parts
   b += h->lrec_bytes();
   if (h->d_prare) b += kMaxExc * 4;
+  if (h->d_prare64) b += kMaxExc * 8;
   if (h->d_err) b += 8;
   if (h->scratch.d) b += cs_fm_index::kScratchBytes;  // the small-batch arena
   return b;
 }
 
-bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed) {
+bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed, uint64_t transient) {
   size_t free_b = 0, total_b = 0;
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return false;
   // the built index leaves an eighth free; a replacement (freed > 0) needs both copies
   // for a moment, within 2 GB of the device's free memory
   const uint64_t net = bytes > freed ? bytes - freed : 0;
-  if (net + total_b / 8 > free_b || bytes + (2ull << 30) > free_b) return false;
+  if (net + total_b / 8 > free_b + transient || bytes + (2ull << 30) > free_b) return false;
   if (!h->hbm_budget) return true;
   const uint64_t have = index_hbm_bytes(h);
   return have + bytes <= h->hbm_budget + freed;

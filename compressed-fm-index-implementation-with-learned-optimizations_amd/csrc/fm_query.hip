@@ -1232,6 +1232,9 @@ static_assert(kLocTile == kLongRegion, "a tile is a region: one block's patterns
 // lockstep (their line reads in flight together) — defined with the walks below
 template <class W>
 __device__ __forceinline__ uint64_t walk_position(const DevIndex& ix, const NodeTable& T, uint64_t row);
+template <class W>
+__device__ __forceinline__ uint64_t walk_position_steps(const DevIndex& ix, const NodeTable& T, uint64_t row,
+                                                        uint64_t& steps);
 template <class W, int U>
 __device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTable& T, uint64_t* pos,
                                                bool* act);
@@ -3010,6 +3013,34 @@ __device__ __forceinline__ void locate_list_general(const DevIndex& ix, NodeTabl
                                                     const OnePass& op, const LongList& ll, uint32_t c);
 
 // k_count_long's search of one pattern q (< npat, the batch's offsets or fixed_m)
+// whether a u64 text position of a rare symbol lies in [q, q + L) (sorted list in global
+// memory; walk_verify() indexes hold a handful — C5: the terminator)
+__device__ __forceinline__ bool rare_in64(const uint64_t* __restrict__ r, uint32_t nr, uint64_t q, uint64_t L) {
+  uint32_t lo = 0, hi = nr;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (r[mid] < q) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo < nr && r[lo] < q + L;
+}
+// A walk-verified candidate's window text[q, q + L) against P[0, L): 1 equal, 0 not, 2 not
+// decidable here (a window through the text's end, or past the packed codes in pc, on an index
+// that keeps no byte text): the pattern takes the general search.
+template <bool kPT, bool kV>
+__device__ __forceinline__ int window_eq_walk(const DevIndex& ix, const uint64_t* pc, const uint8_t* P,
+                                              uint64_t q, uint64_t L) {
+  if constexpr (kPT) {
+    if (q + L <= ix.n && L <= 32ull * kLongPW) {
+      if (!packed_chunk_eq<kV>(ix, pc, q, L)) return 0;
+      // (a rare symbol's code 0 in the packed text stands for no pattern character)
+      return rare_in64(ix.wrare, ix.nwrare, q, L) ? 0 : 1;
+    }
+  }
+  if (ix.wtext) return window_eq_long<kLongWords>(ix, ix.wtext, P, q, L) ? 1 : 0;
+  return 2;
+}
+
 // kWalk (round 6): an index without the full suffix array (DevIndex::wtext:
 // walk lines with text-position marks, the byte text; C5) takes each candidate row's position
 // from its short walk (walk_positions_k: <= pstride - 1 LF steps over walk lines, then the
@@ -3035,7 +3066,8 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
   uint64_t pc[kLongPW];  // kPT: the codes of P[0, k)
   uint64_t base;
   uint32_t cand, qf;
-  const bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+  bool general = !long_stage<kPT, kBytes, kV16>(ix, pats, o0, m, cmap, pc, base, cand, qf, by);
+  bool wgen = false;  // kWalk
   uint64_t res = 0;
   if (!general) {
     // (D) + (E): each candidate's SA entry, then its window (usually one candidate)
@@ -3043,20 +3075,24 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
     while (cand) {
       const uint32_t i = (uint32_t)__ffs(cand) - 1u;
       cand &= cand - 1;
-      uint64_t p;
+      uint64_t p, wsteps = 0;
       if constexpr (kWalk != 0) {
         using WL = std::conditional_t<kWalk == 1, WalkLine, WalkLineW>;
-        uint64_t pos[1] = {base + i};
-        bool act[1] = {true};
-        walk_positions_k<WL, 1>(ix, *ix.table, walk_consts(*ix.table), pos, act);
-        p = pos[0];
+        if constexpr (kBytes) {  // (the twin counts the walk's lines)
+          p = walk_position_steps<WL>(ix, *ix.table, base + i, wsteps);
+        } else {
+          uint64_t pos[1] = {base + i};
+          bool act[1] = {true};
+          walk_positions_k<WL, 1>(ix, *ix.table, walk_consts(*ix.table), pos, act);
+          p = pos[0];
+        }
       } else {
         p = load_sa(ix.vsa, base + i);
       }
       const uint64_t wq = p >= k ? p - k : p + n - k;
-      if constexpr (kBytes) {  // the SA sector, then the window's words
+      if constexpr (kBytes) {  // the SA sector (walk: its lines and the sample), then the window's words
         constexpr uint64_t C = 32ull * kLongPW;
-        by += 32;
+        by += kWalk ? 32 * (wsteps + 1) + 8 : 32;
         if (wq + L > n) by += 64;  // byte by byte, as window_eq counts it
         else if (!kPT) by += 8 * (((wq + L - 1) >> 3) - (wq >> 3) + 1);
         else  // the packed window's 32-B sectors (its bytes [q / 4, (q + L) / 4) rounded out)
@@ -3065,11 +3101,22 @@ __device__ __forceinline__ void count_long_one(const DevIndex& ix, const uint8_t
         continue;
       }
       bool eq;
-      if constexpr (kPT) eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
-      else eq = window_eq_long<kLongWords>(ix, kWalk ? ix.wtext : ix.vtext, pats + o0, wq, L);
+      if constexpr (kWalk != 0) {
+        const int r = window_eq_walk<kPT, kV16 == 3>(ix, pc, pats + o0, wq, L);
+        if (r == 2) {
+          wgen = true;
+          break;
+        }
+        eq = r == 1;
+      } else if constexpr (kPT) {
+        eq = window_eq_packed<kV16 == 3>(ix, pc, pats + o0, wq, L, rare);
+      } else {
+        eq = window_eq_long<kLongWords>(ix, ix.vtext, pats + o0, wq, L);
+      }
       res += eq ? 1u : 0u;
     }
   }
+  if (wgen) general = true;  // (a window the walk path cannot decide: the general search)
   long_list_append(general, q, ll);
   if (general) return;
   if constexpr (kBytes) static_cast<uint64_t*>(co.out)[q] = by;
@@ -3100,7 +3147,7 @@ __global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(kList ? 4 
   }
   if (threadIdx.x < 256)
     cmap[threadIdx.x] = (uint16_t)(ix.table->code[threadIdx.x] | (ix.table->occ_code[threadIdx.x] << 8));
-  if (kPT && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
+  if (kPT && !kWalk && threadIdx.x < ix.nrare) rare[threadIdx.x] = ix.prare[threadIdx.x];
   __syncthreads();
   if constexpr (kList) {
     list_for_each(ll.list, c1, [&](uint64_t q, bool act) {
@@ -4091,6 +4138,32 @@ __device__ __forceinline__ uint64_t walk_position(const DevIndex& ix, const Node
   return 0;
 }
 
+// walk_position and the LF steps it took (measurement twin: bench.py's walk bytes)
+template <class W>
+__device__ __forceinline__ uint64_t walk_position_steps(const DevIndex& ix, const NodeTable& T, uint64_t pos,
+                                                        uint64_t& steps_out) {
+  const uint64_t n = ix.n;
+  const uint64_t row_mask = ix.stride_shift != 0xFFFFFFFFu ? (1ull << ix.stride_shift) - 1 : 0;
+  for (uint64_t steps = 0; steps < n; ++steps) {
+    uint64_t q;
+    uint32_t o;
+    typename W::Raw v;
+    W::locate(pos, q, o);
+    W::load(ix.walk, q, v);
+    const bool mk = W::mark(v, o);
+    const bool rs = row_mask ? (pos & row_mask) == 0 : pos % ix.stride == 0;
+    if (mk || rs) {
+      const uint64_t sidx = mk ? W::mark_rank(v, o) : (row_mask ? pos >> ix.stride_shift : pos / ix.stride);
+      const uint64_t s = (mk ? wssa_at(ix, sidx) : ssa_at(ix, sidx)) + steps;
+      steps_out = steps;
+      return s >= n ? s - n : s;
+    }
+    pos = walk_lf<W, false>(ix, T, v, q, o, pos);
+  }
+  steps_out = n;
+  return 0;
+}
+
 template <class W, int U>
 __device__ __forceinline__ void walk_positions(const DevIndex& ix, const NodeTable& T, uint64_t* pos,
                                                bool* act) {
@@ -4861,9 +4934,12 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
 // CS_FM_DEVICE_TEXT=0 leaves extract to LF inversion from the inverse-SA samples.
 cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st) {
   if (!src || !h->n || h->d_dtext) return CS_OK;
+  // (round 6: without the byte text, a walk_verify() index still takes the 2-bit text of the
+  // build's device text — C5: 8 GB where the 32-GB text does not fit the eighth)
+  const uint8_t* dsrc = src_on_device ? src : nullptr;
   if (const char* e = std::getenv("CS_FM_DEVICE_TEXT"))
-    if (std::atoi(e) == 0) return CS_OK;
-  if (!hbm_room(h, h->n)) return CS_OK;
+    if (std::atoi(e) == 0) return derive_packed_text(h, st, dsrc);
+  if (!hbm_room(h, h->n)) return derive_packed_text(h, st, dsrc);
   FMX_HIP(hipMalloc(&h->d_dtext, h->n + kPartPad));
   FMX_HIP(hipMemsetAsync(static_cast<uint8_t*>(h->d_dtext) + h->n, 0, kPartPad, st));
   FMX_HIP(hipMemcpyAsync(h->d_dtext, src, h->n,
@@ -4878,7 +4954,7 @@ cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_devic
 __global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ text, uint64_t n,
                                                     const NodeTable* __restrict__ table,
                                                     uint64_t* __restrict__ out, uint64_t nw,
-                                                    uint32_t* __restrict__ rare, uint32_t cap,
+                                                    uint64_t* __restrict__ rare, uint32_t cap,
                                                     unsigned int* __restrict__ nrare) {
   __shared__ uint8_t code[256];
   if (threadIdx.x < 256) code[threadIdx.x] = table->occ_code[threadIdx.x];
@@ -4897,7 +4973,7 @@ __global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ 
       const uint32_t d = code[(uint32_t)(x >> (8 * b)) & 0xFFu];
       if (d == kNoCode) {
         const unsigned int e = atomicAdd(nrare, 1u);
-        if (e < cap) rare[e] = (uint32_t)i;
+        if (e < cap) rare[e] = i;
       } else {
         acc |= (uint64_t)d << (2 * (8 * c + b));
       }
@@ -4906,39 +4982,83 @@ __global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ 
   out[w] = acc;
 }
 
+// the last, partial word of the 2-bit text (`len` < 32 characters at text position `at`,
+// from a zero-padded copy): one lane
+__global__ void k_pack_text_tail(const uint8_t* __restrict__ text, uint64_t len, uint64_t at,
+                                 const NodeTable* __restrict__ table, uint64_t* __restrict__ out,
+                                 uint64_t* __restrict__ rare, uint32_t cap, unsigned int* __restrict__ nrare) {
+  if (threadIdx.x != 0) return;
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < len; ++i) {
+    const uint32_t d = table->occ_code[text[i]];
+    if (d == kNoCode) {
+      const unsigned int e = atomicAdd(nrare, 1u);
+      if (e < cap) rare[e] = at + i;
+    } else {
+      acc |= (uint64_t)d << (2 * i);
+    }
+  }
+  *out = acc;
+}
+
 // Long patterns are verified against 32 text characters per 8-B word instead of 8
 // (k_count_long): n / 4 bytes (C4: 1 GB), for narrow lf_exact occurrence-line indexes that
-// keep the full suffix array and the text in HBM (the verification's preconditions), HBM
-// allowing.  Derived from the text, so it is rebuilt on open / import rather than saved.
-// CS_FM_PACKED_TEXT=0 (read at build / open) leaves it out.
-cs_status derive_packed_text(cs_fm_index* h, hipStream_t st) {
-  if (h->d_ptext || !h->d_dtext || !h->d_sa || !h->lf_exact || h->wide || h->line_fmt != kFmtOcc ||
-      h->n >= (1ull << 32))
-    return CS_OK;
+// keep the full suffix array and the text in HBM (the verification's preconditions), and
+// (round 6) for walk_verify() indexes — no full SA, walk lines with text-position marks (C5:
+// 8 GB), whose long patterns are verified at their walks' positions — HBM allowing.  Derived
+// from the text kept in HBM or, for walk_verify() indexes, from the build's device text
+// `src`; rebuilt on open / import rather than saved.  The rare-symbol positions go to d_prare
+// (u32, narrow) or d_prare64 (u64, walk_verify()).  CS_FM_PACKED_TEXT=0 (read at build /
+// open) leaves it out.
+cs_status derive_packed_text(cs_fm_index* h, hipStream_t st, const uint8_t* src) {
+  if (h->d_ptext || h->line_fmt != kFmtOcc || !h->lf_exact || !h->n) return CS_OK;
+  const bool narrow_sa = h->d_sa && !h->wide && h->n < (1ull << 32);
+  const bool walk = h->walk_verify();
+  const uint8_t* text = h->d_dtext ? static_cast<const uint8_t*>(h->d_dtext) : src;
+  if (!text || !(narrow_sa || walk)) return CS_OK;
+  if (narrow_sa && !h->d_dtext) return CS_OK;  // (its verification reads the byte text too)
   if (const char* e = std::getenv("CS_FM_PACKED_TEXT"))
     if (std::atoi(e) == 0) return CS_OK;
   const uint64_t nw = (h->n + 31) / 32;
-  if (!hbm_room(h, nw * 8)) return CS_OK;
+  if (!hbm_room(h, nw * 8, 0, h->d_dtext ? 0 : h->n)) return CS_OK;
   void* pt = nullptr;
   FMX_HIP(hipMalloc(&pt, nw * 8 + kPartPad));
   DevBuf rb;
-  if (rb.alloc(kMaxExc * 4 + 8) != hipSuccess) {
+  if (rb.alloc(kMaxExc * 8 + 8) != hipSuccess) {
     (void)hipFree(pt);
     return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
   }
-  unsigned int* d_n = reinterpret_cast<unsigned int*>(rb.as<uint8_t>() + kMaxExc * 4);
+  unsigned int* d_n = reinterpret_cast<unsigned int*>(rb.as<uint8_t>() + kMaxExc * 8);
   hipError_t e = hipMemsetAsync(d_n, 0, 4, st);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && !h->d_dtext) {
+    // (the caller's text has no kPartPad slack: the last word is packed from a padded copy)
+    const uint64_t full = h->n / 32;
+    if (full)
+      k_pack_text<<<grid_for(full, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(text, full * 32, h->d_table,
+                                                                        static_cast<uint64_t*>(pt), full,
+                                                                        rb.as<uint64_t>(), kMaxExc, d_n);
+    e = hipGetLastError();
+    if (e == hipSuccess && full < nw) {
+      DevBuf tail;
+      e = tail.alloc(64);
+      if (e == hipSuccess) e = hipMemsetAsync(tail.p, 0, 64, st);
+      if (e == hipSuccess) e = hipMemcpyAsync(tail.p, text + full * 32, h->n - full * 32, hipMemcpyDeviceToDevice, st);
+      if (e == hipSuccess)
+        k_pack_text_tail<<<1, 64, 0, st>>>(tail.as<uint8_t>(), h->n - full * 32, full * 32, h->d_table,
+                                           static_cast<uint64_t*>(pt) + full, rb.as<uint64_t>(), kMaxExc, d_n);
+      if (e == hipSuccess) e = hipGetLastError();
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+    }
+  } else if (e == hipSuccess) {
     k_pack_text<<<grid_for(nw, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        static_cast<const uint8_t*>(h->d_dtext), h->n, h->d_table, static_cast<uint64_t*>(pt), nw,
-        rb.as<uint32_t>(), kMaxExc, d_n);
+        text, h->n, h->d_table, static_cast<uint64_t*>(pt), nw, rb.as<uint64_t>(), kMaxExc, d_n);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(pt) + nw * 8, 0, kPartPad, st);
   unsigned int nr = 0;
-  std::vector<uint32_t> pos(kMaxExc);
+  std::vector<uint64_t> pos(kMaxExc);
   if (e == hipSuccess) e = hipMemcpyAsync(&nr, d_n, 4, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(pos.data(), rb.p, kMaxExc * 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(pos.data(), rb.p, kMaxExc * 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (e != hipSuccess || nr > (unsigned)kMaxExc) {  // more rare positions than the list holds
     (void)hipFree(pt);
@@ -4947,15 +5067,27 @@ cs_status derive_packed_text(cs_fm_index* h, hipStream_t st) {
   pos.resize(nr);
   std::sort(pos.begin(), pos.end());
   void* pr = nullptr;
-  if (hipMalloc(&pr, kMaxExc * 4) != hipSuccess ||
-      (nr && hipMemcpy(pr, pos.data(), nr * 4, hipMemcpyHostToDevice) != hipSuccess)) {
-    (void)hipFree(pt);
-    if (pr) (void)hipFree(pr);
-    return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
+  if (walk) {
+    if (hipMalloc(&pr, kMaxExc * 8) != hipSuccess ||
+        (nr && hipMemcpy(pr, pos.data(), nr * 8, hipMemcpyHostToDevice) != hipSuccess)) {
+      (void)hipFree(pt);
+      if (pr) (void)hipFree(pr);
+      return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
+    }
+    h->d_prare64 = pr;
+    h->nrare64 = nr;
+  } else {
+    std::vector<uint32_t> p32(pos.begin(), pos.end());
+    if (hipMalloc(&pr, kMaxExc * 4) != hipSuccess ||
+        (nr && hipMemcpy(pr, p32.data(), nr * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+      (void)hipFree(pt);
+      if (pr) (void)hipFree(pr);
+      return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
+    }
+    h->d_prare = pr;
+    h->nrare = nr;
   }
   h->d_ptext = pt;
-  h->d_prare = pr;
-  h->nrare = nr;
   return CS_OK;
 }
 
@@ -5254,6 +5386,11 @@ unsigned long_list_grid(uint64_t npat, uint32_t want = kLongListGrid) {
 // k_count_long over the batch (from_list: the staged kernel's lists in ll), then k_count_list
 // over what it could not finish.  skip_short (twin): every pattern read, only the long ones
 // searched.
+// whether k_count_long verifies long patterns at their walks' positions (round 6): the
+// index keeps no full SA (DevIndex::vsa) but walk lines and a text to compare against
+inline bool walk_verify(const DevIndex& ix) {
+  return !ix.vsa && ix.walk && ix.wssa && ix.lf_exact && (ix.wtext || (ix.ptext && ix.wrare));
+}
 template <bool kBytes>
 cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const uint64_t* d_offs,
                               uint64_t npat, const CountOut& co, hipStream_t st, uint64_t fixed_m,
@@ -5271,14 +5408,33 @@ cs_status launch_count_long_t(const DevIndex& ix, const uint8_t* d_pats, const u
   // CS_QT_LONG_LOADS8 (CS_FM_LONG_V16=0): 8-B pattern / window loads; the default 16-B vectors
   // for the pattern's packed part and the window (C4 150-mers 1.87 -> 1.55 ms, 64-mers 1.25 ->
   // 1.16-1.21, profiles/r03/long_probe_v16.json; round 4's partial forms 1 / 2 are gone)
-  const int walk = ix.vsa ? 0 : ix.wtext ? (ix.wide ? 2 : 1) : 0;
-  if (walk && !kBytes) {  // (round 6) candidates positioned by their short walks (no full SA)
-    if (routed && walk == 2)
+  const int walk = walk_verify(ix) ? (ix.wide ? 2 : 1) : 0;
+  if (walk && kBytes) {  // the measurement twin of the walk forms (direct launches only)
+    if (walk == 2 && ix.ptext)
+      k_count_long<0, true, true, 3, false, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+    else if (walk == 2)
+      k_count_long<0, false, true, 0, false, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+    else if (ix.ptext)
+      k_count_long<0, true, true, 3, false, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+    else
+      k_count_long<0, false, true, 0, false, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+  } else if (walk) {  // (round 6) candidates positioned by their short walks (no full SA)
+    // against the 2-bit text when the index has it (C5), else the byte text
+    const bool pt = ix.ptext != nullptr && !byte_text;
+    if (routed && walk == 2 && pt)
+      k_count_long<0, true, false, 3, true, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+    else if (routed && walk == 2)
       k_count_long<0, false, false, 0, true, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+    else if (routed && pt)
+      k_count_long<0, true, false, 3, true, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
     else if (routed)
       k_count_long<0, false, false, 0, true, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, false);
+    else if (walk == 2 && pt)
+      k_count_long<0, true, false, 3, false, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
     else if (walk == 2)
       k_count_long<0, false, false, 0, false, 2><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
+    else if (pt)
+      k_count_long<0, true, false, 3, false, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
     else
       k_count_long<0, false, false, 0, false, 1><<<g, kBlk, 0, st>>>(ix, d_pats, d_offs, npat, co, fixed_m, ll, skip_short);
   } else if (routed && ix.ptext && !byte_text && !loads8)  // the routed default
@@ -5321,7 +5477,7 @@ cs_status launch_count_long(const DevIndex& ix, const uint8_t* d_pats, const uin
 bool can_route(const cs_fm_index* h, const DevIndex& ix, uint32_t flags) {
   // (round 6: also indexes without the full SA whose long patterns k_count_long verifies at
   // their walks' positions, DevIndex::wtext — C5)
-  if (h->line_fmt != kFmtOcc || !(ix.vsa || ix.wtext) || !ix.ptab_k) return false;
+  if (h->line_fmt != kFmtOcc || !(ix.vsa || walk_verify(ix)) || !ix.ptab_k) return false;
   return !(flags & CS_QT_NO_ROUTE);
 }
 
@@ -5418,7 +5574,7 @@ cs_status launch_count_ex(const cs_fm_index* h, const uint8_t* d_pats, const uin
     FMX_HIP(hipGetLastError());
     return CS_OK;
   }
-  if (h->line_fmt == kFmtOcc && ix.ptab_k && (ix.vsa || ix.wtext) && !packed &&
+  if (h->line_fmt == kFmtOcc && ix.ptab_k && (ix.vsa || walk_verify(ix)) && !packed &&
       ((flags & CS_Q_LONG) || (!d_offs && fixed_m > kLongPatternM))) {
     // long patterns: one per lane in k_count_long (record, candidates, SA, text window as
     // independent rounds; against the 2-bit text when the index has it), the patterns it
@@ -5471,7 +5627,7 @@ cs_status launch_count_bytes(const cs_fm_index* h, const uint8_t* d_pats, const 
   const DevIndex ix = query_dev(h, flags);
   // the patterns k_count_long counts (CS_Q_LONG: all of them; routed device batches: those
   // of kFastM characters or more) take its twin, the rest the general search's
-  const bool lk = h->line_fmt == kFmtOcc && ix.ptab_k && ix.vsa;
+  const bool lk = h->line_fmt == kFmtOcc && ix.ptab_k && (ix.vsa || walk_verify(ix));
   const bool old = (flags & CS_QT_LONG_ROUND2) != 0;
   if (!(lk && (flags & CS_Q_LONG) && !old))
     FMX_DISPATCH(h, k_count_bytes, grid_for(npat, kBlk, 0xFFFFFFFFu), ix, d_pats, d_offs, npat, d_out);

@@ -165,29 +165,8 @@ cs_status cs_csidx_write(const char* path, const uint8_t* bwt, uint64_t n, const
                          uint64_t nsamples, uint32_t ssa_stride, const uint8_t* text);
 /* Writes the index (HBM images of every structure, plus the text when kept) to dir. */
 cs_status cs_fm_save_directory(const cs_fm_index* h, const char* dir);
-/* The index as a device image, for replication across GPUs (e.g. a broadcast over
- * RCCL instead of building on every GPU): export_meta returns the meta text (the
- * directory format's cs_fmindex.meta) and the byte size of each part; export_parts
- * copies the parts into caller device buffers (asynchronous on stream); import
- * creates an index on `device` from a meta and device buffers holding the parts
- * (copied; the buffers may be freed after the call).  The host text is not part of
- * the image. */
-cs_status cs_fm_export_meta(const cs_fm_index* h, char* meta, uint64_t cap, uint64_t* meta_len,
-                            uint64_t* part_bytes, uint32_t* nparts);
-cs_status cs_fm_export_parts(const cs_fm_index* h, void* const* d_dst, void* stream);
-cs_status cs_fm_import(const char* meta, uint64_t meta_len, const void* const* d_src,
-                       uint32_t nparts, int device, cs_fm_index** out);
-/* The same without staging copies (replication at one index's worth of HBM per GPU):
- * export_part_ptrs gives the device address of each of the index's own parts
- * (read-only, valid while h lives) so a broadcast can send straight from them;
- * import_alloc creates a handle on `device` with its parts allocated (contents
- * undefined) and returns their addresses for the caller to fill, e.g. by receiving the
- * broadcast into them; import_commit (after those copies, on any stream) completes the
- * handle — it must not be queried before. */
-cs_status cs_fm_export_part_ptrs(const cs_fm_index* h, const void** d_parts, uint32_t cap);
-cs_status cs_fm_import_alloc(const char* meta, uint64_t meta_len, int device, cs_fm_index** out,
-                             void** d_parts, uint32_t nparts);
-cs_status cs_fm_import_commit(cs_fm_index* h);
+/* Replication of an index across GPUs (export / import of its device image) and the wire
+ * form of per-shard counts: include/cs_fmindex_replica.h. */
 void cs_fm_destroy(cs_fm_index* h);
 cs_status cs_fm_get_info(const cs_fm_index* h, cs_fm_info* out);
 const char* cs_fm_last_error(void);
@@ -231,7 +210,7 @@ cs_status cs_fm_extract_device(const cs_fm_index* h, const uint64_t* d_pos, cons
                                void* stream);
 
 /* Batched count: pattern q = pats[offs[q] .. offs[q+1]).  Host buffers; offsets must
- * be non-decreasing (checked: CS_ERR_INVALID).  The *_device forms take the same
+ * be non-decreasing (checked: CS_ERR_INVALID).  cs_fm_count_device takes the same
  * layout in device memory, unchecked.  A batch of more than CS_FM_HOST_CHUNK patterns
  * (environment when the handle is created, default 2^21) runs in chunks: each chunk's caller pages are page-locked
  * while the earlier chunks' copies and counts run, and its offsets are checked just before
@@ -246,19 +225,13 @@ cs_status cs_fm_locate_batch(const cs_fm_index* h, const uint8_t* pats, const ui
                              uint64_t npat, uint64_t limit, uint64_t* out_offs, uint64_t* out_pos,
                              uint64_t cap, uint64_t* total, void* stream);
 
-/* Device-resident batch entry points (no host staging, asynchronous on `stream`
- * unless stated).  d_pats may be NULL when every pattern of the batch is empty (the
- * count / locate forms then read d_offs[0] and d_offs[npat] back, synchronising `stream`,
- * and return CS_ERR_INVALID unless they are equal). */
-cs_status cs_fm_count_batch_device(const cs_fm_index* h, const uint8_t* d_pats,
-                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
-                                   void* stream);
-/* The same for npat patterns of one length m laid out back to back (pattern q at
- * d_pats + q*m; k-mer batches): FMIndex::count (src/api/fm_index.cpp:79-101) of each,
- * without an offsets array to read. */
-cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, uint64_t m,
-                                   uint64_t npat, uint64_t* d_out, void* stream);
-/* Query flags (the *_ex entry points).  Every flag leaves the results unchanged and
+/* Device-resident batches (no host staging, asynchronous on `stream` unless stated).
+ * Round 6: one count entry and one locate entry, each with query flags
+ * and an optional caller workspace, replace rounds 2-5's _ex / _ws / _async / fixed ladders.
+ * d_pats may be NULL when every pattern of the batch is empty (the count / locate forms then
+ * read d_offs[0] and d_offs[npat] back, synchronising `stream`, and return CS_ERR_INVALID
+ * unless they are equal). */
+/* Query flags (the `flags` argument of the device entry points).  Every flag leaves the results unchanged and
  * only selects which structures a search may read, so the reference's own loop can
  * be run and timed on any index:
  *   CS_Q_NO_PREFIX     start every search from C[] (fm_index.cpp:84-89): no prefix table
@@ -293,7 +266,6 @@ cs_status cs_fm_count_fixed_device(const cs_fm_index* h, const uint8_t* d_pats, 
 #define CS_Q_NO_VERIFY 16u
 #define CS_Q_LONG 32u
 #define CS_Q_NO_LOC_RECORDS 64u
-
 /* Tuning selectors (flags bits 8-23: equivalent kernels for tests and A/B measurements,
  * results never change) are declared in cs_fmindex_tuning.h (round 6: kept out of the
  * drop-in API; a caller of the reference's interface never needs them). */
@@ -313,12 +285,26 @@ typedef struct cs_count_out {
   uint64_t* d_exc_n;
 } cs_count_out;
 
-/* FMIndex::count (fm_index.cpp:79-101) of a device batch, general form: d_offs as
- * cs_fm_count_batch_device, or NULL for npat patterns of one length fixed_m back to back
- * (cs_fm_count_fixed_device); output as *out; flags CS_Q_*. */
-cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
-                                      const uint64_t* d_offs, uint64_t fixed_m, uint64_t npat,
-                                      const cs_count_out* out, uint32_t flags, void* stream);
+/* Device workspace: a count of a device batch routes its long patterns and the patterns its
+ * one read cannot finish to lists the next kernel takes, and the one-call locate keeps
+ * per-pattern counts, records and tile totals between its kernels.  Without a workspace
+ * (d_work NULL or work_bytes too small) a call allocates that memory itself (stream-ordered);
+ * cs_fm_workspace_bytes(h, npat) bytes serve a count or a one-call locate of up to npat
+ * patterns.  Zero-fill it once before its first use: the calls leave it that way (the list
+ * kernel's last block re-zeroes the counters it used).  Results do not depend on it — each
+ * call's first kernel claims the list kernels' retire word itself — but a first call on
+ * memory that was not zero-filled may scan every list slot.  One workspace serves one call at
+ * a time: calls that share it must be ordered (one stream, or events). */
+uint64_t cs_fm_workspace_bytes(const cs_fm_index* h, uint64_t npat);
+
+/* FMIndex::count (fm_index.cpp:79-101) of every pattern of a device batch: pattern q =
+ * d_pats[d_offs[q] .. d_offs[q+1]) (non-decreasing offsets, unchecked), or, with d_offs NULL,
+ * npat patterns of one length fixed_m back to back (pattern q at d_pats + q*fixed_m; k-mer
+ * batches read no offsets array); counts as *out says (uint64 = the reference's type); flags
+ * CS_Q_* (and CS_QT_*, cs_fmindex_tuning.h); d_work / work_bytes the optional workspace. */
+cs_status cs_fm_count_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                             uint64_t fixed_m, uint64_t npat, const cs_count_out* out, uint32_t flags,
+                             void* d_work, uint64_t work_bytes, void* stream);
 /* The same for 2-bit packed DNA patterns (not a reference form: 8 B per pattern
  * instead of m bytes plus an 8-B offset): pattern q is d_packed[q], character i is
  * "ACGT"[(d_packed[q] >> 2i) & 3], i = 0 .. m-1, m <= 32.  Counts equal count() of the
@@ -326,132 +312,43 @@ cs_status cs_fm_count_batch_device_ex(const cs_fm_index* h, const uint8_t* d_pat
 cs_status cs_fm_count_packed_device(const cs_fm_index* h, const uint64_t* d_packed, uint32_t m,
                                     uint64_t npat, const cs_count_out* out, uint32_t flags,
                                     void* stream);
-/* Measurement twin of cs_fm_count_batch_device: d_out[q] = the algorithmic HBM
- * bytes of query q's search (distinct rank/occurrence lines per rank pair x line
- * size + the prefix-table entry), for roofline accounting (bench.py). */
-cs_status cs_fm_count_bytes_device(const cs_fm_index* h, const uint8_t* d_pats,
-                                   const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
-                                   void* stream);
-cs_status cs_fm_count_bytes_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
-                                      const uint64_t* d_offs, uint64_t npat, uint64_t* d_out,
-                                      uint32_t flags, void* stream);
-/* Measurement twin of the one-call locate's locate records (bench.py's locate roofline):
- * d_hit[q] = 1 when the index's locate records (cs_fm_info.locate_record_bytes) answer
- * pattern q in one read, else 0. */
-cs_status cs_fm_locate_record_hits_device(const cs_fm_index* h, const uint8_t* d_pats,
-                                          const uint64_t* d_offs, uint64_t npat, uint8_t* d_hit,
-                                          void* stream);
-/* locate phase 1: backward search; d_sp[q] = the pattern's record for phase 2 (the
- * first row of its range, or an encoded window of matching rows when the search
- * finished over the left contexts — treat it as opaque), d_out_offs = exclusive scan
- * of min(count, limit) (npat+1 entries).  Synchronises `stream` to return *total. */
+
+/* FMIndex::locate (fm_index.cpp:107-157) of every pattern of a device batch in one call:
+ * d_out_offs (npat + 1 entries) = the exclusive scan of min(count, limit), and
+ * d_out_pos[d_out_offs[q] ..] pattern q's positions in the reference's row order.  Every
+ * index that keeps the full suffix array (occurrence lines, the quaternary and binary wavelet
+ * matrices, learned lines) and occurrence-line indexes with walk lines and text-position
+ * marks (C5) take three launches — search, scan of the per-block totals, positions — and one
+ * host synchronisation; otherwise (and under a CS_Q_NO_* structure flag) the two phases below
+ * run back to back.  CS_Q_LONG sends every pattern to the long-pattern search.  Returns
+ * CS_ERR_CAPACITY with *total set and the offsets written when the positions do not fit `cap`
+ * (positions are then incomplete).  Synchronises `stream`. */
+cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
+                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs, uint64_t* d_out_pos,
+                              uint64_t cap, uint64_t* total, uint32_t flags, void* d_work,
+                              uint64_t work_bytes, void* stream);
+/* locate in two phases, under query flags (e.g. CS_Q_NO_FULL_SA | CS_Q_NO_WALK_LINES runs the
+ * reference's row-sampled SSA walk, fm_index.cpp:125-153, on any index).
+ * Phase 1, the backward search: d_sp[q] = the pattern's record for phase 2 (the first row of
+ * its range, or an encoded window of matching rows when the search finished over the left
+ * contexts — treat it as opaque), d_out_offs = exclusive scan of min(count, limit) (npat+1
+ * entries).  Synchronises `stream` to return *total. */
 cs_status cs_fm_locate_ranges_device(const cs_fm_index* h, const uint8_t* d_pats,
                                      const uint64_t* d_offs, uint64_t npat, uint64_t limit,
                                      uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
-                                     void* stream);
-/* locate phase 2: LF walk to the sampled rows and SSA lookup for every reported
- * row.  d_out_pos has `total` entries.  Synchronises `stream` (error check). */
+                                     uint32_t flags, void* stream);
+/* Phase 2: LF walk to the sampled rows and SSA lookup for every reported row (d_out_pos has
+ * `total` entries).  sync != 0: synchronises `stream` and returns the LF-overrun error
+ * (CS_ERR_LF_OVERRUN, fm_index.cpp:136-138); sync == 0: asynchronous, for timing loops — the
+ * overrun is reported by the next cs_fm_locate_check. */
 cs_status cs_fm_locate_walk_device(const cs_fm_index* h, const uint64_t* d_sp,
                                    const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                                   uint64_t* d_out_pos, void* stream);
-/* Phase 2 without the final synchronisation, for timing loops: the LF-overrun
- * flag is checked by the next cs_fm_locate_check call. */
-cs_status cs_fm_locate_walk_device_async(const cs_fm_index* h, const uint64_t* d_sp,
-                                         const uint64_t* d_out_offs, uint64_t npat,
-                                         uint64_t total, uint64_t* d_out_pos, void* stream);
+                                   uint64_t* d_out_pos, uint32_t flags, int sync, void* stream);
 cs_status cs_fm_locate_check(const cs_fm_index* h, void* stream);
-/* The two phases under query flags (CS_Q_*; e.g. CS_Q_NO_FULL_SA | CS_Q_NO_WALK_LINES
- * runs the reference's row-sampled SSA walk, fm_index.cpp:125-153, on any index). */
-cs_status cs_fm_locate_ranges_device_ex(const cs_fm_index* h, const uint8_t* d_pats,
-                                        const uint64_t* d_offs, uint64_t npat, uint64_t limit,
-                                        uint64_t* d_sp, uint64_t* d_out_offs, uint64_t* total,
-                                        uint32_t flags, void* stream);
-cs_status cs_fm_locate_walk_device_ex(const cs_fm_index* h, const uint64_t* d_sp,
-                                      const uint64_t* d_out_offs, uint64_t npat, uint64_t total,
-                                      uint64_t* d_out_pos, uint32_t flags, void* stream);
-/* Phase 2 under query flags without the final synchronisation (as
- * cs_fm_locate_walk_device_async; the overrun flag goes to the next cs_fm_locate_check). */
-cs_status cs_fm_locate_walk_device_async_ex(const cs_fm_index* h, const uint64_t* d_sp,
-                                            const uint64_t* d_out_offs, uint64_t npat,
-                                            uint64_t total, uint64_t* d_out_pos, uint32_t flags,
-                                            void* stream);
-/* locate of a batch in one call — FMIndex::locate (fm_index.cpp:107-157) for every
- * pattern: d_out_offs (npat + 1 entries) = the exclusive scan of min(count, limit), and
- * d_out_pos[d_out_offs[q] ..] pattern q's positions in the reference's row order.  On
- * occurrence-line indexes with a prefix table and left contexts that keep the full suffix
- * array (C2, C4) or walk lines with text-position marks (C5) three launches — search,
- * scan of the per-block totals, positions — and one host synchronisation; otherwise the
- * two phases above run back to back.  Returns CS_ERR_CAPACITY with *total set and the
- * offsets written when the positions do not fit `cap` (positions are then incomplete).
- * Synchronises `stream`. */
-cs_status cs_fm_locate_device(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                              uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                              uint64_t* d_out_pos, uint64_t cap, uint64_t* total, void* stream);
-/* The same under query flags (CS_Q_*): CS_Q_LONG sends every pattern to the long-pattern
- * search (k_locate_long); any other flag runs the two phases under the flags. */
-cs_status cs_fm_locate_device_ex(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
-                                 void* stream);
-/* Device workspace (round 5): a count of a device batch routes its long patterns and the
- * patterns its one read cannot finish to lists the next kernel takes, and the one-call locate
- * keeps per-pattern counts, records and tile totals between its kernels.  The plain entry
- * points allocate that memory per call (stream-ordered); the *_ws forms take it from the
- * caller — no allocation inside the call.  cs_fm_workspace_bytes(h, npat) bytes serve a
- * count or a one-call locate of up to npat patterns.  Zero-fill it once before its first use:
- * the calls leave it that way (the list kernel's last block re-zeroes the counters it used).
- * Results do not depend on it — each call's first kernel claims the list kernels' retire word
- * itself — but a first call on memory that was not zero-filled may scan every list slot.  One
- * workspace serves one call at a time: calls that share it must be ordered (one stream, or
- * events).  work_bytes smaller than needed: the call allocates as
- * the plain form does. */
-uint64_t cs_fm_workspace_bytes(const cs_fm_index* h, uint64_t npat);
-cs_status cs_fm_count_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                                uint64_t fixed_m, uint64_t npat, const cs_count_out* out,
-                                uint32_t flags, void* d_work, uint64_t work_bytes, void* stream);
-cs_status cs_fm_locate_device_ws(const cs_fm_index* h, const uint8_t* d_pats, const uint64_t* d_offs,
-                                 uint64_t npat, uint64_t limit, uint64_t* d_out_offs,
-                                 uint64_t* d_out_pos, uint64_t cap, uint64_t* total, uint32_t flags,
-                                 void* d_work, uint64_t work_bytes, void* stream);
 
-/* Measurement twin of phase 2 (bench.py's walk roofline): d_steps[j] = the LF steps the
- * walk of reported row j takes before its sample (0 with the full suffix array). */
-cs_status cs_fm_locate_walk_steps_device(const cs_fm_index* h, const uint64_t* d_sp,
-                                         const uint64_t* d_out_offs, uint64_t npat,
-                                         uint64_t total, uint64_t* d_steps, uint32_t flags,
-                                         void* stream);
-
-/* Building blocks, for parity tests (host arrays in/out):
- *   level rank1   — BitVector::rank1 of wavelet level l (src/core/bitvector.cpp:165-230);
- *                   CS_ERR_UNSUPPORTED on an occurrence-line index (no levels)
- *   wavelet rank  — WaveletTree::rank (src/core/wavelet.cpp:59-96)
- *   access        — WaveletTree::access (src/core/wavelet.cpp:102-128) = BWT[i]
- *   LF            — FMIndex::LF (src/api/fm_index.hpp:62-66) */
-cs_status cs_fm_level_rank1(const cs_fm_index* h, int level, const uint64_t* pos, uint64_t k,
-                            uint64_t* out);
-cs_status cs_fm_wt_rank(const cs_fm_index* h, const uint8_t* syms, const uint64_t* pos,
-                        uint64_t k, uint64_t* out);
-cs_status cs_fm_wt_access(const cs_fm_index* h, const uint64_t* pos, uint64_t k, uint8_t* out);
-cs_status cs_fm_lf(const cs_fm_index* h, const uint64_t* rows, uint64_t k, uint64_t* out);
-cs_status cs_fm_get_C(const cs_fm_index* h, uint64_t* out257);
-/* The whole BWT (WaveletTree::access for every row) into device memory d_out (n
- * bytes), asynchronous on stream. */
-cs_status cs_fm_bwt_device(const cs_fm_index* h, uint8_t* d_out, void* stream);
-cs_status cs_fm_get_ssa(const cs_fm_index* h, uint64_t* out, uint64_t cap, uint64_t* len);
-
-/* Wire form of a device count vector for the cross-GPU gather of per-shard counts
- * (shard.py): exact and 1 B per pattern — min(count, 255) as uint8
- * plus a (pattern index, count) pair for each count >= 255 — in one fixed-size buffer
- * of cs_counts_wire_bytes(npat, cap) bytes:
- *   [u64 pairs][u64 cap][cap x (u64 index, u64 count)][npat x u8]
- * `pairs` may exceed cap (the pairs past it are not stored).  Asynchronous on stream. */
-uint64_t cs_counts_wire_bytes(uint64_t npat, uint64_t cap);
-cs_status cs_counts_pack_wire(const uint64_t* d_counts, uint64_t npat, uint64_t cap, void* d_wire,
-                              void* stream);
-
-/* Suffix array of text (host in/out) by the device builder — src/core/sais.hpp:8-16
- * order (a proper prefix sorts first). */
-cs_status cs_sa_build(const uint8_t* text, uint64_t n, uint32_t* sa_out, int device);
+/* Measurement twins and the parity tests' building blocks (per-level BitVector::rank1,
+ * WaveletTree::rank / access, LF, C[], the BWT, the SSA, the suffix array): see
+ * include/cs_fmindex_diag.h. */
 
 #ifdef __cplusplus
 }

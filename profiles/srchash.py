@@ -1,6 +1,6 @@
 """The source hash a PMC profile is keyed by: sha256 over the engine's
-kernel sources — every csrc/*.hip and csrc/*.hpp of the package and include/cs_fmindex.h and
-cs_fmindex_tuning.h —
+kernel sources — every csrc/*.hip and csrc/*.hpp of the package and the C ABI headers
+(include/*.h) —
 so a profile describes exactly the code that ran.  profiles/summarize_legs.py stamps each
 entry of pmc_legs.json with it (computed on the GPU box from the tree that was profiled);
 bench.py attaches a leg's traffic only when the stamp equals the hash of the tree it runs
@@ -15,7 +15,7 @@ PKG = os.path.join(ROOT, "compressed-fm-index-implementation-with-learned-optimi
 
 def kernel_src_hash() -> str:
     files = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.hpp")))
-    files += [os.path.join(ROOT, "include", "cs_fmindex.h"), os.path.join(ROOT, "include", "cs_fmindex_tuning.h")]
+    files += sorted(glob.glob(os.path.join(ROOT, "include", "*.h")))
     h = hashlib.sha256()
     for f in files:
         h.update(os.path.basename(f).encode())

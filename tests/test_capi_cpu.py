@@ -30,7 +30,8 @@ def header_symbols():
 def test_header_declares_boundary():
     syms = header_symbols()
     for s in ["cs_fm_build_from_text", "cs_fm_count", "cs_fm_locate", "cs_fm_extract",
-              "cs_fm_count_batch_device", "cs_fm_locate_ranges_device", "cs_fm_locate_walk_device",
+              "cs_fm_count_device", "cs_fm_locate_device", "cs_fm_locate_ranges_device",
+              "cs_fm_locate_walk_device",
               "cs_fm_open_directory", "cs_fm_destroy"]:
         assert s in syms
 
@@ -114,3 +115,16 @@ def test_tuning_selectors_mirror_header():
     for k, v in bits.items():
         assert getattr(pkg, k) == v, k
     assert "#define CS_QT_" not in open(os.path.join(ROOT, "include", "cs_fmindex.h")).read()
+
+
+def test_dropin_header_is_small():
+    """Round 6: the drop-in header declares at most 30 entry points — one
+    count and one locate entry for device batches (flags + optional workspace) instead of the
+    _ex / _ws / _async ladders; measurement twins and parity building blocks live in
+    cs_fmindex_diag.h, replication in cs_fmindex_replica.h, tuning selectors in
+    cs_fmindex_tuning.h."""
+    src = open(os.path.join(ROOT, "include", "cs_fmindex.h")).read()
+    decls = re.findall(r"^(?:cs_status|uint64_t|void|const char\*) (cs_[a-z0-9_]+)\(", src, re.M)
+    assert len(decls) <= 30, decls
+    for gone in ("_ex", "_ws", "_async"):
+        assert not [d for d in decls if d.endswith(gone)], decls

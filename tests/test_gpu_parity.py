@@ -275,8 +275,10 @@ def test_engine_choice(built):
         assert info.record_bytes == rec, name
         assert info.text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0"), name
         # the 2-bit text of long-pattern verification: occurrence lines (not learned), narrow,
-        # LF one n-cycle, with the full suffix array and the text in HBM
-        ptext = engine == 1 and full_sa and info.text_in_hbm and not wide
+        # LF one n-cycle, with the full suffix array and the text in HBM — or (round 6) without
+        # the full SA, over walk lines with text-position marks (C5's layout: its long
+        # patterns are verified at their walks' positions), from the build's text
+        ptext = engine == 1 and ((full_sa and info.text_in_hbm and not wide) or (not full_sa and marks == 2))
         assert info.packed_text_bytes == ((info.n + 31) // 32 * 8 if ptext else 0), name
         assert info.prefix_bytes == (max(rec, 8) * info.prefix_sigma ** info.prefix_k if info.prefix_k else 0), name
 

@@ -224,6 +224,20 @@ def test_c5_dna_32gb_wide(engine, monkeypatch):
     # exact against the text itself (no reference oracle exists at n >= 2^32)
     _scan_exact(idx, host, P[:100_000], 20_000)
     _scan_exact(idx, host, _qunif(pkg, "dna", 20, 100_000, text.device), 1_000)
+    if engine == "auto":
+        # 64-mers (round 6): routed to k_count_long, whose candidates are
+        # positioned by their short walks and verified against the byte text (no full SA at
+        # n >= 2^32) — exact against the text scan, through the device batch (routed) and the
+        # host batch (CS_Q_LONG)
+        P64 = _qtext(pkg, text, N, 64, 20_000)
+        _, sc64 = _scan_exact(idx, host, P64, 1_000)
+        buf, offs = _flat(P64)
+        d_p = torch.from_numpy(buf).cuda()
+        d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_c = torch.empty(len(P64), dtype=torch.int64, device="cuda")
+        idx.count_batch_device(d_p.data_ptr(), d_o.data_ptr(), len(P64), d_c.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(d_c.cpu().numpy().astype(np.uint64), sc64[0])
     ones = idx.count_batch([bytes([c]) for c in range(256)])
     assert int(ones.sum()) == N and ones[ord("$")] == 1
     _kmer_checksum(idx, b"ACGT", 9, N)
