@@ -147,6 +147,10 @@ struct DevIndex {
   // digit(first character) * 4^ptab_k.
   const void* lrec;
   uint32_t lrec64;
+  // Round 6: the prefix table's digits and the occurrence codes are both the standard DNA code
+  // (A C G T = 0 1 2 3, every other byte in neither alphabet): the staged count maps a
+  // pattern's characters four at a time in registers instead of one LDS lookup each
+  uint32_t dna_std;
 };
 
 // Locate records (narrow lf_exact occurrence-line indexes with 16-B context records, the
@@ -264,6 +268,9 @@ struct LongList {
   uint32_t* cnt2 = nullptr;
   uint32_t* hdr = nullptr;  // listed[kListedLanes] (kListedStride apart), then retire
   uint32_t gen_list = 0;    // the routed count: general-search patterns to list2
+  // the routed count (round 6): patterns whose range needs the context sectors (a second
+  // dependent read) go to list2 with their range too, instead of holding the wave for it
+  uint32_t sector_list = 0;
   // the routed count: per list2 entry the range the staged kernel's table read left (sp in
   // bits 0-31, its width in 32-63; narrow indexes) or kNoRange (the search starts over)
   // (and in the list2 entry's bits 9-26, beside a range, the 2-bit occurrence codes of the

@@ -174,6 +174,15 @@ struct cs_fm_index {
     d.prare = static_cast<const uint32_t*>(d_prare);
     d.lrec = d_sa && lf_exact && !wide ? d_lrec : nullptr;
     d.lrec64 = lrec_w == 64 ? 1u : 0u;
+    d.dna_std = 0;
+    if ((line_fmt == fmx::kFmtOcc || line_fmt == fmx::kFmtLOcc) && ptab_sigma == 4) {
+      bool std_map = true;
+      for (int c = 0; c < 256 && std_map; ++c) {
+        const uint8_t want = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : fmx::kNoCode;
+        std_map = h_table.code[c] == want && h_table.occ_code[c] == want;
+      }
+      d.dna_std = std_map ? 1u : 0u;
+    }
     d.nrare = nrare;
     return d;
   }

@@ -1948,7 +1948,40 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     const uint32_t kk = m[j] - K;
     uint32_t tt = 0, ww = 0, dl = kNoCode;
     bool ok = true, cok = kk <= kCtxQ && (!kLoc || ix.lf_exact);
-    if (ix.ptab_sigma == 4) {
+    if (!kPacked && ix.dna_std) {
+      // the standard DNA code (DevIndex::dna_std) four characters per dword, in registers: the
+      // code of byte b is 2 bit2(b) + (bit1(b) ^ bit2(b)) (A C G T -> 0 1 2 3), the byte is
+      // valid iff "ACGT"[code] gives it back (v_perm_b32), and the dword's four 2-bit codes and
+      // four invalid flags are packed by shifts and one multiply — no LDS lookup, no
+      // per-character compare (round 6: the LDS form below issued ~350 vector instructions
+      // per pattern; profiles/r06)
+      uint32_t dlo = 0, dhi = 0, inv = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kFastM / 4; ++w) {
+        if (4 * w >= nchar) break;
+        const uint32_t x = u[w];
+        const uint32_t b1 = (x >> 1) & 0x01010101u, b2 = (x >> 2) & 0x01010101u;
+        const uint32_t code = (b2 << 1) | (b1 ^ b2);
+        const uint32_t dx = __builtin_amdgcn_perm(0u, 0x54474341u, code) ^ x;  // "ACGT"[code] vs the byte
+        const uint32_t nz = (((dx & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | dx) & 0x80808080u;  // bit 7: byte != 0
+        const uint32_t bad = (((nz >> 7) * 0x01020408u) >> 24) & 0xFu;
+        const uint32_t t2 = code | (code >> 6);
+        const uint32_t p8 = (t2 & 0xFu) | ((t2 >> 12) & 0xF0u);
+        if (w < 4) dlo |= p8 << (8 * w);
+        else dhi |= p8 << (8 * (w - 4));
+        inv |= bad << (4 * w);
+      }
+      const uint64_t rd = rev_pairs64(dlo, dhi);
+      tt = (uint32_t)((rd >> (64 - 2 * wl)) & ((1ull << (2 * K)) - 1ull));
+      ok = (inv & (uint32_t)((((1ull << K) - 1ull) << (wl - K)))) == 0;
+      const uint32_t kq = kk < kCtxQ ? kk : kCtxQ;
+      cok = cok && (inv & ((1u << kq) - 1u)) == 0;
+      ww = kq ? (uint32_t)((rd >> (64 - 2 * kq)) & ((1ull << (2 * kq)) - 1ull)) : 0u;
+      if constexpr (kLR)
+        if (kk >= 1 && kk <= kCtxQ)  // the (k+1)-mer's first character (its table digit)
+          dl = ((inv >> (kk - 1)) & 1u) ? kNoCode
+                                        : (uint32_t)((((uint64_t)dhi << 32 | dlo) >> (2 * (kk - 1))) & 3u);
+    } else if (ix.ptab_sigma == 4) {
       uint32_t dlo = 0, dhi = 0, olo = 0, ohi = 0, inv = 0, oinv = 0;
 #pragma unroll
       for (uint32_t i = 0; i < kFastM; ++i) {
@@ -2211,6 +2244,14 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     } else if (st[j] == 2 && inl[j] && ix.lctx) {
       bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record (or mrec[j] matched them)
       if (!((cm >> j) & 1u)) w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
+    } else if (kSkipLong && !kLoc && ll.sector_list && st[j] == 2 && ix.lctx &&
+               ep[j] - (sp[j] & ~15ull) <= 32) {
+      // (CS_QT_SECTOR_LIST) the sector read left to the list kernel: its range and chain, as a
+      // range too wide for the contexts
+      s_chn[j][threadIdx.x] = list_chain(want[j], k[j]);
+      st[j] = 5;
+      s_rng[j][threadIdx.x][0] = sp[j];
+      s_rng[j][threadIdx.x][1] = ep[j];
     } else if (st[j] == 2 && ix.lctx && ep[j] - (sp[j] & ~15ull) <= 32) {
       bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
@@ -5271,6 +5312,7 @@ DevIndex query_dev(const cs_fm_index* h, uint32_t flags) {
   if (flags & (CS_Q_NO_CONTEXTS | CS_Q_NO_VERIFY | CS_Q_NO_FULL_SA))
     d.vsa = nullptr, d.vtext = nullptr, d.ptext = nullptr, d.wtext = nullptr;
   if (flags & CS_Q_NO_WALK_LINES) d.walk = nullptr, d.wtext = nullptr;
+  if (flags & CS_QT_MAP_LDS) d.dna_std = 0;
   if (flags & (CS_Q_NO_PREFIX | CS_Q_NO_CONTEXTS | CS_Q_NO_FULL_SA | CS_Q_NO_LOC_RECORDS)) d.lrec = nullptr;
   return d;
 }
@@ -5533,6 +5575,7 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
     lb.ll.gen_list = (flags & CS_QT_GENERAL_INLANE) ? 0u : (flags & CS_QT_GENERAL_LIST_ALL) ? 1u
                      : ix.vsa ? h->gen_list_min : 0u;
     lb.ll.grid = h->list_grid;
+    lb.ll.sector_list = (flags & CS_QT_SECTOR_LIST) ? 1u : 0u;
     if (nobar)
       k_count_ctx<OccE, 2, false, false, W, true, false, true><<<g2, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);
