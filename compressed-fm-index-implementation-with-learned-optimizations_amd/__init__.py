@@ -35,7 +35,7 @@ QT_BARRIER, QT_NO_ROUTE, QT_COUNT_U1, QT_COUNT_U4 = 1 << 8, 1 << 9, 1 << 10, 1 <
 QT_LONG_LOADS8, QT_LONG_ROUND2, QT_LONG_BYTE_TEXT, QT_QCTX_UNSTAGED = 1 << 12, 1 << 13, 1 << 14, 1 << 15
 QT_NO_ONEPASS, QT_ONEPASS_SA, QT_LOC_DEFER, QT_LOCATE_U1 = 1 << 16, 1 << 17, 1 << 18, 1 << 19
 QT_WALK_ROWS, QT_WALK_PERSISTENT, QT_GENERAL_INLANE, QT_GENERAL_LIST_ALL = 1 << 20, 1 << 21, 1 << 22, 1 << 23
-QT_SECTOR_LIST, QT_MAP_LDS = 1 << 24, 1 << 25
+QT_MAP_LDS = 1 << 24
 
 _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)

@@ -332,7 +332,7 @@ void read_tuning(cs_fm_index* h) {
       {"CS_FM_WALK_ROWS", "1", CS_QT_WALK_ROWS},          {"CS_FM_WALK_PERSISTENT", "1", CS_QT_WALK_PERSISTENT},
       {"CS_FM_GENERAL_INLANE", "1", CS_QT_GENERAL_INLANE},
       {"CS_FM_GENERAL_LIST_ALL", "1", CS_QT_GENERAL_LIST_ALL},
-      {"CS_FM_SECTOR_LIST", "1", CS_QT_SECTOR_LIST},    {"CS_FM_MAP_LDS", "1", CS_QT_MAP_LDS},
+      {"CS_FM_MAP_LDS", "1", CS_QT_MAP_LDS},
   };
   h->tune = 0;
   for (const Bit& b : bits)

@@ -268,9 +268,6 @@ struct LongList {
   uint32_t* cnt2 = nullptr;
   uint32_t* hdr = nullptr;  // listed[kListedLanes] (kListedStride apart), then retire
   uint32_t gen_list = 0;    // the routed count: general-search patterns to list2
-  // the routed count (round 6): patterns whose range needs the context sectors (a second
-  // dependent read) go to list2 with their range too, instead of holding the wave for it
-  uint32_t sector_list = 0;
   // the routed count: per list2 entry the range the staged kernel's table read left (sp in
   // bits 0-31, its width in 32-63; narrow indexes) or kNoRange (the search starts over)
   // (and in the list2 entry's bits 9-26, beside a range, the 2-bit occurrence codes of the

@@ -23,1011 +23,10 @@
 // an LDS counter and cycle fetch -> walk -> sample with one dependent load per loop
 // iteration.  With walk lines (fm_device.hpp WalkLine) one 32-B read per step gives
 // the symbol, its occ and the sample mark; no separate BWT array is kept.
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-
-#include <algorithm>
-#include <cstdlib>
-#include <type_traits>
-#include <vector>
-#include <cstring>
-#include <mutex>
-
-#include "fm_internal.hpp"
+#include "fm_search.hpp"
 
 namespace fmx {
 namespace {
-
-constexpr unsigned kBlk = 256;
-
-__device__ __forceinline__ void load_table(NodeTable& T, const NodeTable* __restrict__ g) {
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(&T);
-  constexpr int nw = sizeof(NodeTable) / 4;
-  for (int i = threadIdx.x; i < nw; i += blockDim.x) dst[i] = src[i];
-}
-
-// A 2-bit packed DNA pattern (cs_fm_count_packed_device): character i is code
-// (x >> 2i) & 3 of "ACGT".  Indexes like the byte pointer of a byte-string pattern,
-// so every search helper takes either (template parameter PT).
-constexpr uint32_t kDnaSyms = 0x54474341u;  // 'A' 'C' 'G' 'T', little-endian
-struct PackedDna {
-  uint64_t x;
-  __device__ __forceinline__ uint32_t operator[](uint64_t i) const {
-    return (kDnaSyms >> (8u * (uint32_t)((x >> (2 * i)) & 3u))) & 0xFFu;
-  }
-};
-
-
-// One backward-search step (fm_index.cpp:90-96) for a symbol c present in the
-// text: [sp, ep) -> [C[c] + occ(c, sp), C[c] + occ(c, ep)).  Returns false when
-// the range empties (the reference's `return 0`).
-template <class F>
-__device__ __forceinline__ bool search_step(const DevIndex& ix, const NodeTable& T, uint32_t c,
-                                            uint64_t& sp, uint64_t& ep,
-                                            uint64_t* bytes = nullptr) {
-  const uint64_t Cc = T.C[c];
-  if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
-  uint64_t ds = sp, de = ep;
-#pragma unroll
-  for (int l = 0; l < kLevels; ++l) {
-    const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
-    if (!(T.flags[nid] & kPure)) {
-      const uint64_t S = T.S[nid], R = T.R[nid];
-      const void* lv = level_ptr<F>(ix, l);
-      uint32_t qa, oa, qe, oe;
-      F::locate(S + ds, qa, oa);
-      F::locate(S + de, qe, oe);
-      if (bytes) *bytes += (qa == qe ? 1u : 2u) * F::kBytes;  // distinct lines (measurement)
-      typename F::Raw va, ve;
-      F::load(lv, qa, va);
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(va) / sizeof(va[0])); ++k) ve[k] = va[k];
-      if (qe != qa) F::load(lv, qe, ve);  // sp and ep in one line: one read
-      const uint64_t rs = F::base(va) + F::prefix(va, oa) - R;
-      const uint64_t re = F::base(ve) + F::prefix(ve, oe) - R;
-      const bool b = (c >> (7 - l)) & 1u;
-      ds = b ? rs : ds - rs;
-      de = b ? re : de - re;
-    }
-  }
-  sp = Cc + ds;
-  ep = Cc + de;
-  return sp < ep;
-}
-
-// One LF step (fm_index.hpp:62-66): descend the wavelet matrix from row i reading
-// the BWT symbol bit by bit (WaveletTree::access, wavelet.cpp:102-128) while
-// mapping i; the leaf offset is rank(c, i).  Pure nodes cost no load.
-template <class F>
-__device__ __forceinline__ uint64_t lf_step(const DevIndex& ix, const NodeTable& T, uint64_t pos,
-                                            uint32_t* sym_out = nullptr) {
-  uint32_t x = 0;
-#pragma unroll
-  for (int l = 0; l < kLevels; ++l) {
-    const int nid = (1 << l) - 1 + (int)x;
-    const uint8_t f = T.flags[nid];
-    uint32_t b;
-    uint64_t r;
-    if (f & kPure) {
-      b = (f & kPureBit) ? 1u : 0u;
-      r = T.R[nid] + (b ? pos - T.S[nid] : 0);
-    } else {
-      uint32_t q, o;
-      F::locate(pos, q, o);
-      typename F::Raw v;
-      F::load(level_ptr<F>(ix, l), q, v);
-      b = F::bit(v, o);
-      r = F::base(v) + F::prefix(v, o);
-    }
-    pos = b ? T.Z[l] + r : pos - r;
-    x = (x << 1) | b;
-  }
-  if (sym_out) *sym_out = x;
-  return T.C[x] + (pos - T.S8[x]);
-}
-
-// ---- rare-symbol rows of the occurrence-line engine (NodeTable::exc_*) ----
-// number of exception rows < i (lower bound in the ascending list)
-__device__ __forceinline__ uint32_t exc_before(const NodeTable& T, uint64_t i) {
-  uint32_t lo = 0, hi = T.exc_n;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (T.exc_row[mid] < i) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-// occ(c, i) of a rare symbol c
-__device__ __forceinline__ uint64_t exc_rank(const NodeTable& T, uint32_t c, uint64_t i) {
-  uint64_t r = 0;
-  for (uint32_t j = 0; j < T.exc_n && T.exc_row[j] < i; ++j) r += T.exc_sym[j] == c;
-  return r;
-}
-
-// ---- engines: what the kernels call per backward-search step / LF step / rank ----
-// WM<F>: the 8-level wavelet matrix (the reference's WaveletTree) in rank lines F.
-template <class F>
-struct WM {
-  static constexpr bool kCtx = false;  // no left contexts
-  using CtxEnt = uint32_t;
-  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
-                                              uint64_t& sp, uint64_t& ep,
-                                              uint64_t* bytes = nullptr) {
-    return search_step<F>(ix, T, c, sp, ep, bytes);
-  }
-  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
-                                                uint64_t pos, uint32_t* sym = nullptr) {
-    return lf_step<F>(ix, T, pos, sym);
-  }
-  // WaveletTree::rank(c, i) (wavelet.cpp:59-96) for 0 < i <= n, c present
-  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
-                                                  uint32_t c, uint64_t i) {
-    uint64_t d = i;
-    for (int l = 0; l < kLevels; ++l) {
-      const int nid = (1 << l) - 1 + (int)(l ? (c >> (8 - l)) : 0u);
-      if (!(T.flags[nid] & kPure)) {
-        const uint64_t r = rank1_at<F>(level_ptr<F>(ix, l), T.S[nid] + d) - T.R[nid];
-        d = ((c >> (7 - l)) & 1u) ? r : d - r;
-      }
-    }
-    return d;
-  }
-};
-
-// OccE: occurrence lines (fm_device.hpp OccLine).  occ(c, i) = one line read:
-// base(code) + rows of that code before i in the line, minus the rare-symbol rows
-// below i when c has code 0 (they are stored as code 0); rare symbols are counted
-// from the LDS list.  sp and ep in the same line share one read.
-struct OccE {
-  static constexpr bool kCtx = true;  // left contexts (DevIndex::lctx) when built
-  using CtxEnt = uint16_t;
-  __device__ static __forceinline__ uint64_t occ_line(const OccLine::Raw& v, uint32_t code,
-                                                      uint64_t i) {
-    return OccLine::base(v, code, i >> 6) + OccLine::prefix(v, code, (uint32_t)(i & 63));
-  }
-  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
-                                              uint64_t& sp, uint64_t& ep,
-                                              uint64_t* bytes = nullptr) {
-    const uint64_t Cc = T.C[c];
-    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
-    const uint32_t code = T.occ_code[c];
-    uint64_t rs, re;
-    if (code == kNoCode) {
-      rs = exc_rank(T, c, sp);
-      re = exc_rank(T, c, ep);
-    } else {
-      const uint64_t qa = sp >> 6, qe = ep >> 6;
-      if (bytes) *bytes += (qa == qe ? 1u : 2u) * OccLine::kBytes;
-      OccLine::Raw va;
-      OccLine::load(ix.lines, qa, va);
-      OccLine::Raw ve = {va[0], va[1]};
-      if (qe != qa) OccLine::load(ix.lines, qe, ve);
-      rs = occ_line(va, code, sp);
-      re = occ_line(ve, code, ep);
-      if (code == 0 && T.exc_n) {
-        rs -= exc_before(T, sp);
-        re -= exc_before(T, ep);
-      }
-    }
-    sp = Cc + rs;
-    ep = Cc + re;
-    return sp < ep;
-  }
-  // LF(i) = C[BWT[i]] + occ(BWT[i], i), symbol and occ from the same line
-  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
-                                                uint64_t pos, uint32_t* sym_out = nullptr) {
-    OccLine::Raw v;
-    OccLine::load(ix.lines, pos >> 6, v);
-    const uint32_t code = OccLine::code(v, (uint32_t)(pos & 63));
-    uint32_t c = T.occ_sym[code];
-    uint64_t r = occ_line(v, code, pos);
-    if (code == 0 && T.exc_n) {
-      const uint32_t e = exc_before(T, pos);
-      if (e < T.exc_n && T.exc_row[e] == pos) {
-        c = T.exc_sym[e];
-        r = exc_rank(T, c, pos);
-      } else {
-        r -= e;
-      }
-    }
-    if (sym_out) *sym_out = c;
-    return T.C[c] + r;
-  }
-  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
-                                                  uint32_t c, uint64_t i) {
-    const uint32_t code = T.occ_code[c];
-    if (code == kNoCode) return exc_rank(T, c, i);
-    OccLine::Raw v;
-    OccLine::load(ix.lines, i >> 6, v);
-    uint64_t r = occ_line(v, code, i);
-    if (code == 0) r -= exc_before(T, i);
-    return r;
-  }
-};
-
-// LOccE: learned occurrence lines (fm_device.hpp LOccLine), the occurrence engine
-// with 104 rows per line.  occ(c, i) = the model's prediction at the line start + the
-// line's residual + rows of code c before i in the line (bitvector_learned.cpp:152-203:
-// coarse prediction + micro correction + tail popcount); the superblock model is an
-// L2-resident read beside the line.  Rare rows as OccE.
-struct LOccE {
-  static constexpr bool kCtx = true;
-  using CtxEnt = uint16_t;
-  __device__ static __forceinline__ uint64_t line_of(uint64_t i) { return i / LOccLine::kRows; }
-  // occ(code, i) with i in line q
-  __device__ static __forceinline__ uint64_t occ_line(const DevIndex& ix, const LOccLine::Raw& v,
-                                                      uint32_t code, uint64_t q, uint64_t i) {
-    const uint64_t b = q >> ix.lmodel_shift, dq = q - (b << ix.lmodel_shift);
-    const LOccModel* m = static_cast<const LOccModel*>(ix.lmodel) + b;
-    uint64_t start;
-    if (code < 3) {
-      start = m->base[code] + ((m->slope[code] * (104ull * dq)) >> 32) + (int64_t)LOccLine::resid(v, code);
-    } else {
-      start = 104ull * q;
-#pragma unroll
-      for (uint32_t c = 0; c < 3; ++c)
-        start -= m->base[c] + ((m->slope[c] * (104ull * dq)) >> 32) + (int64_t)LOccLine::resid(v, c);
-    }
-    return start + LOccLine::prefix(v, code, (uint32_t)(i - q * LOccLine::kRows));
-  }
-  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
-                                              uint64_t& sp, uint64_t& ep,
-                                              uint64_t* bytes = nullptr) {
-    const uint64_t Cc = T.C[c];
-    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
-    const uint32_t code = T.occ_code[c];
-    uint64_t rs, re;
-    if (code == kNoCode) {
-      rs = exc_rank(T, c, sp);
-      re = exc_rank(T, c, ep);
-    } else {
-      const uint64_t qa = line_of(sp), qe = line_of(ep);
-      if (bytes) *bytes += (qa == qe ? 1u : 2u) * LOccLine::kBytes;
-      LOccLine::Raw va;
-      LOccLine::load(ix.lines, qa, va);
-      LOccLine::Raw ve = {va[0], va[1]};
-      if (qe != qa) LOccLine::load(ix.lines, qe, ve);
-      rs = occ_line(ix, va, code, qa, sp);
-      re = occ_line(ix, ve, code, qe, ep);
-      if (code == 0 && T.exc_n) {
-        rs -= exc_before(T, sp);
-        re -= exc_before(T, ep);
-      }
-    }
-    sp = Cc + rs;
-    ep = Cc + re;
-    return sp < ep;
-  }
-  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
-                                                uint64_t pos, uint32_t* sym_out = nullptr) {
-    const uint64_t q = line_of(pos);
-    LOccLine::Raw v;
-    LOccLine::load(ix.lines, q, v);
-    const uint32_t code = LOccLine::code(v, (uint32_t)(pos - q * LOccLine::kRows));
-    uint32_t c = T.occ_sym[code];
-    uint64_t r = occ_line(ix, v, code, q, pos);
-    if (code == 0 && T.exc_n) {
-      const uint32_t e = exc_before(T, pos);
-      if (e < T.exc_n && T.exc_row[e] == pos) {
-        c = T.exc_sym[e];
-        r = exc_rank(T, c, pos);
-      } else {
-        r -= e;
-      }
-    }
-    if (sym_out) *sym_out = c;
-    return T.C[c] + r;
-  }
-  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
-                                                  uint32_t c, uint64_t i) {
-    const uint32_t code = T.occ_code[c];
-    if (code == kNoCode) return exc_rank(T, c, i);
-    const uint64_t q = line_of(i);
-    LOccLine::Raw v;
-    LOccLine::load(ix.lines, q, v);
-    uint64_t r = occ_line(ix, v, code, q, i);
-    if (code == 0) r -= exc_before(T, i);
-    return r;
-  }
-};
-
-// QWM: quaternary wavelet matrix over dense symbol codes, for alphabets beyond the
-// occurrence engine (e.g. sigma = 256: 4 levels instead of 8).  Level l holds digit
-// l (2 bits, most significant first) of the level-l sequence as occurrence lines
-// (OccLine, 64 rows per 32-B line); the next sequence is the stable 4-way
-// partition by that digit.  A position p maps to the next level as
-// p' = qZ[l][d] + occ_l(d, p) — one line read — or affinely inside a pure node
-// (all its symbols share digit d): p' = qZ[l][d] + R + (p - S).  After the last
-// level, occ(c, i) = p_L(i) - S8[code(c)] (the WaveletTree::rank identity,
-// wavelet.cpp:59-96, in base 4).
-struct QWM {
-  static constexpr bool kCtx = true;
-  using CtxEnt = uint32_t;
-  __device__ static __forceinline__ const void* level(const DevIndex& ix, int l) {
-    return static_cast<const uint8_t*>(ix.lines) + (uint64_t)l * ix.nlines * OccLine::kBytes;
-  }
-  __device__ static __forceinline__ bool step(const DevIndex& ix, const NodeTable& T, uint32_t c,
-                                              uint64_t& sp, uint64_t& ep,
-                                              uint64_t* bytes = nullptr) {
-    const uint64_t Cc = T.C[c];
-    if (Cc == T.C[c + 1]) return false;  // symbol absent: occ == 0 on both ends
-    const uint32_t x = T.occ_code[c];
-    const int L = (int)T.qlevels;
-    uint64_t ps = sp, pe = ep;
-    for (int l = 0; l < L; ++l) {
-      const int nid = qnode_id(l, x >> (2 * (L - l)));
-      const uint32_t d = (x >> (2 * (L - 1 - l))) & 3u;
-      const uint8_t f = T.flags[nid];
-      if (f & kPure) {
-        const uint64_t off = T.qZ[l][d] + T.R[nid] - T.S[nid];
-        ps += off;
-        pe += off;
-      } else {
-        const void* lv = level(ix, l);
-        const uint64_t qa = ps >> 6, qe = pe >> 6;
-        if (bytes) *bytes += (qa == qe ? 1u : 2u) * OccLine::kBytes;
-        OccLine::Raw va;
-        OccLine::load(lv, qa, va);
-        OccLine::Raw ve = {va[0], va[1]};
-        if (qe != qa) OccLine::load(lv, qe, ve);
-        ps = T.qZ[l][d] + OccLine::base(va, d, qa) + OccLine::prefix(va, d, (uint32_t)(ps & 63));
-        pe = T.qZ[l][d] + OccLine::base(ve, d, qe) + OccLine::prefix(ve, d, (uint32_t)(pe & 63));
-      }
-    }
-    sp = Cc + (ps - T.S8[x]);
-    ep = Cc + (pe - T.S8[x]);
-    return sp < ep;
-  }
-  // LF(i): the digits of BWT[i] and its mapped position, one line per level
-  __device__ static __forceinline__ uint64_t lf(const DevIndex& ix, const NodeTable& T,
-                                                uint64_t pos, uint32_t* sym_out = nullptr) {
-    const int L = (int)T.qlevels;
-    uint32_t x = 0;
-    uint64_t p = pos;
-    for (int l = 0; l < L; ++l) {
-      const int nid = qnode_id(l, x);
-      const uint8_t f = T.flags[nid];
-      uint32_t d;
-      if (f & kPure) {
-        d = (f >> 2) & 3u;
-        p = T.qZ[l][d] + T.R[nid] + (p - T.S[nid]);
-      } else {
-        OccLine::Raw v;
-        const uint64_t q = p >> 6;
-        OccLine::load(level(ix, l), q, v);
-        const uint32_t o = (uint32_t)(p & 63);
-        d = OccLine::code(v, o);
-        p = T.qZ[l][d] + OccLine::base(v, d, q) + OccLine::prefix(v, d, o);
-      }
-      x = (x << 2) | d;
-    }
-    const uint32_t c = T.qsym[x];
-    if (sym_out) *sym_out = c;
-    return T.C[c] + (p - T.S8[x]);
-  }
-  __device__ static __forceinline__ uint64_t rank(const DevIndex& ix, const NodeTable& T,
-                                                  uint32_t c, uint64_t i) {
-    uint64_t sp = 0, ep = i;
-    (void)step(ix, T, c, sp, ep);
-    return ep - sp;
-  }
-};
-
-// Start of a backward search (fm_index.cpp:84-89): the first step from C[]
-// (sp = C[c], ep = C[c+1]), or the first k steps from the prefix table when the
-// pattern's last k characters are all in its alphabet.  k receives the characters
-// still to process (P[k-1] .. P[0]).  Requires m >= 1.
-// With context records, *inl receives the entry's contexts (kRecCtx u16 in 6 dwords),
-// or the compact record itself (fm_device.hpp kRec16Ctx) when it holds contexts.
-// maj: a wide compact record's majority contexts (kRec16Maj), when it holds them.
-template <class PT>
-__device__ __forceinline__ void search_start(const DevIndex& ix, const NodeTable& T,
-                                             PT P, uint64_t m,
-                                             uint64_t& sp, uint64_t& ep, uint64_t& k,
-                                             uint64_t* bytes, const uint32_t** inl = nullptr,
-                                             const uint32_t** maj = nullptr) {
-  if (inl) *inl = nullptr;
-  if (maj) *maj = nullptr;
-  if (ix.ptab_k && m >= ix.ptab_k) {
-    uint32_t t = 0;
-    bool ok = true;
-    for (uint32_t i = (uint32_t)(m - ix.ptab_k); i < m; ++i) {
-      const uint32_t d = T.code[P[i]];
-      ok &= d != kNoCode;
-      t = t * ix.ptab_sigma + d;
-    }
-    if (ok && ptab_at(ix, t, sp, ep)) {
-      if (bytes) *bytes += ix.ptab_rec == 1 ? 32u : ix.ptab_rec >= 2 ? 16u : 8u;
-      if (inl && ix.ptab_rec == 3 && ep - sp <= kRecQCtx)
-        *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4 + 2;
-      if (inl && ix.ptab_rec == 1) *inl = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 8 + 2;
-      if ((inl || maj) && ix.ptab_rec == 2) {
-        const uint32_t* r = static_cast<const uint32_t*>(ix.ptab) + (uint64_t)t * 4;
-        if ((r[1] & 15u) != kRec16Wide) {
-          if (inl) *inl = r;
-        } else if (maj && !ix.wide && (r[1] & kRec16Maj)) {
-          *maj = r;
-        }
-      }
-      k = m - ix.ptab_k;
-      return;
-    }
-  }
-  const uint32_t c = P[m - 1];
-  sp = T.C[c];  // occ(c,0)=0, occ(c,n)=freq(c)
-  ep = T.C[c + 1];
-  k = m - 1;
-}
-
-// Backward search of one pattern (fm_index.cpp:84-98).  Returns false when the
-// range empties.  Requires m >= 1, n >= 1.
-template <class E, class PT>
-__device__ __forceinline__ bool backward_search(const DevIndex& ix, const NodeTable& T,
-                                                PT P, uint64_t m,
-                                                uint64_t& sp_out, uint64_t& ep_out,
-                                                uint64_t* bytes = nullptr) {
-  uint64_t sp, ep, k;
-  search_start(ix, T, P, m, sp, ep, k, bytes);
-  if (sp >= ep) return false;
-  uint32_t cn = k ? P[k - 1] : 0u;
-  while (k-- > 0) {
-    const uint32_t c = cn;
-    if (k > 0) cn = P[k - 1];  // prefetch the next character
-    if (!E::step(ix, T, c, sp, ep, bytes)) return false;
-  }
-  sp_out = sp;
-  ep_out = ep;
-  return true;
-}
-
-// The last k <= lctx_q characters P[0..k) over the left contexts of the rows
-// [sp, ep) (fm_device.hpp kCtxQ): the rows whose chain spells P[k-1], ..., P[0].
-// Needs ep - (sp & ~(R-1)) <= 2R, R = rows per 32-B sector (16 for u16 entries, 8
-// for u32).  Returns kCtxNone — the caller keeps stepping — when a character has no
-// code (a rare symbol) or a row in the range has an escaped context; kCtxAbsent when
-// a character does not occur in the text (count 0, as the reference's step);
-// otherwise kCtxOk with bit i of `mm` set when row base + i matches.
-enum : uint32_t { kCtxNone = 0, kCtxAbsent = 1, kCtxOk = 2 };
-// whether a record's inline contexts answer k characters over a w-row range
-__device__ __forceinline__ bool rec_inline(const DevIndex& ix, uint64_t k, uint64_t w) {
-  return ix.ptab_rec == 2 ? k <= (ix.wide ? kRec16QW : kRec16Q)
-                          : ix.ptab_rec == 3 ? w <= kRecQCtx : w <= kRecCtx;
-}
-// inl: the contexts of a context record whose range [sp, ep) is at most kRecCtx rows
-// (already read with the record: no further access), else null.
-template <class Ent, class PT>
-__device__ __forceinline__ uint32_t ctx_match(const DevIndex& ix, const NodeTable& T,
-                                              PT P, uint32_t k,
-                                              uint64_t sp, uint64_t ep, uint32_t& mm,
-                                              uint64_t& base, uint64_t* bytes,
-                                              const uint32_t* inl = nullptr) {
-  constexpr uint32_t R = 32 / sizeof(Ent);
-  constexpr bool kEsc = sizeof(Ent) == 2;
-  const uint32_t sb = kEsc ? 2u : ix.lctx_sb;
-  uint32_t want = 0;
-  for (uint32_t t = 0; t < k; ++t) {  // chain symbol t = P[k-1-t]
-    const uint32_t c = P[k - 1 - t];
-    if (T.C[c] == T.C[c + 1]) return kCtxAbsent;
-    const uint32_t d = T.occ_code[c];
-    // a rare symbol of the occurrence engine; the quaternary matrix codes every present
-    // symbol densely (with 256 symbols one of them is code 0xFF == kNoCode)
-    if (kEsc && d == kNoCode) return kCtxNone;
-    want |= d << (sb * t);
-  }
-  const uint32_t kb = sb * k;
-  const uint32_t mask = (kb >= 32 ? ~0u : ((1u << kb) - 1u)) | (kEsc ? kCtxEsc : 0u);
-  uint4 w[4];
-  uint32_t lo, hi;  // rows [lo, hi) of the 2R from base
-  if (!kEsc && inl) {  // quaternary-matrix record: rows sp, sp+1 (u32 entries)
-    base = sp;
-    lo = 0;
-    hi = (uint32_t)(ep - sp);
-    w[0] = make_uint4(inl[0], inl[1], 0, 0);
-    w[1] = w[2] = w[3] = make_uint4(0, 0, 0, 0);
-  } else if (kEsc && inl) {
-    base = sp;
-    lo = 0;
-    hi = (uint32_t)(ep - sp);
-    if (ix.ptab_rec == 2) {
-      uint32_t d[5];
-      if (ix.wide)
-        rec16w_contexts(inl[1], inl[2], inl[3], d);
-      else
-        rec16_contexts(inl[1], inl[2], inl[3], d);
-      w[0] = make_uint4(d[0], d[1], d[2], d[3]);
-      w[1] = make_uint4(d[4], 0, 0, 0);
-    } else {
-      w[0] = make_uint4(inl[0], inl[1], inl[2], inl[3]);
-      w[1] = make_uint4(inl[4], inl[5], 0, 0);
-    }
-    w[2] = w[3] = make_uint4(0, 0, 0, 0);
-  } else {
-    base = sp & ~(uint64_t)(R - 1);
-    lo = (uint32_t)(sp - base);
-    hi = (uint32_t)(ep - base);
-    const uint4* p = reinterpret_cast<const uint4*>(static_cast<const Ent*>(ix.lctx) + base);
-    const bool two = hi > R;
-    if (bytes) *bytes += two ? 64u : 32u;
-    w[0] = p[0];
-    w[1] = p[1];
-    if (two) {
-      w[2] = p[2];
-      w[3] = p[3];
-    } else {
-      w[2] = w[3] = make_uint4(0, 0, 0, 0);
-    }
-  }
-  const uint32_t* dw = reinterpret_cast<const uint32_t*>(w);
-  uint32_t match = 0, esc = 0;  // bit i: row base + i
-#pragma unroll
-  for (int i = 0; i < (int)(2 * R); ++i) {
-    const uint32_t e = kEsc ? (dw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu : dw[i];
-    match |= (uint32_t)((e & mask) == want) << i;
-    if (kEsc) esc |= (uint32_t)((e & kCtxEsc) != 0) << i;
-  }
-  const uint32_t in = (hi >= 32 ? ~0u : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-  if (esc & in) return kCtxNone;
-  mm = match & in;
-  return kCtxOk;
-}
-
-template <class Ent, class PT>
-__device__ __forceinline__ bool ctx_count(const DevIndex& ix, const NodeTable& T,
-                                          PT P, uint32_t k,
-                                          uint64_t sp, uint64_t ep, uint64_t& cnt,
-                                          uint64_t* bytes, const uint32_t* inl = nullptr) {
-  uint32_t mm = 0;
-  uint64_t base;
-  const uint32_t r = ctx_match<Ent>(ix, T, P, k, sp, ep, mm, base, bytes, inl);
-  if (r == kCtxNone) return false;
-  cnt = r == kCtxOk ? (uint64_t)__popc(mm) : 0;
-  return true;
-}
-
-template <class E, class PT, bool kLA = false>
-__device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTable& T, PT P,
-                                               uint64_t k, uint64_t sp, uint64_t ep,
-                                               uint64_t* bytes, const uint32_t* inl);
-
-// count() of one pattern (fm_index.cpp:84-100), m >= 1, n >= 1: the backward
-// search, finished over the left contexts once at most kCtxQ characters remain and
-// the range is narrow (engines with contexts, when built).
-template <class E, class PT, bool kLA = false>
-__device__ __forceinline__ uint64_t count_pattern(const DevIndex& ix, const NodeTable& T,
-                                                  PT P, uint64_t m,
-                                                  uint64_t* bytes = nullptr) {
-  uint64_t sp, ep, k;
-  const uint32_t *inl, *maj;
-  search_start(ix, T, P, m, sp, ep, k, bytes, &inl, &maj);
-  if (sp >= ep) return 0;
-  if (maj && k == kRec16Q) {  // a wide record's majority contexts (kRec16Maj)
-    uint32_t want = 0;
-    bool ok = true;
-    for (uint32_t t = 0; t < kRec16Q; ++t) {  // chain symbol t = P[k-1-t]
-      const uint32_t d = T.occ_code[P[kRec16Q - 1 - t]];
-      ok &= d != kNoCode;
-      want |= (d & 3u) << (2 * t);
-    }
-    uint64_t c;
-    if (ok && rec16_majority(maj[1], maj[3], want, c)) return c;
-  }
-  return count_rest<E, PT, kLA>(ix, T, P, k, sp, ep, bytes, inl);
-}
-
-// One suffix-array entry: a random read nothing re-reads, non-temporal as the records are
-// (C4 one-call locate 0.835 -> 0.815 ms, 64-mer count 1.268 -> 1.256 ms, three A/B rounds:
-// profiles/r03/ab_nt_sa_load.jsonl)
-__device__ __forceinline__ uint32_t load_sa(const uint32_t* sa, uint64_t r) {
-  return __builtin_nontemporal_load(sa + r);
-}
-
-// Verification against the text (lf_exact indexes that keep the full suffix array and the
-// text in HBM: DevIndex::vsa / vtext).  Row r of [sp, ep) survives the k remaining steps
-// iff its chain spells P[k-1], ..., P[0]; LF^t(r) is the row of the rotation SA[r] - t, so
-// that chain is text[SA[r] - k .. SA[r]) (cyclically, as the rotations).  A narrow range
-// with many characters left is therefore finished by reading its rows' SA entries (one
-// sector: the rows are consecutive) and comparing k text bytes before each — two
-// dependent rounds of reads instead of k rank steps (a 64-mer: 49 steps).  The result is
-// the count the steps would give, exactly.
-constexpr uint32_t kVerifyRows = 8;
-constexpr uint32_t kVerifyWords = 8;  // text words compared per round (64 characters)
-
-// bytes P[j, j + 8) as a little-endian uint64, from realigned dword loads that touch only
-// dwords holding bytes of P[0, k) (bytes at or past k: unspecified)
-__device__ __forceinline__ uint64_t pat8(const uint8_t* P, uint64_t j, uint64_t k) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(P) + j;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-  const uint32_t off = (uint32_t)(a & 3);
-  const uint64_t left = k - j;
-  const uint32_t nb = off + (uint32_t)(left < 8 ? left : 8);  // bytes spanned from w
-  const uint32_t w0 = w[0];
-  const uint32_t w1 = nb > 4 ? w[1] : 0u;
-  const uint32_t w2 = nb > 8 ? w[2] : 0u;
-  const uint64_t lo = ((uint64_t)w1 << 32) | w0;
-  return off ? (lo >> (8 * off)) | ((uint64_t)w2 << (64 - 8 * off)) : lo;
-}
-__device__ __forceinline__ uint64_t pat8(PackedDna P, uint64_t j, uint64_t) {
-  uint64_t x = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < 8; ++i) x |= (uint64_t)P[j + i] << (8 * i);
-  return x;
-}
-// A pattern read byte by byte: copies in kernel arguments or LDS (k_count_one, the
-// resident server), where realigned word loads would force the copy to scratch.
-struct BytePat {
-  const uint8_t* b;
-  __device__ __forceinline__ uint32_t operator[](uint64_t i) const { return b[i]; }
-};
-__device__ __forceinline__ uint64_t pat8(BytePat P, uint64_t j, uint64_t k) {
-  uint64_t x = 0;
-  for (uint32_t i = 0; i < 8 && j + i < k; ++i) x |= (uint64_t)P[j + i] << (8 * i);
-  return x;
-}
-// the mask of the bytes of a chunk at j that lie inside P[0, k)
-__device__ __forceinline__ uint64_t chunk_mask(uint64_t j, uint64_t k) {
-  return k - j >= 8 ? ~0ull : (1ull << (8 * (k - j))) - 1;
-}
-// text[t, t + 8) from the aligned words w0 (holding t) and w1 (the next one)
-__device__ __forceinline__ uint64_t text8(uint64_t w0, uint64_t w1, uint64_t t) {
-  const uint32_t sh = (uint32_t)(t & 7) * 8;
-  return sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-}
-
-// text[q, q + k) == P[0, k), cyclically (positions mod n).  Windows inside [0, n) compare
-// 8 kVerifyWords bytes per round of aligned 8-B loads; a window through the end of the text (a row
-// whose suffix starts fewer than k positions into the text) byte by byte.
-// kLA (long patterns, CS_Q_LONG): rounds of kVerifyWordsLA words, the next round's words loaded before
-// this round compares, so a window of R rounds waits for one HBM round trip plus R - 1
-// overlapped ones instead of R.  The extra registers are why it is a separate kernel.
-constexpr uint32_t kVerifyWordsLA = 16;  // 8 and 12 measured: 150-mers 2.47 / 2.56 vs 2.56·10⁹/s
-template <class PT, bool kLA = false>
-__device__ __forceinline__ bool window_eq(const DevIndex& ix, PT P, uint64_t q, uint64_t k,
-                                          uint64_t* bytes) {
-  const uint64_t n = ix.n;
-  if (q + k > n) {
-    for (uint64_t j = 0; j < k; ++j) {
-      uint64_t t = q + j;
-      if (t >= n) t -= n;
-      if (ix.vtext[t] != (uint8_t)P[j]) return false;
-    }
-    if (bytes) *bytes += 64;
-    return true;
-  }
-  const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
-  const uint64_t last = (q + k - 1) >> 3;  // the last word holding a byte of the window
-  if constexpr (kLA) {
-    constexpr uint32_t V = kVerifyWordsLA;
-    uint64_t w[V + 1];
-    uint64_t a = q >> 3;
-#pragma unroll
-    for (uint32_t i = 0; i <= V; ++i) w[i] = a + i <= last ? tw[a + i] : 0ull;
-    for (uint64_t j0 = 0; j0 < k; j0 += 8 * V) {
-      const bool more = j0 + 8 * V < k;
-      uint64_t x[V];  // the next round's words past w[V] (which it starts with)
-#pragma unroll
-      for (uint32_t i = 0; i < V; ++i) {
-        const uint64_t b = a + V + 1 + i;
-        x[i] = more && b <= last ? tw[b] : 0ull;
-      }
-      if (bytes) *bytes += 8 * V;
-      uint64_t diff = 0;
-#pragma unroll
-      for (uint32_t i = 0; i < V; ++i) {
-        const uint64_t j = j0 + 8 * i;
-        if (j < k) diff |= (text8(w[i], w[i + 1], q + j) ^ pat8(P, j, k)) & chunk_mask(j, k);
-      }
-      if (diff) return false;
-      w[0] = w[V];
-#pragma unroll
-      for (uint32_t i = 0; i < V; ++i) w[i + 1] = x[i];
-      a += V;
-    }
-    return true;
-  }
-  for (uint64_t j0 = 0; j0 < k; j0 += 8 * kVerifyWords) {
-    const uint64_t a = (q + j0) >> 3;
-    uint64_t w[kVerifyWords + 1];
-#pragma unroll
-    for (uint32_t i = 0; i <= kVerifyWords; ++i) w[i] = a + i <= last ? tw[a + i] : 0ull;
-    if (bytes) *bytes += 8 * kVerifyWords;
-    uint64_t diff = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kVerifyWords; ++i) {
-      const uint64_t j = j0 + 8 * i;
-      if (j < k) diff |= (text8(w[i], w[i + 1], q + j) ^ pat8(P, j, k)) & chunk_mask(j, k);
-    }
-    if (diff) return false;
-  }
-  return true;
-}
-
-// The rows of [sp, ep) (at most kVerifyRows) worth a full comparison: for two rows or more,
-// their SA entries (consecutive rows: one sector) in one round, then one aligned 8-B word
-// at the start of every row's window in one round (1-8 of its first characters against
-// the same pattern chunk).  Bit i: row sp + i.
-template <class PT>
-__device__ __forceinline__ uint32_t verify_filter(const DevIndex& ix, PT P, uint64_t k,
-                                                  uint64_t sp, uint64_t ep, uint64_t* bytes) {
-  const uint32_t w = (uint32_t)(ep - sp);
-  if (w == 1) return 1u;
-  const uint64_t n = ix.n;
-  const uint64_t* tw = reinterpret_cast<const uint64_t*>(ix.vtext);
-  uint32_t pos[kVerifyRows];
-#pragma unroll
-  for (uint32_t i = 0; i < kVerifyRows; ++i) pos[i] = i < w ? ix.vsa[sp + i] : 0u;
-  if (bytes) *bytes += 32 + 32ull * w;
-  const uint64_t p0 = pat8(P, 0, k) & chunk_mask(0, k);
-  uint32_t pass = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kVerifyRows; ++i) {
-    if (i >= w) break;
-    const uint64_t p = pos[i];
-    const uint64_t q = p >= k ? p - k : p + n - k;  // P[0] sits at text[q]
-    const uint32_t sh = (uint32_t)(q & 7) * 8;
-    const uint64_t x = tw[q >> 3] >> sh;  // text[q, q + 8 - (q & 7)): inside the word
-    const uint64_t msk = chunk_mask(0, k) & (~0ull >> sh) & (q + 8 <= n ? ~0ull : (1ull << (8 * (n - q))) - 1);
-    if (((x ^ p0) & msk) == 0) pass |= 1u << i;
-  }
-  return pass;
-}
-
-// P[s, ...) as a pattern of its own
-__device__ __forceinline__ const uint8_t* pat_shift(const uint8_t* P, uint64_t s) { return P + s; }
-__device__ __forceinline__ BytePat pat_shift(BytePat P, uint64_t s) { return BytePat{P.b + s}; }
-__device__ __forceinline__ PackedDna pat_shift(PackedDna P, uint64_t s) {
-  return PackedDna{s < 32 ? P.x >> (2 * s) : 0ull};
-}
-
-// The candidate rows base + i (bit i of mm) — their contexts matched P[k - qf, k), or they
-// passed verify_filter (qf = 0): each one's SA entry, then P[0, k - qf) against the text
-// before its suffix's last qf characters.
-template <class PT, bool kLA = false>
-__device__ __forceinline__ uint64_t verify_rows(const DevIndex& ix, PT P, uint64_t k, uint32_t qf,
-                                                uint64_t base, uint32_t mm, uint64_t* bytes) {
-  const uint64_t n = ix.n;
-  uint64_t cnt = 0;
-  while (mm) {
-    const uint32_t i = (uint32_t)__ffs(mm) - 1u;
-    mm &= mm - 1;
-    const uint64_t p = load_sa(ix.vsa, base + i);
-    if (bytes) *bytes += 32;
-    cnt += window_eq<PT, kLA>(ix, P, p >= k ? p - k : p + n - k, k - qf, bytes) ? 1u : 0u;
-  }
-  return cnt;
-}
-
-// The rest of a count() from the range [sp, ep) (non-empty) with P[0..k) still to
-// process (fm_index.cpp:90-98); inl as search_start's.
-template <class E, class PT, bool kLA>
-__device__ __forceinline__ uint64_t count_rest(const DevIndex& ix, const NodeTable& T, PT P,
-                                               uint64_t k, uint64_t sp, uint64_t ep,
-                                               uint64_t* bytes, const uint32_t* inl) {
-  constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);  // context rows per sector
-  bool ctx = E::kCtx && ix.lctx != nullptr;
-  // context characters a record holds inline
-  const uint32_t qi = ix.ptab_rec == 2 ? (ix.wide ? kRec16QW : kRec16Q) : ix.lctx_q;
-  while (k > 0) {
-    // verification against the text pays once it saves more than the one step + context
-    // read it replaces; the contexts (of the record: no read, or of a sector) filter the
-    // rows first, on P's last qf characters
-    const bool ver = ix.vsa && k > (ctx ? ix.lctx_q + 1u : 2u) && k < ix.n;
-    uint32_t qf = 0;
-    if (ctx && k <= ix.lctx_q) qf = (uint32_t)k;
-    else if (ctx && ver) qf = inl && rec_inline(ix, qi, ep - sp) ? qi : ix.lctx_q;
-    if (inl && !(qf && rec_inline(ix, qf, ep - sp))) inl = nullptr;
-    uint32_t mm = 0;
-    uint64_t base = sp;
-    bool cand = false;
-    if (qf && (inl || ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R)) {
-      const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, pat_shift(P, k - qf), qf, sp, ep, mm,
-                                                       base, bytes, inl);
-      if (r == kCtxAbsent) return 0;
-      if (r == kCtxOk) {
-        if (qf == k) return (uint64_t)__popc(mm);
-        cand = true;
-      } else {
-        ctx = false;  // an escaped context or a rare symbol
-      }
-    }
-    if (!cand && ver && ep - sp <= kVerifyRows) {
-      mm = verify_filter(ix, P, k, sp, ep, bytes);
-      base = sp;
-      qf = 0;
-      cand = true;
-    }
-    if (cand) return verify_rows<PT, kLA>(ix, P, k, qf, base, mm, bytes);
-    inl = nullptr;
-    --k;
-    if (!E::step(ix, T, P[k], sp, ep, bytes)) return 0;
-  }
-  return ep - sp;
-}
-
-// Locate records (phase 1 -> phase 2, cs_fm_locate_ranges_device's d_sp): the
-// first row of the range [sp, ep), or — for a search finished over the left
-// contexts (lf_exact indexes only) — the window of matching rows r at k characters
-// before the end: bit 63 set, bits 60-62 k, bits 38-59 the matches relative to the
-// first one (bit i: row r0 + i), bits 0-37 r0.  The final rows are LF^k(r), in the
-// same order (LF keeps the order of rows with equal chains), and with LF one n-cycle
-// SA[LF^k(r)] = SA[r] - k (mod n), so phase 2 walks from r and subtracts k.
-constexpr uint64_t kLocCtx = 1ull << 63;
-constexpr uint64_t kLocRowMask = (1ull << 38) - 1;
-constexpr uint32_t kLocSpanBits = 22;
-// locate phase 2 kernels fused with the records: a lane takes a pattern of at most this
-// many rows (every context window: <= kLocSpanBits); wider ranges go a block per range
-constexpr uint64_t kLocSmall = 32;
-// rows handed to the walk: row | k << kWalkAdjShift (k = positions to subtract)
-constexpr int kWalkAdjShift = 56;
-constexpr uint64_t kWalkRowMask = (1ull << kWalkAdjShift) - 1;
-
-// A window of rows verified against the text (locate_search, indexes with DevIndex::vsa):
-// bits 60-62 zero (a context window has k >= 1 there), bits 38-49 the matches relative to
-// the first one, bits 50-59 k.  Its positions are SA[row] - k as for a context window.
-constexpr uint32_t kLocVerRelBits = 12;
-constexpr uint64_t kLocVerMaxK = (1u << 10) - 1;
-
-// rows, adjustment and match bits of a window record (s & kLocCtx)
-__device__ __forceinline__ void loc_window(uint64_t s, uint64_t& r0, uint64_t& adj, uint32_t& rel) {
-  r0 = s & kLocRowMask;
-  adj = (s >> 60) & 7u;
-  if (adj) {
-    rel = (uint32_t)(s >> 38) & ((1u << kLocSpanBits) - 1u);
-  } else {
-    rel = (uint32_t)(s >> 38) & ((1u << kLocVerRelBits) - 1u);
-    adj = (s >> 50) & kLocVerMaxK;
-  }
-}
-
-// The rows base + i (bit i of mm) whose window text[SA - k, SA - qf) spells P[0, k - qf)
-// (verify_rows' test, as a mask).
-template <class PT>
-__device__ __forceinline__ uint32_t verify_mask(const DevIndex& ix, PT P, uint64_t k, uint32_t qf,
-                                                uint64_t base, uint32_t mm) {
-  const uint64_t n = ix.n;
-  uint32_t out = 0;
-  while (mm) {
-    const uint32_t i = (uint32_t)__ffs(mm) - 1u;
-    mm &= mm - 1;
-    const uint64_t p = load_sa(ix.vsa, base + i);
-    if (window_eq(ix, P, p >= k ? p - k : p + n - k, k - qf, nullptr)) out |= 1u << i;
-  }
-  return out;
-}
-
-// locate()'s search (fm_index.cpp:107-124): the count and the pattern's record — its
-// range's first row, a context window (the last <= 7 characters over the left contexts),
-// or a verified window (long patterns over lf_exact indexes with the full suffix array and
-// the text: the rows of a narrow range whose text before their suffix spells the rest of
-// the pattern, count_rest's verification; SA[r] - k is then the position, so phase 2 reads
-// the same SA entries the verification read).
-template <class E, class PT>
-__device__ __forceinline__ uint64_t locate_search(const DevIndex& ix, const NodeTable& T,
-                                                  PT P, uint64_t m,
-                                                  uint64_t& rec) {
-  uint64_t sp, ep, k;
-  const uint32_t* inl;
-  rec = 0;
-  search_start(ix, T, P, m, sp, ep, k, nullptr, &inl);
-  if (sp >= ep) return 0;
-  constexpr uint32_t R = 32 / sizeof(typename E::CtxEnt);
-  bool ctx = E::kCtx && ix.lctx != nullptr && ix.lf_exact;
-  bool ver = ix.vsa != nullptr;  // implies lf_exact
-  const uint32_t qi = ix.ptab_rec == 2 ? kRec16Q : ix.lctx_q;  // vsa: narrow indexes only
-  while (k > 0) {
-    const uint64_t w = ep - sp;
-    const bool fits = ep - (sp & ~(uint64_t)(R - 1)) <= 2 * R;
-    if (ctx && k <= ix.lctx_q && k <= 7) {
-      const uint32_t* in = inl && rec_inline(ix, k, w) ? inl : nullptr;
-      if (in || fits) {
-        uint32_t mm = 0;
-        uint64_t base;
-        const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, P, (uint32_t)k, sp, ep, mm, base,
-                                                         nullptr, in);
-        if (r == kCtxAbsent || (r == kCtxOk && mm == 0)) return 0;
-        if (r == kCtxOk) {
-          const uint32_t f = (uint32_t)__ffs(mm) - 1u;
-          const uint32_t rel = mm >> f;
-          if ((rel >> kLocSpanBits) == 0) {
-            rec = kLocCtx | (k << 60) | ((uint64_t)rel << 38) | (base + f);
-            return (uint64_t)__popc(mm);
-          }
-        }
-        ctx = false;
-      }
-    }
-    if (ver && k > (ctx ? ix.lctx_q + 1u : 2u) && k < ix.n && k <= kLocVerMaxK) {
-      uint32_t qf = 0, mm = 0;
-      uint64_t base = sp;
-      bool cand = false;
-      if (ctx) {  // filter on P's last qf characters first (count_rest)
-        qf = inl && rec_inline(ix, qi, w) ? qi : ix.lctx_q;
-        const uint32_t* in = inl && rec_inline(ix, qf, w) ? inl : nullptr;
-        if (in || fits) {
-          const uint32_t r = ctx_match<typename E::CtxEnt>(ix, T, pat_shift(P, k - qf), qf, sp, ep,
-                                                           mm, base, nullptr, in);
-          if (r == kCtxAbsent) return 0;
-          if (r == kCtxOk) cand = true;
-          else ctx = false;
-        }
-      }
-      if (!cand && w <= kVerifyRows) {
-        mm = verify_filter(ix, P, k, sp, ep, nullptr);
-        base = sp;
-        qf = 0;
-        cand = true;
-      }
-      if (cand) {
-        mm = verify_mask(ix, P, k, qf, base, mm);
-        if (!mm) return 0;
-        const uint32_t f = (uint32_t)__ffs(mm) - 1u;
-        const uint32_t rel = mm >> f;
-        if ((rel >> kLocVerRelBits) == 0) {
-          rec = kLocCtx | (k << 50) | ((uint64_t)rel << 38) | (base + f);
-          return (uint64_t)__popc(mm);
-        }
-        ver = false;  // matches too far apart for the record: step on
-      }
-    }
-    inl = nullptr;
-    --k;
-    if (!E::step(ix, T, P[k], sp, ep, nullptr)) return 0;
-  }
-  rec = sp;
-  return ep - sp;
-}
-
-// Prefix table entry t: backward search of the k-mer whose j-th character from
-// the end is sym[digit_j(t)] (same steps as above, from C[]).
-template <class E>
-__global__ __launch_bounds__(kBlk) void k_build_ptab(DevIndex ix, uint64_t entries,
-                                                     void* __restrict__ tab, uint64_t wmax) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
-  __syncthreads();
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += stride) {
-    uint64_t rest = t;
-    uint32_t c = T.sym[rest % ix.ptab_sigma];
-    rest /= ix.ptab_sigma;
-    uint64_t sp = T.C[c], ep = T.C[c + 1];
-    bool live = sp < ep;
-    for (uint32_t j = 1; j < ix.ptab_k && live; ++j) {
-      c = T.sym[rest % ix.ptab_sigma];
-      rest /= ix.ptab_sigma;
-      live = E::step(ix, T, c, sp, ep);
-    }
-    if (!live) sp = ep = 0;
-    if (ix.wide)  // packed (sp, width), widths >= wmax escaped (fm_device.hpp ptab_at)
-      static_cast<uint64_t*>(tab)[t] = ep - sp >= wmax ? kPtabEsc << 38 : sp | ((ep - sp) << 38);
-    else
-      static_cast<uint2*>(tab)[t] = make_uint2((uint32_t)sp, (uint32_t)ep);
-  }
-}
-
-// Left contexts (fm_device.hpp kCtxQ): row r follows its LF chain q steps (the
-// first line read is shared by neighbouring lanes, the rest are random).
-template <class E>
-__global__ __launch_bounds__(kBlk) void k_build_lctx(DevIndex ix,
-                                                     typename E::CtxEnt* __restrict__ out) {
-  __shared__ NodeTable T;
-  load_table(T, ix.table);
-  __syncthreads();
-  constexpr bool kEsc = sizeof(typename E::CtxEnt) == 2;
-  const uint32_t q = ix.lctx_q, sb = ix.lctx_sb;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < ix.n; r += stride) {
-    uint64_t p = r;
-    uint32_t v = 0;
-    for (uint32_t t = 0; t < q; ++t) {
-      uint32_t c;
-      p = E::lf(ix, T, p, &c);
-      const uint32_t d = T.occ_code[c];
-      v |= (kEsc && d == kNoCode) ? kCtxEsc : d << (sb * t);
-    }
-    out[r] = (typename E::CtxEnt)v;
-  }
-}
 
 // offs == nullptr: patterns of one length fixed_m at stride fixed_m (cs_fm_count_fixed_device);
 // kPacked: pats holds one uint64 per pattern, fixed_m <= 32 2-bit DNA characters (PackedDna);
@@ -2244,14 +1243,6 @@ void k_count_ctx(DevIndex ix, const uint8_t* __restrict__ pats,
     } else if (st[j] == 2 && inl[j] && ix.lctx) {
       bs[j] = sp[j];  // w[j][0..1] already hold rows sp.. from the record (or mrec[j] matched them)
       if (!((cm >> j) & 1u)) w[j][2] = w[j][3] = make_uint4(0, 0, 0, 0);
-    } else if (kSkipLong && !kLoc && ll.sector_list && st[j] == 2 && ix.lctx &&
-               ep[j] - (sp[j] & ~15ull) <= 32) {
-      // (CS_QT_SECTOR_LIST) the sector read left to the list kernel: its range and chain, as a
-      // range too wide for the contexts
-      s_chn[j][threadIdx.x] = list_chain(want[j], k[j]);
-      st[j] = 5;
-      s_rng[j][threadIdx.x][0] = sp[j];
-      s_rng[j][threadIdx.x][1] = ep[j];
     } else if (st[j] == 2 && ix.lctx && ep[j] - (sp[j] & ~15ull) <= 32) {
       bs[j] = sp[j] & ~15ull;
       const uint4* p = reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(ix.lctx) +
@@ -4595,688 +3586,6 @@ __global__ __launch_bounds__(kBlk) void k_bwt(DevIndex ix, uint8_t* __restrict__
 
 }  // namespace
 
-// Dispatch on the handle's engine / rank-line format.
-#define FMX_DISPATCH(h, KERNEL, GRID, ...)                                      \
-  do {                                                                          \
-    if ((h)->line_fmt == kFmtOcc)                                               \
-      KERNEL<OccE><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                       \
-    else if ((h)->line_fmt == kFmtLOcc)                                         \
-      KERNEL<LOccE><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                      \
-    else if ((h)->line_fmt == kFmtQwm)                                          \
-      KERNEL<QWM><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                        \
-    else if ((h)->line_fmt == kFmtLine32)                                       \
-      KERNEL<WM<Line32>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
-    else if ((h)->line_fmt == kFmtLine32W)                                      \
-      KERNEL<WM<Line32W>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                \
-    else                                                                        \
-      KERNEL<WM<Line64>><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
-    FMX_HIP(hipGetLastError());                                                 \
-  } while (0)
-
-// Same, with a second template argument after the engine.
-#define FMX_DISPATCH2(h, KERNEL, TARG, GRID, ...)                               \
-  do {                                                                          \
-    if ((h)->line_fmt == kFmtOcc)                                               \
-      KERNEL<OccE, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                 \
-    else if ((h)->line_fmt == kFmtLOcc)                                         \
-      KERNEL<LOccE, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                \
-    else if ((h)->line_fmt == kFmtQwm)                                          \
-      KERNEL<QWM, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);                  \
-    else if ((h)->line_fmt == kFmtLine32)                                       \
-      KERNEL<WM<Line32>, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);           \
-    else if ((h)->line_fmt == kFmtLine32W)                                      \
-      KERNEL<WM<Line32W>, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);          \
-    else                                                                        \
-      KERNEL<WM<Line64>, TARG><<<(GRID), kBlk, 0, st>>>(__VA_ARGS__);           \
-    FMX_HIP(hipGetLastError());                                                 \
-  } while (0)
-
-// Same, one 64-lane block.
-#define FMX_DISPATCH1(h, KERNEL, ...)                                           \
-  do {                                                                          \
-    if ((h)->line_fmt == kFmtOcc)                                               \
-      KERNEL<OccE><<<1, 64, 0, st>>>(__VA_ARGS__);                              \
-    else if ((h)->line_fmt == kFmtLOcc)                                         \
-      KERNEL<LOccE><<<1, 64, 0, st>>>(__VA_ARGS__);                             \
-    else if ((h)->line_fmt == kFmtQwm)                                          \
-      KERNEL<QWM><<<1, 64, 0, st>>>(__VA_ARGS__);                               \
-    else if ((h)->line_fmt == kFmtLine32)                                       \
-      KERNEL<WM<Line32>><<<1, 64, 0, st>>>(__VA_ARGS__);                        \
-    else if ((h)->line_fmt == kFmtLine32W)                                      \
-      KERNEL<WM<Line32W>><<<1, 64, 0, st>>>(__VA_ARGS__);                       \
-    else                                                                        \
-      KERNEL<WM<Line64>><<<1, 64, 0, st>>>(__VA_ARGS__);                        \
-    FMX_HIP(hipGetLastError());                                                 \
-  } while (0)
-
-// Prefix table over the frequent alphabet: symbols with at least n/2^20
-// occurrences (all present symbols for small texts), k = largest with
-// sigma^k <= min(2^32, max(4096, n/2)) entries of 8 B (at most 4n bytes, capped at
-// 32 GiB); none when k < 2.  Each character in the table saves one dependent random
-// line read per query, and HBM (288 GB) is not the constraint: C4 k = 14 -> 15 is
-// +14 % count rate; C5 k = 15 -> 16 leaves a range of ~7 rows instead of ~30 for the
-// left contexts.  DNA: k = 12 at 100 MB, 15 at 4 GB, 16 at 32 GB.  Entries are (sp, ep)
-// as 2 x u32, or packed (sp, width) in wide indexes (fm_device.hpp ptab_at).
-// CS_FM_PREFIX_K overrides k (0 = off); CS_FM_PTAB_WMAX lowers the escape width (test
-// hook).
-cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
-  NodeTable& T = h->h_table;
-  std::memset(T.code, kNoCode, sizeof T.code);
-  std::memset(T.sym, 0, sizeof T.sym);
-  h->ptab_k = 0;
-  h->ptab_sigma = 0;
-  const uint64_t n = h->n;
-  if (n == 0) return CS_OK;
-  uint32_t sigma = 0;
-  for (int c = 0; c < 256; ++c) {
-    const uint64_t f = T.C[c + 1] - T.C[c];
-    if (f && f * (1ull << 20) >= n) {
-      T.code[c] = (uint8_t)sigma;
-      T.sym[sigma++] = (uint8_t)c;
-    }
-  }
-  if (sigma == 0) return CS_OK;
-  // Entries: at most n for DNA-like alphabets (sigma <= 4; C2 k = 13, C4 k = 15), 8n for
-  // larger ones, where a table character saves a multi-level step (C3, sigma = 256:
-  // k = 4, 2^32 entries, 34 GB: 2x the count rate of k = 3); at most 2^32, and the
-  // table leaves an eighth of HBM free.
-  uint64_t cap = sigma <= 4 ? n : 8 * n;
-  if (cap < 4096) cap = 4096;
-  if (cap > (1ull << 32)) cap = 1ull << 32;
-  size_t free_b = 0, total_b = 0;
-  FMX_HIP(hipMemGetInfo(&free_b, &total_b));
-  uint64_t budget = free_b > total_b / 8 ? (free_b - total_b / 8) / 8 : 0;
-  if (h->hbm_budget) {  // the index's HBM budget: the largest table that still fits it
-    const uint64_t have = index_hbm_bytes(h);
-    const uint64_t left = h->hbm_budget > have ? (h->hbm_budget - have) / h->ptab_entry_bytes() : 0;
-    if (left < budget) budget = left;
-    if (cap > budget) cap = budget;
-  }
-  if (cap > budget && budget >= 4096) cap = budget;
-  uint32_t k = 0;
-  uint64_t entries = 1;
-  while (k < 32 && entries * sigma <= cap) {
-    entries *= sigma;
-    ++k;
-  }
-  if (const char* e = std::getenv("CS_FM_PREFIX_K")) {
-    const int want = std::atoi(e);
-    k = 0;
-    entries = 1;
-    while ((int)k < want && entries * sigma <= (1ull << 32)) {
-      entries *= sigma;
-      ++k;
-    }
-  }
-  if (k < 2 || sigma < 2) {
-    std::memset(T.code, kNoCode, sizeof T.code);
-    return CS_OK;
-  }
-  FMX_HIP(hipMemcpyAsync(h->d_table, &T, sizeof T, hipMemcpyHostToDevice, st));
-  FMX_HIP(hipMalloc(&h->d_ptab, entries * h->ptab_entry_bytes()));
-  h->ptab_sigma = sigma;
-  h->ptab_k = k;
-  DevIndex ix = h->dev();
-  ix.ptab = nullptr;  // the builder itself searches from C[]
-  uint64_t wmax = kPtabEsc;
-  if (const char* e = std::getenv("CS_FM_PTAB_WMAX")) wmax = std::strtoull(e, nullptr, 10);
-  FMX_DISPATCH(h, k_build_ptab, grid_for(entries, kBlk, 65536), ix, entries, h->d_ptab, wmax);
-  FMX_HIP(hipStreamSynchronize(st));
-  return CS_OK;
-}
-
-// Left contexts: u16 per row over occurrence lines (2n bytes; C4 8 GB), u32 over the
-// quaternary matrix (4n bytes; C3 4 GB); rows rounded up to whole 32-B sectors plus
-// one pad sector.  Skipped (count steps through the rank structure instead) for the
-// binary wavelet matrix, when CS_FM_LCTX=0, or when HBM is short: the index must
-// leave an eighth of the device free (36 GB on MI355X) for the query buffers.
-cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
-  h->d_lctx = nullptr;
-  h->nlctx = 0;
-  h->lctx_q = h->lctx_sb = h->lctx_eb = 0;
-  const bool occ = h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc, qwm = h->line_fmt == kFmtQwm;
-  if (!(occ || qwm) || h->n == 0) return CS_OK;
-  if (const char* e = std::getenv("CS_FM_LCTX"))
-    if (std::atoi(e) == 0) return CS_OK;
-  const uint32_t eb = occ ? 2 : 4, R = 32 / eb;
-  const uint32_t sb = occ ? 2 : 2 * h->h_table.qlevels;
-  const uint32_t q = occ ? kCtxQ : (32 / sb < 16 ? 32 / sb : 16);
-  const uint64_t rows = ((h->n + R - 1) & ~(uint64_t)(R - 1)) + R;
-  if (!hbm_room(h, rows * eb)) return CS_OK;
-  FMX_HIP(hipMalloc(&h->d_lctx, rows * eb));
-  h->nlctx = rows;
-  h->lctx_q = q;
-  h->lctx_sb = sb;
-  h->lctx_eb = eb;
-  FMX_HIP(hipMemsetAsync(static_cast<uint8_t*>(h->d_lctx) + h->n * eb, 0, (rows - h->n) * eb, st));
-  const DevIndex ix = h->dev();
-  if (h->line_fmt == kFmtLOcc)
-    k_build_lctx<LOccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
-        ix, static_cast<uint16_t*>(h->d_lctx));
-  else if (occ)
-    k_build_lctx<OccE><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
-        ix, static_cast<uint16_t*>(h->d_lctx));
-  else
-    k_build_lctx<QWM><<<grid_for(h->n, kBlk, 65536), kBlk, 0, st>>>(
-        ix, static_cast<uint32_t*>(h->d_lctx));
-  FMX_HIP(hipGetLastError());
-  FMX_HIP(hipStreamSynchronize(st));
-  return CS_OK;
-}
-
-// Context records (fm_device.hpp kRecCtx) from the 8-B table and the left contexts:
-// one lane per k-mer.
-__global__ __launch_bounds__(kBlk) void k_fill_records(const uint2* __restrict__ tab,
-                                                       uint64_t entries,
-                                                       const uint16_t* __restrict__ lctx,
-                                                       uint32_t* __restrict__ rec) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
-    const uint2 e = tab[t];
-    const uint32_t w = e.y - e.x;
-    uint32_t d[6] = {0, 0, 0, 0, 0, 0};
-    for (uint32_t i = 0; i < kRecCtx && i < w; ++i) d[i >> 1] |= (uint32_t)lctx[e.x + i] << (16 * (i & 1));
-    uint4* r = reinterpret_cast<uint4*>(rec) + t * 2;
-    r[0] = make_uint4(e.x, w, d[0], d[1]);
-    r[1] = make_uint4(d[2], d[3], d[4], d[5]);
-  }
-}
-
-// Compact 16-B records (fm_device.hpp kRec16Ctx): the width inline when at most
-// kRec16Ctx rows and no row's context is escaped, else kRec16Wide and the width.
-__global__ __launch_bounds__(kBlk) void k_fill_records16(const uint2* __restrict__ tab,
-                                                         uint64_t entries,
-                                                         const uint16_t* __restrict__ lctx,
-                                                         uint4* __restrict__ rec) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
-    const uint2 e = tab[t];
-    const uint32_t w = e.y - e.x;
-    bool esc = false;
-    uint64_t lo = 0;
-    uint32_t hi = 0;
-    for (uint32_t i = 0; i < kRec16Ctx && i < w; ++i) {
-      const uint32_t c = lctx[e.x + i];
-      esc |= (c & kCtxEsc) != 0;
-      if (i < 6)
-        lo |= (uint64_t)(c & 0x3FFu) << (4 + 10 * i);
-      else
-        hi |= (c & 0x3FFu) << (10 * (i - 6));
-    }
-    if (w <= kRec16Ctx && !esc) {
-      rec[t] = make_uint4(e.x, (uint32_t)lo | w, (uint32_t)(lo >> 32), hi);
-      continue;
-    }
-    // a wide range: its two most frequent contexts (Misra-Gries with two counters finds every
-    // context above a third of the rows; a second pass counts the candidates exactly)
-    uint32_t y = kRec16Wide, w3 = 0;
-    if (!esc && w > kRec16Ctx && w <= kRec16MajScan) {
-      uint32_t ca = 0, cb = 0, na = 0, nb = 0;
-      for (uint32_t i = 0; i < w && !esc; ++i) {
-        const uint32_t c = lctx[e.x + i];
-        esc |= (c & kCtxEsc) != 0;
-        const uint32_t v = c & 0x3FFu;
-        if (na && v == ca) ++na;
-        else if (nb && v == cb) ++nb;
-        else if (!na) ca = v, na = 1;
-        else if (!nb) cb = v, nb = 1;
-        else --na, --nb;
-      }
-      uint32_t xa = 0, xb = 0;
-      for (uint32_t i = 0; i < w && !esc; ++i) {
-        const uint32_t v = lctx[e.x + i] & 0x3FFu;
-        xa += na && v == ca;
-        xb += nb && v == cb;
-      }
-      if (!esc && na && xb > xa) {  // A the more frequent
-        const uint32_t tc = ca; ca = cb; cb = tc;
-        const uint32_t tx = xa; xa = xb; xb = tx;
-      }
-      if (!esc && xa && xa <= 0xFFFFu && xb <= 0xFFFFu) {
-        y |= kRec16Maj | (ca << 6) | (xb ? cb << 16 : 0u);
-        if (xa + xb == w) y |= kRec16MajAll;
-        w3 = xa | (xb << 16);
-      }
-    }
-    rec[t] = make_uint4(e.x, y, w, w3);
-  }
-}
-
-// Compact records of a wide index from its packed 8-B table (fm_device.hpp kRec16CtxW):
-// 4-character contexts of rows 0-9, bits 32-37 of sp in dword 3.
-__global__ __launch_bounds__(kBlk) void k_fill_records16_wide(const uint64_t* __restrict__ tab,
-                                                              uint64_t entries,
-                                                              const uint16_t* __restrict__ lctx,
-                                                              uint4* __restrict__ rec) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
-    const uint64_t e = tab[t], w = e >> 38, sp = e & ((1ull << 38) - 1);
-    const uint32_t sph = (uint32_t)(sp >> 32) << 24;
-    if (w == kPtabEsc) {  // the 8-B table escaped this range: the search starts from C[]
-      rec[t] = make_uint4(0u, kRec16Wide, kRec16NoRange, 0u);
-      continue;
-    }
-    bool esc = false;
-    uint32_t y = 0, z = 0, x3 = 0;
-    for (uint32_t i = 0; i < kRec16CtxW && i < w; ++i) {
-      const uint32_t c = lctx[sp + i];
-      esc |= (c & kCtxEsc) != 0;
-      const uint32_t b = c & 0xFFu;
-      if (i < 3)
-        y |= b << (4 + 8 * i);
-      else if (i < 7)
-        z |= b << (8 * (i - 3));
-      else
-        x3 |= b << (8 * (i - 7));
-    }
-    if (w > kRec16CtxW || esc)
-      rec[t] = make_uint4((uint32_t)sp, kRec16Wide, (uint32_t)w, sph);
-    else
-      rec[t] = make_uint4((uint32_t)sp, y | (uint32_t)w, z, x3 | sph);
-  }
-}
-
-// Quaternary-matrix records (fm_device.hpp kRecQCtx): sp, width, contexts of rows 0-1.
-__global__ __launch_bounds__(kBlk) void k_fill_records_q(const uint2* __restrict__ tab,
-                                                         uint64_t entries,
-                                                         const uint32_t* __restrict__ lctx,
-                                                         uint4* __restrict__ rec) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
-    const uint2 e = tab[t];
-    const uint32_t w = e.y - e.x;
-    rec[t] = make_uint4(e.x, w, w > 0 && w <= kRecQCtx ? lctx[e.x] : 0u,
-                        w > 1 && w <= kRecQCtx ? lctx[e.x + 1] : 0u);
-  }
-}
-
-// Replace the 8-B prefix table by 32-B context records (narrow occurrence-engine
-// indexes with left contexts; C4: 34 GB for k = 15) when HBM allows (an eighth of the
-// device stays free) and the table spans at least 13 characters: records pay for
-// patterns of k+1 .. k+7 characters (the 20-mers of the DNA configs from k = 13 on:
-// C2, k = 13: 2.35e10 patterns/s with records, 1.64e10 without) and cost 4x the plain
-// table's reads in bytes otherwise (C2, k = 12: 7.9e9 with records, 9.1e9 without).  CS_FM_CTX_RECORDS=0 keeps the plain table, =1 forces
-// records for any k (test hook), =16 forces the compact 16-B records, which replace the
-// 32-B ones by default from k = 15 when the table's mean range is at most 4 rows (C4:
-// n / 4^15 = 3.7; a range wider than kRec16Ctx rows or a pattern with 6-7 characters
-// left after the table then reads its context sector).
-cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
-  h->ptab_rec = 0;
-  if (!h->d_ptab || !h->ptab_k || !h->d_lctx) return CS_OK;
-  if (h->wide && h->lctx_eb != 2) return CS_OK;  // wide records: occurrence lines only
-  const uint64_t entries = h->ptab_entries();
-  if (h->lctx_eb == 4) {  // quaternary matrix: 16-B records when ranges average <= 2 rows
-    if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
-      if (std::atoi(e) == 0) return CS_OK;
-    if (h->n > kRecQCtx * entries) return CS_OK;
-    // the records replace the 8-B table
-    if (!hbm_room(h, entries * 16, entries * h->ptab_entry_bytes())) return CS_OK;
-    void* rq = nullptr;
-    FMX_HIP(hipMalloc(&rq, entries * 16));
-    k_fill_records_q<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
-        static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint32_t*>(h->d_lctx),
-        static_cast<uint4*>(rq));
-    hipError_t eq = hipGetLastError();
-    if (eq == hipSuccess) eq = hipStreamSynchronize(st);
-    if (eq != hipSuccess) {
-      (void)hipFree(rq);
-      return hip_fail(eq, "context records");
-    }
-    FMX_HIP(hipFree(h->d_ptab));
-    h->d_ptab = rq;
-    h->ptab_rec = 3;
-    return CS_OK;
-  }
-  if (h->lctx_eb != 2) return CS_OK;
-  // a record answers patterns of up to k + q characters: q = 7 (32 B) from k = 13 covers
-  // the 20-mers of the DNA workloads; the compact q = 5 still does from k = 15
-  bool want = h->ptab_k >= 13;
-  uint32_t fmt = h->ptab_k >= 15 && h->n <= 4 * entries ? 2 : 1;
-  if (h->wide) {  // compact only (sp needs more than 32 bits); ranges averaging <= 8 rows
-    want = h->ptab_k >= 15 && h->n <= 8 * entries;
-    fmt = 2;
-  }
-  if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) {
-    want = std::atoi(e) != 0;
-    fmt = h->wide || std::atoi(e) == 16 ? 2 : 1;
-  }
-  if (!want) return CS_OK;
-  const uint64_t bytes = entries * (fmt == 2 ? 16 : 32);
-  // the records replace the 8-B table
-  if (!hbm_room(h, bytes, entries * h->ptab_entry_bytes())) return CS_OK;
-  void* rec = nullptr;
-  FMX_HIP(hipMalloc(&rec, bytes));
-  if (h->wide)
-    k_fill_records16_wide<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
-        static_cast<const uint64_t*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
-        static_cast<uint4*>(rec));
-  else if (fmt == 2)
-    k_fill_records16<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
-        static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
-        static_cast<uint4*>(rec));
-  else
-    k_fill_records<<<grid_for(entries, kBlk, 65536), kBlk, 0, st>>>(
-        static_cast<const uint2*>(h->d_ptab), entries, static_cast<const uint16_t*>(h->d_lctx),
-        static_cast<uint32_t*>(rec));
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) {
-    (void)hipFree(rec);
-    return hip_fail(e, "context records");
-  }
-  FMX_HIP(hipFree(h->d_ptab));
-  h->d_ptab = rec;
-  h->ptab_rec = fmt;
-  return CS_OK;
-}
-
-// The text in HBM for extract (the reference keeps text_, fm_index.hpp:41): n bytes
-// (C4: 4 GB, C5: 32 GB), kept when an eighth of the device stays free;
-// CS_FM_DEVICE_TEXT=0 leaves extract to LF inversion from the inverse-SA samples.
-cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_device, hipStream_t st) {
-  if (!src || !h->n || h->d_dtext) return CS_OK;
-  // (round 6: without the byte text, a walk_verify() index still takes the 2-bit text of the
-  // build's device text — C5: 8 GB where the 32-GB text does not fit the eighth)
-  const uint8_t* dsrc = src_on_device ? src : nullptr;
-  if (const char* e = std::getenv("CS_FM_DEVICE_TEXT"))
-    if (std::atoi(e) == 0) return derive_packed_text(h, st, dsrc);
-  if (!hbm_room(h, h->n)) return derive_packed_text(h, st, dsrc);
-  FMX_HIP(hipMalloc(&h->d_dtext, h->n + kPartPad));
-  FMX_HIP(hipMemsetAsync(static_cast<uint8_t*>(h->d_dtext) + h->n, 0, kPartPad, st));
-  FMX_HIP(hipMemcpyAsync(h->d_dtext, src, h->n,
-                         src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
-  FMX_HIP(hipStreamSynchronize(st));
-  return derive_packed_text(h, st);
-}
-
-// The 2-bit text (cs_fm_index::d_ptext): word w holds the occurrence codes of text[32 w,
-// 32 w + 32), rare symbols as code 0, their positions appended to `rare` (at most cap, the
-// counter counts them all).  A thread per word.
-__global__ __launch_bounds__(kBlk) void k_pack_text(const uint8_t* __restrict__ text, uint64_t n,
-                                                    const NodeTable* __restrict__ table,
-                                                    uint64_t* __restrict__ out, uint64_t nw,
-                                                    uint64_t* __restrict__ rare, uint32_t cap,
-                                                    unsigned int* __restrict__ nrare) {
-  __shared__ uint8_t code[256];
-  if (threadIdx.x < 256) code[threadIdx.x] = table->occ_code[threadIdx.x];
-  __syncthreads();
-  const uint64_t w = blockIdx.x * (uint64_t)kBlk + threadIdx.x;
-  if (w >= nw) return;
-  const uint64_t* tw = reinterpret_cast<const uint64_t*>(text) + 4 * w;  // the text has kPartPad slack
-  uint64_t acc = 0;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const uint64_t x = tw[c];
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const uint64_t i = 32 * w + 8 * c + b;
-      if (i >= n) break;
-      const uint32_t d = code[(uint32_t)(x >> (8 * b)) & 0xFFu];
-      if (d == kNoCode) {
-        const unsigned int e = atomicAdd(nrare, 1u);
-        if (e < cap) rare[e] = i;
-      } else {
-        acc |= (uint64_t)d << (2 * (8 * c + b));
-      }
-    }
-  }
-  out[w] = acc;
-}
-
-// the last, partial word of the 2-bit text (`len` < 32 characters at text position `at`,
-// from a zero-padded copy): one lane
-__global__ void k_pack_text_tail(const uint8_t* __restrict__ text, uint64_t len, uint64_t at,
-                                 const NodeTable* __restrict__ table, uint64_t* __restrict__ out,
-                                 uint64_t* __restrict__ rare, uint32_t cap, unsigned int* __restrict__ nrare) {
-  if (threadIdx.x != 0) return;
-  uint64_t acc = 0;
-  for (uint64_t i = 0; i < len; ++i) {
-    const uint32_t d = table->occ_code[text[i]];
-    if (d == kNoCode) {
-      const unsigned int e = atomicAdd(nrare, 1u);
-      if (e < cap) rare[e] = at + i;
-    } else {
-      acc |= (uint64_t)d << (2 * i);
-    }
-  }
-  *out = acc;
-}
-
-// Long patterns are verified against 32 text characters per 8-B word instead of 8
-// (k_count_long): n / 4 bytes (C4: 1 GB), for narrow lf_exact occurrence-line indexes that
-// keep the full suffix array and the text in HBM (the verification's preconditions), and
-// (round 6) for walk_verify() indexes — no full SA, walk lines with text-position marks (C5:
-// 8 GB), whose long patterns are verified at their walks' positions — HBM allowing.  Derived
-// from the text kept in HBM or, for walk_verify() indexes, from the build's device text
-// `src`; rebuilt on open / import rather than saved.  The rare-symbol positions go to d_prare
-// (u32, narrow) or d_prare64 (u64, walk_verify()).  CS_FM_PACKED_TEXT=0 (read at build /
-// open) leaves it out.
-cs_status derive_packed_text(cs_fm_index* h, hipStream_t st, const uint8_t* src) {
-  if (h->d_ptext || h->line_fmt != kFmtOcc || !h->lf_exact || !h->n) return CS_OK;
-  const bool narrow_sa = h->d_sa && !h->wide && h->n < (1ull << 32);
-  const bool walk = h->walk_verify();
-  const uint8_t* text = h->d_dtext ? static_cast<const uint8_t*>(h->d_dtext) : src;
-  if (!text || !(narrow_sa || walk)) return CS_OK;
-  if (narrow_sa && !h->d_dtext) return CS_OK;  // (its verification reads the byte text too)
-  if (const char* e = std::getenv("CS_FM_PACKED_TEXT"))
-    if (std::atoi(e) == 0) return CS_OK;
-  const uint64_t nw = (h->n + 31) / 32;
-  if (!hbm_room(h, nw * 8, 0, h->d_dtext ? 0 : h->n)) return CS_OK;
-  void* pt = nullptr;
-  FMX_HIP(hipMalloc(&pt, nw * 8 + kPartPad));
-  DevBuf rb;
-  if (rb.alloc(kMaxExc * 8 + 8) != hipSuccess) {
-    (void)hipFree(pt);
-    return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
-  }
-  unsigned int* d_n = reinterpret_cast<unsigned int*>(rb.as<uint8_t>() + kMaxExc * 8);
-  hipError_t e = hipMemsetAsync(d_n, 0, 4, st);
-  if (e == hipSuccess && !h->d_dtext) {
-    // (the caller's text has no kPartPad slack: the last word is packed from a padded copy)
-    const uint64_t full = h->n / 32;
-    if (full)
-      k_pack_text<<<grid_for(full, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(text, full * 32, h->d_table,
-                                                                        static_cast<uint64_t*>(pt), full,
-                                                                        rb.as<uint64_t>(), kMaxExc, d_n);
-    e = hipGetLastError();
-    if (e == hipSuccess && full < nw) {
-      DevBuf tail;
-      e = tail.alloc(64);
-      if (e == hipSuccess) e = hipMemsetAsync(tail.p, 0, 64, st);
-      if (e == hipSuccess) e = hipMemcpyAsync(tail.p, text + full * 32, h->n - full * 32, hipMemcpyDeviceToDevice, st);
-      if (e == hipSuccess)
-        k_pack_text_tail<<<1, 64, 0, st>>>(tail.as<uint8_t>(), h->n - full * 32, full * 32, h->d_table,
-                                           static_cast<uint64_t*>(pt) + full, rb.as<uint64_t>(), kMaxExc, d_n);
-      if (e == hipSuccess) e = hipGetLastError();
-      if (e == hipSuccess) e = hipStreamSynchronize(st);
-    }
-  } else if (e == hipSuccess) {
-    k_pack_text<<<grid_for(nw, kBlk, 0xFFFFFFFFu), kBlk, 0, st>>>(
-        text, h->n, h->d_table, static_cast<uint64_t*>(pt), nw, rb.as<uint64_t>(), kMaxExc, d_n);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipMemsetAsync(static_cast<uint8_t*>(pt) + nw * 8, 0, kPartPad, st);
-  unsigned int nr = 0;
-  std::vector<uint64_t> pos(kMaxExc);
-  if (e == hipSuccess) e = hipMemcpyAsync(&nr, d_n, 4, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipMemcpyAsync(pos.data(), rb.p, kMaxExc * 8, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess || nr > (unsigned)kMaxExc) {  // more rare positions than the list holds
-    (void)hipFree(pt);
-    return e == hipSuccess ? CS_OK : hip_fail(e, "packed text");
-  }
-  pos.resize(nr);
-  std::sort(pos.begin(), pos.end());
-  void* pr = nullptr;
-  if (walk) {
-    if (hipMalloc(&pr, kMaxExc * 8) != hipSuccess ||
-        (nr && hipMemcpy(pr, pos.data(), nr * 8, hipMemcpyHostToDevice) != hipSuccess)) {
-      (void)hipFree(pt);
-      if (pr) (void)hipFree(pr);
-      return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
-    }
-    h->d_prare64 = pr;
-    h->nrare64 = nr;
-  } else {
-    std::vector<uint32_t> p32(pos.begin(), pos.end());
-    if (hipMalloc(&pr, kMaxExc * 4) != hipSuccess ||
-        (nr && hipMemcpy(pr, p32.data(), nr * 4, hipMemcpyHostToDevice) != hipSuccess)) {
-      (void)hipFree(pt);
-      if (pr) (void)hipFree(pr);
-      return hip_fail(hipGetLastError(), "hipMalloc (packed text)");
-    }
-    h->d_prare = pr;
-    h->nrare = nr;
-  }
-  h->d_ptext = pt;
-  return CS_OK;
-}
-
-// Locate records (fm_device.hpp kLocRec*) of the (k+1)-mers c.x, from the k-mer x's context
-// record and left contexts: a lane per k-mer x.  The rows of c.x are the rows r of x whose
-// chain starts with c (BWT[r] = c), in order (LF keeps the order of equal symbols); each
-// gives SA[r] - 1 (mod n) and its chain shifted by one symbol.  o2d: the table digit of
-// occurrence code o in byte o.  A range wider than kLocRecScan rows, or one holding an
-// escaped context, makes all four children kLocRecNone (their locates read the context
-// record instead); a child with more than kLocRecRows rows is kLocRecNone too.
-constexpr uint32_t kLocRecScan = 64;
-__global__ __launch_bounds__(kBlk) void k_fill_locrec(const uint4* __restrict__ rec, uint32_t ptab_rec,
-                                                      uint64_t entries,
-                                                      const uint16_t* __restrict__ lctx,
-                                                      const uint32_t* __restrict__ sa, uint64_t n,
-                                                      uint32_t o2d, uint4* __restrict__ out) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
-    // a 32-B record (ptab_rec 1): sp and the width, the rows' contexts from lctx (as for a
-    // compact record too wide for its inline contexts)
-    const uint4 a = ptab_rec == 1 ? make_uint4(rec[2 * t].x, kRec16Wide, rec[2 * t].y, 0u) : rec[t];
-    const uint32_t wc = a.y & 15u;
-    const bool wide = wc == kRec16Wide;
-    const uint64_t sp = a.x;
-    const uint32_t w = wide ? a.z : wc;
-    bool none = wide && (a.z == kRec16NoRange || a.z > kLocRecScan);
-    uint32_t ctx10[kRec16Ctx];  // inline record: the rows' 5-symbol chains
-    if (!wide) {
-      uint32_t dw[5];
-      rec16_contexts(a.y, a.z, a.w, dw);
-#pragma unroll
-      for (uint32_t i = 0; i < kRec16Ctx; ++i) ctx10[i] = (dw[i >> 1] >> (16 * (i & 1))) & 0x3FFu;
-    }
-    if (wide && !none)
-      for (uint32_t i = 0; i < w; ++i) none |= (lctx[sp + i] & kCtxEsc) != 0;
-#pragma unroll
-    for (uint32_t d = 0; d < 4; ++d) {
-      uint32_t c = 0, cx = 0, sv[kLocRecRows] = {0u, 0u, 0u};
-      for (uint32_t i = 0; i < w && !none; ++i) {
-        const uint32_t e = wide ? lctx[sp + i] : ctx10[i < kRec16Ctx ? i : 0];
-        if (((o2d >> (8 * (e & 3u))) & 0xFFu) != d) continue;
-        if (c < kLocRecRows) {
-          const uint32_t v = sa[sp + i];
-          const uint32_t v1 = v ? v - 1u : (uint32_t)(n - 1);
-#pragma unroll
-          for (uint32_t r = 0; r < kLocRecRows; ++r)
-            if (r == c) sv[r] = v1;
-          cx |= ((e >> 2) & 0xFFu) << (8 * c);
-        }
-        ++c;
-      }
-      out[(uint64_t)d * entries + t] = none || c > kLocRecRows
-                                           ? make_uint4(0u, 0u, 0u, kLocRecNone << 24)
-                                           : make_uint4(sv[0], sv[1], sv[2], cx | (c << 24));
-    }
-  }
-}
-
-// 64-B locate records (fm_device.hpp kLocRec64*): the record of k-mer t from its context
-// record (sp, width, inline contexts) or lctx, and the rows' SA entries
-__global__ __launch_bounds__(kBlk) void k_fill_locrec64(const uint4* __restrict__ rec, uint32_t ptab_rec,
-                                                        uint64_t entries,
-                                                        const uint16_t* __restrict__ lctx,
-                                                        const uint32_t* __restrict__ sa,
-                                                        uint4* __restrict__ out) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < entries; t += gs) {
-    const uint4 a = ptab_rec == 1 ? make_uint4(rec[2 * t].x, kRec16Wide, rec[2 * t].y, 0u) : rec[t];
-    const uint32_t wc = a.y & 15u;
-    const bool wide = wc == kRec16Wide;
-    const uint64_t sp = a.x;
-    const uint32_t w = wide ? a.z : wc;
-    bool none = w > kLocRec64Rows || (wide && a.z == kRec16NoRange);
-    uint32_t ctx10[kRec16Ctx];  // inline record: the rows' 5-symbol chains
-    if (!wide) {
-      uint32_t dw[5];
-      rec16_contexts(a.y, a.z, a.w, dw);
-#pragma unroll
-      for (uint32_t i = 0; i < kRec16Ctx; ++i) ctx10[i] = (dw[i >> 1] >> (16 * (i & 1))) & 0x3FFu;
-    }
-    if (wide && !none)
-      for (uint32_t i = 0; i < w; ++i) none |= (lctx[sp + i] & kCtxEsc) != 0;
-#pragma unroll
-    for (uint32_t c = 0; c < 4; ++c) {
-      uint4 o = make_uint4(~0u, 0u, 0u, 0u);
-      if (!none) {
-        const uint32_t vc = w > 3 * c ? (w - 3 * c < 3 ? w - 3 * c : 3u) : 0u;
-        uint32_t sv[3] = {0u, 0u, 0u}, cx = vc << 30;
-        for (uint32_t i = 0; i < vc; ++i) {
-          const uint32_t r = 3 * c + i;
-          sv[i] = sa[sp + r];
-          cx |= (wide ? (uint32_t)lctx[sp + r] & 0x3FFu : ctx10[r < kRec16Ctx ? r : 0]) << (10 * i);
-        }
-        o = make_uint4(sv[0], sv[1], sv[2], cx);
-      }
-      out[4 * t + c] = o;
-    }
-  }
-}
-
-// Build the locate records when the index can use them: narrow lf_exact occurrence-line
-// indexes with context records (16 B, or 32 B: C2) over a 4-symbol table of k <= 15, the
-// left contexts and the full suffix array (C4: k = 15 -> 4^16 records, 69 GB; C2: k = 13 ->
-// 4^14, 4.3 GB), HBM allowing (an eighth of the
-// device stays free; within CS_FM_HBM_BUDGET).  CS_FM_LOC_RECORDS=0 (read at build / open /
-// import) leaves them out.  Derived from the other parts, not saved.
-cs_status derive_locate_records(cs_fm_index* h, hipStream_t st) {
-  if (h->d_lrec || (h->ptab_rec != 1 && h->ptab_rec != 2) || !h->d_ptab || !h->d_sa || !h->lf_exact || h->wide ||
-      !h->d_lctx || h->lctx_eb != 2 || h->line_fmt != kFmtOcc || h->ptab_sigma != 4 ||
-      h->ptab_k < 1 || h->ptab_k + 1 > 16 || h->n >= (1ull << 32))
-    return CS_OK;
-  if (const char* e = std::getenv("CS_FM_LOC_RECORDS"))
-    if (std::atoi(e) == 0) return CS_OK;
-  // the table digit of each occurrence code; every code must have one
-  uint32_t o2d = 0xFFFFFFFFu;
-  for (int c = 0; c < 256; ++c) {
-    const uint32_t oc = h->h_table.occ_code[c], d = h->h_table.code[c];
-    if (oc < 4 && d < 4) o2d = (o2d & ~(0xFFu << (8 * oc))) | (d << (8 * oc));
-  }
-  for (int oc = 0; oc < 4; ++oc)
-    if (((o2d >> (8 * oc)) & 0xFFu) >= 4) return CS_OK;
-  const uint64_t entries = h->ptab_entries(), bytes = entries * 4 * 16;  // either layout
-  if (!hbm_room(h, bytes)) return CS_OK;
-  // CS_FM_LOC_REC64=0 (read at build / open / import): the 16-B (k+1)-mer records of early
-  // round 4 instead of the 64-B k-mer ones
-  bool w64 = true;
-  if (const char* e = std::getenv("CS_FM_LOC_REC64"))
-    w64 = std::atoi(e) != 0;
-  void* p = nullptr;
-  FMX_HIP(hipMalloc(&p, bytes));
-  if (w64)
-    k_fill_locrec64<<<grid_for(entries, kBlk, 1u << 20), kBlk, 0, st>>>(
-        static_cast<const uint4*>(h->d_ptab), h->ptab_rec, entries, static_cast<const uint16_t*>(h->d_lctx),
-        static_cast<const uint32_t*>(h->d_sa), static_cast<uint4*>(p));
-  else
-    k_fill_locrec<<<grid_for(entries, kBlk, 1u << 20), kBlk, 0, st>>>(
-        static_cast<const uint4*>(h->d_ptab), h->ptab_rec, entries, static_cast<const uint16_t*>(h->d_lctx),
-        static_cast<const uint32_t*>(h->d_sa), h->n, o2d, static_cast<uint4*>(p));
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) {
-    (void)hipFree(p);
-    return hip_fail(e, "locate records");
-  }
-  h->d_lrec = p;
-  h->lrec_w = w64 ? 64 : 16;
-  return CS_OK;
-}
 
 cs_status launch_extract(const cs_fm_index* h, const uint64_t* d_pos, const uint64_t* d_len,
                          const uint64_t* d_out_offs, uint64_t k, uint8_t* d_out, hipStream_t st) {
@@ -5575,7 +3884,6 @@ cs_status launch_count_staged(const cs_fm_index* h, const DevIndex& ix, const ui
     lb.ll.gen_list = (flags & CS_QT_GENERAL_INLANE) ? 0u : (flags & CS_QT_GENERAL_LIST_ALL) ? 1u
                      : ix.vsa ? h->gen_list_min : 0u;
     lb.ll.grid = h->list_grid;
-    lb.ll.sector_list = (flags & CS_QT_SECTOR_LIST) ? 1u : 0u;
     if (nobar)
       k_count_ctx<OccE, 2, false, false, W, true, false, true><<<g2, kBlk, 0, st>>>(
           ix, d_pats, d_offs, npat, co, 0, nullptr, fixed_m, OnePass{}, lb.ll);

@@ -9,7 +9,7 @@
 #ifndef CS_FMINDEX_TUNING_H
 #define CS_FMINDEX_TUNING_H
 
-/* Tuning selectors (round 5): flags bits 8-25 choose among equivalent kernels for tests and
+/* Tuning selectors (round 5): flags bits 8-24 choose among equivalent kernels for tests and
  * A/B measurements — results never change.  A handle takes its defaults from the CS_FM_*
  * environment once, when it is created (build, create, open, import: the variable named
  * beside each bit), and a call's flags are ORed over them: a call can add a selector but
@@ -37,9 +37,6 @@
  *                         the list kernel (CS_FM_GENERAL_INLANE=1)
  *   CS_QT_GENERAL_LIST_ALL routed count: every wave lists its general searches
  *                         (CS_FM_GENERAL_LIST_ALL=1)
- *   CS_QT_SECTOR_LIST     routed count: a pattern whose range needs its context sectors (a
- *                         second dependent read) is listed like a general search, with its
- *                         range, instead of read in the lane (CS_FM_SECTOR_LIST=1)
  *   CS_QT_MAP_LDS         staged count / locate: characters mapped through the LDS symbol table
  *                         even for the standard DNA code (default: four per dword in registers;
  *                         CS_FM_MAP_LDS=1) */
@@ -59,7 +56,6 @@
 #define CS_QT_WALK_PERSISTENT (1u << 21)
 #define CS_QT_GENERAL_INLANE (1u << 22)
 #define CS_QT_GENERAL_LIST_ALL (1u << 23)
-#define CS_QT_SECTOR_LIST (1u << 24)
-#define CS_QT_MAP_LDS (1u << 25)
+#define CS_QT_MAP_LDS (1u << 24)
 
 #endif /* CS_FMINDEX_TUNING_H */

@@ -111,7 +111,7 @@ def test_tuning_selectors_mirror_header():
     pkg = load_pkg()
     src = open(os.path.join(ROOT, "include", "cs_fmindex_tuning.h")).read()
     bits = {k: 1 << int(v) for k, v in re.findall(r"#define CS_(QT_[A-Z0-9_]+) \(1u << (\d+)\)", src)}
-    assert len(bits) == 18
+    assert len(bits) == 17
     for k, v in bits.items():
         assert getattr(pkg, k) == v, k
     assert "#define CS_QT_" not in open(os.path.join(ROOT, "include", "cs_fmindex.h")).read()

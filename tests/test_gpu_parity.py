@@ -735,7 +735,7 @@ def _substrings_and_mutants(t, lengths, per, seed):
 
 
 def _count_bo(g, buf, offs, flags=0):
-    """count of a packed batch (buf, offs) through cs_fm_count_batch_device_ex under flags."""
+    """count of a packed batch (buf, offs) through cs_fm_count_device under flags."""
     d_buf = torch.from_numpy(np.ascontiguousarray(buf).copy()).cuda()
     d_offs = torch.from_numpy(np.asarray(offs).astype(np.int64)).cuda()
     npat = len(offs) - 1
@@ -1212,6 +1212,32 @@ def test_selectors_without_a_variant(pkg):
             assert np.array_equal(np.cumsum([0] + [len(q) for q in got]), woffs.astype(np.int64)), (name, lim)
             flat = [x for q in got for x in q]
             assert np.array_equal(np.asarray(flat, np.int64), wpos.astype(np.int64)), (name, lim)
+
+
+def test_dna_character_map(pkg):
+    """The staged count maps a standard-DNA index's characters four per dword in registers
+    (fm_query.hip, DevIndex::dna_std, round 6) and every other index's through the LDS table;
+    CS_QT_MAP_LDS forces the table.  Patterns of text substrings with one byte replaced by each
+    of the 256 byte values (lowercase acgt, 'N', 0xC1 = 'A' | 0x80, 'E' whose bits read as 'G',
+    NUL) at every position of a 20-mer and a 9-mer, plus uniform patterns, give the oracle's
+    counts both ways."""
+    t = O.gen_dna(91, 120_000).tobytes()
+    g = pkg.FMIndex.build_from_text(t)
+    o = O.Index(t)
+    u8 = np.frombuffer(t, np.uint8)
+    rng = np.random.default_rng(41)
+    pats = []
+    for m, seed in ((20, 3), (9, 4), (31, 5)):
+        base = [bytes(p) for p in O.gen_patterns_text(u8, m, 256, seed=seed)]
+        for b, p in enumerate(base):
+            q = bytearray(p)
+            q[int(rng.integers(0, m))] = b
+            pats += [p, bytes(q)]
+    pats += [bytes(rng.choice(list(b"ACGT"), int(m)).astype(np.uint8)) for m in rng.integers(1, 33, 300)]
+    buf, offs = O.pack_patterns(pats)
+    want = o.count_batch(buf=buf, offs=offs, nthreads=8)
+    assert np.array_equal(_count_bo(g, buf, offs), want)
+    assert np.array_equal(_count_bo(g, buf, offs, flags=pkg.QT_MAP_LDS), want)
 
 
 def test_majority_records_vs_oracle(pkg):
