@@ -18,6 +18,8 @@ import ctypes as C
 import os
 from dataclasses import dataclass
 
+import threading
+
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -41,6 +43,48 @@ _u8p = C.POINTER(C.c_uint8)
 _u64p = C.POINTER(C.c_uint64)
 _u32p = C.POINTER(C.c_uint32)
 _vp = C.c_void_p
+
+
+_opts_tls = threading.local()
+
+
+def _options_text(options) -> str:
+    if isinstance(options, dict):
+        return " ".join(f"{k}={v}" for k, v in options.items())
+    return str(options)
+
+
+def _options_arg(options):
+    """An explicit options string for cs_fm_build_with_options, or None."""
+    return None if options is None else _options_text(options).encode()
+
+
+def _set_thread_options(options):
+    _check(lib().cs_fm_set_build_options(None if options is None else _options_text(options).encode()))
+
+
+class build_options:
+    """with build_options(ENGINE="wavelet", FULL_SA=0): every handle this thread constructs
+    inside (build, create, open_directory, import) uses exactly these choices and reads no
+    CS_FM_* environment variable (cs_fm_set_build_options); nested scopes replace, not merge."""
+
+    def __init__(self, options=None, **kw):
+        self.options = dict(options or {}, **kw)
+
+    def __enter__(self):
+        self.prev = getattr(_opts_tls, "current", None)
+        _set_thread_options(self.options)
+        _opts_tls.current = self.options
+        return self
+
+    def __exit__(self, *a):
+        _set_thread_options(self.prev)
+        _opts_tls.current = self.prev
+
+
+def current_build_options():
+    """The options of the innermost build_options() scope of this thread (None outside)."""
+    return getattr(_opts_tls, "current", None)
 
 
 class cs_build_params(C.Structure):
@@ -74,6 +118,9 @@ SIGNATURES = {
                                         C.POINTER(_vp)]),
     "cs_fm_build_from_device_text": (C.c_int, [_vp, C.c_uint64, C.POINTER(cs_build_params), C.c_int,
                                                C.POINTER(_vp)]),
+    "cs_fm_build_with_options": (C.c_int, [_vp, C.c_uint64, C.c_int, C.POINTER(cs_build_params), C.c_char_p,
+                                           C.c_int, C.POINTER(_vp)]),
+    "cs_fm_set_build_options": (C.c_int, [C.c_char_p]),
     "cs_fm_open_directory": (C.c_int, [C.c_char_p, C.POINTER(_vp)]),
     "cs_fm_open_directory_on": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(_vp)]),
     "cs_fm_save_directory": (C.c_int, [_vp, C.c_char_p]),
@@ -232,22 +279,34 @@ class FMIndex:
 
     # -- construction (fm_index.hpp:19-20) --------------------------------
     @staticmethod
-    def build_from_text(text, params: BuildParams | None = None, device: int | None = None):
+    def build_from_text(text, params: BuildParams | None = None, device: int | None = None,
+                        options=None):
+        """options: build choices (cs_fmindex_tuning.h cs_fm_build_with_options) as a dict
+        {"ENGINE": "wavelet", "FULL_SA": 0} or a "NAME=VALUE ..." string; None takes the
+        thread's build_options() scope, and outside one the CS_FM_* environment."""
         p = (params or BuildParams())._c()
         if device is None:
             device = int(os.environ.get("CS_FM_DEVICE", "0"))
         t = np.frombuffer(_bytes(text) + b"\0", np.uint8)
         n = len(t) - 1
         h = _vp()
-        _check(lib().cs_fm_build_from_text(_u8(t), n, C.byref(p), device, C.byref(h)))
+        o = _options_arg(options)
+        if o is None:
+            _check(lib().cs_fm_build_from_text(_u8(t), n, C.byref(p), device, C.byref(h)))
+        else:
+            _check(lib().cs_fm_build_with_options(t.ctypes.data, n, 0, C.byref(p), o, device, C.byref(h)))
         return FMIndex(h, n)
 
     @staticmethod
     def build_from_device_text(d_text_ptr: int, n: int, params: BuildParams | None = None,
-                               device: int = 0):
+                               device: int = 0, options=None):
         p = (params or BuildParams())._c()
         h = _vp()
-        _check(lib().cs_fm_build_from_device_text(d_text_ptr, n, C.byref(p), device, C.byref(h)))
+        o = _options_arg(options)
+        if o is None:
+            _check(lib().cs_fm_build_from_device_text(d_text_ptr, n, C.byref(p), device, C.byref(h)))
+        else:
+            _check(lib().cs_fm_build_with_options(d_text_ptr, n, 1, C.byref(p), o, device, C.byref(h)))
         return FMIndex(h, n)
 
     @staticmethod

@@ -127,7 +127,7 @@ struct PhaseLog {
   bool on;
   hipStream_t st;
   std::chrono::steady_clock::time_point t0;
-  explicit PhaseLog(hipStream_t s) : on(std::getenv("CS_FM_VERBOSE") != nullptr), st(s),
+  explicit PhaseLog(hipStream_t s) : on(build_opt("CS_FM_VERBOSE") != nullptr), st(s),
                                      t0(std::chrono::steady_clock::now()) {}
   void mark(const char* what) {
     if (!on) return;
@@ -262,7 +262,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
 static uint32_t position_stride(uint32_t stride, bool wide) {
   (void)wide;
   uint32_t p = stride / 8u;
-  if (const char* e = std::getenv("CS_FM_PSTRIDE")) p = (uint32_t)std::atoi(e);
+  if (const char* e = build_opt("CS_FM_PSTRIDE")) p = (uint32_t)std::atoi(e);
   return p ? p : 1u;
 }
 
@@ -310,7 +310,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   // wide index: u64 samples / table entries and 64-B lines (n >= 2^32, or forced
   // by the CS_FM_WIDE test hook)
   h->wide = n >= (1ull << 32);
-  if (const char* e = std::getenv("CS_FM_WIDE"))
+  if (const char* e = build_opt("CS_FM_WIDE"))
     if (std::atoi(e) == 1) h->wide = true;
   h->nsamples = (n + stride - 1) / stride;
   NodeTable& T = h->h_table;
@@ -347,7 +347,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
   FMX_HIP(hipMalloc(&h->d_isa, (h->nisa ? h->nisa : 1) * h->sample_bytes()));
   DevBuf sa_pending;  // with an HBM budget: the full SA, kept at the end if it still fits
   bool bucketed = n >= (1ull << 32);
-  if (const char* e = std::getenv("CS_FM_SA_BUILDER"))
+  if (const char* e = build_opt("CS_FM_SA_BUILDER"))
     if (std::string(e) == "bucketed") bucketed = true;
   if (n && bucketed) {  // BWT + samples pass by pass, no full SA (fm_bwt_bucketed.hip)
     cs_status s = build_bwt_bucketed(d_text, n, stride, h->pstride, h->wide, bwt.as<uint8_t>(), h->d_ssa,
@@ -373,7 +373,7 @@ cs_status build_index_device(const uint8_t* d_text, uint64_t n, uint32_t stride,
     // walk computes, fm_index.cpp:125-153), one read instead of a walk.  4n bytes (C4:
     // 16 GB), an eighth of the device left free; CS_FM_FULL_SA=0 keeps only the samples.
     bool keep = h->lf_exact;
-    if (const char* e = std::getenv("CS_FM_FULL_SA")) keep = keep && std::atoi(e) != 0;
+    if (const char* e = build_opt("CS_FM_FULL_SA")) keep = keep && std::atoi(e) != 0;
     size_t free_b = 0, total_b = 0;
     if (keep && h->hbm_budget) {
       // an HBM budget: the full SA ranks after the count structures, so it is decided
@@ -402,7 +402,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   bool occ = occ_feasible(hist, n, occ_map, occ_sym);
   bool qwm = !occ && n > 0 && n < (1ull << 40);
   bool learned = false;  // learned occurrence lines instead of occurrence lines
-  if (const char* e = std::getenv("CS_FM_ENGINE")) {  // test hooks: force an engine
+  if (const char* e = build_opt("CS_FM_ENGINE")) {  // test hooks: force an engine
     const std::string want(e);
     if (want == "learned") learned = occ;
     if (want == "wavelet") occ = qwm = false;
@@ -419,7 +419,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
     cs_status qs = build_qwm(bwt.as<uint8_t>(), n, hist, h, st);
     if (qs != CS_OK) return qs;
     bool walk = true;
-    if (const char* e = std::getenv("CS_FM_WALK"))  // "0": walk over the matrix levels
+    if (const char* e = build_opt("CS_FM_WALK"))  // "0": walk over the matrix levels
       walk = std::atoi(e) != 0;
     if (walk) {  // walk lines carry level 0: each symbol's first base-4 digit
       CodeMap d0;
@@ -443,7 +443,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
                            : build_occ(bwt.as<uint8_t>(), n, occ_map, h, st);
     if (os != CS_OK) return os;
     bool walk = true;
-    if (const char* e = std::getenv("CS_FM_WALK"))  // "0": walk over the occurrence lines
+    if (const char* e = build_opt("CS_FM_WALK"))  // "0": walk over the occurrence lines
       walk = std::atoi(e) != 0;
     if (walk) {
       os = build_walk(bwt.as<uint8_t>(), n, occ_map, h, st);
@@ -452,7 +452,7 @@ static cs_status finish_index(DevBuf& bwt, const unsigned long long* hist, cs_fm
   } else {
     std::memset(T.occ_code, kNoCode, sizeof T.occ_code);
     h->line_fmt = h->wide ? kFmtLine32W : kFmtLine32;  // Line32 bases are u32
-    if (const char* e = std::getenv("CS_FM_LINE_BYTES"))  // test hook: force 64-B lines
+    if (const char* e = build_opt("CS_FM_LINE_BYTES"))  // test hook: force 64-B lines
       if (std::atoi(e) == 64) h->line_fmt = kFmtLine64;
     h->line_bytes = h->line_fmt == kFmtLine64 ? 64 : 32;
     h->line_bits = h->line_fmt == kFmtLine32 ? Line32::kBits

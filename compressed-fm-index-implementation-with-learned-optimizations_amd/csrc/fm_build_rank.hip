@@ -504,7 +504,7 @@ cs_status build_locc(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_i
                                     rocprim::plus<uint64_t>(), st));
   }
   uint32_t shift = 14;
-  if (const char* e = std::getenv("CS_FM_LEARNED_SHIFT")) shift = (uint32_t)std::atoi(e);
+  if (const char* e = build_opt("CS_FM_LEARNED_SHIFT")) shift = (uint32_t)std::atoi(e);
   for (;;) {
     const uint64_t nsb = ((nl - 1) >> shift) + 1;
     if (h->d_lmodel) (void)hipFree(h->d_lmodel);
@@ -757,12 +757,12 @@ cs_status build_walk(const uint8_t* bwt, uint64_t n, const CodeMap& map, cs_fm_i
                      hipStream_t st) {
   // with the full suffix array kept (lf_exact), locate reads SA[row] and never walks:
   // no walk lines (C4: 3 GB + 4 GB of position samples saved)
-  if (h->d_sa && h->lf_exact && !std::getenv("CS_FM_WALK_MARKS")) {
+  if (h->d_sa && h->lf_exact && !build_opt("CS_FM_WALK_MARKS")) {
     h->walk_marks = 0;
     return CS_OK;
   }
   bool pos_marks = h->lf_exact && h->d_isa && h->nisa == (n + h->pstride - 1) / h->pstride;
-  if (const char* e = std::getenv("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
+  if (const char* e = build_opt("CS_FM_WALK_MARKS"))  // test hook: "row" forces row marks
     if (std::string(e) == "row") pos_marks = false;
   const uint64_t rows = h->wide ? WalkLineW::kRows : WalkLine::kRows;
   if (!hbm_room(h, (n / rows + 1) * 32 + (pos_marks ? h->nisa * (h->wide ? 5u : 4u) : 0))) {

@@ -234,7 +234,7 @@ cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride,
                              bool wide,
                              uint8_t* d_bwt, void* d_ssa, void* d_isa, hipStream_t st) {
   if (n == 0) return CS_OK;
-  const bool verbose = std::getenv("CS_FM_VERBOSE") != nullptr;
+  const bool verbose = build_opt("CS_FM_VERBOSE") != nullptr;
   // ---- codes ----
   DevBuf d_h;
   FMX_HIP(d_h.alloc(256 * 8));
@@ -271,7 +271,7 @@ cs_status build_bwt_bucketed(const uint8_t* d_text, uint64_t n, uint32_t stride,
   FMX_HIP(hipMemGetInfo(&free_b, &total_b));
   uint64_t pmax = free_b / 64;  // ~40 B per element in flight + sort scratch
   if (pmax > (1ull << 31)) pmax = 1ull << 31;
-  if (const char* e = std::getenv("CS_FM_PASS_MAX")) pmax = std::strtoull(e, nullptr, 10);
+  if (const char* e = build_opt("CS_FM_PASS_MAX")) pmax = std::strtoull(e, nullptr, 10);
   struct Pass { uint32_t lo, hi; uint64_t count, row0; };
   std::vector<Pass> passes;
   {

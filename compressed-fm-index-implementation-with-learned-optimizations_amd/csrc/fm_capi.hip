@@ -11,6 +11,8 @@
 #include <new>
 #include <string>
 
+#include <cctype>
+
 #include "fm_internal.hpp"
 
 namespace fmx {
@@ -336,23 +338,91 @@ void read_tuning(cs_fm_index* h) {
   };
   h->tune = 0;
   for (const Bit& b : bits)
-    if (const char* e = std::getenv(b.var))
+    if (const char* e = build_opt(b.var))
       if (std::strcmp(e, b.val) == 0) h->tune |= b.bit;
   h->gen_list_min = 2;
-  if (const char* e = std::getenv("CS_FM_GENERAL_LIST_MIN")) {
+  if (const char* e = build_opt("CS_FM_GENERAL_LIST_MIN")) {
     const long v = std::atol(e);
     if (v >= 1 && v <= 128) h->gen_list_min = (uint32_t)v;
   }
   h->list_grid = 0;
-  if (const char* e = std::getenv("CS_FM_LIST_GRID")) {
+  if (const char* e = build_opt("CS_FM_LIST_GRID")) {
     const long v = std::atol(e);
     if (v >= 1 && v <= (1 << 20)) h->list_grid = (uint32_t)v;
   }
   h->host_chunk = 0;
-  if (const char* e = std::getenv("CS_FM_HOST_CHUNK")) {
+  if (const char* e = build_opt("CS_FM_HOST_CHUNK")) {
     const long long v = std::atoll(e);
     if (v > 0) h->host_chunk = (uint64_t)v;
   }
+}
+
+namespace {
+
+thread_local const BuildOptions* t_build_opts = nullptr;
+thread_local BuildOptions t_thread_opts;  // cs_fm_set_build_options
+
+// every CS_FM_* variable build_opt() is asked for (the build, the structures, the handle's
+// tuning defaults); CS_FM_DEVICE (which device a facade or open_directory uses) is not a build
+// option
+const char* const kBuildOptNames[] = {
+    "CS_FM_VERBOSE",       "CS_FM_PSTRIDE",      "CS_FM_WIDE",          "CS_FM_SA_BUILDER",
+    "CS_FM_FULL_SA",       "CS_FM_ENGINE",       "CS_FM_WALK",          "CS_FM_LINE_BYTES",
+    "CS_FM_LEARNED_SHIFT", "CS_FM_WALK_MARKS",   "CS_FM_PASS_MAX",      "CS_FM_HBM_BUDGET",
+    "CS_FM_PREFIX_K",      "CS_FM_PTAB_WMAX",    "CS_FM_LCTX",          "CS_FM_CTX_RECORDS",
+    "CS_FM_DEVICE_TEXT",   "CS_FM_PACKED_TEXT",  "CS_FM_LOC_RECORDS",   "CS_FM_LOC_REC64",
+    "CS_FM_COUNT_NOBAR",   "CS_FM_LONG_ROUTE",   "CS_FM_COUNT_U",       "CS_FM_LONG_V16",
+    "CS_FM_LONG_KERNEL",   "CS_FM_QCTX_STAGED",  "CS_FM_LOCATE_ONEPASS", "CS_FM_LOC_DEFER",
+    "CS_FM_LOCATE_U",      "CS_FM_WALK_ROWS",    "CS_FM_WALK_PERSISTENT", "CS_FM_GENERAL_INLANE",
+    "CS_FM_GENERAL_LIST_ALL", "CS_FM_MAP_LDS",   "CS_FM_GENERAL_LIST_MIN", "CS_FM_LIST_GRID",
+    "CS_FM_HOST_CHUNK",
+};
+
+}  // namespace
+
+const char* build_opt(const char* name) {
+  const BuildOptions* o = t_build_opts;
+  if (!o) return std::getenv(name);
+  for (const auto& kv : o->kv)
+    if (kv.first == name) return kv.second.c_str();
+  return nullptr;
+}
+
+BuildOptScope::BuildOptScope(const BuildOptions* o) : prev_(t_build_opts) { t_build_opts = o; }
+BuildOptScope::~BuildOptScope() { t_build_opts = prev_; }
+
+bool parse_build_options(const char* text, BuildOptions& o, std::string& err) {
+  o.kv.clear();
+  const std::string s = text ? text : "";
+  size_t i = 0;
+  while (i < s.size()) {
+    while (i < s.size() && (s[i] == ' ' || s[i] == ',' || s[i] == ';' || s[i] == '\t' || s[i] == '\n')) ++i;
+    if (i >= s.size()) break;
+    size_t j = i;
+    while (j < s.size() && s[j] != ' ' && s[j] != ',' && s[j] != ';' && s[j] != '\t' && s[j] != '\n') ++j;
+    const std::string tok = s.substr(i, j - i);
+    i = j;
+    const size_t eq = tok.find('=');
+    if (eq == std::string::npos || eq == 0) {
+      err = "build option without NAME=VALUE: " + tok;
+      return false;
+    }
+    std::string name = tok.substr(0, eq);
+    for (char& c : name) c = (char)std::toupper((unsigned char)c);
+    if (name.rfind("CS_FM_", 0) != 0) name = "CS_FM_" + name;
+    bool known = false;
+    for (const char* k : kBuildOptNames) known = known || name == k;
+    if (!known) {
+      err = "unknown build option: " + tok.substr(0, eq);
+      return false;
+    }
+    std::string val = tok.substr(eq + 1);
+    bool replaced = false;
+    for (auto& kv : o.kv)
+      if (kv.first == name) kv.second = val, replaced = true;
+    if (!replaced) o.kv.emplace_back(std::move(name), std::move(val));
+  }
+  return true;
 }
 
 namespace {
@@ -575,6 +645,38 @@ cs_status cs_fm_build_from_device_text(const uint8_t* d_text, uint64_t n,
     return CS_ERR_INVALID;
   }
   return build_common(d_text, n, p, device, out, nullptr);
+}
+
+cs_status cs_fm_set_build_options(const char* options) {
+  if (!options) {
+    t_build_opts = nullptr;
+    return CS_OK;
+  }
+  BuildOptions o;
+  std::string err;
+  if (!parse_build_options(options, o, err)) {
+    set_error(err);
+    return CS_ERR_INVALID;
+  }
+  t_thread_opts = std::move(o);
+  t_build_opts = &t_thread_opts;
+  return CS_OK;
+}
+
+cs_status cs_fm_build_with_options(const uint8_t* text, uint64_t n, int text_on_device,
+                                   const cs_build_params* p, const char* options, int device,
+                                   cs_fm_index** out) {
+  if (!options) return text_on_device ? cs_fm_build_from_device_text(text, n, p, device, out)
+                                      : cs_fm_build_from_text(text, n, p, device, out);
+  BuildOptions o;
+  std::string err;
+  if (!parse_build_options(options, o, err)) {
+    set_error(err);
+    return CS_ERR_INVALID;
+  }
+  BuildOptScope scope(&o);
+  return text_on_device ? cs_fm_build_from_device_text(text, n, p, device, out)
+                        : cs_fm_build_from_text(text, n, p, device, out);
 }
 
 cs_status cs_fm_create(const uint8_t* bwt, uint64_t n, const uint32_t* ssa, uint64_t nsamples,

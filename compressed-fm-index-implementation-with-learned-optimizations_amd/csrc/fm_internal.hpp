@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <string>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "../../include/cs_fmindex.h"
@@ -238,6 +239,29 @@ uint64_t locate_workspace_bytes(const cs_fm_index* h, uint64_t npat);
 // the tuning defaults of a new handle from the CS_FM_* environment (cs_fm_index::tune,
 // host_chunk; fm_capi.hip): read once when a handle is created, never by a query
 void read_tuning(cs_fm_index* h);
+
+// Build options (cs_fmindex_tuning.h cs_fm_build_with_options, round 6): the CS_FM_* build and
+// tuning variables as NAME=VALUE pairs.  Every builder reads its variables through build_opt():
+// inside a build started with an options string that is the string's value (or none), otherwise
+// the environment — the shim cs_fm_build_from_text and the older callers rely on.  The scope is
+// per thread; a build runs in its caller's thread.
+struct BuildOptions {
+  std::vector<std::pair<std::string, std::string>> kv;
+};
+const char* build_opt(const char* name);
+class BuildOptScope {
+ public:
+  explicit BuildOptScope(const BuildOptions* o);
+  ~BuildOptScope();
+  BuildOptScope(const BuildOptScope&) = delete;
+  BuildOptScope& operator=(const BuildOptScope&) = delete;
+
+ private:
+  const BuildOptions* prev_;
+};
+// "ENGINE=wavelet, FULL_SA=0" -> o (names with or without CS_FM_, upper-cased); false and the
+// offending token in err for a malformed pair or a name no builder reads
+bool parse_build_options(const char* text, BuildOptions& o, std::string& err);
 
 // Query launches (fm_query.hip).
 // d_offs == nullptr: npat patterns of length fixed_m at stride fixed_m; flags CS_Q_*

@@ -264,7 +264,7 @@ bool hbm_room(const cs_fm_index* h, uint64_t bytes, uint64_t freed, uint64_t tra
 }
 
 uint64_t hbm_budget_env() {
-  const char* e = std::getenv("CS_FM_HBM_BUDGET");
+  const char* e = build_opt("CS_FM_HBM_BUDGET");
   if (!e || !*e) return 0;
   char* end = nullptr;
   const double v = std::strtod(e, &end);

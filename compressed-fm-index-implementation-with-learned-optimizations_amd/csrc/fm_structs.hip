@@ -111,7 +111,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
     entries *= sigma;
     ++k;
   }
-  if (const char* e = std::getenv("CS_FM_PREFIX_K")) {
+  if (const char* e = build_opt("CS_FM_PREFIX_K")) {
     const int want = std::atoi(e);
     k = 0;
     entries = 1;
@@ -131,7 +131,7 @@ cs_status build_prefix_table(cs_fm_index* h, hipStream_t st) {
   DevIndex ix = h->dev();
   ix.ptab = nullptr;  // the builder itself searches from C[]
   uint64_t wmax = kPtabEsc;
-  if (const char* e = std::getenv("CS_FM_PTAB_WMAX")) wmax = std::strtoull(e, nullptr, 10);
+  if (const char* e = build_opt("CS_FM_PTAB_WMAX")) wmax = std::strtoull(e, nullptr, 10);
   FMX_DISPATCH(h, k_build_ptab, grid_for(entries, kBlk, 65536), ix, entries, h->d_ptab, wmax);
   FMX_HIP(hipStreamSynchronize(st));
   return CS_OK;
@@ -148,7 +148,7 @@ cs_status build_left_contexts(cs_fm_index* h, hipStream_t st) {
   h->lctx_q = h->lctx_sb = h->lctx_eb = 0;
   const bool occ = h->line_fmt == kFmtOcc || h->line_fmt == kFmtLOcc, qwm = h->line_fmt == kFmtQwm;
   if (!(occ || qwm) || h->n == 0) return CS_OK;
-  if (const char* e = std::getenv("CS_FM_LCTX"))
+  if (const char* e = build_opt("CS_FM_LCTX"))
     if (std::atoi(e) == 0) return CS_OK;
   const uint32_t eb = occ ? 2 : 4, R = 32 / eb;
   const uint32_t sb = occ ? 2 : 2 * h->h_table.qlevels;
@@ -318,7 +318,7 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
   if (h->wide && h->lctx_eb != 2) return CS_OK;  // wide records: occurrence lines only
   const uint64_t entries = h->ptab_entries();
   if (h->lctx_eb == 4) {  // quaternary matrix: 16-B records when ranges average <= 2 rows
-    if (const char* e = std::getenv("CS_FM_CTX_RECORDS"))
+    if (const char* e = build_opt("CS_FM_CTX_RECORDS"))
       if (std::atoi(e) == 0) return CS_OK;
     if (h->n > kRecQCtx * entries) return CS_OK;
     // the records replace the 8-B table
@@ -348,7 +348,7 @@ cs_status build_context_records(cs_fm_index* h, hipStream_t st) {
     want = h->ptab_k >= 15 && h->n <= 8 * entries;
     fmt = 2;
   }
-  if (const char* e = std::getenv("CS_FM_CTX_RECORDS")) {
+  if (const char* e = build_opt("CS_FM_CTX_RECORDS")) {
     want = std::atoi(e) != 0;
     fmt = h->wide || std::atoi(e) == 16 ? 2 : 1;
   }
@@ -390,7 +390,7 @@ cs_status keep_device_text(cs_fm_index* h, const uint8_t* src, bool src_on_devic
   // (round 6: without the byte text, a walk_verify() index still takes the 2-bit text of the
   // build's device text — C5: 8 GB where the 32-GB text does not fit the eighth)
   const uint8_t* dsrc = src_on_device ? src : nullptr;
-  if (const char* e = std::getenv("CS_FM_DEVICE_TEXT"))
+  if (const char* e = build_opt("CS_FM_DEVICE_TEXT"))
     if (std::atoi(e) == 0) return derive_packed_text(h, st, dsrc);
   if (!hbm_room(h, h->n)) return derive_packed_text(h, st, dsrc);
   FMX_HIP(hipMalloc(&h->d_dtext, h->n + kPartPad));
@@ -470,7 +470,7 @@ cs_status derive_packed_text(cs_fm_index* h, hipStream_t st, const uint8_t* src)
   const uint8_t* text = h->d_dtext ? static_cast<const uint8_t*>(h->d_dtext) : src;
   if (!text || !(narrow_sa || walk)) return CS_OK;
   if (narrow_sa && !h->d_dtext) return CS_OK;  // (its verification reads the byte text too)
-  if (const char* e = std::getenv("CS_FM_PACKED_TEXT"))
+  if (const char* e = build_opt("CS_FM_PACKED_TEXT"))
     if (std::atoi(e) == 0) return CS_OK;
   const uint64_t nw = (h->n + 31) / 32;
   if (!hbm_room(h, nw * 8, 0, h->d_dtext ? 0 : h->n)) return CS_OK;
@@ -652,7 +652,7 @@ cs_status derive_locate_records(cs_fm_index* h, hipStream_t st) {
       !h->d_lctx || h->lctx_eb != 2 || h->line_fmt != kFmtOcc || h->ptab_sigma != 4 ||
       h->ptab_k < 1 || h->ptab_k + 1 > 16 || h->n >= (1ull << 32))
     return CS_OK;
-  if (const char* e = std::getenv("CS_FM_LOC_RECORDS"))
+  if (const char* e = build_opt("CS_FM_LOC_RECORDS"))
     if (std::atoi(e) == 0) return CS_OK;
   // the table digit of each occurrence code; every code must have one
   uint32_t o2d = 0xFFFFFFFFu;
@@ -667,7 +667,7 @@ cs_status derive_locate_records(cs_fm_index* h, hipStream_t st) {
   // CS_FM_LOC_REC64=0 (read at build / open / import): the 16-B (k+1)-mer records of early
   // round 4 instead of the 64-B k-mer ones
   bool w64 = true;
-  if (const char* e = std::getenv("CS_FM_LOC_REC64"))
+  if (const char* e = build_opt("CS_FM_LOC_REC64"))
     w64 = std::atoi(e) != 0;
   void* p = nullptr;
   FMX_HIP(hipMalloc(&p, bytes));

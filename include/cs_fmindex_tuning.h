@@ -58,4 +58,35 @@
 #define CS_QT_GENERAL_LIST_ALL (1u << 23)
 #define CS_QT_MAP_LDS (1u << 24)
 
+#include "cs_fmindex.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Build options (round 6): the engine, footprint and tuning-default choices of a build as
+ * "NAME=VALUE" pairs separated by spaces, commas or semicolons.  NAME is one of the CS_FM_*
+ * variables cs_fm_build_from_text reads from the environment, with or without the CS_FM_
+ * prefix, in any case: ENGINE=wavelet|occ|qwm|learned, HBM_BUDGET=40G, FULL_SA=0, WALK=0,
+ * WALK_MARKS=row, PREFIX_K=12, LCTX=0, CTX_RECORDS=0|1|16, LOC_RECORDS=0, LOC_REC64=1,
+ * DEVICE_TEXT=0, PACKED_TEXT=0, WIDE=1, PSTRIDE=8, LINE_BYTES=64, SA_BUILDER=bucketed,
+ * PASS_MAX=<bytes>, the handle defaults of the selectors above (LONG_ROUTE=0, COUNT_U=4 ...),
+ * GENERAL_LIST_MIN, LIST_GRID, HOST_CHUNK.  With an options string (empty included) the build
+ * reads no environment variable: a name not given takes its default.  options == NULL is
+ * cs_fm_build_from_text / cs_fm_build_from_device_text (text_on_device != 0), which read the
+ * environment.  A malformed pair or an unknown name fails with CS_ERR_INVALID
+ * (cs_fm_last_error names it).  Results never depend on the options, only footprint and
+ * throughput do. */
+cs_status cs_fm_build_with_options(const uint8_t* text, uint64_t n, int text_on_device,
+                                   const cs_build_params* p, const char* options, int device,
+                                   cs_fm_index** out);
+/* The calling thread's build options for every handle it constructs from now on — build,
+ * create, open_directory, import — in the same "NAME=VALUE" form; NULL returns the thread to
+ * the environment.  cs_fm_build_with_options's own options take precedence for that call. */
+cs_status cs_fm_set_build_options(const char* options);
+
+#ifdef __cplusplus
+}
+#endif
+
 #endif /* CS_FMINDEX_TUNING_H */

@@ -82,3 +82,22 @@ def fm_golden_cases(*files):
         for c in load_golden(f)["cases"]:
             out.append(pytest.param(c, id="%s:%s" % (f.split(".")[0], c["name"])))
     return out
+
+
+@pytest.fixture
+def build_opts():
+    """build_opts(CS_FM_ENGINE="wavelet", ...): build options (cs_fmindex_tuning.h,
+    cs_fm_set_build_options) for every handle this test constructs from then on, merged over
+    the current ones; the previous options are back when the test ends.  No test chooses an
+    engine through the environment (round 6)."""
+    m = load_pkg()
+    scopes = []
+
+    def set_(**kw):
+        s = m.build_options(dict(m.current_build_options() or {}, **kw))
+        s.__enter__()
+        scopes.append(s)
+
+    yield set_
+    for s in reversed(scopes):
+        s.__exit__(None, None, None)

@@ -128,3 +128,28 @@ def test_dropin_header_is_small():
     assert len(decls) <= 30, decls
     for gone in ("_ex", "_ws", "_async"):
         assert not [d for d in decls if d.endswith(gone)], decls
+
+
+def test_build_options_parse():
+    """Build options (cs_fmindex_tuning.h, round 6): NAME=VALUE pairs with or without the CS_FM_
+    prefix, any case, separated by spaces / commas / semicolons; an unknown name or a pair
+    without '=' is CS_ERR_INVALID naming it, before any device is touched; NULL returns the
+    thread to the environment."""
+    import ctypes as C
+    import numpy as np
+    pkg = load_pkg()
+    L = pkg.lib()
+    assert L.cs_fm_set_build_options(b"ENGINE=wavelet, full_sa=0;CS_FM_PREFIX_K=12 HBM_BUDGET=40G") == pkg.CS_OK
+    assert L.cs_fm_set_build_options(b"") == pkg.CS_OK
+    assert L.cs_fm_set_build_options(b"NO_SUCH_KNOB=1") == pkg.CS_ERR_INVALID
+    assert b"NO_SUCH_KNOB" in L.cs_fm_last_error()
+    assert L.cs_fm_set_build_options(b"ENGINE") == pkg.CS_ERR_INVALID
+    assert L.cs_fm_set_build_options(b"CS_FM_DEVICE=1") == pkg.CS_ERR_INVALID  # not a build option
+    assert L.cs_fm_set_build_options(None) == pkg.CS_OK
+    t = np.frombuffer(b"ACGT$", np.uint8)
+    h = C.c_void_p()
+    p = pkg.cs_build_params()
+    L.cs_default_build_params(C.byref(p))
+    assert L.cs_fm_build_with_options(t.ctypes.data, 4, 0, C.byref(p), b"LCTX=0 BOGUS=2", 0,
+                                      C.byref(h)) == pkg.CS_ERR_INVALID
+    assert b"BOGUS" in L.cs_fm_last_error() and not h.value

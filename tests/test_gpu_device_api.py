@@ -194,14 +194,14 @@ def test_long_routing_concurrent_streams():
 
 
 @pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "learned", "records", "records16"])
-def test_export_import_image(engine, monkeypatch):
+def test_export_import_image(engine, build_opts):
     """The device image (cs_fm_export_meta/_parts -> cs_fm_import): the copy answers
     count / locate / extract exactly as the original (context records and the full
     suffix array included)."""
     if engine in ("records", "records16"):
-        monkeypatch.setenv("CS_FM_CTX_RECORDS", "1" if engine == "records" else "16")
+        build_opts(CS_FM_CTX_RECORDS="1" if engine == "records" else "16")
     elif engine != "auto":
-        monkeypatch.setenv("CS_FM_ENGINE", engine)
+        build_opts(CS_FM_ENGINE=engine)
     pkg = load_pkg()
     t = O.gen_dna(9, 50_000).tobytes()
     g = pkg.FMIndex.build_from_text(t)
@@ -252,7 +252,7 @@ def test_host_batch_buffers_sharing_pages():
 
 
 @pytest.mark.parametrize("chunk", [333_333, 1 << 20, 0])
-def test_host_batch_chunked(chunk, monkeypatch):
+def test_host_batch_chunked(chunk, build_opts):
     """cs_fm_count_batch over a large ragged host batch in chunks (CS_FM_HOST_CHUNK when the
     handle is created; 0 = the
     default 2 M patterns): the caller's pages page-locked piece by piece while earlier chunks
@@ -261,9 +261,9 @@ def test_host_batch_chunked(chunk, monkeypatch):
     pkg = load_pkg()
     t = O.gen_dna(6, 300_000).tobytes()
     if chunk:  # (read when the handle is created)
-        monkeypatch.setenv("CS_FM_HOST_CHUNK", str(chunk))
+        build_opts(CS_FM_HOST_CHUNK=str(chunk))
     g = pkg.FMIndex.build_from_text(t)
-    monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
+    build_opts(CS_FM_HOST_CHUNK=str(10 ** 9))
     g1 = pkg.FMIndex.build_from_text(t)  # one chunk
     rng = np.random.default_rng(3)
     npat = 2_500_000
@@ -286,7 +286,7 @@ def test_host_batch_chunked(chunk, monkeypatch):
     assert (out[lens == 0] == len(t)).all() and (out >= 1).mean() > 0.5
 
 
-def test_host_batch_long_chunks(monkeypatch):
+def test_host_batch_long_chunks(build_opts):
     """Host batches of long patterns take the long-pattern count kernel (CS_Q_LONG) chunk
     by chunk when every pattern of the chunk is longer than 96 characters; the chunk that
     holds a short pattern stays on the staged kernel — the oracle's counts either way."""
@@ -305,25 +305,25 @@ def test_host_batch_long_chunks(monkeypatch):
         pats.append(bytes(p))
     pats[2500] = pats[2500][:20]
     want = [ref.count(p) for p in pats]
-    monkeypatch.setenv("CS_FM_HOST_CHUNK", "1000")  # (read when the handle is created)
+    build_opts(CS_FM_HOST_CHUNK="1000")  # (read when the handle is created)
     g = pkg.FMIndex.build_from_text(t)
     assert g.count_batch(pats).tolist() == want
-    monkeypatch.setenv("CS_FM_HOST_CHUNK", str(10 ** 9))
+    build_opts(CS_FM_HOST_CHUNK=str(10 ** 9))
     g = pkg.FMIndex.build_from_text(t)
     assert g.count_batch(pats[:2000]).tolist() == want[:2000]
     assert g.count_batch(pats).tolist() == want
 
 
 @pytest.mark.parametrize("engine", ["auto", "qwm", "wavelet", "records16"])
-def test_import_alloc_commit(engine, monkeypatch):
+def test_import_alloc_commit(engine, build_opts):
     """Replication without staging copies: the index's own part addresses
     (cs_fm_export_part_ptrs) copied into the parts of a handle allocated for them
     (cs_fm_import_alloc, then cs_fm_import_commit), through torch tensors over the raw
     device memory (shard.device_bytes) — the copy answers as the original."""
     if engine in ("records", "records16"):
-        monkeypatch.setenv("CS_FM_CTX_RECORDS", "1" if engine == "records" else "16")
+        build_opts(CS_FM_CTX_RECORDS="1" if engine == "records" else "16")
     elif engine != "auto":
-        monkeypatch.setenv("CS_FM_ENGINE", engine)
+        build_opts(CS_FM_ENGINE=engine)
     pkg = load_pkg()
     import importlib
     shard = importlib.import_module("cs_fmindex_amd.shard")
@@ -386,7 +386,7 @@ def test_counts_wire(npat, cap):
 
 
 @pytest.mark.parametrize("chunk", [0, 300_000])
-def test_concurrent_host_batches_share_pages(chunk, monkeypatch):
+def test_concurrent_host_batches_share_pages(chunk, build_opts):
     """Two host threads count batches over the same large buffer at once — one the whole
     buffer, one a window starting inside it (overlapping registrations) — on distinct
     streams, in one piece or in chunks whose pages are registered piece by piece
@@ -394,7 +394,7 @@ def test_concurrent_host_batches_share_pages(chunk, monkeypatch):
     single-thread answer, repeatedly."""
     import threading
     if chunk:
-        monkeypatch.setenv("CS_FM_HOST_CHUNK", str(chunk))
+        build_opts(CS_FM_HOST_CHUNK=str(chunk))
     pkg = load_pkg()
     t = O.gen_dna(23, 200_000).tobytes()
     g = pkg.FMIndex.build_from_text(t)
@@ -425,7 +425,7 @@ def test_concurrent_host_batches_share_pages(chunk, monkeypatch):
 
 
 @pytest.mark.parametrize("kind", ["dna", "bytes"])
-def test_hbm_budget(kind, monkeypatch):
+def test_hbm_budget(kind, build_opts):
     """CS_FM_HBM_BUDGET: the optional structures are added in build order while the index
     fits; every budget answers count / locate / extract exactly as the default build, the
     footprint never exceeds max(budget, the base structures), and an ample budget builds
@@ -445,7 +445,7 @@ def test_hbm_budget(kind, monkeypatch):
     del ref
     sizes = []
     for budget in (1, full // 4, full // 2, (3 * full) // 4, full, 10 * full):
-        monkeypatch.setenv("CS_FM_HBM_BUDGET", str(budget))
+        build_opts(CS_FM_HBM_BUDGET=str(budget))
         g = pkg.FMIndex.build_from_text(t)
         nb = int(sum(g.export_meta()[1]))
         sizes.append(nb)

@@ -36,12 +36,8 @@ ENGINE_VARIANTS = {
     # staged count and locate kernels
     "auto_rec16": {"CS_FM_CTX_RECORDS": "16", "CS_FM_COUNT_U": "1", "CS_FM_LOCATE_U": "1"},
     "auto_nosa": {"CS_FM_FULL_SA": "0"},            # locate walks (no full suffix array kept)
-    # the same short walks from an expanded rows buffer instead of straight from the records
-    "auto_nosa_rows": {"CS_FM_FULL_SA": "0", "CS_FM_WALK_ROWS": "1"},
-    # the staged count / locate kernels' general search behind a block barrier (an LDS
-    # copy of the node table; the default reads it through the caches since round 4)
-    "auto_bar": {"CS_FM_COUNT_NOBAR": "0"},
-    "auto_pstride_ssa": {"CS_FM_PSTRIDE": "32"},    # position samples at the SSA's stride
+    # (round 6: auto_nosa_rows, auto_bar and auto_pstride_ssa — CS_QT_WALK_ROWS, CS_QT_BARRIER
+    # and PSTRIDE=32, no default path — are in test_selectors_without_a_variant)
     "qwm": {"CS_FM_ENGINE": "qwm"},                 # quaternary wavelet matrix for every text
     "qwm_unstaged": {"CS_FM_ENGINE": "qwm", "CS_FM_QCTX_STAGED": "0"},  # its count one pattern per lane
     "learned": {"CS_FM_ENGINE": "learned"},         # learned occurrence lines where occurrence lines apply
@@ -60,62 +56,55 @@ ENGINE_VARIANTS = {
     "wide_rec16": {"CS_FM_WIDE": "1", "CS_FM_CTX_RECORDS": "16"},
     "wide_rec16_esc": {"CS_FM_WIDE": "1", "CS_FM_CTX_RECORDS": "16", "CS_FM_PTAB_WMAX": "3"},
 }
-_HOOKS = ("CS_FM_LINE_BYTES", "CS_FM_PREFIX_K", "CS_FM_WIDE", "CS_FM_SA_BUILDER", "CS_FM_PASS_MAX",
-          "CS_FM_ENGINE", "CS_FM_WALK", "CS_FM_WALK_MARKS", "CS_FM_LCTX",
-          "CS_FM_PSTRIDE", "CS_FM_LEARNED_SHIFT", "CS_FM_PTAB_WMAX",
-          "CS_FM_CTX_RECORDS", "CS_FM_FULL_SA", "CS_FM_DEVICE_TEXT", "CS_FM_COUNT_U", "CS_FM_LOCATE_U",
-          "CS_FM_WALK_ROWS", "CS_FM_COUNT_NOBAR", "CS_FM_QCTX_STAGED")
-
 
 @pytest.fixture(scope="module", params=sorted(ENGINE_VARIANTS))
 def pkg(request):
-    """Every test runs on each engine variant (see ENGINE_VARIANTS)."""
-    saved = {k: os.environ.get(k) for k in _HOOKS}
-    for k in _HOOKS:
-        os.environ.pop(k, None)
-    os.environ.update(ENGINE_VARIANTS[request.param])
-    yield load_pkg()
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+    """Every test runs on each engine variant (see ENGINE_VARIANTS): the variant's build
+    options for every handle the module constructs (cs_fm_set_build_options, round 6 — no
+    test reads or writes the environment to choose an engine)."""
+    m = load_pkg()
+    with m.build_options(ENGINE_VARIANTS[request.param]):
+        yield m
 
 
 def _bar_count(g, buf, offs):
     """The staged count kernel's general search behind the block barrier (CS_QT_BARRIER, a
     per-call tuning selector; the default reads the node table through the caches, no
-    barrier, since round 4).  The auto_bar variant covers it on occurrence lines; the learned
-    variants re-count under it (the learned lines' instantiation)."""
+    barrier, since round 4).  The learned variants re-count under it (the learned lines'
+    instantiation); test_selectors_without_a_variant covers the rest."""
     return _count_bo(g, buf, offs, flags=load_pkg().QT_BARRIER)
 
 
+def _opt(name, default=None):
+    """The current build options' value of a CS_FM_* name (ENGINE_VARIANTS, _env)."""
+    cur = load_pkg().current_build_options() or {}
+    v = cur.get(name)
+    return default if v is None else str(v)
+
+
 class _env:
-    """Build-time engine switches (CS_FM_*, read when a handle is created) for the builds
-    inside.  Since round 5 no query reads the environment: per-call kernel choices are the
-    CS_QT_* flags bits (pkg.QT_*)."""
+    """Build options (cs_fmindex_tuning.h, the CS_FM_* names) for the handles constructed
+    inside, over the variant's: a thread scope (cs_fm_set_build_options), not the process
+    environment.  Per-call kernel choices are the CS_QT_* flags bits (pkg.QT_*)."""
 
     def __init__(self, **kw):
         self.kw = kw
 
     def __enter__(self):
-        self.saved = {k: os.environ.get(k) for k in self.kw}
-        os.environ.update(self.kw)
+        m = load_pkg()
+        self.scope = m.build_options(dict(m.current_build_options() or {}, **self.kw))
+        self.scope.__enter__()
 
     def __exit__(self, *a):
-        for k, v in self.saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        self.scope.__exit__(*a)
 
 
 def _learned():
-    return os.environ.get("CS_FM_ENGINE") == "learned"
+    return _opt("CS_FM_ENGINE") == "learned"
 
 
 def _wide():
-    return os.environ.get("CS_FM_WIDE") == "1"
+    return _opt("CS_FM_WIDE") == "1"
 
 
 def _texts():
@@ -221,7 +210,7 @@ def test_engine_choice(built):
     """Occurrence lines iff <= 4 symbols hold all but at most 128 BWT rows, else the
     quaternary matrix (unless an engine is forced); rare rows are listed in the node
     table; both get walk lines for locate."""
-    forced = os.environ.get("CS_FM_ENGINE")
+    forced = _opt("CS_FM_ENGINE")
     # (engine, rare rows, LF one cycle: the text ends in a unique smallest symbol, so the
     # walk lines mark sampled text positions (2) instead of the reference's rows (1))
     want = {"dna_5k": (1, 1, True), "banana": (1, 0, True), "single": (1, 0, True),
@@ -239,11 +228,11 @@ def test_engine_choice(built):
         elif forced == "learned" and engine == 1:
             engine = 3
         marks = 0 if engine == 0 else (2 if cyc else 1)
-        full_sa = (cyc and os.environ.get("CS_FM_FULL_SA") != "0"
-                   and os.environ.get("CS_FM_SA_BUILDER") != "bucketed")
-        if os.environ.get("CS_FM_WALK") == "0":
+        full_sa = (cyc and _opt("CS_FM_FULL_SA") != "0"
+                   and _opt("CS_FM_SA_BUILDER") != "bucketed")
+        if _opt("CS_FM_WALK") == "0":
             marks = 0
-        elif os.environ.get("CS_FM_WALK_MARKS") == "row" and marks:
+        elif _opt("CS_FM_WALK_MARKS") == "row" and marks:
             marks = 1
         elif full_sa:  # locate reads the full suffix array: no walk lines
             marks = 0
@@ -253,27 +242,27 @@ def test_engine_choice(built):
         # left contexts: occurrence lines 7 x 2-bit codes in u16 (16 rows per 32-B
         # sector), quaternary matrix 32 / (2 x levels) dense codes in u32 (8 rows)
         ctx, R = {1: (7, 16), 3: (7, 16), 2: (min(16, 32 // (2 * info.levels)), 8)}.get(engine, (0, 1))
-        if os.environ.get("CS_FM_LCTX") == "0":
+        if _opt("CS_FM_LCTX") == "0":
             ctx = 0
         assert info.context_q == ctx, name
-        wide = os.environ.get("CS_FM_WIDE") == "1"
+        wide = _opt("CS_FM_WIDE") == "1"
         assert info.full_sa_bytes == (4 * info.n if full_sa else 0), name
-        assert info.position_stride == (int(os.environ.get("CS_FM_PSTRIDE", "0")) or 4), name
+        assert info.position_stride == (int(_opt("CS_FM_PSTRIDE", "0")) or 4), name
         assert info.context_bytes == (((info.n + R - 1) // R + 1) * 32 if ctx else 0), name
         # context records: narrow occurrence-line indexes with contexts and a table of
         # 14+ characters (none of these texts) or forced; 16 B when forced compact
-        rec = {"1": 32, "16": 16}.get(os.environ.get("CS_FM_CTX_RECORDS", ""), 0)
+        rec = {"1": 32, "16": 16}.get(_opt("CS_FM_CTX_RECORDS", ""), 0)
         if wide and rec:  # wide indexes: compact records only
             rec = 16
         if not (ctx and engine in (1, 3) and info.prefix_k):
             rec = 0
         # quaternary matrix: 16-B records (u32 contexts of 2 rows) when the table's
         # ranges average at most 2 rows
-        if (engine == 2 and ctx and not wide and info.prefix_k and os.environ.get("CS_FM_CTX_RECORDS") != "0"
+        if (engine == 2 and ctx and not wide and info.prefix_k and _opt("CS_FM_CTX_RECORDS") != "0"
                 and info.n <= 2 * info.prefix_sigma ** info.prefix_k):
             rec = 16
         assert info.record_bytes == rec, name
-        assert info.text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0"), name
+        assert info.text_in_hbm == (_opt("CS_FM_DEVICE_TEXT") != "0"), name
         # the 2-bit text of long-pattern verification: occurrence lines (not learned), narrow,
         # LF one n-cycle, with the full suffix array and the text in HBM — or (round 6) without
         # the full SA, over walk lines with text-position marks (C5's layout: its long
@@ -527,25 +516,17 @@ def test_ssa_strides_vs_oracle(pkg, stride):
 
 def test_prefix_table_sweep(pkg):
     """Prefix tables of every depth give the same counts (k forced 2..8)."""
-    import os
     t = O.gen_dna(9, 30000).tobytes()
     o = O.Index(t)
     rng = np.random.default_rng(2)
     pats = [t[i:i + m] for i, m in zip(rng.integers(0, 29000, 400), rng.integers(1, 25, 400))]
     pats += [bytes(rng.choice(list(b"ACGT$"), int(m)).astype(np.uint8)) for m in rng.integers(1, 12, 100)]
     want = [o.count(p) for p in pats]
-    saved = os.environ.get("CS_FM_PREFIX_K")
-    try:
-        for k in range(2, 9):
-            os.environ["CS_FM_PREFIX_K"] = str(k)
+    for k in range(2, 9):
+        with _env(CS_FM_PREFIX_K=str(k)):
             g = pkg.FMIndex.build_from_text(t)
-            assert g.info().prefix_k == k
-            assert g.count_batch(pats).tolist() == want, k
-    finally:
-        if saved is None:
-            os.environ.pop("CS_FM_PREFIX_K", None)
-        else:
-            os.environ["CS_FM_PREFIX_K"] = saved
+        assert g.info().prefix_k == k
+        assert g.count_batch(pats).tolist() == want, k
 
 
 def test_lf_overrun_message(pkg):
@@ -600,22 +581,15 @@ def test_device_extract(pkg, dtext):
     """Batched extract == text slices (fm_index.cpp:163-167 clamping), for every start
     position of a small text: copied from the text in HBM, or (CS_FM_DEVICE_TEXT=0) by
     LF inversion from inverse-SA samples."""
-    saved = os.environ.get("CS_FM_DEVICE_TEXT")
-    os.environ["CS_FM_DEVICE_TEXT"] = dtext
-    try:
-        for stride in (1, 5, 32):
-            t = O.gen_dna(stride, 3000).tobytes()
+    for stride in (1, 5, 32):
+        t = O.gen_dna(stride, 3000).tobytes()
+        with _env(CS_FM_DEVICE_TEXT=dtext):
             g = pkg.FMIndex.build_from_text(t, pkg.BuildParams(ssa_stride=stride))
-            assert g.info().text_in_hbm == int(dtext)
-            pos = list(range(0, len(t) + 3))
-            lens = [(p * 7) % 45 for p in pos]
-            got = g.extract_batch(pos, lens)
-            assert got == [t[p:p + l] for p, l in zip(pos, lens)]
-    finally:
-        if saved is None:
-            del os.environ["CS_FM_DEVICE_TEXT"]
-        else:
-            os.environ["CS_FM_DEVICE_TEXT"] = saved
+        assert g.info().text_in_hbm == int(dtext)
+        pos = list(range(0, len(t) + 3))
+        lens = [(p * 7) % 45 for p in pos]
+        got = g.extract_batch(pos, lens)
+        assert got == [t[p:p + l] for p, l in zip(pos, lens)]
     g = pkg.FMIndex.build_from_text(b"abab")  # no unique smallest terminator:
     assert g.extract_batch([0, 3], [2, 5]) == [b"ab", b"b"]  # the host text copy, as text_
     assert g.extract(0, 2) == b"ab"
@@ -624,61 +598,45 @@ def test_device_extract(pkg, dtext):
 def test_bucketed_multi_pass(pkg):
     """The bucketed sorter split into many passes (small pass budget) emits the same
     BWT / SSA / counts / positions as the oracle."""
-    saved = {k: os.environ.get(k) for k in ("CS_FM_SA_BUILDER", "CS_FM_PASS_MAX")}
-    try:
-        os.environ["CS_FM_SA_BUILDER"] = "bucketed"
-        base = O.gen_dna(32, 30000).tobytes()[:-1]
-        seg = base[1000:1500]  # 500-char repeat copied 6 times: ~24 refinement rounds
-        rep = b"".join(base[i * 5000:(i + 1) * 5000] + seg for i in range(6)) + b"$"
-        for t, budget in ((O.gen_dna(31, 60000).tobytes(), 4000),
-                          (O.gen_bytes(31, 50000).tobytes(), 4000),
-                          (rep, 4000)):
-            os.environ["CS_FM_PASS_MAX"] = str(budget)
+    base = O.gen_dna(32, 30000).tobytes()[:-1]
+    seg = base[1000:1500]  # 500-char repeat copied 6 times: ~24 refinement rounds
+    rep = b"".join(base[i * 5000:(i + 1) * 5000] + seg for i in range(6)) + b"$"
+    for t, budget in ((O.gen_dna(31, 60000).tobytes(), 4000),
+                      (O.gen_bytes(31, 50000).tobytes(), 4000),
+                      (rep, 4000)):
+        with _env(CS_FM_SA_BUILDER="bucketed", CS_FM_PASS_MAX=str(budget)):
             g = pkg.FMIndex.build_from_text(t)
-            o = O.Index(t)
-            rows = np.arange(len(t), dtype=np.uint64)
-            assert g.wt_access(rows).tobytes() == o.bwt().tobytes()
-            assert g.ssa().tolist() == o.ssa().tolist()
-            pats = [t[i:i + 12] for i in range(0, len(t) - 12, 997)]
-            assert g.count_batch(pats).tolist() == [o.count(p) for p in pats]
-            offs, pos = g.locate_batch(pats, limit=50)
-            for q, p in enumerate(pats):
-                assert pos[offs[q]:offs[q + 1]].tolist() == o.locate(p, limit=50)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        o = O.Index(t)
+        rows = np.arange(len(t), dtype=np.uint64)
+        assert g.wt_access(rows).tobytes() == o.bwt().tobytes()
+        assert g.ssa().tolist() == o.ssa().tolist()
+        pats = [t[i:i + 12] for i in range(0, len(t) - 12, 997)]
+        assert g.count_batch(pats).tolist() == [o.count(p) for p in pats]
+        offs, pos = g.locate_batch(pats, limit=50)
+        for q, p in enumerate(pats):
+            assert pos[offs[q]:offs[q + 1]].tolist() == o.locate(p, limit=50)
 
 
 def test_bucketed_long_repeats(pkg):
     """Exact repeats far longer than one key chunk (20 000-char copies, a 12 000-char
     run of one symbol, a period-3 stretch): the bucketed sorter refines only the
     still-tied suffixes, round after round, and emits the oracle's BWT / SSA."""
-    saved = os.environ.get("CS_FM_SA_BUILDER")
-    try:
-        os.environ["CS_FM_SA_BUILDER"] = "bucketed"
-        base = O.gen_dna(33, 60000).tobytes()[:-1]
-        seg = base[:20000]
-        texts = [
-            base[20000:25000] + seg + base[25000:30000] + seg + base[30000:31000] + seg + b"$",
-            base[:3000] + b"A" * 12000 + base[3000:6000] + b"$",
-            base[:2000] + b"ACG" * 5000 + base[2000:4000] + b"ACG" * 4000 + b"$",
-        ]
-        for t in texts:
+    base = O.gen_dna(33, 60000).tobytes()[:-1]
+    seg = base[:20000]
+    texts = [
+        base[20000:25000] + seg + base[25000:30000] + seg + base[30000:31000] + seg + b"$",
+        base[:3000] + b"A" * 12000 + base[3000:6000] + b"$",
+        base[:2000] + b"ACG" * 5000 + base[2000:4000] + b"ACG" * 4000 + b"$",
+    ]
+    for t in texts:
+        with _env(CS_FM_SA_BUILDER="bucketed"):
             g = pkg.FMIndex.build_from_text(t)
-            o = O.Index(t)
-            rows = np.arange(len(t), dtype=np.uint64)
-            assert g.wt_access(rows).tobytes() == o.bwt().tobytes()
-            assert g.ssa().tolist() == o.ssa().tolist()
-            pats = [t[i:i + 30] for i in range(0, len(t) - 30, 1999)]
-            assert g.count_batch(pats).tolist() == [o.count(p) for p in pats]
-    finally:
-        if saved is None:
-            os.environ.pop("CS_FM_SA_BUILDER", None)
-        else:
-            os.environ["CS_FM_SA_BUILDER"] = saved
+        o = O.Index(t)
+        rows = np.arange(len(t), dtype=np.uint64)
+        assert g.wt_access(rows).tobytes() == o.bwt().tobytes()
+        assert g.ssa().tolist() == o.ssa().tolist()
+        pats = [t[i:i + 30] for i in range(0, len(t) - 30, 1999)]
+        assert g.count_batch(pats).tolist() == [o.count(p) for p in pats]
 
 
 @pytest.mark.parametrize("name", ["banana", "dna_5k", "bytes_5k", "abab_noterm", "rare_N_41",
@@ -708,7 +666,7 @@ def test_create_from_arrays(pkg, name):
             continue
         assert g.locate(p, limit=50) == w
     assert gt.extract(1, 7) == t[1:8]
-    assert gt.info().text_in_hbm == (os.environ.get("CS_FM_DEVICE_TEXT") != "0")
+    assert gt.info().text_in_hbm == (_opt("CS_FM_DEVICE_TEXT") != "0")
     assert g.info().text_in_hbm == 0
     assert gt.extract_batch([1, 0, len(t) - 2], [7, 3, 9]) == [t[1:8], t[0:3], t[-2:]]
     with pytest.raises(RuntimeError):
@@ -1181,11 +1139,13 @@ def test_repetitive_text_vs_oracle(pkg):
 
 
 def test_selectors_without_a_variant(pkg):
-    """The two tuning selectors that no engine variant turns on give the oracle's answers:
-    CS_QT_COUNT_U4 (four patterns per lane in the staged count) on a uniform and a repetitive
-    text, and CS_QT_WALK_PERSISTENT (phase 2's persistent walk kernel; the two phases forced
-    with CS_QT_NO_ONEPASS) on an index without the full suffix array, at limits that cut
-    ranges and at ones that do not."""
+    """The tuning selectors that no engine variant turns on give the oracle's answers:
+    CS_QT_COUNT_U4 (four patterns per lane in the staged count) and CS_QT_BARRIER (its general
+    search behind a block barrier) on a uniform and a repetitive text; CS_QT_WALK_PERSISTENT
+    (phase 2's persistent walk kernel) and CS_QT_WALK_ROWS (walks from an expanded rows buffer),
+    the two phases forced with CS_QT_NO_ONEPASS, on an index without the full suffix array, at
+    limits that cut ranges and at ones that do not; and position samples at the SSA's stride
+    (build option PSTRIDE=32: locate walks and extract by LF inversion)."""
     rng = np.random.default_rng(31)
     seed = rng.choice(list(b"ACGT"), 2000).astype(np.uint8)
     rep = np.tile(seed, 100)
@@ -1204,14 +1164,28 @@ def test_selectors_without_a_variant(pkg):
         buf, offs = O.pack_patterns(pats)
         want = o.count_batch(buf=buf, offs=offs, nthreads=8)
         assert np.array_equal(_count_bo(g, buf, offs, flags=pkg.QT_COUNT_U4), want), name
+        assert np.array_equal(_count_bo(g, buf, offs, flags=pkg.QT_BARRIER), want), name
         sub = pats[::5]
         b2, o2 = O.pack_patterns(sub)
         for lim in (3, 100_000):
             woffs, wpos = o.locate_batch(buf=b2, offs=o2, limit=lim, nthreads=8)
-            got = _locate_one(g, sub, lim, flags=pkg.QT_NO_ONEPASS | pkg.QT_WALK_PERSISTENT)
-            assert np.array_equal(np.cumsum([0] + [len(q) for q in got]), woffs.astype(np.int64)), (name, lim)
-            flat = [x for q in got for x in q]
-            assert np.array_equal(np.asarray(flat, np.int64), wpos.astype(np.int64)), (name, lim)
+            for sel in (pkg.QT_WALK_PERSISTENT, pkg.QT_WALK_ROWS):
+                got = _locate_one(g, sub, lim, flags=pkg.QT_NO_ONEPASS | sel)
+                assert np.array_equal(np.cumsum([0] + [len(q) for q in got]), woffs.astype(np.int64)), (name, lim)
+                flat = [x for q in got for x in q]
+                assert np.array_equal(np.asarray(flat, np.int64), wpos.astype(np.int64)), (name, lim)
+    t = texts["dna"]
+    with _env(CS_FM_PSTRIDE="32", CS_FM_FULL_SA="0", CS_FM_DEVICE_TEXT="0"):
+        g = pkg.FMIndex.build_from_text(t)
+    assert g.info().position_stride == 32
+    o = O.Index(t)
+    pats = [bytes(p) for p in O.gen_patterns_text(np.frombuffer(t, np.uint8), 12, 300, seed=8)]
+    b2, o2 = O.pack_patterns(pats)
+    woffs, wpos = o.locate_batch(buf=b2, offs=o2, limit=50, nthreads=8)
+    got = _locate_one(g, pats, 50)
+    assert [x for q in got for x in q] == wpos.astype(np.int64).tolist()
+    pos = list(range(0, len(t), 997))
+    assert g.extract_batch(pos, [40] * len(pos)) == [t[p:p + 40] for p in pos]
 
 
 def test_dna_character_map(pkg):

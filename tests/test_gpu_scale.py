@@ -146,7 +146,7 @@ def _kmer_checksum(idx, alphabet, k, N):
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C4") == "1", reason="C4 disabled")
 @pytest.mark.parametrize("variant", ["auto", "plain_walk", "learned", "wavelet"])
-def test_c4_dna_4gb(variant, monkeypatch):
+def test_c4_dna_4gb(variant, build_opts):
     """BASELINE configs[3] at full size: the default index (context records, left
     contexts, full suffix array), the same without records and full SA (8-B table,
     context sectors, locate by walk lines), the learned occurrence lines, and (round 6,
@@ -154,10 +154,10 @@ def test_c4_dna_4gb(variant, monkeypatch):
     BitVectors (wavelet.cpp:59-96, bitvector.cpp:165-230) in 32-B rank lines — whose count
     and one-call locate (k_locate_one_gen) are checked against the same text scan."""
     if variant == "plain_walk":
-        monkeypatch.setenv("CS_FM_CTX_RECORDS", "0")
-        monkeypatch.setenv("CS_FM_FULL_SA", "0")
+        build_opts(CS_FM_CTX_RECORDS="0")
+        build_opts(CS_FM_FULL_SA="0")
     elif variant in ("learned", "wavelet"):
-        monkeypatch.setenv("CS_FM_ENGINE", variant)
+        build_opts(CS_FM_ENGINE=variant)
     pkg = load_pkg()
     _trim_pool()
     free0 = torch.cuda.mem_get_info(0)[0]  # (the text is allocated inside _build, 4 GB + 16 B)
@@ -204,13 +204,13 @@ def test_c4_dna_4gb(variant, monkeypatch):
 
 @pytest.mark.skipif(os.environ.get("CS_FM_SKIP_C5") == "1", reason="C5 disabled")
 @pytest.mark.parametrize("engine", ["auto", "wavelet"])
-def test_c5_dna_32gb_wide(engine, monkeypatch):
+def test_c5_dna_32gb_wide(engine, build_opts):
     """BASELINE configs[4]: 32 GB text (n >= 2^32) — wide index (u64 samples) built by
     the pass-by-pass bucketed suffix sorter, with occurrence lines (default for
     DNA) or the wavelet matrix in 32-B wide rank lines (Line32W; opt-in in round 5, back in
     the default suite in round 6: VERDICT r05 item 3)."""
     if engine == "wavelet":
-        monkeypatch.setenv("CS_FM_ENGINE", "wavelet")
+        build_opts(CS_FM_ENGINE="wavelet")
     pkg = load_pkg()
     idx, text, host, N = _build(pkg, "dna", 31_999_999_999)
     info = idx.info()

@@ -28,9 +28,9 @@ def _patterns(t, rng, n):
 
 @pytest.mark.parametrize("engine", ["auto", "wavelet", "qwm", "learned"])
 @pytest.mark.parametrize("kind", ["dna", "bytes"])
-def test_serve_matches_oracle(kind, engine, monkeypatch):
+def test_serve_matches_oracle(kind, engine, build_opts):
     if engine != "auto":
-        monkeypatch.setenv("CS_FM_ENGINE", engine)
+        build_opts(CS_FM_ENGINE=engine)
     pkg = load_pkg()
     base = (O.gen_dna(7, 20_000) if kind == "dna" else O.gen_bytes(7, 20_000)).tobytes()
     # repeats so that long patterns occur more than once
