@@ -27,7 +27,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from srchash import kernel_src_hash  # noqa: E402  (the tree that was profiled)
 
-ONE_CALL = ("k_count_ctx_onepass", "k_count_ctx_onepass_skiplong", "k_locate_long", "k_locate_list",
+ONE_CALL = ("k_count_ctx_onepass", "k_count_ctx_onepass_skiplong", "k_count_qctx_onepass", "k_locate_one_gen",
+            "k_locate_long", "k_locate_list",
             "k_locate_emit", "k_locate_emit_wide", "k_locate_walks", "k_scan_chained", "k_scan_tiles")
 # the kernel that carries each leg's work
 LEG_KERNEL = {"count": "count", "count_u32": "count", "count_packed": "count",
@@ -73,16 +74,17 @@ def short(name):
             return "k_count_ctx_loc"
         return "k_count_ctx%s%s_w%s" % ("_packed" if packed == "true" else "",
                                          "_skiplong" if skip == "true" else "", w)
-    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?(?:, \d+)?(?:, (true|false))?>", name)
-    if m:  # the third argument: the measurement twin (kBytes)
+    m = re.search(r"k_count_long<(\d), (true|false)(?:, (true|false))?(?:, \d+)?(?:, (true|false))?(?:, \d+)?>",
+                  name)
+    if m:  # the third argument: the measurement twin (kBytes); the last (round 6) kWalk
         return "k_count_long%s%s" % ("_ptext" if m.group(2) == "true" else "_btext",
                                      "_bytes" if m.group(3) == "true" else "")
     m = re.search(r"k_count_list<(\d)(?:, (true|false))?>", name)
     if m:
         return "k_count_list_bytes" if m.group(2) == "true" else "k_count_list"
-    m = re.search(r"k_count_qctx<(\d), (\d)>", name)
-    if m:
-        return "k_count_qctx_w%s" % m.group(2)
+    m = re.search(r"k_count_qctx<(\d), (\d)(?:, (true|false))?>", name)
+    if m:  # (round 6) the third argument: the one-call locate's search (kOne)
+        return "k_count_qctx_onepass" if m.group(3) == "true" else "k_count_qctx_w%s" % m.group(2)
     m = re.search(r"k_count<[^,]*?(\w+)(<\w+>)?, (true|false)>", name)
     if m:
         return "k_count_packed" if m.group(3) == "true" else "k_count"
@@ -91,7 +93,7 @@ def short(name):
             return k
     for k in ("k_count_bytes", "k_count_one", "k_count", "k_walk_short", "k_walk_lines", "k_walk_fused_wide",
               "k_walk_fused", "k_walk", "k_locate_walks", "k_scan_chained", "k_scan_tiles",
-              "k_locate_long", "k_locate_list", "k_locate_emit_wide", "k_locate_emit",
+              "k_locate_long", "k_locate_list", "k_locate_emit_wide", "k_locate_emit", "k_locate_one_gen",
               "k_locate_ranges", "k_locate_sa_wide", "k_locate_sa", "k_expand_rows", "k_pack_wire"):
         if k in name:
             return k
