@@ -153,3 +153,21 @@ def test_build_options_parse():
     assert L.cs_fm_build_with_options(t.ctypes.data, 4, 0, C.byref(p), b"LCTX=0 BOGUS=2", 0,
                                       C.byref(h)) == pkg.CS_ERR_INVALID
     assert b"BOGUS" in L.cs_fm_last_error() and not h.value
+
+
+def test_build_option_names_cover_the_builders():
+    """Every CS_FM_* variable a builder reads through build_opt() (and every selector default
+    read_tuning maps) is a name cs_fm_build_with_options accepts, and the list names nothing
+    else: an options scope can set each knob the environment can."""
+    csrc = os.path.join(ROOT, "compressed-fm-index-implementation-with-learned-optimizations_amd", "csrc")
+    used = set()
+    for f in glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")) + \
+            glob.glob(os.path.join(csrc, "*.cpp")):
+        src = open(f).read()
+        used |= set(re.findall(r'build_opt\("(CS_FM_[A-Z_0-9]+)"\)', src))
+        used |= set(re.findall(r'\{"(CS_FM_[A-Z_0-9]+)", "\d+", CS_QT_', src))
+    capi = open(os.path.join(csrc, "fm_capi.hip")).read()
+    a = capi.index("kBuildOptNames[] = {")
+    listed = set(re.findall(r'"(CS_FM_[A-Z_0-9]+)"', capi[a:capi.index("};", a)]))
+    assert used and used == listed, (sorted(used - listed), sorted(listed - used))
+    assert "std::getenv(name)" in capi  # the one environment read: build_opt outside a scope
