@@ -355,7 +355,13 @@ int main(int argc, char** argv) {
   uint64_t *offs, *out, *sink;
   uint2* keys;
   uint16_t* gmap;
-  CK(hipMalloc(&tab, kRecs * 16));
+  // argv[3]: the table's allocation — 0 hipMalloc, 1 hipExtMallocWithFlags(hipDeviceMallocContiguous)
+  // (physically contiguous: address-translation reach); argv[4] = 1: the random and one-shot
+  // shapes only
+  const int alloc = argc > 3 ? std::atoi(argv[3]) : 0;
+  const bool quick = argc > 4 && std::atoi(argv[4]) != 0;
+  if (alloc == 1) CK(hipExtMallocWithFlags(reinterpret_cast<void**>(&tab), kRecs * 16, hipDeviceMallocContiguous));
+  else CK(hipMalloc(&tab, kRecs * 16));
   CK(hipMalloc(&pats, npat * kM + 64));
   CK(hipMalloc(&offs, (npat + 1) * 8));
   CK(hipMalloc(&out, npat * 8));
@@ -371,8 +377,8 @@ int main(int argc, char** argv) {
   k_fill_pats<<<4096, 256>>>(pats, offs, npat);
   CK(hipDeviceSynchronize());
   const double alg = npat * (8.0 + kM + 16 + 8);  // bytes per query the count reads / writes
-  std::printf("{\"npat\": %llu, \"table_gb\": %.2f, \"cus\": %d, \"alg_bytes\": %.0f}\n",
-              (unsigned long long)npat, kRecs * 16 / 1e9, ncu, alg);
+  std::printf("{\"npat\": %llu, \"table_gb\": %.2f, \"cus\": %d, \"alg_bytes\": %.0f, \"alloc\": %d}\n",
+              (unsigned long long)npat, kRecs * 16 / 1e9, ncu, alg, alloc);
   auto report = [&](const char* name, double ms, bool rand_reads) {
     std::printf("{\"shape\": \"%s\", \"ms\": %.4f, \"queries_per_s\": %.4g, \"rand_reads_per_s\": %.4g, "
                 "\"alg_GBps\": %.1f}\n",
@@ -398,6 +404,7 @@ int main(int argc, char** argv) {
          true)
   ONESHOT(1, 8);
   ONESHOT(2, 6);
+  if (quick) return 0;
   ONESHOT(2, 8);
   ONESHOT(4, 6);
 #define ONESHOT_LDS(U, OV, P32)                                                                  \
