@@ -454,27 +454,36 @@ def test_batch_edge_cases(pkg):
     assert g.count_batch(big).tolist() == [o.count(p) for p in big]
 
 
+_LARGE = {}  # (gen, m) -> the text, its batch and the oracle's answers (the same for every variant)
+
+
+def _large_case(gen, m):
+    if (gen, m) not in _LARGE:
+        n = 2_000_000
+        t = (O.gen_dna(42, n) if gen == "dna" else O.gen_bytes(42, n))
+        o = O.Index(t.tobytes())
+        q_text = O.gen_patterns_text(t, m, 20000, seed=4242)
+        alpha = b"ACGT" if gen == "dna" else bytes(range(1, 256))
+        q_unif = O.gen_patterns_uniform(alpha, m, 5000, seed=4243)
+        short = O.gen_patterns_text(t, 3, 300, seed=1)
+        pats = [bytes(p) for p in q_text] + [bytes(p) for p in q_unif] + [bytes(p) for p in short]
+        buf, offs = O.pack_patterns(pats)
+        want = o.count_batch(buf=buf, offs=offs, nthreads=8)
+        woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=1000, nthreads=8)
+        _LARGE[(gen, m)] = (t.tobytes(), buf, offs, want, woffs, wpos)
+    return _LARGE[(gen, m)]
+
+
 @pytest.mark.parametrize("gen,m", [("dna", 20), ("bytes", 8)])
 def test_random_large_vs_oracle(pkg, gen, m):
-    n = 2_000_000
-    t = (O.gen_dna(42, n) if gen == "dna" else O.gen_bytes(42, n))
-    g = pkg.FMIndex.build_from_text(t.tobytes())
-    o = O.Index(t.tobytes())
-    q_text = O.gen_patterns_text(t, m, 20000, seed=4242)
-    alpha = b"ACGT" if gen == "dna" else bytes(range(1, 256))
-    q_unif = O.gen_patterns_uniform(alpha, m, 5000, seed=4243)
-    short = O.gen_patterns_text(t, 3, 300, seed=1)
-    pats = [bytes(p) for p in q_text] + [bytes(p) for p in q_unif] + [bytes(p) for p in short]
-    buf, offs = O.pack_patterns(pats)
-    want = o.count_batch(buf=buf, offs=offs, nthreads=8)
+    t, buf, offs, want, woffs, wpos = _large_case(gen, m)
+    g = pkg.FMIndex.build_from_text(t)
     got = g.count_batch(buf=buf, offs=offs)
     assert np.array_equal(got, want)
     assert (got[:20000] >= 1).all()
     if _learned():
         assert np.array_equal(_bar_count(g, buf, offs), want)
-    lim = 1000
-    woffs, wpos = o.locate_batch(buf=buf, offs=offs, limit=lim, nthreads=8)
-    goffs, gpos = g.locate_batch(buf=buf, offs=offs, limit=lim)
+    goffs, gpos = g.locate_batch(buf=buf, offs=offs, limit=1000)
     assert np.array_equal(goffs, woffs)
     assert np.array_equal(gpos, wpos)
 
