@@ -143,6 +143,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (live[j]) __builtin_nontemporal_store(rec_count(a[j], w[j]), out + q0 + (uint64_t)j * 256);
 }
 
+// ---- the production shape plus the production kernel's extras, one at a time (round 6) -----
+// NALU: a dependent chain of NALU / 2 multiply-shift-add rounds (≈ 3 vector ops each) per
+// pattern, half on the key before the record read, half on the record after it (the
+// production count issues ~1,056 VALU per wave against the one-shot's 326: NALU = 122 at U = 2
+// adds ≈ 730 per wave);
+// kSecond: one lane in 50 makes a second, dependent random 64-B read after its record (the
+// production's context sectors, ~2 % of the 20-mers)
+template <int U, int WPE, int NALU, bool kSecond>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_oneshot_x(
+    const uint4* __restrict__ tab, const uint8_t* __restrict__ pats, const uint64_t* __restrict__ offs,
+    uint64_t npat, uint64_t* __restrict__ out) {
+  const uint64_t q0 = blockIdx.x * (uint64_t)(256 * U) + threadIdx.x;
+  uint32_t t[U], w[U];
+  bool live[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const uint64_t q = q0 + (uint64_t)j * 256;
+    live[j] = q < npat;
+    t[j] = w[j] = 0;
+    if (!live[j]) continue;
+    const uint64_t o = offs[q], m = offs[q + 1] - o;
+    if (m != kM) continue;
+    uint32_t u[5];
+    load_pat(pats, o, u);
+    key(u, t[j], w[j]);
+    uint32_t x = w[j];
+#pragma unroll 1
+    for (int i = 0; i < NALU / 2; ++i) x = x * 0x9E3779B1u + (x >> 7);
+    w[j] ^= (x & 0x80000000u);  // (bit 31 of a 10-bit want: no effect on the match, kept live)
+  }
+  uint4 a[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) a[j] = live[j] ? ld_nt16(tab + t[j]) : make_uint4(0, 0, 0, 0);
+  if constexpr (kSecond) {
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (live[j] && (mix(q0 + j * 256) % 50) == 0) {
+        const uint4 b = ld_nt16(tab + ((t[j] ^ a[j].x) & (kRecs - 1)));
+        a[j].x ^= b.x & 0x80000000u;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    uint32_t x = a[j].x;
+#pragma unroll 1
+    for (int i = 0; i < NALU / 2; ++i) x = x * 0x9E3779B1u + (x >> 7);
+    a[j].y ^= (x & 0x80000000u) >> 31 << 30;  // (bit 30 of y: outside the width and contexts)
+  }
+#pragma unroll
+  for (int j = 0; j < U; ++j)
+    if (live[j]) __builtin_nontemporal_store(rec_count(a[j], w[j]), out + q0 + (uint64_t)j * 256);
+}
+
 // ---- the production shape's prologue: a symbol map staged in LDS from global memory --------
 // kOverlap false: map load -> LDS -> barrier, then offsets and patterns (k_count_ctx, round 5);
 // true: the map load issued first, its LDS store and the barrier after the pattern loads are
@@ -404,6 +457,16 @@ int main(int argc, char** argv) {
          true)
   ONESHOT(1, 8);
   ONESHOT(2, 6);
+#define ONESHOT_X(NALU, SEC)                                                                   \
+  report("oneshot_x U=2 wpe=6 alu=" #NALU " second=" #SEC, median_ms(reps, [&] {              \
+           k_oneshot_x<2, 6, NALU, SEC><<<(unsigned)((npat + 511) / 512), 256>>>(tab, pats, offs, npat, out); \
+         }),                                                                                   \
+         true)
+  ONESHOT_X(0, false);
+  ONESHOT_X(0, true);
+  ONESHOT_X(122, false);
+  ONESHOT_X(122, true);
+  ONESHOT_X(244, false);
   if (quick) return 0;
   ONESHOT(2, 8);
   ONESHOT(4, 6);
